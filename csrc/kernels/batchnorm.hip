@@ -1,0 +1,363 @@
+// Training / inference BatchNorm (+ReLU, +residual) kernels, NHWC bf16 activations, fp32 stats.
+//
+// Replaces TF's FusedBatchNorm / moments + batch_normalization (SURVEY.md §2.12c K4/K5;
+// reference resnet/resnet_model.py:45-48, inception/slim/ops.py:117-131,
+// vgg/nets/resnet_utils.py:254).  Semantics kept from TF 1.x:
+//   * normalisation uses the biased batch variance;
+//   * the moving variance update uses the Bessel-corrected variance when `bessel` is set
+//     (fused BN path of the contrib-slim zoo) and the biased one otherwise (old slim
+//     tf.nn.moments path, inception/slim/ops.py:117-124);
+//   * moving_x -= (moving_x - batch_x) * (1 - decay).
+// Activations are processed 8 channels (16 B) per lane; per-channel partial sums are reduced
+// through LDS and committed with one fp32 atomic per channel per block.
+#include "common.h"
+
+namespace dtm {
+
+template <int V>
+struct Vec;
+template <>
+struct Vec<8> {
+  uint4 u;
+  __device__ __forceinline__ void load(const bf16_t* p) { u = *(const uint4*)p; }
+  __device__ __forceinline__ void store(bf16_t* p) const { *(uint4*)p = u; }
+  __device__ __forceinline__ float get(int e) const {
+    uint32_t w = e < 2 ? u.x : e < 4 ? u.y : e < 6 ? u.z : u.w;
+    return (e & 1) ? hi_bf(w) : lo_bf(w);
+  }
+  __device__ __forceinline__ void unpack(float* f) const {
+    f[0] = lo_bf(u.x); f[1] = hi_bf(u.x); f[2] = lo_bf(u.y); f[3] = hi_bf(u.y);
+    f[4] = lo_bf(u.z); f[5] = hi_bf(u.z); f[6] = lo_bf(u.w); f[7] = hi_bf(u.w);
+  }
+  __device__ __forceinline__ void pack(const float* f) {
+    u = make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
+  }
+};
+template <>
+struct Vec<1> {
+  bf16_t u;
+  __device__ __forceinline__ void load(const bf16_t* p) { u = *p; }
+  __device__ __forceinline__ void store(bf16_t* p) const { *p = u; }
+  __device__ __forceinline__ void unpack(float* f) const { f[0] = bf2f(u); }
+  __device__ __forceinline__ void pack(const float* f) { u = f2bf(f[0]); }
+};
+
+// ---- per-channel sum / sumsq over rows ---------------------------------------------------
+template <int V>
+__global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict__ x, float* __restrict__ stats,
+                                                       long M, int C, long rows_per_block) {
+  __shared__ float red[2][256][V];
+  const int cols = C / V;
+  const int tid = threadIdx.x;
+  const int rpi = cols >= 256 ? 1 : 256 / cols;
+  const long r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  for (int cb = 0; cb < cols; cb += 256) {
+    const int tcol = cb + (cols >= 256 ? tid : tid % cols);
+    const int trow = cols >= 256 ? 0 : tid / cols;
+    float s[V], q[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) s[e] = q[e] = 0.f;
+    if (trow < rpi && tcol < cols) {
+      for (long r = r0 + trow; r < r1; r += rpi) {
+        Vec<V> v; v.load(x + r * C + tcol * V);
+        float f[V]; v.unpack(f);
+#pragma unroll
+        for (int e = 0; e < V; ++e) { s[e] += f[e]; q[e] += f[e] * f[e]; }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e) { red[0][tid][e] = s[e]; red[1][tid][e] = q[e]; }
+    __syncthreads();
+    if (cols >= 256) {
+      if (tcol < cols) {
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          atomicAdd(stats + tcol * V + e, s[e]);
+          atomicAdd(stats + C + tcol * V + e, q[e]);
+        }
+      }
+    } else if (tid < cols) {
+      float S[V], Q[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) S[e] = Q[e] = 0.f;
+      for (int rr = 0; rr < rpi; ++rr)
+#pragma unroll
+        for (int e = 0; e < V; ++e) { S[e] += red[0][rr * cols + tid][e]; Q[e] += red[1][rr * cols + tid][e]; }
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        atomicAdd(stats + tid * V + e, S[e]);
+        atomicAdd(stats + C + tid * V + e, Q[e]);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---- finalize: stats -> scale/shift (+ moving average update) -----------------------------
+// out: [4][C] = scale, shift, mean, rstd
+__global__ void bn_finalize_kernel(const float* __restrict__ stats, const float* __restrict__ gamma,
+                                   const float* __restrict__ beta, float* __restrict__ mov_mean,
+                                   float* __restrict__ mov_var, float* __restrict__ out, int C, float count,
+                                   float eps, float decay, int update, int bessel) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float mean = stats[c] / count;
+  float var = fmaxf(stats[C + c] / count - mean * mean, 0.f);
+  float rstd = rsqrtf(var + eps);
+  float g = gamma ? gamma[c] : 1.f;
+  float b = beta ? beta[c] : 0.f;
+  float sc = g * rstd;
+  out[c] = sc;
+  out[C + c] = b - mean * sc;
+  out[2 * C + c] = mean;
+  out[3 * C + c] = rstd;
+  if (update) {
+    float uvar = (bessel && count > 1.f) ? var * count / (count - 1.f) : var;
+    mov_mean[c] -= (mov_mean[c] - mean) * (1.f - decay);
+    mov_var[c] -= (mov_var[c] - uvar) * (1.f - decay);
+  }
+}
+
+// inference: scale/shift from moving statistics
+__global__ void bn_inference_params_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
+                                           const float* __restrict__ mov_mean, const float* __restrict__ mov_var,
+                                           float* __restrict__ out, int C, float eps) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float rstd = rsqrtf(mov_var[c] + eps);
+  float g = gamma ? gamma[c] : 1.f;
+  float sc = g * rstd;
+  out[c] = sc;
+  out[C + c] = (beta ? beta[c] : 0.f) - mov_mean[c] * sc;
+  out[2 * C + c] = mov_mean[c];
+  out[3 * C + c] = rstd;
+}
+
+// ---- apply: y = act(x*scale + shift [+ res | + res*rscale + rshift]) -----------------------
+// res_mode: 0 none, 1 identity residual, 2 BN'd residual (projection shortcut)
+template <int V>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ x, const float* __restrict__ ss,
+                                                       const bf16_t* __restrict__ res, const float* __restrict__ rss,
+                                                       bf16_t* __restrict__ y, long M, int C, int res_mode, int relu) {
+  const int cols = C / V;
+  const long total = M * cols;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int cv = (int)(i % cols) * V;
+    Vec<V> v; v.load(x + i * V);
+    float f[V]; v.unpack(f);
+#pragma unroll
+    for (int e = 0; e < V; ++e) f[e] = fmaf(f[e], ss[cv + e], ss[C + cv + e]);
+    if (res_mode) {
+      Vec<V> r; r.load(res + i * V);
+      float g[V]; r.unpack(g);
+      if (res_mode == 2) {
+#pragma unroll
+        for (int e = 0; e < V; ++e) f[e] += fmaf(g[e], rss[cv + e], rss[C + cv + e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < V; ++e) f[e] += g[e];
+      }
+    }
+    if (relu) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) f[e] = fmaxf(f[e], 0.f);
+    }
+    Vec<V> o; o.pack(f); o.store(y + i * V);
+  }
+}
+
+// ---- backward -------------------------------------------------------------------------------
+// g = dy * mask, mask: mode 0 none, 1 (y > 0) from tensor y, 2 recompute (x*scale+shift > 0)
+// sums: [2][C] += sum(g), sum(g * xhat),  xhat = (x - mean) * rstd
+template <int V>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                            const bf16_t* __restrict__ ymask, const float* __restrict__ ss,
+                                                            float* __restrict__ sums, long M, int C, int mask_mode,
+                                                            long rows_per_block) {
+  __shared__ float red[2][256][V];
+  const int cols = C / V;
+  const int tid = threadIdx.x;
+  const int rpi = cols >= 256 ? 1 : 256 / cols;
+  const long r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  const float* scale = ss;
+  const float* shift = ss + C;
+  const float* mean = ss + 2 * C;
+  const float* rstd = ss + 3 * C;
+  for (int cb = 0; cb < cols; cb += 256) {
+    const int tcol = cb + (cols >= 256 ? tid : tid % cols);
+    const int trow = cols >= 256 ? 0 : tid / cols;
+    float s[V], q[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) s[e] = q[e] = 0.f;
+    if (trow < rpi && tcol < cols) {
+      const int cv = tcol * V;
+      float mu[V], rs[V], sc[V], sh[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) { mu[e] = mean[cv + e]; rs[e] = rstd[cv + e]; sc[e] = scale[cv + e]; sh[e] = shift[cv + e]; }
+      for (long r = r0 + trow; r < r1; r += rpi) {
+        Vec<V> a, b; a.load(dy + r * C + cv); b.load(x + r * C + cv);
+        float g[V], xv[V]; a.unpack(g); b.unpack(xv);
+        if (mask_mode == 1) {
+          Vec<V> m; m.load(ymask + r * C + cv);
+          float mv[V]; m.unpack(mv);
+#pragma unroll
+          for (int e = 0; e < V; ++e) g[e] = mv[e] > 0.f ? g[e] : 0.f;
+        } else if (mask_mode == 2) {
+#pragma unroll
+          for (int e = 0; e < V; ++e) g[e] = fmaf(xv[e], sc[e], sh[e]) > 0.f ? g[e] : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e) { s[e] += g[e]; q[e] += g[e] * (xv[e] - mu[e]) * rs[e]; }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e) { red[0][tid][e] = s[e]; red[1][tid][e] = q[e]; }
+    __syncthreads();
+    if (cols >= 256) {
+      if (tcol < cols) {
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          atomicAdd(sums + tcol * V + e, s[e]);
+          atomicAdd(sums + C + tcol * V + e, q[e]);
+        }
+      }
+    } else if (tid < cols) {
+      float S[V], Q[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) S[e] = Q[e] = 0.f;
+      for (int rr = 0; rr < rpi; ++rr)
+#pragma unroll
+        for (int e = 0; e < V; ++e) { S[e] += red[0][rr * cols + tid][e]; Q[e] += red[1][rr * cols + tid][e]; }
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        atomicAdd(sums + tid * V + e, S[e]);
+        atomicAdd(sums + C + tid * V + e, Q[e]);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// dx = scale * (g - sum_g/M - xhat * sum_gx/M);  optional gout = g (masked dy, for the
+// residual branch).  training=0: dx = scale * g (inference-mode BN, frozen statistics).
+template <int V>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                           const bf16_t* __restrict__ ymask, const float* __restrict__ ss,
+                                                           const float* __restrict__ sums, bf16_t* __restrict__ dx,
+                                                           bf16_t* __restrict__ gout, long M, int C, int mask_mode,
+                                                           int training) {
+  const int cols = C / V;
+  const long total = M * cols;
+  const float invM = 1.f / (float)M;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int cv = (int)(i % cols) * V;
+    Vec<V> a, b; a.load(dy + i * V); b.load(x + i * V);
+    float g[V], xv[V]; a.unpack(g); b.unpack(xv);
+    if (mask_mode == 1) {
+      Vec<V> m; m.load(ymask + i * V);
+      float mv[V]; m.unpack(mv);
+#pragma unroll
+      for (int e = 0; e < V; ++e) g[e] = mv[e] > 0.f ? g[e] : 0.f;
+    } else if (mask_mode == 2) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) g[e] = fmaf(xv[e], ss[cv + e], ss[C + cv + e]) > 0.f ? g[e] : 0.f;
+    }
+    if (gout) { Vec<V> o; o.pack(g); o.store(gout + i * V); }
+    float r[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const int c = cv + e;
+      if (training) {
+        float xh = (xv[e] - ss[2 * C + c]) * ss[3 * C + c];
+        r[e] = ss[c] * (g[e] - sums[c] * invM - xh * sums[C + c] * invM);
+      } else {
+        r[e] = ss[c] * g[e];
+      }
+    }
+    Vec<V> o; o.pack(r); o.store(dx + i * V);
+  }
+}
+
+// dgamma = sum(g*xhat), dbeta = sum(g)  (accumulated into fp32 grads)
+__global__ void bn_param_grad_kernel(const float* __restrict__ sums, float* __restrict__ dgamma,
+                                     float* __restrict__ dbeta, int C) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  if (dgamma) dgamma[c] += sums[C + c];
+  if (dbeta) dbeta[c] += sums[c];
+}
+
+}  // namespace dtm
+using namespace dtm;
+
+static int grid_for(long work, int cap = 2048) {
+  long b = (work + 255) / 256;
+  return (int)(b < 1 ? 1 : (b > cap ? cap : b));
+}
+static long rows_per_block_for(long M, int C) {
+  // aim for ~1024 blocks, >= 64 rows each
+  long r = (M + 1023) / 1024;
+  if (r < 64) r = 64;
+  return r;
+}
+
+DTM_API void dtm_bn_stats(const void* x, float* stats, long M, int C, void* stream) {
+  long rpb = rows_per_block_for(M, C);
+  int blocks = (int)((M + rpb - 1) / rpb);
+  if (C % 8 == 0)
+    hipLaunchKernelGGL(bn_stats_kernel<8>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, stats, M, C, rpb);
+  else
+    hipLaunchKernelGGL(bn_stats_kernel<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, stats, M, C, rpb);
+}
+
+DTM_API void dtm_bn_finalize(const float* stats, const float* gamma, const float* beta, float* mov_mean,
+                             float* mov_var, float* out, int C, float count, float eps, float decay, int update,
+                             int bessel, void* stream) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, stats, gamma, beta,
+                     mov_mean, mov_var, out, C, count, eps, decay, update, bessel);
+}
+
+DTM_API void dtm_bn_inference_params(const float* gamma, const float* beta, const float* mov_mean,
+                                     const float* mov_var, float* out, int C, float eps, void* stream) {
+  hipLaunchKernelGGL(bn_inference_params_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, gamma, beta,
+                     mov_mean, mov_var, out, C, eps);
+}
+
+DTM_API void dtm_bn_apply(const void* x, const float* ss, const void* res, const float* rss, void* y, long M, int C,
+                          int res_mode, int relu, void* stream) {
+  if (C % 8 == 0)
+    hipLaunchKernelGGL(bn_apply_kernel<8>, dim3(grid_for(M * C / 8)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)x, ss, (const bf16_t*)res, rss, (bf16_t*)y, M, C, res_mode, relu);
+  else
+    hipLaunchKernelGGL(bn_apply_kernel<1>, dim3(grid_for(M * C)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)x, ss, (const bf16_t*)res, rss, (bf16_t*)y, M, C, res_mode, relu);
+}
+
+DTM_API void dtm_bn_bwd_reduce(const void* dy, const void* x, const void* ymask, const float* ss, float* sums, long M,
+                               int C, int mask_mode, void* stream) {
+  long rpb = rows_per_block_for(M, C);
+  int blocks = (int)((M + rpb - 1) / rpb);
+  if (C % 8 == 0)
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<8>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
+                       (const bf16_t*)x, (const bf16_t*)ymask, ss, sums, M, C, mask_mode, rpb);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
+                       (const bf16_t*)x, (const bf16_t*)ymask, ss, sums, M, C, mask_mode, rpb);
+}
+
+DTM_API void dtm_bn_bwd_apply(const void* dy, const void* x, const void* ymask, const float* ss, const float* sums,
+                              void* dx, void* gout, long M, int C, int mask_mode, int training, void* stream) {
+  if (C % 8 == 0)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<8>, dim3(grid_for(M * C / 8)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)ymask, ss, sums, (bf16_t*)dx, (bf16_t*)gout,
+                       M, C, mask_mode, training);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, dim3(grid_for(M * C)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)ymask, ss, sums, (bf16_t*)dx, (bf16_t*)gout,
+                       M, C, mask_mode, training);
+}
+
+DTM_API void dtm_bn_param_grad(const float* sums, float* dgamma, float* dbeta, int C, void* stream) {
+  hipLaunchKernelGGL(bn_param_grad_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, sums, dgamma,
+                     dbeta, C);
+}

@@ -1,0 +1,565 @@
+// Implicit-GEMM convolution kernels for gfx950 (CDNA4), NHWC bf16, fp32 accumulate.
+//
+// Replaces the cuDNN Conv2D / Conv2DBackpropInput / Conv2DBackpropFilter kernels that the
+// reference gets from the TF runtime (call sites e.g.
+// reference vgg/nets/resnet_v1.py:111-128 via slim.conv2d, inception/slim/ops.py:232).
+//
+// Design (MI355X-first, not a translation of any CUDA tiling):
+//  * conv_nt:  C[chan][pix] = W[chan][k] . X[pix][k]  with k = (r, s, c).  Used for forward and
+//    (with a flipped/transposed weight and input dilation UD = forward stride) for dgrad.
+//    MFMA "A" operand = weight rows (output channels), "B" operand = gathered pixel rows, so
+//    each lane of a 16x16 accumulator holds 4 consecutive output channels of one pixel -> one
+//    8-byte NHWC store per lane, no LDS round trip in the epilogue.
+//    Both operands are staged through LDS as [row][64 k] bf16 (128-B rows) with a
+//    chunk ^= (row & 7) XOR swizzle: conflict-free ds_write_b128 and ds_read_b128 for the
+//    v_mfma_f32_16x16x32_bf16 fragment pattern (checked by tools/lds_bank_check.py).
+//    Zero padding comes for free from buffer loads with an out-of-range offset.
+//    Optional fusions: per-input-channel affine+ReLU prologue (the previous layer's BatchNorm
+//    apply, so the normalised activation is never written to HBM), bias/ReLU epilogue, and
+//    per-output-channel sum / sum-of-squares for training BatchNorm (fp32 atomics, one per
+//    channel per wave after a 16-lane shuffle reduction).
+//  * conv_wgrad: dW[ko][(r,s,c)] = sum_pix dY[pix][ko] * X[pix @ tap][c].  Both operands are
+//    k(=pixel)-major in memory, so they are staged as [k/4][row/16][4][16] blocks and read with
+//    ds_read_b64_tr_b16 (the CDNA4 hardware transpose) straight into MFMA fragments.
+//    Split-K over pixels; partial tiles are added into the fp32 gradient with float atomics.
+#include "common.h"
+
+namespace dtm {
+
+struct ConvNTArgs {
+  const bf16_t* x;        // [N][Hin][Win][C]
+  const bf16_t* w;        // [K][R][S][C]
+  bf16_t* y;              // [N][P][Q][K]
+  float* stats;           // nullptr or [2][K] : sum, sumsq of the (bf16-rounded) output
+  const float* bias;      // nullptr or [K]
+  const float* in_scale;  // nullptr or [C]: x <- relu(x*in_scale + in_shift) for in-bounds taps
+  const float* in_shift;
+  uint32_t x_bytes, w_bytes;
+  int N, Hin, Win, C, K, R, S, P, Q;
+  int stride, pad_h, pad_w;  // on the virtual (dilated) input
+  int Hv, Wv;                // virtual input extent (Hin-1)*UD+1
+  int M;                     // N*P*Q
+  int Kg;                    // R*S*C
+  int relu;
+  FastDiv fd_PQ, fd_Q;
+};
+
+template <int PT, int CT, int WP, int WC, int UD>
+__global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
+  constexpr int BK = 64;
+  constexpr int NWP = PT / WP;
+  constexpr int NWC = CT / WC;
+  static_assert(NWP * NWC == 4, "4 waves");
+  constexpr int TP = WP / 16, TC = WC / 16;
+  constexpr int ACH = PT / 32;  // act chunks per thread (PT rows * 8 chunks / 256 threads)
+  constexpr int WCH = CT / 32;
+  constexpr int BUF = (PT + CT) * 128;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wp = wave % NWP, wc = wave / NWP;
+  const int p0 = blockIdx.y * PT, c0 = blockIdx.x * CT;
+  const int ch = tid & 7, rb = tid >> 3;
+
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, a.w_bytes);
+
+  // per-row pixel decode (rows rb + 32*i of the pixel tile)
+  int ih0[ACH], iw0[ACH], pixbase[ACH];
+#pragma unroll
+  for (int i = 0; i < ACH; ++i) {
+    int m = p0 + rb + 32 * i;
+    if (m < a.M) {
+      uint32_t n = fdiv((uint32_t)m, a.fd_PQ);
+      uint32_t rem = m - n * (a.P * a.Q);
+      uint32_t p = fdiv(rem, a.fd_Q);
+      uint32_t q = rem - p * a.Q;
+      ih0[i] = (int)p * a.stride - a.pad_h;
+      iw0[i] = (int)q * a.stride - a.pad_w;
+      pixbase[i] = (int)n * a.Hin * a.Win;
+    } else {
+      ih0[i] = -(1 << 28);
+      iw0[i] = -(1 << 28);
+      pixbase[i] = 0;
+    }
+  }
+  // decode of this thread's k chunk for tile 0; advanced incrementally by 64 per tile
+  int kc = ch * 8;
+  int cc = kc % a.C;
+  int tap = kc / a.C;
+  int rr = tap / a.S, ss = tap - (tap / a.S) * a.S;
+
+  uint4 areg[ACH], wreg[WCH];
+  bool avalid[ACH];
+  int acc_c = 0;  // channel of the current act chunk (for the prologue affine)
+
+  auto gload = [&](int kt) {
+    const int k = kt * BK + ch * 8;
+    const bool kin = (k < a.Kg);
+    acc_c = cc;
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      int ihv = ih0[i] + rr, iwv = iw0[i] + ss;
+      bool v = kin && ihv >= 0 && ihv < a.Hv && iwv >= 0 && iwv < a.Wv;
+      if (UD > 1) v = v && ((ihv % UD) == 0) && ((iwv % UD) == 0);
+      int ih = UD > 1 ? ihv / UD : ihv, iw = UD > 1 ? iwv / UD : iwv;
+      uint32_t off = v ? (uint32_t)(((pixbase[i] + ih * a.Win + iw) * a.C + cc) * 2) : OOB_OFFSET;
+      avalid[i] = v;
+      areg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) {
+      int row = c0 + rb + 32 * i;
+      bool v = kin && row < a.K;
+      uint32_t off = v ? (uint32_t)((row * a.Kg + k) * 2) : OOB_OFFSET;
+      wreg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0));
+    }
+    // advance (rr, ss, cc) by BK
+    cc += BK;
+    while (cc >= a.C) {
+      cc -= a.C;
+      if (++ss == a.S) { ss = 0; ++rr; }
+    }
+  };
+
+  auto swrite = [&](int buf) {
+    char* base = smem + buf * BUF;
+    if (a.in_scale) {
+      // fused BatchNorm-apply + ReLU of the previous layer on the gathered input
+      float sc[8], sh[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { sc[e] = a.in_scale[acc_c + e]; sh[e] = a.in_shift[acc_c + e]; }
+#pragma unroll
+      for (int i = 0; i < ACH; ++i) {
+        if (avalid[i]) {
+          uint32_t u[4] = {areg[i].x, areg[i].y, areg[i].z, areg[i].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float lo = fmaxf(fmaf(lo_bf(u[e]), sc[2 * e], sh[2 * e]), 0.f);
+            float hi = fmaxf(fmaf(hi_bf(u[e]), sc[2 * e + 1], sh[2 * e + 1]), 0.f);
+            u[e] = pack2bf(lo, hi);
+          }
+          areg[i] = make_uint4(u[0], u[1], u[2], u[3]);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      int row = rb + 32 * i;
+      *(uint4*)(base + row * 128 + ((ch ^ (row & 7)) << 4)) = areg[i];
+    }
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) {
+      int row = rb + 32 * i;
+      *(uint4*)(base + PT * 128 + row * 128 + ((ch ^ (row & 7)) << 4)) = wreg[i];
+    }
+  };
+
+  f32x4 acc[TC][TP];
+#pragma unroll
+  for (int i = 0; i < TC; ++i)
+#pragma unroll
+    for (int j = 0; j < TP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (a.Kg + BK - 1) / BK;
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+    const char* base = smem + cur * BUF;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      short8 bf[TP], af[TC];
+#pragma unroll
+      for (int j = 0; j < TP; ++j) {
+        int row = wp * WP + j * 16 + fr;
+        int chn = ks * 4 + fk;
+        bf[j] = *(const short8*)(base + row * 128 + ((chn ^ (row & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < TC; ++i) {
+        int row = wc * WC + i * 16 + fr;
+        int chn = ks * 4 + fk;
+        af[i] = *(const short8*)(base + PT * 128 + row * 128 + ((chn ^ (row & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < TC; ++i)
+#pragma unroll
+        for (int j = 0; j < TP; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) swrite(cur ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: lane holds channels (fk*4 .. +3) of pixel fr for every subtile
+#pragma unroll
+  for (int i = 0; i < TC; ++i) {
+    const int kch = c0 + wc * WC + i * 16 + fk * 4;
+    float bsum[4] = {0.f, 0.f, 0.f, 0.f}, bsq[4] = {0.f, 0.f, 0.f, 0.f};
+    float bia[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.bias && kch < a.K) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bia[r] = a.bias[kch + r];
+    }
+#pragma unroll
+    for (int j = 0; j < TP; ++j) {
+      const int m = p0 + wp * WP + j * 16 + fr;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = acc[i][j][r] + bia[r];
+        if (a.relu) v[r] = fmaxf(v[r], 0.f);
+      }
+      uint32_t lo = pack2bf(v[0], v[1]), hi = pack2bf(v[2], v[3]);
+      if (m < a.M && kch < a.K) {
+        *(uint2*)(a.y + (size_t)m * a.K + kch) = make_uint2(lo, hi);
+        if (a.stats) {
+          float q0 = lo_bf(lo), q1 = hi_bf(lo), q2 = lo_bf(hi), q3 = hi_bf(hi);
+          bsum[0] += q0; bsq[0] += q0 * q0;
+          bsum[1] += q1; bsq[1] += q1 * q1;
+          bsum[2] += q2; bsq[2] += q2 * q2;
+          bsum[3] += q3; bsq[3] += q3 * q3;
+        }
+      }
+    }
+    if (a.stats) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          bsum[r] += __shfl_xor(bsum[r], o, 64);
+          bsq[r] += __shfl_xor(bsq[r], o, 64);
+        }
+      }
+      if (fr == 0 && kch < a.K) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          atomicAdd(a.stats + kch + r, bsum[r]);
+          atomicAdd(a.stats + a.K + kch + r, bsq[r]);
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// weight gradient
+struct ConvWgradArgs {
+  const bf16_t* x;   // [N][H][W][C] forward input
+  const bf16_t* dy;  // [N][P][Q][K]
+  float* dw;         // [K][R][S][C] fp32 accumulated
+  const float* in_scale;  // optional prologue affine+relu on x (same as the forward's)
+  const float* in_shift;
+  uint32_t x_bytes, dy_bytes;
+  int N, H, W, C, K, R, S, P, Q, stride, pad_h, pad_w;
+  int Mpix;  // N*P*Q
+  int Kg;    // R*S*C
+  int pix_per_split;
+  FastDiv fd_PQ, fd_Q;
+};
+
+// byte offset of element (k, m) in a [64 k][ROWS] tile stored as [k/4][m/16][4][16] blocks,
+// with bit 7 flipped for odd (k>>3) so that the two 16-lane groups of a transposed-read half
+// wave hit opposite 128-B halves of the 256-B bank row.
+template <int ROWS>
+__device__ __forceinline__ int tr_off(int k, int m) {
+  constexpr int MB = ROWS / 16;
+  int b = (k >> 2) * MB + (m >> 4);
+  return ((b << 7) + ((k & 3) << 5) + ((m & 15) << 1)) ^ (((k >> 3) & 1) << 7);
+}
+
+template <int MT, int NT, int WM, int WN>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
+  constexpr int BK = 64;
+  constexpr int NWM = MT / WM, NWN = NT / WN;
+  static_assert(NWM * NWN == 4, "4 waves");
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int ACH = MT / 32;  // BK*MT/8 chunks / 256 threads
+  constexpr int BCH = NT / 32;
+  constexpr int BUF = BK * (MT + NT) * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % NWM, wn = wave / NWM;
+  const int n0 = blockIdx.x * NT, m0 = blockIdx.y * MT;
+  const int pix_lo = blockIdx.z * a.pix_per_split;
+  const int pix_hi = min(a.Mpix, pix_lo + a.pix_per_split);
+  if (pix_lo >= pix_hi) return;
+
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const __amdgpu_buffer_rsrc_t dr = make_rsrc(a.dy, a.dy_bytes);
+
+  const int sub = tid & 7, kk = sub >> 1, half = sub & 1, grp = tid >> 3;
+  // A (dy) chunk coordinates
+  int a_k[ACH], a_m[ACH];
+#pragma unroll
+  for (int i = 0; i < ACH; ++i) {
+    int G = grp + 32 * i;
+    a_k[i] = (G / (MT / 16)) * 4 + kk;
+    a_m[i] = (G % (MT / 16)) * 16 + half * 8;
+  }
+  // B (x) chunk coordinates; the column -> (r, s, c) decode is fixed for the block
+  int b_k[BCH], b_n[BCH], b_r[BCH], b_s[BCH], b_c[BCH];
+  bool b_colv[BCH];
+#pragma unroll
+  for (int i = 0; i < BCH; ++i) {
+    int G = grp + 32 * i;
+    b_k[i] = (G / (NT / 16)) * 4 + kk;
+    b_n[i] = (G % (NT / 16)) * 16 + half * 8;
+    int col = n0 + b_n[i];
+    b_colv[i] = col < a.Kg;
+    int tap = col / a.C;
+    b_c[i] = col - tap * a.C;
+    b_r[i] = tap / a.S;
+    b_s[i] = tap - b_r[i] * a.S;
+  }
+
+  uint4 areg[ACH], breg[BCH];
+  bool bval[BCH];
+  int bcc[BCH];
+  auto gload = [&](int pbase) {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      int pix = pbase + a_k[i];
+      int ko = m0 + a_m[i];
+      bool v = pix < pix_hi && ko < a.K;
+      uint32_t off = v ? (uint32_t)(((size_t)pix * a.K + ko) * 2) : OOB_OFFSET;
+      areg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(dr, off, 0, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      int pix = pbase + b_k[i];
+      bool v = b_colv[i] && pix < pix_hi;
+      uint32_t n = fdiv((uint32_t)pix, a.fd_PQ);
+      uint32_t rem = pix - n * (a.P * a.Q);
+      uint32_t p = fdiv(rem, a.fd_Q);
+      uint32_t q = rem - p * a.Q;
+      int ih = (int)p * a.stride - a.pad_h + b_r[i];
+      int iw = (int)q * a.stride - a.pad_w + b_s[i];
+      v = v && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+      uint32_t off = v ? (uint32_t)(((((int)n * a.H + ih) * a.W + iw) * a.C + b_c[i]) * 2) : OOB_OFFSET;
+      bval[i] = v;
+      bcc[i] = b_c[i];
+      breg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+    }
+  };
+  auto swrite = [&](int buf) {
+    char* base = smem + buf * BUF;
+    if (a.in_scale) {
+#pragma unroll
+      for (int i = 0; i < BCH; ++i) {
+        if (bval[i]) {
+          uint32_t u[4] = {breg[i].x, breg[i].y, breg[i].z, breg[i].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            int c = bcc[i] + 2 * e;
+            float lo = fmaxf(fmaf(lo_bf(u[e]), a.in_scale[c], a.in_shift[c]), 0.f);
+            float hi = fmaxf(fmaf(hi_bf(u[e]), a.in_scale[c + 1], a.in_shift[c + 1]), 0.f);
+            u[e] = pack2bf(lo, hi);
+          }
+          breg[i] = make_uint4(u[0], u[1], u[2], u[3]);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) *(uint4*)(base + tr_off<MT>(a_k[i], a_m[i])) = areg[i];
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) *(uint4*)(base + BK * MT * 2 + tr_off<NT>(b_k[i], b_n[i])) = breg[i];
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (pix_hi - pix_lo + BK - 1) / BK;
+  gload(pix_lo);
+  swrite(0);
+  __syncthreads();
+  const int g = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
+  typedef __attribute__((address_space(3))) short4v lds_s4;
+  typedef __attribute__((address_space(3))) char lds_c;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload(pix_lo + (kt + 1) * BK);
+    lds_c* lbase = (lds_c*)(smem + cur * BUF);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      short8 af[TM], bfr[TN];
+      const int kb = ks * 32 + 8 * g;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        int m = wm * WM + i * 16 + 4 * tp;
+        short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s4*)(lbase + tr_off<MT>(kb + tq, m)));
+        short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s4*)(lbase + tr_off<MT>(kb + 4 + tq, m)));
+        af[i] = (short8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        int n = wn * WN + j * 16 + 4 * tp;
+        short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s4*)(lbase + BK * MT * 2 + tr_off<NT>(kb + tq, n)));
+        short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s4*)(lbase + BK * MT * 2 + tr_off<NT>(kb + 4 + tq, n)));
+        bfr[j] = (short8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) swrite(cur ^ 1);
+    __syncthreads();
+  }
+  // epilogue: acc rows = ko (4 consecutive per lane), cols = flattened (r,s,c)
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn * WN + j * 16 + li;
+      const int ko = m0 + wm * WM + i * 16 + g * 4;
+      if (col < a.Kg) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (ko + r < a.K) atomicAdd(a.dw + (size_t)(ko + r) * a.Kg + col, acc[i][j][r]);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// weight re-layouts
+// dgrad weight: Wt[c][R-1-r][S-1-s][k] = W[k][r][s][c]   (bf16 -> bf16)
+__global__ void weight_flip_transpose_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wt,
+                                             int K, int R, int S, int C) {
+  size_t total = (size_t)K * R * S * C;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    // i indexes the destination [c][r'][s'][k]
+    int k = i % K;
+    size_t t = i / K;
+    int s2 = t % S; t /= S;
+    int r2 = t % R;
+    int c = t / R;
+    int r = R - 1 - r2, s = S - 1 - s2;
+    wt[i] = w[(((size_t)k * R + r) * S + s) * C + c];
+  }
+}
+
+}  // namespace dtm
+
+using namespace dtm;
+
+// ------------------------------------------------------------------------------------------
+// host launchers (C ABI, called through ctypes; every launch is on the caller's stream so the
+// whole training step can be captured in one hipGraph)
+struct ConvDesc {
+  int N, H, W, C, K, R, S, P, Q, stride, pad_h, pad_w;
+};
+
+template <int PT, int CT, int WP, int WC, int UD>
+static void launch_nt(const ConvNTArgs& a, hipStream_t st) {
+  dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT);
+  hipLaunchKernelGGL((conv_nt_kernel<PT, CT, WP, WC, UD>), grid, dim3(256), 0, st, a);
+}
+
+static void dispatch_nt(const ConvNTArgs& a, int ud, hipStream_t st) {
+  // tile selection: channel tile 64 for narrow layers, pixel tile 128
+  if (ud == 1) {
+    if (a.K <= 64) launch_nt<128, 64, 32, 64, 1>(a, st);
+    else launch_nt<128, 128, 64, 64, 1>(a, st);
+  } else {
+    if (a.K <= 64) launch_nt<128, 64, 32, 64, 2>(a, st);
+    else launch_nt<128, 128, 64, 64, 2>(a, st);
+  }
+}
+
+DTM_API int dtm_conv_fwd(const void* x, const void* w, void* y, float* stats, const float* bias,
+                         const float* in_scale, const float* in_shift, int relu,
+                         const ConvDesc* d, void* stream) {
+  if (d->C % 8 || d->K % 4) return -1;
+  ConvNTArgs a;
+  a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.y = (bf16_t*)y;
+  a.stats = stats; a.bias = bias; a.in_scale = in_scale; a.in_shift = in_shift;
+  size_t xb = (size_t)d->N * d->H * d->W * d->C * 2, wb = (size_t)d->K * d->R * d->S * d->C * 2;
+  if (xb >= (1ull << 31) || wb >= (1ull << 31)) return -2;
+  a.x_bytes = (uint32_t)xb; a.w_bytes = (uint32_t)wb;
+  a.N = d->N; a.Hin = d->H; a.Win = d->W; a.C = d->C; a.K = d->K; a.R = d->R; a.S = d->S;
+  a.P = d->P; a.Q = d->Q; a.stride = d->stride; a.pad_h = d->pad_h; a.pad_w = d->pad_w;
+  a.Hv = d->H; a.Wv = d->W;
+  a.M = d->N * d->P * d->Q; a.Kg = d->R * d->S * d->C; a.relu = relu;
+  a.fd_PQ = make_fastdiv(d->P * d->Q); a.fd_Q = make_fastdiv(d->Q);
+  dispatch_nt(a, 1, (hipStream_t)stream);
+  return 0;
+}
+
+// dgrad: dx[N][H][W][C] from dy[N][P][Q][K] and the flipped/transposed weight wt[C][R][S][K]
+DTM_API int dtm_conv_dgrad(const void* dy, const void* wt, void* dx, const ConvDesc* d, void* stream) {
+  if (d->K % 8 || d->C % 4) return -1;
+  if (d->stride > 2) return -3;
+  ConvNTArgs a;
+  a.x = (const bf16_t*)dy; a.w = (const bf16_t*)wt; a.y = (bf16_t*)dx;
+  a.stats = nullptr; a.bias = nullptr; a.in_scale = nullptr; a.in_shift = nullptr;
+  size_t xb = (size_t)d->N * d->P * d->Q * d->K * 2, wb = (size_t)d->K * d->R * d->S * d->C * 2;
+  if (xb >= (1ull << 31) || wb >= (1ull << 31)) return -2;
+  a.x_bytes = (uint32_t)xb; a.w_bytes = (uint32_t)wb;
+  a.N = d->N; a.Hin = d->P; a.Win = d->Q; a.C = d->K; a.K = d->C; a.R = d->R; a.S = d->S;
+  a.P = d->H; a.Q = d->W; a.stride = 1;
+  a.pad_h = d->R - 1 - d->pad_h; a.pad_w = d->S - 1 - d->pad_w;
+  a.Hv = (d->P - 1) * d->stride + 1; a.Wv = (d->Q - 1) * d->stride + 1;
+  a.M = d->N * d->H * d->W; a.Kg = d->R * d->S * d->K; a.relu = 0;
+  a.fd_PQ = make_fastdiv(d->H * d->W); a.fd_Q = make_fastdiv(d->W);
+  dispatch_nt(a, d->stride, (hipStream_t)stream);
+  return 0;
+}
+
+template <int MT, int NT, int WM, int WN>
+static void launch_wgrad(const ConvWgradArgs& a, int splits, hipStream_t st) {
+  dim3 grid((a.Kg + NT - 1) / NT, (a.K + MT - 1) / MT, splits);
+  hipLaunchKernelGGL((conv_wgrad_kernel<MT, NT, WM, WN>), grid, dim3(256), 0, st, a);
+}
+
+DTM_API int dtm_conv_wgrad(const void* x, const void* dy, float* dw, const float* in_scale,
+                           const float* in_shift, const ConvDesc* d, int num_cus, void* stream) {
+  if (d->C % 8 || d->K % 8) return -1;
+  ConvWgradArgs a;
+  a.x = (const bf16_t*)x; a.dy = (const bf16_t*)dy; a.dw = dw;
+  a.in_scale = in_scale; a.in_shift = in_shift;
+  size_t xb = (size_t)d->N * d->H * d->W * d->C * 2, yb = (size_t)d->N * d->P * d->Q * d->K * 2;
+  if (xb >= (1ull << 31) || yb >= (1ull << 31)) return -2;
+  a.x_bytes = (uint32_t)xb; a.dy_bytes = (uint32_t)yb;
+  a.N = d->N; a.H = d->H; a.W = d->W; a.C = d->C; a.K = d->K; a.R = d->R; a.S = d->S;
+  a.P = d->P; a.Q = d->Q; a.stride = d->stride; a.pad_h = d->pad_h; a.pad_w = d->pad_w;
+  a.Mpix = d->N * d->P * d->Q; a.Kg = d->R * d->S * d->C;
+  a.fd_PQ = make_fastdiv(d->P * d->Q); a.fd_Q = make_fastdiv(d->Q);
+  const bool small_m = d->K <= 64;
+  const int MT = small_m ? 64 : 128, NT = 128;
+  long tiles = (long)((a.Kg + NT - 1) / NT) * ((a.K + MT - 1) / MT);
+  long target = (long)num_cus * 3;
+  long ksteps = (a.Mpix + 63) / 64;
+  long splits = (target + tiles - 1) / tiles;
+  if (splits > ksteps) splits = ksteps;
+  if (splits < 1) splits = 1;
+  long steps_per = (ksteps + splits - 1) / splits;
+  a.pix_per_split = (int)(steps_per * 64);
+  splits = (a.Mpix + a.pix_per_split - 1) / a.pix_per_split;
+  if (small_m) launch_wgrad<64, 128, 32, 64>(a, (int)splits, (hipStream_t)stream);
+  else launch_wgrad<128, 128, 64, 64>(a, (int)splits, (hipStream_t)stream);
+  return 0;
+}
+
+DTM_API void dtm_weight_flip_transpose(const void* w, void* wt, int K, int R, int S, int C, void* stream) {
+  size_t total = (size_t)K * R * S * C;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(weight_flip_transpose_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)w, (bf16_t*)wt, K, R, S, C);
+}

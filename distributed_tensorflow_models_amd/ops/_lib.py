@@ -1,0 +1,109 @@
+"""ctypes binding of the gfx950 kernel library ``_native/libdtm_kernels.so``.
+
+Every entry point launches on the caller's current HIP stream (``torch.cuda.current_stream()``)
+so whole training steps can be captured into a hipGraph.  On a GPU machine a missing library is a
+hard error (no silent eager fallback); on a CPU-only machine the pure-PyTorch reference path in
+``ops.reference`` is used instead.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_HERE, "_native", "libdtm_kernels.so")
+
+_lib = None
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in
+                ("N", "H", "W", "C", "K", "R", "S", "P", "Q", "stride", "pad_h", "pad_w")]
+
+
+class PoolArgs(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in
+                ("N", "H", "W", "C", "P", "Q", "KH", "KW", "SH", "SW", "PH", "PW")]
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_long
+_F = ctypes.c_float
+
+_SIGS = {
+    "dtm_conv_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, ctypes.POINTER(ConvDesc), _P]),
+    "dtm_conv_dgrad": (_I, [_P, _P, _P, ctypes.POINTER(ConvDesc), _P]),
+    "dtm_conv_wgrad": (_I, [_P, _P, _P, _P, _P, ctypes.POINTER(ConvDesc), _I, _P]),
+    "dtm_weight_flip_transpose": (None, [_P, _P, _I, _I, _I, _I, _P]),
+    "dtm_bn_stats": (None, [_P, _P, _L, _I, _P]),
+    "dtm_bn_finalize": (None, [_P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _I, _I, _P]),
+    "dtm_bn_inference_params": (None, [_P, _P, _P, _P, _P, _I, _F, _P]),
+    "dtm_bn_apply": (None, [_P, _P, _P, _P, _P, _L, _I, _I, _I, _P]),
+    "dtm_bn_bwd_reduce": (None, [_P, _P, _P, _P, _P, _L, _I, _I, _P]),
+    "dtm_bn_bwd_apply": (None, [_P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _P]),
+    "dtm_bn_param_grad": (None, [_P, _P, _P, _I, _P]),
+    "dtm_maxpool_fwd": (None, [_P, _P, _P, ctypes.POINTER(PoolArgs), _P]),
+    "dtm_maxpool_bwd": (None, [_P, _P, _P, ctypes.POINTER(PoolArgs), _P]),
+    "dtm_avgpool_fwd": (None, [_P, _P, ctypes.POINTER(PoolArgs), _I, _P]),
+    "dtm_avgpool_bwd": (None, [_P, _P, ctypes.POINTER(PoolArgs), _I, _P]),
+    "dtm_global_avg_fwd": (None, [_P, _P, _I, _I, _I, _P]),
+    "dtm_global_avg_bwd": (None, [_P, _P, _I, _I, _I, _P]),
+    "dtm_softmax_xent": (None, [_P, _I, _P, _P, _P, _I, _I, _F, _F, _P, _P]),
+    "dtm_opt_chunk_size": (_I, []),
+    "dtm_opt_tensor_bytes": (_I, []),
+    "dtm_opt_chunk_bytes": (_I, []),
+    "dtm_multi_tensor_opt": (None, [_P, _P, _I, _I, _F, _F, _F, _F, _F, _F, _I, _P, _P, _P]),
+    "dtm_check_finite": (None, [_P, _L, _P, _P]),
+    "dtm_f32_to_bf16": (None, [_P, _P, _L, _P]),
+    "dtm_scale": (None, [_P, _L, _F, _P]),
+}
+
+
+def gpu_present():
+    try:
+        return torch.cuda.is_available()
+    except Exception:  # pragma: no cover
+        return False
+
+
+def lib():
+    """Load (once) and return the kernel library; raise loudly if it is missing on a GPU box."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                "native kernel library %s is missing: run `python tools/build_native.py` "
+                "(or __graft_entry__.build())" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def available():
+    return os.path.exists(LIB_PATH) and gpu_present()
+
+
+def stream_ptr():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    """Raw device pointer of a tensor (or None)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+_num_cus = None
+
+
+def num_cus():
+    global _num_cus
+    if _num_cus is None:
+        _num_cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    return _num_cus

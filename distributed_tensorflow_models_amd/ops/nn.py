@@ -1,0 +1,372 @@
+"""Autograd front-end of the gfx950 kernels (NHWC bf16 activations, fp32 master params).
+
+Each public function dispatches on the device of its input:
+  * cuda tensors -> hand-written HIP kernels through ``_lib`` (hard error if missing);
+  * cpu tensors  -> ``reference`` (pure torch, autograd by composition).
+
+Weight gradients of conv/linear layers are accumulated straight into ``param.main_grad`` when
+the parameter has one (a view into the flat fp32 gradient buffer that the BSP all-reduce
+buckets and the fused optimizer consume), and ``grad_ready(param)`` hooks are fired so the
+data-parallel engine can launch a bucket's all-reduce while backward continues.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from . import reference as ref
+from .geometry import conv_geom, pool_geom
+
+_grad_ready_hooks = []
+
+
+def add_grad_ready_hook(fn):
+    _grad_ready_hooks.append(fn)
+    return fn
+
+
+def remove_grad_ready_hook(fn):
+    if fn in _grad_ready_hooks:
+        _grad_ready_hooks.remove(fn)
+
+
+def _notify(p):
+    for h in _grad_ready_hooks:
+        h(p)
+
+
+def _accum_param_grad(p, g):
+    """Route a computed fp32 grad for parameter p; returns what autograd should receive."""
+    mg = getattr(p, "main_grad", None)
+    if mg is not None:
+        mg.add_(g)
+        _notify(p)
+        return None
+    return g
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise RuntimeError("%s failed with code %d" % (what, rc))
+
+
+def weight_bf16(w):
+    """bf16 compute copy of a fp32 master weight (kept fresh by the fused optimizer)."""
+    w16 = getattr(w, "bf16", None)
+    if w16 is None or w16.shape != w.shape:
+        w16 = w.detach().to(torch.bfloat16)
+        try:
+            w.bf16 = w16
+        except Exception:
+            pass
+    return w16
+
+
+# ---------------------------------------------------------------------------------------------
+# convolution
+class _Conv2dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, geom, relu):
+        L = _lib.lib()
+        x = x.contiguous()
+        w16 = weight_bf16(w)
+        y = torch.empty((geom.N, geom.P, geom.Q, geom.K), device=x.device, dtype=torch.bfloat16)
+        d = geom.as_desc(_lib.ConvDesc)
+        _check(L.dtm_conv_fwd(_lib.ptr(x), _lib.ptr(w16), _lib.ptr(y), None, _lib.ptr(b), None, None,
+                              int(relu), ctypes.byref(d), _lib.stream_ptr()), "conv_fwd")
+        ctx.geom, ctx.relu, ctx.has_b = geom, relu, b is not None
+        ctx.save_for_backward(x, w, y if relu else None)
+        ctx.bias_param = b
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L = _lib.lib()
+        x, w, y = ctx.saved_tensors
+        g = ctx.geom
+        dy = dy.contiguous()
+        if ctx.relu:
+            dy = torch.where(y > 0, dy, torch.zeros((), dtype=dy.dtype, device=dy.device))
+        d = g.as_desc(_lib.ConvDesc)
+        s = _lib.stream_ptr()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            w16 = weight_bf16(w)
+            wt = torch.empty((g.C, g.R, g.S, g.K), device=dy.device, dtype=torch.bfloat16)
+            L.dtm_weight_flip_transpose(_lib.ptr(w16), _lib.ptr(wt), g.K, g.R, g.S, g.C, s)
+            dx = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
+            _check(L.dtm_conv_dgrad(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), s), "conv_dgrad")
+        dw = None
+        if ctx.needs_input_grad[1]:
+            mg = getattr(w, "main_grad", None)
+            target = mg if mg is not None else torch.zeros(w.shape, device=dy.device, dtype=torch.float32)
+            _check(L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(target), None, None, ctypes.byref(d),
+                                    _lib.num_cus(), s), "conv_wgrad")
+            if mg is not None:
+                _notify(w)
+            else:
+                dw = target
+        db = None
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            gb = dy.reshape(-1, g.K).float().sum(0)
+            db = _accum_param_grad(ctx.bias_param, gb)
+        return dx, dw, db, None, None
+
+
+def conv2d(x, w, bias=None, stride=1, padding="SAME", relu=False, dilation=1):
+    """NHWC conv. x [N,H,W,C]; w fp32 master [K,R,S,C]; bias [K] or None."""
+    if not x.is_cuda:
+        return ref.conv2d(x, w, bias, stride, padding, relu, dilation)
+    if dilation != 1:
+        raise NotImplementedError("dilated conv on the HIP path (atrous output_stride) is not supported yet")
+    g = conv_geom(tuple(x.shape), tuple(w.shape), stride, padding, dilation)
+    if g.C % 8 != 0:
+        # pad input channels with zeros (first layer: RGB) so every gather chunk is 16 B
+        cp = (g.C + 7) // 8 * 8
+        x = torch.nn.functional.pad(x, (0, cp - g.C))
+        w = _PadChannels.apply(w, cp)
+        g = conv_geom(tuple(x.shape), tuple(w.shape), stride, padding, dilation)
+    return _Conv2dFn.apply(x.to(torch.bfloat16), w, bias, g, relu)
+
+
+class _PadChannels(torch.autograd.Function):
+    """Zero-pad the input-channel dim of a fp32 weight; grads flow back to the unpadded master."""
+
+    @staticmethod
+    def forward(ctx, w, cp):
+        ctx.c = w.shape[-1]
+        ctx.src = w
+        out = torch.nn.functional.pad(w, (0, cp - w.shape[-1]))
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        gw = g[..., :ctx.c].contiguous()
+        return _accum_param_grad(ctx.src, gw), None
+
+
+# ---------------------------------------------------------------------------------------------
+# batch norm (+ReLU, +residual)
+class _BatchNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, res, moving_mean, moving_var, training, decay, eps, relu, bessel):
+        L = _lib.lib()
+        s = _lib.stream_ptr()
+        C = x.shape[-1]
+        M = x.numel() // C
+        x = x.contiguous()
+        ss = torch.empty((4, C), device=x.device, dtype=torch.float32)
+        if training:
+            stats = torch.zeros((2, C), device=x.device, dtype=torch.float32)
+            L.dtm_bn_stats(_lib.ptr(x), _lib.ptr(stats), M, C, s)
+            L.dtm_bn_finalize(_lib.ptr(stats), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(moving_mean),
+                              _lib.ptr(moving_var), _lib.ptr(ss), C, float(M), float(eps), float(decay),
+                              int(moving_mean is not None), int(bessel), s)
+        else:
+            L.dtm_bn_inference_params(_lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(moving_mean), _lib.ptr(moving_var),
+                                      _lib.ptr(ss), C, float(eps), s)
+        y = torch.empty_like(x)
+        if res is not None:
+            res = res.contiguous()
+        L.dtm_bn_apply(_lib.ptr(x), _lib.ptr(ss), _lib.ptr(res), None, _lib.ptr(y), M, C,
+                       1 if res is not None else 0, int(relu), s)
+        ctx.training, ctx.relu, ctx.has_res = training, relu, res is not None
+        ctx.gamma, ctx.beta = gamma, beta
+        ctx.save_for_backward(x, ss, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L = _lib.lib()
+        s = _lib.stream_ptr()
+        x, ss, y = ctx.saved_tensors
+        C = x.shape[-1]
+        M = x.numel() // C
+        dy = dy.contiguous()
+        mask_mode = 1 if ctx.relu else 0
+        sums = torch.zeros((2, C), device=x.device, dtype=torch.float32)
+        L.dtm_bn_bwd_reduce(_lib.ptr(dy), _lib.ptr(x), _lib.ptr(y), _lib.ptr(ss), _lib.ptr(sums), M, C, mask_mode, s)
+        dx = torch.empty_like(x)
+        gout = torch.empty_like(x) if ctx.has_res else None
+        L.dtm_bn_bwd_apply(_lib.ptr(dy), _lib.ptr(x), _lib.ptr(y), _lib.ptr(ss), _lib.ptr(sums), _lib.ptr(dx),
+                           _lib.ptr(gout), M, C, mask_mode, int(ctx.training), s)
+        dg = db = None
+        if ctx.gamma is not None and ctx.needs_input_grad[1]:
+            dg = _accum_param_grad(ctx.gamma, sums[1].clone())
+        if ctx.beta is not None and ctx.needs_input_grad[2]:
+            db = _accum_param_grad(ctx.beta, sums[0].clone())
+        return dx, dg, db, gout, None, None, None, None, None, None, None
+
+
+def batch_norm(x, gamma, beta, moving_mean, moving_var, training=True, decay=0.999, eps=1e-3, relu=False,
+               residual=None, bessel=True):
+    if not x.is_cuda:
+        return ref.batch_norm(x, gamma, beta, moving_mean, moving_var, training, decay, eps, relu, residual, bessel)
+    return _BatchNormFn.apply(x.to(torch.bfloat16), gamma, beta,
+                              None if residual is None else residual.to(torch.bfloat16),
+                              moving_mean, moving_var, bool(training), float(decay), float(eps), bool(relu),
+                              bool(bessel))
+
+
+# ---------------------------------------------------------------------------------------------
+# pooling
+class _MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, g):
+        L = _lib.lib()
+        x = x.contiguous()
+        y = torch.empty((g.N, g.P, g.Q, g.C), device=x.device, dtype=x.dtype)
+        arg = torch.empty((g.N, g.P, g.Q, g.C), device=x.device, dtype=torch.uint8)
+        a = g.as_args(_lib.PoolArgs)
+        L.dtm_maxpool_fwd(_lib.ptr(x), _lib.ptr(y), _lib.ptr(arg), ctypes.byref(a), _lib.stream_ptr())
+        ctx.g = g
+        ctx.save_for_backward(arg)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L = _lib.lib()
+        (arg,) = ctx.saved_tensors
+        g = ctx.g
+        dx = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
+        a = g.as_args(_lib.PoolArgs)
+        L.dtm_maxpool_bwd(_lib.ptr(dy.contiguous()), _lib.ptr(arg), _lib.ptr(dx), ctypes.byref(a), _lib.stream_ptr())
+        return dx, None
+
+
+def max_pool(x, kernel, stride, padding="VALID"):
+    if not x.is_cuda:
+        return ref.max_pool(x, kernel, stride, padding)
+    g = pool_geom(tuple(x.shape), kernel, stride, padding)
+    if g.KH * g.KW > 255:
+        raise ValueError("max-pool window too large for the uint8 argmax")
+    return _MaxPoolFn.apply(x.to(torch.bfloat16), g)
+
+
+class _AvgPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, g, count_pad):
+        L = _lib.lib()
+        y = torch.empty((g.N, g.P, g.Q, g.C), device=x.device, dtype=torch.bfloat16)
+        a = g.as_args(_lib.PoolArgs)
+        L.dtm_avgpool_fwd(_lib.ptr(x.contiguous()), _lib.ptr(y), ctypes.byref(a), int(count_pad), _lib.stream_ptr())
+        ctx.g, ctx.cp = g, count_pad
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L = _lib.lib()
+        g = ctx.g
+        dx = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
+        a = g.as_args(_lib.PoolArgs)
+        L.dtm_avgpool_bwd(_lib.ptr(dy.contiguous()), _lib.ptr(dx), ctypes.byref(a), int(ctx.cp), _lib.stream_ptr())
+        return dx, None, None
+
+
+def avg_pool(x, kernel, stride, padding="VALID", count_pad=False):
+    if not x.is_cuda:
+        return ref.avg_pool(x, kernel, stride, padding, count_pad)
+    g = pool_geom(tuple(x.shape), kernel, stride, padding)
+    return _AvgPoolFn.apply(x.to(torch.bfloat16), g, bool(count_pad))
+
+
+class _GlobalAvgFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        L = _lib.lib()
+        N, H, W, C = x.shape
+        y = torch.empty((N, C), device=x.device, dtype=torch.float32)
+        L.dtm_global_avg_fwd(_lib.ptr(x.contiguous()), _lib.ptr(y), N, H * W, C, _lib.stream_ptr())
+        ctx.shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L = _lib.lib()
+        N, H, W, C = ctx.shape
+        dx = torch.empty((N, H, W, C), device=dy.device, dtype=torch.bfloat16)
+        L.dtm_global_avg_bwd(_lib.ptr(dy.float().contiguous()), _lib.ptr(dx), N, H * W, C, _lib.stream_ptr())
+        return dx
+
+
+def global_avg_pool(x):
+    """mean over H, W -> [N, C] fp32."""
+    if not x.is_cuda:
+        return ref.global_avg_pool(x)
+    return _GlobalAvgFn.apply(x.to(torch.bfloat16))
+
+
+# ---------------------------------------------------------------------------------------------
+# loss
+class _SoftmaxXentFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, smoothing, row_weight):
+        L = _lib.lib()
+        logits = logits.contiguous()
+        B, K = logits.shape
+        loss = torch.empty((B,), device=logits.device, dtype=torch.float32)
+        dl = torch.empty_like(logits)
+        lab = labels.to(torch.int32).contiguous()
+        L.dtm_softmax_xent(_lib.ptr(logits), int(logits.dtype == torch.bfloat16), _lib.ptr(lab), _lib.ptr(loss),
+                           _lib.ptr(dl), B, K, float(smoothing), 1.0,
+                           _lib.ptr(row_weight.float().contiguous()) if row_weight is not None else None,
+                           _lib.stream_ptr())
+        ctx.save_for_backward(dl)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gl):
+        (dl,) = ctx.saved_tensors
+        return (dl.float() * gl.view(-1, 1)).to(dl.dtype), None, None, None
+
+
+def softmax_cross_entropy(logits, labels, smoothing=0.0, row_weight=None):
+    """Per-row softmax cross-entropy with TF label smoothing."""
+    if not logits.is_cuda:
+        return ref.softmax_cross_entropy(logits, labels, smoothing, row_weight)
+    if logits.dtype not in (torch.float32, torch.bfloat16):
+        logits = logits.float()
+    return _SoftmaxXentFn.apply(logits, labels, float(smoothing), row_weight)
+
+
+# ---------------------------------------------------------------------------------------------
+# fully connected (plain library GEMM on hipBLASLt; fp32 master + bf16 compute copy)
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, relu):
+        w16 = weight_bf16(w)
+        x16 = x.to(torch.bfloat16)
+        y = x16 @ w16  # w stored TF-style [in, out]
+        if b is not None:
+            y = y + b.to(torch.bfloat16)
+        if relu:
+            y = torch.relu(y)
+        ctx.save_for_backward(x16, w, y if relu else None)
+        ctx.b, ctx.relu = b, relu
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x16, w, y = ctx.saved_tensors
+        if ctx.relu:
+            dy = torch.where(y > 0, dy, torch.zeros((), dtype=dy.dtype, device=dy.device))
+        dy16 = dy.to(torch.bfloat16)
+        dx = dy16 @ weight_bf16(w).t() if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            gw = (x16.t() @ dy16).float()
+            dw = _accum_param_grad(w, gw)
+        db = None
+        if ctx.b is not None and ctx.needs_input_grad[2]:
+            db = _accum_param_grad(ctx.b, dy16.float().sum(0))
+        return dx, dw, db, None
+
+
+def linear(x, w, b=None, relu=False):
+    """x [B, in] @ w [in, out] (+b)."""
+    if not x.is_cuda:
+        y = x.float() @ w
+        if b is not None:
+            y = y + b
+        return torch.relu(y) if relu else y
+    return _LinearFn.apply(x, w, b, bool(relu))

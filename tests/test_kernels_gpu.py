@@ -1,0 +1,121 @@
+"""Numerics of the HIP kernels against plain PyTorch fp32 references (GPU only)."""
+import pytest
+import torch
+
+from distributed_tensorflow_models_amd.ops import nn as dnn
+from distributed_tensorflow_models_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+CONV_CASES = [
+    # N, H, W, C, K, R, stride, padding
+    (2, 14, 14, 64, 64, 3, 1, "SAME"),
+    (2, 14, 14, 64, 128, 1, 1, "SAME"),
+    (2, 15, 15, 32, 64, 3, 2, "SAME"),      # asymmetric SAME
+    (2, 16, 16, 64, 64, 3, 2, (1, 1)),       # conv2d_same style explicit pad
+    (2, 9, 9, 128, 256, 3, 1, "VALID"),
+    (2, 32, 32, 3, 64, 7, 2, (3, 3)),        # stem (C=3 -> padded)
+    (3, 7, 7, 512, 512, 3, 1, "SAME"),
+    (2, 8, 8, 256, 1000, 1, 1, "SAME"),      # K not a multiple of the tile
+    (1, 17, 17, 192, 160, (1, 7)[0], 1, "SAME"),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_bwd(case):
+    torch.manual_seed(0)
+    N, H, W, C, K, R, st, pad = case
+    x = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16).float()
+    w = (torch.randn(K, R, R, C, device=DEV) * (1.0 / (R * R * C) ** 0.5)).to(torch.bfloat16).float()
+    xr = x.clone().requires_grad_()
+    wr = w.clone().requires_grad_()
+    yr = ref.conv2d(xr, wr, None, st, pad)
+    gy = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(gy)
+
+    xk = x.to(torch.bfloat16).requires_grad_()
+    wk = w.clone().requires_grad_()
+    yk = dnn.conv2d(xk, wk, None, st, pad)
+    assert yk.shape == yr.shape
+    yk.backward(gy.to(torch.bfloat16))
+    torch.cuda.synchronize()
+    assert _rel(yk, yr) < 1e-2
+    assert _rel(xk.grad, xr.grad) < 1e-2
+    assert _rel(wk.grad, wr.grad) < 1e-2
+
+
+def test_conv_bias_relu_and_stats_free():
+    torch.manual_seed(1)
+    x = torch.randn(2, 12, 12, 64, device=DEV).to(torch.bfloat16).float()
+    w = (torch.randn(96, 3, 3, 64, device=DEV) * 0.05).to(torch.bfloat16).float()
+    b = torch.randn(96, device=DEV)
+    yr = ref.conv2d(x, w, b, 1, "SAME", relu=True)
+    yk = dnn.conv2d(x.to(torch.bfloat16), w, b, 1, "SAME", relu=True)
+    assert _rel(yk, yr) < 1e-2
+
+
+@pytest.mark.parametrize("C,relu,res", [(64, True, False), (256, False, True), (40, True, True), (2048, True, False)])
+def test_batch_norm(C, relu, res):
+    torch.manual_seed(2)
+    x = (torch.randn(4, 7, 7, C, device=DEV) * 2 + 0.5).to(torch.bfloat16).float()
+    g = torch.rand(C, device=DEV) + 0.5
+    b = torch.randn(C, device=DEV)
+    r = torch.randn_like(x).to(torch.bfloat16).float() if res else None
+    mm_r, mv_r = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    mm_k, mv_k = mm_r.clone(), mv_r.clone()
+    xr, gr, br = x.clone().requires_grad_(), g.clone().requires_grad_(), b.clone().requires_grad_()
+    rr = r.clone().requires_grad_() if res else None
+    yr = ref.batch_norm(xr, gr, br, mm_r, mv_r, True, 0.9, 1e-3, relu, rr)
+    gy = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(gy)
+    xk, gk, bk = x.to(torch.bfloat16).requires_grad_(), g.clone().requires_grad_(), b.clone().requires_grad_()
+    rk = r.to(torch.bfloat16).requires_grad_() if res else None
+    yk = dnn.batch_norm(xk, gk, bk, mm_k, mv_k, True, 0.9, 1e-3, relu, rk)
+    yk.backward(gy.to(torch.bfloat16))
+    assert _rel(yk, yr) < 1e-2
+    assert _rel(xk.grad, xr.grad) < 2e-2
+    assert _rel(gk.grad, gr.grad) < 1e-2
+    assert _rel(bk.grad, br.grad) < 1e-2
+    assert _rel(mm_k, mm_r) < 1e-4 and _rel(mv_k, mv_r) < 1e-4
+    if res:
+        assert _rel(rk.grad, rr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("k,s,pad", [(3, 2, "SAME"), (2, 2, "VALID"), (3, 2, "VALID"), (1, 2, "VALID"), (3, 1, "SAME")])
+def test_pools(k, s, pad):
+    torch.manual_seed(3)
+    x = torch.randn(2, 13, 13, 64, device=DEV).to(torch.bfloat16).float()
+    for fk, fr in ((dnn.max_pool, ref.max_pool), (dnn.avg_pool, ref.avg_pool)):
+        xr = x.clone().requires_grad_()
+        yr = fr(xr, k, s, pad)
+        gy = torch.randn_like(yr).to(torch.bfloat16).float()
+        yr.backward(gy)
+        xk = x.to(torch.bfloat16).requires_grad_()
+        yk = fk(xk, k, s, pad)
+        yk.backward(gy.to(torch.bfloat16))
+        assert _rel(yk, yr) < 1e-2
+        assert _rel(xk.grad, xr.grad) < 1e-2
+
+
+def test_global_avg_and_xent():
+    torch.manual_seed(4)
+    x = torch.randn(8, 7, 7, 256, device=DEV).to(torch.bfloat16).float()
+    xr = x.clone().requires_grad_()
+    xk = x.to(torch.bfloat16).requires_grad_()
+    pr, pk = ref.global_avg_pool(xr), dnn.global_avg_pool(xk)
+    assert _rel(pk, pr) < 1e-3
+    lab = torch.randint(0, 256, (8,), device=DEV)
+    lr_ = ref.softmax_cross_entropy(pr, lab, 0.1).mean()
+    lk = dnn.softmax_cross_entropy(pk, lab, 0.1).mean()
+    assert abs(lr_.item() - lk.item()) < 1e-3
+    lr_.backward()
+    lk.backward()
+    assert _rel(xk.grad, xr.grad) < 1e-2
