@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-50 v1 (slim geometry) 224x224 bf16 training images/sec on MI355X.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it is launched with
+torch.distributed.run, one rank per GPU, RCCL over xGMI.  W untimed warmup steps, then exactly K
+timed steps bracketed by barrier + device synchronize; the max wall time over ranks is used;
+rank 0 prints ONE JSON line.  Weak scaling: the per-GPU batch is fixed as N grows.
+
+Every timed step is a full training step: forward, softmax-xent loss, backward (hand-written HIP
+conv/BN/pool kernels), bucketed RCCL all-reduce of all 25.6 M gradients (N > 1), and the fused
+momentum-SGD + weight-decay update of every parameter.  Data: synthetic ImageNet-shaped batch
+(random bf16 images, random labels) resident in HBM; weights random-init (no checkpoints/datasets).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+BASELINE_VALUE = None  # the reference publishes no ResNet-50 images/sec
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--model", default="resnet_v1_50")
+    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--graph", type=int, default=0, help="capture the step in a hipGraph")
+    ap.add_argument("--profile-steps", type=int, default=0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+
+    from distributed_tensorflow_models_amd.engine import TrainStep
+    from distributed_tensorflow_models_amd.models import nets_factory
+
+    torch.manual_seed(1234 + rank)
+    net = nets_factory.build(args.model, num_classes=1000).to(dev)
+    B = args.batch
+    step = TrainStep(net, optimizer="momentum", lr=0.1 * world, momentum=0.9, bucket_mb=args.bucket_mb,
+                     label_smoothing=0.0, use_graph=bool(args.graph))
+    S = args.image_size
+    images = torch.randn(B, S, S, 3, device=dev).to(torch.bfloat16)
+    labels = torch.randint(0, 1000, (B,), device=dev)
+
+    for _ in range(args.warmup):
+        step(images, labels)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step(images, labels)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms = dt / args.steps * 1000.0
+    value = world * B * args.steps / dt
+    if rank == 0:
+        out = {
+            "metric": "images/sec (whole node) ResNet-50 224x224 bf16 training",
+            "value": round(value, 2),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
+            "dtype": "bf16",
+            "data": "synthetic (random 224x224x3 bf16 images, random labels, random-init weights)",
+            "config": {"model": args.model, "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
+                       "image_size": S, "parallelism": "dp%d" % world, "optimizer": "momentum-sgd+wd1e-4",
+                       "final_loss": round(float(loss), 4)},
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -287,6 +287,226 @@ __global__ void bn_param_grad_kernel(const float* __restrict__ sums, float* __re
   if (dbeta) dbeta[c] += sums[c];
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Bandwidth-oriented variants for C % 8 == 0 and 256 % (C/8) == 0 (every ResNet/VGG width):
+// each lane owns one fixed 8-channel column (per-channel parameters live in registers) and walks
+// rows with stride 256/(C/8); U independent 16-B loads are in flight per lane.
+constexpr int FU = 4;
+
+__device__ __forceinline__ void unpack8(uint4 u, float* f) {
+  f[0] = lo_bf(u.x); f[1] = hi_bf(u.x); f[2] = lo_bf(u.y); f[3] = hi_bf(u.y);
+  f[4] = lo_bf(u.z); f[5] = hi_bf(u.z); f[6] = lo_bf(u.w); f[7] = hi_bf(u.w);
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  return make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
+}
+
+// LDS reduction of per-lane [8] partials over the RP row-lanes of each column, then atomics
+// out0/out1 point into this block's partial row of the workspace (plain stores; see workspace.hip)
+__device__ __forceinline__ void col_reduce_commit(float (*red)[256][8], const float* s, const float* q, float* out0,
+                                                  float* out1, int cols, int c0) {
+  const int t = threadIdx.x, RP = 256 / cols;
+  if (RP == 1) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { out0[c0 + e] = s[e]; out1[c0 + e] = q[e]; }
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[0][t][e] = s[e]; red[1][t][e] = q[e]; }
+  __syncthreads();
+  // tree over row-lanes: lane t (< 256/2^k) adds partner t + 256/2^(k+1) of the same column
+  for (int h = 128; h >= cols; h >>= 1) {
+    if (t < h) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { red[0][t][e] += red[0][t + h][e]; red[1][t][e] += red[1][t + h][e]; }
+    }
+    __syncthreads();
+  }
+  if (t < cols) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { out0[c0 + e] = red[0][t][e]; out1[c0 + e] = red[1][t][e]; }
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_stats_fast(const bf16_t* __restrict__ x, float* __restrict__ stats, int M,
+                                                     int C, int rpb) {
+  __shared__ float red[2][256][8];
+  const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t & (cols - 1)) * 8;
+  const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
+  float s[8], q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.f;
+  for (int r = r0 + t / cols; r < r1; r += RP * FU) {
+    uint4 v[FU];
+#pragma unroll
+    for (int u = 0; u < FU; ++u) {
+      int rr = r + u * RP;
+      v[u] = rr < r1 ? *(const uint4*)(x + (size_t)rr * C + c0) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < FU; ++u) {
+      float f[8]; unpack8(v[u], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s[e] += f[e]; q[e] += f[e] * f[e]; }
+    }
+  }
+  col_reduce_commit(red, s, q, stats + (size_t)blockIdx.x * 2 * C, stats + (size_t)blockIdx.x * 2 * C + C, cols, c0);
+}
+
+__global__ __launch_bounds__(256) void bn_apply_fast(const bf16_t* __restrict__ x, const float* __restrict__ ss,
+                                                     const bf16_t* __restrict__ res, const float* __restrict__ rss,
+                                                     bf16_t* __restrict__ y, int M, int C, int res_mode, int relu, int rpb) {
+  const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t & (cols - 1)) * 8;
+  float sc[8], sh[8], rsc[8], rsh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = ss[c0 + e]; sh[e] = ss[C + c0 + e];
+    rsc[e] = res_mode == 2 ? rss[c0 + e] : 1.f;
+    rsh[e] = res_mode == 2 ? rss[C + c0 + e] : 0.f;
+  }
+  const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
+  for (int r = r0 + t / cols; r < r1; r += RP * FU) {
+    uint4 v[FU], w[FU];
+#pragma unroll
+    for (int u = 0; u < FU; ++u) {
+      int rr = r + u * RP;
+      bool ok = rr < r1;
+      v[u] = ok ? *(const uint4*)(x + (size_t)rr * C + c0) : make_uint4(0, 0, 0, 0);
+      if (res_mode) w[u] = ok ? *(const uint4*)(res + (size_t)rr * C + c0) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < FU; ++u) {
+      int rr = r + u * RP;
+      if (rr >= r1) break;
+      float f[8]; unpack8(v[u], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = fmaf(f[e], sc[e], sh[e]);
+      if (res_mode) {
+        float g[8]; unpack8(w[u], g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] += fmaf(g[e], rsc[e], rsh[e]);
+      }
+      if (relu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
+      }
+      *(uint4*)(y + (size_t)rr * C + c0) = pack8(f);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_reduce_fast(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                          const bf16_t* __restrict__ ym, const float* __restrict__ ss,
+                                                          float* __restrict__ sums, int M, int C, int mask_mode, int rpb) {
+  __shared__ float red[2][256][8];
+  const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t & (cols - 1)) * 8;
+  float sc[8], sh[8], mu[8], rs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = ss[c0 + e]; sh[e] = ss[C + c0 + e]; mu[e] = ss[2 * C + c0 + e]; rs[e] = ss[3 * C + c0 + e];
+  }
+  const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
+  float s[8], q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.f;
+  for (int r = r0 + t / cols; r < r1; r += RP * FU) {
+    uint4 a[FU], b[FU], m[FU];
+#pragma unroll
+    for (int u = 0; u < FU; ++u) {
+      int rr = r + u * RP;
+      bool ok = rr < r1;
+      size_t o = (size_t)rr * C + c0;
+      a[u] = ok ? *(const uint4*)(dy + o) : make_uint4(0, 0, 0, 0);
+      b[u] = ok ? *(const uint4*)(x + o) : make_uint4(0, 0, 0, 0);
+      if (mask_mode == 1) m[u] = ok ? *(const uint4*)(ym + o) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < FU; ++u) {
+      float g[8], xv[8];
+      unpack8(a[u], g); unpack8(b[u], xv);
+      if (mask_mode == 1) {
+        float mv[8]; unpack8(m[u], mv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = mv[e] > 0.f ? g[e] : 0.f;
+      } else if (mask_mode == 2) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = fmaf(xv[e], sc[e], sh[e]) > 0.f ? g[e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s[e] += g[e]; q[e] += g[e] * (xv[e] - mu[e]) * rs[e]; }
+    }
+  }
+  col_reduce_commit(red, s, q, sums + (size_t)blockIdx.x * 2 * C, sums + (size_t)blockIdx.x * 2 * C + C, cols, c0);
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_fast(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                         const bf16_t* __restrict__ ym, const float* __restrict__ ss,
+                                                         const float* __restrict__ sums, bf16_t* __restrict__ dx,
+                                                         bf16_t* __restrict__ gout, int M, int C, int mask_mode,
+                                                         int training, int rpb) {
+  const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t & (cols - 1)) * 8;
+  const float invM = 1.f / (float)M;
+  float sc[8], sh[8], mu[8], rs[8], A[8], Bq[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = ss[c0 + e]; sh[e] = ss[C + c0 + e]; mu[e] = ss[2 * C + c0 + e]; rs[e] = ss[3 * C + c0 + e];
+    A[e] = training ? sums[c0 + e] * invM : 0.f;
+    Bq[e] = training ? sums[C + c0 + e] * invM : 0.f;
+  }
+  const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
+  for (int r = r0 + t / cols; r < r1; r += RP * FU) {
+    uint4 a[FU], b[FU], m[FU];
+#pragma unroll
+    for (int u = 0; u < FU; ++u) {
+      int rr = r + u * RP;
+      bool ok = rr < r1;
+      size_t o = (size_t)rr * C + c0;
+      a[u] = ok ? *(const uint4*)(dy + o) : make_uint4(0, 0, 0, 0);
+      b[u] = ok ? *(const uint4*)(x + o) : make_uint4(0, 0, 0, 0);
+      if (mask_mode == 1) m[u] = ok ? *(const uint4*)(ym + o) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < FU; ++u) {
+      int rr = r + u * RP;
+      if (rr >= r1) break;
+      size_t o = (size_t)rr * C + c0;
+      float g[8], xv[8];
+      unpack8(a[u], g); unpack8(b[u], xv);
+      if (mask_mode == 1) {
+        float mv[8]; unpack8(m[u], mv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = mv[e] > 0.f ? g[e] : 0.f;
+      } else if (mask_mode == 2) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = fmaf(xv[e], sc[e], sh[e]) > 0.f ? g[e] : 0.f;
+      }
+      if (gout) *(uint4*)(gout + o) = pack8(g);
+      float d[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = sc[e] * (g[e] - A[e] - (xv[e] - mu[e]) * rs[e] * Bq[e]);
+      *(uint4*)(dx + o) = pack8(d);
+    }
+  }
+}
+
+static bool fast_ok(long M, int C) {
+  if (C % 8) return false;
+  int cols = C / 8;
+  return cols <= 256 && (256 % cols) == 0 && M < (1l << 31) && M * (long)C < (1l << 40);
+}
+// grid / rows-per-block for the column-fixed kernels: >= ~8 chunks per lane, <= 2048 blocks
+static void fast_grid(long M, int C, int* blocks, int* rpb) {
+  int cols = C / 8, RP = 256 / cols;
+  long chunks = M * cols;
+  long b = chunks / (256 * 8);
+  if (b < 1) b = 1;
+  if (b > 2048) b = 2048;
+  long r = (M + b - 1) / b;
+  r = (r + RP - 1) / RP * RP;
+  *rpb = (int)r;
+  *blocks = (int)((M + r - 1) / r);
+}
 }  // namespace dtm
 using namespace dtm;
 
@@ -302,6 +522,13 @@ static long rows_per_block_for(long M, int C) {
 }
 
 DTM_API void dtm_bn_stats(const void* x, float* stats, long M, int C, void* stream) {
+  if (fast_ok(M, C)) {
+    int blocks, rpb; fast_grid(M, C, &blocks, &rpb);
+    float* ws = dtm_ws_get((size_t)blocks * 2 * C);
+    hipLaunchKernelGGL(bn_stats_fast, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ws, (int)M, C, rpb);
+    dtm_reduce_rows(ws, blocks, 2 * C, 2 * C, stats, (hipStream_t)stream);
+    return;
+  }
   long rpb = rows_per_block_for(M, C);
   int blocks = (int)((M + rpb - 1) / rpb);
   if (C % 8 == 0)
@@ -325,6 +552,12 @@ DTM_API void dtm_bn_inference_params(const float* gamma, const float* beta, cons
 
 DTM_API void dtm_bn_apply(const void* x, const float* ss, const void* res, const float* rss, void* y, long M, int C,
                           int res_mode, int relu, void* stream) {
+  if (fast_ok(M, C)) {
+    int blocks, rpb; fast_grid(M, C, &blocks, &rpb);
+    hipLaunchKernelGGL(bn_apply_fast, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ss,
+                       (const bf16_t*)res, rss, (bf16_t*)y, (int)M, C, res_mode, relu, rpb);
+    return;
+  }
   if (C % 8 == 0)
     hipLaunchKernelGGL(bn_apply_kernel<8>, dim3(grid_for(M * C / 8)), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)x, ss, (const bf16_t*)res, rss, (bf16_t*)y, M, C, res_mode, relu);
@@ -335,6 +568,14 @@ DTM_API void dtm_bn_apply(const void* x, const float* ss, const void* res, const
 
 DTM_API void dtm_bn_bwd_reduce(const void* dy, const void* x, const void* ymask, const float* ss, float* sums, long M,
                                int C, int mask_mode, void* stream) {
+  if (fast_ok(M, C)) {
+    int blocks, rpb; fast_grid(M, C, &blocks, &rpb);
+    float* ws = dtm_ws_get((size_t)blocks * 2 * C);
+    hipLaunchKernelGGL(bn_bwd_reduce_fast, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
+                       (const bf16_t*)x, (const bf16_t*)ymask, ss, ws, (int)M, C, mask_mode, rpb);
+    dtm_reduce_rows(ws, blocks, 2 * C, 2 * C, sums, (hipStream_t)stream);
+    return;
+  }
   long rpb = rows_per_block_for(M, C);
   int blocks = (int)((M + rpb - 1) / rpb);
   if (C % 8 == 0)
@@ -347,6 +588,13 @@ DTM_API void dtm_bn_bwd_reduce(const void* dy, const void* x, const void* ymask,
 
 DTM_API void dtm_bn_bwd_apply(const void* dy, const void* x, const void* ymask, const float* ss, const float* sums,
                               void* dx, void* gout, long M, int C, int mask_mode, int training, void* stream) {
+  if (fast_ok(M, C)) {
+    int blocks, rpb; fast_grid(M, C, &blocks, &rpb);
+    hipLaunchKernelGGL(bn_bwd_apply_fast, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
+                       (const bf16_t*)x, (const bf16_t*)ymask, ss, sums, (bf16_t*)dx, (bf16_t*)gout, (int)M, C,
+                       mask_mode, training, rpb);
+    return;
+  }
   if (C % 8 == 0)
     hipLaunchKernelGGL(bn_bwd_apply_kernel<8>, dim3(grid_for(M * C / 8)), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)ymask, ss, sums, (bf16_t*)dx, (bf16_t*)gout,

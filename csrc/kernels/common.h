@@ -54,3 +54,7 @@ __host__ static inline FastDiv make_fastdiv(uint32_t d) {
   f.m = (uint32_t)m; f.s = s;
   return f;
 }
+
+// workspace arena + two-stage reduction (workspace.hip)
+float* dtm_ws_get(size_t floats);
+void dtm_reduce_rows(const float* ws, int rows, int width, int ld, float* out, hipStream_t st);

@@ -235,12 +235,11 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
           bsq[r] += __shfl_xor(bsq[r], o, 64);
         }
       }
+      // one partial row per (pixel tile, pixel wave): [sum(K) | sumsq(K)], reduced by reduce_rows
       if (fr == 0 && kch < a.K) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          atomicAdd(a.stats + kch + r, bsum[r]);
-          atomicAdd(a.stats + a.K + kch + r, bsq[r]);
-        }
+        float* row = a.stats + (size_t)(blockIdx.y * NWP + wp) * (2 * a.K);
+        *(float4*)(row + kch) = make_float4(bsum[0], bsum[1], bsum[2], bsum[3]);
+        *(float4*)(row + a.K + kch) = make_float4(bsq[0], bsq[1], bsq[2], bsq[3]);
       }
     }
   }
@@ -497,7 +496,16 @@ DTM_API int dtm_conv_fwd(const void* x, const void* w, void* y, float* stats, co
   a.Hv = d->H; a.Wv = d->W;
   a.M = d->N * d->P * d->Q; a.Kg = d->R * d->S * d->C; a.relu = relu;
   a.fd_PQ = make_fastdiv(d->P * d->Q); a.fd_Q = make_fastdiv(d->Q);
+  int rows = 0;
+  if (stats) {
+    const int nwp = d->K <= 64 ? 4 : 2;  // pixel waves of the tile chosen by dispatch_nt
+    rows = ((a.M + 127) / 128) * nwp;
+    float* ws = dtm_ws_get((size_t)rows * 2 * d->K);
+    if (!ws) return -4;
+    a.stats = ws;
+  }
   dispatch_nt(a, 1, (hipStream_t)stream);
+  if (stats) dtm_reduce_rows(a.stats, rows, 2 * d->K, 2 * d->K, stats, (hipStream_t)stream);
   return 0;
 }
 

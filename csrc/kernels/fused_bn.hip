@@ -1,0 +1,226 @@
+// BatchNorm decomposed for conv fusion (training mode):
+//   stats (sum, sumsq)  <- conv epilogue          (no separate statistics pass)
+//   ss = finalize(stats, gamma, beta)             (per-channel, tiny; updates moving averages)
+//   a  = relu(x*scale + shift)                    <- next conv's operand prologue (never stored)
+//        or y = act(x*scale + shift + residual)   <- bn_apply (block outputs)
+// Backward mirrors it:
+//   bn_apply_bwd:  g = dy*[y>0];  dx = g*scale;  dres = g (or g*rscale);  sums (Σg·x, Σg) for dss
+//   act_bwd:       same for the prologue-fused activation (mask recomputed from x)
+//   finalize_bwd:  dss -> (dsum, dsumsq), dgamma, dbeta
+//   stats_combine: dx_total = dx + dsum + 2*x*dsumsq   (the gradient through the statistics)
+// Together these equal the textbook BN backward dx = scale*(g - mean(g) - xhat*mean(g*xhat)).
+// Lane mapping: one fixed 8-channel column per lane (parameters in registers), 16-B accesses.
+#include "common.h"
+
+namespace dtm {
+
+constexpr int FU2 = 4;
+
+__device__ __forceinline__ void up8(uint4 u, float* f) {
+  f[0] = lo_bf(u.x); f[1] = hi_bf(u.x); f[2] = lo_bf(u.y); f[3] = hi_bf(u.y);
+  f[4] = lo_bf(u.z); f[5] = hi_bf(u.z); f[6] = lo_bf(u.w); f[7] = hi_bf(u.w);
+}
+__device__ __forceinline__ uint4 pk8(const float* f) {
+  return make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
+}
+
+__device__ __forceinline__ void reduce_commit2(float (*red)[256][8], const float* s, const float* q, float* out0,
+                                               float* out1, int cols, int c0) {
+  const int t = threadIdx.x, RP = 256 / cols;
+  if (RP == 1) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { out0[c0 + e] = s[e]; out1[c0 + e] = q[e]; }
+    return;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[0][t][e] = s[e]; red[1][t][e] = q[e]; }
+  __syncthreads();
+  for (int h = 128; h >= cols; h >>= 1) {
+    if (t < h) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { red[0][t][e] += red[0][t + h][e]; red[1][t][e] += red[1][t + h][e]; }
+    }
+    __syncthreads();
+  }
+  if (t < cols) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { out0[c0 + e] = red[0][t][e]; out1[c0 + e] = red[1][t][e]; }
+  }
+}
+
+// y = act(x) path backward.  mode: 0 = plain BN (no relu), 1 = relu with mask from y, 2 = relu with
+// mask recomputed from x*scale+shift.  res_mode 0/1/2 as in bn_apply.
+// sx: [2][C] += (Σ g·x, Σ g)  (the dss of x's BN);  sr: same for a BN'd residual.
+__global__ __launch_bounds__(256) void bn_apply_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                                                           const bf16_t* __restrict__ x, const float* __restrict__ ss,
+                                                           const bf16_t* __restrict__ r, const float* __restrict__ rss,
+                                                           bf16_t* __restrict__ dx, bf16_t* __restrict__ dres,
+                                                           float* __restrict__ sx, float* __restrict__ sr, int M, int C,
+                                                           int mode, int res_mode, int rpb) {
+  __shared__ float red[2][256][8];
+  const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t & (cols - 1)) * 8;
+  float sc[8], sh[8], rsc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = ss[c0 + e]; sh[e] = ss[C + c0 + e];
+    rsc[e] = res_mode == 2 ? rss[c0 + e] : 1.f;
+  }
+  float a1[8], a0[8], b1[8], b0[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a1[e] = a0[e] = b1[e] = b0[e] = 0.f;
+  const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
+  for (int row = r0 + t / cols; row < r1; row += RP * FU2) {
+    uint4 vdy[FU2], vy[FU2], vx[FU2], vr[FU2];
+#pragma unroll
+    for (int u = 0; u < FU2; ++u) {
+      int rr = row + u * RP;
+      bool ok = rr < r1;
+      size_t o = (size_t)rr * C + c0;
+      uint4 z = make_uint4(0, 0, 0, 0);
+      vdy[u] = ok ? *(const uint4*)(dy + o) : z;
+      vx[u] = ok ? *(const uint4*)(x + o) : z;
+      if (mode == 1) vy[u] = ok ? *(const uint4*)(y + o) : z;
+      if (res_mode == 2) vr[u] = ok ? *(const uint4*)(r + o) : z;
+    }
+#pragma unroll
+    for (int u = 0; u < FU2; ++u) {
+      int rr = row + u * RP;
+      if (rr >= r1) break;
+      size_t o = (size_t)rr * C + c0;
+      float g[8], xv[8];
+      up8(vdy[u], g); up8(vx[u], xv);
+      if (mode == 1) {
+        float yv[8]; up8(vy[u], yv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = yv[e] > 0.f ? g[e] : 0.f;
+      } else if (mode == 2) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = fmaf(xv[e], sc[e], sh[e]) > 0.f ? g[e] : 0.f;
+      }
+      float d[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { d[e] = g[e] * sc[e]; a1[e] += g[e] * xv[e]; a0[e] += g[e]; }
+      *(uint4*)(dx + o) = pk8(d);
+      if (res_mode == 1) {
+        *(uint4*)(dres + o) = pk8(g);
+      } else if (res_mode == 2) {
+        float rv[8], dr[8]; up8(vr[u], rv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { dr[e] = g[e] * rsc[e]; b1[e] += g[e] * rv[e]; b0[e] += g[e]; }
+        *(uint4*)(dres + o) = pk8(dr);
+      }
+    }
+  }
+  // partial row per block in the workspace: [Σg·x | Σg | (residual) Σg·r | Σg]
+  float* row = sx + (size_t)blockIdx.x * 4 * C;
+  reduce_commit2(red, a1, a0, row, row + C, cols, c0);
+  if (res_mode == 2) reduce_commit2(red, b1, b0, row + 2 * C, row + 3 * C, cols, c0);
+}
+
+// dx = dy + dsum[c] + 2*x*dsumsq[c]   (in place on dy allowed)
+__global__ __launch_bounds__(256) void stats_combine_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                            const float* __restrict__ dstats, bf16_t* __restrict__ out,
+                                                            int M, int C, int rpb) {
+  const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t & (cols - 1)) * 8;
+  float a[8], b[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { a[e] = dstats[c0 + e]; b[e] = 2.f * dstats[C + c0 + e]; }
+  const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
+  for (int row = r0 + t / cols; row < r1; row += RP * FU2) {
+    uint4 vd[FU2], vx[FU2];
+#pragma unroll
+    for (int u = 0; u < FU2; ++u) {
+      int rr = row + u * RP;
+      bool ok = rr < r1;
+      size_t o = (size_t)rr * C + c0;
+      vd[u] = ok ? *(const uint4*)(dy + o) : make_uint4(0, 0, 0, 0);
+      vx[u] = ok ? *(const uint4*)(x + o) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < FU2; ++u) {
+      int rr = row + u * RP;
+      if (rr >= r1) break;
+      float d[8], xv[8];
+      up8(vd[u], d); up8(vx[u], xv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] += a[e] + b[e] * xv[e];
+      *(uint4*)(out + (size_t)rr * C + c0) = pk8(d);
+    }
+  }
+}
+
+// finalize backward: dss [4][C] (dscale, dshift, dmean, drstd) -> dstats [2][C], dgamma, dbeta
+// ss holds the forward's [scale, shift, mean, rstd].
+__global__ void bn_finalize_bwd_kernel(const float* __restrict__ dss, const float* __restrict__ ss,
+                                       const float* __restrict__ gamma, float* __restrict__ dstats,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta, int C, float count) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float scale = ss[c], mean = ss[2 * C + c], rstd = ss[3 * C + c];
+  const float g = gamma ? gamma[c] : 1.f;
+  const float dsc = dss[c], dsh = dss[C + c];
+  // shift = beta - mean*scale ; scale = g*rstd
+  const float dscale_tot = dsc - dsh * mean;
+  const float dmean = dss[2 * C + c] - dsh * scale;
+  const float drstd = dss[3 * C + c] + dscale_tot * g;
+  if (dgamma) dgamma[c] += dscale_tot * rstd;
+  if (dbeta) dbeta[c] += dsh;
+  // rstd = (var+eps)^-1/2, var = sumsq/M - mean^2, mean = sum/M
+  const float dvar = drstd * (-0.5f) * rstd * rstd * rstd;
+  dstats[c] = dmean / count - dvar * 2.f * mean / count;
+  dstats[C + c] = dvar / count;
+}
+
+static void grid2(long M, int C, int* blocks, int* rpb) {
+  int cols = C / 8, RP = 256 / cols;
+  long chunks = M * cols;
+  long b = chunks / (256 * 8);
+  if (b < 1) b = 1;
+  if (b > 2048) b = 2048;
+  long r = (M + b - 1) / b;
+  r = (r + RP - 1) / RP * RP;
+  *rpb = (int)r;
+  *blocks = (int)((M + r - 1) / r);
+}
+
+}  // namespace dtm
+using namespace dtm;
+
+static int shape_ok(long M, int C) {
+  if (C % 8) return 0;
+  int cols = C / 8;
+  return cols <= 256 && (256 % cols) == 0 && M < (1l << 31);
+}
+
+DTM_API int dtm_bn_apply_bwd(const void* dy, const void* y, const void* x, const float* ss, const void* r,
+                             const float* rss, void* dx, void* dres, float* sx, float* sr, long M, int C, int mode,
+                             int res_mode, void* stream) {
+  if (!shape_ok(M, C)) return -1;
+  int blocks, rpb;
+  grid2(M, C, &blocks, &rpb);
+  float* ws = dtm_ws_get((size_t)blocks * 4 * C);
+  if (!ws) return -4;
+  hipLaunchKernelGGL(bn_apply_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
+                     (const bf16_t*)y, (const bf16_t*)x, ss, (const bf16_t*)r, rss, (bf16_t*)dx, (bf16_t*)dres, ws,
+                     nullptr, (int)M, C, mode, res_mode, rpb);
+  dtm_reduce_rows(ws, blocks, 2 * C, 4 * C, sx, (hipStream_t)stream);
+  if (res_mode == 2) dtm_reduce_rows(ws + 2 * C, blocks, 2 * C, 4 * C, sr, (hipStream_t)stream);
+  return 0;
+}
+
+DTM_API int dtm_stats_combine(const void* dy, const void* x, const float* dstats, void* out, long M, int C,
+                              void* stream) {
+  if (!shape_ok(M, C)) return -1;
+  int blocks, rpb;
+  grid2(M, C, &blocks, &rpb);
+  hipLaunchKernelGGL(stats_combine_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
+                     (const bf16_t*)x, dstats, (bf16_t*)out, (int)M, C, rpb);
+  return 0;
+}
+
+DTM_API void dtm_bn_finalize_bwd(const float* dss, const float* ss, const float* gamma, float* dstats, float* dgamma,
+                                 float* dbeta, int C, float count, void* stream) {
+  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, dss, ss, gamma,
+                     dstats, dgamma, dbeta, C, count);
+}

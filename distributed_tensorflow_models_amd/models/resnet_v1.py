@@ -1,0 +1,145 @@
+"""ResNet v1 (slim geometry): resnet_v1_{50,101,152,200}.
+
+Structure and variable names follow reference vgg/nets/resnet_v1.py:78-375 and
+vgg/nets/resnet_utils.py:59-272:
+  * stride is applied in the 3x3 of the LAST unit of blocks 1-3 (spatial 56 -> 28 -> 14 -> 7 -> 7);
+  * projection shortcut (1x1 conv + BN, no activation) only when the depth changes, otherwise
+    ``subsample`` = 1x1 max-pool with the unit stride;
+  * conv2d_same: explicit symmetric pad (k-1)//2 + VALID when stride > 1;
+  * resnet_arg_scope: L2 1e-4, BN decay 0.997, eps 1e-5, scale=True, variance-scaling init,
+    max_pool2d padding SAME.
+Variables: resnet_v1_50/conv1/weights, resnet_v1_50/conv1/BatchNorm/{gamma,beta,moving_*},
+resnet_v1_50/block1/unit_1/bottleneck_v1/{shortcut,conv1,conv2,conv3}/..., resnet_v1_50/logits/{weights,biases}.
+"""
+import torch
+
+from ..ops import nn as F
+from .layers import Conv2d, Layer, _join
+
+
+def resnet_arg_scope(weight_decay=0.0001, batch_norm_decay=0.997, batch_norm_epsilon=1e-5, batch_norm_scale=True):
+    return dict(weight_decay=weight_decay, init="variance_scaling",
+                normalizer=dict(decay=batch_norm_decay, epsilon=batch_norm_epsilon, scale=batch_norm_scale,
+                                bessel=True))
+
+
+def subsample(x, factor):
+    if factor == 1:
+        return x
+    return F.max_pool(x, 1, factor, "VALID")
+
+
+def conv2d_same_padding(kernel, stride, rate=1):
+    if stride == 1:
+        return "SAME"
+    keff = kernel + (kernel - 1) * (rate - 1)
+    total = keff - 1
+    beg = total // 2
+    if total - beg != beg:
+        raise NotImplementedError("even kernel conv2d_same")
+    return (beg, beg)
+
+
+class BottleneckV1(Layer):
+    def __init__(self, scope, depth_in, depth, depth_bottleneck, stride, sc, rate=1):
+        super().__init__(scope)
+        self.stride = stride
+        wd, init, bn = sc["weight_decay"], sc["init"], sc["normalizer"]
+        if depth != depth_in:
+            self.shortcut = Conv2d(_join(scope, "shortcut"), depth_in, depth, 1, stride, "SAME", activation=None,
+                                   normalizer=bn, weight_decay=wd, init=init)
+        else:
+            self.shortcut = None
+        self.conv1 = Conv2d(_join(scope, "conv1"), depth_in, depth_bottleneck, 1, 1, "SAME", "relu", bn, None, wd, init)
+        self.conv2 = Conv2d(_join(scope, "conv2"), depth_bottleneck, depth_bottleneck, 3, stride,
+                            conv2d_same_padding(3, stride, rate), "relu", bn, None, wd, init, rate=rate)
+        self.conv3 = Conv2d(_join(scope, "conv3"), depth_bottleneck, depth, 1, 1, "SAME", None, bn, None, wd, init)
+
+    def forward(self, x, training=True):
+        sc = self.shortcut(x, training) if self.shortcut is not None else subsample(x, self.stride)
+        r = self.conv1(x, training)
+        r = self.conv2(r, training)
+        return self.conv3(r, training, residual=sc, residual_act="relu")
+
+
+BLOCKS = {
+    50: [(64, 3, 2), (128, 4, 2), (256, 6, 2), (512, 3, 1)],
+    101: [(64, 3, 2), (128, 4, 2), (256, 23, 2), (512, 3, 1)],
+    152: [(64, 3, 2), (128, 8, 2), (256, 36, 2), (512, 3, 1)],
+    200: [(64, 3, 2), (128, 24, 2), (256, 36, 2), (512, 3, 1)],
+}
+
+
+class ResNetV1(Layer):
+    default_image_size = 224
+
+    def __init__(self, depth=50, num_classes=1000, global_pool=True, spatial_squeeze=True, scope=None,
+                 arg_scope=None, blocks=None, include_root_block=True, in_channels=3):
+        scope = scope or "resnet_v1_%d" % depth
+        super().__init__(scope)
+        sc = arg_scope or resnet_arg_scope()
+        self.num_classes, self.global_pool, self.spatial_squeeze = num_classes, global_pool, spatial_squeeze
+        self.include_root_block = include_root_block
+        cin = in_channels
+        if include_root_block:
+            self.conv1 = Conv2d(_join(scope, "conv1"), cin, 64, 7, 2, conv2d_same_padding(7, 2), "relu",
+                                sc["normalizer"], None, sc["weight_decay"], sc["init"])
+            cin = 64
+        units = []
+        self.block_ends = []
+        for bi, (base, n, stride) in enumerate(blocks or BLOCKS[depth]):
+            for ui in range(n):
+                s = stride if ui == n - 1 else 1
+                units.append(BottleneckV1(_join(scope, "block%d/unit_%d/bottleneck_v1" % (bi + 1, ui + 1)), cin,
+                                          base * 4, base, s, sc))
+                cin = base * 4
+            self.block_ends.append((len(units) - 1, _join(scope, "block%d" % (bi + 1))))
+        self.units = torch.nn.ModuleList(units)
+        self.num_features = cin
+        if num_classes:
+            self.logits = Conv2d(_join(scope, "logits"), cin, num_classes, 1, 1, "SAME", None, None, True,
+                                 sc["weight_decay"], sc["init"])
+        else:
+            self.logits = None
+
+    def forward(self, x, training=True, end_points=None):
+        net = x
+        if self.include_root_block:
+            net = self.conv1(net, training)
+            net = F.max_pool(net, 3, 2, "SAME")
+        ends = dict(self.block_ends)
+        for i, u in enumerate(self.units):
+            net = u(net, training)
+            if end_points is not None:
+                end_points[u.scope] = net
+                if i in ends:
+                    end_points[ends[i]] = net
+        if self.global_pool:
+            net = F.global_avg_pool(net).reshape(net.shape[0], 1, 1, -1)
+            if end_points is not None:
+                end_points["global_pool"] = net
+        if self.logits is not None:
+            net = self.logits(net.to(torch.bfloat16) if net.is_cuda else net, training)
+            if end_points is not None:
+                end_points[self.scope + "/logits"] = net
+            if self.spatial_squeeze:
+                net = net.reshape(net.shape[0], -1)
+            if end_points is not None:
+                end_points["predictions"] = torch.softmax(net.float(), -1)
+        return net
+
+
+def resnet_v1_50(num_classes=1000, **kw):
+    return ResNetV1(50, num_classes, **kw)
+
+
+def resnet_v1_101(num_classes=1000, **kw):
+    return ResNetV1(101, num_classes, **kw)
+
+
+def resnet_v1_152(num_classes=1000, **kw):
+    return ResNetV1(152, num_classes, **kw)
+
+
+def resnet_v1_200(num_classes=1000, **kw):
+    return ResNetV1(200, num_classes, **kw)

@@ -57,6 +57,9 @@ _SIGS = {
     "dtm_check_finite": (None, [_P, _L, _P, _P]),
     "dtm_f32_to_bf16": (None, [_P, _P, _L, _P]),
     "dtm_scale": (None, [_P, _L, _F, _P]),
+    "dtm_bn_apply_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _P]),
+    "dtm_stats_combine": (_I, [_P, _P, _P, _P, _L, _I, _P]),
+    "dtm_bn_finalize_bwd": (None, [_P, _P, _P, _P, _P, _P, _I, _F, _P]),
 }
 
 

@@ -1,0 +1,200 @@
+"""Conv + BatchNorm(+ReLU)(+residual) fusion on the HIP path.
+
+A BatchNorm that follows a conv is split into:
+  * statistics  - accumulated in the producing conv's epilogue (``_ConvBNFn``),
+  * finalize    - per-channel scale/shift (+ moving averages) (``_BNFinalizeFn``),
+  * apply       - either folded into the NEXT conv's operand prologue (the normalised activation is
+                  never written to HBM: ``LazyBN`` consumed by ``conv_bn``), or materialised once by
+                  ``_BNApplyFn`` (block outputs, residual add, pool inputs).
+Each piece is an autograd Function with a hand-written backward kernel, so gradients compose
+exactly to TF's fused BatchNorm gradient (tests/test_fused_gpu.py checks it against torch).
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from .geometry import conv_geom
+from .lazy import LazyBN, as_tensor  # noqa: F401
+from .nn import _accum_param_grad, _check, _notify, weight_bf16
+
+
+# ---------------------------------------------------------------------------------------------
+class _ConvBNFn(torch.autograd.Function):
+    """y_raw, stats = conv(relu(x_raw*in_scale+in_shift) or x_raw, w); stats = (Σy, Σy²) per channel."""
+
+    @staticmethod
+    def forward(ctx, x, in_ss, w, geom, want_stats):
+        L = _lib.lib()
+        s = _lib.stream_ptr()
+        w16 = weight_bf16(w)
+        y = torch.empty((geom.N, geom.P, geom.Q, geom.K), device=x.device, dtype=torch.bfloat16)
+        stats = torch.zeros((2, geom.K), device=x.device, dtype=torch.float32) if want_stats else None
+        d = geom.as_desc(_lib.ConvDesc)
+        sc = in_ss[0] if in_ss is not None else None
+        sh = in_ss[1] if in_ss is not None else None
+        _check(L.dtm_conv_fwd(_lib.ptr(x), _lib.ptr(w16), _lib.ptr(y), _lib.ptr(stats), None, _lib.ptr(sc),
+                              _lib.ptr(sh), 0, ctypes.byref(d), s), "conv_fwd")
+        ctx.geom = geom
+        ctx.save_for_backward(x, in_ss, w, y)
+        if stats is None:
+            return y
+        return y, stats
+
+    @staticmethod
+    def backward(ctx, dy, dstats=None):
+        L = _lib.lib()
+        s = _lib.stream_ptr()
+        x, in_ss, w, y = ctx.saved_tensors
+        g = ctx.geom
+        M_out = g.N * g.P * g.Q
+        dy = dy.contiguous()
+        if dstats is not None:
+            comb = torch.empty_like(dy)
+            _check(L.dtm_stats_combine(_lib.ptr(dy), _lib.ptr(y), _lib.ptr(dstats.contiguous()), _lib.ptr(comb),
+                                       M_out, g.K, s), "stats_combine")
+            dy = comb
+        d = g.as_desc(_lib.ConvDesc)
+        sc = in_ss[0] if in_ss is not None else None
+        sh = in_ss[1] if in_ss is not None else None
+        dx = d_in = None
+        if ctx.needs_input_grad[0] or (in_ss is not None and ctx.needs_input_grad[1]):
+            w16 = weight_bf16(w)
+            wt = torch.empty((g.C, g.R, g.S, g.K), device=dy.device, dtype=torch.bfloat16)
+            L.dtm_weight_flip_transpose(_lib.ptr(w16), _lib.ptr(wt), g.K, g.R, g.S, g.C, s)
+            da = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
+            _check(L.dtm_conv_dgrad(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(da), ctypes.byref(d), s), "conv_dgrad")
+            if in_ss is not None:
+                dx = torch.empty_like(da)
+                sums = torch.zeros((4, g.C), device=dy.device, dtype=torch.float32)
+                M_in = g.N * g.H * g.W
+                _check(L.dtm_bn_apply_bwd(_lib.ptr(da), None, _lib.ptr(x), _lib.ptr(in_ss), None, None,
+                                          _lib.ptr(dx), None, _lib.ptr(sums), None, M_in, g.C, 2, 0, s),
+                       "act_bwd")
+                d_in = sums
+            else:
+                dx = da
+        if ctx.needs_input_grad[2]:
+            mg = getattr(w, "main_grad", None)
+            target = mg if mg is not None else torch.zeros(w.shape, device=dy.device, dtype=torch.float32)
+            _check(L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(target), _lib.ptr(sc), _lib.ptr(sh),
+                                    ctypes.byref(d), _lib.num_cus(), s), "conv_wgrad")
+            if mg is not None:
+                _notify(w)
+                dw = None
+            else:
+                dw = target
+        else:
+            dw = None
+        return dx, d_in, dw, None, None
+
+
+class _BNFinalizeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, stats, gamma, beta, mm, mv, count, eps, decay, bessel, update):
+        L = _lib.lib()
+        C = stats.shape[1]
+        ss = torch.empty((4, C), device=stats.device, dtype=torch.float32)
+        L.dtm_bn_finalize(_lib.ptr(stats), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(mm), _lib.ptr(mv), _lib.ptr(ss),
+                          C, float(count), float(eps), float(decay), int(update and mm is not None), int(bessel),
+                          _lib.stream_ptr())
+        ctx.save_for_backward(ss)
+        ctx.gamma, ctx.beta, ctx.count = gamma, beta, count
+        return ss
+
+    @staticmethod
+    def backward(ctx, dss):
+        L = _lib.lib()
+        (ss,) = ctx.saved_tensors
+        C = ss.shape[1]
+        dstats = torch.empty((2, C), device=ss.device, dtype=torch.float32)
+        gmg = getattr(ctx.gamma, "main_grad", None) if ctx.gamma is not None else None
+        bmg = getattr(ctx.beta, "main_grad", None) if ctx.beta is not None else None
+        dg = None if (ctx.gamma is None or gmg is not None) else torch.zeros(C, device=ss.device)
+        db = None if (ctx.beta is None or bmg is not None) else torch.zeros(C, device=ss.device)
+        L.dtm_bn_finalize_bwd(_lib.ptr(dss.contiguous()), _lib.ptr(ss), _lib.ptr(ctx.gamma), _lib.ptr(dstats),
+                              _lib.ptr(gmg if gmg is not None else dg), _lib.ptr(bmg if bmg is not None else db), C,
+                              float(ctx.count), _lib.stream_ptr())
+        if gmg is not None:
+            _notify(ctx.gamma)
+        if bmg is not None:
+            _notify(ctx.beta)
+        return dstats, dg, db, None, None, None, None, None, None, None
+
+
+class _BNApplyFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, ss, res, res_ss, relu):
+        L = _lib.lib()
+        C = x.shape[-1]
+        M = x.numel() // C
+        y = torch.empty_like(x)
+        res_mode = 0 if res is None else (2 if res_ss is not None else 1)
+        L.dtm_bn_apply(_lib.ptr(x), _lib.ptr(ss), _lib.ptr(res), _lib.ptr(res_ss), _lib.ptr(y), M, C, res_mode,
+                       int(relu), _lib.stream_ptr())
+        ctx.relu, ctx.res_mode = relu, res_mode
+        ctx.save_for_backward(x, ss, res, res_ss, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L = _lib.lib()
+        x, ss, res, rss, y = ctx.saved_tensors
+        C = x.shape[-1]
+        M = x.numel() // C
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if ctx.res_mode else None
+        sx = torch.zeros((4, C), device=x.device, dtype=torch.float32)
+        sr = torch.zeros((4, C), device=x.device, dtype=torch.float32) if ctx.res_mode == 2 else None
+        _check(L.dtm_bn_apply_bwd(_lib.ptr(dy.contiguous()), _lib.ptr(y), _lib.ptr(x), _lib.ptr(ss), _lib.ptr(res),
+                                  _lib.ptr(rss), _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(sx), _lib.ptr(sr), M, C,
+                                  1 if ctx.relu else 0, ctx.res_mode, _lib.stream_ptr()), "bn_apply_bwd")
+        return dx, sx, dres, sr, None
+
+
+def bn_apply(raw, ss, relu, residual=None):
+    """y = relu?(raw*scale+shift + residual); residual may be a tensor or a LazyBN (BN'd shortcut)."""
+    if residual is None:
+        return _BNApplyFn.apply(raw, ss, None, None, bool(relu))
+    if isinstance(residual, LazyBN):
+        if residual.relu:
+            residual = residual.materialize()
+        else:
+            return _BNApplyFn.apply(raw, ss, residual.raw, residual.ss, bool(relu))
+    return _BNApplyFn.apply(raw, ss, residual.to(torch.bfloat16).contiguous(), None, bool(relu))
+
+
+def bn_inference_ss(bn):
+    """Differentiable [4, C] scale/shift from moving statistics (frozen BN / eval)."""
+    rstd = torch.rsqrt(bn.moving_variance + bn.eps)
+    scale = rstd if bn.gamma is None else bn.gamma * rstd
+    shift = -bn.moving_mean * scale if bn.beta is None else bn.beta - bn.moving_mean * scale
+    return torch.stack([scale, shift, bn.moving_mean.expand_as(scale), rstd.expand_as(scale)]).contiguous()
+
+
+def conv_bn(x, w, bn, stride, padding, training, relu):
+    """Fused conv -> BatchNorm; returns a LazyBN.  x: tensor or LazyBN(relu=True) (prologue-fused)."""
+    in_ss = None
+    if isinstance(x, LazyBN):
+        if x.relu:
+            in_ss, x = x.ss, x.raw
+        else:
+            x = x.materialize()
+    g = conv_geom(tuple(x.shape), tuple(w.shape), stride, padding)
+    if g.C % 8 != 0:
+        from .nn import _PadChannels
+        if in_ss is not None:
+            raise ValueError("prologue fusion needs C % 8 == 0")
+        cp = (g.C + 7) // 8 * 8
+        x = torch.nn.functional.pad(x, (0, cp - g.C))
+        w = _PadChannels.apply(w, cp)
+        g = conv_geom(tuple(x.shape), tuple(w.shape), stride, padding)
+    x = x.to(torch.bfloat16).contiguous()
+    if training:
+        y, stats = _ConvBNFn.apply(x, in_ss, w, g, True)
+        ss = _BNFinalizeFn.apply(stats, bn.gamma, bn.beta, bn.moving_mean, bn.moving_variance,
+                                 float(g.N * g.P * g.Q), bn.eps, bn.decay, bn.bessel, True)
+    else:
+        y = _ConvBNFn.apply(x, in_ss, w, g, False)
+        ss = bn_inference_ss(bn)
+    return LazyBN(y, ss, relu)

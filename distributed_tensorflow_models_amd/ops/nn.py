@@ -16,6 +16,7 @@ import torch
 from . import _lib
 from . import reference as ref
 from .geometry import conv_geom, pool_geom
+from .lazy import as_tensor
 
 _grad_ready_hooks = []
 
@@ -115,6 +116,7 @@ class _Conv2dFn(torch.autograd.Function):
 
 def conv2d(x, w, bias=None, stride=1, padding="SAME", relu=False, dilation=1):
     """NHWC conv. x [N,H,W,C]; w fp32 master [K,R,S,C]; bias [K] or None."""
+    x = as_tensor(x)
     if not x.is_cuda:
         return ref.conv2d(x, w, bias, stride, padding, relu, dilation)
     if dilation != 1:
@@ -126,7 +128,30 @@ def conv2d(x, w, bias=None, stride=1, padding="SAME", relu=False, dilation=1):
         x = torch.nn.functional.pad(x, (0, cp - g.C))
         w = _PadChannels.apply(w, cp)
         g = conv_geom(tuple(x.shape), tuple(w.shape), stride, padding, dilation)
+    if g.K % 8 != 0:
+        # pad output channels (e.g. 10 / 1001 classes) to the 8-channel store granule
+        kp = (g.K + 7) // 8 * 8
+        wp = _PadOutChannels.apply(w, kp)
+        bp = _PadOutChannels.apply(bias, kp) if bias is not None else None
+        g = conv_geom(tuple(x.shape), tuple(wp.shape), stride, padding, dilation)
+        y = _Conv2dFn.apply(x.to(torch.bfloat16), wp, bp, g, relu)
+        return y[..., :w.shape[0]].contiguous()
     return _Conv2dFn.apply(x.to(torch.bfloat16), w, bias, g, relu)
+
+
+class _PadOutChannels(torch.autograd.Function):
+    """Zero-pad dim 0 (output channels) of a fp32 weight / bias."""
+
+    @staticmethod
+    def forward(ctx, w, kp):
+        ctx.k = w.shape[0]
+        ctx.src = w
+        pad = [0, 0] * (w.dim() - 1) + [0, kp - w.shape[0]]
+        return torch.nn.functional.pad(w, pad)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _accum_param_grad(ctx.src, g[:ctx.k].contiguous()), None
 
 
 class _PadChannels(torch.autograd.Function):
@@ -200,6 +225,8 @@ class _BatchNormFn(torch.autograd.Function):
 
 def batch_norm(x, gamma, beta, moving_mean, moving_var, training=True, decay=0.999, eps=1e-3, relu=False,
                residual=None, bessel=True):
+    x = as_tensor(x)
+    residual = as_tensor(residual) if residual is not None else None
     if not x.is_cuda:
         return ref.batch_norm(x, gamma, beta, moving_mean, moving_var, training, decay, eps, relu, residual, bessel)
     return _BatchNormFn.apply(x.to(torch.bfloat16), gamma, beta,
@@ -235,6 +262,7 @@ class _MaxPoolFn(torch.autograd.Function):
 
 
 def max_pool(x, kernel, stride, padding="VALID"):
+    x = as_tensor(x)
     if not x.is_cuda:
         return ref.max_pool(x, kernel, stride, padding)
     g = pool_geom(tuple(x.shape), kernel, stride, padding)
@@ -264,6 +292,7 @@ class _AvgPoolFn(torch.autograd.Function):
 
 
 def avg_pool(x, kernel, stride, padding="VALID", count_pad=False):
+    x = as_tensor(x)
     if not x.is_cuda:
         return ref.avg_pool(x, kernel, stride, padding, count_pad)
     g = pool_geom(tuple(x.shape), kernel, stride, padding)
@@ -291,6 +320,7 @@ class _GlobalAvgFn(torch.autograd.Function):
 
 def global_avg_pool(x):
     """mean over H, W -> [N, C] fp32."""
+    x = as_tensor(x)
     if not x.is_cuda:
         return ref.global_avg_pool(x)
     return _GlobalAvgFn.apply(x.to(torch.bfloat16))
@@ -364,6 +394,7 @@ class _LinearFn(torch.autograd.Function):
 
 def linear(x, w, b=None, relu=False):
     """x [B, in] @ w [in, out] (+b)."""
+    x = as_tensor(x)
     if not x.is_cuda:
         y = x.float() @ w
         if b is not None:

@@ -1,0 +1,125 @@
+"""BSP data parallelism: bucketed gradient all-reduce over RCCL (xGMI), overlapped with backward.
+
+Replaces the reference's PS-side SyncReplicasOptimizer (ConditionalAccumulator per variable +
+chief queue runner + sync token queue; e.g. reference
+alexnet/cifar10_alexnet_bsp.py:79-94, inception/imagenet_inception_bsp.py:123-157).
+
+Design (MI355X-first):
+  * all fp32 gradients live in ONE flat buffer laid out in backward (reverse-registration)
+    order; every parameter gets ``param.main_grad`` = its view.  Conv wgrad kernels add into it
+    directly with fp32 atomics, so there is no per-parameter grad copy or bucket pack kernel;
+  * the buffer is cut into ~``bucket_mb`` contiguous buckets (a tensor larger than a bucket - e.g.
+    VGG-16's 411 MB fc6 gradient - is split across several buckets so its all-reduce pipelines);
+  * when the last gradient of a bucket is produced (``grad_ready`` fired by the ops, or autograd
+    post-accumulate hooks for plain torch ops), the bucket's all_reduce(SUM) is issued
+    asynchronously; RCCL's internal stream waits on the compute stream at issue time, so the
+    reduction overlaps the rest of backward;
+  * averaging (1/W) and the per-rank batch weight (C15, b_r / b_nominal) are folded into the
+    optimizer's grad_scale / the loss scale - no extra pass over the gradients.
+With world_size == 1 no collective is issued.
+"""
+import torch
+import torch.distributed as dist
+
+from ..ops import nn as opsnn
+
+
+class BSPDataParallel:
+    def __init__(self, params, bucket_mb=32.0, process_group=None, device=None, overlap=True, grad_dtype=torch.float32):
+        self.params = [p for p in params if p.requires_grad]
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        dev = device or self.params[0].device
+        total = sum(p.numel() for p in self.params)
+        self.flat = torch.zeros(total, dtype=grad_dtype, device=dev)
+        # backward order ~ reverse of registration order
+        order = list(reversed(self.params))
+        self.offsets = {}
+        off = 0
+        for p in order:
+            self.offsets[p] = off
+            p.main_grad = self.flat[off:off + p.numel()].view(p.shape)
+            off += p.numel()
+        # buckets over the flat buffer
+        cap = max(1, int(bucket_mb * (1 << 20) / self.flat.element_size()))
+        self.buckets = []  # (start, end)
+        start = 0
+        while start < total:
+            end = min(total, start + cap)
+            self.buckets.append((start, end))
+            start = end
+        # param -> list of (bucket index, element count inside that bucket)
+        self.contrib = {}
+        self.need = [0] * len(self.buckets)
+        for p in order:
+            s, e = self.offsets[p], self.offsets[p] + p.numel()
+            lst = []
+            for bi, (bs, be) in enumerate(self.buckets):
+                lo, hi = max(s, bs), min(e, be)
+                if lo < hi:
+                    lst.append((bi, hi - lo))
+                    self.need[bi] += hi - lo
+            self.contrib[p] = lst
+        self.overlap = overlap
+        self._have = [0] * len(self.buckets)
+        self._launched = [False] * len(self.buckets)
+        self._works = []
+        self._seen = set()
+        self._hook = opsnn.add_grad_ready_hook(self._on_ready)
+        self._acc_hooks = []
+        for p in self.params:
+            if hasattr(p, "register_post_accumulate_grad_hook"):
+                self._acc_hooks.append(p.register_post_accumulate_grad_hook(self._on_accumulated))
+
+    def close(self):
+        opsnn.remove_grad_ready_hook(self._hook)
+        for h in self._acc_hooks:
+            h.remove()
+
+    # ------------------------------------------------------------------------------------------
+    def zero_grad(self):
+        self.flat.zero_()
+        self._have = [0] * len(self.buckets)
+        self._launched = [False] * len(self.buckets)
+        self._works = []
+        self._seen = set()
+
+    def _on_accumulated(self, p):
+        # plain autograd path (CPU ops / torch fallbacks): move .grad into the flat buffer
+        if p.grad is not None:
+            p.main_grad.add_(p.grad.to(p.main_grad.dtype))
+            p.grad = None
+        self._on_ready(p)
+
+    def _on_ready(self, p):
+        lst = self.contrib.get(p)
+        if lst is None or p in self._seen:
+            return
+        self._seen.add(p)
+        for bi, n in lst:
+            self._have[bi] += n
+            if self.overlap and self._have[bi] == self.need[bi]:
+                self._launch(bi)
+
+    def _launch(self, bi):
+        if self._launched[bi]:
+            return
+        self._launched[bi] = True
+        if self.world == 1:
+            return
+        s, e = self.buckets[bi]
+        self._works.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+
+    def finish(self):
+        """Launch any bucket not yet reduced (unused params / no overlap) and make the current
+        stream wait for every reduction."""
+        for bi in range(len(self.buckets)):
+            if not self._launched[bi]:
+                self._launch(bi)
+        for w in self._works:
+            w.wait()
+        self._works = []
+
+    @property
+    def grad_scale(self):
+        return 1.0 / self.world
