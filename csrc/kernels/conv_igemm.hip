@@ -54,12 +54,20 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
   constexpr int ACH = PT / 32;  // act chunks per thread (PT rows * 8 chunks / 256 threads)
   constexpr int WCH = CT / 32;
   constexpr int BUF = (PT + CT) * 128;
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  constexpr int MAXC = 512;  // prologue scale/shift staged in LDS for C <= MAXC (bottleneck widths)
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF + MAXC * 8];
+  float* s_scale = (float*)(smem + 2 * BUF);
+  float* s_shift = s_scale + MAXC;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wp = wave % NWP, wc = wave / NWP;
   const int p0 = blockIdx.y * PT, c0 = blockIdx.x * CT;
   const int ch = tid & 7, rb = tid >> 3;
+  const bool lds_ss = a.in_scale && a.C <= MAXC;
+  if (lds_ss) {
+    for (int c = tid; c < a.C; c += 256) { s_scale[c] = a.in_scale[c]; s_shift[c] = a.in_shift[c]; }
+    __syncthreads();
+  }
 
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
   const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, a.w_bytes);
@@ -127,8 +135,14 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
     if (a.in_scale) {
       // fused BatchNorm-apply + ReLU of the previous layer on the gathered input
       float sc[8], sh[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { sc[e] = a.in_scale[acc_c + e]; sh[e] = a.in_shift[acc_c + e]; }
+      if (lds_ss) {
+        const float4 s0 = *(const float4*)(s_scale + acc_c), s1 = *(const float4*)(s_scale + acc_c + 4);
+        const float4 h0 = *(const float4*)(s_shift + acc_c), h1 = *(const float4*)(s_shift + acc_c + 4);
+        sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+        sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w; sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
+      } else {
+        for (int e = 0; e < 8; ++e) { sc[e] = a.in_scale[acc_c + e]; sh[e] = a.in_shift[acc_c + e]; }
+      }
 #pragma unroll
       for (int i = 0; i < ACH; ++i) {
         if (avalid[i]) {
@@ -280,9 +294,20 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
   constexpr int ACH = MT / 32;  // BK*MT/8 chunks / 256 threads
   constexpr int BCH = NT / 32;
   constexpr int BUF = BK * (MT + NT) * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF + NT * 8];
+  float* s_scale = (float*)(smem + 2 * BUF);  // prologue scale/shift of this block's NT columns
+  float* s_shift = s_scale + NT;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (a.in_scale) {
+    for (int j = tid; j < NT; j += 256) {
+      int col = blockIdx.x * NT + j;
+      int c = col < a.Kg ? col % a.C : 0;
+      s_scale[j] = a.in_scale[c];
+      s_shift[j] = a.in_shift[c];
+    }
+    __syncthreads();
+  }
   const int wm = wave % NWM, wn = wave / NWM;
   const int n0 = blockIdx.x * NT, m0 = blockIdx.y * MT;
   const int pix_lo = blockIdx.z * a.pix_per_split;
@@ -353,11 +378,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
       for (int i = 0; i < BCH; ++i) {
         if (bval[i]) {
           uint32_t u[4] = {breg[i].x, breg[i].y, breg[i].z, breg[i].w};
+          const float4 s0 = *(const float4*)(s_scale + b_n[i]), s1 = *(const float4*)(s_scale + b_n[i] + 4);
+          const float4 h0 = *(const float4*)(s_shift + b_n[i]), h1 = *(const float4*)(s_shift + b_n[i] + 4);
+          const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+          const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            int c = bcc[i] + 2 * e;
-            float lo = fmaxf(fmaf(lo_bf(u[e]), a.in_scale[c], a.in_shift[c]), 0.f);
-            float hi = fmaxf(fmaf(hi_bf(u[e]), a.in_scale[c + 1], a.in_shift[c + 1]), 0.f);
+            float lo = fmaxf(fmaf(lo_bf(u[e]), sc[2 * e], sh[2 * e]), 0.f);
+            float hi = fmaxf(fmaf(hi_bf(u[e]), sc[2 * e + 1], sh[2 * e + 1]), 0.f);
             u[e] = pack2bf(lo, hi);
           }
           breg[i] = make_uint4(u[0], u[1], u[2], u[3]);

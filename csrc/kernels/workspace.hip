@@ -27,7 +27,44 @@ float* dtm_ws_get(size_t floats) {
   return g_ws;
 }
 
-// out[j] (+)= sum_r ws[r*ld + j], j < width
+// out[j] (+)= sum_r ws[r*ld + j], j < width.  16 column-quads x 16 row-lanes per block, float4 loads,
+// 4 rows in flight per lane, LDS combine, one atomic per output per block.
+__global__ __launch_bounds__(256) void reduce_rows4_kernel(const float* __restrict__ ws, int rows, int width, int ld,
+                                                           float* __restrict__ out, int rpb) {
+  __shared__ float4 red[16][16];
+  const int cg = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int col = (blockIdx.x * 16 + cg) * 4;
+  const int r0 = blockIdx.y * rpb, r1 = min(rows, r0 + rpb);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col < width) {
+    int r = r0 + rl;
+    for (; r + 48 < r1; r += 64) {
+      float4 a = *(const float4*)(ws + (size_t)r * ld + col);
+      float4 b = *(const float4*)(ws + (size_t)(r + 16) * ld + col);
+      float4 c = *(const float4*)(ws + (size_t)(r + 32) * ld + col);
+      float4 d = *(const float4*)(ws + (size_t)(r + 48) * ld + col);
+      s.x += (a.x + b.x) + (c.x + d.x); s.y += (a.y + b.y) + (c.y + d.y);
+      s.z += (a.z + b.z) + (c.z + d.z); s.w += (a.w + b.w) + (c.w + d.w);
+    }
+    for (; r < r1; r += 16) {
+      float4 a = *(const float4*)(ws + (size_t)r * ld + col);
+      s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+    }
+  }
+  red[rl][cg] = s;
+  __syncthreads();
+  if (rl == 0 && col < width) {
+    float4 t = red[0][cg];
+    for (int i = 1; i < 16; ++i) { float4 u = red[i][cg]; t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w; }
+    if (gridDim.y == 1) {
+      out[col] += t.x; out[col + 1] += t.y; out[col + 2] += t.z; out[col + 3] += t.w;
+    } else {
+      atomicAdd(out + col, t.x); atomicAdd(out + col + 1, t.y);
+      atomicAdd(out + col + 2, t.z); atomicAdd(out + col + 3, t.w);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ ws, int rows, int width, int ld,
                                                           float* __restrict__ out, int chunks) {
   const int j = blockIdx.x * 256 + threadIdx.x;
@@ -39,6 +76,13 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
 }
 
 void dtm_reduce_rows(const float* ws, int rows, int width, int ld, float* out, hipStream_t st) {
+  if (width % 4 == 0 && ld % 4 == 0) {
+    int rpb = 256;                         // 16 rows per lane
+    int ychunks = (rows + rpb - 1) / rpb;  // <= ~100 atomics per output
+    hipLaunchKernelGGL(reduce_rows4_kernel, dim3((width + 63) / 64, ychunks), dim3(256), 0, st, ws, rows, width, ld,
+                       out, rpb);
+    return;
+  }
   int chunks = rows >= 512 ? 32 : (rows >= 64 ? 8 : 1);
   hipLaunchKernelGGL(reduce_rows_kernel, dim3((width + 255) / 256, chunks), dim3(256), 0, st, ws, rows, width, ld, out,
                      chunks);

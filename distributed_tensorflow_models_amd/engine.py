@@ -6,6 +6,7 @@ runs, one multi-tensor optimizer launch, TF 1.x optimizer / loss semantics.
 """
 import torch
 
+from .ops import fused as _fused
 from .ops import nn as F
 from .ops.optim import FusedOptimizer
 from .parallel.bsp import BSPDataParallel
@@ -53,9 +54,14 @@ class TrainStep:
 
     def __call__(self, images, labels):
         self.dp.zero_grad()
-        out = self.model(images, training=True)
-        loss = self.loss_fn(out, labels)
-        loss.backward()
+        if images.is_cuda:
+            _fused.arena.begin_step(images.device)
+        try:
+            out = self.model(images, training=True)
+            loss = self.loss_fn(out, labels)
+            loss.backward()
+        finally:
+            _fused.arena.end_step()
         self.dp.finish()
         self.opt.step(self.current_lr(), grad_scale=self.dp.grad_scale)
         self.global_step += 1

@@ -19,6 +19,48 @@ from .lazy import LazyBN, as_tensor  # noqa: F401
 from .nn import _accum_param_grad, _check, _notify, weight_bf16
 
 
+class ZeroArena:
+    """Per-step pool of zero-initialised fp32 scratch (BN statistics, per-channel grad sums).
+
+    One memset at step start replaces ~150 small zero-fill kernels per ResNet-50 step.  Only used
+    between ``begin_step`` and ``end_step`` (the training engine brackets every step)."""
+
+    def __init__(self, floats=1 << 22):
+        self.floats = floats
+        self.buf = None
+        self.off = 0
+        self.high = 0
+        self.active = False
+
+    def begin_step(self, device):
+        if self.buf is None or self.buf.device != device:
+            self.buf = torch.zeros(self.floats, device=device, dtype=torch.float32)
+            self.high = 0
+        elif self.high:
+            self.buf[:self.high].zero_()
+        self.off = 0
+        self.active = True
+
+    def end_step(self):
+        self.high = max(self.high, self.off)
+        self.active = False
+
+    def zeros(self, shape, device):
+        n = 1
+        for s in shape:
+            n *= int(s)
+        if self.active and self.buf is not None and self.buf.device == device:
+            n_al = (n + 63) // 64 * 64
+            if self.off + n_al <= self.floats:
+                v = self.buf[self.off:self.off + n].view(*shape)
+                self.off += n_al
+                return v
+        return torch.zeros(shape, device=device, dtype=torch.float32)
+
+
+arena = ZeroArena()
+
+
 # ---------------------------------------------------------------------------------------------
 class _ConvBNFn(torch.autograd.Function):
     """y_raw, stats = conv(relu(x_raw*in_scale+in_shift) or x_raw, w); stats = (Σy, Σy²) per channel."""
@@ -29,7 +71,7 @@ class _ConvBNFn(torch.autograd.Function):
         s = _lib.stream_ptr()
         w16 = weight_bf16(w)
         y = torch.empty((geom.N, geom.P, geom.Q, geom.K), device=x.device, dtype=torch.bfloat16)
-        stats = torch.zeros((2, geom.K), device=x.device, dtype=torch.float32) if want_stats else None
+        stats = arena.zeros((2, geom.K), x.device) if want_stats else None
         d = geom.as_desc(_lib.ConvDesc)
         sc = in_ss[0] if in_ss is not None else None
         sh = in_ss[1] if in_ss is not None else None
@@ -66,7 +108,7 @@ class _ConvBNFn(torch.autograd.Function):
             _check(L.dtm_conv_dgrad(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(da), ctypes.byref(d), s), "conv_dgrad")
             if in_ss is not None:
                 dx = torch.empty_like(da)
-                sums = torch.zeros((4, g.C), device=dy.device, dtype=torch.float32)
+                sums = arena.zeros((4, g.C), dy.device)
                 M_in = g.N * g.H * g.W
                 _check(L.dtm_bn_apply_bwd(_lib.ptr(da), None, _lib.ptr(x), _lib.ptr(in_ss), None, None,
                                           _lib.ptr(dx), None, _lib.ptr(sums), None, M_in, g.C, 2, 0, s),
@@ -144,8 +186,8 @@ class _BNApplyFn(torch.autograd.Function):
         M = x.numel() // C
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if ctx.res_mode else None
-        sx = torch.zeros((4, C), device=x.device, dtype=torch.float32)
-        sr = torch.zeros((4, C), device=x.device, dtype=torch.float32) if ctx.res_mode == 2 else None
+        sx = arena.zeros((4, C), x.device)
+        sr = arena.zeros((4, C), x.device) if ctx.res_mode == 2 else None
         _check(L.dtm_bn_apply_bwd(_lib.ptr(dy.contiguous()), _lib.ptr(y), _lib.ptr(x), _lib.ptr(ss), _lib.ptr(res),
                                   _lib.ptr(rss), _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(sx), _lib.ptr(sr), M, C,
                                   1 if ctx.relu else 0, ctx.res_mode, _lib.stream_ptr()), "bn_apply_bwd")

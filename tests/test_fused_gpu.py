@@ -16,7 +16,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("fused", ["1", "0"])
-@pytest.mark.parametrize("base,batch", [(8, 4), (16, 16)])
+@pytest.mark.parametrize("base,batch", [(16, 16), (16, 32)])
 def test_small_resnet_matches_reference(fused, base, batch, monkeypatch):
     monkeypatch.setenv("DTM_FUSED_BN", fused)
     torch.manual_seed(0)
