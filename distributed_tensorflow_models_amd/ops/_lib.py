@@ -60,6 +60,8 @@ _SIGS = {
     "dtm_bn_apply_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _P]),
     "dtm_stats_combine": (_I, [_P, _P, _P, _P, _L, _I, _P]),
     "dtm_bn_finalize_bwd": (None, [_P, _P, _P, _P, _P, _P, _I, _F, _P]),
+    "dtm_lrn": (_I, [_P, _P, _P, _L, _I, _I, _F, _F, _F, _I, _P]),
+    "dtm_ws_reserve": (_I, [_L]),
 }
 
 

@@ -1,0 +1,239 @@
+"""ASP: asynchronous parameter-store data parallelism (reference vgg/cifar10_vgg_asp.py,
+inception/imagenet_inception_asp.py).
+
+The reference keeps variables on PS tasks and every worker runs ``apply_gradients`` on them
+independently (Hogwild at op granularity).  MI355X-native redesign: the parameter store is a set
+of *owner shards* (round-robin over tensors, like ``replica_device_setter``) that every worker
+maps directly:
+
+  * GPU mode: owner k's shard lives in GPU k's HBM; the other ranks open it through HIP IPC
+    handles (exchanged via the c10d TCPStore) and read / update it in place over xGMI peer
+    access - no owner-side server loop, no message matching;
+  * host mode (CPU runs, tests, or when peer IPC is unavailable): shards live in a file-backed
+    shared mapping under /dev/shm (``torch.from_file(shared=True)``) - exactly the reference's
+    "variables on the PS CPU" placement.
+
+Per worker step: pull (copy every shard into the local replica) -> forward/backward on local
+weights -> push (apply this worker's gradient to the owner shard with the TF update rule; no
+averaging, no barrier).  ``global_step`` is an atomic counter in the TCPStore, incremented once
+per worker step (TF ASP semantics).  Concurrent pushes to one shard race exactly as Hogwild does.
+"""
+import os
+import pickle
+import time
+
+import torch
+import torch.distributed as dist
+
+from . import process_group as pg
+
+STORE_PREFIX = "dtm_asp"
+
+
+def owner_map(params, world):
+    """Round-robin tensor -> owner rank (replica_device_setter semantics, C14)."""
+    return {i: i % world for i in range(len(params))}
+
+
+class ParamStore:
+    def __init__(self, params, optimizer="sgd", lr=0.01, momentum=0.9, rho=0.9, epsilon=1e-10, mode=None,
+                 store=None, run_id="0", weight_decays=None):
+        self.params = [p for p in params if p.requires_grad]
+        self.rank, self.world = pg.rank(), pg.world_size()
+        self.owner = owner_map(self.params, self.world)
+        self.kind, self.lr, self.mu, self.rho, self.eps = optimizer, lr, momentum, rho, epsilon
+        self.wd = [float(getattr(p, "weight_decay", 0.0)) for p in self.params] if weight_decays is None \
+            else list(weight_decays)
+        self.store = store if store is not None else _default_store()
+        self.run_id = run_id
+        gpu = self.params[0].is_cuda
+        self.mode = mode or ("ipc" if gpu else "shm")
+        self.shards = {}   # param index -> dict(param=..., s1=..., s2=...) views into owner memory
+        self._build()
+
+    # -----------------------------------------------------------------------------------------
+    def _build(self):
+        nslots = {"sgd": 0, "momentum": 1, "rmsprop": 2}[self.kind]
+        # one flat buffer per owner: [params | slot1 | slot2]
+        per_owner = {}
+        for i, p in enumerate(self.params):
+            per_owner.setdefault(self.owner[i], []).append(i)
+        self.layout = {}
+        for k, idxs in per_owner.items():
+            off = 0
+            for i in idxs:
+                self.layout[i] = (k, off)
+                off += self.params[i].numel()
+            per_owner[k] = (idxs, off)
+        self.flat = {}
+        for k, (idxs, n) in per_owner.items():
+            total = n * (1 + nslots)
+            self.flat[k] = self._open_flat(k, total, init_from=(idxs, n) if k == self.rank or self.mode == "shm"
+                                           else None)
+        if self.mode == "shm" and self.rank == 0:
+            pass
+        pg.barrier()
+        for i, p in enumerate(self.params):
+            k, off = self.layout[i]
+            n_owner = per_owner[k][1]
+            buf = self.flat[k]
+            sh = {"param": buf[off:off + p.numel()].view(p.shape)}
+            if nslots >= 1:
+                sh["s1"] = buf[n_owner + off:n_owner + off + p.numel()].view(p.shape)
+            if nslots >= 2:
+                sh["s2"] = buf[2 * n_owner + off:2 * n_owner + off + p.numel()].view(p.shape)
+            self.shards[i] = sh
+
+    def _open_flat(self, k, total, init_from):
+        if self.mode == "shm":
+            path = "/dev/shm/%s_%s_owner%d" % (STORE_PREFIX, self.run_id, k)
+            if self.rank == k:
+                buf = torch.from_file(path, shared=True, size=total, dtype=torch.float32)
+                self._init_owner(buf, k)
+                self.store.set("%s/%s/ready%d" % (STORE_PREFIX, self.run_id, k), "1")
+            else:
+                self.store.wait(["%s/%s/ready%d" % (STORE_PREFIX, self.run_id, k)])
+                buf = torch.from_file(path, shared=True, size=total, dtype=torch.float32)
+            return buf
+        # ipc: owner allocates in its HBM, publishes the handle; others open it
+        from torch.multiprocessing.reductions import reduce_tensor
+        key = "%s/%s/ipc%d" % (STORE_PREFIX, self.run_id, k)
+        if self.rank == k:
+            buf = torch.zeros(total, dtype=torch.float32, device=self.params[0].device)
+            self._init_owner(buf, k)
+            torch.cuda.synchronize()
+            self._owned = buf
+            fn, args = reduce_tensor(buf)
+            self.store.set(key, pickle.dumps((fn, args)))
+            return buf
+        self.store.wait([key])
+        fn, args = pickle.loads(self.store.get(key))
+        return fn(*args)
+
+    def _init_owner(self, buf, k):
+        n_owner = sum(self.params[i].numel() for i in self.layout if self.layout[i][0] == k)
+        with torch.no_grad():
+            for i, p in enumerate(self.params):
+                kk, off = self.layout[i]
+                if kk == k:
+                    buf[off:off + p.numel()].copy_(p.detach().reshape(-1).to(buf.device))
+            if self.kind == "rmsprop":
+                buf[2 * n_owner:3 * n_owner].fill_(1.0)  # TF RMSProp ms slot init 1.0
+
+    # -----------------------------------------------------------------------------------------
+    @torch.no_grad()
+    def pull(self):
+        """Copy the current shared parameters into the local replica (M1)."""
+        for i, p in enumerate(self.params):
+            p.copy_(self.shards[i]["param"].to(p.device, non_blocking=True))
+            w16 = getattr(p, "bf16", None)
+            if w16 is not None:
+                w16.copy_(p)
+
+    @torch.no_grad()
+    def push(self, grads, lr=None, grad_scale=1.0):
+        """Apply this worker's gradients to the owner shards with the TF rule (M2)."""
+        lr = self.lr if lr is None else lr
+        for i, p in enumerate(self.params):
+            g = grads[i]
+            if g is None:
+                continue
+            sh = self.shards[i]
+            w = sh["param"]
+            g = g.to(w.device, non_blocking=True).float() * grad_scale + self.wd[i] * w
+            if self.kind == "sgd":
+                w.sub_(lr * g)
+            elif self.kind == "momentum":
+                sh["s1"].mul_(self.mu).add_(g)
+                w.sub_(lr * sh["s1"])
+            else:
+                sh["s2"].mul_(self.rho).add_((1 - self.rho) * g * g)
+                sh["s1"].mul_(self.mu).add_(lr * g * torch.rsqrt(sh["s2"] + self.eps))
+                w.sub_(sh["s1"])
+        if self.params[0].is_cuda:
+            torch.cuda.synchronize()
+
+    def increment_global_step(self):
+        return int(self.store.add("%s/%s/global_step" % (STORE_PREFIX, self.run_id), 1))
+
+    def global_step(self):
+        return int(self.store.add("%s/%s/global_step" % (STORE_PREFIX, self.run_id), 0))
+
+    def close(self):
+        pg.barrier()
+        if self.mode == "shm" and self.rank in self.flat:
+            try:
+                os.remove("/dev/shm/%s_%s_owner%d" % (STORE_PREFIX, self.run_id, self.rank))
+            except OSError:
+                pass
+
+
+def _default_store():
+    if pg.world_size() > 1:
+        # the default process group's store (TCPStore on rank 0)
+        from torch.distributed import distributed_c10d as c10d
+        return c10d._get_default_store()
+    return _LocalStore()
+
+
+class _LocalStore:
+    """Single-process stand-in for the c10d store API used here."""
+
+    def __init__(self):
+        self.d = {}
+
+    def set(self, k, v):
+        self.d[k] = v if isinstance(v, bytes) else str(v).encode()
+
+    def get(self, k):
+        return self.d[k]
+
+    def add(self, k, n):
+        v = int(self.d.get(k, b"0")) + n
+        self.d[k] = str(v).encode()
+        return v
+
+    def wait(self, keys, timeout=None):
+        for k in keys:
+            if k not in self.d:
+                raise KeyError(k)
+
+
+class ASPTrainStep:
+    """Worker step in ASP mode: pull -> fwd/bwd -> push; no collective on the critical path."""
+
+    def __init__(self, model, loss_fn, store: ParamStore, lr_schedule=None, ssp_clock=None):
+        self.model, self.loss_fn, self.store = model, loss_fn, store
+        self.lr_schedule = lr_schedule
+        self.ssp = ssp_clock
+        self.local_step = 0
+
+    def __call__(self, images, labels):
+        self.store.pull()
+        for p in self.store.params:
+            p.grad = None
+        out = self.model(images, training=True)
+        loss = self.loss_fn(out, labels)
+        loss.backward()
+        gs = self.store.global_step()
+        lr = self.lr_schedule(gs) if self.lr_schedule else None
+        self.store.push([getattr(p, "main_grad", None) if p.grad is None else p.grad for p in self.store.params],
+                        lr=lr)
+        gstep = self.store.increment_global_step()
+        self.local_step += 1
+        if self.ssp is not None:
+            self.ssp.tick(self.local_step)
+        return loss.detach(), gstep
+
+
+def wait_all_done(store, world, run_id, timeout_s=600):
+    """Workers finishing at different speeds (ASP) meet here before teardown."""
+    k = "%s/%s/done" % (STORE_PREFIX, run_id)
+    store.add(k, 1)
+    t0 = time.time()
+    while int(store.add(k, 0)) < world:
+        if time.time() - t0 > timeout_s:
+            raise TimeoutError("ASP teardown")
+        time.sleep(0.01)
+    if dist.is_available() and dist.is_initialized():
+        pass
