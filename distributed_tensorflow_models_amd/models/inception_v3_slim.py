@@ -1,0 +1,192 @@
+"""Inception-v3 in the bundled *old* TF-Slim (reference inception/slim/inception_model.py:54-358,
+wrapper inception/inception_model.py:49-96) - the model of the inception_{bsp,asp,ssp} trainers.
+
+Checkpoint layout is reproduced exactly (golden: inception/slim/collections_test.py:35-117):
+no top-level prefix, default op scopes uniquified per variable scope ('Conv', 'Conv_1', ...),
+conv = weights + BatchNorm{beta, moving_mean, moving_variance} (scale=False: no gamma), aux head
+'aux_logits/{proj,Conv,FC}', classifier 'logits/logits/{weights,biases}'.
+Defaults (inception_v3_parameters): weight decay 4e-5 on conv+fc weights, conv stddev 0.1,
+BN decay 0.9997 eps 1e-3 (biased moving variance - tf.nn.moments path), dropout keep 0.8.
+Returns (logits, aux_logits) in training mode; the trainer weights the aux loss by 0.4.
+"""
+import torch
+
+from ..ops import nn as F
+from .layers import BatchNorm, Conv2d, Dropout, FullyConnected, Layer
+
+
+class _Scope:
+    """old-slim default scope names: ops.conv2d -> 'Conv', 'Conv_1', ... inside one variable scope."""
+
+    def __init__(self, prefix):
+        self.prefix = prefix
+        self.counts = {}
+
+    def name(self, scope, default):
+        if scope is not None:
+            return self.prefix + scope
+        n = self.counts.get(default, 0)
+        self.counts[default] = n + 1
+        return self.prefix + (default if n == 0 else "%s_%d" % (default, n))
+
+
+class InceptionV3Slim(Layer):
+    default_image_size = 299
+
+    def __init__(self, num_classes=1001, dropout_keep_prob=0.8, weight_decay=0.00004, stddev=0.1,
+                 batch_norm_decay=0.9997, batch_norm_epsilon=0.001, scope=""):
+        super().__init__(scope)
+        self._bn = dict(decay=batch_norm_decay, epsilon=batch_norm_epsilon, scale=False, bessel=False)
+        self._wd, self._std = weight_decay, stddev
+        self.layers = torch.nn.ModuleDict()
+        self.plan = []
+        self.num_classes = num_classes
+        c = self._stem(scope)
+        for name, width in (("mixed_35x35x256a", 32), ("mixed_35x35x288a", 64), ("mixed_35x35x288b", 64)):
+            c = self._mixed35(scope + name, c, width)
+        c = self._mixed17a(scope + "mixed_17x17x768a", c)
+        for name, w in (("mixed_17x17x768b", 128), ("mixed_17x17x768c", 160), ("mixed_17x17x768d", 160),
+                        ("mixed_17x17x768e", 192)):
+            c = self._mixed17(scope + name, c, w)
+        # aux head
+        sc = _Scope(scope + "aux_logits/")
+        self.aux_proj = self._conv(sc.name("proj", "Conv"), c, 128, 1)
+        self.aux_conv = self._conv(sc.name(None, "Conv"), 128, 768, 5, padding="VALID", stddev=0.01)
+        self.aux_fc = FullyConnected(sc.name(None, "FC"), 768, num_classes, None, None, True, weight_decay,
+                                     ("truncated_normal", 0.001), 0.0)
+        c = self._mixed17_1280(scope + "mixed_17x17x1280a", c)
+        c = self._mixed8(scope + "mixed_8x8x2048a", c)
+        c = self._mixed8(scope + "mixed_8x8x2048b", c)
+        self.dropout = Dropout(scope + "logits/dropout", dropout_keep_prob)
+        self.fc = FullyConnected(scope + "logits/logits", c, num_classes, None, None, True, weight_decay,
+                                 ("truncated_normal", 0.01), 0.0)
+
+    # ---- builders -------------------------------------------------------------------------------
+    def _conv(self, name, cin, cout, k, stride=1, padding="SAME", stddev=None):
+        c = Conv2d(name, cin, cout, k, stride, padding, "relu", dict(self._bn), False, self._wd,
+                   ("truncated_normal", self._std if stddev is None else stddev))
+        self.layers[name.replace("/", "__") or "root"] = c
+        return c
+
+    def _stem(self, scope):
+        sc = _Scope(scope)
+        self.stem = [self._conv(sc.name("conv0", "Conv"), 3, 32, 3, 2, "VALID"),
+                     self._conv(sc.name("conv1", "Conv"), 32, 32, 3, 1, "VALID"),
+                     self._conv(sc.name("conv2", "Conv"), 32, 64, 3, 1, "SAME"),
+                     "pool1",
+                     self._conv(sc.name("conv3", "Conv"), 64, 80, 1, 1, "VALID"),
+                     self._conv(sc.name("conv4", "Conv"), 80, 192, 3, 1, "VALID"),
+                     "pool2"]
+        return 192
+
+    def _mixed35(self, s, cin, pool_w):
+        b = {}
+        b["branch1x1"] = [self._conv(_Scope(s + "/branch1x1/").name(None, "Conv"), cin, 64, 1)]
+        sc = _Scope(s + "/branch5x5/")
+        b["branch5x5"] = [self._conv(sc.name(None, "Conv"), cin, 48, 1), self._conv(sc.name(None, "Conv"), 48, 64, 5)]
+        sc = _Scope(s + "/branch3x3dbl/")
+        b["branch3x3dbl"] = [self._conv(sc.name(None, "Conv"), cin, 64, 1), self._conv(sc.name(None, "Conv"), 64, 96, 3),
+                             self._conv(sc.name(None, "Conv"), 96, 96, 3)]
+        b["branch_pool"] = ["avg3", self._conv(_Scope(s + "/branch_pool/").name(None, "Conv"), cin, pool_w, 1)]
+        self.plan.append((s, "cat", [b["branch1x1"], b["branch5x5"], b["branch3x3dbl"], b["branch_pool"]]))
+        return 64 + 64 + 96 + pool_w
+
+    def _mixed17a(self, s, cin):
+        br3 = [self._conv(_Scope(s + "/branch3x3/").name(None, "Conv"), cin, 384, 3, 2, "VALID")]
+        sc = _Scope(s + "/branch3x3dbl/")
+        dbl = [self._conv(sc.name(None, "Conv"), cin, 64, 1), self._conv(sc.name(None, "Conv"), 64, 96, 3),
+               self._conv(sc.name(None, "Conv"), 96, 96, 3, 2, "VALID")]
+        self.plan.append((s, "cat", [br3, dbl, ["max3s2"]]))
+        return 384 + 96 + cin
+
+    def _mixed17(self, s, cin, w):
+        b1 = [self._conv(_Scope(s + "/branch1x1/").name(None, "Conv"), cin, 192, 1)]
+        sc = _Scope(s + "/branch7x7/")
+        b7 = [self._conv(sc.name(None, "Conv"), cin, w, 1), self._conv(sc.name(None, "Conv"), w, w, (1, 7)),
+              self._conv(sc.name(None, "Conv"), w, 192, (7, 1))]
+        sc = _Scope(s + "/branch7x7dbl/")
+        b7d = [self._conv(sc.name(None, "Conv"), cin, w, 1), self._conv(sc.name(None, "Conv"), w, w, (7, 1)),
+               self._conv(sc.name(None, "Conv"), w, w, (1, 7)), self._conv(sc.name(None, "Conv"), w, w, (7, 1)),
+               self._conv(sc.name(None, "Conv"), w, 192, (1, 7))]
+        bp = ["avg3", self._conv(_Scope(s + "/branch_pool/").name(None, "Conv"), cin, 192, 1)]
+        self.plan.append((s, "cat", [b1, b7, b7d, bp]))
+        if s.endswith("mixed_17x17x768e"):
+            self.plan.append((s, "aux", None))
+        return 768
+
+    def _mixed17_1280(self, s, cin):
+        sc = _Scope(s + "/branch3x3/")
+        b3 = [self._conv(sc.name(None, "Conv"), cin, 192, 1), self._conv(sc.name(None, "Conv"), 192, 320, 3, 2, "VALID")]
+        sc = _Scope(s + "/branch7x7x3/")
+        b7 = [self._conv(sc.name(None, "Conv"), cin, 192, 1), self._conv(sc.name(None, "Conv"), 192, 192, (1, 7)),
+              self._conv(sc.name(None, "Conv"), 192, 192, (7, 1)),
+              self._conv(sc.name(None, "Conv"), 192, 192, 3, 2, "VALID")]
+        self.plan.append((s, "cat", [b3, b7, ["max3s2"]]))
+        return 320 + 192 + cin
+
+    def _mixed8(self, s, cin):
+        b1 = [self._conv(_Scope(s + "/branch1x1/").name(None, "Conv"), cin, 320, 1)]
+        sc = _Scope(s + "/branch3x3/")
+        b3 = [self._conv(sc.name(None, "Conv"), cin, 384, 1),
+              ("split", self._conv(sc.name(None, "Conv"), 384, 384, (1, 3)), self._conv(sc.name(None, "Conv"), 384, 384, (3, 1)))]
+        sc = _Scope(s + "/branch3x3dbl/")
+        b3d = [self._conv(sc.name(None, "Conv"), cin, 448, 1), self._conv(sc.name(None, "Conv"), 448, 384, 3),
+               ("split", self._conv(sc.name(None, "Conv"), 384, 384, (1, 3)),
+                self._conv(sc.name(None, "Conv"), 384, 384, (3, 1)))]
+        bp = ["avg3", self._conv(_Scope(s + "/branch_pool/").name(None, "Conv"), cin, 192, 1)]
+        self.plan.append((s, "cat", [b1, b3, b3d, bp]))
+        return 320 + 768 + 768 + 192
+
+    # ---- forward --------------------------------------------------------------------------------
+    @staticmethod
+    def _run(branch, x, training):
+        for op in branch:
+            if op == "avg3":
+                x = F.avg_pool(x, 3, 1, "SAME")
+            elif op == "max3s2":
+                x = F.max_pool(x, 3, 2, "VALID")
+            elif isinstance(op, tuple):
+                x = torch.cat([_t(op[1](x, training)), _t(op[2](x, training))], dim=-1)
+            else:
+                x = op(x, training)
+        return x
+
+    def forward(self, x, training=True, end_points=None):
+        net = x
+        for op in self.stem:
+            net = F.max_pool(net, 3, 2, "VALID") if isinstance(op, str) else op(net, training)
+        aux = None
+        for name, kind, branches in self.plan:
+            if kind == "aux":
+                a = F.avg_pool(net, 5, 3, "VALID")
+                a = self.aux_conv(self.aux_proj(a, training), training)
+                aux = self.aux_fc(_t(a).reshape(a.shape[0], -1), training)
+                if end_points is not None:
+                    end_points["aux_logits"] = aux
+                continue
+            net = torch.cat([_t(self._run(b, net, training)) for b in branches], dim=-1)
+            if end_points is not None:
+                end_points[name] = net
+        k = net.shape[1]
+        net = F.avg_pool(net, (k, net.shape[2]), 1, "VALID")
+        net = self.dropout(_t(net).reshape(net.shape[0], -1), training)
+        logits = self.fc(net, training)
+        if end_points is not None:
+            end_points["logits"] = logits
+            end_points["predictions"] = torch.softmax(logits.float(), -1)
+        if training:
+            return logits, aux
+        return logits
+
+
+def _t(x):
+    from ..ops.lazy import as_tensor
+    return as_tensor(x)
+
+
+def inference(num_classes=1001, for_training=True, **kw):
+    """inception/inception_model.py:inference equivalent (returns the module)."""
+    return InceptionV3Slim(num_classes=num_classes, **kw)
+
+
+BN_CLS = BatchNorm  # re-export for tests
