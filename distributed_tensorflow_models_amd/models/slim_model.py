@@ -1,0 +1,46 @@
+"""Wrap functional slim-style model code (compat.slim) as an nn.Module.
+
+The first (build) pass creates every variable in a private VariableStore with its TF name; the
+Module registers them so ``.to(device)``, optimizers, DP buckets and the Saver see them.  Each
+forward re-executes the model function, re-using the variables by name (graph = code).
+"""
+import re
+
+import torch
+
+from ..compat import slim
+
+
+class SlimModel(torch.nn.Module):
+    def __init__(self, fn, image_size, num_classes=None, in_channels=3, build_batch=1, name=None, **kw):
+        super().__init__()
+        self.fn, self.kw = fn, kw
+        self.num_classes = num_classes
+        self.default_image_size = image_size
+        self.scope = name or getattr(fn, "__name__", "slim_model")
+        self.store = slim.VariableStore()
+        hw = image_size if isinstance(image_size, (tuple, list)) else (image_size, image_size)
+        with torch.no_grad():
+            self._run(torch.zeros(build_batch, hw[0], hw[1], in_channels), training=False, end_points=None)
+        for n, v in self.store.vars.items():
+            if v.dtype.is_floating_point:
+                self.register_parameter(re.sub(r"[^0-9a-zA-Z_]", "_", n), v)
+            else:
+                self.register_buffer(re.sub(r"[^0-9a-zA-Z_]", "_", n), v.data)
+
+    def _run(self, x, training, end_points):
+        with slim.use_store(self.store):
+            slim.begin_pass()
+            with slim.training_mode(training):
+                kw = dict(self.kw)
+                if self.num_classes is not None:
+                    kw["num_classes"] = self.num_classes
+                out = self.fn(x, is_training=training, **kw)
+        if isinstance(out, tuple) and len(out) == 2 and isinstance(out[1], dict):
+            out, ep = out
+            if end_points is not None:
+                end_points.update(ep)
+        return out
+
+    def forward(self, x, training=True, end_points=None):
+        return self._run(x, training, end_points)
