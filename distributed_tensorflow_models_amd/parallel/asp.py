@@ -159,6 +159,12 @@ class ParamStore:
     def global_step(self):
         return int(self.store.add("%s/%s/global_step" % (STORE_PREFIX, self.run_id), 0))
 
+    def set_global_step(self, n):
+        """Resume: move the shared counter to ``n`` (chief only, before workers start)."""
+        cur = self.global_step()
+        if n != cur:
+            self.store.add("%s/%s/global_step" % (STORE_PREFIX, self.run_id), int(n) - cur)
+
     def close(self):
         pg.barrier()
         if self.mode == "shm" and self.rank in self.flat:

@@ -1,0 +1,17 @@
+"""Entry script: reference (none: headline benchmark model, slim resnet_v1_50) (preset ``resnet50``, default sync mode ``bsp``).
+
+Accepts the reference flags (--job_name/--ps_hosts/--worker_hosts/--task_id/--batch_size/--data_dir/
+--train_dir/--max_steps ...) plus the MI355X extras (--sync_mode, --synthetic_data, --fresh, ...).
+"""
+from ..compat import flags
+from .. import trainer
+
+trainer.define_common_flags(flags, "resnet50")
+
+
+def main(_argv=None):
+    return trainer.train("resnet50", flags, default_mode="bsp")
+
+
+if __name__ == "__main__":
+    flags.run(main)
