@@ -302,42 +302,16 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
 }
 
-// LDS reduction of per-lane [8] partials over the RP row-lanes of each column, then atomics
-// out0/out1 point into this block's partial row of the workspace (plain stores; see workspace.hip)
-__device__ __forceinline__ void col_reduce_commit(float (*red)[256][8], const float* s, const float* q, float* out0,
-                                                  float* out1, int cols, int c0) {
-  const int t = threadIdx.x, RP = 256 / cols;
-  if (RP == 1) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { out0[c0 + e] = s[e]; out1[c0 + e] = q[e]; }
-    return;
-  }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) { red[0][t][e] = s[e]; red[1][t][e] = q[e]; }
-  __syncthreads();
-  // tree over row-lanes: lane t (< 256/2^k) adds partner t + 256/2^(k+1) of the same column
-  for (int h = 128; h >= cols; h >>= 1) {
-    if (t < h) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { red[0][t][e] += red[0][t + h][e]; red[1][t][e] += red[1][t + h][e]; }
-    }
-    __syncthreads();
-  }
-  if (t < cols) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { out0[c0 + e] = red[0][t][e]; out1[c0 + e] = red[1][t][e]; }
-  }
-}
 
 __global__ __launch_bounds__(256) void bn_stats_fast(const bf16_t* __restrict__ x, float* __restrict__ stats, int M,
                                                      int C, int rpb) {
   __shared__ float red[2][256][8];
-  const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t & (cols - 1)) * 8;
+  const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t % cols) * 8, lr0 = t / cols;
   const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
   float s[8], q[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.f;
-  for (int r = r0 + t / cols; r < r1; r += RP * FU) {
+  for (int r = lr0 < RP ? r0 + lr0 : r1; r < r1; r += RP * FU) {
     uint4 v[FU];
 #pragma unroll
     for (int u = 0; u < FU; ++u) {
@@ -351,13 +325,13 @@ __global__ __launch_bounds__(256) void bn_stats_fast(const bf16_t* __restrict__ 
       for (int e = 0; e < 8; ++e) { s[e] += f[e]; q[e] += f[e] * f[e]; }
     }
   }
-  col_reduce_commit(red, s, q, stats + (size_t)blockIdx.x * 2 * C, stats + (size_t)blockIdx.x * 2 * C + C, cols, c0);
+  col_reduce8(red, s, q, stats + (size_t)blockIdx.x * 2 * C, stats + (size_t)blockIdx.x * 2 * C + C, cols, c0);
 }
 
 __global__ __launch_bounds__(256) void bn_apply_fast(const bf16_t* __restrict__ x, const float* __restrict__ ss,
                                                      const bf16_t* __restrict__ res, const float* __restrict__ rss,
                                                      bf16_t* __restrict__ y, int M, int C, int res_mode, int relu, int rpb) {
-  const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t & (cols - 1)) * 8;
+  const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t % cols) * 8, lr0 = t / cols;
   float sc[8], sh[8], rsc[8], rsh[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -366,7 +340,7 @@ __global__ __launch_bounds__(256) void bn_apply_fast(const bf16_t* __restrict__ 
     rsh[e] = res_mode == 2 ? rss[C + c0 + e] : 0.f;
   }
   const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
-  for (int r = r0 + t / cols; r < r1; r += RP * FU) {
+  for (int r = lr0 < RP ? r0 + lr0 : r1; r < r1; r += RP * FU) {
     uint4 v[FU], w[FU];
 #pragma unroll
     for (int u = 0; u < FU; ++u) {
@@ -400,7 +374,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_fast(const bf16_t* __restri
                                                           const bf16_t* __restrict__ ym, const float* __restrict__ ss,
                                                           float* __restrict__ sums, int M, int C, int mask_mode, int rpb) {
   __shared__ float red[2][256][8];
-  const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t & (cols - 1)) * 8;
+  const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t % cols) * 8, lr0 = t / cols;
   float sc[8], sh[8], mu[8], rs[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -410,7 +384,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_fast(const bf16_t* __restri
   float s[8], q[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.f;
-  for (int r = r0 + t / cols; r < r1; r += RP * FU) {
+  for (int r = lr0 < RP ? r0 + lr0 : r1; r < r1; r += RP * FU) {
     uint4 a[FU], b[FU], m[FU];
 #pragma unroll
     for (int u = 0; u < FU; ++u) {
@@ -437,7 +411,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_fast(const bf16_t* __restri
       for (int e = 0; e < 8; ++e) { s[e] += g[e]; q[e] += g[e] * (xv[e] - mu[e]) * rs[e]; }
     }
   }
-  col_reduce_commit(red, s, q, sums + (size_t)blockIdx.x * 2 * C, sums + (size_t)blockIdx.x * 2 * C + C, cols, c0);
+  col_reduce8(red, s, q, sums + (size_t)blockIdx.x * 2 * C, sums + (size_t)blockIdx.x * 2 * C + C, cols, c0);
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_apply_fast(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
@@ -445,7 +419,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fast(const bf16_t* __restric
                                                          const float* __restrict__ sums, bf16_t* __restrict__ dx,
                                                          bf16_t* __restrict__ gout, int M, int C, int mask_mode,
                                                          int training, int rpb) {
-  const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t & (cols - 1)) * 8;
+  const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t % cols) * 8, lr0 = t / cols;
   const float invM = 1.f / (float)M;
   float sc[8], sh[8], mu[8], rs[8], A[8], Bq[8];
 #pragma unroll
@@ -455,7 +429,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fast(const bf16_t* __restric
     Bq[e] = training ? sums[C + c0 + e] * invM : 0.f;
   }
   const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
-  for (int r = r0 + t / cols; r < r1; r += RP * FU) {
+  for (int r = lr0 < RP ? r0 + lr0 : r1; r < r1; r += RP * FU) {
     uint4 a[FU], b[FU], m[FU];
 #pragma unroll
     for (int u = 0; u < FU; ++u) {
@@ -493,7 +467,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fast(const bf16_t* __restric
 static bool fast_ok(long M, int C) {
   if (C % 8) return false;
   int cols = C / 8;
-  return cols <= 256 && (256 % cols) == 0 && M < (1l << 31) && M * (long)C < (1l << 40);
+  return cols <= 256 && M < (1l << 31) && M * (long)C < (1l << 40);
 }
 // grid / rows-per-block for the column-fixed kernels: >= ~8 chunks per lane, <= 2048 blocks
 static void fast_grid(long M, int C, int* blocks, int* rpb) {

@@ -58,3 +58,43 @@ __host__ static inline FastDiv make_fastdiv(uint32_t d) {
 // workspace arena + two-stage reduction (workspace.hip)
 float* dtm_ws_get(size_t floats);
 void dtm_reduce_rows(const float* ws, int rows, int width, int ld, float* out, hipStream_t st);
+
+// Column-fixed lane mapping used by the BN kernels: lane t owns channel block (t % cols) * 8 and
+// row-lane t / cols; with RP = 256 / cols row-lanes, lanes >= RP*cols idle (C/8 need not divide 256).
+// col_reduce8 sums the per-lane [8] partials of the RP row-lanes of each column in LDS and writes
+// the per-block partial row out0[c0..c0+7], out1[...] (plain stores; reduced later by reduce_rows).
+__device__ __forceinline__ void col_reduce8(float (*red)[256][8], const float* s, const float* q, float* out0,
+                                            float* out1, int cols, int c0) {
+  const int t = threadIdx.x, RP = 256 / cols;
+  if (RP == 1) {
+    if (t < cols) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { out0[c0 + e] = s[e]; out1[c0 + e] = q[e]; }
+    }
+    return;
+  }
+  __syncthreads();  // red may still be read by a previous call
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[0][t][e] = s[e]; red[1][t][e] = q[e]; }
+  __syncthreads();
+  int P = 1;
+  while (P * 2 <= RP) P *= 2;
+  if (P < RP) {  // fold the row-lanes beyond the largest power of two
+    if (t < (RP - P) * cols) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { red[0][t][e] += red[0][t + P * cols][e]; red[1][t][e] += red[1][t + P * cols][e]; }
+    }
+    __syncthreads();
+  }
+  for (int h = P / 2; h >= 1; h >>= 1) {
+    if (t < h * cols) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { red[0][t][e] += red[0][t + h * cols][e]; red[1][t][e] += red[1][t + h * cols][e]; }
+    }
+    __syncthreads();
+  }
+  if (t < cols) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { out0[c0 + e] = red[0][t][e]; out1[c0 + e] = red[1][t][e]; }
+  }
+}

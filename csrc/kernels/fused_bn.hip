@@ -24,30 +24,6 @@ __device__ __forceinline__ uint4 pk8(const float* f) {
   return make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
 }
 
-__device__ __forceinline__ void reduce_commit2(float (*red)[256][8], const float* s, const float* q, float* out0,
-                                               float* out1, int cols, int c0) {
-  const int t = threadIdx.x, RP = 256 / cols;
-  if (RP == 1) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { out0[c0 + e] = s[e]; out1[c0 + e] = q[e]; }
-    return;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int e = 0; e < 8; ++e) { red[0][t][e] = s[e]; red[1][t][e] = q[e]; }
-  __syncthreads();
-  for (int h = 128; h >= cols; h >>= 1) {
-    if (t < h) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { red[0][t][e] += red[0][t + h][e]; red[1][t][e] += red[1][t + h][e]; }
-    }
-    __syncthreads();
-  }
-  if (t < cols) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { out0[c0 + e] = red[0][t][e]; out1[c0 + e] = red[1][t][e]; }
-  }
-}
 
 // y = act(x) path backward.  mode: 0 = plain BN (no relu), 1 = relu with mask from y, 2 = relu with
 // mask recomputed from x*scale+shift.  res_mode 0/1/2 as in bn_apply.
@@ -59,7 +35,7 @@ __global__ __launch_bounds__(256) void bn_apply_bwd_kernel(const bf16_t* __restr
                                                            float* __restrict__ sx, float* __restrict__ sr, int M, int C,
                                                            int mode, int res_mode, int rpb) {
   __shared__ float red[2][256][8];
-  const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t & (cols - 1)) * 8;
+  const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t % cols) * 8, lr0 = t / cols;
   float sc[8], sh[8], rsc[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -70,7 +46,7 @@ __global__ __launch_bounds__(256) void bn_apply_bwd_kernel(const bf16_t* __restr
 #pragma unroll
   for (int e = 0; e < 8; ++e) a1[e] = a0[e] = b1[e] = b0[e] = 0.f;
   const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
-  for (int row = r0 + t / cols; row < r1; row += RP * FU2) {
+  for (int row = lr0 < RP ? r0 + lr0 : r1; row < r1; row += RP * FU2) {
     uint4 vdy[FU2], vy[FU2], vx[FU2], vr[FU2];
 #pragma unroll
     for (int u = 0; u < FU2; ++u) {
@@ -114,20 +90,20 @@ __global__ __launch_bounds__(256) void bn_apply_bwd_kernel(const bf16_t* __restr
   }
   // partial row per block in the workspace: [Σg·x | Σg | (residual) Σg·r | Σg]
   float* row = sx + (size_t)blockIdx.x * 4 * C;
-  reduce_commit2(red, a1, a0, row, row + C, cols, c0);
-  if (res_mode == 2) reduce_commit2(red, b1, b0, row + 2 * C, row + 3 * C, cols, c0);
+  col_reduce8(red, a1, a0, row, row + C, cols, c0);
+  if (res_mode == 2) col_reduce8(red, b1, b0, row + 2 * C, row + 3 * C, cols, c0);
 }
 
 // dx = dy + dsum[c] + 2*x*dsumsq[c]   (in place on dy allowed)
 __global__ __launch_bounds__(256) void stats_combine_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                             const float* __restrict__ dstats, bf16_t* __restrict__ out,
                                                             int M, int C, int rpb) {
-  const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t & (cols - 1)) * 8;
+  const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t % cols) * 8, lr0 = t / cols;
   float a[8], b[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { a[e] = dstats[c0 + e]; b[e] = 2.f * dstats[C + c0 + e]; }
   const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
-  for (int row = r0 + t / cols; row < r1; row += RP * FU2) {
+  for (int row = lr0 < RP ? r0 + lr0 : r1; row < r1; row += RP * FU2) {
     uint4 vd[FU2], vx[FU2];
 #pragma unroll
     for (int u = 0; u < FU2; ++u) {
@@ -190,7 +166,7 @@ using namespace dtm;
 static int shape_ok(long M, int C) {
   if (C % 8) return 0;
   int cols = C / 8;
-  return cols <= 256 && (256 % cols) == 0 && M < (1l << 31);
+  return cols <= 256 && M < (1l << 31);
 }
 
 DTM_API int dtm_bn_apply_bwd(const void* dy, const void* y, const void* x, const float* ss, const void* r,

@@ -103,6 +103,8 @@ class ParamStore:
             self._init_owner(buf, k)
             torch.cuda.synchronize()
             self._owned = buf
+            if self.world == 1:
+                return buf
             fn, args = reduce_tensor(buf)
             self.store.set(key, pickle.dumps((fn, args)))
             return buf

@@ -317,6 +317,10 @@ def train(preset, flags, default_mode="bsp"):
         store.pull()
     sv.maybe_save(int(gstep), force=True)
     metrics.close()
+    if store is not None:  # owners keep their shards alive until every worker is done with them
+        from .parallel.asp import wait_all_done
+        wait_all_done(store.store, world, store.run_id)
+        store.close()
     pg.barrier()
     return 0
 

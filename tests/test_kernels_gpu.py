@@ -62,7 +62,7 @@ def test_conv_bias_relu_and_stats_free():
     assert _rel(yk, yr) < 1e-2
 
 
-@pytest.mark.parametrize("C,relu,res", [(64, True, False), (256, False, True), (40, True, True), (2048, True, False)])
+@pytest.mark.parametrize("C,relu,res", [(64, True, False), (256, False, True), (40, True, True), (2048, True, False), (80, True, True), (1280, False, False), (192, True, False)])
 def test_batch_norm(C, relu, res):
     torch.manual_seed(2)
     x = (torch.randn(4, 7, 7, C, device=DEV) * 2 + 0.5).to(torch.bfloat16).float()

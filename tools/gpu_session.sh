@@ -19,3 +19,12 @@ if [[ "$MODE" == *prof* || "$MODE" == all ]]; then
   echo "stats: $f"
   head -40 "$f" | cut -c1-220
 fi
+if [[ "$MODE" == *trainers* ]]; then
+  # every entry script for a few steps on the GPU (synthetic data where the dataset is absent)
+  for t in cifar10_cnn_bsp cifar10_alexnet_bsp cifar10_vgg_bsp cifar10_vgg_asp cifar10_resnet_bsp cifar10_cifarnet_bsp mnist_lenet_bsp imagenet_inception_bsp imagenet_inception_ssp; do
+    timeout -k 10 300 python -m distributed_tensorflow_models_amd.trainers.$t --max_steps ${TSTEPS:-6} --synthetic_data --fresh --train_dir /tmp/tr_$t --data_dir /nonexistent > gpurun_out/trainer_$t.log 2>&1 || { echo "trainer $t failed"; tail -30 gpurun_out/trainer_$t.log; exit 1; }
+    echo "== $t"; tail -n 2 gpurun_out/trainer_$t.log
+  done
+  timeout -k 10 300 python -m distributed_tensorflow_models_amd.trainers.cifar10_cnn_eval --checkpoint_dir /tmp/tr_cifar10_cnn_bsp --eval_dir /tmp/ev_cnn --run_once --data_dir /nonexistent > gpurun_out/eval_cnn.log 2>&1 || { echo "eval failed"; tail -30 gpurun_out/eval_cnn.log; exit 1; }
+  tail -n 2 gpurun_out/eval_cnn.log
+fi
