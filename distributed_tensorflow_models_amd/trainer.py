@@ -104,6 +104,7 @@ def define_common_flags(flags, preset):
             ("resnet_size", I, 32, "The size of the ResNet model to use."),
             ("protocol", S, "grpc", "accepted for compatibility; transport is RCCL/gloo"),
             ("save_interval_secs", I, p["save_secs"], "Save interval seconds."),
+            ("save_every_steps", I, 0, "also checkpoint every N global steps (0 = time-based only)"),
             ("save_summaries_secs", I, 180, "(unused, as in the reference)"),
             ("initial_learning_rate", Fl, p["lr"], "Initial learning rate."),
             ("num_epochs_per_decay", Fl, p["decay_epochs"], "Epochs after which learning rate decays."),
@@ -309,7 +310,7 @@ def train(preset, flags, default_mode="bsp"):
                 acc = (out.float().argmax(-1) == labels).float().mean().item()
             logging.info("train-batch precision @ 1 = %.3f", acc)
         if mode == "bsp" or is_chief:
-            sv.maybe_save(gs)
+            sv.maybe_save(gs, force=bool(FLAGS.save_every_steps) and gs % FLAGS.save_every_steps == 0)
         step += 1
     if mode in ("asp", "ssp"):
         if clock is not None:

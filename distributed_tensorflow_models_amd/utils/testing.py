@@ -1,0 +1,38 @@
+"""Multi-process test harness: run ``fn(rank, world, *args)`` in ``world`` spawned processes over
+a gloo process group on 127.0.0.1 (CPU), collecting each rank's return value."""
+import os
+import socket
+import tempfile
+
+import torch
+import torch.multiprocessing as mp
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _entry(rank, fn, world, port, outdir, args):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), DTM_RUN_ID="t%d" % port)
+    torch.set_num_threads(max(1, (os.cpu_count() or 2) // world))
+    from ..parallel import process_group as pg
+    pg.init(backend="gloo", timeout_s=120)
+    try:
+        out = fn(rank, world, *args)
+        torch.save(out, os.path.join(outdir, "r%d.pt" % rank))
+    finally:
+        pg.barrier()
+        pg.destroy()
+
+
+def run_workers(fn, world, *args):
+    """Returns [result_rank0, result_rank1, ...]; raises if any rank fails."""
+    port = free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_entry, args=(fn, world, port, d, args), nprocs=world, join=True, start_method="spawn")
+        return [torch.load(os.path.join(d, "r%d.pt" % r), weights_only=True) for r in range(world)]

@@ -1,0 +1,86 @@
+"""Entry scripts end-to-end on CPU: every trainer runs a few steps with the reference flags,
+writes TF-layout checkpoints, resumes, and the evaluator restores EMA shadows (SURVEY.md §2.4,
+C55-C59, §5.4)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = "distributed_tensorflow_models_amd.trainers."
+
+
+def _run(mod, *args, timeout=600):
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, "-m", PKG + mod] + list(args), cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=timeout)
+    assert p.returncode == 0, (p.stdout + p.stderr)[-4000:]
+    return p.stdout + p.stderr
+
+
+@pytest.mark.parametrize("mod,batch,style", [
+    ("cifar10_cnn_bsp", 8, "cnn"), ("cifar10_alexnet_bsp", 4, "standard"), ("cifar10_vgg_bsp", 2, "standard"),
+    ("cifar10_vgg_asp", 2, "standard"), ("cifar10_resnet_bsp", 4, "short"), ("cifar10_cifarnet_bsp", 8, "standard"),
+    ("mnist_lenet_bsp", 8, "standard"), ("imagenet_inception_bsp", 1, "short"), ("imagenet_inception_ssp", 1, "short"),
+])
+def test_trainer_runs_and_checkpoints(tmp_path, mod, batch, style):
+    d = str(tmp_path / "train")
+    out = _run(mod, "--max_steps=2", "--batch_size=%d" % batch, "--train_dir=" + d, "--data_dir=/nonexistent",
+               "--synthetic_data")
+    line = [l for l in out.splitlines() if "step 1 " in l]
+    assert line, out[-2000:]
+    if style == "short":
+        assert "(gs 2), loss= " in line[0] and "samples/s" in line[0]
+    else:
+        assert "(global_step 2), loss = " in line[0] and "examples/sec" in line[0]
+        assert line[0].startswith("time: ") == (style == "standard")
+    assert os.path.exists(os.path.join(d, "model.ckpt-2.index"))
+    assert os.path.exists(os.path.join(d, "checkpoint"))
+
+
+def test_resume_and_ema_eval(tmp_path):
+    from distributed_tensorflow_models_amd.ckpt.bundle import BundleReader
+    from distributed_tensorflow_models_amd import evaluator
+    from distributed_tensorflow_models_amd.models import nets_factory
+    d = str(tmp_path / "train")
+    _run("cifar10_cnn_bsp", "--max_steps=2", "--batch_size=8", "--train_dir=" + d)
+    out = _run("cifar10_cnn_bsp", "--max_steps=4", "--batch_size=8", "--train_dir=" + d)
+    assert "restored" in out and "step 2 (global_step 3)" in out
+    r = BundleReader(os.path.join(d, "model.ckpt-4"))
+    names = set(r.names())
+    # reference cnn layout: global step is the unnamed tf.Variable(0); EMA shadows for every weight
+    assert "Variable" in names and int(r.get_tensor("Variable")) == 4
+    assert "local3/weights/ExponentialMovingAverage" in names
+    model = nets_factory.build("cifar10_cnn", 10)
+    evaluator.restore_for_eval(model, os.path.join(d, "model.ckpt-4"), use_ema=True)
+    ema = r.get_tensor("local3/weights/ExponentialMovingAverage")
+    raw = r.get_tensor("local3/weights")
+    assert not np.allclose(ema, raw)
+    got = [p for p in model.parameters() if p.tf_name == "local3/weights"][0]
+    np.testing.assert_allclose(got.detach().numpy().reshape(ema.shape), ema, rtol=0, atol=0)
+    ev = _run("cifar10_cnn_eval", "--checkpoint_dir=" + d, "--eval_dir=" + str(tmp_path / "eval"), "--run_once",
+              "--num_examples=16", "--batch_size=8")
+    assert "precision @ 1 = " in ev and "global_step: 4" in ev
+    assert any(f.startswith("events.out.tfevents") for f in os.listdir(tmp_path / "eval"))
+
+
+def test_fresh_wipes_train_dir(tmp_path):
+    d = str(tmp_path / "train")
+    _run("cifar10_cifarnet_bsp", "--max_steps=2", "--batch_size=4", "--train_dir=" + d)
+    out = _run("cifar10_cifarnet_bsp", "--max_steps=1", "--batch_size=4", "--train_dir=" + d, "--fresh")
+    assert "restored" not in out
+    assert not os.path.exists(os.path.join(d, "model.ckpt-2.index"))
+
+
+def test_launcher_dry_run():
+    from distributed_tensorflow_models_amd.parallel import launcher
+    cmds, ev = launcher.build_commands("inception", "ssp", 8, ["--batch_size=32"], 29500, eval_=True)
+    assert len(cmds) == 8 and cmds[7][2]["RANK"] == "7" and cmds[0][2]["MASTER_ADDR"] == "127.0.0.1"
+    assert cmds[0][1][2].endswith("imagenet_inception_ssp")
+    assert ev[1][2].endswith("imagenet_inception_eval")
+    mod, extra = launcher.resolve("resnet", "asp")  # any model in any mode via --sync_mode
+    assert mod == "cifar10_resnet_bsp" and extra == ["--sync_mode=asp"]
