@@ -203,6 +203,10 @@ def truncated_normal_initializer(mean=0.0, stddev=1.0):
 trunc_normal = truncated_normal_initializer
 
 
+def random_normal_initializer(mean=0.0, stddev=1.0):
+    return ("normal", stddev)
+
+
 def xavier_initializer():
     return "xavier"
 
@@ -336,7 +340,8 @@ def _pair(v):
 @add_arg_scope
 def batch_norm(inputs, decay=0.999, center=True, scale=False, epsilon=0.001, activation_fn=None,
                is_training=None, trainable=True, scope=None, reuse=None, updates_collections=None,
-               param_initializers=None, fused=None, outputs_collections=None, bessel=None):
+               param_initializers=None, fused=None, outputs_collections=None, bessel=None, data_format=None,
+               zero_debias_moving_mean=False):
     is_training = _store.training if is_training is None else is_training
     x = as_tensor(inputs)
     C = x.shape[-1]
@@ -354,6 +359,42 @@ def batch_norm(inputs, decay=0.999, center=True, scale=False, epsilon=0.001, act
     y = F.batch_norm(x, gamma, beta, mm.data, mv.data, is_training, decay, epsilon, relu_fused, None,
                      True if bessel is None else bessel)
     return y if relu_fused else _act(y, activation_fn)
+
+
+@add_arg_scope
+def instance_norm(inputs, center=True, scale=True, epsilon=1e-6, activation_fn=None, param_initializers=None,
+                  reuse=None, variables_collections=None, outputs_collections=None, trainable=True, data_format=None,
+                  scope=None):
+    """tf.contrib.layers.instance_norm: per-sample, per-channel normalisation over H, W (NHWC)."""
+    x = as_tensor(inputs)
+    C = x.shape[-1]
+    pi = param_initializers or {}
+    with variable_scope(scope, "InstanceNorm", reuse=reuse):
+        beta = variable("beta", (C,), initializer=pi.get("beta", ("constant", 0.0)), trainable=trainable) \
+            if center else None
+        gamma = variable("gamma", (C,), initializer=pi.get("gamma", ("constant", 1.0)), trainable=trainable) \
+            if scale else None
+    xf = x.float()
+    mean = xf.mean(dim=(1, 2), keepdim=True)
+    var = xf.var(dim=(1, 2), keepdim=True, unbiased=False)
+    y = (xf - mean) * torch.rsqrt(var + epsilon)
+    if gamma is not None:
+        y = y * gamma
+    if beta is not None:
+        y = y + beta
+    return _act(y.to(x.dtype), activation_fn)
+
+
+def leaky_relu(x, alpha=0.2):
+    x = as_tensor(x)
+    return torch.nn.functional.leaky_relu(x, alpha)
+
+
+def reflect_pad(x, top, bottom, left, right):
+    """tf.pad(..., 'REFLECT') on NHWC."""
+    x = as_tensor(x)
+    y = torch.nn.functional.pad(x.permute(0, 3, 1, 2), (left, right, top, bottom), mode="reflect")
+    return y.permute(0, 2, 3, 1).contiguous()
 
 
 @add_arg_scope
@@ -381,6 +422,33 @@ def conv2d(inputs, num_outputs, kernel_size, stride=1, padding="SAME", data_form
 
 
 convolution2d = conv2d
+
+
+@add_arg_scope
+def conv2d_transpose(inputs, num_outputs, kernel_size, stride=1, padding="SAME", data_format=None,
+                     activation_fn=torch.relu, normalizer_fn=None, normalizer_params=None,
+                     weights_initializer="xavier", weights_regularizer=None, biases_initializer=("constant", 0.0),
+                     biases_regularizer=None, reuse=None, variables_collections=None, outputs_collections=None,
+                     trainable=True, scope=None):
+    """slim.conv2d_transpose: TF filter [kh, kw, num_outputs, in] (stored [in, kh, kw, out])."""
+    x = as_tensor(inputs)
+    kh, kw = _pair(kernel_size)
+    cin = x.shape[-1]
+    with variable_scope(scope, "Conv2d_transpose", reuse=reuse):
+        w = variable("weights", (cin, kh, kw, num_outputs), initializer=weights_initializer,
+                     regularizer=weights_regularizer, trainable=trainable, tf_layout="KRSC->HWIO")
+        b = None
+        if normalizer_fn is None and biases_initializer is not None:
+            b = variable("biases", (num_outputs,), initializer=biases_initializer, regularizer=biases_regularizer,
+                         trainable=trainable)
+        st = stride if isinstance(stride, int) else stride[0]
+        y = F.conv2d_transpose(x, w, b, st, padding)
+        if normalizer_fn is not None:
+            return normalizer_fn(y, activation_fn=activation_fn, **(normalizer_params or {}))
+    return _act(y, activation_fn)
+
+
+convolution2d_transpose = conv2d_transpose
 
 
 @add_arg_scope
@@ -467,12 +535,15 @@ def flatten(inputs, scope=None, outputs_collections=None):
 
 
 def repeat(inputs, repetitions, layer, *args, **kwargs):
-    """slim.repeat: layer applied n times under scope/scope_1.. (names 'conv1/conv1_1' ...)."""
-    scope = kwargs.pop("scope", None) or getattr(layer, "__name__", "repeat")
-    net = inputs
-    with variable_scope(scope):
+    """slim.repeat: ``layer`` applied n times inside variable scope ``scope`` (default-named
+    'Repeat', 'Repeat_1', ...) with per-call scopes '<scope>_1', '<scope>_2', ... where <scope>
+    falls back to the layer's __name__ (e.g. 'conv1/conv1_1', 'Repeat/block35_1')."""
+    scope = kwargs.pop("scope", None)
+    with variable_scope(scope, default_name="Repeat"):
+        base = scope.split("/")[-1] if scope else getattr(layer, "__name__", "repeat")
+        net = inputs
         for i in range(repetitions):
-            net = layer(net, *args, scope="%s_%d" % (scope.split("/")[-1], i + 1), **kwargs)
+            net = layer(net, *args, scope="%s_%d" % (base, i + 1), **kwargs)
     return net
 
 

@@ -20,8 +20,15 @@ class SlimModel(torch.nn.Module):
         self.scope = name or getattr(fn, "__name__", "slim_model")
         self.store = slim.VariableStore()
         hw = image_size if isinstance(image_size, (tuple, list)) else (image_size, image_size)
+        # build in training mode so training-only variables (e.g. NASNet aux heads) exist too;
+        # the pass's moving-statistics update is undone below (moving_* are constant-initialised)
         with torch.no_grad():
-            self._run(torch.zeros(build_batch, hw[0], hw[1], in_channels), training=False, end_points=None)
+            self._run(torch.zeros(max(build_batch, 2), hw[0], hw[1], in_channels), training=True, end_points=None)
+            for n, v in self.store.vars.items():
+                if n.endswith("moving_mean"):
+                    v.data.zero_()
+                elif n.endswith("moving_variance"):
+                    v.data.fill_(1.0)
         for n, v in self.store.vars.items():
             if v.dtype.is_floating_point:
                 self.register_parameter(re.sub(r"[^0-9a-zA-Z_]", "_", n), v)

@@ -117,20 +117,20 @@ def _mixed_v1(net, name, b0, b1a, b1b, b2a, b2b, b3, conv5_name="Conv2d_0b_3x3")
 def inception_v1_base(images, ep):
     with slim.arg_scope([slim.conv2d, slim.fully_connected], weights_initializer=slim.trunc_normal(stddev=0.01)):
         with slim.arg_scope([slim.conv2d, slim.max_pool2d], stride=1, padding="SAME"):
-            net = slim.conv2d(images, 64, 7, stride=2, scope="Conv2d_1a_7x7")
-            net = slim.max_pool2d(net, 3, stride=2, scope="MaxPool_2a_3x3")
-            net = slim.conv2d(net, 64, 1, scope="Conv2d_2b_1x1")
-            net = slim.conv2d(net, 192, 3, scope="Conv2d_2c_3x3")
-            net = slim.max_pool2d(net, 3, stride=2, scope="MaxPool_3a_3x3")
+            net = ep["Conv2d_1a_7x7"] = slim.conv2d(images, 64, 7, stride=2, scope="Conv2d_1a_7x7")
+            net = ep["MaxPool_2a_3x3"] = slim.max_pool2d(net, 3, stride=2, scope="MaxPool_2a_3x3")
+            net = ep["Conv2d_2b_1x1"] = slim.conv2d(net, 64, 1, scope="Conv2d_2b_1x1")
+            net = ep["Conv2d_2c_3x3"] = slim.conv2d(net, 192, 3, scope="Conv2d_2c_3x3")
+            net = ep["MaxPool_3a_3x3"] = slim.max_pool2d(net, 3, stride=2, scope="MaxPool_3a_3x3")
             net = ep["Mixed_3b"] = _mixed_v1(net, "Mixed_3b", 64, 96, 128, 16, 32, 32)
             net = ep["Mixed_3c"] = _mixed_v1(net, "Mixed_3c", 128, 128, 192, 32, 96, 64)
-            net = slim.max_pool2d(net, 3, stride=2, scope="MaxPool_4a_3x3")
+            net = ep["MaxPool_4a_3x3"] = slim.max_pool2d(net, 3, stride=2, scope="MaxPool_4a_3x3")
             net = ep["Mixed_4b"] = _mixed_v1(net, "Mixed_4b", 192, 96, 208, 16, 48, 64)
             net = ep["Mixed_4c"] = _mixed_v1(net, "Mixed_4c", 160, 112, 224, 24, 64, 64)
             net = ep["Mixed_4d"] = _mixed_v1(net, "Mixed_4d", 128, 128, 256, 24, 64, 64)
             net = ep["Mixed_4e"] = _mixed_v1(net, "Mixed_4e", 112, 144, 288, 32, 64, 64)
             net = ep["Mixed_4f"] = _mixed_v1(net, "Mixed_4f", 256, 160, 320, 32, 128, 128)
-            net = slim.max_pool2d(net, 2, stride=2, scope="MaxPool_5a_2x2")
+            net = ep["MaxPool_5a_2x2"] = slim.max_pool2d(net, 2, stride=2, scope="MaxPool_5a_2x2")
             net = ep["Mixed_5b"] = _mixed_v1(net, "Mixed_5b", 256, 160, 320, 32, 128, 128, "Conv2d_0a_3x3")
             net = ep["Mixed_5c"] = _mixed_v1(net, "Mixed_5c", 384, 192, 384, 48, 128, 128)
     return net
@@ -202,10 +202,12 @@ def inception_v2_base(images, ep, use_separable_conv=True):
         else:
             net = slim.conv2d(images, d(64), 7, stride=2, weights_initializer=slim.trunc_normal(1.0),
                               scope="Conv2d_1a_7x7")
-        net = slim.max_pool2d(net, 3, stride=2, scope="MaxPool_2a_3x3")
-        net = slim.conv2d(net, d(64), 1, scope="Conv2d_2b_1x1", weights_initializer=slim.trunc_normal(0.1))
-        net = slim.conv2d(net, d(192), 3, scope="Conv2d_2c_3x3")
-        net = slim.max_pool2d(net, 3, stride=2, scope="MaxPool_3a_3x3")
+        ep["Conv2d_1a_7x7"] = net
+        net = ep["MaxPool_2a_3x3"] = slim.max_pool2d(net, 3, stride=2, scope="MaxPool_2a_3x3")
+        net = ep["Conv2d_2b_1x1"] = slim.conv2d(net, d(64), 1, scope="Conv2d_2b_1x1",
+                                                weights_initializer=slim.trunc_normal(0.1))
+        net = ep["Conv2d_2c_3x3"] = slim.conv2d(net, d(192), 3, scope="Conv2d_2c_3x3")
+        net = ep["MaxPool_3a_3x3"] = slim.max_pool2d(net, 3, stride=2, scope="MaxPool_3a_3x3")
 
         def mixed(net, name, b0, b1, b2, b3, pool="avg"):
             with slim.variable_scope(name):

@@ -139,6 +139,85 @@ def conv2d(x, w, bias=None, stride=1, padding="SAME", relu=False, dilation=1):
     return _Conv2dFn.apply(x.to(torch.bfloat16), w, bias, g, relu)
 
 
+class _Conv2dTransposeFn(torch.autograd.Function):
+    """y = C^T x for the conv C: y-space -> x-space with weight w [Cx, R, S, Cy] (KRSC) and
+    geometry ``geom`` (input = y-space).  Forward is C's dgrad kernel, backward is C's forward
+    (dx) and C's wgrad with the roles of input / output-grad swapped (dw)."""
+
+    @staticmethod
+    def forward(ctx, x, w, geom):
+        L = _lib.lib()
+        s = _lib.stream_ptr()
+        g = geom
+        x = x.contiguous()
+        w16 = weight_bf16(w)
+        wt = torch.empty((g.C, g.R, g.S, g.K), device=x.device, dtype=torch.bfloat16)
+        L.dtm_weight_flip_transpose(_lib.ptr(w16), _lib.ptr(wt), g.K, g.R, g.S, g.C, s)
+        y = torch.empty((g.N, g.H, g.W, g.C), device=x.device, dtype=torch.bfloat16)
+        d = g.as_desc(_lib.ConvDesc)
+        _check(L.dtm_conv_dgrad(_lib.ptr(x), _lib.ptr(wt), _lib.ptr(y), ctypes.byref(d), s), "conv_transpose")
+        ctx.geom = g
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L = _lib.lib()
+        s = _lib.stream_ptr()
+        x, w = ctx.saved_tensors
+        g = ctx.geom
+        dy = dy.contiguous().to(torch.bfloat16)
+        d = g.as_desc(_lib.ConvDesc)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty((g.N, g.P, g.Q, g.K), device=dy.device, dtype=torch.bfloat16)
+            _check(L.dtm_conv_fwd(_lib.ptr(dy), _lib.ptr(weight_bf16(w)), _lib.ptr(dx), None, None, None, None, 0,
+                                  ctypes.byref(d), s), "conv_transpose_bwd_data")
+        dw = None
+        if ctx.needs_input_grad[1]:
+            mg = getattr(w, "main_grad", None)
+            target = mg if mg is not None else torch.zeros(w.shape, device=dy.device, dtype=torch.float32)
+            _check(L.dtm_conv_wgrad(_lib.ptr(dy), _lib.ptr(x), _lib.ptr(target), None, None, ctypes.byref(d),
+                                    _lib.num_cus(), s), "conv_transpose_bwd_filter")
+            if mg is not None:
+                _notify(w)
+            else:
+                dw = target
+        return dx, dw, None
+
+
+def conv2d_transpose(x, w, bias=None, stride=2, padding="SAME", relu=False):
+    """TF conv2d_transpose, NHWC.  x [N,Hx,Wx,Cx]; w fp32 master [Cx, R, S, Cy] (KRSC of the conv
+    this op is the gradient of; TF filter [R,S,Cy,Cx] = w.permute(1,2,3,0)); -> [N,Hy,Wy,Cy] with
+    Hy = Hx*stride (SAME) or (Hx-1)*stride+R (VALID)."""
+    x = as_tensor(x)
+    Cx, R, S, Cy = w.shape
+    N, Hx, Wx, _ = x.shape
+    if str(padding).upper() == "SAME":
+        Hy, Wy = Hx * stride, Wx * stride
+    else:
+        Hy, Wy = (Hx - 1) * stride + R, (Wx - 1) * stride + S
+    if not x.is_cuda:
+        y = ref.conv2d_transpose(x, w.permute(1, 2, 3, 0), stride, padding, (Hy, Wy))
+    else:
+        wp, xp = w, x.to(torch.bfloat16)
+        if Cy % 8:
+            wp = _PadChannels.apply(wp, (Cy + 7) // 8 * 8)
+        if Cx % 8:
+            cxp = (Cx + 7) // 8 * 8
+            wp = _PadOutChannels.apply(wp, cxp)
+            xp = torch.nn.functional.pad(xp, (0, cxp - Cx))
+        g = conv_geom((N, Hy, Wy, wp.shape[-1]), tuple(wp.shape), stride, padding)
+        if (g.P, g.Q) != (Hx, Wx):
+            raise ValueError("conv2d_transpose geometry mismatch: %s vs input %s" % ((g.P, g.Q), (Hx, Wx)))
+        y = _Conv2dTransposeFn.apply(xp, wp, g)
+        if Cy % 8:
+            y = y[..., :Cy].contiguous()
+    if bias is not None:
+        y = y + bias.to(y.dtype)
+    return torch.relu(y) if relu else y
+
+
 class _PadOutChannels(torch.autograd.Function):
     """Zero-pad dim 0 (output channels) of a fp32 weight / bias."""
 
