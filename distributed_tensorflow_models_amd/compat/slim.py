@@ -215,16 +215,31 @@ def variance_scaling_initializer(factor=2.0, mode="FAN_IN", uniform=False):
     return ("variance_scaling", (factor, mode))
 
 
-def l2_regularizer(scale):
-    return ("l2", float(scale))
+class _Regularizer(tuple):
+    """(kind, scale) record consumed by ``variable`` (L2 becomes coupled weight decay in the
+    fused optimizer) that is also callable like slim's regularizer fns: reg(tensor) -> loss
+    (inception/slim/losses.py:37-99)."""
+
+    def __call__(self, t):
+        kind, scale = self
+        t = t.float()
+        if kind == "l2":
+            return scale * (t ** 2).sum() / 2.0
+        if kind == "l1":
+            return scale * t.abs().sum()
+        return scale[0] * t.abs().sum() + scale[1] * (t ** 2).sum() / 2.0
 
 
-def l1_regularizer(scale):
-    return ("l1", float(scale))
+def l2_regularizer(scale=1.0, scope=None):
+    return _Regularizer(("l2", float(scale)))
 
 
-def l1_l2_regularizer(scale_l1=1.0, scale_l2=1.0):
-    return ("l1_l2", (float(scale_l1), float(scale_l2)))
+def l1_regularizer(scale=1.0, scope=None):
+    return _Regularizer(("l1", float(scale)))
+
+
+def l1_l2_regularizer(scale_l1=1.0, scale_l2=1.0, scope=None):
+    return _Regularizer(("l1_l2", (float(scale_l1), float(scale_l2))))
 
 
 @add_arg_scope

@@ -65,6 +65,31 @@ class StalenessClock:
         self.store.set(self.prefix + str(self.rank), str(1 << 40))
 
 
+class SspManager:
+    """Compatibility factory for the reference's ``SspManager(num_of_replicas, max_stale)``
+    (inception/ssp_manager.py: Thrift ``CheckStaleness`` server on PS 0 + per-worker clients).
+    There is no server process here: the "server" is the c10d store every rank already shares,
+    and a client's ``check_staleness(task_index, local_step)`` is ``StalenessClock.tick``."""
+
+    def __init__(self, num_of_replicas, max_stale=5, run_id="0"):
+        self.world, self.max_stale, self.run_id = int(num_of_replicas), int(max_stale), run_id
+        self._clock = None
+
+    def create_rpc_server(self, host=None):
+        return self  # nothing to serve; kept so reference-style call sites still work
+
+    def serve(self):
+        return None
+
+    def create_rpc_client(self, host=None):
+        return self
+
+    def check_staleness(self, task_index, local_step):
+        if self._clock is None:
+            self._clock = StalenessClock(self.max_stale, rank=task_index, world=self.world, run_id=self.run_id)
+        return self._clock.tick(local_step)
+
+
 def main():  # debug CLI (replaces CheckStaleness-remote): print the clock of a running job
     import argparse
     import datetime
