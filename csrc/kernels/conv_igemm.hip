@@ -209,10 +209,18 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
     __syncthreads();
   }
 
-  // epilogue: lane holds channels (fk*4 .. +3) of pixel fr for every subtile
+  // epilogue: lane holds channels (fk*4 .. +3) of pixel fr for every subtile.  Bias/ReLU and the
+  // BatchNorm statistics (from the bf16-rounded outputs) are done in registers; the tile is then
+  // staged through LDS (padded rows: conflict-free 8-B lane writes) so that every global store is a
+  // full 16-B chunk and consecutive lanes cover whole NHWC pixel rows (coalesced, 256-B rows for
+  // CT = 128) instead of 16 scattered 32-B pieces per wave instruction.
+  constexpr int OROW = CT * 2 + 16;
+  static_assert(PT * OROW <= 2 * BUF, "output staging fits in the operand buffers");
+  const bool staged = (a.K & 7) == 0;
 #pragma unroll
   for (int i = 0; i < TC; ++i) {
-    const int kch = c0 + wc * WC + i * 16 + fk * 4;
+    const int kloc = wc * WC + i * 16 + fk * 4;
+    const int kch = c0 + kloc;
     float bsum[4] = {0.f, 0.f, 0.f, 0.f}, bsq[4] = {0.f, 0.f, 0.f, 0.f};
     float bia[4] = {0.f, 0.f, 0.f, 0.f};
     if (a.bias && kch < a.K) {
@@ -221,7 +229,8 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
     }
 #pragma unroll
     for (int j = 0; j < TP; ++j) {
-      const int m = p0 + wp * WP + j * 16 + fr;
+      const int mloc = wp * WP + j * 16 + fr;
+      const int m = p0 + mloc;
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -229,15 +238,17 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
         if (a.relu) v[r] = fmaxf(v[r], 0.f);
       }
       uint32_t lo = pack2bf(v[0], v[1]), hi = pack2bf(v[2], v[3]);
-      if (m < a.M && kch < a.K) {
+      if (staged) {
+        *(uint2*)(smem + mloc * OROW + kloc * 2) = make_uint2(lo, hi);
+      } else if (m < a.M && kch < a.K) {
         *(uint2*)(a.y + (size_t)m * a.K + kch) = make_uint2(lo, hi);
-        if (a.stats) {
-          float q0 = lo_bf(lo), q1 = hi_bf(lo), q2 = lo_bf(hi), q3 = hi_bf(hi);
-          bsum[0] += q0; bsq[0] += q0 * q0;
-          bsum[1] += q1; bsq[1] += q1 * q1;
-          bsum[2] += q2; bsq[2] += q2 * q2;
-          bsum[3] += q3; bsq[3] += q3 * q3;
-        }
+      }
+      if (a.stats && m < a.M && kch < a.K) {
+        float q0 = lo_bf(lo), q1 = hi_bf(lo), q2 = lo_bf(hi), q3 = hi_bf(hi);
+        bsum[0] += q0; bsq[0] += q0 * q0;
+        bsum[1] += q1; bsq[1] += q1 * q1;
+        bsum[2] += q2; bsq[2] += q2 * q2;
+        bsum[3] += q3; bsq[3] += q3 * q3;
       }
     }
     if (a.stats) {
@@ -257,6 +268,18 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
       }
     }
   }
+  if (staged) {
+    __syncthreads();
+    constexpr int CPR = CT / 8;  // 16-B chunks per pixel row of the tile
+#pragma unroll
+    for (int it = 0; it < PT * CPR / 256; ++it) {
+      const int idx = it * 256 + tid;
+      const int row = idx / CPR, chn = idx % CPR;
+      const int m = p0 + row, kc = c0 + chn * 8;
+      if (m < a.M && kc < a.K)
+        *(uint4*)(a.y + (size_t)m * a.K + kc) = *(const uint4*)(smem + row * OROW + chn * 16);
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -264,7 +287,7 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
 struct ConvWgradArgs {
   const bf16_t* x;   // [N][H][W][C] forward input
   const bf16_t* dy;  // [N][P][Q][K]
-  float* dw;         // [K][R][S][C] fp32 accumulated
+  float* dw;         // workspace slabs [splits][K][R*S*C] fp32 (summed into the gradient afterwards)
   const float* in_scale;  // optional prologue affine+relu on x (same as the forward's)
   const float* in_shift;
   uint32_t x_bytes, dy_bytes;
@@ -312,7 +335,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
   const int n0 = blockIdx.x * NT, m0 = blockIdx.y * MT;
   const int pix_lo = blockIdx.z * a.pix_per_split;
   const int pix_hi = min(a.Mpix, pix_lo + a.pix_per_split);
-  if (pix_lo >= pix_hi) return;
+  // (an empty split still runs: it stores a zero slab, which the reduction relies on)
 
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
   const __amdgpu_buffer_rsrc_t dr = make_rsrc(a.dy, a.dy_bytes);
@@ -446,7 +469,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
     if (kt + 1 < nk) swrite(cur ^ 1);
     __syncthreads();
   }
-  // epilogue: acc rows = ko (4 consecutive per lane), cols = flattened (r,s,c)
+  // epilogue: acc rows = ko (4 consecutive per lane), cols = flattened (r,s,c).  Each pixel split
+  // writes its partial tile to its own workspace slab (plain stores); dtm_reduce_rows then sums the
+  // slabs into dW.  (Split-K fp32 atomics onto the same tile serialise at the memory-side atomic
+  // units: up to hundreds of splits hit one 64-KB tile for the K x 64 1x1 layers.)
+  float* slab = a.dw + (size_t)blockIdx.z * a.K * a.Kg;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -456,7 +483,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
       if (col < a.Kg) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (ko + r < a.K) atomicAdd(a.dw + (size_t)(ko + r) * a.Kg + col, acc[i][j][r]);
+          if (ko + r < a.K) slab[(size_t)(ko + r) * a.Kg + col] = acc[i][j][r];
       }
     }
   }
@@ -587,8 +614,13 @@ DTM_API int dtm_conv_wgrad(const void* x, const void* dy, float* dw, const float
   long steps_per = (ksteps + splits - 1) / splits;
   a.pix_per_split = (int)(steps_per * 64);
   splits = (a.Mpix + a.pix_per_split - 1) / a.pix_per_split;
+  float* ws = dtm_ws_get((size_t)splits * a.K * a.Kg);
+  if (!ws) return -4;
+  a.dw = ws;
   if (small_m) launch_wgrad<64, 128, 32, 64>(a, (int)splits, (hipStream_t)stream);
   else launch_wgrad<128, 128, 64, 64>(a, (int)splits, (hipStream_t)stream);
+  // dW += sum over the split slabs (every slab element is written: tiles cover [K][Kg] exactly)
+  dtm_reduce_rows(ws, (int)splits, a.K * a.Kg, a.K * a.Kg, dw, (hipStream_t)stream);
   return 0;
 }
 
