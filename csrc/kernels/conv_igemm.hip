@@ -26,6 +26,15 @@
 
 namespace dtm {
 
+// XCD-aware block remap (8 XCDs, each with its own L2; the hardware deals workgroup L to XCD L % 8):
+// returns a logical tile id such that the workgroups of one XCD get a contiguous logical range, so
+// the tiles that share an operand (all channel tiles of one pixel tile, all tiles of one split)
+// hit the same L2.  Bijective for any count (guide T1).
+__device__ __forceinline__ int xcd_remap(int L, int nwg) {
+  const int xcd = L & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
+}
+
 struct ConvNTArgs {
   const bf16_t* x;        // [N][Hin][Win][C]
   const bf16_t* w;        // [K][R][S][C]
@@ -42,6 +51,11 @@ struct ConvNTArgs {
   int Kg;                    // R*S*C
   int relu;
   FastDiv fd_PQ, fd_Q;
+  // optional epilogue post-ops on the coalesced 16-B output chunks (used by dgrad):
+  const bf16_t* add_src;  // out += add_src (the other consumer's gradient of a shared input)
+  const bf16_t* act_x;    // fused activation backward of the input's BatchNorm+ReLU prologue:
+  const float* act_ss;    //   g = out * [act_x*scale + shift > 0]; out <- g*scale;
+  float* act_sums;        //   partial rows per pixel tile: [sum g*act_x (K) | sum g (K)]
 };
 
 template <int PT, int CT, int WP, int WC, int UD>
@@ -61,7 +75,9 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wp = wave % NWP, wc = wave / NWP;
-  const int p0 = blockIdx.y * PT, c0 = blockIdx.x * CT;
+  const int tile = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const int bx = tile % gridDim.x, by = tile / gridDim.x;
+  const int p0 = by * PT, c0 = bx * CT;
   const int ch = tid & 7, rb = tid >> 3;
   const bool lds_ss = a.in_scale && a.C <= MAXC;
   if (lds_ss) {
@@ -97,14 +113,18 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
   int tap = kc / a.C;
   int rr = tap / a.S, ss = tap - (tap / a.S) * a.S;
 
-  uint4 areg[ACH], wreg[WCH];
-  bool avalid[ACH];
-  int acc_c = 0;  // channel of the current act chunk (for the prologue affine)
+  // one register stage of the operand pipeline (a 2-deep register prefetch was measured: it spills
+  // at 128x128 and is 20-60 % slower at 128x64 from the lost occupancy)
+  struct Stage {
+    uint4 a[ACH], w[WCH];
+    bool v[ACH];
+    int c;  // channel of this stage's activation chunk (for the prologue affine)
+  };
 
-  auto gload = [&](int kt) {
+  auto gload = [&](int kt, Stage& st) {
     const int k = kt * BK + ch * 8;
     const bool kin = (k < a.Kg);
-    acc_c = cc;
+    st.c = cc;
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       int ihv = ih0[i] + rr, iwv = iw0[i] + ss;
@@ -112,15 +132,15 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
       if (UD > 1) v = v && ((ihv % UD) == 0) && ((iwv % UD) == 0);
       int ih = UD > 1 ? ihv / UD : ihv, iw = UD > 1 ? iwv / UD : iwv;
       uint32_t off = v ? (uint32_t)(((pixbase[i] + ih * a.Win + iw) * a.C + cc) * 2) : OOB_OFFSET;
-      avalid[i] = v;
-      areg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+      st.v[i] = v;
+      st.a[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
     }
 #pragma unroll
     for (int i = 0; i < WCH; ++i) {
       int row = c0 + rb + 32 * i;
       bool v = kin && row < a.K;
       uint32_t off = v ? (uint32_t)((row * a.Kg + k) * 2) : OOB_OFFSET;
-      wreg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0));
+      st.w[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0));
     }
     // advance (rr, ss, cc) by BK
     cc += BK;
@@ -130,42 +150,42 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
     }
   };
 
-  auto swrite = [&](int buf) {
+  auto swrite = [&](int buf, Stage& st) {
     char* base = smem + buf * BUF;
     if (a.in_scale) {
       // fused BatchNorm-apply + ReLU of the previous layer on the gathered input
       float sc[8], sh[8];
       if (lds_ss) {
-        const float4 s0 = *(const float4*)(s_scale + acc_c), s1 = *(const float4*)(s_scale + acc_c + 4);
-        const float4 h0 = *(const float4*)(s_shift + acc_c), h1 = *(const float4*)(s_shift + acc_c + 4);
+        const float4 s0 = *(const float4*)(s_scale + st.c), s1 = *(const float4*)(s_scale + st.c + 4);
+        const float4 h0 = *(const float4*)(s_shift + st.c), h1 = *(const float4*)(s_shift + st.c + 4);
         sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
         sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w; sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
       } else {
-        for (int e = 0; e < 8; ++e) { sc[e] = a.in_scale[acc_c + e]; sh[e] = a.in_shift[acc_c + e]; }
+        for (int e = 0; e < 8; ++e) { sc[e] = a.in_scale[st.c + e]; sh[e] = a.in_shift[st.c + e]; }
       }
 #pragma unroll
       for (int i = 0; i < ACH; ++i) {
-        if (avalid[i]) {
-          uint32_t u[4] = {areg[i].x, areg[i].y, areg[i].z, areg[i].w};
+        if (st.v[i]) {
+          uint32_t u[4] = {st.a[i].x, st.a[i].y, st.a[i].z, st.a[i].w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             float lo = fmaxf(fmaf(lo_bf(u[e]), sc[2 * e], sh[2 * e]), 0.f);
             float hi = fmaxf(fmaf(hi_bf(u[e]), sc[2 * e + 1], sh[2 * e + 1]), 0.f);
             u[e] = pack2bf(lo, hi);
           }
-          areg[i] = make_uint4(u[0], u[1], u[2], u[3]);
+          st.a[i] = make_uint4(u[0], u[1], u[2], u[3]);
         }
       }
     }
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       int row = rb + 32 * i;
-      *(uint4*)(base + row * 128 + ((ch ^ (row & 7)) << 4)) = areg[i];
+      *(uint4*)(base + row * 128 + ((ch ^ (row & 7)) << 4)) = st.a[i];
     }
 #pragma unroll
     for (int i = 0; i < WCH; ++i) {
       int row = rb + 32 * i;
-      *(uint4*)(base + PT * 128 + row * 128 + ((ch ^ (row & 7)) << 4)) = wreg[i];
+      *(uint4*)(base + PT * 128 + row * 128 + ((ch ^ (row & 7)) << 4)) = st.w[i];
     }
   };
 
@@ -175,14 +195,8 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
 #pragma unroll
     for (int j = 0; j < TP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (a.Kg + BK - 1) / BK;
-  gload(0);
-  swrite(0);
-  __syncthreads();
   const int fr = lane & 15, fk = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload(kt + 1);
+  auto compute = [&](int cur) {
     const char* base = smem + cur * BUF;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -205,7 +219,18 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
         for (int j = 0; j < TP; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) swrite(cur ^ 1);
+  };
+
+  const int nk = (a.Kg + BK - 1) / BK;
+  Stage st;
+  gload(0, st);
+  swrite(0, st);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1, st);
+    compute(cur);
+    if (kt + 1 < nk) swrite(cur ^ 1, st);
     __syncthreads();
   }
 
@@ -262,7 +287,7 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
       }
       // one partial row per (pixel tile, pixel wave): [sum(K) | sumsq(K)], reduced by reduce_rows
       if (fr == 0 && kch < a.K) {
-        float* row = a.stats + (size_t)(blockIdx.y * NWP + wp) * (2 * a.K);
+        float* row = a.stats + (size_t)(by * NWP + wp) * (2 * a.K);
         *(float4*)(row + kch) = make_float4(bsum[0], bsum[1], bsum[2], bsum[3]);
         *(float4*)(row + a.K + kch) = make_float4(bsq[0], bsq[1], bsq[2], bsq[3]);
       }
@@ -271,13 +296,72 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
   if (staged) {
     __syncthreads();
     constexpr int CPR = CT / 8;  // 16-B chunks per pixel row of the tile
+    constexpr int NIT = PT * CPR / 256;
+    const int chn = tid % CPR;   // fixed per thread (256 % CPR == 0)
+    const int kc = c0 + chn * 8;
+    const bool act = a.act_x != nullptr;
+    float sc[8], sh[8], sgx[8], sg[8];
 #pragma unroll
-    for (int it = 0; it < PT * CPR / 256; ++it) {
+    for (int e = 0; e < 8; ++e) { sc[e] = 1.f; sh[e] = 0.f; sgx[e] = 0.f; sg[e] = 0.f; }
+    if (act && kc < a.K) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { sc[e] = a.act_ss[kc + e]; sh[e] = a.act_ss[a.K + kc + e]; }
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
       const int idx = it * 256 + tid;
-      const int row = idx / CPR, chn = idx % CPR;
-      const int m = p0 + row, kc = c0 + chn * 8;
-      if (m < a.M && kc < a.K)
-        *(uint4*)(a.y + (size_t)m * a.K + kc) = *(const uint4*)(smem + row * OROW + chn * 16);
+      const int row = idx / CPR;
+      const int m = p0 + row;
+      if (m < a.M && kc < a.K) {
+        uint4 v = *(const uint4*)(smem + row * OROW + chn * 16);
+        const size_t o = (size_t)m * a.K + kc;
+        if (a.add_src || act) {
+          float f[8];
+          f[0] = lo_bf(v.x); f[1] = hi_bf(v.x); f[2] = lo_bf(v.y); f[3] = hi_bf(v.y);
+          f[4] = lo_bf(v.z); f[5] = hi_bf(v.z); f[6] = lo_bf(v.w); f[7] = hi_bf(v.w);
+          if (a.add_src) {
+            const uint4 r = *(const uint4*)(a.add_src + o);
+            f[0] += lo_bf(r.x); f[1] += hi_bf(r.x); f[2] += lo_bf(r.y); f[3] += hi_bf(r.y);
+            f[4] += lo_bf(r.z); f[5] += hi_bf(r.z); f[6] += lo_bf(r.w); f[7] += hi_bf(r.w);
+          }
+          if (act) {
+            const uint4 xu = *(const uint4*)(a.act_x + o);
+            float xv[8];
+            xv[0] = lo_bf(xu.x); xv[1] = hi_bf(xu.x); xv[2] = lo_bf(xu.y); xv[3] = hi_bf(xu.y);
+            xv[4] = lo_bf(xu.z); xv[5] = hi_bf(xu.z); xv[6] = lo_bf(xu.w); xv[7] = hi_bf(xu.w);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float g = fmaf(xv[e], sc[e], sh[e]) > 0.f ? f[e] : 0.f;
+              sgx[e] += g * xv[e];
+              sg[e] += g;
+              f[e] = g * sc[e];
+            }
+          }
+          v = make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
+        }
+        *(uint4*)(a.y + o) = v;
+      }
+    }
+    if (act) {
+      // reduce the per-thread partial sums over the threads sharing this chunk column, one partial
+      // row per pixel tile (reduced over tiles by dtm_reduce_rows)
+      __syncthreads();
+      float* red = (float*)smem;  // [256][16]
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { red[tid * 16 + e] = sgx[e]; red[tid * 16 + 8 + e] = sg[e]; }
+      __syncthreads();
+      if (tid < CPR && kc < a.K) {
+        float tx[8], tg[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { tx[e] = 0.f; tg[e] = 0.f; }
+        for (int t = tid; t < 256; t += CPR) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { tx[e] += red[t * 16 + e]; tg[e] += red[t * 16 + 8 + e]; }
+        }
+        float* prow = a.act_sums + (size_t)by * (2 * a.K);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { prow[kc + e] = tx[e]; prow[a.K + kc + e] = tg[e]; }
+      }
     }
   }
 }
@@ -322,9 +406,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
   float* s_shift = s_scale + NT;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int gxy = gridDim.x * gridDim.y;
+  const int tile = xcd_remap((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x, gxy * gridDim.z);
+  const int bz = tile / gxy, by = (tile % gxy) / gridDim.x, bx = tile % gridDim.x;
   if (a.in_scale) {
     for (int j = tid; j < NT; j += 256) {
-      int col = blockIdx.x * NT + j;
+      int col = bx * NT + j;
       int c = col < a.Kg ? col % a.C : 0;
       s_scale[j] = a.in_scale[c];
       s_shift[j] = a.in_shift[c];
@@ -332,8 +419,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
     __syncthreads();
   }
   const int wm = wave % NWM, wn = wave / NWM;
-  const int n0 = blockIdx.x * NT, m0 = blockIdx.y * MT;
-  const int pix_lo = blockIdx.z * a.pix_per_split;
+  const int n0 = bx * NT, m0 = by * MT;
+  const int pix_lo = bz * a.pix_per_split;
   const int pix_hi = min(a.Mpix, pix_lo + a.pix_per_split);
   // (an empty split still runs: it stores a zero slab, which the reduction relies on)
 
@@ -473,7 +560,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
   // writes its partial tile to its own workspace slab (plain stores); dtm_reduce_rows then sums the
   // slabs into dW.  (Split-K fp32 atomics onto the same tile serialise at the memory-side atomic
   // units: up to hundreds of splits hit one 64-KB tile for the K x 64 1x1 layers.)
-  float* slab = a.dw + (size_t)blockIdx.z * a.K * a.Kg;
+  float* slab = a.dw + (size_t)bz * a.K * a.Kg;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -543,6 +630,7 @@ DTM_API int dtm_conv_fwd(const void* x, const void* w, void* y, float* stats, co
   ConvNTArgs a;
   a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.y = (bf16_t*)y;
   a.stats = stats; a.bias = bias; a.in_scale = in_scale; a.in_shift = in_shift;
+  a.add_src = nullptr; a.act_x = nullptr; a.act_ss = nullptr; a.act_sums = nullptr;
   size_t xb = (size_t)d->N * d->H * d->W * d->C * 2, wb = (size_t)d->K * d->R * d->S * d->C * 2;
   if (xb >= (1ull << 31) || wb >= (1ull << 31)) return -2;
   a.x_bytes = (uint32_t)xb; a.w_bytes = (uint32_t)wb;
@@ -564,13 +652,21 @@ DTM_API int dtm_conv_fwd(const void* x, const void* w, void* y, float* stats, co
   return 0;
 }
 
-// dgrad: dx[N][H][W][C] from dy[N][P][Q][K] and the flipped/transposed weight wt[C][R][S][K]
-DTM_API int dtm_conv_dgrad(const void* dy, const void* wt, void* dx, const ConvDesc* d, void* stream) {
+// dgrad: dx[N][H][W][C] from dy[N][P][Q][K] and the flipped/transposed weight wt[C][R][S][K].
+// Optional epilogue post-ops (nullptr = off):
+//   add_src [N][H][W][C]: dx += add_src (gradient of the same input from its other consumer);
+//   act_x [N][H][W][C] + act_ss [4][C] (scale, shift, ...): the input was relu(act_x*scale+shift)
+//   (BatchNorm+ReLU fused into this conv's forward prologue); dx <- [act_x*scale+shift>0]*dx*scale and
+//   act_sums[2][C] += (sum g*act_x, sum g) with g the masked gradient (the BN scale/shift grads).
+DTM_API int dtm_conv_dgrad_ex(const void* dy, const void* wt, void* dx, const ConvDesc* d, const void* add_src,
+                              const void* act_x, const float* act_ss, float* act_sums, void* stream) {
   if (d->K % 8 || d->C % 4) return -1;
   if (d->stride > 2) return -3;
+  if ((add_src || act_x) && d->C % 8) return -5;
   ConvNTArgs a;
   a.x = (const bf16_t*)dy; a.w = (const bf16_t*)wt; a.y = (bf16_t*)dx;
   a.stats = nullptr; a.bias = nullptr; a.in_scale = nullptr; a.in_shift = nullptr;
+  a.add_src = (const bf16_t*)add_src; a.act_x = (const bf16_t*)act_x; a.act_ss = act_ss; a.act_sums = nullptr;
   size_t xb = (size_t)d->N * d->P * d->Q * d->K * 2, wb = (size_t)d->K * d->R * d->S * d->C * 2;
   if (xb >= (1ull << 31) || wb >= (1ull << 31)) return -2;
   a.x_bytes = (uint32_t)xb; a.w_bytes = (uint32_t)wb;
@@ -580,8 +676,19 @@ DTM_API int dtm_conv_dgrad(const void* dy, const void* wt, void* dx, const ConvD
   a.Hv = (d->P - 1) * d->stride + 1; a.Wv = (d->Q - 1) * d->stride + 1;
   a.M = d->N * d->H * d->W; a.Kg = d->R * d->S * d->K; a.relu = 0;
   a.fd_PQ = make_fastdiv(d->H * d->W); a.fd_Q = make_fastdiv(d->W);
+  const int rows = (a.M + 127) / 128;  // pixel tiles (PT = 128 for every dispatch_nt variant)
+  if (act_x) {
+    float* ws = dtm_ws_get((size_t)rows * 2 * d->C);
+    if (!ws) return -4;
+    a.act_sums = ws;
+  }
   dispatch_nt(a, d->stride, (hipStream_t)stream);
+  if (act_x) dtm_reduce_rows(a.act_sums, rows, 2 * d->C, 2 * d->C, act_sums, (hipStream_t)stream);
   return 0;
+}
+
+DTM_API int dtm_conv_dgrad(const void* dy, const void* wt, void* dx, const ConvDesc* d, void* stream) {
+  return dtm_conv_dgrad_ex(dy, wt, dx, d, nullptr, nullptr, nullptr, nullptr, stream);
 }
 
 template <int MT, int NT, int WM, int WN>

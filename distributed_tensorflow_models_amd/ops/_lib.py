@@ -34,6 +34,7 @@ _F = ctypes.c_float
 _SIGS = {
     "dtm_conv_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, ctypes.POINTER(ConvDesc), _P]),
     "dtm_conv_dgrad": (_I, [_P, _P, _P, ctypes.POINTER(ConvDesc), _P]),
+    "dtm_conv_dgrad_ex": (_I, [_P, _P, _P, ctypes.POINTER(ConvDesc), _P, _P, _P, _P, _P]),
     "dtm_conv_wgrad": (_I, [_P, _P, _P, _P, _P, ctypes.POINTER(ConvDesc), _I, _P]),
     "dtm_weight_flip_transpose": (None, [_P, _P, _I, _I, _I, _I, _P]),
     "dtm_bn_stats": (None, [_P, _P, _L, _I, _P]),

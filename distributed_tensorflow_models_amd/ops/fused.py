@@ -61,12 +61,54 @@ class ZeroArena:
 arena = ZeroArena()
 
 
+class _GradSlot:
+    """Gradient hand-off for a tensor read by several fused ops (a ResNet block input feeds conv1
+    and the shortcut).  Every consumer's backward but the last stashes its input-gradient here and
+    returns None; the last one folds the stash into its own dgrad epilogue (``add_src``), so the
+    autograd engine never launches a separate add over the whole activation."""
+    __slots__ = ("pending", "buf")
+
+    def __init__(self):
+        self.pending = 0
+        self.buf = None
+
+
+def _slot_register(x):
+    if not (torch.is_grad_enabled() and x.requires_grad and x.is_cuda):
+        return None
+    s = getattr(x, "_dtm_slot", None)
+    if s is None:
+        s = _GradSlot()
+        try:
+            x._dtm_slot = s
+        except Exception:
+            return None
+    s.pending += 1
+    return s
+
+
+def _slot_take(slot):
+    """-> (is_last_consumer, stashed_gradient_or_None)"""
+    if slot is None:
+        return True, None
+    slot.pending -= 1
+    buf = slot.buf
+    if slot.pending == 0:
+        slot.buf = None
+        return True, buf
+    return False, buf
+
+
+def _slot_stash(slot, g):
+    slot.buf = g if slot.buf is None else slot.buf + g
+
+
 # ---------------------------------------------------------------------------------------------
 class _ConvBNFn(torch.autograd.Function):
     """y_raw, stats = conv(relu(x_raw*in_scale+in_shift) or x_raw, w); stats = (Σy, Σy²) per channel."""
 
     @staticmethod
-    def forward(ctx, x, in_ss, w, geom, want_stats):
+    def forward(ctx, x, in_ss, w, geom, want_stats, slot=None):
         L = _lib.lib()
         s = _lib.stream_ptr()
         w16 = weight_bf16(w)
@@ -78,6 +120,7 @@ class _ConvBNFn(torch.autograd.Function):
         _check(L.dtm_conv_fwd(_lib.ptr(x), _lib.ptr(w16), _lib.ptr(y), _lib.ptr(stats), None, _lib.ptr(sc),
                               _lib.ptr(sh), 0, ctypes.byref(d), s), "conv_fwd")
         ctx.geom = geom
+        ctx.slot = slot
         ctx.save_for_backward(x, in_ss, w, y)
         if stats is None:
             return y
@@ -101,21 +144,23 @@ class _ConvBNFn(torch.autograd.Function):
         sh = in_ss[1] if in_ss is not None else None
         dx = d_in = None
         if ctx.needs_input_grad[0] or (in_ss is not None and ctx.needs_input_grad[1]):
+            last, add_src = _slot_take(ctx.slot)
             w16 = weight_bf16(w)
             wt = torch.empty((g.C, g.R, g.S, g.K), device=dy.device, dtype=torch.bfloat16)
             L.dtm_weight_flip_transpose(_lib.ptr(w16), _lib.ptr(wt), g.K, g.R, g.S, g.C, s)
-            da = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
-            _check(L.dtm_conv_dgrad(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(da), ctypes.byref(d), s), "conv_dgrad")
+            dx = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
             if in_ss is not None:
-                dx = torch.empty_like(da)
-                sums = arena.zeros((4, g.C), dy.device)
-                M_in = g.N * g.H * g.W
-                _check(L.dtm_bn_apply_bwd(_lib.ptr(da), None, _lib.ptr(x), _lib.ptr(in_ss), None, None,
-                                          _lib.ptr(dx), None, _lib.ptr(sums), None, M_in, g.C, 2, 0, s),
-                       "act_bwd")
-                d_in = sums
+                # BN+ReLU of the input was fused into the forward prologue: mask, scale and the BN
+                # parameter-gradient sums are done in the dgrad epilogue
+                d_in = arena.zeros((4, g.C), dy.device)
+                _check(L.dtm_conv_dgrad_ex(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), None,
+                                           _lib.ptr(x), _lib.ptr(in_ss), _lib.ptr(d_in), s), "conv_dgrad_act")
             else:
-                dx = da
+                _check(L.dtm_conv_dgrad_ex(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d),
+                                           _lib.ptr(add_src) if last else None, None, None, None, s), "conv_dgrad")
+                if not last:
+                    _slot_stash(ctx.slot, dx)
+                    dx = None
         if ctx.needs_input_grad[2]:
             mg = getattr(w, "main_grad", None)
             target = mg if mg is not None else torch.zeros(w.shape, device=dy.device, dtype=torch.float32)
@@ -128,7 +173,7 @@ class _ConvBNFn(torch.autograd.Function):
                 dw = target
         else:
             dw = None
-        return dx, d_in, dw, None, None
+        return dx, d_in, dw, None, None, None
 
 
 class _BNFinalizeFn(torch.autograd.Function):
@@ -166,7 +211,7 @@ class _BNFinalizeFn(torch.autograd.Function):
 
 class _BNApplyFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, ss, res, res_ss, relu):
+    def forward(ctx, x, ss, res, res_ss, relu, res_slot=None):
         L = _lib.lib()
         C = x.shape[-1]
         M = x.numel() // C
@@ -174,7 +219,7 @@ class _BNApplyFn(torch.autograd.Function):
         res_mode = 0 if res is None else (2 if res_ss is not None else 1)
         L.dtm_bn_apply(_lib.ptr(x), _lib.ptr(ss), _lib.ptr(res), _lib.ptr(res_ss), _lib.ptr(y), M, C, res_mode,
                        int(relu), _lib.stream_ptr())
-        ctx.relu, ctx.res_mode = relu, res_mode
+        ctx.relu, ctx.res_mode, ctx.res_slot = relu, res_mode, res_slot
         ctx.save_for_backward(x, ss, res, res_ss, y if relu else None)
         return y
 
@@ -191,7 +236,14 @@ class _BNApplyFn(torch.autograd.Function):
         _check(L.dtm_bn_apply_bwd(_lib.ptr(dy.contiguous()), _lib.ptr(y), _lib.ptr(x), _lib.ptr(ss), _lib.ptr(res),
                                   _lib.ptr(rss), _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(sx), _lib.ptr(sr), M, C,
                                   1 if ctx.relu else 0, ctx.res_mode, _lib.stream_ptr()), "bn_apply_bwd")
-        return dx, sx, dres, sr, None
+        if ctx.res_slot is not None:
+            last, buf = _slot_take(ctx.res_slot)
+            if not last:
+                _slot_stash(ctx.res_slot, dres)
+                dres = None
+            elif buf is not None:
+                dres = dres + buf
+        return dx, sx, dres, sr, None, None
 
 
 def bn_apply(raw, ss, relu, residual=None):
@@ -203,7 +255,9 @@ def bn_apply(raw, ss, relu, residual=None):
             residual = residual.materialize()
         else:
             return _BNApplyFn.apply(raw, ss, residual.raw, residual.ss, bool(relu))
-    return _BNApplyFn.apply(raw, ss, residual.to(torch.bfloat16).contiguous(), None, bool(relu))
+    res = residual.to(torch.bfloat16).contiguous()
+    slot = _slot_register(res) if res is residual else None
+    return _BNApplyFn.apply(raw, ss, res, None, bool(relu), slot)
 
 
 def bn_inference_ss(bn):
@@ -231,12 +285,15 @@ def conv_bn(x, w, bn, stride, padding, training, relu):
         x = torch.nn.functional.pad(x, (0, cp - g.C))
         w = _PadChannels.apply(w, cp)
         g = conv_geom(tuple(x.shape), tuple(w.shape), stride, padding)
-    x = x.to(torch.bfloat16).contiguous()
+    xb = x.to(torch.bfloat16).contiguous()
+    # a shared (materialised) input: hand the gradient between its consumers (see _GradSlot)
+    slot = _slot_register(xb) if (xb is x and in_ss is None) else None
+    x = xb
     if training:
-        y, stats = _ConvBNFn.apply(x, in_ss, w, g, True)
+        y, stats = _ConvBNFn.apply(x, in_ss, w, g, True, slot)
         ss = _BNFinalizeFn.apply(stats, bn.gamma, bn.beta, bn.moving_mean, bn.moving_variance,
                                  float(g.N * g.P * g.Q), bn.eps, bn.decay, bn.bessel, True)
     else:
-        y = _ConvBNFn.apply(x, in_ss, w, g, False)
+        y = _ConvBNFn.apply(x, in_ss, w, g, False, slot)
         ss = bn_inference_ss(bn)
     return LazyBN(y, ss, relu)

@@ -25,7 +25,7 @@ SHAPES = [  # H, C, K, R, stride, pad, count in resnet50
 ]
 
 
-def timeit(fn, n=10):
+def timeit(fn, n=20):
     for _ in range(2):
         fn()
     torch.cuda.synchronize()
@@ -61,14 +61,17 @@ def main():
         td = timeit(lambda: L.dtm_conv_dgrad(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), s))
         tw = timeit(lambda: L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(dw), None, None, ctypes.byref(d),
                                              _lib.num_cus(), s))
-        xc = x.permute(0, 3, 1, 2)
-        wc = w.permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
-        xg = xc.detach().requires_grad_()
-        wg = wc.detach().requires_grad_()
-        mf = timeit(lambda: torch.nn.functional.conv2d(xc, wc, None, st, pad))
-        yy = torch.nn.functional.conv2d(xg, wg, None, st, pad)
-        gy = torch.randn_like(yy)
-        mb = timeit(lambda: torch.autograd.grad(torch.nn.functional.conv2d(xg, wg, None, st, pad), (xg, wg), gy)) - mf
+        mf = mb = 0.0
+        if not os.environ.get("NOMIO"):
+            xc = x.permute(0, 3, 1, 2)
+            wc = w.permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
+            xg = xc.detach().requires_grad_()
+            wg = wc.detach().requires_grad_()
+            mf = timeit(lambda: torch.nn.functional.conv2d(xc, wc, None, st, pad))
+            yy = torch.nn.functional.conv2d(xg, wg, None, st, pad)
+            gy = torch.randn_like(yy)
+            mb = timeit(lambda: torch.autograd.grad(torch.nn.functional.conv2d(xg, wg, None, st, pad), (xg, wg),
+                                                    gy)) - mf
         for k, v in (("fwd", tf), ("dgrad", td), ("wgrad", tw), ("miopen_fwd", mf), ("miopen_bwd", mb)):
             tot[k] += v * cnt
         name = "H%d C%d K%d R%d s%d x%d" % (H, C, K, R, st, cnt)
