@@ -25,6 +25,19 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 BASELINE_VALUE = None  # the reference publishes no ResNet-50 images/sec
+HEADLINE_METRIC = "images/sec (whole node) ResNet-50 224\u00d7224 bf16 at 1/2/4/8 MI355X"  # BASELINE.json
+
+# BASELINE.json configs: model name -> (image size, classes, per-GPU batch, optimizer, extra TrainStep kwargs)
+PRESETS = {
+    "resnet_v1_50": (224, 1000, 256, "momentum", {}),
+    # config #4: old-slim Inception-v3 as the reference trains it (RMSProp, label smoothing, aux head)
+    "inception_v3_slim_old": (299, 1001, 128, "rmsprop", dict(label_smoothing=0.1, aux_weight=0.4, rho=0.9,
+                                                              epsilon=1.0)),
+    # config #5: VGG-16 with the reference's CIFAR geometry (10 classes, 134.3 M params)
+    "vgg_16": (32, 10, 512, "sgd", {}),
+    # config #1 plumbing model
+    "lenet": (28, 10, 512, "sgd", {}),
+}
 
 
 def main():
@@ -32,9 +45,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
-    ap.add_argument("--model", default="resnet_v1_50")
-    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: the preset's)")
+    ap.add_argument("--model", default="resnet_v1_50", choices=sorted(PRESETS))
+    ap.add_argument("--image-size", type=int, default=0)
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--graph", type=int, default=0, help="capture the step in a hipGraph")
     ap.add_argument("--profile-steps", type=int, default=0)
@@ -52,13 +65,16 @@ def main():
     from distributed_tensorflow_models_amd.models import nets_factory
 
     torch.manual_seed(1234 + rank)
-    net = nets_factory.build(args.model, num_classes=1000).to(dev)
-    B = args.batch
-    step = TrainStep(net, optimizer="momentum", lr=0.1 * world, momentum=0.9, bucket_mb=args.bucket_mb,
-                     label_smoothing=0.0, use_graph=bool(args.graph))
-    S = args.image_size
-    images = torch.randn(B, S, S, 3, device=dev).to(torch.bfloat16)
-    labels = torch.randint(0, 1000, (B,), device=dev)
+    S0, ncls, B0, opt, extra = PRESETS[args.model]
+    S = args.image_size or S0
+    B = args.batch or B0
+    kw = {"fc_conv_padding": "SAME"} if args.model == "vgg_16" else {}
+    net = nets_factory.build(args.model, num_classes=ncls, **kw).to(dev)
+    step = TrainStep(net, optimizer=opt, lr=0.1 * world if opt == "momentum" else 0.01 * world, momentum=0.9,
+                     bucket_mb=args.bucket_mb, use_graph=bool(args.graph), **extra)
+    cin = 1 if args.model == "lenet" else 3
+    images = torch.randn(B, S, S, cin, device=dev).to(torch.bfloat16)
+    labels = torch.randint(0, ncls, (B,), device=dev)
 
     for _ in range(args.warmup):
         step(images, labels)
@@ -80,7 +96,8 @@ def main():
     value = world * B * args.steps / dt
     if rank == 0:
         out = {
-            "metric": "images/sec (whole node) ResNet-50 224x224 bf16 training",
+            "metric": HEADLINE_METRIC if args.model == "resnet_v1_50" else
+            "images/sec (whole node) %s %dx%d bf16 training" % (args.model, S, S),
             "value": round(value, 2),
             "unit": "images/sec",
             "n_gpus": world,
@@ -91,9 +108,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
             "dtype": "bf16",
-            "data": "synthetic (random 224x224x3 bf16 images, random labels, random-init weights)",
+            "data": "synthetic (random %dx%dx%d bf16 images, random labels, random-init weights)" % (S, S, cin),
             "config": {"model": args.model, "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
-                       "image_size": S, "parallelism": "dp%d" % world, "optimizer": "momentum-sgd+wd1e-4",
+                       "image_size": S, "parallelism": "dp%d" % world,
+                       "optimizer": {"momentum": "momentum-sgd+wd", "rmsprop": "rmsprop(TF)+wd", "sgd": "sgd+wd"}[opt],
                        "final_loss": round(float(loss), 4)},
         }
         print(json.dumps(out), flush=True)

@@ -612,15 +612,33 @@ static void launch_nt(const ConvNTArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((conv_nt_kernel<PT, CT, WP, WC, UD>), grid, dim3(256), 0, st, a);
 }
 
-static void dispatch_nt(const ConvNTArgs& a, int ud, hipStream_t st) {
-  // tile selection: channel tile 64 for narrow layers, pixel tile 128
-  if (ud == 1) {
-    if (a.K <= 64) launch_nt<128, 64, 32, 64, 1>(a, st);
-    else launch_nt<128, 128, 64, 64, 1>(a, st);
-  } else {
-    if (a.K <= 64) launch_nt<128, 64, 32, 64, 2>(a, st);
-    else launch_nt<128, 128, 64, 64, 2>(a, st);
+// tile variants: 0 = 128 pix x 128 ch (4 waves 2x2 of 64x64), 1 = 128 x 64 (4x1 of 32x64),
+// 2 = 64 x 128 (2x2 of 32x64; 3 blocks/CU by LDS).  DTM_CONV_TILE forces one (A/B experiments).
+struct TileCfg {
+  int id, PT, NWP;
+};
+static int g_tile_env = -2;
+static TileCfg pick_tile(const ConvNTArgs& a) {
+  if (g_tile_env == -2) {
+    const char* e = getenv("DTM_CONV_TILE");
+    g_tile_env = e ? atoi(e) : -1;
   }
+  int id = g_tile_env >= 0 ? g_tile_env : (a.K <= 64 ? 1 : 0);
+  if (id == 1) return {1, 128, 4};
+  if (id == 2) return {2, 64, 2};
+  return {0, 128, 2};
+}
+
+template <int UD>
+static void dispatch_ud(const ConvNTArgs& a, const TileCfg& t, hipStream_t st) {
+  if (t.id == 1) launch_nt<128, 64, 32, 64, UD>(a, st);
+  else if (t.id == 2) launch_nt<64, 128, 32, 64, UD>(a, st);
+  else launch_nt<128, 128, 64, 64, UD>(a, st);
+}
+
+static void dispatch_nt(const ConvNTArgs& a, int ud, const TileCfg& t, hipStream_t st) {
+  if (ud == 1) dispatch_ud<1>(a, t, st);
+  else dispatch_ud<2>(a, t, st);
 }
 
 DTM_API int dtm_conv_fwd(const void* x, const void* w, void* y, float* stats, const float* bias,
@@ -640,14 +658,14 @@ DTM_API int dtm_conv_fwd(const void* x, const void* w, void* y, float* stats, co
   a.M = d->N * d->P * d->Q; a.Kg = d->R * d->S * d->C; a.relu = relu;
   a.fd_PQ = make_fastdiv(d->P * d->Q); a.fd_Q = make_fastdiv(d->Q);
   int rows = 0;
+  const TileCfg tc = pick_tile(a);
   if (stats) {
-    const int nwp = d->K <= 64 ? 4 : 2;  // pixel waves of the tile chosen by dispatch_nt
-    rows = ((a.M + 127) / 128) * nwp;
+    rows = ((a.M + tc.PT - 1) / tc.PT) * tc.NWP;  // one partial row per (pixel tile, pixel wave)
     float* ws = dtm_ws_get((size_t)rows * 2 * d->K);
     if (!ws) return -4;
     a.stats = ws;
   }
-  dispatch_nt(a, 1, (hipStream_t)stream);
+  dispatch_nt(a, 1, tc, (hipStream_t)stream);
   if (stats) dtm_reduce_rows(a.stats, rows, 2 * d->K, 2 * d->K, stats, (hipStream_t)stream);
   return 0;
 }
@@ -676,13 +694,14 @@ DTM_API int dtm_conv_dgrad_ex(const void* dy, const void* wt, void* dx, const Co
   a.Hv = (d->P - 1) * d->stride + 1; a.Wv = (d->Q - 1) * d->stride + 1;
   a.M = d->N * d->H * d->W; a.Kg = d->R * d->S * d->K; a.relu = 0;
   a.fd_PQ = make_fastdiv(d->H * d->W); a.fd_Q = make_fastdiv(d->W);
-  const int rows = (a.M + 127) / 128;  // pixel tiles (PT = 128 for every dispatch_nt variant)
+  const TileCfg tc = pick_tile(a);
+  const int rows = (a.M + tc.PT - 1) / tc.PT;  // pixel tiles
   if (act_x) {
     float* ws = dtm_ws_get((size_t)rows * 2 * d->C);
     if (!ws) return -4;
     a.act_sums = ws;
   }
-  dispatch_nt(a, d->stride, (hipStream_t)stream);
+  dispatch_nt(a, d->stride, tc, (hipStream_t)stream);
   if (act_x) dtm_reduce_rows(a.act_sums, rows, 2 * d->C, 2 * d->C, act_sums, (hipStream_t)stream);
   return 0;
 }
