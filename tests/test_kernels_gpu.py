@@ -119,3 +119,15 @@ def test_global_avg_and_xent():
     lr_.backward()
     lk.backward()
     assert _rel(xk.grad, xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("distort,size", [(True, 24), (False, 24), (True, 32)])
+def test_image_augment_kernel_matches_oracle(distort, size):
+    """HIP crop/flip/brightness/contrast/standardise kernel vs the torch oracle, same random params."""
+    import numpy as np
+    from distributed_tensorflow_models_amd.data import cifar10
+    imgs = torch.randint(0, 256, (16, 32, 32, 3), dtype=torch.uint8)
+    ref_out = cifar10.augment(imgs, size, distort, np.random.RandomState(3), torch.float32)
+    got = cifar10.augment(imgs.to(DEV), size, distort, np.random.RandomState(3), torch.float32)
+    torch.cuda.synchronize()
+    assert got.is_cuda and _rel(got.cpu(), ref_out) < 1e-4
