@@ -31,6 +31,7 @@ EVAL_DEFAULTS = {
     "cifarnet": ("/home/ubuntu/cifar10/eval", "/home/ubuntu/cifar10/train", 60, 1000, False, False),
     "inception": ("/home/ubuntu/imagenet/eval", "/home/ubuntu/imagenet/train/", 300, 200, True, True),
     "resnet50": ("/tmp/resnet50_eval", "/tmp/resnet50_train", 300, 1000, False, True),
+    "mobilenet_v1": ("/tmp/mobilenet_v1_eval", "/tmp/mobilenet_v1_train", 300, 50000, False, True),
     "lenet": ("/tmp/lenet_eval", "/tmp/lenet_train", 60, 1000, False, False),
 }
 
@@ -109,6 +110,8 @@ def evaluate(preset, flags):
     top5 = EVAL_DEFAULTS[preset][5]
     device = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
     kw = {"resnet_size": F.resnet_size} if cfg["model"] == "cifar10_resnet_v2" else {}
+    if cfg["model"].startswith("mobilenet") and "depth_multiplier" in F and F.depth_multiplier != 1.0:
+        kw["depth_multiplier"] = F.depth_multiplier
     model = trainer.build_model_for_eval(preset, **kw).to(device)
     model.eval()
     if os.path.isdir(F.eval_dir):

@@ -34,10 +34,11 @@ TRAINERS = {
     ("inception", "ssp"): "imagenet_inception_ssp",
     ("resnet50", "bsp"): "imagenet_resnet50_bsp",
     ("lenet", "bsp"): "mnist_lenet_bsp",
+    ("mobilenet", "bsp"): "mobilenet_v1_train",
 }
 EVALS = {"cnn": "cifar10_cnn_eval", "alexnet": "cifar10_alexnet_eval", "vgg": "cifar10_vgg_eval",
          "resnet": "cifar10_resnet_eval", "cifarnet": "cifar10_cifarnet_eval",
-         "inception": "imagenet_inception_eval"}
+         "inception": "imagenet_inception_eval", "mobilenet": "mobilenet_v1_eval"}
 
 
 def resolve(model, mode):

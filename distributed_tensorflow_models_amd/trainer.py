@@ -73,6 +73,12 @@ PRESETS = {
                       max_steps=10000000, save_secs=600, log_style="short", max_to_keep=5, nan_guard=True,
                       train_dir="/home/ubuntu/imagenet/train/", data_dir="/home/ubuntu/imagenet/data/",
                       wipe=False),
+    # vgg/nets/mobilenet_v1_train.py:57-160 (SGD 0.045, x0.94 every 2.5 epochs, batch 64)
+    "mobilenet_v1": dict(model="mobilenet_v1", num_classes=1001, dataset="imagenet", image_size=224, batch_size=64,
+                         lr=0.045, lr_scale_workers=False, decay_epochs=2.5, decay_factor=0.94, optimizer="sgd",
+                         ema=None, wd_all=None, max_steps=10000000, save_secs=100,
+                         log_style="short", max_to_keep=5, train_dir="/tmp/mobilenet_v1_train",
+                         data_dir="/tmp/imagenet"),
     # headline benchmark model (north star) - slim resnet_v1_50 on synthetic ImageNet
     "resnet50": dict(model="resnet_v1_50", num_classes=1000, dataset="synthetic_imagenet", image_size=224,
                      batch_size=256, lr=0.1, lr_scale_workers=True, decay_epochs=30.0, decay_factor=0.1,
@@ -121,6 +127,8 @@ def define_common_flags(flags, preset):
             ("batch_weight", Fl, 1.0, "per-rank gradient weight b_r/b_nominal (C15)"),
             ("fault_inject", S, "", "rank:step -> hard-exit that rank at that step (resume tests)"),
             ("seed", I, 0, "random seed"),
+            ("depth_multiplier", Fl, 1.0, "MobileNet depth multiplier"),
+            ("fine_tune_checkpoint", S, "", "initialise model variables from this checkpoint (fresh runs only)"),
     ):
         fn(name, default, h)
         flags.FLAGS.reset(name)  # the entry script's preset defaults win
@@ -198,6 +206,8 @@ def train(preset, flags, default_mode="bsp"):
     mkw = dict(cfg.get("model_kw", {}))
     if cfg["model"] == "cifar10_resnet_v2":
         mkw["resnet_size"] = FLAGS.resnet_size
+    if cfg["model"].startswith("mobilenet") and FLAGS.depth_multiplier != 1.0:
+        mkw["depth_multiplier"] = FLAGS.depth_multiplier
     model = nets_factory.build(cfg["model"], num_classes=cfg["num_classes"], **mkw).to(device)
     if cfg.get("wd_all") is not None:  # loss += wd * sum(l2_loss(v) for v in trainable_variables())
         for p in model.parameters():
@@ -262,6 +272,13 @@ def train(preset, flags, default_mode="bsp"):
         raise ValueError("sync_mode must be bsp, asp or ssp")
     if path:
         logging.info("rank %d restored %s (global_step %d)", rank, path, int(gstep))
+    elif FLAGS.fine_tune_checkpoint:
+        # model variables only (no slots, no global step: the schedule restarts), missing ones keep
+        # their initialisation (e.g. a new logits layer)
+        ft = [v for v in model_variables(model, None, None)]
+        missing = Saver(ft).restore(FLAGS.fine_tune_checkpoint, strict=False)
+        logging.info("fine-tuning from %s (%d variables not in the checkpoint)", FLAGS.fine_tune_checkpoint,
+                     len(missing or []))
     saver = Saver(vars_, max_to_keep=cfg["max_to_keep"])
     if is_chief and os.path.isdir(FLAGS.train_dir):
         saver.recover_last_checkpoints(FLAGS.train_dir)

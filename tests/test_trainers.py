@@ -26,6 +26,7 @@ def _run(mod, *args, timeout=600):
     ("cifar10_cnn_bsp", 8, "cnn"), ("cifar10_alexnet_bsp", 4, "standard"), ("cifar10_vgg_bsp", 2, "standard"),
     ("cifar10_vgg_asp", 2, "standard"), ("cifar10_resnet_bsp", 4, "short"), ("cifar10_cifarnet_bsp", 8, "standard"),
     ("mnist_lenet_bsp", 8, "standard"), ("imagenet_inception_bsp", 1, "short"), ("imagenet_inception_ssp", 1, "short"),
+    ("mobilenet_v1_train", 2, "short"),
 ])
 def test_trainer_runs_and_checkpoints(tmp_path, mod, batch, style):
     d = str(tmp_path / "train")
