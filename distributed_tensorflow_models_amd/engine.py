@@ -6,6 +6,7 @@ runs, one multi-tensor optimizer launch, TF 1.x optimizer / loss semantics.
 """
 import torch
 
+from .ops import _lib
 from .ops import fused as _fused
 from .ops import nn as F
 from .ops.optim import FusedOptimizer
@@ -22,7 +23,7 @@ def prepare_compute_copies(model):
 class TrainStep:
     def __init__(self, model, optimizer="momentum", lr=0.1, momentum=0.9, rho=0.9, epsilon=1e-10, bucket_mb=32.0,
                  label_smoothing=0.0, aux_weight=0.4, ema_decay=None, lr_schedule=None, use_graph=False,
-                 process_group=None, weight_decay=None, batch_weight=1.0):
+                 process_group=None, weight_decay=None, batch_weight=1.0, nan_guard=True, timer=None):
         self.model = model
         prepare_compute_copies(model)
         params = [p for p in model.parameters() if p.requires_grad]
@@ -35,6 +36,10 @@ class TrainStep:
         self.batch_weight = batch_weight
         self.global_step = 0
         self.use_graph = use_graph
+        self.nan_guard = nan_guard
+        self.last_skip = None   # device int32 flag of the last step (1 = non-finite grads, update skipped)
+        self.skipped = 0        # host count, updated by poll_skipped()
+        self.timer = timer      # utils.metrics.StepTimer for fwd/bwd/allreduce/optimizer HIP-event sections
 
     def loss_fn(self, out, labels):
         aux = None
@@ -52,17 +57,65 @@ class TrainStep:
             return float(self.lr_schedule(self.global_step))
         return self.lr
 
+    def _mark(self, name):
+        if self.timer is not None:
+            self.timer.mark(name)
+
     def __call__(self, images, labels):
+        rng = _range_push("train_step")
         self.dp.zero_grad()
+        self._mark("start")
         if images.is_cuda:
             _fused.arena.begin_step(images.device)
         try:
             out = self.model(images, training=True)
             loss = self.loss_fn(out, labels)
+            self._mark("fwd")
             loss.backward()
+            self._mark("bwd")
         finally:
             _fused.arena.end_step()
         self.dp.finish()
-        self.opt.step(self.current_lr(), grad_scale=self.dp.grad_scale)
+        self._mark("allreduce")
+        skip = None
+        if self.nan_guard:
+            # NaN/Inf guard on the reduced gradient: identical on every rank after the all-reduce,
+            # so all replicas skip the same update
+            flat = self.dp.flat
+            if flat.is_cuda:
+                skip = torch.zeros(1, device=flat.device, dtype=torch.int32)
+                _lib.lib().dtm_check_finite(_lib.ptr(flat), flat.numel(), _lib.ptr(skip), _lib.stream_ptr())
+            else:
+                skip = torch.tensor([0 if bool(torch.isfinite(flat).all()) else 1], dtype=torch.int32)
+            self.last_skip = skip
+        self.opt.step(self.current_lr(), grad_scale=self.dp.grad_scale, skip_flag=skip)
+        self._mark("optimizer")
         self.global_step += 1
+        _range_pop(rng)
         return loss.detach()
+
+    def poll_skipped(self):
+        """Host-side check of the last step's guard (one small sync; call when logging)."""
+        if self.last_skip is not None and int(self.last_skip.item()) != 0:
+            self.skipped += 1
+            return True
+        return False
+
+
+def _range_push(name):
+    """roctx range (torch.cuda.nvtx maps to roctx on ROCm builds); no-op when unavailable."""
+    try:
+        if torch.cuda.is_available():
+            torch.cuda.nvtx.range_push(name)
+            return True
+    except Exception:
+        pass
+    return False
+
+
+def _range_pop(active):
+    if active:
+        try:
+            torch.cuda.nvtx.range_pop()
+        except Exception:
+            pass

@@ -23,7 +23,7 @@ from .compat.train import ExponentialDecay, Server
 from .engine import TrainStep
 from .models import nets_factory
 from .parallel import process_group as pg
-from .utils.metrics import JsonlMetrics, format_step
+from .utils.metrics import JsonlMetrics, StepTimer, format_step
 from .utils.profiler import StepTracer
 
 CIFAR_TRAIN = 50000
@@ -241,7 +241,8 @@ def train(preset, flags, default_mode="bsp"):
     if mode == "bsp":
         step_fn = TrainStep(model, bucket_mb=FLAGS.bucket_mb, label_smoothing=cfg.get("label_smoothing", 0.0),
                             aux_weight=cfg.get("aux_weight", 0.4), ema_decay=cfg.get("ema"), lr_schedule=sched,
-                            batch_weight=FLAGS.batch_weight, **opt_kw)
+                            batch_weight=FLAGS.batch_weight,
+                            timer=StepTimer() if (FLAGS.metrics_file and rank == 0) else None, **opt_kw)
         vars_ = model_variables(model, step_fn.opt, gstep)
         vars_[-1].name = cfg.get("global_step_name", "global_step")
         if path:
@@ -316,11 +317,17 @@ def train(preset, flags, default_mode="bsp"):
         dt = time.time() - t0
         if cfg.get("nan_guard") and math.isnan(loss_v):  # imagenet_inception_bsp.py:191
             raise FloatingPointError("Model diverged with loss = NaN")
+        if mode == "bsp" and need_log and step_fn.poll_skipped():
+            logging.warning("step %d: non-finite gradients, update skipped (%d so far)", step, step_fn.skipped)
         gstep.fill_(gs)
         if step % max(FLAGS.log_every, 1) == 0:
             print(format_step(cfg["log_style"], step, gs, loss_v, B / max(dt, 1e-9), dt), flush=True)
+            extra = step_fn.timer.sections() if (mode == "bsp" and step_fn.timer is not None) else {}
+            if device.type == "cuda" and metrics.f is not None:
+                extra["max_mem_gb"] = torch.cuda.max_memory_allocated(device) / 2 ** 30
             metrics.write(step=step, global_step=gs, loss=loss_v, lr=sched(gs), images_per_sec=B / max(dt, 1e-9),
-                          node_images_per_sec=world * B / max(dt, 1e-9), step_ms=dt * 1e3, world=world, mode=mode)
+                          node_images_per_sec=world * B / max(dt, 1e-9), step_ms=dt * 1e3, world=world, mode=mode,
+                          **extra)
         if cfg.get("train_accuracy_every") and step % cfg["train_accuracy_every"] == 0 and is_chief:
             with torch.no_grad():
                 out = model(images, training=False)
