@@ -11,6 +11,7 @@
 """
 import os
 import re
+import threading
 
 import numpy as np
 import torch
@@ -146,8 +147,53 @@ class Saver:
             raise ValueError("duplicate variable names: %s" % dup[:5])
         self.max_to_keep = max_to_keep
         self.last_checkpoints = []
+        self._thread = None
+        self._error = None
 
-    def save(self, save_path, global_step=None, write_state=True):
+    def _snapshot(self):
+        """Device -> pinned host copies of every variable (HWIO transpose done on the device), queued
+        on the current stream; returns (arrays-producer, event)."""
+        host = []
+        for v in self.vars:
+            t = v.tensor.detach()
+            if v.layout == "KRSC->HWIO":
+                t = t.permute(1, 2, 3, 0)
+            t = t.contiguous()
+            if t.is_cuda:
+                h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+                h.copy_(t, non_blocking=True)
+            else:
+                h = t.clone()
+            host.append((v.name, h))
+        ev = None
+        if any(v.tensor.is_cuda for v in self.vars):
+            ev = torch.cuda.Event()
+            ev.record()
+
+        def arrays():
+            from .bundle import DT_BFLOAT16
+            out = {}
+            for name, h in host:
+                if h.dtype == torch.bfloat16:
+                    out[name] = (h.view(torch.int16).numpy().view(np.uint16), DT_BFLOAT16)
+                else:
+                    out[name] = h.numpy()
+            return out
+        return arrays, ev
+
+    def wait(self):
+        """Block until an in-flight asynchronous save has been written."""
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
+        if self._error is not None:
+            err, self._error = self._error, None
+            raise err
+
+    def save(self, save_path, global_step=None, write_state=True, async_=False):
+        """Write ``<save_path>-<global_step>``.  With ``async_`` the variables are snapshotted to
+        pinned host memory on the device stream and the bundle is written by a background thread,
+        so the training loop continues immediately (at most one save in flight)."""
         if global_step is not None:
             step = int(global_step.item() if torch.is_tensor(global_step) else global_step)
             prefix = "%s-%d" % (save_path, step)
@@ -155,7 +201,26 @@ class Saver:
             prefix = save_path
         d = os.path.dirname(prefix) or "."
         os.makedirs(d, exist_ok=True)
+        self.wait()
+        if async_:
+            arrays, ev = self._snapshot()
+
+            def run():
+                try:
+                    if ev is not None:
+                        ev.synchronize()
+                    write_bundle(prefix, arrays())
+                    self._finish_save(prefix, d, write_state)
+                except Exception as e:  # surfaced by the next wait()/save()
+                    self._error = e
+            self._thread = threading.Thread(target=run, name="ckpt-writer", daemon=True)
+            self._thread.start()
+            return prefix
         write_bundle(prefix, {v.name: v.export() for v in self.vars})
+        self._finish_save(prefix, d, write_state)
+        return prefix
+
+    def _finish_save(self, prefix, d, write_state):
         if prefix in self.last_checkpoints:
             self.last_checkpoints.remove(prefix)
         self.last_checkpoints.append(prefix)
@@ -167,7 +232,6 @@ class Saver:
                     os.remove(full)
         if write_state:
             _write_state(d, prefix, self.last_checkpoints)
-        return prefix
 
     def restore(self, save_path, strict=True):
         r = BundleReader(save_path)

@@ -217,12 +217,19 @@ class Supervisor:
     def save_path(self):
         return os.path.join(self.logdir, "model.ckpt")
 
-    def maybe_save(self, step, force=False):
+    def maybe_save(self, step, force=False, async_=True):
+        """Periodic saves are asynchronous (pinned-host snapshot + writer thread); a forced (final)
+        save is synchronous and also drains any save still in flight."""
         if not (self.is_chief and self.logdir and self.saver is not None):
             return None
         if force or (self.save_model_secs and time.time() - self._last_save >= self.save_model_secs):
             self._last_save = time.time()
-            return self.saver.save(self.save_path(), global_step=step)
+            use_async = async_ and not force and hasattr(self.saver, "wait")
+            path = self.saver.save(self.save_path(), global_step=step, async_=use_async) if use_async else \
+                self.saver.save(self.save_path(), global_step=step)
+            if force and hasattr(self.saver, "wait"):
+                self.saver.wait()
+            return path
         return None
 
     def should_stop(self):

@@ -121,3 +121,22 @@ def test_saver_state_file_and_retention(tmp_path):
     S.Saver([S.TFVar("conv/weights", w2, "KRSC->HWIO"), S.TFVar("conv/biases", b2),
              S.TFVar("global_step", g2)]).restore(S.latest_checkpoint(d))
     assert torch.equal(w2, w) and torch.equal(b2, b) and int(g2) == 30
+
+
+def test_async_save_matches_sync(tmp_path):
+    import torch
+    from distributed_tensorflow_models_amd.ckpt.bundle import BundleReader
+    from distributed_tensorflow_models_amd.ckpt.saver import Saver, TFVar
+    w = torch.randn(8, 3, 3, 4)
+    b = torch.randn(8).to(torch.bfloat16)
+    gs = torch.tensor(7, dtype=torch.int64)
+    vs = [TFVar("conv/weights", w, "KRSC->HWIO"), TFVar("conv/biases", b), TFVar("global_step", gs)]
+    s1, s2 = Saver(vs), Saver(vs)
+    p1 = s1.save(str(tmp_path / "a" / "model.ckpt"), global_step=gs)
+    p2 = s2.save(str(tmp_path / "b" / "model.ckpt"), global_step=gs, async_=True)
+    w.add_(1.0)          # mutate after the snapshot: the async checkpoint must hold the old values
+    s2.wait()
+    r1, r2 = BundleReader(p1), BundleReader(p2)
+    for n in ("conv/weights", "conv/biases", "global_step"):
+        np.testing.assert_array_equal(r1.get_tensor(n), r2.get_tensor(n))
+    assert (tmp_path / "b" / "checkpoint").exists()
