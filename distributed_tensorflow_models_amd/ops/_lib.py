@@ -11,7 +11,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_HERE, "_native", "libdtm_kernels.so")
+LIB_PATH = os.environ.get("DTM_KERNELS_SO") or os.path.join(_HERE, "_native", "libdtm_kernels.so")  # A/B override
 
 _lib = None
 
