@@ -595,6 +595,26 @@ __global__ void weight_flip_transpose_kernel(const bf16_t* __restrict__ w, bf16_
   }
 }
 
+// one launch refreshing the flipped/transposed dgrad copies of many conv weights (after the
+// optimizer step) instead of one tiny launch per conv in every backward
+struct FlipDesc {
+  const bf16_t* w;
+  bf16_t* wt;
+  int K, R, S, C;
+};
+__global__ void weight_flip_batched_kernel(const FlipDesc* __restrict__ descs) {
+  const FlipDesc f = descs[blockIdx.y];
+  const size_t total = (size_t)f.K * f.R * f.S * f.C;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    int k = i % f.K;
+    size_t t = i / f.K;
+    int s2 = t % f.S; t /= f.S;
+    int r2 = t % f.R;
+    int c = t / f.R;
+    f.wt[i] = f.w[(((size_t)k * f.R + (f.R - 1 - r2)) * f.S + (f.S - 1 - s2)) * f.C + c];
+  }
+}
+
 }  // namespace dtm
 
 using namespace dtm;
@@ -748,6 +768,14 @@ DTM_API int dtm_conv_wgrad(const void* x, const void* dy, float* dw, const float
   // dW += sum over the split slabs (every slab element is written: tiles cover [K][Kg] exactly)
   dtm_reduce_rows(ws, (int)splits, a.K * a.Kg, a.K * a.Kg, dw, (hipStream_t)stream);
   return 0;
+}
+
+DTM_API int dtm_flip_desc_bytes() { return (int)sizeof(FlipDesc); }
+
+DTM_API void dtm_weight_flip_transpose_batched(const void* descs, int n, void* stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(weight_flip_batched_kernel, dim3(64, n), dim3(256), 0, (hipStream_t)stream,
+                     (const FlipDesc*)descs);
 }
 
 DTM_API void dtm_weight_flip_transpose(const void* w, void* wt, int K, int R, int S, int C, void* stream) {

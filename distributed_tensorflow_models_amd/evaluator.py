@@ -68,6 +68,8 @@ def restore_for_eval(model, path, use_ema):
         shadow = name + "/ExponentialMovingAverage"
         vs.append(TFVar(shadow if (use_ema and trainable and shadow in names) else name, t, layout))
     Saver(vs).restore(path)
+    from .ops.nn import invalidate_weight_copies
+    invalidate_weight_copies(model.parameters())
 
 
 def _inputs(preset, flags, device):

@@ -37,6 +37,8 @@ _SIGS = {
     "dtm_conv_dgrad_ex": (_I, [_P, _P, _P, ctypes.POINTER(ConvDesc), _P, _P, _P, _P, _P]),
     "dtm_conv_wgrad": (_I, [_P, _P, _P, _P, _P, ctypes.POINTER(ConvDesc), _I, _P]),
     "dtm_weight_flip_transpose": (None, [_P, _P, _I, _I, _I, _I, _P]),
+    "dtm_weight_flip_transpose_batched": (None, [_P, _I, _P]),
+    "dtm_flip_desc_bytes": (_I, []),
     "dtm_bn_stats": (None, [_P, _P, _L, _I, _P]),
     "dtm_bn_finalize": (None, [_P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _I, _I, _P]),
     "dtm_bn_inference_params": (None, [_P, _P, _P, _P, _P, _I, _F, _P]),

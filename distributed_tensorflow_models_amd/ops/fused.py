@@ -16,7 +16,7 @@ import torch
 from . import _lib
 from .geometry import conv_geom
 from .lazy import LazyBN, as_tensor  # noqa: F401
-from .nn import _accum_param_grad, _check, _notify, weight_bf16
+from .nn import _accum_param_grad, _check, _notify, weight_bf16, weight_flipped
 
 
 class ZeroArena:
@@ -145,9 +145,7 @@ class _ConvBNFn(torch.autograd.Function):
         dx = d_in = None
         if ctx.needs_input_grad[0] or (in_ss is not None and ctx.needs_input_grad[1]):
             last, add_src = _slot_take(ctx.slot)
-            w16 = weight_bf16(w)
-            wt = torch.empty((g.C, g.R, g.S, g.K), device=dy.device, dtype=torch.bfloat16)
-            L.dtm_weight_flip_transpose(_lib.ptr(w16), _lib.ptr(wt), g.K, g.R, g.S, g.C, s)
+            wt = weight_flipped(w, g.K, g.R, g.S, g.C)
             dx = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
             if in_ss is not None:
                 # BN+ReLU of the input was fused into the forward prologue: mask, scale and the BN

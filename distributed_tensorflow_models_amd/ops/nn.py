@@ -63,6 +63,66 @@ def weight_bf16(w):
     return w16
 
 
+# flipped/transposed bf16 weight copies for dgrad ([C][R][S][K] from [K][R][S][C]).  A copy is valid
+# for one weights version; FusedOptimizer bumps the version and refreshes every registered copy in
+# one batched launch right after its update, so backward normally finds them ready.
+WEIGHT_VERSION = [0]
+FLIP_REGISTRY = {}   # id(param) -> (param, wt buffer)
+
+
+def weight_flipped(w, K, R, S, C):
+    c = getattr(w, "_flip", None)
+    if c is not None and c[0] == WEIGHT_VERSION[0] and c[1].shape == (C, R, S, K):
+        return c[1]
+    L = _lib.lib()
+    wt = c[1] if (c is not None and c[1].shape == (C, R, S, K)) else \
+        torch.empty((C, R, S, K), device=w.device, dtype=torch.bfloat16)
+    L.dtm_weight_flip_transpose(_lib.ptr(weight_bf16(w)), _lib.ptr(wt), K, R, S, C, _lib.stream_ptr())
+    if isinstance(w, torch.nn.Parameter):
+        try:
+            w._flip = (WEIGHT_VERSION[0], wt)
+            FLIP_REGISTRY[id(w)] = (w, wt)
+        except Exception:
+            pass
+    return wt
+
+
+def refresh_flipped(stream=None):
+    """After a weight update: one batched launch re-deriving every registered dgrad copy."""
+    WEIGHT_VERSION[0] += 1
+    if not FLIP_REGISTRY:
+        return
+    L = _lib.lib()
+    entries = list(FLIP_REGISTRY.values())
+    key = tuple(id(w) for w, _ in entries)
+    cache = refresh_flipped.__dict__.get("table")
+    if cache is None or cache[0] != key:
+        nb = L.dtm_flip_desc_bytes()
+        import numpy as np
+        tab = np.zeros((len(entries), nb // 8), dtype=np.int64)
+        for i, (w, wt) in enumerate(entries):
+            C, R, S, K = wt.shape
+            tab[i, 0] = weight_bf16(w).data_ptr()
+            tab[i, 1] = wt.data_ptr()
+            tab[i, 2:4] = np.array([K, R, S, C], dtype=np.int32).view(np.int64)
+        dev_tab = torch.from_numpy(tab.view(np.uint8).reshape(-1).copy()).to(entries[0][0].device)
+        refresh_flipped.table = cache = (key, dev_tab, len(entries))
+    L.dtm_weight_flip_transpose_batched(_lib.ptr(cache[1]), cache[2], stream or _lib.stream_ptr())
+    for w, wt in entries:
+        w._flip = (WEIGHT_VERSION[0], wt)
+
+
+def invalidate_weight_copies(params):
+    """Weights changed outside the optimizer (checkpoint restore, ASP pull, broadcast): refresh the
+    bf16 compute copies and drop the flipped dgrad copies."""
+    with torch.no_grad():
+        for p in params:
+            w16 = getattr(p, "bf16", None)
+            if w16 is not None and w16.shape == p.shape:
+                w16.copy_(p)
+    WEIGHT_VERSION[0] += 1
+
+
 # ---------------------------------------------------------------------------------------------
 # convolution
 class _Conv2dFn(torch.autograd.Function):
@@ -92,9 +152,7 @@ class _Conv2dFn(torch.autograd.Function):
         s = _lib.stream_ptr()
         dx = None
         if ctx.needs_input_grad[0]:
-            w16 = weight_bf16(w)
-            wt = torch.empty((g.C, g.R, g.S, g.K), device=dy.device, dtype=torch.bfloat16)
-            L.dtm_weight_flip_transpose(_lib.ptr(w16), _lib.ptr(wt), g.K, g.R, g.S, g.C, s)
+            wt = weight_flipped(w, g.K, g.R, g.S, g.C)
             dx = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
             _check(L.dtm_conv_dgrad(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), s), "conv_dgrad")
         dw = None

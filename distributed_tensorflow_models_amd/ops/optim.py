@@ -115,6 +115,8 @@ class FusedOptimizer:
         if self._dev is not None:
             self.set_dynamic(lr, grad_scale)
             self.launch(skip_flag)
+            from .nn import refresh_flipped
+            refresh_flipped()
         else:
             self._step_cpu(lr, grad_scale, skip_flag)
         self.num_updates += 1

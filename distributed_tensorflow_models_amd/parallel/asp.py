@@ -126,11 +126,13 @@ class ParamStore:
     @torch.no_grad()
     def pull(self):
         """Copy the current shared parameters into the local replica (M1)."""
+        from ..ops.nn import WEIGHT_VERSION
         for i, p in enumerate(self.params):
             p.copy_(self.shards[i]["param"].to(p.device, non_blocking=True))
             w16 = getattr(p, "bf16", None)
             if w16 is not None:
                 w16.copy_(p)
+        WEIGHT_VERSION[0] += 1
 
     @torch.no_grad()
     def push(self, grads, lr=None, grad_scale=1.0):

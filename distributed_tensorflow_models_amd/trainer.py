@@ -250,6 +250,8 @@ def train(preset, flags, default_mode="bsp"):
         if world > 1:  # one collective replaces the reference's chief-init + 1 s polling of workers
             pg.broadcast_tensors([v.tensor for v in vars_ if v.tensor.is_floating_point()] +
                                  [b for b in model.buffers()])
+        from .ops.nn import invalidate_weight_copies
+        invalidate_weight_copies(model.parameters())  # bf16 compute copies follow the restored weights
         step_fn.global_step = int(gstep)
         step_fn.opt.num_updates = int(gstep)
     elif mode in ("asp", "ssp"):
