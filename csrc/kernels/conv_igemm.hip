@@ -58,7 +58,7 @@ struct ConvNTArgs {
   float* act_sums;        //   partial rows per pixel tile: [sum g*act_x (K) | sum g (K)]
 };
 
-template <int PT, int CT, int WP, int WC, int UD>
+template <int PT, int CT, int WP, int WC, int UD, int NBUF>
 __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
   constexpr int BK = 64;
   constexpr int NWP = PT / WP;
@@ -69,8 +69,8 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
   constexpr int WCH = CT / 32;
   constexpr int BUF = (PT + CT) * 128;
   constexpr int MAXC = 512;  // prologue scale/shift staged in LDS for C <= MAXC (bottleneck widths)
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF + MAXC * 8];
-  float* s_scale = (float*)(smem + 2 * BUF);
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF + MAXC * 8];
+  float* s_scale = (float*)(smem + NBUF * BUF);
   float* s_shift = s_scale + MAXC;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -227,11 +227,23 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
   swrite(0, st);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload(kt + 1, st);
-    compute(cur);
-    if (kt + 1 < nk) swrite(cur ^ 1, st);
-    __syncthreads();
+    if constexpr (NBUF == 2) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) gload(kt + 1, st);
+      compute(cur);
+      if (kt + 1 < nk) swrite(cur ^ 1, st);
+      __syncthreads();
+    } else {
+      // single LDS buffer (less LDS -> more resident blocks for short-K layers): the next tile's
+      // global loads still overlap the MFMAs; the LDS write waits for every wave's reads
+      if (kt + 1 < nk) gload(kt + 1, st);
+      compute(0);
+      __syncthreads();
+      if (kt + 1 < nk) {
+        swrite(0, st);
+        __syncthreads();
+      }
+    }
   }
 
   // epilogue: lane holds channels (fk*4 .. +3) of pixel fr for every subtile.  Bias/ReLU and the
@@ -240,7 +252,7 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
   // full 16-B chunk and consecutive lanes cover whole NHWC pixel rows (coalesced, 256-B rows for
   // CT = 128) instead of 16 scattered 32-B pieces per wave instruction.
   constexpr int OROW = CT * 2 + 16;
-  static_assert(PT * OROW <= 2 * BUF, "output staging fits in the operand buffers");
+  static_assert(PT * OROW <= NBUF * BUF, "output staging fits in the operand buffers");
   const bool staged = (a.K & 7) == 0;
 #pragma unroll
   for (int i = 0; i < TC; ++i) {
@@ -626,14 +638,15 @@ struct ConvDesc {
   int N, H, W, C, K, R, S, P, Q, stride, pad_h, pad_w;
 };
 
-template <int PT, int CT, int WP, int WC, int UD>
+template <int PT, int CT, int WP, int WC, int UD, int NBUF = 2>
 static void launch_nt(const ConvNTArgs& a, hipStream_t st) {
   dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT);
-  hipLaunchKernelGGL((conv_nt_kernel<PT, CT, WP, WC, UD>), grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((conv_nt_kernel<PT, CT, WP, WC, UD, NBUF>), grid, dim3(256), 0, st, a);
 }
 
 // tile variants: 0 = 128 pix x 128 ch (4 waves 2x2 of 64x64), 1 = 128 x 64 (4x1 of 32x64),
-// 2 = 64 x 128 (2x2 of 32x64; 3 blocks/CU by LDS).  DTM_CONV_TILE forces one (A/B experiments).
+// 2 = 64 x 128 (2x2 of 32x64; 3 blocks/CU by LDS), 3 / 4 = 1 / 2 with a single LDS buffer
+// (more resident blocks).  DTM_CONV_TILE forces one (A/B experiments).
 struct TileCfg {
   int id, PT, NWP;
 };
@@ -643,9 +656,13 @@ static TileCfg pick_tile(const ConvNTArgs& a) {
     const char* e = getenv("DTM_CONV_TILE");
     g_tile_env = e ? atoi(e) : -1;
   }
-  int id = g_tile_env >= 0 ? g_tile_env : (a.K <= 64 ? 1 : 0);
-  if (id == 1) return {1, 128, 4};
-  if (id == 2) return {2, 64, 2};
+  // measured per ResNet-50 shape (tools/conv_microbench.py, DTM_CONV_TILE sweep): the single-buffer
+  // variants win almost everywhere (more resident blocks hide the short-K latency); the 2-buffer
+  // 128x128 tile keeps the small-M / deep-K layers (7x7 maps, K-reduction >= 2048)
+  int id = g_tile_env;
+  if (id < 0) id = a.K <= 64 ? 3 : ((a.M <= 16384 && a.Kg >= 2048) ? 0 : 4);
+  if (id == 1 || id == 3) return {id, 128, 4};
+  if (id == 2 || id == 4) return {id, 64, 2};
   return {0, 128, 2};
 }
 
@@ -653,6 +670,8 @@ template <int UD>
 static void dispatch_ud(const ConvNTArgs& a, const TileCfg& t, hipStream_t st) {
   if (t.id == 1) launch_nt<128, 64, 32, 64, UD>(a, st);
   else if (t.id == 2) launch_nt<64, 128, 32, 64, UD>(a, st);
+  else if (t.id == 3) launch_nt<128, 64, 32, 64, UD, 1>(a, st);
+  else if (t.id == 4) launch_nt<64, 128, 32, 64, UD, 1>(a, st);
   else launch_nt<128, 128, 64, 64, UD>(a, st);
 }
 
