@@ -404,7 +404,7 @@ __device__ __forceinline__ int tr_off(int k, int m) {
   return ((b << 7) + ((k & 3) << 5) + ((m & 15) << 1)) ^ (((k >> 3) & 1) << 7);
 }
 
-template <int MT, int NT, int WM, int WN>
+template <int MT, int NT, int WM, int WN, int NBUF>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
   constexpr int BK = 64;
   constexpr int NWM = MT / WM, NWN = NT / WN;
@@ -413,8 +413,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
   constexpr int ACH = MT / 32;  // BK*MT/8 chunks / 256 threads
   constexpr int BCH = NT / 32;
   constexpr int BUF = BK * (MT + NT) * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF + NT * 8];
-  float* s_scale = (float*)(smem + 2 * BUF);  // prologue scale/shift of this block's NT columns
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF + NT * 8];
+  float* s_scale = (float*)(smem + NBUF * BUF);  // prologue scale/shift of this block's NT columns
   float* s_shift = s_scale + NT;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -534,7 +534,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
   typedef __attribute__((address_space(3))) short4v lds_s4;
   typedef __attribute__((address_space(3))) char lds_c;
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
+    const int cur = NBUF == 2 ? (kt & 1) : 0;
     if (kt + 1 < nk) gload(pix_lo + (kt + 1) * BK);
     lds_c* lbase = (lds_c*)(smem + cur * BUF);
 #pragma unroll
@@ -565,8 +565,16 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) swrite(cur ^ 1);
-    __syncthreads();
+    if constexpr (NBUF == 2) {
+      if (kt + 1 < nk) swrite(cur ^ 1);
+      __syncthreads();
+    } else {
+      __syncthreads();
+      if (kt + 1 < nk) {
+        swrite(0);
+        __syncthreads();
+      }
+    }
   }
   // epilogue: acc rows = ko (4 consecutive per lane), cols = flattened (r,s,c).  Each pixel split
   // writes its partial tile to its own workspace slab (plain stores); dtm_reduce_rows then sums the
@@ -749,10 +757,10 @@ DTM_API int dtm_conv_dgrad(const void* dy, const void* wt, void* dx, const ConvD
   return dtm_conv_dgrad_ex(dy, wt, dx, d, nullptr, nullptr, nullptr, nullptr, stream);
 }
 
-template <int MT, int NT, int WM, int WN>
+template <int MT, int NT, int WM, int WN, int NBUF = 2>
 static void launch_wgrad(const ConvWgradArgs& a, int splits, hipStream_t st) {
   dim3 grid((a.Kg + NT - 1) / NT, (a.K + MT - 1) / MT, splits);
-  hipLaunchKernelGGL((conv_wgrad_kernel<MT, NT, WM, WN>), grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((conv_wgrad_kernel<MT, NT, WM, WN, NBUF>), grid, dim3(256), 0, st, a);
 }
 
 DTM_API int dtm_conv_wgrad(const void* x, const void* dy, float* dw, const float* in_scale,
@@ -768,7 +776,15 @@ DTM_API int dtm_conv_wgrad(const void* x, const void* dy, float* dw, const float
   a.P = d->P; a.Q = d->Q; a.stride = d->stride; a.pad_h = d->pad_h; a.pad_w = d->pad_w;
   a.Mpix = d->N * d->P * d->Q; a.Kg = d->R * d->S * d->C;
   a.fd_PQ = make_fastdiv(d->P * d->Q); a.fd_Q = make_fastdiv(d->Q);
-  const bool small_m = d->K <= 64;
+  // wgrad tile variants: 0 = 128 (K) x 128 (RSC) 2 LDS buffers, 1 = 64 x 128, 2 = 64 x 128 single
+  // buffer, 3 = 128 x 128 single buffer.  DTM_WGRAD_TILE forces one (A/B experiments).
+  static int wenv = -2;
+  if (wenv == -2) {
+    const char* e = getenv("DTM_WGRAD_TILE");
+    wenv = e ? atoi(e) : -1;
+  }
+  int wt = wenv >= 0 ? wenv : (d->K <= 64 ? 1 : 0);
+  const bool small_m = (wt == 1 || wt == 2);
   const int MT = small_m ? 64 : 128, NT = 128;
   long tiles = (long)((a.Kg + NT - 1) / NT) * ((a.K + MT - 1) / MT);
   long target = (long)num_cus * 3;
@@ -782,7 +798,9 @@ DTM_API int dtm_conv_wgrad(const void* x, const void* dy, float* dw, const float
   float* ws = dtm_ws_get((size_t)splits * a.K * a.Kg);
   if (!ws) return -4;
   a.dw = ws;
-  if (small_m) launch_wgrad<64, 128, 32, 64>(a, (int)splits, (hipStream_t)stream);
+  if (wt == 1) launch_wgrad<64, 128, 32, 64>(a, (int)splits, (hipStream_t)stream);
+  else if (wt == 2) launch_wgrad<64, 128, 32, 64, 1>(a, (int)splits, (hipStream_t)stream);
+  else if (wt == 3) launch_wgrad<128, 128, 64, 64, 1>(a, (int)splits, (hipStream_t)stream);
   else launch_wgrad<128, 128, 64, 64>(a, (int)splits, (hipStream_t)stream);
   // dW += sum over the split slabs (every slab element is written: tiles cover [K][Kg] exactly)
   dtm_reduce_rows(ws, (int)splits, a.K * a.Kg, a.K * a.Kg, dw, (hipStream_t)stream);
