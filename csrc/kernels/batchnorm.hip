@@ -370,6 +370,30 @@ __global__ __launch_bounds__(256) void bn_apply_fast(const bf16_t* __restrict__ 
   }
 }
 
+// y = act(x*scale + shift + res[n][h*s][w*s]): identity residual read through a 1x1 stride-s
+// subsample of the block input (slim resnet_v1 `subsample`), so the subsampled tensor is never stored.
+__global__ __launch_bounds__(256) void bn_apply_res_strided(const bf16_t* __restrict__ x, const float* __restrict__ ss,
+                                                            const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
+                                                            uint32_t M, int C, int relu, FastDiv fd_cols, FastDiv fd_Wo,
+                                                            FastDiv fd_Ho, int Ho, int Wo, int Hi, int Wi, int s) {
+  const uint32_t cols = C >> 3, total = M * cols;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const uint32_t r = fdiv(i, fd_cols), c0 = (i - r * cols) * 8;
+    const uint32_t t = fdiv(r, fd_Wo), w = r - t * Wo;
+    const uint32_t n = fdiv(t, fd_Ho), h = t - n * Ho;
+    const size_t rr = ((size_t)n * Hi + (size_t)h * s) * Wi + (size_t)w * s;
+    float f[8], g[8];
+    unpack8(*(const uint4*)(x + (size_t)r * C + c0), f);
+    unpack8(*(const uint4*)(res + rr * C + c0), g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      f[e] = fmaf(f[e], ss[c0 + e], ss[C + c0 + e]) + g[e];
+      if (relu) f[e] = fmaxf(f[e], 0.f);
+    }
+    *(uint4*)(y + (size_t)r * C + c0) = pack8(f);
+  }
+}
+
 __global__ __launch_bounds__(256) void bn_bwd_reduce_fast(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                           const bf16_t* __restrict__ ym, const float* __restrict__ ss,
                                                           float* __restrict__ sums, int M, int C, int mask_mode, int rpb) {
@@ -538,6 +562,20 @@ DTM_API void dtm_bn_apply(const void* x, const float* ss, const void* res, const
   else
     hipLaunchKernelGGL(bn_apply_kernel<1>, dim3(grid_for(M * C)), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)x, ss, (const bf16_t*)res, rss, (bf16_t*)y, M, C, res_mode, relu);
+}
+
+// res [N][Hi][Wi][C] read at (n, h*s, w*s) for every output pixel of x / y [N][Ho][Wo][C]
+DTM_API int dtm_bn_apply_res_strided(const void* x, const float* ss, const void* res, void* y, int N, int Ho, int Wo,
+                                     int C, int Hi, int Wi, int s, int relu, void* stream) {
+  if (C % 8 || (long)N * Ho * Wo * (C / 8) >= (1l << 31) || (Ho - 1) * s >= Hi || (Wo - 1) * s >= Wi) return -1;
+  const uint32_t M = (uint32_t)N * Ho * Wo;
+  const long total = (long)M * (C / 8);
+  long blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(bn_apply_res_strided, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ss,
+                     (const bf16_t*)res, (bf16_t*)y, M, C, relu, make_fastdiv(C / 8), make_fastdiv(Wo),
+                     make_fastdiv(Ho), Ho, Wo, Hi, Wi, s);
+  return 0;
 }
 
 DTM_API void dtm_bn_bwd_reduce(const void* dy, const void* x, const void* ymask, const float* ss, float* sums, long M,

@@ -53,6 +53,8 @@ struct ConvNTArgs {
   FastDiv fd_PQ, fd_Q;
   // optional epilogue post-ops on the coalesced 16-B output chunks (used by dgrad):
   const bf16_t* add_src;  // out += add_src (the other consumer's gradient of a shared input)
+  int add_stride;         //   > 1: add_src is [N][add_H][add_W][K], added at pixels (h, w) % add_stride == 0
+  int add_H, add_W;       //   (the gradient of a strided subsample of this tensor)
   const bf16_t* act_x;    // fused activation backward of the input's BatchNorm+ReLU prologue:
   const float* act_ss;    //   g = out * [act_x*scale + shift > 0]; out <- g*scale;
   float* act_sums;        //   partial rows per pixel tile: [sum g*act_x (K) | sum g (K)]
@@ -332,9 +334,20 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
           f[0] = lo_bf(v.x); f[1] = hi_bf(v.x); f[2] = lo_bf(v.y); f[3] = hi_bf(v.y);
           f[4] = lo_bf(v.z); f[5] = hi_bf(v.z); f[6] = lo_bf(v.w); f[7] = hi_bf(v.w);
           if (a.add_src) {
-            const uint4 r = *(const uint4*)(a.add_src + o);
-            f[0] += lo_bf(r.x); f[1] += hi_bf(r.x); f[2] += lo_bf(r.y); f[3] += hi_bf(r.y);
-            f[4] += lo_bf(r.z); f[5] += hi_bf(r.z); f[6] += lo_bf(r.w); f[7] += hi_bf(r.w);
+            const bf16_t* src = a.add_src + o;
+            if (a.add_stride > 1) {
+              const uint32_t n = fdiv((uint32_t)m, a.fd_PQ), rem = m - n * (a.P * a.Q);
+              const uint32_t h = fdiv(rem, a.fd_Q), w = rem - h * a.Q;
+              const int s = a.add_stride;
+              src = (h % s == 0 && w % s == 0)
+                        ? a.add_src + ((size_t)((int)n * a.add_H + (int)h / s) * a.add_W + (int)w / s) * a.K + kc
+                        : nullptr;
+            }
+            if (src) {
+              const uint4 r = *(const uint4*)src;
+              f[0] += lo_bf(r.x); f[1] += hi_bf(r.x); f[2] += lo_bf(r.y); f[3] += hi_bf(r.y);
+              f[4] += lo_bf(r.z); f[5] += hi_bf(r.z); f[6] += lo_bf(r.w); f[7] += hi_bf(r.w);
+            }
           }
           if (act) {
             const uint4 xu = *(const uint4*)(a.act_x + o);
@@ -696,6 +709,7 @@ DTM_API int dtm_conv_fwd(const void* x, const void* w, void* y, float* stats, co
   a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.y = (bf16_t*)y;
   a.stats = stats; a.bias = bias; a.in_scale = in_scale; a.in_shift = in_shift;
   a.add_src = nullptr; a.act_x = nullptr; a.act_ss = nullptr; a.act_sums = nullptr;
+  a.add_stride = 1; a.add_H = a.add_W = 0;
   size_t xb = (size_t)d->N * d->H * d->W * d->C * 2, wb = (size_t)d->K * d->R * d->S * d->C * 2;
   if (xb >= (1ull << 31) || wb >= (1ull << 31)) return -2;
   a.x_bytes = (uint32_t)xb; a.w_bytes = (uint32_t)wb;
@@ -720,18 +734,23 @@ DTM_API int dtm_conv_fwd(const void* x, const void* w, void* y, float* stats, co
 // dgrad: dx[N][H][W][C] from dy[N][P][Q][K] and the flipped/transposed weight wt[C][R][S][K].
 // Optional epilogue post-ops (nullptr = off):
 //   add_src [N][H][W][C]: dx += add_src (gradient of the same input from its other consumer);
+//   add_stride > 1: add_src is [N][(H-1)/s+1][(W-1)/s+1][C], the gradient of x[:, ::s, ::s] (a 1x1
+//   stride-s subsample shortcut), added at the pixels that subsample read;
 //   act_x [N][H][W][C] + act_ss [4][C] (scale, shift, ...): the input was relu(act_x*scale+shift)
 //   (BatchNorm+ReLU fused into this conv's forward prologue); dx <- [act_x*scale+shift>0]*dx*scale and
 //   act_sums[2][C] += (sum g*act_x, sum g) with g the masked gradient (the BN scale/shift grads).
 DTM_API int dtm_conv_dgrad_ex(const void* dy, const void* wt, void* dx, const ConvDesc* d, const void* add_src,
-                              const void* act_x, const float* act_ss, float* act_sums, void* stream) {
+                              int add_stride, const void* act_x, const float* act_ss, float* act_sums, void* stream) {
   if (d->K % 8 || d->C % 4) return -1;
+  if (add_stride < 1 || (add_stride > 1 && !add_src)) return -6;
   if (d->stride > 2) return -3;
   if ((add_src || act_x) && d->C % 8) return -5;
   ConvNTArgs a;
   a.x = (const bf16_t*)dy; a.w = (const bf16_t*)wt; a.y = (bf16_t*)dx;
   a.stats = nullptr; a.bias = nullptr; a.in_scale = nullptr; a.in_shift = nullptr;
   a.add_src = (const bf16_t*)add_src; a.act_x = (const bf16_t*)act_x; a.act_ss = act_ss; a.act_sums = nullptr;
+  a.add_stride = add_stride;
+  a.add_H = (d->H - 1) / add_stride + 1; a.add_W = (d->W - 1) / add_stride + 1;
   size_t xb = (size_t)d->N * d->P * d->Q * d->K * 2, wb = (size_t)d->K * d->R * d->S * d->C * 2;
   if (xb >= (1ull << 31) || wb >= (1ull << 31)) return -2;
   a.x_bytes = (uint32_t)xb; a.w_bytes = (uint32_t)wb;
@@ -754,7 +773,7 @@ DTM_API int dtm_conv_dgrad_ex(const void* dy, const void* wt, void* dx, const Co
 }
 
 DTM_API int dtm_conv_dgrad(const void* dy, const void* wt, void* dx, const ConvDesc* d, void* stream) {
-  return dtm_conv_dgrad_ex(dy, wt, dx, d, nullptr, nullptr, nullptr, nullptr, stream);
+  return dtm_conv_dgrad_ex(dy, wt, dx, d, nullptr, 1, nullptr, nullptr, nullptr, stream);
 }
 
 template <int MT, int NT, int WM, int WN, int NBUF = 2>

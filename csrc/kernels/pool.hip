@@ -195,6 +195,129 @@ __global__ __launch_bounds__(256) void global_avg_bwd_kernel(const float* __rest
   }
 }
 
+// ---- BatchNorm-apply + ReLU fused into a max pool (ResNet stem: conv1 -> BN -> ReLU -> 3x3/2 pool) ----
+// The normalised activation relu(x*scale + shift) is formed on the fly from the raw conv output and
+// never stored.  Backward: each input pixel gathers the gradient of the windows whose argmax it is,
+// applies the ReLU mask (recomputed from x) and the BN scale, and accumulates the BN parameter-gradient
+// partial sums (sum g*x, sum g) per block (reduced by reduce_rows), exactly as bn_apply_bwd does.
+__global__ __launch_bounds__(256) void maxpool_bnrelu_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ ss,
+                                                                 bf16_t* __restrict__ y, uint8_t* __restrict__ arg,
+                                                                 PoolArgs a, FastDiv fd_cols, FastDiv fd_Q, FastDiv fd_P) {
+  const uint32_t cols = a.C >> 3, total = (uint32_t)a.N * a.P * a.Q * cols;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const uint32_t o = fdiv(i, fd_cols), cv = (i - o * cols) * 8;
+    const uint32_t t = fdiv(o, fd_Q), q = o - t * a.Q;
+    const uint32_t n = fdiv(t, fd_P), p = t - n * a.P;
+    float sc[8], sh[8], best[8];
+    uint32_t bi[8];
+    {
+      const float4 s0 = *(const float4*)(ss + cv), s1 = *(const float4*)(ss + cv + 4);
+      const float4 h0 = *(const float4*)(ss + a.C + cv), h1 = *(const float4*)(ss + a.C + cv + 4);
+      sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+      sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w; sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    for (int r = 0; r < a.KH; ++r) {
+      const int h = (int)p * a.SH - a.PH + r;
+      if (h < 0 || h >= a.H) continue;
+      for (int s = 0; s < a.KW; ++s) {
+        const int w = (int)q * a.SW - a.PW + s;
+        if (w < 0 || w >= a.W) continue;
+        float f[8];
+        ld<8>(x + (((size_t)n * a.H + h) * a.W + w) * a.C + cv, f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = fmaxf(fmaf(f[e], sc[e], sh[e]), 0.f);
+          if (v > best[e]) { best[e] = v; bi[e] = (uint32_t)(r * a.KW + s); }
+        }
+      }
+    }
+    st<8>(y + (size_t)o * a.C + cv, best);
+    *(uint2*)(arg + (size_t)o * a.C + cv) = make_uint2(bi[0] | bi[1] << 8 | bi[2] << 16 | bi[3] << 24,
+                                                      bi[4] | bi[5] << 8 | bi[6] << 16 | bi[7] << 24);
+  }
+}
+
+// WM = max windows covering one input pixel per dimension (ceil(k / stride)); all candidate window
+// loads of FU rows are issued before any is consumed (predicated, no data-dependent branches).
+template <int WM, int FU>
+__global__ __launch_bounds__(256) void maxpool_bnrelu_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                                 const uint8_t* __restrict__ arg,
+                                                                 const bf16_t* __restrict__ x, const float* __restrict__ ss,
+                                                                 bf16_t* __restrict__ dx, float* __restrict__ part,
+                                                                 PoolArgs a, FastDiv fd_W, FastDiv fd_H, int rpb) {
+  __shared__ float red[2][256][8];
+  const int cols = a.C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t % cols) * 8, lr0 = t / cols;
+  float sc[8], sh[8], a1[8], a0[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { sc[e] = ss[c0 + e]; sh[e] = ss[a.C + c0 + e]; a1[e] = 0.f; a0[e] = 0.f; }
+  const int M = a.N * a.H * a.W;
+  const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
+  for (int row0 = lr0 < RP ? r0 + lr0 : r1; row0 < r1; row0 += RP * FU) {
+    uint4 gv[FU][WM * WM];
+    uint2 av[FU][WM * WM];
+    uint32_t want[FU][WM * WM];
+    uint4 xvv[FU];
+#pragma unroll
+    for (int u = 0; u < FU; ++u) {
+      const int row = row0 + u * RP;
+      const bool rok = row < r1;
+      const uint32_t rr = rok ? (uint32_t)row : (uint32_t)r0;
+      const uint32_t tt = fdiv(rr, fd_W), w = rr - tt * a.W;
+      const uint32_t n = fdiv(tt, fd_H), h = tt - n * a.H;
+      const int plo = first_win((int)h + a.PH - a.KH + 1, a.SH);
+      const int qlo = first_win((int)w + a.PW - a.KW + 1, a.SW);
+#pragma unroll
+      for (int i = 0; i < WM; ++i) {
+#pragma unroll
+        for (int j = 0; j < WM; ++j) {
+          const int p = plo + i, q = qlo + j;
+          const int r = (int)h - (p * a.SH - a.PH), s = (int)w - (q * a.SW - a.PW);
+          const bool ok = rok && p < a.P && q < a.Q && r >= 0 && r < a.KH && s >= 0 && s < a.KW;
+          const size_t oo = ok ? (((size_t)n * a.P + p) * a.Q + q) * a.C + c0 : (size_t)c0;
+          gv[u][i * WM + j] = *(const uint4*)(dy + oo);
+          av[u][i * WM + j] = *(const uint2*)(arg + oo);
+          want[u][i * WM + j] = ok ? (uint32_t)(r * a.KW + s) : 0xffffffffu;
+        }
+      }
+      xvv[u] = *(const uint4*)(x + (size_t)rr * a.C + c0);
+    }
+#pragma unroll
+    for (int u = 0; u < FU; ++u) {
+      const int row = row0 + u * RP;
+      if (row >= r1) break;
+      float acc[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+#pragma unroll
+      for (int k = 0; k < WM * WM; ++k) {
+        float g[8];
+        g[0] = lo_bf(gv[u][k].x); g[1] = hi_bf(gv[u][k].x); g[2] = lo_bf(gv[u][k].y); g[3] = hi_bf(gv[u][k].y);
+        g[4] = lo_bf(gv[u][k].z); g[5] = hi_bf(gv[u][k].z); g[6] = lo_bf(gv[u][k].w); g[7] = hi_bf(gv[u][k].w);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t b = ((e < 4 ? av[u][k].x : av[u][k].y) >> (8 * (e & 3))) & 0xffu;
+          if (b == want[u][k]) acc[e] += g[e];
+        }
+      }
+      float xv[8], d[8];
+      xv[0] = lo_bf(xvv[u].x); xv[1] = hi_bf(xvv[u].x); xv[2] = lo_bf(xvv[u].y); xv[3] = hi_bf(xvv[u].y);
+      xv[4] = lo_bf(xvv[u].z); xv[5] = hi_bf(xvv[u].z); xv[6] = lo_bf(xvv[u].w); xv[7] = hi_bf(xvv[u].w);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float g = fmaf(xv[e], sc[e], sh[e]) > 0.f ? acc[e] : 0.f;
+        d[e] = g * sc[e];
+        a1[e] += g * xv[e];
+        a0[e] += g;
+      }
+      st<8>(dx + (size_t)row * a.C + c0, d);
+    }
+  }
+  float* prow = part + (size_t)blockIdx.x * 2 * a.C;
+  col_reduce8(red, a1, a0, prow, prow + a.C, cols, c0);
+}
+
 }  // namespace dtm
 using namespace dtm;
 
@@ -246,4 +369,41 @@ DTM_API void dtm_global_avg_fwd(const void* x, float* y, int N, int HW, int C, v
 DTM_API void dtm_global_avg_bwd(const float* dy, void* dx, int N, int HW, int C, void* stream) {
   hipLaunchKernelGGL(global_avg_bwd_kernel, dim3(pgrid((long)N * HW * C)), dim3(256), 0, (hipStream_t)stream, dy,
                      (bf16_t*)dx, N, HW, C);
+}
+
+// y = maxpool(relu(x*scale + shift)) with a uint8 argmax per output element (ss = [scale; shift; ...])
+DTM_API int dtm_maxpool_bnrelu_fwd(const void* x, const float* ss, void* y, void* arg, const PoolArgs* a, void* stream) {
+  if (a->C % 8 || a->KH * a->KW > 255 || (long)a->N * a->H * a->W * a->C >= (1l << 31)) return -1;
+  const long work = (long)a->N * a->P * a->Q * (a->C / 8);
+  hipLaunchKernelGGL(maxpool_bnrelu_fwd_kernel, dim3(pgrid(work)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                     ss, (bf16_t*)y, (uint8_t*)arg, *a, make_fastdiv(a->C / 8), make_fastdiv(a->Q), make_fastdiv(a->P));
+  return 0;
+}
+
+// dx = [x*scale+shift > 0] * scale * maxpool_grad(dy);  sums[0..1][C] += (sum g*x, sum g)
+DTM_API int dtm_maxpool_bnrelu_bwd(const void* dy, const void* arg, const void* x, const float* ss, void* dx,
+                                   float* sums, const PoolArgs* a, void* stream) {
+  if (a->C % 8 || a->C / 8 > 256 || (long)a->N * a->H * a->W * a->C >= (1l << 31)) return -1;
+  if ((a->KH + a->SH - 1) / a->SH > 3 || (a->KW + a->SW - 1) / a->SW > 3) return -2;
+  const int cols = a->C / 8, RP = 256 / cols;
+  const long M = (long)a->N * a->H * a->W;
+  long b = M * cols / (256 * 8);
+  if (b < 1) b = 1;
+  if (b > 2048) b = 2048;
+  long rpb = (M + b - 1) / b;
+  rpb = (rpb + RP - 1) / RP * RP;
+  const int blocks = (int)((M + rpb - 1) / rpb);
+  float* ws = dtm_ws_get((size_t)blocks * 2 * a->C);
+  if (!ws) return -4;
+  const int wm = max((a->KH + a->SH - 1) / a->SH, (a->KW + a->SW - 1) / a->SW);
+  if (wm <= 2)
+    hipLaunchKernelGGL((maxpool_bnrelu_bwd_kernel<2, 2>), dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)dy, (const uint8_t*)arg, (const bf16_t*)x, ss, (bf16_t*)dx, ws, *a,
+                       make_fastdiv(a->W), make_fastdiv(a->H), (int)rpb);
+  else
+    hipLaunchKernelGGL((maxpool_bnrelu_bwd_kernel<3, 1>), dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)dy, (const uint8_t*)arg, (const bf16_t*)x, ss, (bf16_t*)dx, ws, *a,
+                       make_fastdiv(a->W), make_fastdiv(a->H), (int)rpb);
+  dtm_reduce_rows(ws, blocks, 2 * a->C, 2 * a->C, sums, (hipStream_t)stream);
+  return 0;
 }

@@ -14,7 +14,8 @@ resnet_v1_50/block1/unit_1/bottleneck_v1/{shortcut,conv1,conv2,conv3}/..., resne
 import torch
 
 from ..ops import nn as F
-from .layers import Conv2d, Layer, _join
+from ..ops.lazy import Subsampled, as_tensor
+from .layers import Conv2d, Layer, _join, fused_enabled
 
 
 def resnet_arg_scope(weight_decay=0.0001, batch_norm_decay=0.997, batch_norm_epsilon=1e-5, batch_norm_scale=True):
@@ -23,10 +24,14 @@ def resnet_arg_scope(weight_decay=0.0001, batch_norm_decay=0.997, batch_norm_eps
                                 bessel=True))
 
 
-def subsample(x, factor):
+def subsample(x, factor, lazy=False):
+    """1x1 max-pool with stride ``factor`` (resnet_utils.subsample).  ``lazy``: on the fused HIP path
+    return a ``Subsampled`` view that the unit's output BN-apply reads strided (never stored)."""
     if factor == 1:
         return x
-    return F.max_pool(x, 1, factor, "VALID")
+    if lazy and x.is_cuda and fused_enabled():
+        return Subsampled(x, factor)
+    return F.max_pool(as_tensor(x), 1, factor, "VALID")
 
 
 def conv2d_same_padding(kernel, stride, rate=1):
@@ -56,7 +61,8 @@ class BottleneckV1(Layer):
         self.conv3 = Conv2d(_join(scope, "conv3"), depth_bottleneck, depth, 1, 1, "SAME", None, bn, None, wd, init)
 
     def forward(self, x, training=True):
-        sc = self.shortcut(x, training) if self.shortcut is not None else subsample(x, self.stride)
+        sc = self.shortcut(x, training) if self.shortcut is not None else \
+            subsample(x, self.stride, lazy=self.conv3.bn is not None)
         r = self.conv1(x, training)
         r = self.conv2(r, training)
         return self.conv3(r, training, residual=sc, residual_act="relu")

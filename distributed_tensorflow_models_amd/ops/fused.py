@@ -15,7 +15,7 @@ import torch
 
 from . import _lib
 from .geometry import conv_geom
-from .lazy import LazyBN, as_tensor  # noqa: F401
+from .lazy import LazyBN, Subsampled, as_tensor  # noqa: F401
 from .nn import _accum_param_grad, _check, _notify, weight_bf16, weight_flipped
 
 
@@ -65,12 +65,16 @@ class _GradSlot:
     """Gradient hand-off for a tensor read by several fused ops (a ResNet block input feeds conv1
     and the shortcut).  Every consumer's backward but the last stashes its input-gradient here and
     returns None; the last one folds the stash into its own dgrad epilogue (``add_src``), so the
-    autograd engine never launches a separate add over the whole activation."""
-    __slots__ = ("pending", "buf")
+    autograd engine never launches a separate add over the whole activation.  A stash may be the
+    gradient of a stride-s subsample of the tensor (``stride`` > 1): the dgrad epilogue adds it at
+    the subsampled pixels."""
+    __slots__ = ("pending", "buf", "stride", "shape")
 
-    def __init__(self):
+    def __init__(self, shape):
         self.pending = 0
         self.buf = None
+        self.stride = 1
+        self.shape = tuple(shape)
 
 
 def _slot_register(x):
@@ -78,7 +82,7 @@ def _slot_register(x):
         return None
     s = getattr(x, "_dtm_slot", None)
     if s is None:
-        s = _GradSlot()
+        s = _GradSlot(x.shape)
         try:
             x._dtm_slot = s
         except Exception:
@@ -87,20 +91,34 @@ def _slot_register(x):
     return s
 
 
+def _unstride(slot, g, stride):
+    """Full-resolution gradient of x from the gradient of x[:, ::stride, ::stride]."""
+    if stride == 1:
+        return g
+    full = torch.zeros(slot.shape, device=g.device, dtype=g.dtype)
+    full[:, ::stride, ::stride, :] = g
+    return full
+
+
 def _slot_take(slot):
-    """-> (is_last_consumer, stashed_gradient_or_None)"""
+    """-> (is_last_consumer, stashed_gradient_or_None, its stride)"""
     if slot is None:
-        return True, None
+        return True, None, 1
     slot.pending -= 1
-    buf = slot.buf
+    buf, stride = slot.buf, slot.stride
     if slot.pending == 0:
-        slot.buf = None
-        return True, buf
-    return False, buf
+        slot.buf, slot.stride = None, 1
+        return True, buf, stride
+    return False, buf, stride
 
 
-def _slot_stash(slot, g):
-    slot.buf = g if slot.buf is None else slot.buf + g
+def _slot_stash(slot, g, stride=1):
+    if slot.buf is None:
+        slot.buf, slot.stride = g, stride
+    elif slot.stride == stride:
+        slot.buf = slot.buf + g
+    else:
+        slot.buf, slot.stride = _unstride(slot, slot.buf, slot.stride) + _unstride(slot, g, stride), 1
 
 
 # ---------------------------------------------------------------------------------------------
@@ -144,18 +162,20 @@ class _ConvBNFn(torch.autograd.Function):
         sh = in_ss[1] if in_ss is not None else None
         dx = d_in = None
         if ctx.needs_input_grad[0] or (in_ss is not None and ctx.needs_input_grad[1]):
-            last, add_src = _slot_take(ctx.slot)
+            last, add_src, add_stride = _slot_take(ctx.slot)
             wt = weight_flipped(w, g.K, g.R, g.S, g.C)
             dx = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
             if in_ss is not None:
                 # BN+ReLU of the input was fused into the forward prologue: mask, scale and the BN
                 # parameter-gradient sums are done in the dgrad epilogue
                 d_in = arena.zeros((4, g.C), dy.device)
-                _check(L.dtm_conv_dgrad_ex(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), None,
+                _check(L.dtm_conv_dgrad_ex(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), None, 1,
                                            _lib.ptr(x), _lib.ptr(in_ss), _lib.ptr(d_in), s), "conv_dgrad_act")
             else:
+                use_add = last and add_src is not None
                 _check(L.dtm_conv_dgrad_ex(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d),
-                                           _lib.ptr(add_src) if last else None, None, None, None, s), "conv_dgrad")
+                                           _lib.ptr(add_src) if use_add else None, add_stride if use_add else 1,
+                                           None, None, None, s), "conv_dgrad")
                 if not last:
                     _slot_stash(ctx.slot, dx)
                     dx = None
@@ -209,16 +229,24 @@ class _BNFinalizeFn(torch.autograd.Function):
 
 class _BNApplyFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, ss, res, res_ss, relu, res_slot=None):
+    def forward(ctx, x, ss, res, res_ss, relu, res_slot=None, res_stride=1):
         L = _lib.lib()
         C = x.shape[-1]
         M = x.numel() // C
         y = torch.empty_like(x)
         res_mode = 0 if res is None else (2 if res_ss is not None else 1)
-        L.dtm_bn_apply(_lib.ptr(x), _lib.ptr(ss), _lib.ptr(res), _lib.ptr(res_ss), _lib.ptr(y), M, C, res_mode,
-                       int(relu), _lib.stream_ptr())
-        ctx.relu, ctx.res_mode, ctx.res_slot = relu, res_mode, res_slot
-        ctx.save_for_backward(x, ss, res, res_ss, y if relu else None)
+        if res_stride > 1:
+            N, Ho, Wo, _ = x.shape
+            _check(L.dtm_bn_apply_res_strided(_lib.ptr(x), _lib.ptr(ss), _lib.ptr(res), _lib.ptr(y), N, Ho, Wo, C,
+                                              res.shape[1], res.shape[2], res_stride, int(relu), _lib.stream_ptr()),
+                   "bn_apply_res_strided")
+        else:
+            L.dtm_bn_apply(_lib.ptr(x), _lib.ptr(ss), _lib.ptr(res), _lib.ptr(res_ss), _lib.ptr(y), M, C, res_mode,
+                           int(relu), _lib.stream_ptr())
+        ctx.relu, ctx.res_mode, ctx.res_slot, ctx.res_stride = relu, res_mode, res_slot, res_stride
+        ctx.res_shape = None if res is None else tuple(res.shape)
+        # the residual itself is only read back for a BN'd residual (res_mode 2)
+        ctx.save_for_backward(x, ss, res if res_mode == 2 else None, res_ss, y if relu else None)
         return y
 
     @staticmethod
@@ -234,20 +262,35 @@ class _BNApplyFn(torch.autograd.Function):
         _check(L.dtm_bn_apply_bwd(_lib.ptr(dy.contiguous()), _lib.ptr(y), _lib.ptr(x), _lib.ptr(ss), _lib.ptr(res),
                                   _lib.ptr(rss), _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(sx), _lib.ptr(sr), M, C,
                                   1 if ctx.relu else 0, ctx.res_mode, _lib.stream_ptr()), "bn_apply_bwd")
+        st = ctx.res_stride
         if ctx.res_slot is not None:
-            last, buf = _slot_take(ctx.res_slot)
+            last, buf, bst = _slot_take(ctx.res_slot)
             if not last:
-                _slot_stash(ctx.res_slot, dres)
+                _slot_stash(ctx.res_slot, dres, st)
                 dres = None
-            elif buf is not None:
-                dres = dres + buf
-        return dx, sx, dres, sr, None, None
+            elif buf is not None or st > 1:
+                dres = _unstride(ctx.res_slot, dres, st)
+                if buf is not None:
+                    dres = dres + _unstride(ctx.res_slot, buf, bst)
+        elif st > 1:
+            full = torch.zeros(ctx.res_shape, device=dres.device, dtype=dres.dtype)
+            full[:, ::st, ::st, :] = dres
+            dres = full
+        return dx, sx, dres, sr, None, None, None
 
 
 def bn_apply(raw, ss, relu, residual=None):
-    """y = relu?(raw*scale+shift + residual); residual may be a tensor or a LazyBN (BN'd shortcut)."""
+    """y = relu?(raw*scale+shift + residual); residual may be a tensor, a LazyBN (BN'd shortcut) or a
+    Subsampled block input (strided identity shortcut)."""
     if residual is None:
         return _BNApplyFn.apply(raw, ss, None, None, bool(relu))
+    if isinstance(residual, Subsampled):
+        src = residual.src
+        if isinstance(src, LazyBN):
+            src = src.materialize()
+        res = src.to(torch.bfloat16).contiguous()
+        slot = _slot_register(res) if res is src else None
+        return _BNApplyFn.apply(raw, ss, res, None, bool(relu), slot, residual.stride)
     if isinstance(residual, LazyBN):
         if residual.relu:
             residual = residual.materialize()

@@ -34,5 +34,30 @@ class LazyBN:
         return bn_apply(self.raw, self.ss, relu, residual)
 
 
+class Subsampled:
+    """x[:, ::s, ::s, :] (slim resnet_v1 ``subsample`` = 1x1 max-pool with stride s) kept as (src, s):
+    as a block's identity residual it is read strided by the output BN-apply and its gradient is added
+    strided in the other consumer's dgrad epilogue, so the subsampled tensor and its gradient are
+    never stored."""
+
+    __slots__ = ("src", "stride")
+
+    def __init__(self, src, stride):
+        self.src, self.stride = src, stride
+
+    @property
+    def shape(self):
+        n, h, w, c = self.src.shape
+        return (n, (h - 1) // self.stride + 1, (w - 1) // self.stride + 1, c)
+
+    @property
+    def is_cuda(self):
+        return self.src.is_cuda
+
+    def materialize(self):
+        from . import nn as F
+        return F.max_pool(self.src, 1, self.stride, "VALID")
+
+
 def as_tensor(x):
-    return x.materialize() if isinstance(x, LazyBN) else x
+    return x.materialize() if isinstance(x, (LazyBN, Subsampled)) else x

@@ -16,7 +16,7 @@ import torch
 from . import _lib
 from . import reference as ref
 from .geometry import conv_geom, pool_geom
-from .lazy import as_tensor
+from .lazy import LazyBN, as_tensor
 
 _grad_ready_hooks = []
 
@@ -398,7 +398,43 @@ class _MaxPoolFn(torch.autograd.Function):
         return dx, None
 
 
+class _MaxPoolBNReluFn(torch.autograd.Function):
+    """maxpool(relu(raw*scale + shift)) without storing the normalised activation (the ResNet stem's
+    BN -> ReLU -> max pool); backward returns the raw-input gradient and the [4, C] scale/shift sums."""
+
+    @staticmethod
+    def forward(ctx, raw, ss, g):
+        L = _lib.lib()
+        y = torch.empty((g.N, g.P, g.Q, g.C), device=raw.device, dtype=torch.bfloat16)
+        arg = torch.empty((g.N, g.P, g.Q, g.C), device=raw.device, dtype=torch.uint8)
+        a = g.as_args(_lib.PoolArgs)
+        _check(L.dtm_maxpool_bnrelu_fwd(_lib.ptr(raw), _lib.ptr(ss), _lib.ptr(y), _lib.ptr(arg), ctypes.byref(a),
+                                        _lib.stream_ptr()), "maxpool_bnrelu_fwd")
+        ctx.g = g
+        ctx.save_for_backward(raw, ss, arg)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .fused import arena
+        L = _lib.lib()
+        raw, ss, arg = ctx.saved_tensors
+        g = ctx.g
+        dx = torch.empty_like(raw)
+        sums = arena.zeros((4, g.C), raw.device)
+        a = g.as_args(_lib.PoolArgs)
+        _check(L.dtm_maxpool_bnrelu_bwd(_lib.ptr(dy.contiguous()), _lib.ptr(arg), _lib.ptr(raw), _lib.ptr(ss),
+                                        _lib.ptr(dx), _lib.ptr(sums), ctypes.byref(a), _lib.stream_ptr()),
+               "maxpool_bnrelu_bwd")
+        return dx, sums, None
+
+
 def max_pool(x, kernel, stride, padding="VALID"):
+    if isinstance(x, LazyBN) and x.relu and x.raw.is_cuda and x.raw.dtype == torch.bfloat16 \
+            and x.raw.shape[-1] % 8 == 0 and x.raw.is_contiguous():
+        g = pool_geom(tuple(x.raw.shape), kernel, stride, padding)
+        if g.KH * g.KW <= 255 and -(-g.KH // g.SH) <= 3 and -(-g.KW // g.SW) <= 3:
+            return _MaxPoolBNReluFn.apply(x.raw, x.ss.contiguous(), g)
     x = as_tensor(x)
     if not x.is_cuda:
         return ref.max_pool(x, kernel, stride, padding)
