@@ -505,6 +505,91 @@ static void fast_grid(long M, int C, int* blocks, int* rpb) {
   *rpb = (int)r;
   *blocks = (int)((M + r - 1) / r);
 }
+// ---- statistics reduction + finalize in one launch -------------------------------------------
+// Partial rows ws[rows][2K] (sum | sumsq per producer tile) are summed column-wise by a 2-D grid into
+// a self-cleaning fp32 accumulator with memory-side atomics; the last block to finish (counter) reads
+// the totals back with atomic exchanges (which also re-zero the accumulator), and writes
+// ss = [scale; shift; mean; rstd] and the moving averages -- the finalize of bn_finalize_kernel
+// without a separate launch.  Correctness of the hand-off: each block's atomics complete (s_waitcnt in
+// the issuing wave) before its counter increment, and the totals are read with memory-side atomics
+// (never a stale L2 line of another XCD).
+__global__ __launch_bounds__(256) void stats_reduce_finalize_kernel(
+    const float* __restrict__ ws, int rows, int K, int rpb, float* acc, unsigned* counter,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ mov_mean,
+    float* __restrict__ mov_var, float* __restrict__ out, float count, float eps, float decay, int update, int bessel) {
+  __shared__ float4 red[16][16];
+  __shared__ int is_last;
+  const int width = 2 * K;
+  const int cg = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int col = (blockIdx.x * 16 + cg) * 4;
+  const int r0 = blockIdx.y * rpb, r1 = min(rows, r0 + rpb);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col < width) {
+    int r = r0 + rl;
+    for (; r + 48 < r1; r += 64) {
+      float4 a = *(const float4*)(ws + (size_t)r * width + col);
+      float4 b = *(const float4*)(ws + (size_t)(r + 16) * width + col);
+      float4 c = *(const float4*)(ws + (size_t)(r + 32) * width + col);
+      float4 d = *(const float4*)(ws + (size_t)(r + 48) * width + col);
+      s.x += (a.x + b.x) + (c.x + d.x); s.y += (a.y + b.y) + (c.y + d.y);
+      s.z += (a.z + b.z) + (c.z + d.z); s.w += (a.w + b.w) + (c.w + d.w);
+    }
+    for (; r < r1; r += 16) {
+      float4 a = *(const float4*)(ws + (size_t)r * width + col);
+      s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+    }
+  }
+  red[rl][cg] = s;
+  __syncthreads();
+  if (rl == 0 && col < width) {
+    float4 t = red[0][cg];
+    for (int i = 1; i < 16; ++i) { float4 u = red[i][cg]; t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w; }
+    atomicAdd(acc + col, t.x); atomicAdd(acc + col + 1, t.y);
+    atomicAdd(acc + col + 2, t.z); atomicAdd(acc + col + 3, t.w);
+  }
+  // The partial-total atomics above are issued by wave 0 (rl == 0 <=> threadIdx.x < 16), the same wave
+  // that bumps the counter: waiting for its memory counters to drain orders them before the bump
+  // without an L2 write-back fence (all traffic here is memory-side atomics).
+  static_assert(16 <= 64, "partial-total atomics must come from wave 0");
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned nblk = gridDim.x * gridDim.y;
+    is_last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1;
+  }
+  __syncthreads();
+  if (!is_last) return;
+  for (int cb = 0; cb < K; cb += 2048) {
+    // all totals of this chunk are fetched (and re-zeroed) before any is used: 16 atomics in flight
+    float sv[8], qv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = cb + i * 256 + threadIdx.x;
+      sv[i] = c < K ? atomicExch(acc + c, 0.f) : 0.f;
+      qv[i] = c < K ? atomicExch(acc + K + c, 0.f) : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+    const int c = cb + i * 256 + threadIdx.x;
+    if (c >= K) break;
+    const float sum = sv[i], sq = qv[i];
+    const float mean = sum / count;
+    const float var = fmaxf(sq / count - mean * mean, 0.f);
+    const float rstd = rsqrtf(var + eps);
+    const float sc = (gamma ? gamma[c] : 1.f) * rstd;
+    out[c] = sc;
+    out[K + c] = (beta ? beta[c] : 0.f) - mean * sc;
+    out[2 * K + c] = mean;
+    out[3 * K + c] = rstd;
+    if (update) {
+      const float uvar = (bessel && count > 1.f) ? var * count / (count - 1.f) : var;
+      mov_mean[c] -= (mov_mean[c] - mean) * (1.f - decay);
+      mov_var[c] -= (mov_var[c] - uvar) * (1.f - decay);
+    }
+    }
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace dtm
 using namespace dtm;
 
@@ -620,4 +705,31 @@ DTM_API void dtm_bn_bwd_apply(const void* dy, const void* x, const void* ymask, 
 DTM_API void dtm_bn_param_grad(const float* sums, float* dgamma, float* dbeta, int C, void* stream) {
   hipLaunchKernelGGL(bn_param_grad_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, sums, dgamma,
                      dbeta, C);
+}
+
+// self-cleaning accumulator + completion counter for stats_reduce_finalize (stream-ordered use)
+static float* g_fin_acc = nullptr;
+static unsigned* g_fin_counter = nullptr;
+static int g_fin_k = 0;
+
+// ss[4][K] (+ moving averages) from the partial statistics rows ws[rows][2K], one launch.
+int dtm_bn_stats_finalize(const float* ws, int rows, int K, const float* gamma, const float* beta, float* mov_mean,
+                          float* mov_var, float* ss, float count, float eps, float decay, int update, int bessel,
+                          hipStream_t st) {
+  if (K > g_fin_k) {
+    hipDeviceSynchronize();
+    if (g_fin_acc) hipFree(g_fin_acc);
+    if (!g_fin_counter && hipMalloc(&g_fin_counter, 64) != hipSuccess) return -4;
+    if (hipMalloc(&g_fin_acc, (size_t)2 * K * sizeof(float)) != hipSuccess) { g_fin_acc = nullptr; g_fin_k = 0; return -4; }
+    hipMemset(g_fin_acc, 0, (size_t)2 * K * sizeof(float));
+    hipMemset(g_fin_counter, 0, 64);
+    hipDeviceSynchronize();
+    g_fin_k = K;
+  }
+  if (K % 2) return -1;  // float4 columns over [2K]
+  const int rpb = 256;
+  const int ychunks = (rows + rpb - 1) / rpb;
+  hipLaunchKernelGGL(stats_reduce_finalize_kernel, dim3((2 * K + 63) / 64, ychunks), dim3(256), 0, st, ws, rows, K, rpb,
+                     g_fin_acc, g_fin_counter, gamma, beta, mov_mean, mov_var, ss, count, eps, decay, update, bessel);
+  return 0;
 }

@@ -701,13 +701,13 @@ static void dispatch_nt(const ConvNTArgs& a, int ud, const TileCfg& t, hipStream
   else dispatch_ud<2>(a, t, st);
 }
 
-DTM_API int dtm_conv_fwd(const void* x, const void* w, void* y, float* stats, const float* bias,
-                         const float* in_scale, const float* in_shift, int relu,
-                         const ConvDesc* d, void* stream) {
+static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, const float* bias, const float* in_scale,
+                         const float* in_shift, int relu, const ConvDesc* d, hipStream_t stream, float** rows_ws,
+                         int* nrows) {
   if (d->C % 8 || d->K % 4) return -1;
   ConvNTArgs a;
   a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.y = (bf16_t*)y;
-  a.stats = stats; a.bias = bias; a.in_scale = in_scale; a.in_shift = in_shift;
+  a.stats = nullptr; a.bias = bias; a.in_scale = in_scale; a.in_shift = in_shift;
   a.add_src = nullptr; a.act_x = nullptr; a.act_ss = nullptr; a.act_sums = nullptr;
   a.add_stride = 1; a.add_H = a.add_W = 0;
   size_t xb = (size_t)d->N * d->H * d->W * d->C * 2, wb = (size_t)d->K * d->R * d->S * d->C * 2;
@@ -726,9 +726,36 @@ DTM_API int dtm_conv_fwd(const void* x, const void* w, void* y, float* stats, co
     if (!ws) return -4;
     a.stats = ws;
   }
-  dispatch_nt(a, 1, tc, (hipStream_t)stream);
-  if (stats) dtm_reduce_rows(a.stats, rows, 2 * d->K, 2 * d->K, stats, (hipStream_t)stream);
+  dispatch_nt(a, 1, tc, stream);
+  *rows_ws = a.stats;
+  *nrows = rows;
   return 0;
+}
+
+DTM_API int dtm_conv_fwd(const void* x, const void* w, void* y, float* stats, const float* bias,
+                         const float* in_scale, const float* in_shift, int relu,
+                         const ConvDesc* d, void* stream) {
+  float* ws = nullptr;
+  int rows = 0;
+  int rc = conv_fwd_impl(x, w, y, stats != nullptr, bias, in_scale, in_shift, relu, d, (hipStream_t)stream, &ws, &rows);
+  if (rc) return rc;
+  if (stats) dtm_reduce_rows(ws, rows, 2 * d->K, 2 * d->K, stats, (hipStream_t)stream);
+  return 0;
+}
+
+// Training conv -> BatchNorm statistics -> finalize in two launches: the conv (statistics partial
+// rows from its epilogue) and stats_reduce_finalize, which writes ss = [scale; shift; mean; rstd] and
+// updates the moving averages (see batchnorm.hip).
+DTM_API int dtm_conv_fwd_bn(const void* x, const void* w, void* y, const float* in_scale, const float* in_shift,
+                            const float* gamma, const float* beta, float* mov_mean, float* mov_var, float* ss,
+                            float count, float eps, float decay, int update, int bessel, const ConvDesc* d,
+                            void* stream) {
+  float* ws = nullptr;
+  int rows = 0;
+  int rc = conv_fwd_impl(x, w, y, true, nullptr, in_scale, in_shift, 0, d, (hipStream_t)stream, &ws, &rows);
+  if (rc) return rc;
+  return dtm_bn_stats_finalize(ws, rows, d->K, gamma, beta, mov_mean, mov_var, ss, count, eps, decay, update, bessel,
+                               (hipStream_t)stream);
 }
 
 // dgrad: dx[N][H][W][C] from dy[N][P][Q][K] and the flipped/transposed weight wt[C][R][S][K].

@@ -126,6 +126,69 @@ __global__ __launch_bounds__(256) void stats_combine_kernel(const bf16_t* __rest
   }
 }
 
+// stats_combine with the finalize backward folded in: the per-channel (dsum, dsumsq) are computed
+// from dss = [dscale; dshift; dmean; drstd], ss = [scale; shift; mean; rstd] and gamma in registers
+// (bn_finalize_bwd_kernel's algebra), and block 0 accumulates dgamma / dbeta.
+__device__ __forceinline__ void fin_bwd_channel(const float* dss, const float* ss, const float* gamma, int C, int c,
+                                                float count, float* ds, float* dq, float* dg, float* db) {
+  const float scale = ss[c], mean = ss[2 * C + c], rstd = ss[3 * C + c];
+  const float g = gamma ? gamma[c] : 1.f;
+  const float dsc = dss[c], dsh = dss[C + c];
+  const float dscale_tot = dsc - dsh * mean;
+  const float dmean = dss[2 * C + c] - dsh * scale;
+  const float drstd = dss[3 * C + c] + dscale_tot * g;
+  const float dvar = drstd * (-0.5f) * rstd * rstd * rstd;
+  *ds = dmean / count - dvar * 2.f * mean / count;
+  *dq = dvar / count;
+  *dg = dscale_tot * rstd;
+  *db = dsh;
+}
+
+__global__ __launch_bounds__(256) void stats_combine_fin_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                                const float* __restrict__ dss, const float* __restrict__ ss,
+                                                                const float* __restrict__ gamma, float count,
+                                                                float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                                bf16_t* __restrict__ out, int M, int C, int rpb) {
+  __shared__ float s_ab[2][2048];
+  const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t % cols) * 8, lr0 = t / cols;
+  for (int c = t; c < C; c += 256) {  // one channel per thread, shared through LDS
+    float ds, dq, dg, db;
+    fin_bwd_channel(dss, ss, gamma, C, c, count, &ds, &dq, &dg, &db);
+    s_ab[0][c] = ds;
+    s_ab[1][c] = 2.f * dq;
+    if (blockIdx.x == 0) {
+      if (dgamma) dgamma[c] += dg;
+      if (dbeta) dbeta[c] += db;
+    }
+  }
+  __syncthreads();
+  float a[8], b[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { a[e] = s_ab[0][c0 + e]; b[e] = s_ab[1][c0 + e]; }
+  const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
+  for (int row = lr0 < RP ? r0 + lr0 : r1; row < r1; row += RP * FU2) {
+    uint4 vd[FU2], vx[FU2];
+#pragma unroll
+    for (int u = 0; u < FU2; ++u) {
+      int rr = row + u * RP;
+      bool ok = rr < r1;
+      size_t o = (size_t)rr * C + c0;
+      vd[u] = ok ? *(const uint4*)(dy + o) : make_uint4(0, 0, 0, 0);
+      vx[u] = ok ? *(const uint4*)(x + o) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < FU2; ++u) {
+      int rr = row + u * RP;
+      if (rr >= r1) break;
+      float d[8], xv[8];
+      up8(vd[u], d); up8(vx[u], xv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] += a[e] + b[e] * xv[e];
+      *(uint4*)(out + (size_t)rr * C + c0) = pk8(d);
+    }
+  }
+}
+
 // finalize backward: dss [4][C] (dscale, dshift, dmean, drstd) -> dstats [2][C], dgamma, dbeta
 // ss holds the forward's [scale, shift, mean, rstd].
 __global__ void bn_finalize_bwd_kernel(const float* __restrict__ dss, const float* __restrict__ ss,
@@ -199,4 +262,14 @@ DTM_API void dtm_bn_finalize_bwd(const float* dss, const float* ss, const float*
                                  float* dbeta, int C, float count, void* stream) {
   hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, dss, ss, gamma,
                      dstats, dgamma, dbeta, C, count);
+}
+
+DTM_API int dtm_stats_combine_fin(const void* dy, const void* x, const float* dss, const float* ss, const float* gamma,
+                                  float count, float* dgamma, float* dbeta, void* out, long M, int C, void* stream) {
+  if (!shape_ok(M, C) || C > 2048) return -1;
+  int blocks, rpb;
+  grid2(M, C, &blocks, &rpb);
+  hipLaunchKernelGGL(stats_combine_fin_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
+                     (const bf16_t*)x, dss, ss, gamma, count, dgamma, dbeta, (bf16_t*)out, (int)M, C, rpb);
+  return 0;
 }

@@ -45,6 +45,8 @@ _SIGS = {
     "dtm_bn_apply": (None, [_P, _P, _P, _P, _P, _L, _I, _I, _I, _P]),
     "dtm_maxpool_bnrelu_fwd": (_I, [_P, _P, _P, _P, ctypes.POINTER(PoolArgs), _P]),
     "dtm_maxpool_bnrelu_bwd": (_I, [_P, _P, _P, _P, _P, _P, ctypes.POINTER(PoolArgs), _P]),
+    "dtm_conv_fwd_bn": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _I, _I, ctypes.POINTER(ConvDesc), _P]),
+    "dtm_stats_combine_fin": (_I, [_P, _P, _P, _P, _P, _F, _P, _P, _P, _L, _I, _P]),
     "dtm_bn_apply_res_strided": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "dtm_bn_bwd_reduce": (None, [_P, _P, _P, _P, _P, _L, _I, _I, _P]),
     "dtm_bn_bwd_apply": (None, [_P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _P]),

@@ -2,7 +2,8 @@
 
 A BatchNorm that follows a conv is split into:
   * statistics  - accumulated in the producing conv's epilogue (``_ConvBNFn``),
-  * finalize    - per-channel scale/shift (+ moving averages) (``_BNFinalizeFn``),
+  * finalize    - per-channel scale/shift (+ moving averages), fused into the statistics reduction
+                  (``_ConvBNFn``; ``_BNFinalizeFn`` is the standalone form),
   * apply       - either folded into the NEXT conv's operand prologue (the normalised activation is
                   never written to HBM: ``LazyBN`` consumed by ``conv_bn``), or materialised once by
                   ``_BNApplyFn`` (block outputs, residual add, pool inputs).
@@ -123,39 +124,66 @@ def _slot_stash(slot, g, stride=1):
 
 # ---------------------------------------------------------------------------------------------
 class _ConvBNFn(torch.autograd.Function):
-    """y_raw, stats = conv(relu(x_raw*in_scale+in_shift) or x_raw, w); stats = (Σy, Σy²) per channel."""
+    """Training: (y_raw, ss) = conv(relu(x_raw*in_scale+in_shift) or x_raw, w) with the BatchNorm
+    statistics from the conv epilogue and the finalize (ss = [scale; shift; mean; rstd], moving averages)
+    fused into the statistics reduction.  Inference (bn=None): y_raw only.
+    Backward: the finalize backward is folded into the stats-combine pass (dgamma / dbeta included)."""
 
     @staticmethod
-    def forward(ctx, x, in_ss, w, geom, want_stats, slot=None):
+    def forward(ctx, x, in_ss, w, gamma, beta, geom, bn, slot=None):
         L = _lib.lib()
         s = _lib.stream_ptr()
         w16 = weight_bf16(w)
         y = torch.empty((geom.N, geom.P, geom.Q, geom.K), device=x.device, dtype=torch.bfloat16)
-        stats = arena.zeros((2, geom.K), x.device) if want_stats else None
         d = geom.as_desc(_lib.ConvDesc)
         sc = in_ss[0] if in_ss is not None else None
         sh = in_ss[1] if in_ss is not None else None
-        _check(L.dtm_conv_fwd(_lib.ptr(x), _lib.ptr(w16), _lib.ptr(y), _lib.ptr(stats), None, _lib.ptr(sc),
-                              _lib.ptr(sh), 0, ctypes.byref(d), s), "conv_fwd")
+        ss = None
+        if bn is not None:
+            ss = torch.empty((4, geom.K), device=x.device, dtype=torch.float32)
+            count = float(geom.N * geom.P * geom.Q)
+            _check(L.dtm_conv_fwd_bn(_lib.ptr(x), _lib.ptr(w16), _lib.ptr(y), _lib.ptr(sc), _lib.ptr(sh),
+                                     _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(bn.moving_mean),
+                                     _lib.ptr(bn.moving_variance), _lib.ptr(ss), count, float(bn.eps),
+                                     float(bn.decay), 1, int(bn.bessel), ctypes.byref(d), s), "conv_fwd_bn")
+            ctx.count = count
+        else:
+            _check(L.dtm_conv_fwd(_lib.ptr(x), _lib.ptr(w16), _lib.ptr(y), None, None, _lib.ptr(sc), _lib.ptr(sh), 0,
+                                  ctypes.byref(d), s), "conv_fwd")
         ctx.geom = geom
         ctx.slot = slot
-        ctx.save_for_backward(x, in_ss, w, y)
-        if stats is None:
+        ctx.has_gamma, ctx.has_beta = gamma is not None, beta is not None
+        ctx.save_for_backward(x, in_ss, w, y, ss, gamma, beta)
+        if ss is None:
             return y
-        return y, stats
+        return y, ss
 
     @staticmethod
-    def backward(ctx, dy, dstats=None):
+    def backward(ctx, dy, dss=None):
         L = _lib.lib()
         s = _lib.stream_ptr()
-        x, in_ss, w, y = ctx.saved_tensors
+        x, in_ss, w, y, ss, gamma, beta = ctx.saved_tensors
         g = ctx.geom
         M_out = g.N * g.P * g.Q
         dy = dy.contiguous()
-        if dstats is not None:
+        dgamma = dbeta = None
+        if ss is not None and dss is not None:
+            gmg = getattr(gamma, "main_grad", None) if gamma is not None else None
+            bmg = getattr(beta, "main_grad", None) if beta is not None else None
+            if gamma is not None and gmg is None:
+                dgamma = torch.zeros(g.K, device=dy.device)
+            if beta is not None and bmg is None:
+                dbeta = torch.zeros(g.K, device=dy.device)
             comb = torch.empty_like(dy)
-            _check(L.dtm_stats_combine(_lib.ptr(dy), _lib.ptr(y), _lib.ptr(dstats.contiguous()), _lib.ptr(comb),
-                                       M_out, g.K, s), "stats_combine")
+            _check(L.dtm_stats_combine_fin(_lib.ptr(dy), _lib.ptr(y), _lib.ptr(dss.contiguous()), _lib.ptr(ss),
+                                           _lib.ptr(gamma), ctx.count,
+                                           _lib.ptr(gmg if gmg is not None else dgamma),
+                                           _lib.ptr(bmg if bmg is not None else dbeta), _lib.ptr(comb), M_out, g.K, s),
+                   "stats_combine_fin")
+            if gmg is not None:
+                _notify(gamma)
+            if bmg is not None:
+                _notify(beta)
             dy = comb
         d = g.as_desc(_lib.ConvDesc)
         sc = in_ss[0] if in_ss is not None else None
@@ -191,7 +219,7 @@ class _ConvBNFn(torch.autograd.Function):
                 dw = target
         else:
             dw = None
-        return dx, d_in, dw, None, None, None
+        return dx, d_in, dw, dgamma, dbeta, None, None, None
 
 
 class _BNFinalizeFn(torch.autograd.Function):
@@ -331,10 +359,8 @@ def conv_bn(x, w, bn, stride, padding, training, relu):
     slot = _slot_register(xb) if (xb is x and in_ss is None) else None
     x = xb
     if training:
-        y, stats = _ConvBNFn.apply(x, in_ss, w, g, True, slot)
-        ss = _BNFinalizeFn.apply(stats, bn.gamma, bn.beta, bn.moving_mean, bn.moving_variance,
-                                 float(g.N * g.P * g.Q), bn.eps, bn.decay, bn.bessel, True)
+        y, ss = _ConvBNFn.apply(x, in_ss, w, bn.gamma, bn.beta, g, bn, slot)
     else:
-        y = _ConvBNFn.apply(x, in_ss, w, g, False, slot)
+        y = _ConvBNFn.apply(x, in_ss, w, None, None, g, None, slot)
         ss = bn_inference_ss(bn)
     return LazyBN(y, ss, relu)
