@@ -58,7 +58,160 @@ struct ConvNTArgs {
   const bf16_t* act_x;    // fused activation backward of the input's BatchNorm+ReLU prologue:
   const float* act_ss;    //   g = out * [act_x*scale + shift > 0]; out <- g*scale;
   float* act_sums;        //   partial rows per pixel tile: [sum g*act_x (K) | sum g (K)]
+  const bf16_t* zero;     // >= 16 B of zeros: the LDS-DMA source of padding / out-of-range chunks
 };
+
+// Shared epilogue of the conv_nt kernels (register-staged and LDS-DMA): acc[TC][TP] of wave (wp, wc)
+// for the tile at pixel p0 / channel c0; smem must hold PT * (2*CT + 16) bytes and be free.
+template <int PT, int CT, int WP, int WC>
+__device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&acc)[WC / 16][WP / 16], char* smem,
+                                                 int p0, int c0, int by) {
+  constexpr int NWP = PT / WP;
+  constexpr int TP = WP / 16, TC = WC / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wp = wave % NWP, wc = wave / NWP;
+  const int fr = lane & 15, fk = lane >> 4;
+  // epilogue: lane holds channels (fk*4 .. +3) of pixel fr for every subtile.  Bias/ReLU and the
+  // BatchNorm statistics (from the bf16-rounded outputs) are done in registers; the tile is then
+  // staged through LDS (padded rows: conflict-free 8-B lane writes) so that every global store is a
+  // full 16-B chunk and consecutive lanes cover whole NHWC pixel rows (coalesced, 256-B rows for
+  // CT = 128) instead of 16 scattered 32-B pieces per wave instruction.
+  constexpr int OROW = CT * 2 + 16;
+  const bool staged = (a.K & 7) == 0;
+#pragma unroll
+  for (int i = 0; i < TC; ++i) {
+    const int kloc = wc * WC + i * 16 + fk * 4;
+    const int kch = c0 + kloc;
+    float bsum[4] = {0.f, 0.f, 0.f, 0.f}, bsq[4] = {0.f, 0.f, 0.f, 0.f};
+    float bia[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.bias && kch < a.K) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bia[r] = a.bias[kch + r];
+    }
+#pragma unroll
+    for (int j = 0; j < TP; ++j) {
+      const int mloc = wp * WP + j * 16 + fr;
+      const int m = p0 + mloc;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = acc[i][j][r] + bia[r];
+        if (a.relu) v[r] = fmaxf(v[r], 0.f);
+      }
+      uint32_t lo = pack2bf(v[0], v[1]), hi = pack2bf(v[2], v[3]);
+      if (staged) {
+        *(uint2*)(smem + mloc * OROW + kloc * 2) = make_uint2(lo, hi);
+      } else if (m < a.M && kch < a.K) {
+        *(uint2*)(a.y + (size_t)m * a.K + kch) = make_uint2(lo, hi);
+      }
+      if (a.stats && m < a.M && kch < a.K) {
+        float q0 = lo_bf(lo), q1 = hi_bf(lo), q2 = lo_bf(hi), q3 = hi_bf(hi);
+        bsum[0] += q0; bsq[0] += q0 * q0;
+        bsum[1] += q1; bsq[1] += q1 * q1;
+        bsum[2] += q2; bsq[2] += q2 * q2;
+        bsum[3] += q3; bsq[3] += q3 * q3;
+      }
+    }
+    if (a.stats) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          bsum[r] += __shfl_xor(bsum[r], o, 64);
+          bsq[r] += __shfl_xor(bsq[r], o, 64);
+        }
+      }
+      // one partial row per (pixel tile, pixel wave): [sum(K) | sumsq(K)], reduced by reduce_rows
+      if (fr == 0 && kch < a.K) {
+        float* row = a.stats + (size_t)(by * NWP + wp) * (2 * a.K);
+        *(float4*)(row + kch) = make_float4(bsum[0], bsum[1], bsum[2], bsum[3]);
+        *(float4*)(row + a.K + kch) = make_float4(bsq[0], bsq[1], bsq[2], bsq[3]);
+      }
+    }
+  }
+  if (staged) {
+    __syncthreads();
+    constexpr int CPR = CT / 8;  // 16-B chunks per pixel row of the tile
+    constexpr int NIT = PT * CPR / 256;
+    const int chn = tid % CPR;   // fixed per thread (256 % CPR == 0)
+    const int kc = c0 + chn * 8;
+    const bool act = a.act_x != nullptr;
+    float sc[8], sh[8], sgx[8], sg[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sc[e] = 1.f; sh[e] = 0.f; sgx[e] = 0.f; sg[e] = 0.f; }
+    if (act && kc < a.K) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { sc[e] = a.act_ss[kc + e]; sh[e] = a.act_ss[a.K + kc + e]; }
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int idx = it * 256 + tid;
+      const int row = idx / CPR;
+      const int m = p0 + row;
+      if (m < a.M && kc < a.K) {
+        uint4 v = *(const uint4*)(smem + row * OROW + chn * 16);
+        const size_t o = (size_t)m * a.K + kc;
+        if (a.add_src || act) {
+          float f[8];
+          f[0] = lo_bf(v.x); f[1] = hi_bf(v.x); f[2] = lo_bf(v.y); f[3] = hi_bf(v.y);
+          f[4] = lo_bf(v.z); f[5] = hi_bf(v.z); f[6] = lo_bf(v.w); f[7] = hi_bf(v.w);
+          if (a.add_src) {
+            const bf16_t* src = a.add_src + o;
+            if (a.add_stride > 1) {
+              const uint32_t n = fdiv((uint32_t)m, a.fd_PQ), rem = m - n * (a.P * a.Q);
+              const uint32_t h = fdiv(rem, a.fd_Q), w = rem - h * a.Q;
+              const int s = a.add_stride;
+              src = (h % s == 0 && w % s == 0)
+                        ? a.add_src + ((size_t)((int)n * a.add_H + (int)h / s) * a.add_W + (int)w / s) * a.K + kc
+                        : nullptr;
+            }
+            if (src) {
+              const uint4 r = *(const uint4*)src;
+              f[0] += lo_bf(r.x); f[1] += hi_bf(r.x); f[2] += lo_bf(r.y); f[3] += hi_bf(r.y);
+              f[4] += lo_bf(r.z); f[5] += hi_bf(r.z); f[6] += lo_bf(r.w); f[7] += hi_bf(r.w);
+            }
+          }
+          if (act) {
+            const uint4 xu = *(const uint4*)(a.act_x + o);
+            float xv[8];
+            xv[0] = lo_bf(xu.x); xv[1] = hi_bf(xu.x); xv[2] = lo_bf(xu.y); xv[3] = hi_bf(xu.y);
+            xv[4] = lo_bf(xu.z); xv[5] = hi_bf(xu.z); xv[6] = lo_bf(xu.w); xv[7] = hi_bf(xu.w);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float g = fmaf(xv[e], sc[e], sh[e]) > 0.f ? f[e] : 0.f;
+              sgx[e] += g * xv[e];
+              sg[e] += g;
+              f[e] = g * sc[e];
+            }
+          }
+          v = make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
+        }
+        *(uint4*)(a.y + o) = v;
+      }
+    }
+    if (act) {
+      // reduce the per-thread partial sums over the threads sharing this chunk column, one partial
+      // row per pixel tile (reduced over tiles by dtm_reduce_rows)
+      __syncthreads();
+      float* red = (float*)smem;  // [256][16]
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { red[tid * 16 + e] = sgx[e]; red[tid * 16 + 8 + e] = sg[e]; }
+      __syncthreads();
+      if (tid < CPR && kc < a.K) {
+        float tx[8], tg[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { tx[e] = 0.f; tg[e] = 0.f; }
+        for (int t = tid; t < 256; t += CPR) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { tx[e] += red[t * 16 + e]; tg[e] += red[t * 16 + 8 + e]; }
+        }
+        float* prow = a.act_sums + (size_t)by * (2 * a.K);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { prow[kc + e] = tx[e]; prow[a.K + kc + e] = tg[e]; }
+      }
+    }
+  }
+}
 
 template <int PT, int CT, int WP, int WC, int UD, int NBUF>
 __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
@@ -248,147 +401,137 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
     }
   }
 
-  // epilogue: lane holds channels (fk*4 .. +3) of pixel fr for every subtile.  Bias/ReLU and the
-  // BatchNorm statistics (from the bf16-rounded outputs) are done in registers; the tile is then
-  // staged through LDS (padded rows: conflict-free 8-B lane writes) so that every global store is a
-  // full 16-B chunk and consecutive lanes cover whole NHWC pixel rows (coalesced, 256-B rows for
-  // CT = 128) instead of 16 scattered 32-B pieces per wave instruction.
+  static_assert(PT * (CT * 2 + 16) <= NBUF * BUF, "output staging fits in the operand buffers");
+  conv_nt_epilogue<PT, CT, WP, WC>(a, acc, smem, p0, c0, by);
+}
+
+
+// LDS-DMA variant (no input prologue): both operand tiles go global -> LDS with
+// global_load_lds_dwordx4 (no VGPR round trip, no ds_write pass).  One wave-instruction writes 1 KiB
+// = 8 rows x 128 B contiguously (lane i at +16 i), so the XOR swizzle of the LDS image (chunk ^ row&7)
+// is applied on the SOURCE side: lane i loads logical chunk (i&7) ^ (i>>3) of row i>>3 of its group,
+// a chunk index that is fixed per lane for every group and k-tile.  Padding / out-of-range chunks
+// are loaded from a zero buffer.  Two LDS buffers; the DMA of k-tile t+1 is in flight during the
+// MFMAs of tile t; one barrier per k-tile (each wave drains its own DMA, vmcnt(0), before it).
+// Measured (tools/conv_microbench.py, DTM_CONV_TILE=10..12): 5-10 % faster than the register-staged
+// kernel on isolated deep-reduction layers, neutral inside the ResNet-50 step -> opt-in only.
+template <int PT, int CT, int WP, int WC, int UD>
+__global__ __launch_bounds__(256) void conv_nt_dma_kernel(ConvNTArgs a) {
+  constexpr int BK = 64;
+  constexpr int NWP = PT / WP;
+  constexpr int NWC = CT / WC;
+  static_assert(NWP * NWC == 4, "4 waves");
+  constexpr int TP = WP / 16, TC = WC / 16;
+  constexpr int AI = PT / 32, WI = CT / 32;  // 8-row DMA groups per wave per k-tile
+  constexpr int BUF = (PT + CT) * 128;
   constexpr int OROW = CT * 2 + 16;
-  static_assert(PT * OROW <= NBUF * BUF, "output staging fits in the operand buffers");
-  const bool staged = (a.K & 7) == 0;
+  constexpr int SM = 2 * BUF > PT * OROW ? 2 * BUF : PT * OROW;
+  __shared__ __attribute__((aligned(16))) char smem[SM];
+  typedef __attribute__((address_space(1))) const void gvoid;
+  typedef __attribute__((address_space(3))) void lvoid;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tile = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const int bx = tile % gridDim.x, by = tile / gridDim.x;
+  const int p0 = by * PT, c0 = bx * CT;
+  const int lr = lane >> 3;
+  const int ch = (lane & 7) ^ lr;
+
+  int ih0[AI], iw0[AI], pixbase[AI];
 #pragma unroll
-  for (int i = 0; i < TC; ++i) {
-    const int kloc = wc * WC + i * 16 + fk * 4;
-    const int kch = c0 + kloc;
-    float bsum[4] = {0.f, 0.f, 0.f, 0.f}, bsq[4] = {0.f, 0.f, 0.f, 0.f};
-    float bia[4] = {0.f, 0.f, 0.f, 0.f};
-    if (a.bias && kch < a.K) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bia[r] = a.bias[kch + r];
-    }
-#pragma unroll
-    for (int j = 0; j < TP; ++j) {
-      const int mloc = wp * WP + j * 16 + fr;
-      const int m = p0 + mloc;
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        v[r] = acc[i][j][r] + bia[r];
-        if (a.relu) v[r] = fmaxf(v[r], 0.f);
-      }
-      uint32_t lo = pack2bf(v[0], v[1]), hi = pack2bf(v[2], v[3]);
-      if (staged) {
-        *(uint2*)(smem + mloc * OROW + kloc * 2) = make_uint2(lo, hi);
-      } else if (m < a.M && kch < a.K) {
-        *(uint2*)(a.y + (size_t)m * a.K + kch) = make_uint2(lo, hi);
-      }
-      if (a.stats && m < a.M && kch < a.K) {
-        float q0 = lo_bf(lo), q1 = hi_bf(lo), q2 = lo_bf(hi), q3 = hi_bf(hi);
-        bsum[0] += q0; bsq[0] += q0 * q0;
-        bsum[1] += q1; bsq[1] += q1 * q1;
-        bsum[2] += q2; bsq[2] += q2 * q2;
-        bsum[3] += q3; bsq[3] += q3 * q3;
-      }
-    }
-    if (a.stats) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          bsum[r] += __shfl_xor(bsum[r], o, 64);
-          bsq[r] += __shfl_xor(bsq[r], o, 64);
-        }
-      }
-      // one partial row per (pixel tile, pixel wave): [sum(K) | sumsq(K)], reduced by reduce_rows
-      if (fr == 0 && kch < a.K) {
-        float* row = a.stats + (size_t)(by * NWP + wp) * (2 * a.K);
-        *(float4*)(row + kch) = make_float4(bsum[0], bsum[1], bsum[2], bsum[3]);
-        *(float4*)(row + a.K + kch) = make_float4(bsq[0], bsq[1], bsq[2], bsq[3]);
-      }
+  for (int j = 0; j < AI; ++j) {
+    const int m = p0 + 8 * (wave + 4 * j) + lr;
+    if (m < a.M) {
+      uint32_t n = fdiv((uint32_t)m, a.fd_PQ);
+      uint32_t rem = m - n * (a.P * a.Q);
+      uint32_t p = fdiv(rem, a.fd_Q);
+      uint32_t q = rem - p * a.Q;
+      ih0[j] = (int)p * a.stride - a.pad_h;
+      iw0[j] = (int)q * a.stride - a.pad_w;
+      pixbase[j] = (int)n * a.Hin * a.Win;
+    } else {
+      ih0[j] = -(1 << 28);
+      iw0[j] = -(1 << 28);
+      pixbase[j] = 0;
     }
   }
-  if (staged) {
-    __syncthreads();
-    constexpr int CPR = CT / 8;  // 16-B chunks per pixel row of the tile
-    constexpr int NIT = PT * CPR / 256;
-    const int chn = tid % CPR;   // fixed per thread (256 % CPR == 0)
-    const int kc = c0 + chn * 8;
-    const bool act = a.act_x != nullptr;
-    float sc[8], sh[8], sgx[8], sg[8];
+  int cc = (ch * 8) % a.C;
+  int tap = (ch * 8) / a.C;
+  int rr = tap / a.S, ss = tap - (tap / a.S) * a.S;
+  const char* xg = (const char*)a.x;
+  const char* wg = (const char*)a.w;
+  const char* zg = (const char*)a.zero;
+
+  auto issue = [&](int kt, int buf) {
+    char* base = smem + buf * BUF;
+    const int k = kt * BK + ch * 8;
+    const bool kin = k < a.Kg;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { sc[e] = 1.f; sh[e] = 0.f; sgx[e] = 0.f; sg[e] = 0.f; }
-    if (act && kc < a.K) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { sc[e] = a.act_ss[kc + e]; sh[e] = a.act_ss[a.K + kc + e]; }
+    for (int j = 0; j < AI; ++j) {
+      const int ihv = ih0[j] + rr, iwv = iw0[j] + ss;
+      bool v = kin && ihv >= 0 && ihv < a.Hv && iwv >= 0 && iwv < a.Wv;
+      if (UD > 1) v = v && ((ihv % UD) == 0) && ((iwv % UD) == 0);
+      const int ih = UD > 1 ? ihv / UD : ihv, iw = UD > 1 ? iwv / UD : iwv;
+      const char* src = v ? xg + (size_t)((pixbase[j] + ih * a.Win + iw) * a.C + cc) * 2 : zg;
+      __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(base + (wave + 4 * j) * 1024), 16, 0, 0);
     }
 #pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int idx = it * 256 + tid;
-      const int row = idx / CPR;
-      const int m = p0 + row;
-      if (m < a.M && kc < a.K) {
-        uint4 v = *(const uint4*)(smem + row * OROW + chn * 16);
-        const size_t o = (size_t)m * a.K + kc;
-        if (a.add_src || act) {
-          float f[8];
-          f[0] = lo_bf(v.x); f[1] = hi_bf(v.x); f[2] = lo_bf(v.y); f[3] = hi_bf(v.y);
-          f[4] = lo_bf(v.z); f[5] = hi_bf(v.z); f[6] = lo_bf(v.w); f[7] = hi_bf(v.w);
-          if (a.add_src) {
-            const bf16_t* src = a.add_src + o;
-            if (a.add_stride > 1) {
-              const uint32_t n = fdiv((uint32_t)m, a.fd_PQ), rem = m - n * (a.P * a.Q);
-              const uint32_t h = fdiv(rem, a.fd_Q), w = rem - h * a.Q;
-              const int s = a.add_stride;
-              src = (h % s == 0 && w % s == 0)
-                        ? a.add_src + ((size_t)((int)n * a.add_H + (int)h / s) * a.add_W + (int)w / s) * a.K + kc
-                        : nullptr;
-            }
-            if (src) {
-              const uint4 r = *(const uint4*)src;
-              f[0] += lo_bf(r.x); f[1] += hi_bf(r.x); f[2] += lo_bf(r.y); f[3] += hi_bf(r.y);
-              f[4] += lo_bf(r.z); f[5] += hi_bf(r.z); f[6] += lo_bf(r.w); f[7] += hi_bf(r.w);
-            }
-          }
-          if (act) {
-            const uint4 xu = *(const uint4*)(a.act_x + o);
-            float xv[8];
-            xv[0] = lo_bf(xu.x); xv[1] = hi_bf(xu.x); xv[2] = lo_bf(xu.y); xv[3] = hi_bf(xu.y);
-            xv[4] = lo_bf(xu.z); xv[5] = hi_bf(xu.z); xv[6] = lo_bf(xu.w); xv[7] = hi_bf(xu.w);
+    for (int j = 0; j < WI; ++j) {
+      const int row = c0 + 8 * (wave + 4 * j) + lr;
+      const bool v = kin && row < a.K;
+      const char* src = v ? wg + ((size_t)row * a.Kg + k) * 2 : zg;
+      __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(base + PT * 128 + (wave + 4 * j) * 1024), 16, 0, 0);
+    }
+    cc += BK;
+    while (cc >= a.C) {
+      cc -= a.C;
+      if (++ss == a.S) { ss = 0; ++rr; }
+    }
+  };
+
+  f32x4 acc[TC][TP];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float g = fmaf(xv[e], sc[e], sh[e]) > 0.f ? f[e] : 0.f;
-              sgx[e] += g * xv[e];
-              sg[e] += g;
-              f[e] = g * sc[e];
-            }
-          }
-          v = make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
-        }
-        *(uint4*)(a.y + o) = v;
+  for (int i = 0; i < TC; ++i)
+#pragma unroll
+    for (int j = 0; j < TP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int wp = wave % NWP, wc = wave / NWP;
+  const int fr = lane & 15, fk = lane >> 4;
+  auto compute = [&](int cur) {
+    const char* base = smem + cur * BUF;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      short8 bf[TP], af[TC];
+#pragma unroll
+      for (int j = 0; j < TP; ++j) {
+        int row = wp * WP + j * 16 + fr;
+        int chn = ks * 4 + fk;
+        bf[j] = *(const short8*)(base + row * 128 + ((chn ^ (row & 7)) << 4));
       }
-    }
-    if (act) {
-      // reduce the per-thread partial sums over the threads sharing this chunk column, one partial
-      // row per pixel tile (reduced over tiles by dtm_reduce_rows)
-      __syncthreads();
-      float* red = (float*)smem;  // [256][16]
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { red[tid * 16 + e] = sgx[e]; red[tid * 16 + 8 + e] = sg[e]; }
-      __syncthreads();
-      if (tid < CPR && kc < a.K) {
-        float tx[8], tg[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { tx[e] = 0.f; tg[e] = 0.f; }
-        for (int t = tid; t < 256; t += CPR) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) { tx[e] += red[t * 16 + e]; tg[e] += red[t * 16 + 8 + e]; }
-        }
-        float* prow = a.act_sums + (size_t)by * (2 * a.K);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { prow[kc + e] = tx[e]; prow[a.K + kc + e] = tg[e]; }
+      for (int i = 0; i < TC; ++i) {
+        int row = wc * WC + i * 16 + fr;
+        int chn = ks * 4 + fk;
+        af[i] = *(const short8*)(base + PT * 128 + row * 128 + ((chn ^ (row & 7)) << 4));
       }
+#pragma unroll
+      for (int i = 0; i < TC; ++i)
+#pragma unroll
+        for (int j = 0; j < TP; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
+  };
+
+  const int nk = (a.Kg + BK - 1) / BK;
+  issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // tile kt landed for every wave; buffer (kt+1)&1 is no longer read
+    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+    compute(kt & 1);
   }
+  __syncthreads();  // the epilogue reuses the operand buffers
+  conv_nt_epilogue<PT, CT, WP, WC>(a, acc, smem, p0, c0, by);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -659,6 +802,22 @@ struct ConvDesc {
   int N, H, W, C, K, R, S, P, Q, stride, pad_h, pad_w;
 };
 
+static const bf16_t* zero_chunk() {
+  static void* z = nullptr;
+  if (!z) {
+    if (hipMalloc(&z, 4096) != hipSuccess) return nullptr;
+    hipMemset(z, 0, 4096);
+    hipDeviceSynchronize();
+  }
+  return (const bf16_t*)z;
+}
+
+template <int PT, int CT, int WP, int WC, int UD>
+static void launch_nt_dma(const ConvNTArgs& a, hipStream_t st) {
+  dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT);
+  hipLaunchKernelGGL((conv_nt_dma_kernel<PT, CT, WP, WC, UD>), grid, dim3(256), 0, st, a);
+}
+
 template <int PT, int CT, int WP, int WC, int UD, int NBUF = 2>
 static void launch_nt(const ConvNTArgs& a, hipStream_t st) {
   dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT);
@@ -667,7 +826,7 @@ static void launch_nt(const ConvNTArgs& a, hipStream_t st) {
 
 // tile variants: 0 = 128 pix x 128 ch (4 waves 2x2 of 64x64), 1 = 128 x 64 (4x1 of 32x64),
 // 2 = 64 x 128 (2x2 of 32x64; 3 blocks/CU by LDS), 3 / 4 = 1 / 2 with a single LDS buffer
-// (more resident blocks).  DTM_CONV_TILE forces one (A/B experiments).
+// (more resident blocks); 10-12 = LDS-DMA 128x128 / 64x128 / 128x64 (opt-in).  DTM_CONV_TILE forces one.
 struct TileCfg {
   int id, PT, NWP;
 };
@@ -682,8 +841,13 @@ static TileCfg pick_tile(const ConvNTArgs& a) {
   // 128x128 tile keeps the small-M / deep-K layers (7x7 maps, K-reduction >= 2048)
   int id = g_tile_env;
   if (id < 0) id = a.K <= 64 ? 3 : ((a.M <= 16384 && a.Kg >= 2048) ? 0 : 4);
+  // LDS-DMA variants (10-12, opt-in) need an operand without the prologue affine
+  if (id >= 10 && a.in_scale) id = a.K <= 64 ? 3 : 4;
   if (id == 1 || id == 3) return {id, 128, 4};
   if (id == 2 || id == 4) return {id, 64, 2};
+  if (id == 10) return {id, 128, 2};
+  if (id == 11) return {id, 64, 2};
+  if (id == 12) return {id, 128, 4};
   return {0, 128, 2};
 }
 
@@ -693,8 +857,14 @@ static void dispatch_ud(const ConvNTArgs& a, const TileCfg& t, hipStream_t st) {
   else if (t.id == 2) launch_nt<64, 128, 32, 64, UD>(a, st);
   else if (t.id == 3) launch_nt<128, 64, 32, 64, UD, 1>(a, st);
   else if (t.id == 4) launch_nt<64, 128, 32, 64, UD, 1>(a, st);
+  else if (t.id == 10) launch_nt_dma<128, 128, 64, 64, UD>(a, st);
+  else if (t.id == 11) launch_nt_dma<64, 128, 32, 64, UD>(a, st);
+  else if (t.id == 12) launch_nt_dma<128, 64, 32, 64, UD>(a, st);
   else launch_nt<128, 128, 64, 64, UD>(a, st);
 }
+
+// tile override for A/B tests (-1 = the shape policy), same as DTM_CONV_TILE
+DTM_API void dtm_conv_set_tile(int id) { g_tile_env = id; }
 
 static void dispatch_nt(const ConvNTArgs& a, int ud, const TileCfg& t, hipStream_t st) {
   if (ud == 1) dispatch_ud<1>(a, t, st);
@@ -710,6 +880,7 @@ static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, cons
   a.stats = nullptr; a.bias = bias; a.in_scale = in_scale; a.in_shift = in_shift;
   a.add_src = nullptr; a.act_x = nullptr; a.act_ss = nullptr; a.act_sums = nullptr;
   a.add_stride = 1; a.add_H = a.add_W = 0;
+  a.zero = zero_chunk();
   size_t xb = (size_t)d->N * d->H * d->W * d->C * 2, wb = (size_t)d->K * d->R * d->S * d->C * 2;
   if (xb >= (1ull << 31) || wb >= (1ull << 31)) return -2;
   a.x_bytes = (uint32_t)xb; a.w_bytes = (uint32_t)wb;
@@ -777,6 +948,7 @@ DTM_API int dtm_conv_dgrad_ex(const void* dy, const void* wt, void* dx, const Co
   a.stats = nullptr; a.bias = nullptr; a.in_scale = nullptr; a.in_shift = nullptr;
   a.add_src = (const bf16_t*)add_src; a.act_x = (const bf16_t*)act_x; a.act_ss = act_ss; a.act_sums = nullptr;
   a.add_stride = add_stride;
+  a.zero = zero_chunk();
   a.add_H = (d->H - 1) / add_stride + 1; a.add_W = (d->W - 1) / add_stride + 1;
   size_t xb = (size_t)d->N * d->P * d->Q * d->K * 2, wb = (size_t)d->K * d->R * d->S * d->C * 2;
   if (xb >= (1ull << 31) || wb >= (1ull << 31)) return -2;

@@ -131,3 +131,27 @@ def test_image_augment_kernel_matches_oracle(distort, size):
     got = cifar10.augment(imgs.to(DEV), size, distort, np.random.RandomState(3), torch.float32)
     torch.cuda.synchronize()
     assert got.is_cuda and _rel(got.cpu(), ref_out) < 1e-4
+
+
+@pytest.mark.parametrize("tile", [10, 11, 12])
+def test_conv_lds_dma_tiles_match_default(tile):
+    """The opt-in LDS-DMA conv kernels (DTM_CONV_TILE=10..12) give the default kernel's results
+    (fwd with padding, stride-2 dgrad through the dilated path)."""
+    from distributed_tensorflow_models_amd.ops import _lib
+    from distributed_tensorflow_models_amd.ops import nn as F
+    outs = []
+    for t in (-1, tile):
+        _lib.lib().dtm_conv_set_tile(t)
+        try:
+            torch.manual_seed(0)
+            x = torch.randn(4, 15, 15, 64, device="cuda").to(torch.bfloat16).requires_grad_()
+            w = (torch.randn(96, 3, 3, 64, device="cuda") * 0.05).requires_grad_()
+            y = F.conv2d(x, w, None, 2, "SAME")
+            y.float().square().sum().backward()
+            torch.cuda.synchronize()
+            outs.append((y.detach().float(), x.grad.float()))
+        finally:
+            _lib.lib().dtm_conv_set_tile(-1)
+    for i, k in enumerate(("y", "dx")):
+        a, b = outs[0][i], outs[1][i]
+        assert ((a - b).norm() / b.norm()).item() < 1e-2, k
