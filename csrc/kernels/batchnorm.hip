@@ -328,9 +328,12 @@ __global__ __launch_bounds__(256) void bn_stats_fast(const bf16_t* __restrict__ 
   col_reduce8(red, s, q, stats + (size_t)blockIdx.x * 2 * C, stats + (size_t)blockIdx.x * 2 * C + C, cols, c0);
 }
 
+// mask (optional, relu only): one bit per output element, bit e of byte (row*C + c0)/8 = [y > 0] for
+// channel c0+e -- the ReLU mask the backward needs, 1/16 of the bytes of y.
 __global__ __launch_bounds__(256) void bn_apply_fast(const bf16_t* __restrict__ x, const float* __restrict__ ss,
                                                      const bf16_t* __restrict__ res, const float* __restrict__ rss,
-                                                     bf16_t* __restrict__ y, int M, int C, int res_mode, int relu, int rpb) {
+                                                     bf16_t* __restrict__ y, uint8_t* __restrict__ mask, int M, int C,
+                                                     int res_mode, int relu, int rpb) {
   const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t % cols) * 8, lr0 = t / cols;
   float sc[8], sh[8], rsc[8], rsh[8];
 #pragma unroll
@@ -362,8 +365,13 @@ __global__ __launch_bounds__(256) void bn_apply_fast(const bf16_t* __restrict__ 
         for (int e = 0; e < 8; ++e) f[e] += fmaf(g[e], rsc[e], rsh[e]);
       }
       if (relu) {
+        uint32_t bits = 0;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
+        for (int e = 0; e < 8; ++e) {
+          bits |= (f[e] > 0.f ? 1u : 0u) << e;
+          f[e] = fmaxf(f[e], 0.f);
+        }
+        if (mask) mask[((size_t)rr * C + c0) >> 3] = (uint8_t)bits;
       }
       *(uint4*)(y + (size_t)rr * C + c0) = pack8(f);
     }
@@ -374,6 +382,7 @@ __global__ __launch_bounds__(256) void bn_apply_fast(const bf16_t* __restrict__ 
 // subsample of the block input (slim resnet_v1 `subsample`), so the subsampled tensor is never stored.
 __global__ __launch_bounds__(256) void bn_apply_res_strided(const bf16_t* __restrict__ x, const float* __restrict__ ss,
                                                             const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
+                                                            uint8_t* __restrict__ mask,
                                                             uint32_t M, int C, int relu, FastDiv fd_cols, FastDiv fd_Wo,
                                                             FastDiv fd_Ho, int Ho, int Wo, int Hi, int Wi, int s) {
   const uint32_t cols = C >> 3, total = M * cols;
@@ -385,11 +394,14 @@ __global__ __launch_bounds__(256) void bn_apply_res_strided(const bf16_t* __rest
     float f[8], g[8];
     unpack8(*(const uint4*)(x + (size_t)r * C + c0), f);
     unpack8(*(const uint4*)(res + rr * C + c0), g);
+    uint32_t bits = 0;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       f[e] = fmaf(f[e], ss[c0 + e], ss[C + c0 + e]) + g[e];
+      bits |= (f[e] > 0.f ? 1u : 0u) << e;
       if (relu) f[e] = fmaxf(f[e], 0.f);
     }
+    if (relu && mask) mask[((size_t)r * C + c0) >> 3] = (uint8_t)bits;
     *(uint4*)(y + (size_t)r * C + c0) = pack8(f);
   }
 }
@@ -633,32 +645,40 @@ DTM_API void dtm_bn_inference_params(const float* gamma, const float* beta, cons
                      mov_mean, mov_var, out, C, eps);
 }
 
-DTM_API void dtm_bn_apply(const void* x, const float* ss, const void* res, const float* rss, void* y, long M, int C,
-                          int res_mode, int relu, void* stream) {
+// mask: optional ReLU bitmask output (fast path only; returns -7 when it cannot be produced)
+DTM_API int dtm_bn_apply2(const void* x, const float* ss, const void* res, const float* rss, void* y, void* mask, long M,
+                          int C, int res_mode, int relu, void* stream) {
   if (fast_ok(M, C)) {
     int blocks, rpb; fast_grid(M, C, &blocks, &rpb);
     hipLaunchKernelGGL(bn_apply_fast, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ss,
-                       (const bf16_t*)res, rss, (bf16_t*)y, (int)M, C, res_mode, relu, rpb);
-    return;
+                       (const bf16_t*)res, rss, (bf16_t*)y, (uint8_t*)mask, (int)M, C, res_mode, relu, rpb);
+    return 0;
   }
+  if (mask) return -7;
   if (C % 8 == 0)
     hipLaunchKernelGGL(bn_apply_kernel<8>, dim3(grid_for(M * C / 8)), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)x, ss, (const bf16_t*)res, rss, (bf16_t*)y, M, C, res_mode, relu);
   else
     hipLaunchKernelGGL(bn_apply_kernel<1>, dim3(grid_for(M * C)), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)x, ss, (const bf16_t*)res, rss, (bf16_t*)y, M, C, res_mode, relu);
+  return 0;
+}
+
+DTM_API void dtm_bn_apply(const void* x, const float* ss, const void* res, const float* rss, void* y, long M, int C,
+                          int res_mode, int relu, void* stream) {
+  dtm_bn_apply2(x, ss, res, rss, y, nullptr, M, C, res_mode, relu, stream);
 }
 
 // res [N][Hi][Wi][C] read at (n, h*s, w*s) for every output pixel of x / y [N][Ho][Wo][C]
-DTM_API int dtm_bn_apply_res_strided(const void* x, const float* ss, const void* res, void* y, int N, int Ho, int Wo,
-                                     int C, int Hi, int Wi, int s, int relu, void* stream) {
+DTM_API int dtm_bn_apply_res_strided(const void* x, const float* ss, const void* res, void* y, void* mask, int N, int Ho,
+                                     int Wo, int C, int Hi, int Wi, int s, int relu, void* stream) {
   if (C % 8 || (long)N * Ho * Wo * (C / 8) >= (1l << 31) || (Ho - 1) * s >= Hi || (Wo - 1) * s >= Wi) return -1;
   const uint32_t M = (uint32_t)N * Ho * Wo;
   const long total = (long)M * (C / 8);
   long blocks = (total + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(bn_apply_res_strided, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ss,
-                     (const bf16_t*)res, (bf16_t*)y, M, C, relu, make_fastdiv(C / 8), make_fastdiv(Wo),
+                     (const bf16_t*)res, (bf16_t*)y, (uint8_t*)mask, M, C, relu, make_fastdiv(C / 8), make_fastdiv(Wo),
                      make_fastdiv(Ho), Ho, Wo, Hi, Wi, s);
   return 0;
 }

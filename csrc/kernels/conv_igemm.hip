@@ -59,6 +59,7 @@ struct ConvNTArgs {
   const float* act_ss;    //   g = out * [act_x*scale + shift > 0]; out <- g*scale;
   float* act_sums;        //   partial rows per pixel tile: [sum g*act_x (K) | sum g (K)]
   const bf16_t* zero;     // >= 16 B of zeros: the LDS-DMA source of padding / out-of-range chunks
+  int act_unscaled;       // act path: out <- g (not g*scale); the producer's conv+BN backward scales it
 };
 
 // Shared epilogue of the conv_nt kernels (register-staged and LDS-DMA): acc[TC][TP] of wave (wp, wc)
@@ -181,7 +182,7 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
               const float g = fmaf(xv[e], sc[e], sh[e]) > 0.f ? f[e] : 0.f;
               sgx[e] += g * xv[e];
               sg[e] += g;
-              f[e] = g * sc[e];
+              f[e] = a.act_unscaled ? g : g * sc[e];
             }
           }
           v = make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
@@ -880,6 +881,7 @@ static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, cons
   a.stats = nullptr; a.bias = bias; a.in_scale = in_scale; a.in_shift = in_shift;
   a.add_src = nullptr; a.act_x = nullptr; a.act_ss = nullptr; a.act_sums = nullptr;
   a.add_stride = 1; a.add_H = a.add_W = 0;
+  a.act_unscaled = 0;
   a.zero = zero_chunk();
   size_t xb = (size_t)d->N * d->H * d->W * d->C * 2, wb = (size_t)d->K * d->R * d->S * d->C * 2;
   if (xb >= (1ull << 31) || wb >= (1ull << 31)) return -2;
@@ -938,7 +940,8 @@ DTM_API int dtm_conv_fwd_bn(const void* x, const void* w, void* y, const float* 
 //   (BatchNorm+ReLU fused into this conv's forward prologue); dx <- [act_x*scale+shift>0]*dx*scale and
 //   act_sums[2][C] += (sum g*act_x, sum g) with g the masked gradient (the BN scale/shift grads).
 DTM_API int dtm_conv_dgrad_ex(const void* dy, const void* wt, void* dx, const ConvDesc* d, const void* add_src,
-                              int add_stride, const void* act_x, const float* act_ss, float* act_sums, void* stream) {
+                              int add_stride, const void* act_x, const float* act_ss, float* act_sums,
+                              int act_unscaled, void* stream) {
   if (d->K % 8 || d->C % 4) return -1;
   if (add_stride < 1 || (add_stride > 1 && !add_src)) return -6;
   if (d->stride > 2) return -3;
@@ -948,6 +951,7 @@ DTM_API int dtm_conv_dgrad_ex(const void* dy, const void* wt, void* dx, const Co
   a.stats = nullptr; a.bias = nullptr; a.in_scale = nullptr; a.in_shift = nullptr;
   a.add_src = (const bf16_t*)add_src; a.act_x = (const bf16_t*)act_x; a.act_ss = act_ss; a.act_sums = nullptr;
   a.add_stride = add_stride;
+  a.act_unscaled = act_unscaled;
   a.zero = zero_chunk();
   a.add_H = (d->H - 1) / add_stride + 1; a.add_W = (d->W - 1) / add_stride + 1;
   size_t xb = (size_t)d->N * d->P * d->Q * d->K * 2, wb = (size_t)d->K * d->R * d->S * d->C * 2;
@@ -972,7 +976,7 @@ DTM_API int dtm_conv_dgrad_ex(const void* dy, const void* wt, void* dx, const Co
 }
 
 DTM_API int dtm_conv_dgrad(const void* dy, const void* wt, void* dx, const ConvDesc* d, void* stream) {
-  return dtm_conv_dgrad_ex(dy, wt, dx, d, nullptr, 1, nullptr, nullptr, nullptr, stream);
+  return dtm_conv_dgrad_ex(dy, wt, dx, d, nullptr, 1, nullptr, nullptr, nullptr, 0, stream);
 }
 
 template <int MT, int NT, int WM, int WN, int NBUF = 2>

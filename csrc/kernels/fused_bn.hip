@@ -28,12 +28,17 @@ __device__ __forceinline__ uint4 pk8(const float* f) {
 // y = act(x) path backward.  mode: 0 = plain BN (no relu), 1 = relu with mask from y, 2 = relu with
 // mask recomputed from x*scale+shift.  res_mode 0/1/2 as in bn_apply.
 // sx: [2][C] += (Σ g·x, Σ g)  (the dss of x's BN);  sr: same for a BN'd residual.
+// mode 3: relu with the mask from the forward's bitmask (1 bit / element).  unscaled bit 0 (x) / bit 1
+// (BN'd residual): that input's producer is a training conv+BN whose backward applies the BN scale
+// itself (stats_combine_fin prescale), so the gradient handed to it is g, not g*scale; when dx and
+// dres are both g, only dx is written and the caller aliases dres to it.
 __global__ __launch_bounds__(256) void bn_apply_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                                                           const uint8_t* __restrict__ ymask,
                                                            const bf16_t* __restrict__ x, const float* __restrict__ ss,
                                                            const bf16_t* __restrict__ r, const float* __restrict__ rss,
                                                            bf16_t* __restrict__ dx, bf16_t* __restrict__ dres,
                                                            float* __restrict__ sx, float* __restrict__ sr, int M, int C,
-                                                           int mode, int res_mode, int rpb) {
+                                                           int mode, int res_mode, int unscaled, int rpb) {
   __shared__ float red[2][256][8];
   const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t % cols) * 8, lr0 = t / cols;
   float sc[8], sh[8], rsc[8];
@@ -42,12 +47,14 @@ __global__ __launch_bounds__(256) void bn_apply_bwd_kernel(const bf16_t* __restr
     sc[e] = ss[c0 + e]; sh[e] = ss[C + c0 + e];
     rsc[e] = res_mode == 2 ? rss[c0 + e] : 1.f;
   }
+  const bool ux = unscaled & 1, ur = (unscaled >> 1) & 1;
   float a1[8], a0[8], b1[8], b0[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) a1[e] = a0[e] = b1[e] = b0[e] = 0.f;
   const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
   for (int row = lr0 < RP ? r0 + lr0 : r1; row < r1; row += RP * FU2) {
     uint4 vdy[FU2], vy[FU2], vx[FU2], vr[FU2];
+    uint32_t mb[FU2];
 #pragma unroll
     for (int u = 0; u < FU2; ++u) {
       int rr = row + u * RP;
@@ -57,6 +64,7 @@ __global__ __launch_bounds__(256) void bn_apply_bwd_kernel(const bf16_t* __restr
       vdy[u] = ok ? *(const uint4*)(dy + o) : z;
       vx[u] = ok ? *(const uint4*)(x + o) : z;
       if (mode == 1) vy[u] = ok ? *(const uint4*)(y + o) : z;
+      if (mode == 3) mb[u] = ok ? (uint32_t)ymask[o >> 3] : 0u;
       if (res_mode == 2) vr[u] = ok ? *(const uint4*)(r + o) : z;
     }
 #pragma unroll
@@ -73,18 +81,37 @@ __global__ __launch_bounds__(256) void bn_apply_bwd_kernel(const bf16_t* __restr
       } else if (mode == 2) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) g[e] = fmaf(xv[e], sc[e], sh[e]) > 0.f ? g[e] : 0.f;
+      } else if (mode == 3) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = (mb[u] >> e) & 1u ? g[e] : 0.f;
       }
-      float d[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { d[e] = g[e] * sc[e]; a1[e] += g[e] * xv[e]; a0[e] += g[e]; }
-      *(uint4*)(dx + o) = pk8(d);
-      if (res_mode == 1) {
+      for (int e = 0; e < 8; ++e) { a1[e] += g[e] * xv[e]; a0[e] += g[e]; }
+      if (res_mode == 2) {
+        float rv[8]; up8(vr[u], rv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { b1[e] += g[e] * rv[e]; b0[e] += g[e]; }
+      }
+      if (ux) {
+        *(uint4*)(dx + o) = pk8(g);
+      } else {
+        float d[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[e] = g[e] * sc[e];
+        *(uint4*)(dx + o) = pk8(d);
+      }
+      // dres: skipped when it equals dx (the caller aliases the two)
+      if (res_mode == 1 && !ux) {
         *(uint4*)(dres + o) = pk8(g);
-      } else if (res_mode == 2) {
-        float rv[8], dr[8]; up8(vr[u], rv);
+      } else if (res_mode == 2 && !(ux && ur)) {
+        if (ur) {
+          *(uint4*)(dres + o) = pk8(g);
+        } else {
+          float dr[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) { dr[e] = g[e] * rsc[e]; b1[e] += g[e] * rv[e]; b0[e] += g[e]; }
-        *(uint4*)(dres + o) = pk8(dr);
+          for (int e = 0; e < 8; ++e) dr[e] = g[e] * rsc[e];
+          *(uint4*)(dres + o) = pk8(dr);
+        }
       }
     }
   }
@@ -148,7 +175,8 @@ __global__ __launch_bounds__(256) void stats_combine_fin_kernel(const bf16_t* __
                                                                 const float* __restrict__ dss, const float* __restrict__ ss,
                                                                 const float* __restrict__ gamma, float count,
                                                                 float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                                bf16_t* __restrict__ out, int M, int C, int rpb) {
+                                                                bf16_t* __restrict__ out, int M, int C, int prescale,
+                                                                int rpb) {
   __shared__ float s_ab[2][2048];
   const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t % cols) * 8, lr0 = t / cols;
   for (int c = t; c < C; c += 256) {  // one channel per thread, shared through LDS
@@ -162,9 +190,13 @@ __global__ __launch_bounds__(256) void stats_combine_fin_kernel(const bf16_t* __
     }
   }
   __syncthreads();
-  float a[8], b[8];
+  float a[8], b[8], sc[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) { a[e] = s_ab[0][c0 + e]; b[e] = s_ab[1][c0 + e]; }
+  for (int e = 0; e < 8; ++e) {
+    a[e] = s_ab[0][c0 + e];
+    b[e] = s_ab[1][c0 + e];
+    sc[e] = prescale ? ss[c0 + e] : 1.f;  // dy is the unscaled g: the BN-apply gradient is g*scale
+  }
   const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
   for (int row = lr0 < RP ? r0 + lr0 : r1; row < r1; row += RP * FU2) {
     uint4 vd[FU2], vx[FU2];
@@ -183,7 +215,7 @@ __global__ __launch_bounds__(256) void stats_combine_fin_kernel(const bf16_t* __
       float d[8], xv[8];
       up8(vd[u], d); up8(vx[u], xv);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) d[e] += a[e] + b[e] * xv[e];
+      for (int e = 0; e < 8; ++e) d[e] = fmaf(d[e], sc[e], a[e] + b[e] * xv[e]);
       *(uint4*)(out + (size_t)rr * C + c0) = pk8(d);
     }
   }
@@ -232,17 +264,18 @@ static int shape_ok(long M, int C) {
   return cols <= 256 && M < (1l << 31);
 }
 
-DTM_API int dtm_bn_apply_bwd(const void* dy, const void* y, const void* x, const float* ss, const void* r,
-                             const float* rss, void* dx, void* dres, float* sx, float* sr, long M, int C, int mode,
-                             int res_mode, void* stream) {
+DTM_API int dtm_bn_apply_bwd(const void* dy, const void* y, const void* ymask, const void* x, const float* ss,
+                             const void* r, const float* rss, void* dx, void* dres, float* sx, float* sr, long M, int C,
+                             int mode, int res_mode, int unscaled, void* stream) {
   if (!shape_ok(M, C)) return -1;
+  if ((mode == 3 && !ymask) || (mode == 1 && !y)) return -2;
   int blocks, rpb;
   grid2(M, C, &blocks, &rpb);
   float* ws = dtm_ws_get((size_t)blocks * 4 * C);
   if (!ws) return -4;
   hipLaunchKernelGGL(bn_apply_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
-                     (const bf16_t*)y, (const bf16_t*)x, ss, (const bf16_t*)r, rss, (bf16_t*)dx, (bf16_t*)dres, ws,
-                     nullptr, (int)M, C, mode, res_mode, rpb);
+                     (const bf16_t*)y, (const uint8_t*)ymask, (const bf16_t*)x, ss, (const bf16_t*)r, rss, (bf16_t*)dx,
+                     (bf16_t*)dres, ws, nullptr, (int)M, C, mode, res_mode, unscaled, rpb);
   dtm_reduce_rows(ws, blocks, 2 * C, 4 * C, sx, (hipStream_t)stream);
   if (res_mode == 2) dtm_reduce_rows(ws + 2 * C, blocks, 2 * C, 4 * C, sr, (hipStream_t)stream);
   return 0;
@@ -265,11 +298,12 @@ DTM_API void dtm_bn_finalize_bwd(const float* dss, const float* ss, const float*
 }
 
 DTM_API int dtm_stats_combine_fin(const void* dy, const void* x, const float* dss, const float* ss, const float* gamma,
-                                  float count, float* dgamma, float* dbeta, void* out, long M, int C, void* stream) {
+                                  float count, float* dgamma, float* dbeta, void* out, long M, int C, int prescale,
+                                  void* stream) {
   if (!shape_ok(M, C) || C > 2048) return -1;
   int blocks, rpb;
   grid2(M, C, &blocks, &rpb);
   hipLaunchKernelGGL(stats_combine_fin_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
-                     (const bf16_t*)x, dss, ss, gamma, count, dgamma, dbeta, (bf16_t*)out, (int)M, C, rpb);
+                     (const bf16_t*)x, dss, ss, gamma, count, dgamma, dbeta, (bf16_t*)out, (int)M, C, prescale, rpb);
   return 0;
 }

@@ -246,7 +246,8 @@ __global__ __launch_bounds__(256) void maxpool_bnrelu_bwd_kernel(const bf16_t* _
                                                                  const uint8_t* __restrict__ arg,
                                                                  const bf16_t* __restrict__ x, const float* __restrict__ ss,
                                                                  bf16_t* __restrict__ dx, float* __restrict__ part,
-                                                                 PoolArgs a, FastDiv fd_W, FastDiv fd_H, int rpb) {
+                                                                 PoolArgs a, FastDiv fd_W, FastDiv fd_H, int unscaled,
+                                                                 int rpb) {
   __shared__ float red[2][256][8];
   const int cols = a.C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t % cols) * 8, lr0 = t / cols;
   float sc[8], sh[8], a1[8], a0[8];
@@ -307,7 +308,7 @@ __global__ __launch_bounds__(256) void maxpool_bnrelu_bwd_kernel(const bf16_t* _
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float g = fmaf(xv[e], sc[e], sh[e]) > 0.f ? acc[e] : 0.f;
-        d[e] = g * sc[e];
+        d[e] = unscaled ? g : g * sc[e];
         a1[e] += g * xv[e];
         a0[e] += g;
       }
@@ -382,7 +383,7 @@ DTM_API int dtm_maxpool_bnrelu_fwd(const void* x, const float* ss, void* y, void
 
 // dx = [x*scale+shift > 0] * scale * maxpool_grad(dy);  sums[0..1][C] += (sum g*x, sum g)
 DTM_API int dtm_maxpool_bnrelu_bwd(const void* dy, const void* arg, const void* x, const float* ss, void* dx,
-                                   float* sums, const PoolArgs* a, void* stream) {
+                                   float* sums, const PoolArgs* a, int unscaled, void* stream) {
   if (a->C % 8 || a->C / 8 > 256 || (long)a->N * a->H * a->W * a->C >= (1l << 31)) return -1;
   if ((a->KH + a->SH - 1) / a->SH > 3 || (a->KW + a->SW - 1) / a->SW > 3) return -2;
   const int cols = a->C / 8, RP = 256 / cols;
@@ -399,11 +400,11 @@ DTM_API int dtm_maxpool_bnrelu_bwd(const void* dy, const void* arg, const void* 
   if (wm <= 2)
     hipLaunchKernelGGL((maxpool_bnrelu_bwd_kernel<2, 2>), dim3(blocks), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)dy, (const uint8_t*)arg, (const bf16_t*)x, ss, (bf16_t*)dx, ws, *a,
-                       make_fastdiv(a->W), make_fastdiv(a->H), (int)rpb);
+                       make_fastdiv(a->W), make_fastdiv(a->H), unscaled, (int)rpb);
   else
     hipLaunchKernelGGL((maxpool_bnrelu_bwd_kernel<3, 1>), dim3(blocks), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)dy, (const uint8_t*)arg, (const bf16_t*)x, ss, (bf16_t*)dx, ws, *a,
-                       make_fastdiv(a->W), make_fastdiv(a->H), (int)rpb);
+                       make_fastdiv(a->W), make_fastdiv(a->H), unscaled, (int)rpb);
   dtm_reduce_rows(ws, blocks, 2 * a->C, 2 * a->C, sums, (hipStream_t)stream);
   return 0;
 }

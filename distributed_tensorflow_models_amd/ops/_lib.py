@@ -34,7 +34,7 @@ _F = ctypes.c_float
 _SIGS = {
     "dtm_conv_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, ctypes.POINTER(ConvDesc), _P]),
     "dtm_conv_dgrad": (_I, [_P, _P, _P, ctypes.POINTER(ConvDesc), _P]),
-    "dtm_conv_dgrad_ex": (_I, [_P, _P, _P, ctypes.POINTER(ConvDesc), _P, _I, _P, _P, _P, _P]),
+    "dtm_conv_dgrad_ex": (_I, [_P, _P, _P, ctypes.POINTER(ConvDesc), _P, _I, _P, _P, _P, _I, _P]),
     "dtm_conv_wgrad": (_I, [_P, _P, _P, _P, _P, ctypes.POINTER(ConvDesc), _I, _P]),
     "dtm_weight_flip_transpose": (None, [_P, _P, _I, _I, _I, _I, _P]),
     "dtm_weight_flip_transpose_batched": (None, [_P, _I, _P]),
@@ -43,12 +43,13 @@ _SIGS = {
     "dtm_bn_finalize": (None, [_P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _I, _I, _P]),
     "dtm_bn_inference_params": (None, [_P, _P, _P, _P, _P, _I, _F, _P]),
     "dtm_bn_apply": (None, [_P, _P, _P, _P, _P, _L, _I, _I, _I, _P]),
+    "dtm_bn_apply2": (_I, [_P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _P]),
     "dtm_maxpool_bnrelu_fwd": (_I, [_P, _P, _P, _P, ctypes.POINTER(PoolArgs), _P]),
-    "dtm_maxpool_bnrelu_bwd": (_I, [_P, _P, _P, _P, _P, _P, ctypes.POINTER(PoolArgs), _P]),
+    "dtm_maxpool_bnrelu_bwd": (_I, [_P, _P, _P, _P, _P, _P, ctypes.POINTER(PoolArgs), _I, _P]),
     "dtm_conv_set_tile": (None, [_I]),
     "dtm_conv_fwd_bn": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _I, _I, ctypes.POINTER(ConvDesc), _P]),
-    "dtm_stats_combine_fin": (_I, [_P, _P, _P, _P, _P, _F, _P, _P, _P, _L, _I, _P]),
-    "dtm_bn_apply_res_strided": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "dtm_stats_combine_fin": (_I, [_P, _P, _P, _P, _P, _F, _P, _P, _P, _L, _I, _I, _P]),
+    "dtm_bn_apply_res_strided": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "dtm_bn_bwd_reduce": (None, [_P, _P, _P, _P, _P, _L, _I, _I, _P]),
     "dtm_bn_bwd_apply": (None, [_P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _P]),
     "dtm_bn_param_grad": (None, [_P, _P, _P, _I, _P]),
@@ -66,7 +67,7 @@ _SIGS = {
     "dtm_check_finite": (None, [_P, _L, _P, _P]),
     "dtm_f32_to_bf16": (None, [_P, _P, _L, _P]),
     "dtm_scale": (None, [_P, _L, _F, _P]),
-    "dtm_bn_apply_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _P]),
+    "dtm_bn_apply_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _I, _P]),
     "dtm_stats_combine": (_I, [_P, _P, _P, _P, _L, _I, _P]),
     "dtm_bn_finalize_bwd": (None, [_P, _P, _P, _P, _P, _P, _I, _F, _P]),
     "dtm_lrn": (_I, [_P, _P, _P, _L, _I, _I, _F, _F, _F, _I, _P]),

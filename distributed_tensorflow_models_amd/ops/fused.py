@@ -130,7 +130,7 @@ class _ConvBNFn(torch.autograd.Function):
     Backward: the finalize backward is folded into the stats-combine pass (dgamma / dbeta included)."""
 
     @staticmethod
-    def forward(ctx, x, in_ss, w, gamma, beta, geom, bn, slot=None):
+    def forward(ctx, x, in_ss, w, gamma, beta, geom, bn, slot=None, in_unscaled=False):
         L = _lib.lib()
         s = _lib.stream_ptr()
         w16 = weight_bf16(w)
@@ -152,6 +152,7 @@ class _ConvBNFn(torch.autograd.Function):
                                   ctypes.byref(d), s), "conv_fwd")
         ctx.geom = geom
         ctx.slot = slot
+        ctx.in_unscaled = bool(in_unscaled)
         ctx.has_gamma, ctx.has_beta = gamma is not None, beta is not None
         ctx.save_for_backward(x, in_ss, w, y, ss, gamma, beta)
         if ss is None:
@@ -175,16 +176,20 @@ class _ConvBNFn(torch.autograd.Function):
             if beta is not None and bmg is None:
                 dbeta = torch.zeros(g.K, device=dy.device)
             comb = torch.empty_like(dy)
+            # dy is the unscaled g (every consumer of a training LazyBN returns it, see LazyBN)
             _check(L.dtm_stats_combine_fin(_lib.ptr(dy), _lib.ptr(y), _lib.ptr(dss.contiguous()), _lib.ptr(ss),
                                            _lib.ptr(gamma), ctx.count,
                                            _lib.ptr(gmg if gmg is not None else dgamma),
-                                           _lib.ptr(bmg if bmg is not None else dbeta), _lib.ptr(comb), M_out, g.K, s),
+                                           _lib.ptr(bmg if bmg is not None else dbeta), _lib.ptr(comb), M_out, g.K, 1,
+                                           s),
                    "stats_combine_fin")
             if gmg is not None:
                 _notify(gamma)
             if bmg is not None:
                 _notify(beta)
             dy = comb
+        elif ss is not None:
+            dy = (dy.float() * ss[0]).to(dy.dtype)  # no statistics gradient: only the BN-apply scale
         d = g.as_desc(_lib.ConvDesc)
         sc = in_ss[0] if in_ss is not None else None
         sh = in_ss[1] if in_ss is not None else None
@@ -198,12 +203,13 @@ class _ConvBNFn(torch.autograd.Function):
                 # parameter-gradient sums are done in the dgrad epilogue
                 d_in = arena.zeros((4, g.C), dy.device)
                 _check(L.dtm_conv_dgrad_ex(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), None, 1,
-                                           _lib.ptr(x), _lib.ptr(in_ss), _lib.ptr(d_in), s), "conv_dgrad_act")
+                                           _lib.ptr(x), _lib.ptr(in_ss), _lib.ptr(d_in), int(ctx.in_unscaled), s),
+                       "conv_dgrad_act")
             else:
                 use_add = last and add_src is not None
                 _check(L.dtm_conv_dgrad_ex(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d),
                                            _lib.ptr(add_src) if use_add else None, add_stride if use_add else 1,
-                                           None, None, None, s), "conv_dgrad")
+                                           None, None, None, 0, s), "conv_dgrad")
                 if not last:
                     _slot_stash(ctx.slot, dx)
                     dx = None
@@ -219,7 +225,7 @@ class _ConvBNFn(torch.autograd.Function):
                 dw = target
         else:
             dw = None
-        return dx, d_in, dw, dgamma, dbeta, None, None, None
+        return dx, d_in, dw, dgamma, dbeta, None, None, None, None
 
 
 class _BNFinalizeFn(torch.autograd.Function):
@@ -256,40 +262,55 @@ class _BNFinalizeFn(torch.autograd.Function):
 
 
 class _BNApplyFn(torch.autograd.Function):
+    """y = act(x*scale + shift [+ res | + res*rscale + rshift]); ReLU mask kept as a bitmask.
+    unscaled: bit 0 / bit 1 = x / the BN'd residual comes from a training conv+BN (LazyBN.unscaled)."""
+
     @staticmethod
-    def forward(ctx, x, ss, res, res_ss, relu, res_slot=None, res_stride=1):
+    def forward(ctx, x, ss, res, res_ss, relu, res_slot=None, res_stride=1, unscaled=0):
         L = _lib.lib()
         C = x.shape[-1]
         M = x.numel() // C
         y = torch.empty_like(x)
         res_mode = 0 if res is None else (2 if res_ss is not None else 1)
+        want_mask = relu and torch.is_grad_enabled() and C % 8 == 0
+        mask = torch.empty(M * C // 8, device=x.device, dtype=torch.uint8) if want_mask else None
         if res_stride > 1:
             N, Ho, Wo, _ = x.shape
-            _check(L.dtm_bn_apply_res_strided(_lib.ptr(x), _lib.ptr(ss), _lib.ptr(res), _lib.ptr(y), N, Ho, Wo, C,
-                                              res.shape[1], res.shape[2], res_stride, int(relu), _lib.stream_ptr()),
-                   "bn_apply_res_strided")
+            _check(L.dtm_bn_apply_res_strided(_lib.ptr(x), _lib.ptr(ss), _lib.ptr(res), _lib.ptr(y), _lib.ptr(mask), N,
+                                              Ho, Wo, C, res.shape[1], res.shape[2], res_stride, int(relu),
+                                              _lib.stream_ptr()), "bn_apply_res_strided")
         else:
-            L.dtm_bn_apply(_lib.ptr(x), _lib.ptr(ss), _lib.ptr(res), _lib.ptr(res_ss), _lib.ptr(y), M, C, res_mode,
-                           int(relu), _lib.stream_ptr())
+            rc = L.dtm_bn_apply2(_lib.ptr(x), _lib.ptr(ss), _lib.ptr(res), _lib.ptr(res_ss), _lib.ptr(y), _lib.ptr(mask),
+                                 M, C, res_mode, int(relu), _lib.stream_ptr())
+            if rc == -7:  # no bitmask on this shape: keep y for the mask
+                mask = None
+                L.dtm_bn_apply2(_lib.ptr(x), _lib.ptr(ss), _lib.ptr(res), _lib.ptr(res_ss), _lib.ptr(y), None, M, C,
+                                res_mode, int(relu), _lib.stream_ptr())
         ctx.relu, ctx.res_mode, ctx.res_slot, ctx.res_stride = relu, res_mode, res_slot, res_stride
+        ctx.unscaled = int(unscaled) if res_mode == 2 else int(unscaled) & 1
         ctx.res_shape = None if res is None else tuple(res.shape)
         # the residual itself is only read back for a BN'd residual (res_mode 2)
-        ctx.save_for_backward(x, ss, res if res_mode == 2 else None, res_ss, y if relu else None)
+        ctx.save_for_backward(x, ss, res if res_mode == 2 else None, res_ss,
+                              y if (relu and mask is None) else None, mask)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         L = _lib.lib()
-        x, ss, res, rss, y = ctx.saved_tensors
+        x, ss, res, rss, y, mask = ctx.saved_tensors
         C = x.shape[-1]
         M = x.numel() // C
+        ux, ur = bool(ctx.unscaled & 1), bool(ctx.unscaled & 2)
         dx = torch.empty_like(x)
-        dres = torch.empty_like(x) if ctx.res_mode else None
+        # dres aliases dx when both are g (identity residual with an unscaled x, or both BN'd unscaled)
+        alias = (ctx.res_mode == 1 and ux) or (ctx.res_mode == 2 and ux and ur)
+        dres = None if not ctx.res_mode else (dx if alias else torch.empty_like(x))
         sx = arena.zeros((4, C), x.device)
         sr = arena.zeros((4, C), x.device) if ctx.res_mode == 2 else None
-        _check(L.dtm_bn_apply_bwd(_lib.ptr(dy.contiguous()), _lib.ptr(y), _lib.ptr(x), _lib.ptr(ss), _lib.ptr(res),
-                                  _lib.ptr(rss), _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(sx), _lib.ptr(sr), M, C,
-                                  1 if ctx.relu else 0, ctx.res_mode, _lib.stream_ptr()), "bn_apply_bwd")
+        mode = 3 if mask is not None else (1 if ctx.relu else 0)
+        _check(L.dtm_bn_apply_bwd(_lib.ptr(dy.contiguous()), _lib.ptr(y), _lib.ptr(mask), _lib.ptr(x), _lib.ptr(ss),
+                                  _lib.ptr(res), _lib.ptr(rss), _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(sx), _lib.ptr(sr),
+                                  M, C, mode, ctx.res_mode, ctx.unscaled, _lib.stream_ptr()), "bn_apply_bwd")
         st = ctx.res_stride
         if ctx.res_slot is not None:
             last, buf, bst = _slot_take(ctx.res_slot)
@@ -304,29 +325,31 @@ class _BNApplyFn(torch.autograd.Function):
             full = torch.zeros(ctx.res_shape, device=dres.device, dtype=dres.dtype)
             full[:, ::st, ::st, :] = dres
             dres = full
-        return dx, sx, dres, sr, None, None, None
+        return dx, sx, dres, sr, None, None, None, None
 
 
-def bn_apply(raw, ss, relu, residual=None):
+def bn_apply(raw, ss, relu, residual=None, unscaled=False):
     """y = relu?(raw*scale+shift + residual); residual may be a tensor, a LazyBN (BN'd shortcut) or a
-    Subsampled block input (strided identity shortcut)."""
+    Subsampled block input (strided identity shortcut).  ``unscaled``: raw's LazyBN.unscaled."""
+    ux = 1 if unscaled else 0
     if residual is None:
-        return _BNApplyFn.apply(raw, ss, None, None, bool(relu))
+        return _BNApplyFn.apply(raw, ss, None, None, bool(relu), None, 1, ux)
     if isinstance(residual, Subsampled):
         src = residual.src
         if isinstance(src, LazyBN):
             src = src.materialize()
         res = src.to(torch.bfloat16).contiguous()
         slot = _slot_register(res) if res is src else None
-        return _BNApplyFn.apply(raw, ss, res, None, bool(relu), slot, residual.stride)
+        return _BNApplyFn.apply(raw, ss, res, None, bool(relu), slot, residual.stride, ux)
     if isinstance(residual, LazyBN):
         if residual.relu:
             residual = residual.materialize()
         else:
-            return _BNApplyFn.apply(raw, ss, residual.raw, residual.ss, bool(relu))
+            return _BNApplyFn.apply(raw, ss, residual.raw, residual.ss, bool(relu), None, 1,
+                                    ux | (2 if residual.unscaled else 0))
     res = residual.to(torch.bfloat16).contiguous()
     slot = _slot_register(res) if res is residual else None
-    return _BNApplyFn.apply(raw, ss, res, None, bool(relu), slot)
+    return _BNApplyFn.apply(raw, ss, res, None, bool(relu), slot, 1, ux)
 
 
 def bn_inference_ss(bn):
@@ -340,9 +363,10 @@ def bn_inference_ss(bn):
 def conv_bn(x, w, bn, stride, padding, training, relu):
     """Fused conv -> BatchNorm; returns a LazyBN.  x: tensor or LazyBN(relu=True) (prologue-fused)."""
     in_ss = None
+    in_unscaled = False
     if isinstance(x, LazyBN):
         if x.relu:
-            in_ss, x = x.ss, x.raw
+            in_ss, in_unscaled, x = x.ss, x.unscaled, x.raw
         else:
             x = x.materialize()
     g = conv_geom(tuple(x.shape), tuple(w.shape), stride, padding)
@@ -359,8 +383,8 @@ def conv_bn(x, w, bn, stride, padding, training, relu):
     slot = _slot_register(xb) if (xb is x and in_ss is None) else None
     x = xb
     if training:
-        y, ss = _ConvBNFn.apply(x, in_ss, w, bn.gamma, bn.beta, g, bn, slot)
+        y, ss = _ConvBNFn.apply(x, in_ss, w, bn.gamma, bn.beta, g, bn, slot, in_unscaled)
     else:
-        y = _ConvBNFn.apply(x, in_ss, w, None, None, g, None, slot)
+        y = _ConvBNFn.apply(x, in_ss, w, None, None, g, None, slot, in_unscaled)
         ss = bn_inference_ss(bn)
-    return LazyBN(y, ss, relu)
+    return LazyBN(y, ss, relu, unscaled=training)

@@ -2,12 +2,17 @@
 
 
 class LazyBN:
-    """relu?(raw*scale + shift) kept as (raw, ss); ``ss`` is [4, C] (scale, shift, mean, rstd)."""
+    """relu?(raw*scale + shift) kept as (raw, ss); ``ss`` is [4, C] (scale, shift, mean, rstd).
 
-    __slots__ = ("raw", "ss", "relu")
+    ``unscaled``: ``raw`` comes from a training conv+BN whose backward applies the BN scale itself, so
+    every consumer (all of them are fused ops: conv prologue, BN-apply, BN+ReLU+max-pool) hands back the
+    gradient of the normalised pre-activation g rather than g*scale -- one elementwise multiply and, at
+    a ResNet unit output, one whole gradient tensor fewer."""
 
-    def __init__(self, raw, ss, relu):
-        self.raw, self.ss, self.relu = raw, ss, relu
+    __slots__ = ("raw", "ss", "relu", "unscaled")
+
+    def __init__(self, raw, ss, relu, unscaled=False):
+        self.raw, self.ss, self.relu, self.unscaled = raw, ss, relu, unscaled
 
     @property
     def shape(self):
@@ -31,7 +36,7 @@ class LazyBN:
     def materialize(self, residual=None, residual_act=None):
         from .fused import bn_apply
         relu = self.relu if residual is None else residual_act == "relu"
-        return bn_apply(self.raw, self.ss, relu, residual)
+        return bn_apply(self.raw, self.ss, relu, residual, unscaled=self.unscaled)
 
 
 class Subsampled:

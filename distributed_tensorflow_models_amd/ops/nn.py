@@ -403,14 +403,14 @@ class _MaxPoolBNReluFn(torch.autograd.Function):
     BN -> ReLU -> max pool); backward returns the raw-input gradient and the [4, C] scale/shift sums."""
 
     @staticmethod
-    def forward(ctx, raw, ss, g):
+    def forward(ctx, raw, ss, g, unscaled=False):
         L = _lib.lib()
         y = torch.empty((g.N, g.P, g.Q, g.C), device=raw.device, dtype=torch.bfloat16)
         arg = torch.empty((g.N, g.P, g.Q, g.C), device=raw.device, dtype=torch.uint8)
         a = g.as_args(_lib.PoolArgs)
         _check(L.dtm_maxpool_bnrelu_fwd(_lib.ptr(raw), _lib.ptr(ss), _lib.ptr(y), _lib.ptr(arg), ctypes.byref(a),
                                         _lib.stream_ptr()), "maxpool_bnrelu_fwd")
-        ctx.g = g
+        ctx.g, ctx.unscaled = g, bool(unscaled)
         ctx.save_for_backward(raw, ss, arg)
         return y
 
@@ -424,9 +424,9 @@ class _MaxPoolBNReluFn(torch.autograd.Function):
         sums = arena.zeros((4, g.C), raw.device)
         a = g.as_args(_lib.PoolArgs)
         _check(L.dtm_maxpool_bnrelu_bwd(_lib.ptr(dy.contiguous()), _lib.ptr(arg), _lib.ptr(raw), _lib.ptr(ss),
-                                        _lib.ptr(dx), _lib.ptr(sums), ctypes.byref(a), _lib.stream_ptr()),
-               "maxpool_bnrelu_bwd")
-        return dx, sums, None
+                                        _lib.ptr(dx), _lib.ptr(sums), ctypes.byref(a), int(ctx.unscaled),
+                                        _lib.stream_ptr()), "maxpool_bnrelu_bwd")
+        return dx, sums, None, None
 
 
 def max_pool(x, kernel, stride, padding="VALID"):
@@ -434,7 +434,7 @@ def max_pool(x, kernel, stride, padding="VALID"):
             and x.raw.shape[-1] % 8 == 0 and x.raw.is_contiguous():
         g = pool_geom(tuple(x.raw.shape), kernel, stride, padding)
         if g.KH * g.KW <= 255 and -(-g.KH // g.SH) <= 3 and -(-g.KW // g.SW) <= 3:
-            return _MaxPoolBNReluFn.apply(x.raw, x.ss.contiguous(), g)
+            return _MaxPoolBNReluFn.apply(x.raw, x.ss.contiguous(), g, x.unscaled)
     x = as_tensor(x)
     if not x.is_cuda:
         return ref.max_pool(x, kernel, stride, padding)
