@@ -535,6 +535,197 @@ __global__ __launch_bounds__(256) void conv_nt_dma_kernel(ConvNTArgs a) {
   conv_nt_epilogue<PT, CT, WP, WC>(a, acc, smem, p0, c0, by);
 }
 
+// Deep-K pipelined variant: both operand tiles go global -> LDS by LDS-DMA into an NS-slot ring with
+// ONE raw s_barrier per k-tile and a counted vmcnt, so NS-2 k-tiles stay in flight across the
+// barrier (an LDS-DMA is a pending write on the vector-memory counter: __syncthreads() would drain it).
+// Waves 2x2, each (PT/2) x (CT/2).  With the prologue (BatchNorm-apply + ReLU of the previous layer)
+// each lane transforms the chunks it DMA'd itself, in LDS, after its own vmcnt wait and before the
+// barrier that publishes the stage; padding / out-of-range chunks (from the zero buffer) are left at
+// zero, their validity recomputed from a lagging copy of the k iterator.  All LDS is ONE __shared__
+// array (a second object makes hipcc drain vmcnt before the fragment reads).
+template <int PT, int CT, int NS, int UD, bool PRO>
+__global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
+  constexpr int BK = 64;
+  constexpr int WP = PT / 2, WC = CT / 2;
+  constexpr int TP = WP / 16, TC = WC / 16;
+  constexpr int AI = PT / 32, WI = CT / 32;  // 8-row DMA groups per wave per k-tile
+  constexpr int G = AI + WI;                 // DMA instructions per wave per k-tile
+  constexpr int BUF = (PT + CT) * 128;
+  constexpr int OROW = CT * 2 + 16;
+  constexpr int MAXC = 512;
+  constexpr int RING = NS * BUF > PT * OROW ? NS * BUF : PT * OROW;
+  __shared__ __attribute__((aligned(16))) char smem[RING + (PRO ? MAXC * 8 : 0)];
+  typedef __attribute__((address_space(1))) const void gvoid;
+  typedef __attribute__((address_space(3))) void lvoid;
+  static_assert(G <= 31 && NS >= 2 && NS <= 4, "vmcnt range");
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tile = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const int bx = tile % gridDim.x, by = tile / gridDim.x;
+  const int p0 = by * PT, c0 = bx * CT;
+  const int lr = lane >> 3;
+  const int ch = (lane & 7) ^ lr;  // logical 16-B chunk this lane moves (source-side swizzle)
+  float* s_scale = (float*)(smem + RING);
+  float* s_shift = s_scale + MAXC;
+  if constexpr (PRO) {
+    for (int c = tid; c < a.C; c += 256) { s_scale[c] = a.in_scale[c]; s_shift[c] = a.in_shift[c]; }
+    __syncthreads();
+  }
+
+  int ih0[AI], iw0[AI], pixbase[AI];
+#pragma unroll
+  for (int j = 0; j < AI; ++j) {
+    const int m = p0 + 8 * (wave + 4 * j) + lr;
+    if (m < a.M) {
+      uint32_t n = fdiv((uint32_t)m, a.fd_PQ);
+      uint32_t rem = m - n * (a.P * a.Q);
+      uint32_t p = fdiv(rem, a.fd_Q);
+      uint32_t q = rem - p * a.Q;
+      ih0[j] = (int)p * a.stride - a.pad_h;
+      iw0[j] = (int)q * a.stride - a.pad_w;
+      pixbase[j] = (int)n * a.Hin * a.Win;
+    } else {
+      ih0[j] = -(1 << 28);
+      iw0[j] = -(1 << 28);
+      pixbase[j] = 0;
+    }
+  }
+  // issue-side k iterator of this lane's chunk, and (prologue) the lagging transform-side copy
+  int cc = (ch * 8) % a.C, tap = (ch * 8) / a.C;
+  int rr = tap / a.S, ss = tap - (tap / a.S) * a.S;
+  int tcc = cc, trr = rr, tss = ss;
+  const char* xg = (const char*)a.x;
+  const char* wg = (const char*)a.w;
+  const char* zg = (const char*)a.zero;
+
+  // branch-free validity (bitwise &, unsigned range checks): hipcc turns && chains around the
+  // DMA into exec-masked branches
+  auto valid_at = [&](int j, int r, int s, int& ih, int& iw) -> bool {
+    const int ihv = ih0[j] + r, iwv = iw0[j] + s;
+    bool v = ((unsigned)ihv < (unsigned)a.Hv) & ((unsigned)iwv < (unsigned)a.Wv);
+    if (UD > 1) v = v & (((ihv | iwv) & (UD - 1)) == 0);
+    ih = UD > 1 ? ihv / UD : ihv;
+    iw = UD > 1 ? iwv / UD : iwv;
+    return v;
+  };
+
+  auto issue = [&](int kt, int slot) {
+    char* base = smem + slot * BUF;
+    const int k = kt * BK + ch * 8;
+    const bool kin = k < a.Kg;
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+      int ih, iw;
+      const bool v = kin & valid_at(j, rr, ss, ih, iw);
+      const char* src = xg + (size_t)(uint32_t)(((pixbase[j] + ih * a.Win + iw) * a.C + cc) * 2);
+      __builtin_amdgcn_global_load_lds((gvoid*)(v ? src : zg), (lvoid*)(base + (wave + 4 * j) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < WI; ++j) {
+      const int row = c0 + 8 * (wave + 4 * j) + lr;
+      const bool v = kin & (row < a.K);
+      const char* src = wg + (size_t)(uint32_t)((row * a.Kg + k) * 2);
+      __builtin_amdgcn_global_load_lds((gvoid*)(v ? src : zg), (lvoid*)(base + PT * 128 + (wave + 4 * j) * 1024), 16,
+                                       0, 0);
+    }
+    cc += BK;
+    while (cc >= a.C) {
+      cc -= a.C;
+      if (++ss == a.S) { ss = 0; ++rr; }
+    }
+  };
+
+  auto transform = [&](int kt, int slot) {
+    char* base = smem + slot * BUF;
+    const bool kin = kt * BK + ch * 8 < a.Kg;
+    if (kin) {
+      const float4 s0 = *(const float4*)(s_scale + tcc), s1 = *(const float4*)(s_scale + tcc + 4);
+      const float4 h0 = *(const float4*)(s_shift + tcc), h1 = *(const float4*)(s_shift + tcc + 4);
+      const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+      for (int j = 0; j < AI; ++j) {
+        int ih, iw;
+        if (valid_at(j, trr, tss, ih, iw)) {
+          uint4* p = (uint4*)(base + (wave + 4 * j) * 1024 + lane * 16);
+          const uint4 q = *p;
+          uint32_t u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float lo = fmaxf(fmaf(lo_bf(u[e]), sc[2 * e], sh[2 * e]), 0.f);
+            const float hi = fmaxf(fmaf(hi_bf(u[e]), sc[2 * e + 1], sh[2 * e + 1]), 0.f);
+            u[e] = pack2bf(lo, hi);
+          }
+          *p = make_uint4(u[0], u[1], u[2], u[3]);
+        }
+      }
+    }
+    tcc += BK;
+    while (tcc >= a.C) {
+      tcc -= a.C;
+      if (++tss == a.S) { tss = 0; ++trr; }
+    }
+  };
+
+  f32x4 acc[TC][TP];
+#pragma unroll
+  for (int i = 0; i < TC; ++i)
+#pragma unroll
+    for (int j = 0; j < TP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int wp = wave % 2, wc = wave / 2;
+  const int fr = lane & 15, fk = lane >> 4;
+  auto compute = [&](int slot) {
+    // all 2 x (TP + TC) fragment reads of the k-tile first: the ks = 1 reads are in flight under the
+    // ks = 0 MFMAs (counted lgkmcnt) instead of a full LDS round trip between the two halves
+    const char* base = smem + slot * BUF;
+    short8 bf[2][TP], af[2][TC];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int chn = ks * 4 + fk;
+#pragma unroll
+      for (int j = 0; j < TP; ++j) {
+        const int row = wp * WP + j * 16 + fr;
+        bf[ks][j] = *(const short8*)(base + row * 128 + ((chn ^ (row & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < TC; ++i) {
+        const int row = wc * WC + i * 16 + fr;
+        af[ks][i] = *(const short8*)(base + PT * 128 + row * 128 + ((chn ^ (row & 7)) << 4));
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < TC; ++i)
+#pragma unroll
+        for (int j = 0; j < TP; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bf[ks][j], acc[i][j], 0, 0, 0);
+  };
+
+  const int nk = (a.Kg + BK - 1) / BK;
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) issue(s, s);
+  int slot = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    // this wave's DMA of k-tile kt has landed once at most the later stages are still counted
+    const int ahead = min(nk - 1, kt + NS - 2) - kt;
+    if (NS >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
+    else if (NS >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (PRO) transform(kt, slot);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // stage kt visible to all waves; stage kt-1 no longer read
+    if (kt + NS - 1 < nk) issue(kt + NS - 1, slot == 0 ? NS - 1 : slot - 1);
+    compute(slot);
+    slot = slot == NS - 1 ? 0 : slot + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // the epilogue reuses the ring
+  conv_nt_epilogue<PT, CT, WP, WC>(a, acc, smem, p0, c0, by);
+}
+
 // ------------------------------------------------------------------------------------------
 // weight gradient
 struct ConvWgradArgs {
@@ -819,6 +1010,13 @@ static void launch_nt_dma(const ConvNTArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((conv_nt_dma_kernel<PT, CT, WP, WC, UD>), grid, dim3(256), 0, st, a);
 }
 
+template <int PT, int CT, int NS, int UD>
+static void launch_pipe(const ConvNTArgs& a, hipStream_t st) {
+  dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT);
+  if (a.in_scale) hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, true>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, false>), grid, dim3(256), 0, st, a);
+}
+
 template <int PT, int CT, int WP, int WC, int UD, int NBUF = 2>
 static void launch_nt(const ConvNTArgs& a, hipStream_t st) {
   dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT);
@@ -841,9 +1039,15 @@ static TileCfg pick_tile(const ConvNTArgs& a) {
   // variants win almost everywhere (more resident blocks hide the short-K latency); the 2-buffer
   // 128x128 tile keeps the small-M / deep-K layers (7x7 maps, K-reduction >= 2048)
   int id = g_tile_env;
+  // the pipelined LDS-DMA 128x128 tile (2 slots, 2 blocks/CU) wins every deep-reduction layer without the
+  // prologue (tools/conv_tile_sweep.py: 3x3 at 14x14 / 7x7 -13..-18 %, deep 1x1 -5..-16 %)
+  if (id < 0 && !a.in_scale && a.Kg >= 1024) id = 21;
   if (id < 0) id = a.K <= 64 ? 3 : ((a.M <= 16384 && a.Kg >= 2048) ? 0 : 4);
   // LDS-DMA variants (10-12, opt-in) need an operand without the prologue affine
-  if (id >= 10 && a.in_scale) id = a.K <= 64 ? 3 : 4;
+  if (id >= 10 && id < 20 && a.in_scale) id = a.K <= 64 ? 3 : 4;
+  // pipelined LDS-DMA variants (20-23) stage the prologue affine in LDS: C <= 512
+  if (id >= 20 && a.in_scale && a.C > 512) id = 0;
+  if (id >= 20 && id <= 23) return {id, 128, 2};
   if (id == 1 || id == 3) return {id, 128, 4};
   if (id == 2 || id == 4) return {id, 64, 2};
   if (id == 10) return {id, 128, 2};
@@ -861,6 +1065,10 @@ static void dispatch_ud(const ConvNTArgs& a, const TileCfg& t, hipStream_t st) {
   else if (t.id == 10) launch_nt_dma<128, 128, 64, 64, UD>(a, st);
   else if (t.id == 11) launch_nt_dma<64, 128, 32, 64, UD>(a, st);
   else if (t.id == 12) launch_nt_dma<128, 64, 32, 64, UD>(a, st);
+  else if (t.id == 20) launch_pipe<128, 128, 3, UD>(a, st);
+  else if (t.id == 21) launch_pipe<128, 128, 2, UD>(a, st);
+  else if (t.id == 22) launch_pipe<128, 128, 4, UD>(a, st);
+  else if (t.id == 23) launch_pipe<128, 64, 3, UD>(a, st);
   else launch_nt<128, 128, 64, 64, UD>(a, st);
 }
 

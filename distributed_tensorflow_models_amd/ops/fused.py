@@ -360,12 +360,32 @@ def bn_inference_ss(bn):
     return torch.stack([scale, shift, bn.moving_mean.expand_as(scale), rstd.expand_as(scale)]).contiguous()
 
 
+def _prologue_fused(x_shape, w_shape, stride):
+    """Fuse the input's BatchNorm-apply + ReLU into this conv's operand prologue, or materialise it?
+
+    The prologue re-transforms every gathered element (R*S times per input element for an RxS conv)
+    in the conv AND in its wgrad, and keeps the conv off the pipelined LDS-DMA tile.  Measured per
+    ResNet-50 layer (tools/conv_tile_sweep.py, WGRAD=1; batch 256): for the stride-1 3x3 convs at
+    14x14 and 7x7 the prologue costs fwd +49/+59 us and wgrad +44/+38 us, a separate apply pass
+    15/9 us (+ the same again in backward) -> materialise; at 28x28 / 56x56 and for 1x1 convs the
+    prologue is cheaper than the extra activation round trips -> fuse.
+    DTM_PROLOGUE = auto (default) | fused | apply."""
+    import os
+    mode = os.environ.get("DTM_PROLOGUE", "auto")
+    if mode in ("fused", "apply"):
+        return mode == "fused"
+    _, H, W, _ = x_shape
+    _, R, S, _ = w_shape
+    st = stride if isinstance(stride, int) else stride[0]
+    return not (R * S > 1 and st == 1 and H * W <= 14 * 14)
+
+
 def conv_bn(x, w, bn, stride, padding, training, relu):
     """Fused conv -> BatchNorm; returns a LazyBN.  x: tensor or LazyBN(relu=True) (prologue-fused)."""
     in_ss = None
     in_unscaled = False
     if isinstance(x, LazyBN):
-        if x.relu:
+        if x.relu and _prologue_fused(tuple(x.shape), tuple(w.shape), stride):
             in_ss, in_unscaled, x = x.ss, x.unscaled, x.raw
         else:
             x = x.materialize()

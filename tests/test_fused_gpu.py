@@ -15,10 +15,11 @@ def _rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
-@pytest.mark.parametrize("fused", ["1", "0"])
+@pytest.mark.parametrize("fused,prologue", [("1", "auto"), ("1", "fused"), ("1", "apply"), ("0", "auto")])
 @pytest.mark.parametrize("base,batch", [(16, 16), (16, 32)])
-def test_small_resnet_matches_reference(fused, base, batch, monkeypatch):
+def test_small_resnet_matches_reference(fused, prologue, base, batch, monkeypatch):
     monkeypatch.setenv("DTM_FUSED_BN", fused)
+    monkeypatch.setenv("DTM_PROLOGUE", prologue)
     torch.manual_seed(0)
     net_cpu = ResNetV1(blocks=[(base, 2, 2), (2 * base, 2, 1)], num_classes=10, scope="r")
     net_gpu = copy.deepcopy(net_cpu).cuda()

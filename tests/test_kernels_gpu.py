@@ -133,6 +133,50 @@ def test_image_augment_kernel_matches_oracle(distort, size):
     assert got.is_cuda and _rel(got.cpu(), ref_out) < 1e-4
 
 
+@pytest.mark.parametrize("tile", [20, 21, 22, 23])
+@pytest.mark.parametrize("prologue", [False, True])
+@pytest.mark.parametrize("case", [(4, 15, 15, 64, 96, 3, 2), (2, 14, 14, 128, 256, 3, 1), (3, 7, 7, 512, 200, 1, 1),
+                                  (2, 9, 9, 24, 40, 3, 1)])
+def test_conv_pipelined_tiles_match_reference(tile, prologue, case):
+    """The pipelined LDS-DMA conv kernels (DTM_CONV_TILE=20..23; ring of k-tiles, counted vmcnt, the
+    BatchNorm-apply prologue transformed in LDS) against the fp32 reference: forward (with and without
+    the prologue, zero padding kept zero), dgrad (stride-2 through the dilated path)."""
+    import ctypes
+
+    from distributed_tensorflow_models_amd.ops import _lib
+    from distributed_tensorflow_models_amd.ops.geometry import conv_geom
+    N, H, W, C, K, R, st = case
+    torch.manual_seed(0)
+    L = _lib.lib()
+    x = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(K, R, R, C, device=DEV) / (R * R * C) ** 0.5).to(torch.bfloat16)
+    sc = torch.rand(C, device=DEV) + 0.5
+    sh = torch.randn(C, device=DEV) * 0.5
+    g = conv_geom(tuple(x.shape), tuple(w.shape), st, "SAME")
+    d = g.as_desc(_lib.ConvDesc)
+    xin = torch.relu(x.float() * sc + sh).to(torch.bfloat16).float() if prologue else x.float()
+    yr = ref.conv2d(xin, w.float(), None, st, "SAME")
+    dy = torch.randn_like(yr).to(torch.bfloat16)
+    xr = xin.clone().requires_grad_()
+    ref.conv2d(xr, w.float(), None, st, "SAME").backward(dy.float())
+    wt = torch.empty(C, R, R, K, device=DEV, dtype=torch.bfloat16)
+    L.dtm_weight_flip_transpose(_lib.ptr(w), _lib.ptr(wt), K, R, R, C, _lib.stream_ptr())
+    y = torch.empty(N, g.P, g.Q, K, device=DEV, dtype=torch.bfloat16)
+    dx = torch.empty_like(x)
+    L.dtm_conv_set_tile(tile)
+    try:
+        rc = L.dtm_conv_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(y), None, None, _lib.ptr(sc) if prologue else None,
+                            _lib.ptr(sh) if prologue else None, 0, ctypes.byref(d), _lib.stream_ptr())
+        assert rc == 0
+        rc = L.dtm_conv_dgrad(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), _lib.stream_ptr())
+        assert rc == 0
+        torch.cuda.synchronize()
+    finally:
+        L.dtm_conv_set_tile(-1)
+    assert _rel(y, yr) < 1e-2
+    assert _rel(dx, xr.grad) < 1e-2
+
+
 @pytest.mark.parametrize("tile", [10, 11, 12])
 def test_conv_lds_dma_tiles_match_default(tile):
     """The opt-in LDS-DMA conv kernels (DTM_CONV_TILE=10..12) give the default kernel's results

@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""A/B sweep of the conv_nt tile variants (DTM_CONV_TILE ids) on the ResNet-50 shapes, in ONE process
+with interleaved rounds (per-shape median over rounds): forward, forward with the BatchNorm-apply
+prologue, and dgrad.  Usage: TILES=-1,20,21 python tools/conv_tile_sweep.py"""
+import ctypes
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_tensorflow_models_amd.ops import _lib  # noqa: E402
+from distributed_tensorflow_models_amd.ops.geometry import conv_geom  # noqa: E402
+from tools.conv_microbench import SHAPES  # noqa: E402
+
+B = int(os.environ.get("B", "256"))
+TILES = [int(t) for t in os.environ.get("TILES", "-1,20,21,22,23").split(",")]
+ROUNDS = int(os.environ.get("ROUNDS", "3"))
+ONLY = os.environ.get("ONLY")
+
+
+def timed(fn, n=10):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    s.record()
+    for _ in range(n):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / n * 1e3  # us
+
+
+def main():
+    L = _lib.lib()
+    st = _lib.stream_ptr()
+    print("%-24s %-6s " % ("shape", "pass") + " ".join("%8s" % ("t%d" % t) for t in TILES) + "   best", flush=True)
+    tot = {t: 0.0 for t in TILES}
+    for (H, C, K, R, stride, pad, cnt) in SHAPES[1:]:
+        if ONLY and ONLY not in "%d_%d_%d_%d" % (H, C, K, R):
+            continue
+        x = torch.randn(B, H, H, C, device="cuda").to(torch.bfloat16)
+        w = (torch.randn(K, R, R, C, device="cuda") * 0.05).to(torch.bfloat16)
+        g = conv_geom(tuple(x.shape), tuple(w.shape), stride, (pad, pad))
+        d = g.as_desc(_lib.ConvDesc)
+        y = torch.empty(B, g.P, g.Q, K, device="cuda", dtype=torch.bfloat16)
+        dy = torch.randn_like(y)
+        wt = torch.empty(C, R, R, K, device="cuda", dtype=torch.bfloat16)
+        L.dtm_weight_flip_transpose(_lib.ptr(w), _lib.ptr(wt), K, R, R, C, st)
+        dx = torch.empty_like(x)
+        sc = torch.rand(C, device="cuda") + 0.5
+        sh = torch.randn(C, device="cuda") * 0.1
+        passes = {
+            "fwd": lambda: L.dtm_conv_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(y), None, None, None, None, 0,
+                                          ctypes.byref(d), st),
+            "fwd+p": lambda: L.dtm_conv_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(y), None, None, _lib.ptr(sc),
+                                            _lib.ptr(sh), 0, ctypes.byref(d), st),
+            "dgrad": lambda: L.dtm_conv_dgrad(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), st),
+        }
+        if os.environ.get("WGRAD"):
+            dw = torch.zeros(K, R, R, C, device="cuda")
+            ss4 = torch.stack([sc, sh, sh, sc]).contiguous()
+            mask = torch.empty(x.numel() // 8, device="cuda", dtype=torch.uint8)
+            xa = torch.empty_like(x)
+            ext = {
+                "wgrad": lambda: L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(dw), None, None, ctypes.byref(d),
+                                                  _lib.num_cus(), st),
+                "wgrad+p": lambda: L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(dw), _lib.ptr(sc), _lib.ptr(sh),
+                                                    ctypes.byref(d), _lib.num_cus(), st),
+                "apply": lambda: L.dtm_bn_apply2(_lib.ptr(x), _lib.ptr(ss4), None, None, _lib.ptr(xa), _lib.ptr(mask),
+                                                 x.numel() // C, C, 0, 1, st),
+            }
+            for pname, fn in ext.items():
+                v = statistics.median([timed(fn) for _ in range(ROUNDS)])
+                print("H%-3d C%-4d K%-4d R%d s%d x%d %-7s %8.1f" % (H, C, K, R, stride, cnt, pname, v), flush=True)
+        for pname, fn in passes.items():
+            res = {t: [] for t in TILES}
+            for _ in range(ROUNDS):
+                for t in TILES:
+                    L.dtm_conv_set_tile(t)
+                    res[t].append(timed(fn))
+            L.dtm_conv_set_tile(-1)
+            med = {t: statistics.median(v) for t, v in res.items()}
+            for t in TILES:
+                tot[t] += med[t] * cnt
+            best = min(med, key=med.get)
+            print("H%-3d C%-4d K%-4d R%d s%d x%d %-6s " % (H, C, K, R, stride, cnt, pname) +
+                  " ".join("%8.1f" % med[t] for t in TILES) + "   t%d" % best, flush=True)
+    print("weighted total (us): " + " ".join("t%d=%.0f" % (t, v) for t, v in tot.items()), flush=True)
+
+
+if __name__ == "__main__":
+    main()
