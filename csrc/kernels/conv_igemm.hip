@@ -944,6 +944,166 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
   }
 }
 
+// Pipelined LDS-DMA weight gradient (no input prologue): both pixel-major operand tiles go global ->
+// LDS by LDS-DMA straight into the [k/4][row/16][4][16] transposed-read image.  An LDS-DMA writes
+// lane-linear 16-B slots, so each lane loads the chunk whose tr_off position is its slot (the inverse
+// of tr_off, fixed per lane for every k-tile).  NS-slot ring, one raw barrier per k-tile, counted
+// vmcnt; waves 2x2 of (MT/2) x (NT/2).
+template <int ROWS>
+__device__ __forceinline__ void tr_inv(int q, int& k, int& m) {
+  constexpr int MB = ROWS / 16;
+  const int b1 = q >> 3, kq = b1 / MB;
+  k = kq * 4 + ((q & 7) >> 1);
+  const int b = b1 ^ ((kq >> 1) & 1);
+  m = (b % MB) * 16 + (q & 1) * 8;
+}
+
+template <int MT, int NT, int NS>
+__global__ __launch_bounds__(256) void conv_wgrad_pipe_kernel(ConvWgradArgs a) {
+  constexpr int BK = 64;
+  constexpr int WM = MT / 2, WN = NT / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int AI = MT / 32, BI = NT / 32;  // 1-KiB DMA pieces per wave per k-tile
+  constexpr int G = AI + BI;
+  constexpr int BUF = BK * (MT + NT) * 2;
+  __shared__ __attribute__((aligned(16))) char smem[NS * BUF];
+  typedef __attribute__((address_space(1))) const void gvoid;
+  typedef __attribute__((address_space(3))) void lvoid;
+  static_assert(G <= 31 && NS >= 2 && NS <= 3, "vmcnt range");
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int gxy = gridDim.x * gridDim.y;
+  const int tile = xcd_remap((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x, gxy * gridDim.z);
+  const int bz = tile / gxy, by = (tile % gxy) / gridDim.x, bx = tile % gridDim.x;
+  const int wm = wave % 2, wn = wave / 2;
+  const int n0 = bx * NT, m0 = by * MT;
+  const int pix_lo = bz * a.pix_per_split;
+  const int pix_hi = min(a.Mpix, pix_lo + a.pix_per_split);
+
+  // per-lane chunk coordinates of its DMA slots
+  int a_k[AI], a_off[AI];
+  bool a_colv[AI];
+#pragma unroll
+  for (int j = 0; j < AI; ++j) {
+    int k, m;
+    tr_inv<MT>((wave + 4 * j) * 64 + lane, k, m);
+    a_k[j] = k;
+    a_colv[j] = m0 + m < a.K;
+    a_off[j] = m0 + m;
+  }
+  int b_k[BI], b_r[BI], b_s[BI], b_c[BI];
+  bool b_colv[BI];
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    int k, m;
+    tr_inv<NT>((wave + 4 * j) * 64 + lane, k, m);
+    b_k[j] = k;
+    const int col = n0 + m;
+    b_colv[j] = col < a.Kg;
+    const int tap = col / a.C;
+    b_c[j] = col - tap * a.C;
+    b_r[j] = tap / a.S;
+    b_s[j] = tap - b_r[j] * a.S;
+  }
+  const char* xg = (const char*)a.x;
+  const char* dg = (const char*)a.dy;
+  const char* zg = (const char*)a.in_shift;  // the host passes a zero chunk here (no prologue in this kernel)
+
+  auto issue = [&](int pbase, int slot) {
+    char* base = smem + slot * BUF;
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+      const int pix = pbase + a_k[j];
+      const bool v = (pix < pix_hi) & a_colv[j];
+      const char* src = dg + (size_t)(uint32_t)((pix * a.K + a_off[j]) * 2);
+      __builtin_amdgcn_global_load_lds((gvoid*)(v ? src : zg), (lvoid*)(base + (wave + 4 * j) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+      const int pix = pbase + b_k[j];
+      const uint32_t n = fdiv((uint32_t)pix, a.fd_PQ);
+      const uint32_t rem = pix - n * (a.P * a.Q);
+      const uint32_t p = fdiv(rem, a.fd_Q);
+      const uint32_t q = rem - p * a.Q;
+      const int ih = (int)p * a.stride - a.pad_h + b_r[j];
+      const int iw = (int)q * a.stride - a.pad_w + b_s[j];
+      const bool v = (pix < pix_hi) & b_colv[j] & ((unsigned)ih < (unsigned)a.H) & ((unsigned)iw < (unsigned)a.W);
+      const char* src = xg + (size_t)(uint32_t)(((((int)n * a.H + ih) * a.W + iw) * a.C + b_c[j]) * 2);
+      __builtin_amdgcn_global_load_lds((gvoid*)(v ? src : zg), (lvoid*)(base + BK * MT * 2 + (wave + 4 * j) * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
+  typedef __attribute__((address_space(3))) short4v lds_s4;
+  typedef __attribute__((address_space(3))) char lds_c;
+  auto compute = [&](int slot) {
+    lds_c* lbase = (lds_c*)(smem + slot * BUF);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      short8 af[TM], bfr[TN];
+      const int kb = ks * 32 + 8 * g;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = wm * WM + i * 16 + 4 * tp;
+        short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lbase + tr_off<MT>(kb + tq, m)));
+        short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lbase + tr_off<MT>(kb + 4 + tq, m)));
+        af[i] = (short8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = wn * WN + j * 16 + 4 * tp;
+        short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lbase + BK * MT * 2 + tr_off<NT>(kb + tq, n)));
+        short4v hi =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lbase + BK * MT * 2 + tr_off<NT>(kb + 4 + tq, n)));
+        bfr[j] = (short8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  const int nk = (pix_hi - pix_lo + BK - 1) / BK;
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) issue(pix_lo + s * BK, s);
+  int slot = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = min(nk - 1, kt + NS - 2) - kt;
+    if (NS >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + NS - 1 < nk) issue(pix_lo + (kt + NS - 1) * BK, slot == 0 ? NS - 1 : slot - 1);
+    compute(slot);
+    slot = slot == NS - 1 ? 0 : slot + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float* slab = a.dw + (size_t)bz * a.K * a.Kg;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn * WN + j * 16 + li;
+      const int ko = m0 + wm * WM + i * 16 + g * 4;
+      if (col < a.Kg) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (ko + r < a.K) slab[(size_t)(ko + r) * a.Kg + col] = acc[i][j][r];
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // weight re-layouts
 // dgrad weight: Wt[c][R-1-r][S-1-s][k] = W[k][r][s][c]   (bf16 -> bf16)
@@ -1041,7 +1201,7 @@ static TileCfg pick_tile(const ConvNTArgs& a) {
   int id = g_tile_env;
   // the pipelined LDS-DMA 128x128 tile (2 slots, 2 blocks/CU) wins every deep-reduction layer without the
   // prologue (tools/conv_tile_sweep.py: 3x3 at 14x14 / 7x7 -13..-18 %, deep 1x1 -5..-16 %)
-  if (id < 0 && !a.in_scale && a.Kg >= 1024) id = 21;
+  if (id == -1 && !a.in_scale && a.Kg >= 1024) id = 21;  // (-3: the policy without it, for A/B runs)
   if (id < 0) id = a.K <= 64 ? 3 : ((a.M <= 16384 && a.Kg >= 2048) ? 0 : 4);
   // LDS-DMA variants (10-12, opt-in) need an operand without the prologue affine
   if (id >= 10 && id < 20 && a.in_scale) id = a.K <= 64 ? 3 : 4;
@@ -1193,6 +1353,15 @@ static void launch_wgrad(const ConvWgradArgs& a, int splits, hipStream_t st) {
   hipLaunchKernelGGL((conv_wgrad_kernel<MT, NT, WM, WN, NBUF>), grid, dim3(256), 0, st, a);
 }
 
+// wgrad tile override (-1 = policy) and the blocks-per-CU target of the split count for the pipelined
+// kernels (A/B sweeps: tools/conv_tile_sweep.py)
+static int g_wgrad_env = -2;
+static int g_wgrad_occ = 4;
+DTM_API void dtm_conv_set_wgrad_tile(int id, int occ) {
+  g_wgrad_env = id;
+  if (occ > 0) g_wgrad_occ = occ;
+}
+
 DTM_API int dtm_conv_wgrad(const void* x, const void* dy, float* dw, const float* in_scale,
                            const float* in_shift, const ConvDesc* d, int num_cus, void* stream) {
   if (d->C % 8 || d->K % 8) return -1;
@@ -1208,18 +1377,28 @@ DTM_API int dtm_conv_wgrad(const void* x, const void* dy, float* dw, const float
   a.fd_PQ = make_fastdiv(d->P * d->Q); a.fd_Q = make_fastdiv(d->Q);
   // wgrad tile variants: 0 = 128 (K) x 128 (RSC) 2 LDS buffers, 1 = 64 x 128, 2 = 64 x 128 single
   // buffer, 3 = 128 x 128 single buffer.  DTM_WGRAD_TILE forces one (A/B experiments).
-  static int wenv = -2;
-  if (wenv == -2) {
+  if (g_wgrad_env == -2) {
     const char* e = getenv("DTM_WGRAD_TILE");
-    wenv = e ? atoi(e) : -1;
+    g_wgrad_env = e ? atoi(e) : -1;
   }
+  const int wenv = g_wgrad_env;
   int wt = wenv >= 0 ? wenv : (d->K <= 64 ? 1 : 0);
+  int occ = g_wgrad_occ;
+  // policy (tools/conv_tile_sweep.py WTILES sweep, ResNet-50 shapes): the pipelined kernel at 2 blocks
+  // per CU wins every layer with K > 64 (-10..-25 %); 4 blocks' worth of splits for the deep 3x3 7x7s
+  if (wenv == -1 && !in_scale && d->K > 64) {  // (-3: the policy without it, for A/B runs)
+    wt = 10;
+    occ = (d->R * d->S > 1 && a.Mpix <= 16384) ? 4 : 2;
+  }
+  if (wt >= 10 && in_scale) wt = d->K <= 64 ? 1 : 0;  // the pipelined kernels have no input prologue
   const bool small_m = (wt == 1 || wt == 2);
   const int MT = small_m ? 64 : 128, NT = 128;
   long tiles = (long)((a.Kg + NT - 1) / NT) * ((a.K + MT - 1) / MT);
-  long target = (long)num_cus * 3;
+  long target = (long)num_cus * (wt >= 10 ? occ : 3);
   long ksteps = (a.Mpix + 63) / 64;
-  long splits = (target + tiles - 1) / tiles;
+  // the pipelined kernels run 2 blocks/CU: fill whole rounds of resident blocks (floor), a last
+  // round with a few blocks doubles a layer's time
+  long splits = wt >= 10 ? target / tiles : (target + tiles - 1) / tiles;
   if (splits > ksteps) splits = ksteps;
   if (splits < 1) splits = 1;
   long steps_per = (ksteps + splits - 1) / splits;
@@ -1228,7 +1407,14 @@ DTM_API int dtm_conv_wgrad(const void* x, const void* dy, float* dw, const float
   float* ws = dtm_ws_get((size_t)splits * a.K * a.Kg);
   if (!ws) return -4;
   a.dw = ws;
-  if (wt == 1) launch_wgrad<64, 128, 32, 64>(a, (int)splits, (hipStream_t)stream);
+  if (wt >= 10) {
+    a.in_shift = (const float*)zero_chunk();  // the zero DMA source
+    dim3 grid((a.Kg + NT - 1) / NT, (a.K + MT - 1) / MT, splits);
+    if (wt == 11)
+      hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 128, 3>), grid, dim3(256), 0, (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 128, 2>), grid, dim3(256), 0, (hipStream_t)stream, a);
+  } else if (wt == 1) launch_wgrad<64, 128, 32, 64>(a, (int)splits, (hipStream_t)stream);
   else if (wt == 2) launch_wgrad<64, 128, 32, 64, 1>(a, (int)splits, (hipStream_t)stream);
   else if (wt == 3) launch_wgrad<128, 128, 64, 64, 1>(a, (int)splits, (hipStream_t)stream);
   else launch_wgrad<128, 128, 64, 64>(a, (int)splits, (hipStream_t)stream);

@@ -177,6 +177,39 @@ def test_conv_pipelined_tiles_match_reference(tile, prologue, case):
     assert _rel(dx, xr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("tile", [10, 11])
+@pytest.mark.parametrize("case", [(4, 15, 15, 64, 96, 3, 2), (2, 14, 14, 128, 256, 3, 1), (3, 7, 7, 512, 200, 1, 1),
+                                  (2, 9, 9, 24, 40, 3, 1), (5, 8, 8, 64, 64, 1, 1)])
+def test_conv_wgrad_pipelined_tiles_match_reference(tile, case):
+    """The pipelined LDS-DMA wgrad kernels (inverse transposed-read image mapping for the DMA slots,
+    split-K slabs) against the fp32 reference, including K / R*S*C tails and empty splits."""
+    import ctypes
+
+    from distributed_tensorflow_models_amd.ops import _lib
+    from distributed_tensorflow_models_amd.ops.geometry import conv_geom
+    N, H, W, C, K, R, st = case
+    torch.manual_seed(0)
+    L = _lib.lib()
+    x = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(K, R, R, C, device=DEV) / (R * R * C) ** 0.5).to(torch.bfloat16)
+    g = conv_geom(tuple(x.shape), tuple(w.shape), st, "SAME")
+    d = g.as_desc(_lib.ConvDesc)
+    wr = w.float().clone().requires_grad_()
+    yr = ref.conv2d(x.float(), wr, None, st, "SAME")
+    dy = torch.randn_like(yr).to(torch.bfloat16)
+    yr.backward(dy.float())
+    dw = torch.zeros(K, R, R, C, device=DEV)
+    L.dtm_conv_set_wgrad_tile(tile, 0)
+    try:
+        rc = L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(dw), None, None, ctypes.byref(d), _lib.num_cus(),
+                              _lib.stream_ptr())
+        assert rc == 0
+        torch.cuda.synchronize()
+    finally:
+        L.dtm_conv_set_wgrad_tile(-1, 0)
+    assert _rel(dw, wr.grad) < 1e-2
+
+
 @pytest.mark.parametrize("tile", [10, 11, 12])
 def test_conv_lds_dma_tiles_match_default(tile):
     """The opt-in LDS-DMA conv kernels (DTM_CONV_TILE=10..12) give the default kernel's results

@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Same-process A/B of whole ResNet-50 training steps under kernel-policy variants (interleaved rounds,
+median ms/step per variant; one device, one process: MI355X_MICROARCH 'DVFS give-back' / rule 24).
+
+VARIANTS="base=;noW=wtile:-3;noT=tile:-3;fused=prologue:fused" python tools/ab_step.py
+keys: tile (conv_nt tile id), wtile[:occ] (wgrad tile id / blocks-per-CU target), prologue (DTM_PROLOGUE)."""
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_tensorflow_models_amd.engine import TrainStep  # noqa: E402
+from distributed_tensorflow_models_amd.models import nets_factory  # noqa: E402
+from distributed_tensorflow_models_amd.ops import _lib  # noqa: E402
+
+
+def apply(cfg):
+    L = _lib.lib()
+    L.dtm_conv_set_tile(int(cfg.get("tile", -1)))
+    wt = cfg.get("wtile", "-1").split(":")
+    L.dtm_conv_set_wgrad_tile(int(wt[0]), int(wt[1]) if len(wt) > 1 else 0)
+    os.environ["DTM_PROLOGUE"] = cfg.get("prologue", "auto")
+
+
+def main():
+    variants = []
+    for item in os.environ.get("VARIANTS", "base=").split(";"):
+        name, _, spec = item.partition("=")
+        cfg = dict(kv.split(":", 1) for kv in spec.split(",") if kv)
+        variants.append((name, cfg))
+    B = int(os.environ.get("B", "256"))
+    steps, rounds = int(os.environ.get("STEPS", "6")), int(os.environ.get("ROUNDS", "4"))
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    net = nets_factory.build("resnet_v1_50", num_classes=1000).to(dev)
+    step = TrainStep(net, optimizer="momentum", lr=0.1, momentum=0.9)
+    x = torch.randn(B, 224, 224, 3, device=dev).to(torch.bfloat16)
+    y = torch.randint(0, 1000, (B,), device=dev)
+    res = {n: [] for n, _ in variants}
+    for n, cfg in variants:  # warm every variant (workspace growth, first-touch)
+        apply(cfg)
+        for _ in range(2):
+            step(x, y)
+    torch.cuda.synchronize()
+    for r in range(rounds):
+        for n, cfg in variants:
+            apply(cfg)
+            step(x, y)
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for _ in range(steps):
+                step(x, y)
+            torch.cuda.synchronize()
+            res[n].append((time.perf_counter() - t) / steps * 1e3)
+        print("round %d: " % r + " ".join("%s=%.3f" % (n, res[n][-1]) for n, _ in variants), flush=True)
+    base = statistics.median(res[variants[0][0]])
+    for n, _ in variants:
+        m = statistics.median(res[n])
+        print("%-10s median %.3f ms/step  min %.3f  (%+.2f %% vs %s)  %.0f img/s" % (
+            n, m, min(res[n]), (m / base - 1) * 100, variants[0][0], B / m * 1e3), flush=True)
+    apply({})
+
+
+if __name__ == "__main__":
+    main()

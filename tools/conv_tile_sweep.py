@@ -36,6 +36,7 @@ def main():
     st = _lib.stream_ptr()
     print("%-24s %-6s " % ("shape", "pass") + " ".join("%8s" % ("t%d" % t) for t in TILES) + "   best", flush=True)
     tot = {t: 0.0 for t in TILES}
+    wtot = {}
     for (H, C, K, R, stride, pad, cnt) in SHAPES[1:]:
         if ONLY and ONLY not in "%d_%d_%d_%d" % (H, C, K, R):
             continue
@@ -73,6 +74,24 @@ def main():
             for pname, fn in ext.items():
                 v = statistics.median([timed(fn) for _ in range(ROUNDS)])
                 print("H%-3d C%-4d K%-4d R%d s%d x%d %-7s %8.1f" % (H, C, K, R, stride, cnt, pname, v), flush=True)
+        if os.environ.get("WTILES"):
+            wts = [tuple(int(u) for u in t.split(":")) for t in os.environ["WTILES"].split(",")]
+            dw = torch.zeros(K, R, R, C, device="cuda")
+            fn = lambda: L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(dw), None, None, ctypes.byref(d),  # noqa
+                                          _lib.num_cus(), st)
+            res = {t: [] for t in wts}
+            for _ in range(ROUNDS):
+                for t in wts:
+                    L.dtm_conv_set_wgrad_tile(t[0], t[1] if len(t) > 1 else 0)
+                    res[t].append(timed(fn))
+            L.dtm_conv_set_wgrad_tile(-1, 4)
+            med = {t: statistics.median(v) for t, v in res.items()}
+            for t in wts:
+                wtot[t] = wtot.get(t, 0.0) + med[t] * cnt
+            print("H%-3d C%-4d K%-4d R%d s%d x%d %-6s " % (H, C, K, R, stride, cnt, "wgrad") +
+                  " ".join("%s=%.1f" % (":".join(map(str, t)), med[t]) for t in wts), flush=True)
+            if os.environ.get("WONLY"):
+                continue
         for pname, fn in passes.items():
             res = {t: [] for t in TILES}
             for _ in range(ROUNDS):
@@ -87,6 +106,8 @@ def main():
             print("H%-3d C%-4d K%-4d R%d s%d x%d %-6s " % (H, C, K, R, stride, cnt, pname) +
                   " ".join("%8.1f" % med[t] for t in TILES) + "   t%d" % best, flush=True)
     print("weighted total (us): " + " ".join("t%d=%.0f" % (t, v) for t, v in tot.items()), flush=True)
+    if wtot:
+        print("wgrad weighted total (us): " + " ".join("%s=%.0f" % (":".join(map(str, t)), v) for t, v in wtot.items()))
 
 
 if __name__ == "__main__":
