@@ -60,6 +60,7 @@ struct ConvNTArgs {
   float* act_sums;        //   partial rows per pixel tile: [sum g*act_x (K) | sum g (K)]
   const bf16_t* zero;     // >= 16 B of zeros: the LDS-DMA source of padding / out-of-range chunks
   int act_unscaled;       // act path: out <- g (not g*scale); the producer's conv+BN backward scales it
+  int pix_bytes;          // byte pitch of one input pixel (C*2, or less for the packed-row stem view)
 };
 
 // Shared epilogue of the conv_nt kernels (register-staged and LDS-DMA): acc[TC][TP] of wave (wp, wc)
@@ -287,7 +288,7 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
       bool v = kin && ihv >= 0 && ihv < a.Hv && iwv >= 0 && iwv < a.Wv;
       if (UD > 1) v = v && ((ihv % UD) == 0) && ((iwv % UD) == 0);
       int ih = UD > 1 ? ihv / UD : ihv, iw = UD > 1 ? iwv / UD : iwv;
-      uint32_t off = v ? (uint32_t)(((pixbase[i] + ih * a.Win + iw) * a.C + cc) * 2) : OOB_OFFSET;
+      uint32_t off = v ? (uint32_t)((pixbase[i] + ih * a.Win + iw) * a.pix_bytes + cc * 2) : OOB_OFFSET;
       st.v[i] = v;
       st.a[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
     }
@@ -473,7 +474,7 @@ __global__ __launch_bounds__(256) void conv_nt_dma_kernel(ConvNTArgs a) {
       bool v = kin && ihv >= 0 && ihv < a.Hv && iwv >= 0 && iwv < a.Wv;
       if (UD > 1) v = v && ((ihv % UD) == 0) && ((iwv % UD) == 0);
       const int ih = UD > 1 ? ihv / UD : ihv, iw = UD > 1 ? iwv / UD : iwv;
-      const char* src = v ? xg + (size_t)((pixbase[j] + ih * a.Win + iw) * a.C + cc) * 2 : zg;
+      const char* src = v ? xg + (size_t)((pixbase[j] + ih * a.Win + iw) * a.pix_bytes + cc * 2) : zg;
       __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(base + (wave + 4 * j) * 1024), 16, 0, 0);
     }
 #pragma unroll
@@ -617,7 +618,7 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
     for (int j = 0; j < AI; ++j) {
       int ih, iw;
       const bool v = kin & valid_at(j, rr, ss, ih, iw);
-      const char* src = xg + (size_t)(uint32_t)(((pixbase[j] + ih * a.Win + iw) * a.C + cc) * 2);
+      const char* src = xg + (size_t)(uint32_t)((pixbase[j] + ih * a.Win + iw) * a.pix_bytes + cc * 2);
       __builtin_amdgcn_global_load_lds((gvoid*)(v ? src : zg), (lvoid*)(base + (wave + 4 * j) * 1024), 16, 0, 0);
     }
 #pragma unroll
@@ -740,6 +741,7 @@ struct ConvWgradArgs {
   int Kg;    // R*S*C
   int pix_per_split;
   FastDiv fd_PQ, fd_Q;
+  int pix_bytes;  // byte pitch of one x pixel (C*2, or less for the packed-row stem view)
 };
 
 // byte offset of element (k, m) in a [64 k][ROWS] tile stored as [k/4][m/16][4][16] blocks,
@@ -835,7 +837,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
       int ih = (int)p * a.stride - a.pad_h + b_r[i];
       int iw = (int)q * a.stride - a.pad_w + b_s[i];
       v = v && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-      uint32_t off = v ? (uint32_t)(((((int)n * a.H + ih) * a.W + iw) * a.C + b_c[i]) * 2) : OOB_OFFSET;
+      uint32_t off = v ? (uint32_t)((((int)n * a.H + ih) * a.W + iw) * a.pix_bytes + b_c[i] * 2) : OOB_OFFSET;
       bval[i] = v;
       bcc[i] = b_c[i];
       breg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
@@ -1028,7 +1030,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_pipe_kernel(ConvWgradArgs a) {
       const int ih = (int)p * a.stride - a.pad_h + b_r[j];
       const int iw = (int)q * a.stride - a.pad_w + b_s[j];
       const bool v = (pix < pix_hi) & b_colv[j] & ((unsigned)ih < (unsigned)a.H) & ((unsigned)iw < (unsigned)a.W);
-      const char* src = xg + (size_t)(uint32_t)(((((int)n * a.H + ih) * a.W + iw) * a.C + b_c[j]) * 2);
+      const char* src = xg + (size_t)(uint32_t)((((int)n * a.H + ih) * a.W + iw) * a.pix_bytes + b_c[j] * 2);
       __builtin_amdgcn_global_load_lds((gvoid*)(v ? src : zg), (lvoid*)(base + BK * MT * 2 + (wave + 4 * j) * 1024),
                                        16, 0, 0);
     }
@@ -1152,6 +1154,7 @@ using namespace dtm;
 // whole training step can be captured in one hipGraph)
 struct ConvDesc {
   int N, H, W, C, K, R, S, P, Q, stride, pad_h, pad_w;
+  int pix_bytes;  // 0 = C*2 (dense NHWC); else the input pixel pitch in bytes (packed-row stem view)
 };
 
 static const bf16_t* zero_chunk() {
@@ -1251,7 +1254,8 @@ static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, cons
   a.add_stride = 1; a.add_H = a.add_W = 0;
   a.act_unscaled = 0;
   a.zero = zero_chunk();
-  size_t xb = (size_t)d->N * d->H * d->W * d->C * 2, wb = (size_t)d->K * d->R * d->S * d->C * 2;
+  a.pix_bytes = d->pix_bytes > 0 ? d->pix_bytes : d->C * 2;
+  size_t xb = (size_t)d->N * d->H * d->W * a.pix_bytes, wb = (size_t)d->K * d->R * d->S * d->C * 2;
   if (xb >= (1ull << 31) || wb >= (1ull << 31)) return -2;
   a.x_bytes = (uint32_t)xb; a.w_bytes = (uint32_t)wb;
   a.N = d->N; a.Hin = d->H; a.Win = d->W; a.C = d->C; a.K = d->K; a.R = d->R; a.S = d->S;
@@ -1322,6 +1326,7 @@ DTM_API int dtm_conv_dgrad_ex(const void* dy, const void* wt, void* dx, const Co
   a.act_unscaled = act_unscaled;
   a.zero = zero_chunk();
   a.add_H = (d->H - 1) / add_stride + 1; a.add_W = (d->W - 1) / add_stride + 1;
+  a.pix_bytes = d->K * 2;
   size_t xb = (size_t)d->N * d->P * d->Q * d->K * 2, wb = (size_t)d->K * d->R * d->S * d->C * 2;
   if (xb >= (1ull << 31) || wb >= (1ull << 31)) return -2;
   a.x_bytes = (uint32_t)xb; a.w_bytes = (uint32_t)wb;
@@ -1368,7 +1373,8 @@ DTM_API int dtm_conv_wgrad(const void* x, const void* dy, float* dw, const float
   ConvWgradArgs a;
   a.x = (const bf16_t*)x; a.dy = (const bf16_t*)dy; a.dw = dw;
   a.in_scale = in_scale; a.in_shift = in_shift;
-  size_t xb = (size_t)d->N * d->H * d->W * d->C * 2, yb = (size_t)d->N * d->P * d->Q * d->K * 2;
+  a.pix_bytes = d->pix_bytes > 0 ? d->pix_bytes : d->C * 2;
+  size_t xb = (size_t)d->N * d->H * d->W * a.pix_bytes, yb = (size_t)d->N * d->P * d->Q * d->K * 2;
   if (xb >= (1ull << 31) || yb >= (1ull << 31)) return -2;
   a.x_bytes = (uint32_t)xb; a.dy_bytes = (uint32_t)yb;
   a.N = d->N; a.H = d->H; a.W = d->W; a.C = d->C; a.K = d->K; a.R = d->R; a.S = d->S;

@@ -18,7 +18,7 @@ _lib = None
 
 class ConvDesc(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in
-                ("N", "H", "W", "C", "K", "R", "S", "P", "Q", "stride", "pad_h", "pad_w")]
+                ("N", "H", "W", "C", "K", "R", "S", "P", "Q", "stride", "pad_h", "pad_w", "pix_bytes")]
 
 
 class PoolArgs(ctypes.Structure):

@@ -328,6 +328,100 @@ class _BNApplyFn(torch.autograd.Function):
         return dx, sx, dres, sr, None, None, None, None
 
 
+class _StemConvBNFn(torch.autograd.Function):
+    """Training/inference conv+BN of a stem convolution (few input channels, stride 2, explicit pad;
+    the ResNet 7x7/2 on RGB: reference vgg/nets/resnet_v1.py:226 via resnet_utils.conv2d_same) as a
+    packed-row implicit GEMM.  The zero-bordered input is stored [N][Hp][Wp][4] (8-byte pixels), so
+    one kernel row of taps for one output pixel -- S taps x 4 channels -- is a single contiguous
+    64-byte run: the conv is run as an R x 1 conv over 32 'channels' with an 8-byte pixel pitch
+    (ConvDesc.pix_bytes).  Reduction K*R*S*C = 7*32 = 224 instead of 7*7*8 = 392 (C padded to 8), and
+    64-B contiguous gathers instead of 16-B ones.  No input gradient (images)."""
+
+    @staticmethod
+    def forward(ctx, x, w, gamma, beta, geom, bn, pad):
+        L = _lib.lib()
+        s = _lib.stream_ptr()
+        N, H, W, C = x.shape
+        K, R, S, _ = w.shape
+        st, P, Q = geom.stride, geom.P, geom.Q
+        Hp = max(H + 2 * pad, st * (P - 1) + R)
+        Wp = max(W + 2 * pad, st * (Q - 1) + 8)
+        Wp += Wp % 2  # 16-B aligned rows (the 64-B runs start at 16*q bytes)
+        xp = torch.nn.functional.pad(x.to(torch.bfloat16), (0, 4 - C, pad, Wp - W - pad, pad, Hp - H - pad))
+        wv = torch.zeros((K, R, 8, 4), device=x.device, dtype=torch.bfloat16)
+        wv[:, :, :S, :C] = weight_bf16(w)
+        d = _lib.ConvDesc(N, Hp, Wp, 32, K, R, 1, P, Q, st, 0, 0, 8)
+        y = torch.empty((N, P, Q, K), device=x.device, dtype=torch.bfloat16)
+        ss = None
+        if bn is not None:
+            ss = torch.empty((4, K), device=x.device, dtype=torch.float32)
+            ctx.count = float(N * P * Q)
+            _check(L.dtm_conv_fwd_bn(_lib.ptr(xp), _lib.ptr(wv), _lib.ptr(y), None, None, _lib.ptr(gamma),
+                                     _lib.ptr(beta), _lib.ptr(bn.moving_mean), _lib.ptr(bn.moving_variance),
+                                     _lib.ptr(ss), ctx.count, float(bn.eps), float(bn.decay), 1, int(bn.bessel),
+                                     ctypes.byref(d), s), "stem_conv_fwd_bn")
+        else:
+            _check(L.dtm_conv_fwd(_lib.ptr(xp), _lib.ptr(wv), _lib.ptr(y), None, None, None, None, 0,
+                                  ctypes.byref(d), s), "stem_conv_fwd")
+        ctx.d = (N, Hp, Wp, K, R, S, C, P, Q, st)
+        ctx.save_for_backward(xp, w, y, ss, gamma, beta)
+        if ss is None:
+            return y
+        return y, ss
+
+    @staticmethod
+    def backward(ctx, dy, dss=None):
+        L = _lib.lib()
+        s = _lib.stream_ptr()
+        xp, w, y, ss, gamma, beta = ctx.saved_tensors
+        N, Hp, Wp, K, R, S, C, P, Q, st = ctx.d
+        dy = dy.contiguous()
+        dgamma = dbeta = None
+        if ss is not None and dss is not None:
+            gmg = getattr(gamma, "main_grad", None) if gamma is not None else None
+            bmg = getattr(beta, "main_grad", None) if beta is not None else None
+            if gamma is not None and gmg is None:
+                dgamma = torch.zeros(K, device=dy.device)
+            if beta is not None and bmg is None:
+                dbeta = torch.zeros(K, device=dy.device)
+            comb = torch.empty_like(dy)
+            _check(L.dtm_stats_combine_fin(_lib.ptr(dy), _lib.ptr(y), _lib.ptr(dss.contiguous()), _lib.ptr(ss),
+                                           _lib.ptr(gamma), ctx.count,
+                                           _lib.ptr(gmg if gmg is not None else dgamma),
+                                           _lib.ptr(bmg if bmg is not None else dbeta), _lib.ptr(comb), N * P * Q, K,
+                                           1, s), "stats_combine_fin")
+            if gmg is not None:
+                _notify(gamma)
+            if bmg is not None:
+                _notify(beta)
+            dy = comb
+        elif ss is not None:
+            dy = (dy.float() * ss[0]).to(dy.dtype)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            d = _lib.ConvDesc(N, Hp, Wp, 32, K, R, 1, P, Q, st, 0, 0, 8)
+            tv = torch.zeros((K, R, 8, 4), device=dy.device, dtype=torch.float32)
+            _check(L.dtm_conv_wgrad(_lib.ptr(xp), _lib.ptr(dy), _lib.ptr(tv), None, None, ctypes.byref(d),
+                                    _lib.num_cus(), s), "stem_conv_wgrad")
+            dw = _accum_param_grad(w, tv[:, :, :S, :C])
+        return None, dw, dgamma, dbeta, None, None, None
+
+
+def _stem_eligible(x, w, stride, padding):
+    """The packed-row stem path: a plain (non-lazy) input without gradient, <= 4 channels, stride 2,
+    S <= 7 taps per kernel row (S x 4 channels fit one 64-byte run), symmetric explicit padding."""
+    import os
+    if os.environ.get("DTM_STEM", "1") == "0" or isinstance(x, (LazyBN, Subsampled)):
+        return False
+    if not (x.is_cuda and x.dim() == 4 and w.dim() == 4) or x.requires_grad:
+        return False
+    K, R, S, C = w.shape
+    st = stride if isinstance(stride, int) else stride[0]
+    if isinstance(padding, str) or not isinstance(padding, (tuple, list)) or padding[0] != padding[1]:
+        return False
+    return C <= 4 and x.shape[-1] == C and st == 2 and S <= 7 and K % 4 == 0
+
+
 def bn_apply(raw, ss, relu, residual=None, unscaled=False):
     """y = relu?(raw*scale+shift + residual); residual may be a tensor, a LazyBN (BN'd shortcut) or a
     Subsampled block input (strided identity shortcut).  ``unscaled``: raw's LazyBN.unscaled."""
@@ -390,6 +484,13 @@ def conv_bn(x, w, bn, stride, padding, training, relu):
         else:
             x = x.materialize()
     g = conv_geom(tuple(x.shape), tuple(w.shape), stride, padding)
+    if in_ss is None and _stem_eligible(x, w, stride, padding):
+        if training:
+            y, ss = _StemConvBNFn.apply(x, w, bn.gamma, bn.beta, g, bn, int(padding[0]))
+        else:
+            y = _StemConvBNFn.apply(x, w, None, None, g, None, int(padding[0]))
+            ss = bn_inference_ss(bn)
+        return LazyBN(y, ss, relu, unscaled=training)
     if g.C % 8 != 0:
         from .nn import _PadChannels
         if in_ss is not None:

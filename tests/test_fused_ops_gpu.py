@@ -183,3 +183,35 @@ def test_bn_relu_maxpool_fused(H, pool, pad, st):
     msg = " ".join("%s=%.4f" % kv for kv in errs.items())
     # argmax ties / relu-mask flips from bf16 rounding move a few gradients (see test_conv_bn_chain_prologue)
     assert errs["y"] < 1e-2 and all(v < 1.2e-1 for v in errs.values()), msg
+
+
+@pytest.mark.parametrize("H,W,C,N", [(32, 32, 3, 4), (36, 30, 3, 2), (224, 224, 3, 2), (17, 23, 1, 3)])
+def test_stem_packed_row_conv_bn(H, W, C, N):
+    """The packed-row stem path (7x7/2, explicit pad 3, C <= 4: an R x 1 conv over 32 'channels' with an
+    8-byte pixel pitch) against torch fp32: output, BN moving statistics, weight/gamma/beta grads."""
+    torch.manual_seed(0)
+    x = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(64, 7, 7, C, device=DEV) / (49 * C) ** 0.5).to(torch.bfloat16).float()
+    bn = _bn(64)
+    bn_r = _bn(64)
+    with torch.no_grad():
+        bn_r.gamma.copy_(bn.gamma)
+        bn_r.beta.copy_(bn.beta)
+    assert fused._stem_eligible(x, w, 2, (3, 3))
+    wr = w.clone().requires_grad_()
+    gr, br = bn.gamma.detach().clone().requires_grad_(), bn.beta.detach().clone().requires_grad_()
+    yr = ref.batch_norm(ref.conv2d(x.float(), wr, None, 2, (3, 3)), gr, br, bn_r.moving_mean, bn_r.moving_variance,
+                        True, 0.9, 1e-3, True)
+    gy = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(gy)
+    wk = w.clone().requires_grad_()
+    lz = fused.conv_bn(x, wk, bn, 2, (3, 3), True, True)
+    yk = lz.materialize()
+    assert yk.shape == yr.shape
+    yk.backward(gy.to(torch.bfloat16))
+    torch.cuda.synchronize()
+    errs = dict(y=_rel(yk, yr), dw=_rel(wk.grad, wr.grad), dgamma=_rel(bn.gamma.grad, gr.grad),
+                dbeta=_rel(bn.beta.grad, br.grad), mm=_rel(bn.moving_mean, bn_r.moving_mean),
+                mv=_rel(bn.moving_variance, bn_r.moving_variance))
+    # same bf16 ReLU-mask flip noise on dgamma / dbeta / dw as test_conv_bn_single (tol 5e-2 with relu)
+    assert all(v < 5e-2 for v in errs.values()), errs

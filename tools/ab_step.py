@@ -3,7 +3,8 @@
 median ms/step per variant; one device, one process: MI355X_MICROARCH 'DVFS give-back' / rule 24).
 
 VARIANTS="base=;noW=wtile:-3;noT=tile:-3;fused=prologue:fused" python tools/ab_step.py
-keys: tile (conv_nt tile id), wtile[:occ] (wgrad tile id / blocks-per-CU target), prologue (DTM_PROLOGUE)."""
+keys: tile (conv_nt tile id), wtile[:occ] (wgrad tile id / blocks-per-CU target), prologue (DTM_PROLOGUE),
+stem (DTM_STEM: 1 = packed-row stem path)."""
 import os
 import statistics
 import sys
@@ -23,6 +24,7 @@ def apply(cfg):
     wt = cfg.get("wtile", "-1").split(":")
     L.dtm_conv_set_wgrad_tile(int(wt[0]), int(wt[1]) if len(wt) > 1 else 0)
     os.environ["DTM_PROLOGUE"] = cfg.get("prologue", "auto")
+    os.environ["DTM_STEM"] = cfg.get("stem", "1")
 
 
 def main():
