@@ -61,13 +61,34 @@ struct ConvNTArgs {
   const bf16_t* zero;     // >= 16 B of zeros: the LDS-DMA source of padding / out-of-range chunks
   int act_unscaled;       // act path: out <- g (not g*scale); the producer's conv+BN backward scales it
   int pix_bytes;          // byte pitch of one input pixel (C*2, or less for the packed-row stem view)
+  bf16_t* dump;           // >= 16 B scratch: target of the out-of-range stores of the exact-count epilogue
 };
 
 // Shared epilogue of the conv_nt kernels (register-staged and LDS-DMA): acc[TC][TP] of wave (wp, wc)
 // for the tile at pixel p0 / channel c0; smem must hold PT * (2*CT + 16) bytes and be free.
-template <int PT, int CT, int WP, int WC>
+// RAWB: raw s_barrier (+ lgkmcnt) instead of __syncthreads(), so LDS-DMA prefetches of the next tile stay
+// in flight across the epilogue; EXACT: every thread issues exactly PT*CT/8/256 staged 16-B stores
+// (out-of-range ones go to a.dump), a lower bound the persistent kernel's counted vmcnt relies on.
+template <bool RAWB>
+__device__ __forceinline__ void epi_barrier() {
+  if constexpr (RAWB) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  } else {
+    __syncthreads();
+  }
+}
+
+// STG: 1 = LDS-staged stores (K % 8 == 0), 2 = direct 8-B stores.  Kept compile-time: a runtime choice
+// between an LDS and a global pointer makes hipcc emit flat stores, which wait on both counters.
+// SACC (statistics accumulate, persistent kernels): the BatchNorm sums are not shuffle-reduced per tile;
+// each thread adds the bf16 outputs of its fixed 8-channel chunk column in the staged-store loop to
+// ssum / ssq (registers, across all the block's tiles) and the kernel reduces them once at its end.
+template <int PT, int CT, int WP, int WC, int STG, bool RAWB = false, bool EXACT = false, bool NOBIAS = false,
+          bool SACC = false>
 __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&acc)[WC / 16][WP / 16], char* smem,
-                                                 int p0, int c0, int by) {
+                                                 int p0, int c0, int by, float* ssum = nullptr,
+                                                 float* ssq = nullptr) {
   constexpr int NWP = PT / WP;
   constexpr int TP = WP / 16, TC = WC / 16;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -79,14 +100,14 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
   // full 16-B chunk and consecutive lanes cover whole NHWC pixel rows (coalesced, 256-B rows for
   // CT = 128) instead of 16 scattered 32-B pieces per wave instruction.
   constexpr int OROW = CT * 2 + 16;
-  const bool staged = (a.K & 7) == 0;
+  constexpr bool staged = STG == 1;
 #pragma unroll
   for (int i = 0; i < TC; ++i) {
     const int kloc = wc * WC + i * 16 + fk * 4;
     const int kch = c0 + kloc;
     float bsum[4] = {0.f, 0.f, 0.f, 0.f}, bsq[4] = {0.f, 0.f, 0.f, 0.f};
     float bia[4] = {0.f, 0.f, 0.f, 0.f};
-    if (a.bias && kch < a.K) {
+    if (!NOBIAS && a.bias && kch < a.K) {  // (NOBIAS: no global load whose wait would drain a prefetch)
 #pragma unroll
       for (int r = 0; r < 4; ++r) bia[r] = a.bias[kch + r];
     }
@@ -98,15 +119,15 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         v[r] = acc[i][j][r] + bia[r];
-        if (a.relu) v[r] = fmaxf(v[r], 0.f);
+        if (!NOBIAS && a.relu) v[r] = fmaxf(v[r], 0.f);
       }
       uint32_t lo = pack2bf(v[0], v[1]), hi = pack2bf(v[2], v[3]);
-      if (staged) {
+      if constexpr (staged) {
         *(uint2*)(smem + mloc * OROW + kloc * 2) = make_uint2(lo, hi);
       } else if (m < a.M && kch < a.K) {
         *(uint2*)(a.y + (size_t)m * a.K + kch) = make_uint2(lo, hi);
       }
-      if (a.stats && m < a.M && kch < a.K) {
+      if (!SACC && a.stats && m < a.M && kch < a.K) {
         float q0 = lo_bf(lo), q1 = hi_bf(lo), q2 = lo_bf(hi), q3 = hi_bf(hi);
         bsum[0] += q0; bsq[0] += q0 * q0;
         bsum[1] += q1; bsq[1] += q1 * q1;
@@ -114,7 +135,7 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
         bsum[3] += q3; bsq[3] += q3 * q3;
       }
     }
-    if (a.stats) {
+    if (!SACC && a.stats) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
 #pragma unroll
@@ -131,8 +152,8 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
       }
     }
   }
-  if (staged) {
-    __syncthreads();
+  if constexpr (staged) {
+    epi_barrier<RAWB>();
     constexpr int CPR = CT / 8;  // 16-B chunks per pixel row of the tile
     constexpr int NIT = PT * CPR / 256;
     const int chn = tid % CPR;   // fixed per thread (256 % CPR == 0)
@@ -150,10 +171,19 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
       const int idx = it * 256 + tid;
       const int row = idx / CPR;
       const int m = p0 + row;
-      if (m < a.M && kc < a.K) {
+      const bool inb = m < a.M && kc < a.K;
+      if (EXACT || inb) {
         uint4 v = *(const uint4*)(smem + row * OROW + chn * 16);
         const size_t o = (size_t)m * a.K + kc;
-        if (a.add_src || act) {
+        if constexpr (SACC) {
+          if (inb) {
+            const float q[8] = {lo_bf(v.x), hi_bf(v.x), lo_bf(v.y), hi_bf(v.y),
+                                lo_bf(v.z), hi_bf(v.z), lo_bf(v.w), hi_bf(v.w)};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { ssum[e] += q[e]; ssq[e] = fmaf(q[e], q[e], ssq[e]); }
+          }
+        }
+        if (inb && (a.add_src || act)) {
           float f[8];
           f[0] = lo_bf(v.x); f[1] = hi_bf(v.x); f[2] = lo_bf(v.y); f[3] = hi_bf(v.y);
           f[4] = lo_bf(v.z); f[5] = hi_bf(v.z); f[6] = lo_bf(v.w); f[7] = hi_bf(v.w);
@@ -188,17 +218,17 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
           }
           v = make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
         }
-        *(uint4*)(a.y + o) = v;
+        *(uint4*)(inb ? a.y + o : a.dump) = v;
       }
     }
     if (act) {
       // reduce the per-thread partial sums over the threads sharing this chunk column, one partial
       // row per pixel tile (reduced over tiles by dtm_reduce_rows)
-      __syncthreads();
+      epi_barrier<RAWB>();
       float* red = (float*)smem;  // [256][16]
 #pragma unroll
       for (int e = 0; e < 8; ++e) { red[tid * 16 + e] = sgx[e]; red[tid * 16 + 8 + e] = sg[e]; }
-      __syncthreads();
+      epi_barrier<RAWB>();
       if (tid < CPR && kc < a.K) {
         float tx[8], tg[8];
 #pragma unroll
@@ -404,7 +434,8 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
   }
 
   static_assert(PT * (CT * 2 + 16) <= NBUF * BUF, "output staging fits in the operand buffers");
-  conv_nt_epilogue<PT, CT, WP, WC>(a, acc, smem, p0, c0, by);
+  if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1>(a, acc, smem, p0, c0, by);
+  else conv_nt_epilogue<PT, CT, WP, WC, 2>(a, acc, smem, p0, c0, by);
 }
 
 
@@ -533,7 +564,8 @@ __global__ __launch_bounds__(256) void conv_nt_dma_kernel(ConvNTArgs a) {
     compute(kt & 1);
   }
   __syncthreads();  // the epilogue reuses the operand buffers
-  conv_nt_epilogue<PT, CT, WP, WC>(a, acc, smem, p0, c0, by);
+  if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1>(a, acc, smem, p0, c0, by);
+  else conv_nt_epilogue<PT, CT, WP, WC, 2>(a, acc, smem, p0, c0, by);
 }
 
 // Deep-K pipelined variant: both operand tiles go global -> LDS by LDS-DMA into an NS-slot ring with
@@ -724,7 +756,193 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // the epilogue reuses the ring
-  conv_nt_epilogue<PT, CT, WP, WC>(a, acc, smem, p0, c0, by);
+  if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1>(a, acc, smem, p0, c0, by);
+  else conv_nt_epilogue<PT, CT, WP, WC, 2>(a, acc, smem, p0, c0, by);
+}
+
+// Persistent streaming kernel for the short-reduction 1x1 stride-1 convs (K*R*S*C = 64 * NKT <= 256:
+// the 56x56 / 28x28 expand and reduce layers and their dgrads).  They are pure HBM streams (read
+// M x Kg, write M x K), so each block keeps its channel tile of the weights resident in LDS and walks
+// pixel tiles p = y, y + gridDim.y, ...: the LDS-DMA of tile i+1 is issued before the MFMAs of tile i
+// and stays in flight through tile i's epilogue (raw barriers; counted vmcnt with the epilogue's exact
+// store count as the lower bound).  Optional BatchNorm-apply + ReLU prologue transformed in LDS.
+// 16-B LDS-DMA issued through inline asm: hipcc does not see it as an LDS write, so it inserts none of
+// its conservative vmcnt(0) waits before later LDS reads/writes (every use is ordered by this file's own
+// counted vmcnt + barrier).  Its own waits for its own loads stay correct: the count is in issue order.
+__device__ __forceinline__ void glds16(const void* gptr, const void* lds) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr), "s"(l) : "memory", "m0");
+}
+
+template <int PT, int CT, int NKT, bool PRO>
+__global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int ntiles) {
+  constexpr int WP = PT / 2, WC = CT / 2;
+  constexpr int TP = WP / 16, TC = WC / 16;
+  constexpr int AI = PT / 32, WI = CT / 32;      // 1-KiB DMA pieces per wave per 64-k sub-tile
+  constexpr int ABUF = NKT * PT * 128;           // one pixel tile, all k
+  constexpr int WBUF = NKT * CT * 128;
+  constexpr int OROW = CT * 2 + 16;
+  constexpr int STG = PT * OROW > 16384 ? PT * OROW : 16384;
+  constexpr int NIT = PT * (CT / 8) / 256;      // exact staged stores per thread per tile
+  constexpr int MAXC = 512;
+  constexpr int OFF_A = WBUF, OFF_S = WBUF + 2 * ABUF, OFF_P = OFF_S + STG;
+  __shared__ __attribute__((aligned(16))) char smem[OFF_P + (PRO ? MAXC * 8 : 0)];
+  typedef __attribute__((address_space(1))) const void gvoid;
+  typedef __attribute__((address_space(3))) void lvoid;
+  static_assert(NIT >= 1 && NIT <= 15, "vmcnt lower bound");
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nb = gridDim.x * gridDim.y;
+  const int bid = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, nb);
+  const int bx = bid % gridDim.x, by0 = bid / gridDim.x;
+  const int c0 = bx * CT;
+  const int lr = lane >> 3;
+  const int ch = (lane & 7) ^ lr;
+  const char* xg = (const char*)a.x;
+  const char* wg = (const char*)a.w;
+  const char* zg = (const char*)a.zero;
+  float* s_scale = (float*)(smem + OFF_P);
+  float* s_shift = s_scale + MAXC;
+  if constexpr (PRO) {
+    for (int c = tid; c < a.C; c += 256) { s_scale[c] = a.in_scale[c]; s_shift[c] = a.in_shift[c]; }
+  }
+  // resident weight tile: NKT sub-tiles [CT][64] (128-B rows, chunk ^= row & 7)
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+    for (int j = 0; j < WI; ++j) {
+      const int row = c0 + 8 * (wave + 4 * j) + lr;
+      const int k = kt * 64 + ch * 8;
+      const bool v = (row < a.K) & (k < a.Kg);
+      const char* src = wg + (size_t)(uint32_t)((row * a.Kg + k) * 2);
+      __builtin_amdgcn_global_load_lds((gvoid*)(v ? src : zg), (lvoid*)(smem + kt * CT * 128 + (wave + 4 * j) * 1024),
+                                       16, 0, 0);
+    }
+  }
+  // The DMA source addresses are kept live until the end of the iteration (asm use below): hipcc
+  // waits vmcnt(0) before any instruction that overwrites an in-flight LDS-DMA's address VGPRs, which
+  // would drain the prefetch at the first fragment read.
+  const char* srcs[NKT * AI];
+  auto issue = [&](int t, int buf) {
+    char* base = smem + OFF_A + buf * ABUF;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      const int k = kt * 64 + ch * 8;
+#pragma unroll
+      for (int j = 0; j < AI; ++j) {
+        const int m = t * PT + 8 * (wave + 4 * j) + lr;
+        const bool v = (m < a.M) & (k < a.Kg);
+        const char* src = xg + (size_t)(uint32_t)(m * a.pix_bytes + k * 2);
+        srcs[kt * AI + j] = v ? src : zg;
+        glds16(srcs[kt * AI + j], base + kt * PT * 128 + (wave + 4 * j) * 1024);
+      }
+    }
+  };
+  auto transform = [&](int t, int buf) {
+    char* base = smem + OFF_A + buf * ABUF;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      const int k = kt * 64 + ch * 8;
+      if (k < a.Kg) {
+        const float4 s0 = *(const float4*)(s_scale + k), s1 = *(const float4*)(s_scale + k + 4);
+        const float4 h0 = *(const float4*)(s_shift + k), h1 = *(const float4*)(s_shift + k + 4);
+        const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+        for (int j = 0; j < AI; ++j) {
+          const int m = t * PT + 8 * (wave + 4 * j) + lr;
+          if (m < a.M) {
+            uint4* pp = (uint4*)(base + kt * PT * 128 + (wave + 4 * j) * 1024 + lane * 16);
+            const uint4 q = *pp;
+            uint32_t u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float lo = fmaxf(fmaf(lo_bf(u[e]), sc[2 * e], sh[2 * e]), 0.f);
+              const float hi = fmaxf(fmaf(hi_bf(u[e]), sc[2 * e + 1], sh[2 * e + 1]), 0.f);
+              u[e] = pack2bf(lo, hi);
+            }
+            *pp = make_uint4(u[0], u[1], u[2], u[3]);
+          }
+        }
+      }
+    }
+  };
+
+  const int wp = wave % 2, wc = wave / 2;
+  const int fr = lane & 15, fk = lane >> 4;
+  float ssum[8], ssq[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { ssum[e] = 0.f; ssq[e] = 0.f; }
+  int t = by0;
+  if (t < ntiles) issue(t, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // weights (+ prologue affine) resident, tile 0 landed
+  int buf = 0;
+  for (int it = 0; t < ntiles; ++it, t += gridDim.y) {
+    // this wave's DMA of tile t has landed once at most the previous epilogue's NIT stores are pending
+    if (it > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIT) : "memory");
+    if constexpr (PRO) transform(t, buf);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // tile t visible; the other buffer and the stage area are free
+    if (t + (int)gridDim.y < ntiles) issue(t + gridDim.y, buf ^ 1);
+    f32x4 acc[TC][TP];
+#pragma unroll
+    for (int i = 0; i < TC; ++i)
+#pragma unroll
+      for (int j = 0; j < TP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const char* abase = smem + OFF_A + buf * ABUF;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        short8 bf[TP], af[TC];
+        const int chn = ks * 4 + fk;
+#pragma unroll
+        for (int j = 0; j < TP; ++j) {
+          const int row = wp * WP + j * 16 + fr;
+          bf[j] = *(const short8*)(abase + kt * PT * 128 + row * 128 + ((chn ^ (row & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < TC; ++i) {
+          const int row = wc * WC + i * 16 + fr;
+          af[i] = *(const short8*)(smem + kt * CT * 128 + row * 128 + ((chn ^ (row & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < TC; ++i)
+#pragma unroll
+          for (int j = 0; j < TP; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    conv_nt_epilogue<PT, CT, WP, WC, 1, true, true, true, true>(a, acc, smem + OFF_S, t * PT, c0, t, ssum, ssq);
+#pragma unroll
+    for (int i = 0; i < NKT * AI; ++i) asm volatile("" ::"v"(srcs[i]));
+    buf ^= 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (a.stats) {
+    // one partial row per worker (pixel-tile walker): [sum(K) | sumsq(K)], this block's CT channels
+    constexpr int CPR = CT / 8, RPT = 256 / CPR;
+    __syncthreads();
+    float* red = (float*)(smem + OFF_S);  // [256][16]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { red[tid * 16 + e] = ssum[e]; red[tid * 16 + 8 + e] = ssq[e]; }
+    __syncthreads();
+    // tree over the RPT threads of each chunk column (thread tid owns column tid % CPR)
+    for (int h = RPT / 2; h >= 1; h >>= 1) {
+      if (tid < h * CPR) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) red[tid * 16 + e] += red[(tid + h * CPR) * 16 + e];
+      }
+      __syncthreads();
+    }
+    const int kc = c0 + tid * 8;
+    if (tid < CPR && kc < a.K) {
+      float* row = a.stats + (size_t)by0 * (2 * a.K);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { row[kc + e] = red[tid * 16 + e]; row[a.K + kc + e] = red[tid * 16 + 8 + e]; }
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1180,6 +1398,71 @@ static void launch_pipe(const ConvNTArgs& a, hipStream_t st) {
   else hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, false>), grid, dim3(256), 0, st, a);
 }
 
+static int device_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  return cus;
+}
+
+static bf16_t* dump_chunk() {
+  static void* z = nullptr;
+  if (!z && hipMalloc(&z, 4096) != hipSuccess) return nullptr;
+  return (bf16_t*)z;
+}
+
+// persistent streaming 1x1 kernel: blocks = resident capacity (occupancy x CUs), channel tiles x
+// pixel-tile workers
+template <int PT, int CT, int NKT, bool PRO>
+static int stream_workers_k(const ConvNTArgs& a) {
+  static int occ = 0;
+  if (!occ) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv1x1_stream_kernel<PT, CT, NKT, PRO>, 256, 0) !=
+            hipSuccess || occ <= 0)
+      occ = 1;
+  }
+  const int ctiles = (a.K + CT - 1) / CT;
+  const int ntiles = (a.M + PT - 1) / PT;
+  int workers = (occ * device_cus() + ctiles - 1) / ctiles;
+  if (workers > ntiles) workers = ntiles;
+  if (workers < 1) workers = 1;
+  return workers;
+}
+
+template <int PT, int CT, int NKT, bool PRO>
+static void launch_stream_k(const ConvNTArgs& a, hipStream_t st) {
+  const int ctiles = (a.K + CT - 1) / CT;
+  const int ntiles = (a.M + PT - 1) / PT;
+  hipLaunchKernelGGL((conv1x1_stream_kernel<PT, CT, NKT, PRO>), dim3(ctiles, stream_workers_k<PT, CT, NKT, PRO>(a)),
+                     dim3(256), 0, st, a, ntiles);
+}
+
+template <int CT, int NKT>
+static void launch_stream(const ConvNTArgs& a, hipStream_t st) {
+  if (a.in_scale) launch_stream_k<64, CT, NKT, true>(a, st);
+  else launch_stream_k<64, CT, NKT, false>(a, st);
+}
+
+// statistics partial rows of the streaming kernel (tile id 30 / 31): one per worker
+static int stream_rows(const ConvNTArgs& a, int id) {
+  const bool pro = a.in_scale != nullptr, k1 = a.Kg <= 64;
+  if (id == 30) {
+    if (k1) return pro ? stream_workers_k<64, 128, 1, true>(a) : stream_workers_k<64, 128, 1, false>(a);
+    return pro ? stream_workers_k<64, 128, 2, true>(a) : stream_workers_k<64, 128, 2, false>(a);
+  }
+  if (k1) return pro ? stream_workers_k<64, 64, 1, true>(a) : stream_workers_k<64, 64, 1, false>(a);
+  return pro ? stream_workers_k<64, 64, 2, true>(a) : stream_workers_k<64, 64, 2, false>(a);
+}
+
+static bool stream_ok(const ConvNTArgs& a) {
+  return !a.bias && !a.relu && a.R == 1 && a.S == 1 && a.stride == 1 && a.pad_h == 0 && a.pad_w == 0 && a.Hv == a.Hin && a.Wv == a.Win &&
+         a.P == a.Hin && a.Q == a.Win && a.Kg % 64 == 0 && a.Kg <= 128 && a.K % 8 == 0 &&
+         (!a.in_scale || a.C <= 512) && a.dump != nullptr;
+}
+
 template <int PT, int CT, int WP, int WC, int UD, int NBUF = 2>
 static void launch_nt(const ConvNTArgs& a, hipStream_t st) {
   dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT);
@@ -1204,6 +1487,10 @@ static TileCfg pick_tile(const ConvNTArgs& a) {
   int id = g_tile_env;
   // the pipelined LDS-DMA 128x128 tile (2 slots, 2 blocks/CU) wins every deep-reduction layer without the
   // prologue (tools/conv_tile_sweep.py: 3x3 at 14x14 / 7x7 -13..-18 %, deep 1x1 -5..-16 %)
+  if (id == -4) id = -1;  // (-4: the policy without the streaming kernel, for A/B runs)
+  else if (id == -1 && a.Kg == 64 && stream_ok(a)) id = a.K >= 128 ? 30 : 31;
+  // (the persistent streaming 1x1 kernel: the 64-deep 56x56 expand / reduce layers and their dgrads are
+  // HBM streams: -20..-33 % (tools/conv_tile_sweep.py); at Kg 128 its 1 block/CU loses)
   if (id == -1 && !a.in_scale && a.Kg >= 1024) id = 21;  // (-3: the policy without it, for A/B runs)
   if (id < 0) id = a.K <= 64 ? 3 : ((a.M <= 16384 && a.Kg >= 2048) ? 0 : 4);
   // LDS-DMA variants (10-12, opt-in) need an operand without the prologue affine
@@ -1211,6 +1498,10 @@ static TileCfg pick_tile(const ConvNTArgs& a) {
   // pipelined LDS-DMA variants (20-23) stage the prologue affine in LDS: C <= 512
   if (id >= 20 && a.in_scale && a.C > 512) id = 0;
   if (id >= 20 && id <= 23) return {id, 128, 2};
+  if (id == 30 || id == 31) {
+    if (stream_ok(a)) return {id, 64, 2};
+    id = a.K <= 64 ? 3 : 4;
+  }
   if (id == 1 || id == 3) return {id, 128, 4};
   if (id == 2 || id == 4) return {id, 64, 2};
   if (id == 10) return {id, 128, 2};
@@ -1228,7 +1519,13 @@ static void dispatch_ud(const ConvNTArgs& a, const TileCfg& t, hipStream_t st) {
   else if (t.id == 10) launch_nt_dma<128, 128, 64, 64, UD>(a, st);
   else if (t.id == 11) launch_nt_dma<64, 128, 32, 64, UD>(a, st);
   else if (t.id == 12) launch_nt_dma<128, 64, 32, 64, UD>(a, st);
-  else if (t.id == 20) launch_pipe<128, 128, 3, UD>(a, st);
+  else if (t.id == 30 && UD == 1) {
+    if (a.Kg <= 64) launch_stream<128, 1>(a, st);
+    else launch_stream<128, 2>(a, st);
+  } else if (t.id == 31 && UD == 1) {
+    if (a.Kg <= 64) launch_stream<64, 1>(a, st);
+    else launch_stream<64, 2>(a, st);
+  } else if (t.id == 20) launch_pipe<128, 128, 3, UD>(a, st);
   else if (t.id == 21) launch_pipe<128, 128, 2, UD>(a, st);
   else if (t.id == 22) launch_pipe<128, 128, 4, UD>(a, st);
   else if (t.id == 23) launch_pipe<128, 64, 3, UD>(a, st);
@@ -1254,6 +1551,7 @@ static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, cons
   a.add_stride = 1; a.add_H = a.add_W = 0;
   a.act_unscaled = 0;
   a.zero = zero_chunk();
+  a.dump = dump_chunk();
   a.pix_bytes = d->pix_bytes > 0 ? d->pix_bytes : d->C * 2;
   size_t xb = (size_t)d->N * d->H * d->W * a.pix_bytes, wb = (size_t)d->K * d->R * d->S * d->C * 2;
   if (xb >= (1ull << 31) || wb >= (1ull << 31)) return -2;
@@ -1266,7 +1564,8 @@ static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, cons
   int rows = 0;
   const TileCfg tc = pick_tile(a);
   if (stats) {
-    rows = ((a.M + tc.PT - 1) / tc.PT) * tc.NWP;  // one partial row per (pixel tile, pixel wave)
+    rows = (tc.id == 30 || tc.id == 31) ? stream_rows(a, tc.id)    // one per streaming worker
+                                         : ((a.M + tc.PT - 1) / tc.PT) * tc.NWP;  // per (pixel tile, pixel wave)
     float* ws = dtm_ws_get((size_t)rows * 2 * d->K);
     if (!ws) return -4;
     a.stats = ws;
@@ -1325,6 +1624,7 @@ DTM_API int dtm_conv_dgrad_ex(const void* dy, const void* wt, void* dx, const Co
   a.add_stride = add_stride;
   a.act_unscaled = act_unscaled;
   a.zero = zero_chunk();
+  a.dump = dump_chunk();
   a.add_H = (d->H - 1) / add_stride + 1; a.add_W = (d->W - 1) / add_stride + 1;
   a.pix_bytes = d->K * 2;
   size_t xb = (size_t)d->N * d->P * d->Q * d->K * 2, wb = (size_t)d->K * d->R * d->S * d->C * 2;

@@ -133,10 +133,11 @@ def test_image_augment_kernel_matches_oracle(distort, size):
     assert got.is_cuda and _rel(got.cpu(), ref_out) < 1e-4
 
 
-@pytest.mark.parametrize("tile", [20, 21, 22, 23])
+@pytest.mark.parametrize("tile", [20, 21, 22, 23, 30, 31])
 @pytest.mark.parametrize("prologue", [False, True])
 @pytest.mark.parametrize("case", [(4, 15, 15, 64, 96, 3, 2), (2, 14, 14, 128, 256, 3, 1), (3, 7, 7, 512, 200, 1, 1),
-                                  (2, 9, 9, 24, 40, 3, 1)])
+                                  (2, 9, 9, 24, 40, 3, 1), (4, 12, 12, 64, 256, 1, 1), (3, 7, 7, 128, 96, 1, 1),
+                                  (2, 9, 9, 64, 64, 1, 1), (2, 30, 30, 128, 64, 1, 1)])
 def test_conv_pipelined_tiles_match_reference(tile, prologue, case):
     """The pipelined LDS-DMA conv kernels (DTM_CONV_TILE=20..23; ring of k-tiles, counted vmcnt, the
     BatchNorm-apply prologue transformed in LDS) against the fp32 reference: forward (with and without
@@ -163,10 +164,12 @@ def test_conv_pipelined_tiles_match_reference(tile, prologue, case):
     L.dtm_weight_flip_transpose(_lib.ptr(w), _lib.ptr(wt), K, R, R, C, _lib.stream_ptr())
     y = torch.empty(N, g.P, g.Q, K, device=DEV, dtype=torch.bfloat16)
     dx = torch.empty_like(x)
+    stats = torch.zeros(2, K, device=DEV)
     L.dtm_conv_set_tile(tile)
     try:
-        rc = L.dtm_conv_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(y), None, None, _lib.ptr(sc) if prologue else None,
-                            _lib.ptr(sh) if prologue else None, 0, ctypes.byref(d), _lib.stream_ptr())
+        rc = L.dtm_conv_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(y), _lib.ptr(stats), None,
+                            _lib.ptr(sc) if prologue else None, _lib.ptr(sh) if prologue else None, 0,
+                            ctypes.byref(d), _lib.stream_ptr())
         assert rc == 0
         rc = L.dtm_conv_dgrad(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), _lib.stream_ptr())
         assert rc == 0
@@ -175,6 +178,9 @@ def test_conv_pipelined_tiles_match_reference(tile, prologue, case):
         L.dtm_conv_set_tile(-1)
     assert _rel(y, yr) < 1e-2
     assert _rel(dx, xr.grad) < 1e-2
+    # BatchNorm statistics from the epilogue = sums of the kernel's own bf16 outputs
+    yf = y.float().reshape(-1, K)
+    assert _rel(stats[0], yf.sum(0)) < 1e-3 and _rel(stats[1], yf.square().sum(0)) < 1e-3
 
 
 @pytest.mark.parametrize("tile", [10, 11])

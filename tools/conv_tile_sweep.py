@@ -58,6 +58,12 @@ def main():
                                             _lib.ptr(sh), 0, ctypes.byref(d), st),
             "dgrad": lambda: L.dtm_conv_dgrad(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), st),
         }
+        if os.environ.get("STATS"):
+            stats = torch.zeros(2, K, device="cuda")
+            passes["fwd+ps"] = lambda: L.dtm_conv_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(y), _lib.ptr(stats), None,
+                                                      _lib.ptr(sc), _lib.ptr(sh), 0, ctypes.byref(d), st)
+            passes["fwd+s"] = lambda: L.dtm_conv_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(y), _lib.ptr(stats), None,
+                                                     None, None, 0, ctypes.byref(d), st)
         if os.environ.get("WGRAD"):
             dw = torch.zeros(K, R, R, C, device="cuda")
             ss4 = torch.stack([sc, sh, sh, sc]).contiguous()
