@@ -15,7 +15,7 @@ import torch
 
 from ..ops import nn as F
 from ..ops.lazy import Subsampled, as_tensor
-from .layers import Conv2d, Layer, _join, fused_enabled
+from .layers import Conv2d, Layer, _join, apply_activation, fused_enabled
 
 
 def resnet_arg_scope(weight_decay=0.0001, batch_norm_decay=0.997, batch_norm_epsilon=1e-5, batch_norm_scale=True):
@@ -60,12 +60,65 @@ class BottleneckV1(Layer):
                             conv2d_same_padding(3, stride, rate), "relu", bn, None, wd, init, rate=rate)
         self.conv3 = Conv2d(_join(scope, "conv3"), depth_bottleneck, depth, 1, 1, "SAME", None, bn, None, wd, init)
 
-    def forward(self, x, training=True):
+    def forward(self, x, training=True, end_points=None):
         sc = self.shortcut(x, training) if self.shortcut is not None else \
-            subsample(x, self.stride, lazy=self.conv3.bn is not None)
-        r = self.conv1(x, training)
-        r = self.conv2(r, training)
-        return self.conv3(r, training, residual=sc, residual_act="relu")
+            subsample(x, self.stride, lazy=self.conv3.bn is not None and end_points is None)
+        r1 = self.conv1(x, training)
+        r2 = self.conv2(r1, training)
+        if end_points is not None:
+            # slim collects every conv output (outputs_collections) plus the unit output
+            r3 = self.conv3(r2, training)
+            y = apply_activation(as_tensor(r3) + as_tensor(sc), "relu")
+            if self.shortcut is not None:
+                end_points[self.shortcut.scope] = as_tensor(sc)
+            for c, v in ((self.conv1, r1), (self.conv2, r2), (self.conv3, r3)):
+                end_points[c.scope] = as_tensor(v)
+            end_points[self.scope] = y
+            return y
+        return self.conv3(r2, training, residual=sc, residual_act="relu")
+
+
+def stack_blocks_plan(blocks, output_stride=None, store_non_strided_activations=False):
+    """The unit schedule of resnet_utils.stack_blocks_dense (reference vgg/nets/resnet_utils.py:125-219).
+
+    blocks: [(base_depth, num_units, stride)], stride applied in the LAST unit of the block
+    (resnet_v1_block / resnet_v2_block).  Returns [([(unit_stride, unit_rate), ...], block_end_subsample)]:
+    once the running stride reaches ``output_stride`` every further unit runs with stride 1 and an
+    atrous rate that absorbs the skipped strides.  ``store_non_strided_activations`` moves the last
+    unit's stride to a subsample at the block end (the block endpoint is then undecimated)."""
+    current_stride, rate = 1, 1
+    plan = []
+    for base, n, stride in blocks:
+        units, block_stride = [], 1
+        for i in range(n):
+            s = stride if i == n - 1 else 1
+            if store_non_strided_activations and i == n - 1:
+                block_stride, s = s, 1
+            if output_stride is not None and current_stride == output_stride:
+                units.append((1, rate))
+                rate *= s
+            else:
+                units.append((s, 1))
+                current_stride *= s
+                if output_stride is not None and current_stride > output_stride:
+                    raise ValueError("The target output_stride cannot be reached.")
+        if output_stride is not None and current_stride == output_stride:
+            rate *= block_stride
+            sub = 1
+        else:
+            sub = block_stride
+            current_stride *= block_stride
+            if output_stride is not None and current_stride > output_stride:
+                raise ValueError("The target output_stride cannot be reached.")
+        plan.append((units, sub))
+    if output_stride is not None and current_stride != output_stride:
+        raise ValueError("The target output_stride cannot be reached.")
+    return plan
+
+
+def resnet_v1_block(scope, base_depth, num_units, stride):
+    """resnet_v1.resnet_v1_block: (base_depth, num_units, stride) in this module's block format."""
+    return (base_depth, num_units, stride)
 
 
 BLOCKS = {
@@ -80,26 +133,33 @@ class ResNetV1(Layer):
     default_image_size = 224
 
     def __init__(self, depth=50, num_classes=1000, global_pool=True, spatial_squeeze=True, scope=None,
-                 arg_scope=None, blocks=None, include_root_block=True, in_channels=3):
+                 arg_scope=None, blocks=None, include_root_block=True, in_channels=3, output_stride=None,
+                 store_non_strided_activations=False):
         scope = scope or "resnet_v1_%d" % depth
         super().__init__(scope)
         sc = arg_scope or resnet_arg_scope()
         self.num_classes, self.global_pool, self.spatial_squeeze = num_classes, global_pool, spatial_squeeze
         self.include_root_block = include_root_block
+        self.output_stride = output_stride
         cin = in_channels
         if include_root_block:
+            if output_stride is not None:
+                if output_stride % 4 != 0:
+                    raise ValueError("The output_stride needs to be a multiple of 4.")
+                output_stride //= 4
             self.conv1 = Conv2d(_join(scope, "conv1"), cin, 64, 7, 2, conv2d_same_padding(7, 2), "relu",
                                 sc["normalizer"], None, sc["weight_decay"], sc["init"])
             cin = 64
+        blocks = blocks or BLOCKS[depth]
+        plan = stack_blocks_plan(blocks, output_stride, store_non_strided_activations)
         units = []
         self.block_ends = []
-        for bi, (base, n, stride) in enumerate(blocks or BLOCKS[depth]):
-            for ui in range(n):
-                s = stride if ui == n - 1 else 1
+        for bi, ((base, n, _), (uplan, sub)) in enumerate(zip(blocks, plan)):
+            for ui, (s, rate) in enumerate(uplan):
                 units.append(BottleneckV1(_join(scope, "block%d/unit_%d/bottleneck_v1" % (bi + 1, ui + 1)), cin,
-                                          base * 4, base, s, sc))
+                                          base * 4, base, s, sc, rate=rate))
                 cin = base * 4
-            self.block_ends.append((len(units) - 1, _join(scope, "block%d" % (bi + 1))))
+            self.block_ends.append((len(units) - 1, _join(scope, "block%d" % (bi + 1)), sub))
         self.units = torch.nn.ModuleList(units)
         self.num_features = cin
         if num_classes:
@@ -112,14 +172,17 @@ class ResNetV1(Layer):
         net = x
         if self.include_root_block:
             net = self.conv1(net, training)
-            net = F.max_pool(net, 3, 2, "SAME")
-        ends = dict(self.block_ends)
-        for i, u in enumerate(self.units):
-            net = u(net, training)
             if end_points is not None:
-                end_points[u.scope] = net
-                if i in ends:
-                    end_points[ends[i]] = net
+                end_points[self.conv1.scope] = as_tensor(net)
+            net = F.max_pool(net, 3, 2, "SAME")
+        ends = {i: (name, sub) for i, name, sub in self.block_ends}
+        for i, u in enumerate(self.units):
+            net = u(net, training, end_points) if end_points is not None else u(net, training)
+            if i in ends:
+                name, sub = ends[i]
+                if end_points is not None:
+                    end_points[name] = net
+                net = subsample(net, sub)
         if self.global_pool:
             net = F.global_avg_pool(net).reshape(net.shape[0], 1, 1, -1)
             if end_points is not None:
@@ -129,7 +192,11 @@ class ResNetV1(Layer):
             if end_points is not None:
                 end_points[self.scope + "/logits"] = net
             if self.spatial_squeeze:
+                if net.shape[1] != 1 or net.shape[2] != 1:
+                    raise ValueError("spatial_squeeze needs a 1x1 logits map, got %s" % (tuple(net.shape),))
                 net = net.reshape(net.shape[0], -1)
+                if end_points is not None:
+                    end_points[self.scope + "/spatial_squeeze"] = net
             if end_points is not None:
                 end_points["predictions"] = torch.softmax(net.float(), -1)
         return net

@@ -41,16 +41,18 @@ def _subsample(x, factor, scope=None):
     return x if factor == 1 else F.max_pool(x, 1, factor, "VALID")
 
 
-def _conv2d_same(x, num_outputs, k, stride, scope):
+def _conv2d_same(x, num_outputs, k, stride, scope, rate=1):
+    """resnet_utils.conv2d_same: SAME for stride 1, else explicit symmetric pad of the (dilated)
+    kernel + VALID (reference vgg/nets/resnet_utils.py:77-122)."""
     if stride == 1:
-        return slim.conv2d(x, num_outputs, k, stride=1, padding="SAME", scope=scope)
-    pad = (k - 1) // 2
-    return slim.conv2d(x, num_outputs, k, stride=stride, padding=(pad, pad), scope=scope)
+        return slim.conv2d(x, num_outputs, k, stride=1, rate=rate, padding="SAME", scope=scope)
+    pad = ((k - 1) * rate) // 2
+    return slim.conv2d(x, num_outputs, k, stride=stride, rate=rate, padding=(pad, pad), scope=scope)
 
 
-def _bottleneck_v2(x, depth, depth_bottleneck, stride, scope):
+def _bottleneck_v2(x, depth, depth_bottleneck, stride, scope, rate=1, ep=None):
     with slim.variable_scope(scope):
-        with slim.variable_scope("bottleneck_v2"):
+        with slim.variable_scope("bottleneck_v2") as vs:
             depth_in = as_tensor(x).shape[-1]
             preact = slim.batch_norm(x, activation_fn=relu, scope="preact")
             if depth == depth_in:
@@ -58,41 +60,73 @@ def _bottleneck_v2(x, depth, depth_bottleneck, stride, scope):
             else:
                 shortcut = slim.conv2d(preact, depth, 1, stride=stride, normalizer_fn=None, activation_fn=None,
                                        scope="shortcut")
+                if ep is not None:
+                    ep[vs + "/shortcut"] = shortcut
             r = slim.conv2d(preact, depth_bottleneck, 1, stride=1, scope="conv1")
-            r = _conv2d_same(r, depth_bottleneck, 3, stride, "conv2")
-            r = slim.conv2d(r, depth, 1, stride=1, normalizer_fn=None, activation_fn=None, scope="conv3")
-            return as_tensor(shortcut) + as_tensor(r)
+            r2 = _conv2d_same(r, depth_bottleneck, 3, stride, "conv2", rate=rate)
+            r3 = slim.conv2d(r2, depth, 1, stride=1, normalizer_fn=None, activation_fn=None, scope="conv3")
+            out = as_tensor(shortcut) + as_tensor(r3)
+            if ep is not None:
+                for name, v in (("conv1", r), ("conv2", r2), ("conv3", r3)):
+                    ep[vs + "/" + name] = v
+                ep[vs] = out
+            return out
 
 
 RESNET_V2_BLOCKS = {50: [3, 4, 6, 3], 101: [3, 4, 23, 3], 152: [3, 8, 36, 3], 200: [3, 24, 36, 3]}
 
 
+def resnet_v2_block(scope, base_depth, num_units, stride):
+    """resnet_v2.resnet_v2_block (stride in the last unit) as (base_depth, num_units, stride)."""
+    return (base_depth, num_units, stride)
+
+
 def resnet_v2(images, num_classes=1000, is_training=True, depth=50, weight_decay=0.0001, scope=None,
-              global_pool=True, spatial_squeeze=True):
+              global_pool=True, spatial_squeeze=True, blocks=None, output_stride=None, include_root_block=True,
+              store_non_strided_activations=False):
+    """slim resnet_v2 generator (reference vgg/nets/resnet_v2.py:111-224): pre-activation
+    bottlenecks, root conv without BN, ``postnorm`` BN-ReLU, atrous ``output_stride``.  Endpoints:
+    every conv output, unit, block, global_pool, logits, spatial_squeeze, predictions."""
+    from .resnet_v1 import stack_blocks_plan
     scope = scope or "resnet_v2_%d" % depth
     ep = {}
     bn = dict(decay=0.997, epsilon=1e-5, scale=True)
+    if blocks is None:
+        blocks = [(base, n, 2 if bi < 3 else 1) for bi, (base, n) in
+                  enumerate(zip([64, 128, 256, 512], RESNET_V2_BLOCKS[depth]))]
+    if include_root_block and output_stride is not None:
+        if output_stride % 4 != 0:
+            raise ValueError("The output_stride needs to be a multiple of 4.")
+        output_stride //= 4
+    plan = stack_blocks_plan(blocks, output_stride, store_non_strided_activations)
     with slim.arg_scope([slim.conv2d], weights_regularizer=slim.l2_regularizer(weight_decay),
                         weights_initializer=slim.variance_scaling_initializer(), activation_fn=relu,
                         normalizer_fn=slim.batch_norm, normalizer_params=bn):
         with slim.arg_scope([slim.batch_norm], **bn), slim.arg_scope([slim.max_pool2d], padding="SAME"):
-            with slim.variable_scope(scope):
-                with slim.arg_scope([slim.conv2d], activation_fn=None, normalizer_fn=None):
-                    net = _conv2d_same(images, 64, 7, 2, "conv1")
-                net = slim.max_pool2d(net, 3, stride=2, scope="pool1")
-                for bi, (base, n) in enumerate(zip([64, 128, 256, 512], RESNET_V2_BLOCKS[depth])):
+            with slim.variable_scope(scope) as vs:
+                net = images
+                if include_root_block:
+                    with slim.arg_scope([slim.conv2d], activation_fn=None, normalizer_fn=None):
+                        net = _conv2d_same(net, 64, 7, 2, "conv1")
+                    ep[vs + "/conv1"] = net
+                    net = slim.max_pool2d(net, 3, stride=2, scope="pool1")
+                for bi, ((base, n, _), (uplan, sub)) in enumerate(zip(blocks, plan)):
                     with slim.variable_scope("block%d" % (bi + 1)):
-                        for u in range(n):
-                            stride = 2 if (u == n - 1 and bi < 3) else 1
-                            net = _bottleneck_v2(net, base * 4, base, stride, "unit_%d" % (u + 1))
-                    ep["%s/block%d" % (scope, bi + 1)] = net
+                        for u, (stride, rate) in enumerate(uplan):
+                            net = _bottleneck_v2(net, base * 4, base, stride, "unit_%d" % (u + 1), rate, ep)
+                    ep["%s/block%d" % (vs, bi + 1)] = net
+                    net = _subsample(net, sub)
                 net = slim.batch_norm(net, activation_fn=relu, scope="postnorm")
                 if global_pool:
                     net = F.global_avg_pool(net).reshape(net.shape[0], 1, 1, -1)
+                    ep["global_pool"] = net
                 if num_classes:
                     net = slim.conv2d(net, num_classes, 1, activation_fn=None, normalizer_fn=None, scope="logits")
+                    ep[vs + "/logits"] = net
                     if spatial_squeeze:
                         net = _squeeze(net)
+                        ep[vs + "/spatial_squeeze"] = net
+                    ep["predictions"] = torch.softmax(as_tensor(net).float(), -1)
     return net, ep
 
 

@@ -178,7 +178,7 @@ def conv2d(x, w, bias=None, stride=1, padding="SAME", relu=False, dilation=1):
     if not x.is_cuda:
         return ref.conv2d(x, w, bias, stride, padding, relu, dilation)
     if dilation != 1:
-        raise NotImplementedError("dilated conv on the HIP path (atrous output_stride) is not supported yet")
+        return _atrous_conv2d(x, w, bias, stride, padding, relu, dilation)
     g = conv_geom(tuple(x.shape), tuple(w.shape), stride, padding, dilation)
     if g.C % 8 != 0:
         # pad input channels with zeros (first layer: RGB) so every gather chunk is 16 B
@@ -195,6 +195,29 @@ def conv2d(x, w, bias=None, stride=1, padding="SAME", relu=False, dilation=1):
         y = _Conv2dFn.apply(x.to(torch.bfloat16), wp, bp, g, relu)
         return y[..., :w.shape[0]].contiguous()
     return _Conv2dFn.apply(x.to(torch.bfloat16), w, bias, g, relu)
+
+
+def _atrous_conv2d(x, w, bias, stride, padding, relu, rate):
+    """Dilated (atrous) conv as space-to-batch -> dense VALID conv -> batch-to-space, the
+    decomposition TF's atrous_conv2d uses (the conv itself runs on the dense HIP implicit-GEMM
+    kernel; the two re-layouts are plain strided copies whose backward autograd derives).
+
+    Output pixel o = a + rate*i (phase a) only reads input pixels a + rate*(i + k), so each of the
+    rate x rate phases is an ordinary conv over the phase-subsampled, padded input.  Used by the
+    ResNet ``output_stride`` (atrous) mode (reference vgg/nets/resnet_utils.py:125-219)."""
+    if stride != 1:
+        raise ValueError("atrous conv requires stride 1 (TF atrous_conv2d has no stride)")
+    g = conv_geom(tuple(x.shape), tuple(w.shape), 1, padding, rate)
+    N, H, W, C = x.shape
+    Hp, Wp = H + g.pad_h + g.pad_b, W + g.pad_w + g.pad_r
+    Hq, Wq = -(-Hp // rate) * rate, -(-Wp // rate) * rate
+    xp = torch.nn.functional.pad(x, (0, 0, g.pad_w, g.pad_r + Wq - Wp, g.pad_h, g.pad_b + Hq - Hp))
+    xs = xp.reshape(N, Hq // rate, rate, Wq // rate, rate, C).permute(2, 4, 0, 1, 3, 5)
+    xs = xs.reshape(rate * rate * N, Hq // rate, Wq // rate, C)
+    ys = conv2d(xs, w, bias, 1, "VALID", relu)
+    ho, wo, K = ys.shape[1], ys.shape[2], ys.shape[3]
+    y = ys.reshape(rate, rate, N, ho, wo, K).permute(2, 3, 0, 4, 1, 5).reshape(N, ho * rate, wo * rate, K)
+    return y[:, :g.P, :g.Q].contiguous()
 
 
 class _Conv2dTransposeFn(torch.autograd.Function):

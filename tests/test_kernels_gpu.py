@@ -52,6 +52,27 @@ def test_conv_fwd_bwd(case):
     assert _rel(wk.grad, wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,C,K,R,rate,pad", [(2, 21, 64, 64, 3, 2, "SAME"), (2, 11, 128, 64, 3, 4, "SAME"),
+                                                 (1, 17, 32, 48, 3, 2, "VALID")])
+def test_atrous_conv_fwd_bwd(N, H, C, K, R, rate, pad):
+    """Dilated conv (ResNet output_stride mode): space-to-batch around the dense HIP conv."""
+    torch.manual_seed(3)
+    x = torch.randn(N, H, H, C, device=DEV).to(torch.bfloat16).float()
+    w = (torch.randn(K, R, R, C, device=DEV) * (1.0 / (R * R * C) ** 0.5)).to(torch.bfloat16).float()
+    xr, wr = x.clone().requires_grad_(), w.clone().requires_grad_()
+    yr = ref.conv2d(xr, wr, None, 1, pad, False, rate)
+    gy = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(gy)
+    xk, wk = x.to(torch.bfloat16).requires_grad_(), w.clone().requires_grad_()
+    yk = dnn.conv2d(xk, wk, None, 1, pad, dilation=rate)
+    assert yk.shape == yr.shape
+    yk.backward(gy.to(torch.bfloat16))
+    torch.cuda.synchronize()
+    assert _rel(yk, yr) < 1e-2
+    assert _rel(xk.grad, xr.grad) < 1e-2
+    assert _rel(wk.grad, wr.grad) < 1e-2
+
+
 def test_conv_bias_relu_and_stats_free():
     torch.manual_seed(1)
     x = torch.randn(2, 12, 12, 64, device=DEV).to(torch.bfloat16).float()

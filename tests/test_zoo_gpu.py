@@ -96,6 +96,27 @@ def test_zoo_train_step_and_oracle(name, size, nc, B):
     assert all(torch.isfinite(g).all() for g in grads)
 
 
+@pytest.mark.parametrize("name", ["resnet_v1_50", "resnet_v2_50"])
+def test_atrous_resnet_output_stride_16(name):
+    """Dense-prediction mode (output_stride 16: block4 runs with rate 2 on the dilated-conv path,
+    mixed with the fused conv+BN units) against the fp32 oracle, then one backward."""
+    torch.manual_seed(0)
+    cpu = nets_factory.build(name, 10, output_stride=16, global_pool=False, spatial_squeeze=False)
+    gpu = copy.deepcopy(cpu).to(DEV)
+    x = torch.randn(2, 129, 129, 3)
+    with torch.no_grad():
+        want = cpu(x, training=False)
+        got = gpu(x.to(DEV, torch.bfloat16), training=False)
+    assert list(got.shape) == [2, 9, 9, 10] == list(want.shape)
+    assert _rel(got, want) < 6e-2
+    out = gpu(x.to(DEV, torch.bfloat16), training=True)
+    out.float().square().mean().backward()
+    torch.cuda.synchronize()
+    grads = [p.grad for p in gpu.parameters() if p.requires_grad and p.grad is not None]
+    assert len(grads) > 0.9 * sum(1 for p in gpu.parameters() if p.requires_grad)
+    assert all(torch.isfinite(g).all() for g in grads)
+
+
 def _gan(fn, *a, **k):
     st = slim.VariableStore()
     st.device = DEV
