@@ -1,10 +1,16 @@
-"""Small elementwise ops (ReLU/ReLU6/add/dropout).
+"""Small elementwise ops (ReLU/ReLU6/add/dropout) and InTopK.
 
 On the hot path of the benchmark models these are fused into the conv / BatchNorm kernels
 (epilogue ReLU, BN+residual+ReLU); the stand-alone forms below serve the remaining model-zoo
-call sites.  Dropout uses a counter-based hash mask (regenerated in backward, nothing stored).
+call sites.  Dropout (K15) runs the HIP kernel in ``csrc/kernels/elementwise.hip``: the keep mask is
+a counter-based hash of (seed, element index), regenerated in backward, never stored.  The CPU
+path evaluates the same hash with int64 tensor arithmetic, so both produce the identical mask.
 """
+import ctypes
+
 import torch
+
+from . import _lib
 
 
 def relu(x):
@@ -19,25 +25,103 @@ def add(x, y):
     return x + y.to(x.dtype)
 
 
+def _s64(c):
+    return c - (1 << 64) if c >= (1 << 63) else c
+
+
+_GOLD, _M1, _M2 = _s64(0x9E3779B97F4A7C15), _s64(0xBF58476D1CE4E5B9), _s64(0x94D049BB133111EB)
+
+
+def _lsr(z, s):
+    """Logical right shift of int64 lanes (torch's >> is arithmetic)."""
+    return (z >> s) & ((1 << (64 - s)) - 1)
+
+
+def hash_u32(seed, n, device="cpu"):
+    """The kernel's splitmix64-finaliser hash of (seed, i) for i < n, as int64 values in [0, 2^32)."""
+    i = torch.arange(1, n + 1, dtype=torch.int64, device=device)
+    z = _s64(seed % (1 << 64)) + i * _GOLD
+    z = (z ^ _lsr(z, 30)) * _M1
+    z = (z ^ _lsr(z, 27)) * _M2
+    z = z ^ _lsr(z, 31)
+    return _lsr(z, 32)
+
+
+def _threshold(keep):
+    t = int(keep * 4294967296.0)
+    return min(t, 0xFFFFFFFF)
+
+
+def dropout_mask(shape, keep, seed, device="cpu"):
+    n = 1
+    for s in shape:
+        n *= int(s)
+    return (hash_u32(seed, n, device) < _threshold(keep)).reshape(shape)
+
+
+def _dropout_hip(x, keep, seed):
+    x = x.contiguous()
+    if x.data_ptr() % 16:
+        x = x.clone()
+    y = torch.empty_like(x)
+    dt = {torch.float32: 0, torch.bfloat16: 1}[x.dtype]
+    rc = _lib.lib().dtm_dropout(_lib.ptr(x), _lib.ptr(y), x.numel(), dt, ctypes.c_float(keep),
+                                ctypes.c_ulonglong(seed), _lib.stream_ptr())
+    if rc:
+        raise RuntimeError("dtm_dropout failed (%d)" % rc)
+    return y
+
+
 class _DropoutFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, keep, seed):
-        g = torch.Generator(device=x.device)
-        g.manual_seed(seed)
-        mask = (torch.rand(x.shape, generator=g, device=x.device) < keep)
-        ctx.save_for_backward(mask)
-        ctx.keep = keep
-        return torch.where(mask, x / keep, torch.zeros((), dtype=x.dtype, device=x.device))
+        ctx.keep, ctx.seed = keep, seed
+        if x.is_cuda:
+            return _dropout_hip(x, keep, seed)
+        mask = dropout_mask(x.shape, keep, seed)
+        return torch.where(mask, x / keep, torch.zeros((), dtype=x.dtype))
 
     @staticmethod
     def backward(ctx, g):
-        (mask,) = ctx.saved_tensors
-        return torch.where(mask, g / ctx.keep, torch.zeros((), dtype=g.dtype, device=g.device)), None, None
+        if g.is_cuda:
+            return _dropout_hip(g, ctx.keep, ctx.seed), None, None
+        mask = dropout_mask(g.shape, ctx.keep, ctx.seed)
+        return torch.where(mask, g / ctx.keep, torch.zeros((), dtype=g.dtype)), None, None
 
 
 _seed = [1234]
 
 
-def dropout(x, keep_prob):
+def next_seed():
     _seed[0] = (_seed[0] * 6364136223846793005 + 1442695040888963407) % (1 << 62)
-    return _DropoutFn.apply(x, float(keep_prob), int(_seed[0] % (1 << 31)))
+    return int(_seed[0])
+
+
+def dropout(x, keep_prob, seed=None):
+    """Inverted dropout: kept elements scaled by 1/keep_prob (tf.nn.dropout)."""
+    if keep_prob >= 1.0:
+        return x
+    if x.is_cuda and x.dtype not in (torch.float32, torch.bfloat16):
+        x = x.float()
+    return _DropoutFn.apply(x, float(keep_prob), next_seed() if seed is None else int(seed))
+
+
+def in_top_k(predictions, targets, k):
+    """tf.nn.in_top_k: bool [B]; ties at the k-th value count as in, non-finite targets never do."""
+    if predictions.is_cuda:
+        p = predictions.contiguous()
+        if p.dtype not in (torch.float32, torch.bfloat16):
+            p = p.float()
+        t = targets.to(torch.int32).contiguous()
+        out = torch.empty(p.shape[0], dtype=torch.uint8, device=p.device)
+        rc = _lib.lib().dtm_in_top_k(_lib.ptr(p), _lib.ptr(t), _lib.ptr(out), p.shape[0], p.shape[1], int(k),
+                                     1 if p.dtype == torch.bfloat16 else 0, _lib.stream_ptr())
+        if rc:
+            raise RuntimeError("dtm_in_top_k failed (%d)" % rc)
+        return out.bool()
+    p = predictions.float()
+    t = targets.long()
+    valid = (t >= 0) & (t < p.shape[1])
+    xt = p.gather(1, t.clamp(0, p.shape[1] - 1)[:, None])
+    greater = (p > xt).sum(1)
+    return valid & torch.isfinite(xt[:, 0]) & (greater < k)

@@ -140,3 +140,30 @@ def test_imagenet_batch_inputs_from_tfrecords(tmp_path):
     x, y = bi.next_batch()
     bi.close()
     assert tuple(x.shape) == (4, 32, 32, 3) and set(y.tolist()) <= set(range(1, 7))
+
+
+# ---------------------------------------------------------------------------------------------
+# dropout hash mask / in_top_k (CPU forms of the HIP kernels in csrc/kernels/elementwise.hip)
+def test_dropout_mask_rate_determinism_and_grad():
+    from distributed_tensorflow_models_amd.ops import elementwise as E
+    m = E.dropout_mask((200000,), 0.3, seed=7)
+    assert abs(m.float().mean().item() - 0.3) < 0.01
+    assert torch.equal(m, E.dropout_mask((200000,), 0.3, seed=7))
+    assert not torch.equal(m, E.dropout_mask((200000,), 0.3, seed=8))
+    x = torch.randn(64, 33, requires_grad=True)
+    y = E.dropout(x, 0.5, seed=11)
+    mask = E.dropout_mask(x.shape, 0.5, 11)
+    torch.testing.assert_close(y, torch.where(mask, x * 2, torch.zeros(())))
+    y.sum().backward()
+    torch.testing.assert_close(x.grad, mask.float() * 2)
+
+
+def test_in_top_k_tf_semantics():
+    from distributed_tensorflow_models_amd.ops import elementwise as E
+    p = torch.tensor([[0.1, 0.3, 0.3, 0.2], [1.0, 2.0, 3.0, 4.0], [float("nan"), 1.0, 0.0, 0.0],
+                      [0.0, 0.0, 0.0, 0.0]])
+    t = torch.tensor([2, 0, 0, 3])
+    assert E.in_top_k(p, t, 1).tolist() == [True, False, False, True]   # tie with the max counts as in
+    assert E.in_top_k(p, t, 3).tolist() == [True, False, False, True]
+    assert E.in_top_k(p, t, 4).tolist() == [True, True, False, True]
+    assert E.in_top_k(p, torch.tensor([5, -1, 1, 0]), 4).tolist() == [False, False, True, True]

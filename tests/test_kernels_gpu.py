@@ -259,3 +259,31 @@ def test_conv_lds_dma_tiles_match_default(tile):
     for i, k in enumerate(("y", "dx")):
         a, b = outs[0][i], outs[1][i]
         assert ((a - b).norm() / b.norm()).item() < 1e-2, k
+
+
+@pytest.mark.parametrize("dtype,n", [(torch.bfloat16, 4096 * 33 + 5), (torch.float32, 1000003), (torch.bfloat16, 7)])
+def test_dropout_kernel_matches_hash_mask(dtype, n):
+    """HIP dropout regenerates exactly the CPU hash mask (forward and backward, nothing stored)."""
+    from distributed_tensorflow_models_amd.ops import elementwise as E
+    x = torch.randn(n, device=DEV).to(dtype).requires_grad_()
+    y = E.dropout(x, 0.7, seed=123456789)
+    mask = E.dropout_mask((n,), 0.7, 123456789).to(DEV)
+    want = torch.where(mask, x.detach().float() / 0.7, torch.zeros((), device=DEV))
+    torch.testing.assert_close(y.float(), want, rtol=1e-2 if dtype == torch.bfloat16 else 1e-6, atol=1e-6)
+    g = torch.randn(n, device=DEV).to(dtype)
+    y.backward(g)
+    torch.testing.assert_close(x.grad.float(), torch.where(mask, g.float() / 0.7, torch.zeros((), device=DEV)),
+                               rtol=1e-2 if dtype == torch.bfloat16 else 1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("B,K,dtype", [(256, 1000, torch.bfloat16), (37, 10, torch.float32), (5, 1001, torch.float32)])
+def test_in_top_k_kernel(B, K, dtype):
+    from distributed_tensorflow_models_amd.ops import elementwise as E
+    torch.manual_seed(5)
+    p = torch.randn(B, K).to(dtype)
+    p[0, :] = 0.0                      # all-tie row
+    t = torch.randint(0, K, (B,))
+    t[1] = -1                          # invalid label
+    for k in (1, 5):
+        got = E.in_top_k(p.to(DEV), t.to(DEV), k).cpu()
+        assert torch.equal(got, E.in_top_k(p.float(), t, k))
