@@ -130,14 +130,22 @@ class _ConvBNFn(torch.autograd.Function):
     Backward: the finalize backward is folded into the stats-combine pass (dgamma / dbeta included)."""
 
     @staticmethod
-    def forward(ctx, x, in_ss, w, gamma, beta, geom, bn, slot=None, in_unscaled=False):
+    def forward(ctx, x, in_ss, w, gamma, beta, geom, bn, slot=None, in_unscaled=False, x_mat=None):
         L = _lib.lib()
         s = _lib.stream_ptr()
         w16 = weight_bf16(w)
         y = torch.empty((geom.N, geom.P, geom.Q, geom.K), device=x.device, dtype=torch.bfloat16)
         d = geom.as_desc(_lib.ConvDesc)
-        sc = in_ss[0] if in_ss is not None else None
-        sh = in_ss[1] if in_ss is not None else None
+        # x_mat: relu(x*scale+shift) already materialised (``_prologue_mode`` 'mat'): forward conv and
+        # wgrad read it without the prologue; the dgrad epilogue still does the activation backward from
+        # the raw x and in_ss, so the materialisation has no backward pass of its own
+        ctx.mat = x_mat is not None
+        sc = in_ss[0] if (in_ss is not None and x_mat is None) else None
+        sh = in_ss[1] if (in_ss is not None and x_mat is None) else None
+        if x_mat is not None:
+            x, x_raw = x_mat, x
+        else:
+            x_raw = None
         ss = None
         if bn is not None:
             ss = torch.empty((4, geom.K), device=x.device, dtype=torch.float32)
@@ -154,7 +162,7 @@ class _ConvBNFn(torch.autograd.Function):
         ctx.slot = slot
         ctx.in_unscaled = bool(in_unscaled)
         ctx.has_gamma, ctx.has_beta = gamma is not None, beta is not None
-        ctx.save_for_backward(x, in_ss, w, y, ss, gamma, beta)
+        ctx.save_for_backward(x, in_ss, w, y, ss, gamma, beta, x_raw)
         if ss is None:
             return y
         return y, ss
@@ -163,7 +171,9 @@ class _ConvBNFn(torch.autograd.Function):
     def backward(ctx, dy, dss=None):
         L = _lib.lib()
         s = _lib.stream_ptr()
-        x, in_ss, w, y, ss, gamma, beta = ctx.saved_tensors
+        x, in_ss, w, y, ss, gamma, beta, x_raw = ctx.saved_tensors
+        if x_raw is None:
+            x_raw = x
         g = ctx.geom
         M_out = g.N * g.P * g.Q
         dy = dy.contiguous()
@@ -191,8 +201,8 @@ class _ConvBNFn(torch.autograd.Function):
         elif ss is not None:
             dy = (dy.float() * ss[0]).to(dy.dtype)  # no statistics gradient: only the BN-apply scale
         d = g.as_desc(_lib.ConvDesc)
-        sc = in_ss[0] if in_ss is not None else None
-        sh = in_ss[1] if in_ss is not None else None
+        sc = in_ss[0] if (in_ss is not None and not ctx.mat) else None
+        sh = in_ss[1] if (in_ss is not None and not ctx.mat) else None
         dx = d_in = None
         if ctx.needs_input_grad[0] or (in_ss is not None and ctx.needs_input_grad[1]):
             last, add_src, add_stride = _slot_take(ctx.slot)
@@ -203,7 +213,7 @@ class _ConvBNFn(torch.autograd.Function):
                 # parameter-gradient sums are done in the dgrad epilogue
                 d_in = arena.zeros((4, g.C), dy.device)
                 _check(L.dtm_conv_dgrad_ex(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), None, 1,
-                                           _lib.ptr(x), _lib.ptr(in_ss), _lib.ptr(d_in), int(ctx.in_unscaled), s),
+                                           _lib.ptr(x_raw), _lib.ptr(in_ss), _lib.ptr(d_in), int(ctx.in_unscaled), s),
                        "conv_dgrad_act")
             else:
                 use_add = last and add_src is not None
@@ -225,7 +235,7 @@ class _ConvBNFn(torch.autograd.Function):
                 dw = target
         else:
             dw = None
-        return dx, d_in, dw, dgamma, dbeta, None, None, None, None
+        return dx, d_in, dw, dgamma, dbeta, None, None, None, None, None
 
 
 class _BNFinalizeFn(torch.autograd.Function):
@@ -446,6 +456,16 @@ def bn_apply(raw, ss, relu, residual=None, unscaled=False):
     return _BNApplyFn.apply(raw, ss, res, None, bool(relu), slot, 1, ux)
 
 
+def bn_apply_nograd(raw, ss):
+    """relu(raw*scale + shift) as a plain bf16 tensor (no autograd node, no ReLU mask)."""
+    L = _lib.lib()
+    C = raw.shape[-1]
+    y = torch.empty_like(raw)
+    _check(L.dtm_bn_apply2(_lib.ptr(raw), _lib.ptr(ss), None, None, _lib.ptr(y), None, raw.numel() // C, C, 0, 1,
+                           _lib.stream_ptr()), "bn_apply")
+    return y
+
+
 def bn_inference_ss(bn):
     """Differentiable [4, C] scale/shift from moving statistics (frozen BN / eval)."""
     rstd = torch.rsqrt(bn.moving_variance + bn.eps)
@@ -454,35 +474,47 @@ def bn_inference_ss(bn):
     return torch.stack([scale, shift, bn.moving_mean.expand_as(scale), rstd.expand_as(scale)]).contiguous()
 
 
-def _prologue_fused(x_shape, w_shape, stride):
-    """Fuse the input's BatchNorm-apply + ReLU into this conv's operand prologue, or materialise it?
+def _prologue_mode(x_shape, w_shape, stride):
+    """How a conv consumes its input's BatchNorm-apply + ReLU (a LazyBN):
 
-    The prologue re-transforms every gathered element (R*S times per input element for an RxS conv)
-    in the conv AND in its wgrad, and keeps the conv off the pipelined LDS-DMA tile.  Measured per
-    ResNet-50 layer (tools/conv_tile_sweep.py, WGRAD=1; batch 256): for the stride-1 3x3 convs at
-    14x14 and 7x7 the prologue costs fwd +49/+59 us and wgrad +44/+38 us, a separate apply pass
-    15/9 us (+ the same again in backward) -> materialise; at 28x28 / 56x56 and for 1x1 convs the
-    prologue is cheaper than the extra activation round trips -> fuse.
-    DTM_PROLOGUE = auto (default) | fused | apply."""
+    'fused' - in the conv's operand prologue (and again in its wgrad): the normalised activation is
+              never stored, but every gathered element is re-transformed R*S times per pass and the
+              conv stays off the pipelined LDS-DMA tile;
+    'mat'   - materialised once by a forward-only BN-apply pass (read raw + write bf16); the conv and its
+              wgrad read it plainly, and the dgrad epilogue still does the activation backward from the
+              raw tensor, so there is no backward pass for it;
+    'apply' - the autograd BN-apply (its own backward pass) - the pre-'mat' form, kept for A/B runs.
+    Measured per ResNet-50 layer (tools/conv_tile_sweep.py with WGRAD=1, batch 256): the prologue
+    costs fwd +13..+66 us and wgrad +12..+68 us per layer, a materialising pass 6..35 us -> 'mat' wins
+    every conv except the stride-2 3x3 at 56x56, where it is neutral.
+    DTM_PROLOGUE = auto (default) | fused | mat | apply | legacy."""
     import os
     mode = os.environ.get("DTM_PROLOGUE", "auto")
-    if mode in ("fused", "apply"):
-        return mode == "fused"
+    if mode in ("fused", "apply", "mat"):
+        return mode
     _, H, W, _ = x_shape
     _, R, S, _ = w_shape
     st = stride if isinstance(stride, int) else stride[0]
-    return not (R * S > 1 and st == 1 and H * W <= 14 * 14)
+    if mode == "legacy":  # the previous policy: autograd apply for the stride-1 3x3 convs at <= 14x14
+        return "apply" if (R * S > 1 and st == 1 and H * W <= 14 * 14) else "fused"
+    if st > 1 and H * W >= 56 * 56:
+        return "fused"
+    return "mat"
 
 
 def conv_bn(x, w, bn, stride, padding, training, relu):
     """Fused conv -> BatchNorm; returns a LazyBN.  x: tensor or LazyBN(relu=True) (prologue-fused)."""
     in_ss = None
     in_unscaled = False
+    x_mat = None
     if isinstance(x, LazyBN):
-        if x.relu and _prologue_fused(tuple(x.shape), tuple(w.shape), stride):
-            in_ss, in_unscaled, x = x.ss, x.unscaled, x.raw
-        else:
+        mode = _prologue_mode(tuple(x.shape), tuple(w.shape), stride) if x.relu else "apply"
+        if mode == "apply" or x.ss.shape[1] % 8 != 0:
             x = x.materialize()
+        else:
+            in_ss, in_unscaled, x = x.ss, x.unscaled, x.raw
+            if mode == "mat":
+                x_mat = bn_apply_nograd(x, in_ss)
     g = conv_geom(tuple(x.shape), tuple(w.shape), stride, padding)
     if in_ss is None and _stem_eligible(x, w, stride, padding):
         if training:
@@ -504,7 +536,7 @@ def conv_bn(x, w, bn, stride, padding, training, relu):
     slot = _slot_register(xb) if (xb is x and in_ss is None) else None
     x = xb
     if training:
-        y, ss = _ConvBNFn.apply(x, in_ss, w, bn.gamma, bn.beta, g, bn, slot, in_unscaled)
+        y, ss = _ConvBNFn.apply(x, in_ss, w, bn.gamma, bn.beta, g, bn, slot, in_unscaled, x_mat)
     else:
         y = _ConvBNFn.apply(x, in_ss, w, None, None, g, None, slot, in_unscaled)
         ss = bn_inference_ss(bn)
