@@ -22,12 +22,25 @@ __device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t i) {
   return (uint32_t)(z >> 32);
 }
 
+// Per-step stream offset: a device counter the training engine advances once per step, read by
+// the kernel at run time, so a step replayed from a hipGraph (seed baked in at capture) still
+// draws a fresh mask every step.  off == 0 leaves the seed untouched (bit-identical CPU form).
+__device__ __forceinline__ uint64_t mix_seed(uint64_t seed, uint64_t off) {
+  if (off == 0) return seed;
+  uint64_t z = off * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return seed ^ z ^ (z >> 31);
+}
+
 // keep iff hash < keep_prob * 2^32 (threshold computed on the host)
 template <bool BF16>
 __global__ __launch_bounds__(256) void dropout_kernel(const void* __restrict__ xv, void* __restrict__ yv, long n,
-                                                      uint32_t thresh, float inv_keep, uint64_t seed) {
+                                                      uint32_t thresh, float inv_keep, uint64_t seed0,
+                                                      const unsigned long long* __restrict__ seed_off) {
   const long base = ((long)blockIdx.x * 256 + threadIdx.x) * 8;
   if (base >= n) return;
+  const uint64_t seed = seed_off ? mix_seed(seed0, *seed_off) : seed0;
   float v[8];
   if (BF16) {
     const bf16_t* x = (const bf16_t*)xv;
@@ -95,7 +108,7 @@ using namespace dtm;
 
 // dtype: 0 = fp32, 1 = bf16.  Same seed => same mask (backward passes the upstream gradient).
 DTM_API int dtm_dropout(const void* x, void* y, long n, int dtype, float keep_prob, unsigned long long seed,
-                        hipStream_t st) {
+                        const unsigned long long* seed_off, hipStream_t st) {
   if (n <= 0) return 0;
   if (!(keep_prob > 0.f && keep_prob <= 1.f)) return 1;
   const double t = (double)keep_prob * 4294967296.0;
@@ -103,9 +116,9 @@ DTM_API int dtm_dropout(const void* x, void* y, long n, int dtype, float keep_pr
   const long threads = (n + 7) / 8;
   const unsigned grid = (unsigned)((threads + 255) / 256);
   if (dtype == 1)
-    dropout_kernel<true><<<grid, 256, 0, st>>>(x, y, n, thresh, 1.f / keep_prob, seed);
+    dropout_kernel<true><<<grid, 256, 0, st>>>(x, y, n, thresh, 1.f / keep_prob, seed, seed_off);
   else
-    dropout_kernel<false><<<grid, 256, 0, st>>>(x, y, n, thresh, 1.f / keep_prob, seed);
+    dropout_kernel<false><<<grid, 256, 0, st>>>(x, y, n, thresh, 1.f / keep_prob, seed, seed_off);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

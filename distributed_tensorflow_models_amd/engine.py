@@ -7,6 +7,7 @@ runs, one multi-tensor optimizer launch, TF 1.x optimizer / loss semantics.
 import torch
 
 from .ops import _lib
+from .ops import elementwise as _elementwise
 from .ops import fused as _fused
 from .ops import nn as F
 from .ops.optim import FusedOptimizer
@@ -40,6 +41,8 @@ class TrainStep:
         self.last_skip = None   # device int32 flag of the last step (1 = non-finite grads, update skipped)
         self.skipped = 0        # host count, updated by poll_skipped()
         self.timer = timer      # utils.metrics.StepTimer for fwd/bwd/allreduce/optimizer HIP-event sections
+        self._graph = None
+        self._eager_steps = 0
 
     def loss_fn(self, out, labels):
         aux = None
@@ -61,12 +64,12 @@ class TrainStep:
         if self.timer is not None:
             self.timer.mark(name)
 
-    def __call__(self, images, labels):
-        rng = _range_push("train_step")
+    def _forward_backward(self, images, labels):
         self.dp.zero_grad()
         self._mark("start")
         if images.is_cuda:
             _fused.arena.begin_step(images.device)
+            _elementwise.advance_seed_offset(images.device)  # fresh dropout masks, replay included
         try:
             out = self.model(images, training=True)
             loss = self.loss_fn(out, labels)
@@ -88,11 +91,63 @@ class TrainStep:
             else:
                 skip = torch.tensor([0 if bool(torch.isfinite(flat).all()) else 1], dtype=torch.int32)
             self.last_skip = skip
+        return loss.detach(), skip
+
+    def __call__(self, images, labels):
+        if self.use_graph and images.is_cuda:
+            return self._graph_step(images, labels)
+        rng = _range_push("train_step")
+        loss, skip = self._forward_backward(images, labels)
         self.opt.step(self.current_lr(), grad_scale=self.dp.grad_scale, skip_flag=skip)
         self._mark("optimizer")
         self.global_step += 1
         _range_pop(rng)
-        return loss.detach()
+        return loss
+
+    # ---- hipGraph path -----------------------------------------------------------------------
+    # The whole step (zero-grad memset, forward, backward with its hook-issued bucket all-reduces,
+    # NaN guard, fused optimizer, dgrad weight-copy refresh) is captured once into a hipGraph and
+    # replayed: one host submission per step instead of ~600 kernel launches, so launch-bound
+    # models (LeNet, CIFAR nets, small batches) stop being host-bound.  Per-step scalars (lr, EMA
+    # decay, 1/W) live in a device buffer staged before every replay (FusedOptimizer.set_dynamic);
+    # host counters (global_step, EMA num_updates) advance outside the graph.  The first
+    # ``graph_warmup`` steps run eagerly so every lazily grown workspace, the zero-arena high-water
+    # mark and the weight-flip table exist before capture (no allocation inside the graph).
+    graph_warmup = 2
+
+    def _graph_step(self, images, labels):
+        if self._graph is None and self._eager_steps < self.graph_warmup:
+            self._eager_steps += 1
+            self.use_graph = False
+            try:
+                return self(images, labels)
+            finally:
+                self.use_graph = True
+        if self._graph is None:
+            self._static_x = images.clone()
+            self._static_y = labels.clone()
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            timer, self.timer = self.timer, None  # no event records inside the capture
+            try:
+                with torch.cuda.graph(g):
+                    loss, skip = self._forward_backward(self._static_x, self._static_y)
+                    self.opt.launch(skip)
+                    from .ops.nn import refresh_flipped
+                    refresh_flipped()
+            finally:
+                self.timer = timer
+            self._graph, self._static_loss = g, loss
+        else:
+            if images.data_ptr() != self._static_x.data_ptr():
+                self._static_x.copy_(images, non_blocking=True)
+            if labels.data_ptr() != self._static_y.data_ptr():
+                self._static_y.copy_(labels, non_blocking=True)
+        self.opt.set_dynamic(self.current_lr(), self.dp.grad_scale)
+        self._graph.replay()
+        self.opt.num_updates += 1
+        self.global_step += 1
+        return self._static_loss.clone()
 
     def poll_skipped(self):
         """Host-side check of the last step's guard (one small sync; call when logging)."""

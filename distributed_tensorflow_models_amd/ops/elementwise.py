@@ -47,6 +47,35 @@ def hash_u32(seed, n, device="cpu"):
     return _lsr(z, 32)
 
 
+_M64 = (1 << 64) - 1
+
+
+def mix_seed(seed, off):
+    """Host form of the kernel's per-step stream offset (``mix_seed`` in elementwise.hip)."""
+    if off == 0:
+        return seed
+    z = (off * 0x9E3779B97F4A7C15) & _M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return (seed ^ z ^ (z >> 31)) & _M64
+
+
+# device int64 counter per GPU, advanced once per training step by the engine (captured into the
+# hipGraph, so replays advance it too); the dropout kernel reads it at run time
+_seed_off = {}
+
+
+def seed_offset(device):
+    t = _seed_off.get(device.index)
+    if t is None:
+        t = _seed_off[device.index] = torch.zeros(1, dtype=torch.int64, device=device)
+    return t
+
+
+def advance_seed_offset(device):
+    seed_offset(device).add_(1)
+
+
 def _threshold(keep):
     t = int(keep * 4294967296.0)
     return min(t, 0xFFFFFFFF)
@@ -66,7 +95,7 @@ def _dropout_hip(x, keep, seed):
     y = torch.empty_like(x)
     dt = {torch.float32: 0, torch.bfloat16: 1}[x.dtype]
     rc = _lib.lib().dtm_dropout(_lib.ptr(x), _lib.ptr(y), x.numel(), dt, ctypes.c_float(keep),
-                                ctypes.c_ulonglong(seed), _lib.stream_ptr())
+                                ctypes.c_ulonglong(seed), _lib.ptr(seed_offset(x.device)), _lib.stream_ptr())
     if rc:
         raise RuntimeError("dtm_dropout failed (%d)" % rc)
     return y

@@ -77,7 +77,11 @@ class FusedOptimizer:
         self._chunks_dev = torch.from_numpy(ct.view(np.uint8).reshape(-1).copy()).to(dev)
         self._nchunks = len(chunks)
         self._dyn = torch.zeros(3, dtype=torch.float32, device=dev)
-        self._dyn_host = torch.zeros(3, dtype=torch.float32).pin_memory()
+        # ring of pinned staging rows: the host runs ahead of the GPU, so a row is reused only
+        # after the copy that last read it has executed (its event), never overwritten in flight
+        self._dyn_ring = torch.zeros((16, 3), dtype=torch.float32).pin_memory()
+        self._dyn_ev = [None] * 16
+        self._dyn_i = 0
         self._dev = dev
 
     @staticmethod
@@ -97,10 +101,18 @@ class FusedOptimizer:
 
     def set_dynamic(self, lr, grad_scale=1.0):
         """Stage per-step scalars on the device (safe to call before a hipGraph replay)."""
-        self._dyn_host[0] = float(lr)
-        self._dyn_host[1] = float(self.ema_decay_now())
-        self._dyn_host[2] = float(grad_scale)
-        self._dyn.copy_(self._dyn_host, non_blocking=True)
+        i = self._dyn_i
+        self._dyn_i = (i + 1) % len(self._dyn_ev)
+        if self._dyn_ev[i] is not None:
+            self._dyn_ev[i].synchronize()
+        row = self._dyn_ring[i]
+        row[0] = float(lr)
+        row[1] = float(self.ema_decay_now())
+        row[2] = float(grad_scale)
+        self._dyn.copy_(row, non_blocking=True)
+        ev = self._dyn_ev[i] or torch.cuda.Event()
+        ev.record()
+        self._dyn_ev[i] = ev
 
     def launch(self, skip_flag=None):
         """Issue the fused update reading lr/ema/grad_scale from the device scalars."""

@@ -120,6 +120,7 @@ def define_common_flags(flags, preset):
             ("max_staleness", I, 5, "SSP staleness bound in local steps"),
             ("synthetic_data", B, False, "use HBM-resident synthetic batches"),
             ("bucket_mb", Fl, 32.0, "all-reduce bucket size (MB)"),
+            ("use_hipgraph", B, False, "capture the BSP training step in a hipGraph (launch-bound models)"),
             ("trace_steps", S, "", "a:b -> export a Chrome trace of steps [a, b)"),
             ("fresh", B, False, "wipe train_dir before training (the reference always did)"),
             ("log_every", I, 1, "log the per-step line every N steps"),
@@ -241,8 +242,9 @@ def train(preset, flags, default_mode="bsp"):
     if mode == "bsp":
         step_fn = TrainStep(model, bucket_mb=FLAGS.bucket_mb, label_smoothing=cfg.get("label_smoothing", 0.0),
                             aux_weight=cfg.get("aux_weight", 0.4), ema_decay=cfg.get("ema"), lr_schedule=sched,
-                            batch_weight=FLAGS.batch_weight,
-                            timer=StepTimer() if (FLAGS.metrics_file and rank == 0) else None, **opt_kw)
+                            batch_weight=FLAGS.batch_weight, use_graph=FLAGS.use_hipgraph,
+                            timer=StepTimer() if (FLAGS.metrics_file and rank == 0 and not FLAGS.use_hipgraph)
+                            else None, **opt_kw)
         vars_ = model_variables(model, step_fn.opt, gstep)
         vars_[-1].name = cfg.get("global_step_name", "global_step")
         if path:

@@ -118,3 +118,38 @@ def test_launcher_restart_resumes_after_rank_failure(tmp_path):
     assert "==== restart 1 ====" in log0 and "restored" in log0
     st = get_checkpoint_state(train_dir)
     assert st.model_checkpoint_path.endswith("model.ckpt-6")
+
+
+# ---------------------------------------------------------------------------------------------
+# GPU: the bucketed, hook-driven all-reduce with the real HIP kernels producing the gradients.
+# RCCL refuses two ranks on one device, so the 1-GPU box runs two gloo ranks that share cuda:0
+# (gloo reduces device tensors through host staging).  Both ranks see the SAME batch, so the
+# averaged gradient equals the single-rank gradient exactly (x + x then * 1/2) even with BN.
+
+def _bsp_gpu_worker(rank, world, steps=2):
+    from distributed_tensorflow_models_amd.engine import TrainStep
+    from distributed_tensorflow_models_amd.models import nets_factory
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    torch.manual_seed(0)
+    model = nets_factory.build("resnet_v1_50", num_classes=16).to(dev)
+    step = TrainStep(model, optimizer="momentum", lr=0.05, momentum=0.9, bucket_mb=4.0)
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(4, 64, 64, 3, generator=g).to(dev, torch.bfloat16)
+    y = torch.randint(0, 16, (4,), generator=g).to(dev)
+    losses = [float(step(x, y)) for _ in range(steps)]
+    torch.cuda.synchronize()
+    out = {"params": torch.cat([p.detach().float().reshape(-1) for p in model.parameters()]).cpu(),
+           "losses": losses, "buckets": len(step.dp.buckets), "launched": sum(step.dp._launched)}
+    step.dp.close()
+    return out
+
+
+@pytest.mark.gpu
+def test_bsp_gpu_two_ranks_hip_kernels_match_single_rank():
+    single = _bsp_gpu_worker(0, 1)
+    two = run_workers(_bsp_gpu_worker, 2)
+    assert two[0]["buckets"] > 4 and two[0]["launched"] == two[0]["buckets"]
+    assert torch.equal(two[0]["params"], two[1]["params"])
+    torch.testing.assert_close(two[0]["params"], single["params"], rtol=1e-5, atol=1e-6)
+    assert two[0]["losses"] == pytest.approx(single["losses"], rel=1e-5)

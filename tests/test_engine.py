@@ -69,3 +69,56 @@ def test_nan_guard_skips_update_gpu():
     torch.cuda.synchronize()
     assert step.poll_skipped()
     assert all(torch.equal(a, p.detach()) for a, p in zip(before, m.parameters()))
+
+
+def _run_steps(name, use_graph, steps, size, ncls, opt="momentum", ema=None, sched=None, lr=0.05):
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = nets_factory.build(name, num_classes=ncls).to(dev)
+    step = TrainStep(model, optimizer=opt, lr=lr, momentum=0.9, use_graph=use_graph, ema_decay=ema,
+                     lr_schedule=sched)
+    g = torch.Generator().manual_seed(3)
+    cin = 1 if name == "lenet" else 3
+    xs = [torch.randn(4, size, size, cin, generator=g).to(dev, torch.bfloat16) for _ in range(2)]
+    ys = [torch.randint(0, ncls, (4,), generator=g).to(dev) for _ in range(2)]
+    losses = [float(step(xs[i % 2], ys[i % 2])) for i in range(steps)]
+    torch.cuda.synchronize()
+    params = torch.cat([p.detach().float().reshape(-1) for p in model.parameters()])
+    emas = (torch.cat([step.opt.state[p]["ema"].reshape(-1) for p in step.opt.params]) if ema else None)
+    step.dp.close()
+    return losses, params, emas, step
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,size,ncls", [("resnet_v1_50", 64, 16), ("cifar10_cnn", 24, 10)])
+def test_hipgraph_step_matches_eager(name, size, ncls):
+    """Captured-and-replayed steps (alternating input buffers, lr schedule and EMA decay staged per
+    replay) follow the eager trajectory."""
+    sched = lambda s: 0.05 * (0.5 ** (s // 3))  # noqa: E731
+    le, pe, ee, _ = _run_steps(name, False, 6, size, ncls, ema=0.99, sched=sched)
+    lg, pg_, eg, st = _run_steps(name, True, 6, size, ncls, ema=0.99, sched=sched)
+    assert st._graph is not None and st.global_step == 6 and st.opt.num_updates == 6
+    assert lg == pytest.approx(le, rel=2e-2, abs=2e-3)
+    torch.testing.assert_close(pg_, pe, rtol=2e-2, atol=2e-3)
+    torch.testing.assert_close(eg, ee, rtol=2e-2, atol=2e-3)
+
+
+@pytest.mark.gpu
+def test_hipgraph_replay_draws_fresh_dropout_masks():
+    """LeNet (dropout before the logits) under hipGraph replay: the device seed offset advances
+    every replayed step, so masks differ step to step although the host seed was baked in."""
+    from distributed_tensorflow_models_amd.ops import elementwise as E
+    dev = torch.device("cuda", 0)
+    off0 = int(E.seed_offset(dev).item())
+    losses, params, _, st = _run_steps("lenet", True, 6, 28, 10, opt="sgd", lr=1e-4)
+    assert st._graph is not None
+    assert int(E.seed_offset(dev).item()) == off0 + 6
+    assert all(math.isfinite(v) for v in losses) and bool(torch.isfinite(params).all())
+    x = torch.randn(1 << 16, device=dev)
+    E._seed_off[dev.index].fill_(5)
+    a = E.dropout(x, 0.5, seed=99)
+    E._seed_off[dev.index].fill_(6)
+    b = E.dropout(x, 0.5, seed=99)
+    assert not torch.equal(a, b)
+    want = E.dropout_mask(x.shape, 0.5, E.mix_seed(99, 6)).to(dev)
+    assert torch.equal(b != 0, want & (x != 0))
