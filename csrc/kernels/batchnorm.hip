@@ -747,8 +747,8 @@ int dtm_bn_stats_finalize(const float* ws, int rows, int K, const float* gamma, 
     g_fin_k = K;
   }
   if (K % 2) return -1;  // float4 columns over [2K]
-  const int rpb = 256;
-  const int ychunks = (rows + rpb - 1) / rpb;
+  int rpb, ychunks;
+  dtm_reduce_split(rows, (2 * K + 63) / 64, &rpb, &ychunks);
   hipLaunchKernelGGL(stats_reduce_finalize_kernel, dim3((2 * K + 63) / 64, ychunks), dim3(256), 0, st, ws, rows, K, rpb,
                      g_fin_acc, g_fin_counter, gamma, beta, mov_mean, mov_var, ss, count, eps, decay, update, bessel);
   return 0;

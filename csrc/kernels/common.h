@@ -58,6 +58,7 @@ __host__ static inline FastDiv make_fastdiv(uint32_t d) {
 // workspace arena + two-stage reduction (workspace.hip)
 float* dtm_ws_get(size_t floats);
 void dtm_reduce_rows(const float* ws, int rows, int width, int ld, float* out, hipStream_t st);
+void dtm_reduce_split(int rows, int xblocks, int* rpb, int* ychunks);
 int dtm_bn_stats_finalize(const float* ws, int rows, int K, const float* gamma, const float* beta, float* mov_mean,
                           float* mov_var, float* ss, float count, float eps, float decay, int update, int bessel,
                           hipStream_t st);

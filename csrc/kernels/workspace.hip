@@ -75,10 +75,38 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
   else atomicAdd(out + j, s);
 }
 
+// Row split of a [rows][width] partial-sum reduction (16 lanes x 4 columns, 16 row lanes per block).
+// The partial slabs are only a few MB, so a small grid is latency-bound (64 blocks took 7-10 us);
+// more row chunks mean more atomics per output column.  Policy (A/B-able at run time):
+// g_red_target = total blocks wanted (0 = legacy fixed 256 rows per block), g_red_maxy = cap on row
+// chunks (= atomics per output column).
+static int g_red_target = 0, g_red_maxy = 64;
+DTM_API void dtm_set_reduce_policy(int target_blocks, int max_chunks) {
+  g_red_target = target_blocks;
+  g_red_maxy = max_chunks > 0 ? max_chunks : 1;
+}
+
+void dtm_reduce_split(int rows, int xblocks, int* rpb, int* ychunks) {
+  if (g_red_target <= 0) {
+    *rpb = 256;
+    *ychunks = (rows + 255) / 256;
+    return;
+  }
+  int want = (g_red_target + xblocks - 1) / xblocks;
+  if (want > g_red_maxy) want = g_red_maxy;
+  int maxy = (rows + 15) / 16;
+  if (want > maxy) want = maxy;
+  if (want < 1) want = 1;
+  int r = (rows + want - 1) / want;
+  r = (r + 15) / 16 * 16;
+  *rpb = r;
+  *ychunks = (rows + r - 1) / r;
+}
+
 void dtm_reduce_rows(const float* ws, int rows, int width, int ld, float* out, hipStream_t st) {
   if (width % 4 == 0 && ld % 4 == 0) {
-    int rpb = 256;                         // 16 rows per lane
-    int ychunks = (rows + rpb - 1) / rpb;  // <= ~100 atomics per output
+    int rpb, ychunks;
+    dtm_reduce_split(rows, (width + 63) / 64, &rpb, &ychunks);
     hipLaunchKernelGGL(reduce_rows4_kernel, dim3((width + 63) / 64, ychunks), dim3(256), 0, st, ws, rows, width, ld,
                        out, rpb);
     return;

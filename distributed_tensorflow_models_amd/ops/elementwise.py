@@ -66,6 +66,9 @@ _seed_off = {}
 
 
 def seed_offset(device):
+    device = torch.device(device)
+    if device.index is None:
+        device = torch.device(device.type, torch.cuda.current_device())
     t = _seed_off.get(device.index)
     if t is None:
         t = _seed_off[device.index] = torch.zeros(1, dtype=torch.int64, device=device)

@@ -4,7 +4,8 @@ median ms/step per variant; one device, one process: MI355X_MICROARCH 'DVFS give
 
 VARIANTS="base=;noW=wtile:-3;noT=tile:-3;fused=prologue:fused" python tools/ab_step.py
 keys: tile (conv_nt tile id), wtile[:occ] (wgrad tile id / blocks-per-CU target), prologue (DTM_PROLOGUE),
-stem (DTM_STEM: 1 = packed-row stem path)."""
+stem (DTM_STEM: 1 = packed-row stem path), red (target_blocks:max_chunks of the partial-sum
+reductions; 0 = legacy 256 rows per block)."""
 import os
 import statistics
 import sys
@@ -23,6 +24,8 @@ def apply(cfg):
     L.dtm_conv_set_tile(int(cfg.get("tile", -1)))
     wt = cfg.get("wtile", "-1").split(":")
     L.dtm_conv_set_wgrad_tile(int(wt[0]), int(wt[1]) if len(wt) > 1 else 0)
+    red = cfg.get("red", "0:64").split(":")
+    L.dtm_set_reduce_policy(int(red[0]), int(red[1]))
     os.environ["DTM_PROLOGUE"] = cfg.get("prologue", "auto")
     os.environ["DTM_STEM"] = cfg.get("stem", "1")
 
