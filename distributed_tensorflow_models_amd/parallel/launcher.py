@@ -19,6 +19,8 @@ import subprocess
 import sys
 import time
 
+from ..utils import heartbeat as hbmod
+
 PKG = "distributed_tensorflow_models_amd.trainers"
 
 # (model, mode) -> trainer module; model -> eval module (train.sh:29-61 path conventions)
@@ -70,10 +72,12 @@ def _gpu_count():
         return 0
 
 
-def build_commands(model, mode, nproc, extra, port, eval_=True):
+def build_commands(model, mode, nproc, extra, port, eval_=True, hb_dir=None):
     mod, mode_args = resolve(model, mode)
     env_base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(nproc),
                     DTM_RUN_ID=str(port))
+    if hb_dir:
+        env_base[hbmod.ENV_DIR] = hb_dir
     env_base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     cmds = []
     for r in range(nproc):
@@ -110,41 +114,60 @@ def _kill_group(p, sig=signal.SIGTERM):
         pass
 
 
-def _supervise(procs, poll_s=0.2, grace_s=10.0):
+HANG_EXIT = 124  # exit code reported for a job stopped by the hang detector (as timeout(1) does)
+
+
+def _stop_all(procs, poll_s, grace_s):
+    for p in procs:
+        if p.poll() is None:
+            _kill_group(p)
+    t0 = time.time()
+    while any(p.poll() is None for p in procs) and time.time() - t0 < grace_s:
+        time.sleep(poll_s)
+    for p in procs:
+        if p.poll() is None:
+            _kill_group(p, signal.SIGKILL)
+            p.wait()
+
+
+def _supervise(procs, poll_s=0.2, grace_s=10.0, hb_dir=None, hang_timeout=0.0):
     """Wait for all ranks; when one fails, stop the rest (a dead peer would otherwise leave the
-    survivors blocked in a collective until its timeout).  Returns the first non-zero exit code."""
-    failed = 0
+    survivors blocked in a collective until its timeout).  With ``hang_timeout`` > 0 a rank whose
+    heartbeat is older than that is treated as failed too (a hung rank never exits by itself).
+    Returns the first non-zero exit code (HANG_EXIT for a detected hang)."""
+    started = time.time()
     while True:
         codes = [p.poll() for p in procs]
         bad = [c for c in codes if c not in (None, 0)]
-        if bad and not failed:
-            failed = bad[0]
-            for p in procs:
-                if p.poll() is None:
-                    _kill_group(p)
-            t0 = time.time()
-            while any(p.poll() is None for p in procs) and time.time() - t0 < grace_s:
-                time.sleep(poll_s)
-            for p in procs:
-                if p.poll() is None:
-                    _kill_group(p, signal.SIGKILL)
-                    p.wait()
-            return failed
+        if bad:
+            _stop_all(procs, poll_s, grace_s)
+            return bad[0]
         if all(c is not None for c in codes):
             return 0
+        if hang_timeout > 0 and hb_dir:
+            live = [r for r, c in enumerate(codes) if c is None]
+            stale = [r for r in hbmod.stale_ranks(hb_dir, len(procs), hang_timeout, started) if r in live]
+            if stale:
+                print("launcher: rank(s) %s sent no heartbeat for %.0f s - treating the job as hung"
+                      % (stale, hang_timeout), flush=True)
+                _stop_all(procs, poll_s, grace_s)
+                return HANG_EXIT
         time.sleep(poll_s)
 
 
 def launch(model, mode, nproc, extra, log_dir, eval_=False, eval_delay=20.0, wait=True, port=None,
-           max_restarts=0):
-    """Start ``nproc`` ranks (+ evaluator); with ``max_restarts`` > 0 a failed job is restarted
-    (fresh rendezvous port) and resumes from the latest checkpoint in its train_dir."""
+           max_restarts=0, hang_timeout=0.0):
+    """Start ``nproc`` ranks (+ evaluator); with ``max_restarts`` > 0 a failed (or, with
+    ``hang_timeout`` > 0, hung) job is restarted (fresh rendezvous port) and resumes from the latest
+    checkpoint in its train_dir."""
     os.makedirs(log_dir, exist_ok=True)
+    hb_dir = os.path.join(log_dir, "heartbeat")
     evp = None
     attempt = 0
     with open(os.path.join(log_dir, "pids"), "w") as pf:
         while True:
-            cmds, ev = build_commands(model, mode, nproc, extra, port or free_port(), eval_)
+            hbmod.clear(hb_dir)
+            cmds, ev = build_commands(model, mode, nproc, extra, port or free_port(), eval_, hb_dir)
             # a restart must resume, so never pass --fresh again
             if attempt:
                 cmds = [(n, [a for a in c if a not in ("--fresh", "--fresh=true", "--fresh=True")],
@@ -159,7 +182,7 @@ def launch(model, mode, nproc, extra, log_dir, eval_=False, eval_delay=20.0, wai
                 pf.flush()
             if not wait:
                 return procs
-            rc = _supervise(procs)
+            rc = _supervise(procs, hb_dir=hb_dir, hang_timeout=hang_timeout)
             if rc == 0 or attempt >= max_restarts:
                 break
             attempt += 1
@@ -198,6 +221,8 @@ def main(argv=None):
     ap.add_argument("--eval_delay", type=float, default=20.0)
     ap.add_argument("--stop", action="store_true")
     ap.add_argument("--max_restarts", type=int, default=0, help="restart a failed job and resume")
+    ap.add_argument("--hang_timeout", type=float, default=0.0,
+                    help="seconds without a rank heartbeat before the job counts as hung (0 = off)")
     ap.add_argument("--dry_run", action="store_true")
     a, extra = ap.parse_known_args(argv)
     if extra and extra[0] == "--":
@@ -215,7 +240,8 @@ def main(argv=None):
             print("%s: RANK=%s WORLD_SIZE=%s %s" % (name, env.get("RANK", "-"), env.get("WORLD_SIZE", "-"),
                                                    " ".join(cmd)))
         return 0
-    return launch(a.model, a.mode, nproc, extra, log_dir, a.eval, a.eval_delay, max_restarts=a.max_restarts)
+    return launch(a.model, a.mode, nproc, extra, log_dir, a.eval, a.eval_delay, max_restarts=a.max_restarts,
+                  hang_timeout=a.hang_timeout)
 
 
 if __name__ == "__main__":

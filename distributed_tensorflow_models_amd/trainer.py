@@ -23,6 +23,7 @@ from .compat.train import ExponentialDecay, Server
 from .engine import TrainStep
 from .models import nets_factory
 from .parallel import process_group as pg
+from .utils.heartbeat import Heartbeat
 from .utils.metrics import JsonlMetrics, StepTimer, format_step
 from .utils.profiler import StepTracer
 
@@ -126,7 +127,7 @@ def define_common_flags(flags, preset):
             ("log_every", I, 1, "log the per-step line every N steps"),
             ("metrics_file", S, "", "JSONL metrics path (rank 0)"),
             ("batch_weight", Fl, 1.0, "per-rank gradient weight b_r/b_nominal (C15)"),
-            ("fault_inject", S, "", "rank:step -> hard-exit that rank at that step (resume tests)"),
+            ("fault_inject", S, "", "rank:step[:hang] -> hard-exit (or hang) that rank at that step (resume tests)"),
             ("seed", I, 0, "random seed"),
             ("depth_multiplier", Fl, 1.0, "MobileNet depth multiplier"),
             ("fine_tune_checkpoint", S, "", "initialise model variables from this checkpoint (fresh runs only)"),
@@ -295,14 +296,19 @@ def train(preset, flags, default_mode="bsp"):
     tracer = StepTracer(FLAGS.trace_steps, os.path.join(FLAGS.train_dir, "traces"), rank)
     fault = None
     if FLAGS.fault_inject and os.environ.get("DTM_ATTEMPT", "0") == "0":  # only the first attempt
-        fr, fs = FLAGS.fault_inject.split(":")
-        fault = (int(fr), int(fs))
+        parts = FLAGS.fault_inject.split(":")
+        fault = (int(parts[0]), int(parts[1]), parts[2] if len(parts) > 2 else "exit")
+    heartbeat = Heartbeat(rank)
 
     # ---- loop (reference hot loop) ------------------------------------------------
     step = start if mode == "bsp" else 0
     loss_v = float("nan")
     while step < FLAGS.max_steps:
         if fault and fault[0] == rank and fault[1] == step:
+            if fault[2] == "hang":
+                logging.error("fault injection: rank %d hangs at step %d", rank, step)
+                while True:  # a wedged rank: alive, silent, never reaches the next collective
+                    time.sleep(3600)
             logging.error("fault injection: rank %d exits at step %d", rank, step)
             os._exit(17)
         tracer.step(step)
@@ -339,6 +345,7 @@ def train(preset, flags, default_mode="bsp"):
             logging.info("train-batch precision @ 1 = %.3f", acc)
         if mode == "bsp" or is_chief:
             sv.maybe_save(gs, force=bool(FLAGS.save_every_steps) and gs % FLAGS.save_every_steps == 0)
+        heartbeat.beat(step)
         step += 1
     if mode in ("asp", "ssp"):
         if clock is not None:

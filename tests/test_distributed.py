@@ -154,3 +154,38 @@ def test_bsp_gpu_two_ranks_hip_kernels_match_single_rank():
     # BN statistics are summed with fp32 atomics (order varies run to run): not bit-exact across runs
     torch.testing.assert_close(two[0]["params"], single["params"], rtol=1e-3, atol=1e-5)
     assert two[0]["losses"] == pytest.approx(single["losses"], rel=1e-4)
+
+
+def test_launcher_detects_hung_rank_and_resumes(tmp_path):
+    """A rank that stops making progress (alive, silent) is caught by the heartbeat monitor; the job
+    is stopped and restarted from the latest checkpoint."""
+    from distributed_tensorflow_models_amd.ckpt.saver import get_checkpoint_state
+    from distributed_tensorflow_models_amd.parallel import launcher
+    train_dir = str(tmp_path / "train")
+    extra = ["--max_steps=6", "--batch_size=4", "--train_dir=" + train_dir, "--data_dir=/nonexistent",
+             "--save_every_steps=1", "--fault_inject=1:3:hang", "--fresh"]
+    env_keep = dict(os.environ)
+    os.environ["OMP_NUM_THREADS"] = "2"
+    t0 = time.time()
+    try:
+        rc = launcher.launch("cnn", "bsp", 2, extra, str(tmp_path / "logs"), max_restarts=1, hang_timeout=20.0)
+    finally:
+        os.environ.clear()
+        os.environ.update(env_keep)
+    log1 = open(tmp_path / "logs" / "worker_1.log").read()
+    assert rc == 0, log1[-3000:]
+    assert "hangs at step 3" in log1 and "==== restart 1 ====" in log1
+    assert get_checkpoint_state(train_dir).model_checkpoint_path.endswith("model.ckpt-6")
+    assert time.time() - t0 < 240
+
+
+def test_heartbeat_staleness(tmp_path):
+    from distributed_tensorflow_models_amd.utils import heartbeat as hb
+    d = str(tmp_path / "hb")
+    h = hb.Heartbeat(0, d, min_interval_s=0.0)
+    h.beat(5)
+    assert hb.read(d, 0)[0] == 5
+    now = time.time()
+    assert hb.stale_ranks(d, 2, 10.0, started_at=now - 5, now=now) == []         # rank 1 still starting
+    assert hb.stale_ranks(d, 2, 10.0, started_at=now - 30, now=now) == [1]       # rank 1 never beat
+    assert hb.stale_ranks(d, 2, 10.0, started_at=now - 30, now=now + 60) == [0, 1]
