@@ -1327,22 +1327,6 @@ __global__ __launch_bounds__(256) void conv_wgrad_pipe_kernel(ConvWgradArgs a) {
 // ------------------------------------------------------------------------------------------
 // weight re-layouts
 // dgrad weight: Wt[c][R-1-r][S-1-s][k] = W[k][r][s][c]   (bf16 -> bf16)
-__global__ void weight_flip_transpose_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wt,
-                                             int K, int R, int S, int C) {
-  size_t total = (size_t)K * R * S * C;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
-       i += (size_t)gridDim.x * blockDim.x) {
-    // i indexes the destination [c][r'][s'][k]
-    int k = i % K;
-    size_t t = i / K;
-    int s2 = t % S; t /= S;
-    int r2 = t % R;
-    int c = t / R;
-    int r = R - 1 - r2, s = S - 1 - s2;
-    wt[i] = w[(((size_t)k * R + r) * S + s) * C + c];
-  }
-}
-
 // one launch refreshing the flipped/transposed dgrad copies of many conv weights (after the
 // optimizer step) instead of one tiny launch per conv in every backward
 struct FlipDesc {
@@ -1350,17 +1334,51 @@ struct FlipDesc {
   bf16_t* wt;
   int K, R, S, C;
 };
-__global__ void weight_flip_batched_kernel(const FlipDesc* __restrict__ descs) {
-  const FlipDesc f = descs[blockIdx.y];
-  const size_t total = (size_t)f.K * f.R * f.S * f.C;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    int k = i % f.K;
-    size_t t = i / f.K;
-    int s2 = t % f.S; t /= f.S;
-    int r2 = t % f.R;
-    int c = t / f.R;
-    f.wt[i] = f.w[(((size_t)k * f.R + (f.R - 1 - r2)) * f.S + (f.S - 1 - s2)) * f.C + c];
+// One 64(k) x 64(c) tile of one tap through LDS: the source rows are read along c and the flipped
+// destination rows written along k, both coalesced (the old per-element gather read with a stride
+// of R*S*C elements: 0.17 TB/s, 2.9 ms per VGG-16 step for its 103 M-element fc6 kernel).
+constexpr int FLIP_T = 64;
+__device__ __forceinline__ void flip_tile(const FlipDesc& f, int tile, uint16_t (*lds)[FLIP_T + 2]) {
+  const int kt = (f.K + FLIP_T - 1) / FLIP_T, ct = (f.C + FLIP_T - 1) / FLIP_T;
+  const int rs = tile / (kt * ct), rem = tile % (kt * ct);
+  const int k0 = (rem / ct) * FLIP_T, c0 = (rem % ct) * FLIP_T;
+  const int r = rs / f.S, s = rs % f.S;
+  const int rs2 = (f.R - 1 - r) * f.S + (f.S - 1 - s);  // flipped tap in the destination
+  const uint16_t* w = (const uint16_t*)f.w;
+  uint16_t* wt = (uint16_t*)f.wt;
+  const size_t RS = (size_t)f.R * f.S;
+#pragma unroll 4
+  for (int i = threadIdx.x; i < FLIP_T * FLIP_T; i += 256) {
+    const int kk = i / FLIP_T, cc = i % FLIP_T;
+    const int k = k0 + kk, c = c0 + cc;
+    if (k < f.K && c < f.C) lds[kk][cc] = w[((size_t)k * RS + rs) * f.C + c];
   }
+  __syncthreads();
+#pragma unroll 4
+  for (int i = threadIdx.x; i < FLIP_T * FLIP_T; i += 256) {
+    const int cc = i / FLIP_T, kk = i % FLIP_T;
+    const int k = k0 + kk, c = c0 + cc;
+    if (k < f.K && c < f.C) wt[((size_t)c * RS + rs2) * f.K + k] = lds[kk][cc];
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ int flip_tiles(const FlipDesc& f) {
+  return ((f.K + FLIP_T - 1) / FLIP_T) * ((f.C + FLIP_T - 1) / FLIP_T) * f.R * f.S;
+}
+
+// grid (blocks per weight, weights): each block strides over its weight's tiles
+__global__ __launch_bounds__(256) void weight_flip_batched_kernel(const FlipDesc* __restrict__ descs) {
+  __shared__ uint16_t lds[FLIP_T][FLIP_T + 2];
+  const FlipDesc f = descs[blockIdx.y];
+  const int n = flip_tiles(f);
+  for (int t = blockIdx.x; t < n; t += gridDim.x) flip_tile(f, t, lds);
+}
+
+__global__ __launch_bounds__(256) void weight_flip_tiled_kernel(FlipDesc f) {
+  __shared__ uint16_t lds[FLIP_T][FLIP_T + 2];
+  const int n = flip_tiles(f);
+  for (int t = blockIdx.x; t < n; t += gridDim.x) flip_tile(f, t, lds);
 }
 
 }  // namespace dtm
@@ -1733,14 +1751,15 @@ DTM_API int dtm_flip_desc_bytes() { return (int)sizeof(FlipDesc); }
 
 DTM_API void dtm_weight_flip_transpose_batched(const void* descs, int n, void* stream) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(weight_flip_batched_kernel, dim3(64, n), dim3(256), 0, (hipStream_t)stream,
+  // 512 blocks per weight: a small weight's extra blocks exit at once, a large one's stride over
+  // its tiles with the chip covered
+  hipLaunchKernelGGL(weight_flip_batched_kernel, dim3(512, n), dim3(256), 0, (hipStream_t)stream,
                      (const FlipDesc*)descs);
 }
 
 DTM_API void dtm_weight_flip_transpose(const void* w, void* wt, int K, int R, int S, int C, void* stream) {
-  size_t total = (size_t)K * R * S * C;
-  int blocks = (int)((total + 255) / 256);
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(weight_flip_transpose_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16_t*)w, (bf16_t*)wt, K, R, S, C);
+  FlipDesc f{(const bf16_t*)w, (bf16_t*)wt, K, R, S, C};
+  int tiles = ((K + FLIP_T - 1) / FLIP_T) * ((C + FLIP_T - 1) / FLIP_T) * R * S;
+  int blocks = tiles < 2048 ? tiles : 2048;
+  hipLaunchKernelGGL(weight_flip_tiled_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, f);
 }

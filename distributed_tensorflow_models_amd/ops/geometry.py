@@ -113,3 +113,22 @@ def pool_geom(x_shape, kernel, stride, padding="VALID"):
         P = (H + 2 * ph - kh) // sh + 1
         Q = (W + 2 * pw - kw) // sw + 1
     return PoolGeom(N, H, W, C, P, Q, kh, kw, sh, sw, pt, pl, pb, pr)
+
+
+def live_taps(g):
+    """Kernel rows [r0, r1) / cols [s0, s1) that touch at least one real input pixel for some output.
+
+    Taps outside fall on zero padding for EVERY output pixel (e.g. VGG-16's fc6 as a 7x7 'SAME'
+    conv over a 1x1 map in the CIFAR geometry: only the centre tap is live), so the conv equals the
+    conv with the kernel cropped to the live window and the paddings reduced to match."""
+    st = g.stride
+    r0 = max(0, g.pad_h - (g.P - 1) * st)
+    r1 = min(g.R - 1, g.H - 1 + g.pad_h) + 1
+    s0 = max(0, g.pad_w - (g.Q - 1) * st)
+    s1 = min(g.S - 1, g.W - 1 + g.pad_w) + 1
+    return r0, r1, s0, s1
+
+
+def cropped_geom(g, r0, r1, s0, s1):
+    return ConvGeom(g.N, g.H, g.W, g.C, g.K, r1 - r0, s1 - s0, g.P, g.Q, g.stride, g.pad_h - r0, g.pad_w - s0,
+                    g.pad_b - (g.R - r1), g.pad_r - (g.S - s1), g.dilation)

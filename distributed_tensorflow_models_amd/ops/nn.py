@@ -15,7 +15,7 @@ import torch
 
 from . import _lib
 from . import reference as ref
-from .geometry import conv_geom, pool_geom
+from .geometry import conv_geom, cropped_geom, live_taps, pool_geom
 from .lazy import LazyBN, as_tensor
 
 _grad_ready_hooks = []
@@ -180,6 +180,12 @@ def conv2d(x, w, bias=None, stride=1, padding="SAME", relu=False, dilation=1):
     if dilation != 1:
         return _atrous_conv2d(x, w, bias, stride, padding, relu, dilation)
     g = conv_geom(tuple(x.shape), tuple(w.shape), stride, padding, dilation)
+    r0, r1, s0, s1 = live_taps(g)
+    if (r1 - r0, s1 - s0) != (g.R, g.S):
+        # taps that only ever read zero padding are skipped: their products are zero, and so is
+        # their weight gradient (VGG-16 fc6 on a 1x1 map: 49x fewer MACs in fwd, dgrad and wgrad)
+        w = _CropTaps.apply(w, r0, r1, s0, s1)
+        g = cropped_geom(g, r0, r1, s0, s1)
     if g.C % 8 != 0:
         # pad input channels with zeros (first layer: RGB) so every gather chunk is 16 B
         cp = (g.C + 7) // 8 * 8
@@ -297,6 +303,31 @@ def conv2d_transpose(x, w, bias=None, stride=2, padding="SAME", relu=False):
     if bias is not None:
         y = y + bias.to(y.dtype)
     return torch.relu(y) if relu else y
+
+
+class _CropTaps(torch.autograd.Function):
+    """fp32 master [K,R,S,C] -> its live-tap window [K, r0:r1, s0:s1, C] (contiguous) with the bf16
+    compute copy cropped alongside; the window's gradient lands in the master's main_grad slice."""
+
+    @staticmethod
+    def forward(ctx, w, r0, r1, s0, s1):
+        ctx.src, ctx.win = w, (r0, r1, s0, s1)
+        out = w.detach()[:, r0:r1, s0:s1, :].contiguous()
+        out.bf16 = weight_bf16(w)[:, r0:r1, s0:s1, :].contiguous()
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        r0, r1, s0, s1 = ctx.win
+        p = ctx.src
+        mg = getattr(p, "main_grad", None)
+        if mg is not None:
+            mg[:, r0:r1, s0:s1, :].add_(g)
+            _notify(p)
+            return None, None, None, None, None
+        full = torch.zeros(p.shape, device=g.device, dtype=g.dtype)
+        full[:, r0:r1, s0:s1, :] = g
+        return full, None, None, None, None
 
 
 class _PadOutChannels(torch.autograd.Function):

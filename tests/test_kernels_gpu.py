@@ -288,3 +288,60 @@ def test_in_top_k_kernel(B, K, dtype):
     for k in (1, 5):
         got = E.in_top_k(p.to(DEV), t.to(DEV), k).cpu()
         assert torch.equal(got, E.in_top_k(p.float(), t, k))
+
+
+def test_weight_flip_tiled_and_batched():
+    """dgrad weight copies [C][R'][S'][K] (taps flipped) from [K][R][S][C]: the single-weight and the
+    batched (post-optimizer refresh) launches, ragged 64-tiles included."""
+    import numpy as np
+    from distributed_tensorflow_models_amd.ops import _lib
+    L = _lib.lib()
+    shapes = [(64, 3, 3, 64), (100, 7, 7, 24), (2048, 1, 1, 512), (8, 1, 1, 8), (72, 5, 3, 136)]
+    ws = [torch.randn(s, device=DEV).to(torch.bfloat16) for s in shapes]
+    want = [w.flip(1, 2).permute(3, 1, 2, 0).contiguous() for w in ws]
+    for w, ref_ in zip(ws, want):
+        K, R, S, C = w.shape
+        wt = torch.empty(C, R, S, K, device=DEV, dtype=torch.bfloat16)
+        L.dtm_weight_flip_transpose(_lib.ptr(w), _lib.ptr(wt), K, R, S, C, _lib.stream_ptr())
+        assert torch.equal(wt, ref_)
+    outs = [torch.empty_like(r) for r in want]
+    nb = L.dtm_flip_desc_bytes()
+    tab = np.zeros((len(ws), nb // 8), dtype=np.int64)
+    for i, (w, o) in enumerate(zip(ws, outs)):
+        tab[i, 0], tab[i, 1] = w.data_ptr(), o.data_ptr()
+        K, R, S, C = w.shape
+        tab[i, 2:4] = np.array([K, R, S, C], dtype=np.int32).view(np.int64)
+    dev_tab = torch.from_numpy(tab.view(np.uint8).reshape(-1).copy()).to(DEV)
+    L.dtm_weight_flip_transpose_batched(_lib.ptr(dev_tab), len(ws), _lib.stream_ptr())
+    torch.cuda.synchronize()
+    for o, r in zip(outs, want):
+        assert torch.equal(o, r)
+
+
+@pytest.mark.parametrize("H,R,K,C,use_main_grad", [(1, 7, 256, 64, True), (2, 5, 24, 16, False), (3, 7, 16, 8, True)])
+def test_conv_dead_taps_cropped(H, R, K, C, use_main_grad):
+    """Taps that only ever read zero padding are cropped away (VGG fc6 on a 1x1 map): y, dx and
+    the full-size dw (zeros on the dead taps) match the fp32 reference of the uncropped conv."""
+    from distributed_tensorflow_models_amd.ops import nn as F
+    from distributed_tensorflow_models_amd.ops import reference as ref
+    torch.manual_seed(0)
+    x = torch.randn(8, H, H, C)
+    w = torch.nn.Parameter(torch.randn(K, R, R, C) * 0.1)
+    dy = torch.randn(8, H, H, K)
+    xr = x.clone().requires_grad_()
+    wr = w.detach().clone().requires_grad_()
+    yr = ref.conv2d(xr, wr, None, 1, "SAME", False, 1)
+    yr.backward(dy)
+    wg = torch.nn.Parameter(w.detach().to(DEV))
+    if use_main_grad:
+        wg.main_grad = torch.zeros(wg.shape, device=DEV)
+    xg = x.to(DEV, torch.bfloat16).requires_grad_()
+    y = F.conv2d(xg, wg, None, 1, "SAME")
+    y.backward(dy.to(DEV, torch.bfloat16))
+    dw = wg.main_grad if use_main_grad else wg.grad
+    for a, b in ((y, yr), (xg.grad, xr.grad), (dw, wr.grad)):
+        a = a.float().cpu()
+        assert ((a - b).norm() / b.norm()).item() < 2e-2
+    c = R // 2
+    if H == 1:
+        assert float(dw.abs().sum() - dw[:, c, c].abs().sum()) == 0.0  # only the centre tap is live
