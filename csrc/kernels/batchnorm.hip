@@ -333,7 +333,7 @@ __global__ __launch_bounds__(256) void bn_stats_fast(const bf16_t* __restrict__ 
 __global__ __launch_bounds__(256) void bn_apply_fast(const bf16_t* __restrict__ x, const float* __restrict__ ss,
                                                      const bf16_t* __restrict__ res, const float* __restrict__ rss,
                                                      bf16_t* __restrict__ y, uint8_t* __restrict__ mask, int M, int C,
-                                                     int res_mode, int relu, int rpb) {
+                                                     int res_mode, int relu, int rpb, int ldy) {
   const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t % cols) * 8, lr0 = t / cols;
   float sc[8], sh[8], rsc[8], rsh[8];
 #pragma unroll
@@ -373,7 +373,7 @@ __global__ __launch_bounds__(256) void bn_apply_fast(const bf16_t* __restrict__ 
         }
         if (mask) mask[((size_t)rr * C + c0) >> 3] = (uint8_t)bits;
       }
-      *(uint4*)(y + (size_t)rr * C + c0) = pack8(f);
+      *(uint4*)(y + (size_t)rr * ldy + c0) = pack8(f);  // ldy > C: a channel slice of a concat
     }
   }
 }
@@ -651,7 +651,7 @@ DTM_API int dtm_bn_apply2(const void* x, const float* ss, const void* res, const
   if (fast_ok(M, C)) {
     int blocks, rpb; fast_grid(M, C, &blocks, &rpb);
     hipLaunchKernelGGL(bn_apply_fast, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ss,
-                       (const bf16_t*)res, rss, (bf16_t*)y, (uint8_t*)mask, (int)M, C, res_mode, relu, rpb);
+                       (const bf16_t*)res, rss, (bf16_t*)y, (uint8_t*)mask, (int)M, C, res_mode, relu, rpb, C);
     return 0;
   }
   if (mask) return -7;
@@ -661,6 +661,19 @@ DTM_API int dtm_bn_apply2(const void* x, const float* ss, const void* res, const
   else
     hipLaunchKernelGGL(bn_apply_kernel<1>, dim3(grid_for(M * C)), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)x, ss, (const bf16_t*)res, rss, (bf16_t*)y, M, C, res_mode, relu);
+  return 0;
+}
+
+// Zero-copy concat: y = relu?(x*scale + shift) written as channels [0, C) of rows of
+// ldy channels -- the caller passes y = concat buffer + channel offset, so an Inception branch output
+// lands in its slice of the block output and no concat copy exists.  16-B aligned slices only.
+DTM_API int dtm_bn_apply_ld(const void* x, const float* ss, void* y, void* mask, long M, int C, int relu, int ldy,
+                            void* stream) {
+  if (!fast_ok(M, C) || ldy < C || ldy % 8 || ((uintptr_t)y & 15) || M * (long)ldy >= (1l << 40)) return -1;
+  int blocks, rpb; fast_grid(M, C, &blocks, &rpb);
+  hipLaunchKernelGGL(bn_apply_fast, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ss,
+                     (const bf16_t*)nullptr, (const float*)nullptr, (bf16_t*)y, (uint8_t*)mask, (int)M, C, 0, relu, rpb,
+                     ldy);
   return 0;
 }
 

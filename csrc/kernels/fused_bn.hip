@@ -38,7 +38,7 @@ __global__ __launch_bounds__(256) void bn_apply_bwd_kernel(const bf16_t* __restr
                                                            const bf16_t* __restrict__ r, const float* __restrict__ rss,
                                                            bf16_t* __restrict__ dx, bf16_t* __restrict__ dres,
                                                            float* __restrict__ sx, float* __restrict__ sr, int M, int C,
-                                                           int mode, int res_mode, int unscaled, int rpb) {
+                                                           int mode, int res_mode, int unscaled, int rpb, int lddy) {
   __shared__ float red[2][256][8];
   const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t % cols) * 8, lr0 = t / cols;
   float sc[8], sh[8], rsc[8];
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void bn_apply_bwd_kernel(const bf16_t* __restr
       bool ok = rr < r1;
       size_t o = (size_t)rr * C + c0;
       uint4 z = make_uint4(0, 0, 0, 0);
-      vdy[u] = ok ? *(const uint4*)(dy + o) : z;
+      vdy[u] = ok ? *(const uint4*)(dy + (size_t)rr * lddy + c0) : z;  // lddy > C: a concat slice
       vx[u] = ok ? *(const uint4*)(x + o) : z;
       if (mode == 1) vy[u] = ok ? *(const uint4*)(y + o) : z;
       if (mode == 3) mb[u] = ok ? (uint32_t)ymask[o >> 3] : 0u;
@@ -275,9 +275,26 @@ DTM_API int dtm_bn_apply_bwd(const void* dy, const void* y, const void* ymask, c
   if (!ws) return -4;
   hipLaunchKernelGGL(bn_apply_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
                      (const bf16_t*)y, (const uint8_t*)ymask, (const bf16_t*)x, ss, (const bf16_t*)r, rss, (bf16_t*)dx,
-                     (bf16_t*)dres, ws, nullptr, (int)M, C, mode, res_mode, unscaled, rpb);
+                     (bf16_t*)dres, ws, nullptr, (int)M, C, mode, res_mode, unscaled, rpb, C);
   dtm_reduce_rows(ws, blocks, 2 * C, 4 * C, sx, (hipStream_t)stream);
   if (res_mode == 2) dtm_reduce_rows(ws + 2 * C, blocks, 2 * C, 4 * C, sr, (hipStream_t)stream);
+  return 0;
+}
+
+// backward of dtm_bn_apply_ld: dy is the channel slice [0, C) of rows of lddy channels (the concat's
+// gradient read in place), ReLU from the forward bitmask, no residual
+DTM_API int dtm_bn_apply_bwd_ld(const void* dy, const void* ymask, const void* x, const float* ss, void* dx, float* sx,
+                                long M, int C, int unscaled, int lddy, void* stream) {
+  if (!shape_ok(M, C) || !ymask || lddy < C || lddy % 8 || ((uintptr_t)dy & 15)) return -1;
+  int blocks, rpb;
+  grid2(M, C, &blocks, &rpb);
+  float* ws = dtm_ws_get((size_t)blocks * 4 * C);
+  if (!ws) return -4;
+  hipLaunchKernelGGL(bn_apply_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
+                     (const bf16_t*)nullptr, (const uint8_t*)ymask, (const bf16_t*)x, ss, (const bf16_t*)nullptr,
+                     (const float*)nullptr, (bf16_t*)dx, (bf16_t*)nullptr, ws, nullptr, (int)M, C, 3, 0, unscaled & 1,
+                     rpb, lddy);
+  dtm_reduce_rows(ws, blocks, 2 * C, 4 * C, sx, (hipStream_t)stream);
   return 0;
 }
 

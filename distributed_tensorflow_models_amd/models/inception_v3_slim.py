@@ -12,6 +12,7 @@ Returns (logits, aux_logits) in training mode; the trainer weights the aux loss 
 import torch
 
 from ..ops import nn as F
+from ..ops.fused import concat_channels
 from .layers import BatchNorm, Conv2d, Dropout, FullyConnected, Layer
 
 
@@ -146,10 +147,11 @@ class InceptionV3Slim(Layer):
             elif op == "max3s2":
                 x = F.max_pool(x, 3, 2, "VALID")
             elif isinstance(op, tuple):
-                x = torch.cat([_t(op[1](x, training)), _t(op[2](x, training))], dim=-1)
+                # a 'split' pair ends the branch with two channel parts
+                return [op[1](x, training), op[2](x, training)]
             else:
                 x = op(x, training)
-        return x
+        return [x]
 
     def forward(self, x, training=True, end_points=None):
         net = x
@@ -164,7 +166,8 @@ class InceptionV3Slim(Layer):
                 if end_points is not None:
                     end_points["aux_logits"] = aux
                 continue
-            net = torch.cat([_t(self._run(b, net, training)) for b in branches], dim=-1)
+            # branch outputs written straight into their channel slices (zero-copy concat)
+            net = concat_channels([p for b in branches for p in self._run(b, net, training)])
             if end_points is not None:
                 end_points[name] = net
         k = net.shape[1]

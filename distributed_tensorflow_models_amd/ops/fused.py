@@ -541,3 +541,85 @@ def conv_bn(x, w, bn, stride, padding, training, relu):
         y = _ConvBNFn.apply(x, in_ss, w, None, None, g, None, slot, in_unscaled)
         ss = bn_inference_ss(bn)
     return LazyBN(y, ss, relu, unscaled=training)
+
+
+# ---------------------------------------------------------------------------------------------
+class _ConcatBNApplyFn(torch.autograd.Function):
+    """Zero-copy channel concat (Inception mixed blocks, reference
+    inception/slim/inception_model.py tf.concat(axis=3, ...)): every LazyBN part's BN-apply(+ReLU)
+    writes straight into its channel slice of the block output (row pitch = total channels), and in
+    backward its BN-apply gradient reads the slice of the concat gradient in place - neither the
+    concat copy nor the split copies of its gradient exist.  Plain-tensor parts (max-pool branches)
+    are copied into their slice.  meta: per part ('bn', C, relu, unscaled) or ('t', C)."""
+
+    @staticmethod
+    def forward(ctx, meta, *ts):
+        L = _lib.lib()
+        first = ts[0]
+        N, H, W = first.shape[:3]
+        Ct = sum(m[1] for m in meta)
+        M = N * H * W
+        out = torch.empty((N, H, W, Ct), device=first.device, dtype=torch.bfloat16)
+        saved, off, i = [], 0, 0
+        s = _lib.stream_ptr()
+        for m in meta:
+            C = m[1]
+            if m[0] == "bn":
+                raw, ss = ts[i], ts[i + 1]
+                i += 2
+                mask = torch.empty(M * C // 8, device=raw.device, dtype=torch.uint8)
+                _check(L.dtm_bn_apply_ld(_lib.ptr(raw), _lib.ptr(ss), ctypes.c_void_p(out.data_ptr() + 2 * off),
+                                         _lib.ptr(mask), M, C, int(m[2]), Ct, s), "bn_apply_ld")
+                saved += [raw, ss, mask]
+            else:
+                out[..., off:off + C].copy_(ts[i])
+                i += 1
+            off += C
+        ctx.meta = meta
+        ctx.save_for_backward(*saved)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        L = _lib.lib()
+        dout = dout.contiguous()
+        saved = list(ctx.saved_tensors)
+        Ct = dout.shape[-1]
+        M = dout.numel() // Ct
+        s = _lib.stream_ptr()
+        grads, off, j = [], 0, 0
+        for m in ctx.meta:
+            C = m[1]
+            if m[0] == "bn":
+                raw, ss, mask = saved[j:j + 3]
+                j += 3
+                dx = torch.empty_like(raw)
+                sx = arena.zeros((4, C), raw.device)
+                _check(L.dtm_bn_apply_bwd_ld(ctypes.c_void_p(dout.data_ptr() + 2 * off), _lib.ptr(mask), _lib.ptr(raw),
+                                             _lib.ptr(ss), _lib.ptr(dx), _lib.ptr(sx), M, C, int(m[3]), Ct, s),
+                       "bn_apply_bwd_ld")
+                grads += [dx, sx]
+            else:
+                grads.append(dout[..., off:off + C])
+            off += C
+        return (None,) + tuple(grads)
+
+
+def concat_channels(parts):
+    """Channel concat of NHWC parts (LazyBN or tensors) with the zero-copy path when every slice is
+    16-byte aligned and each LazyBN part fits the fast BN-apply (C % 8 == 0); otherwise torch.cat."""
+    cuda = all(p.is_cuda for p in parts)
+    ok = cuda and all(p.shape[-1] % 8 == 0 and tuple(p.shape[:3]) == tuple(parts[0].shape[:3]) for p in parts)
+    ok = ok and any(isinstance(p, LazyBN) for p in parts)
+    if not ok:
+        return torch.cat([as_tensor(p) for p in parts], dim=-1)
+    meta, ts = [], []
+    for p in parts:
+        if isinstance(p, LazyBN) and p.relu and p.raw.dtype == torch.bfloat16 and p.shape[-1] // 8 <= 256:
+            meta.append(("bn", p.shape[-1], True, bool(p.unscaled)))
+            ts += [p.raw.contiguous(), p.ss]
+        else:
+            t = as_tensor(p)
+            meta.append(("t", t.shape[-1]))
+            ts.append(t)
+    return _ConcatBNApplyFn.apply(meta, *ts)

@@ -152,3 +152,65 @@ def test_gans_forward_backward(kind):
     torch.cuda.synchronize()
     params = [v for v in st.vars.values() if v.requires_grad]
     assert all(v.grad is not None and torch.isfinite(v.grad).all() for v in params)
+
+
+@pytest.mark.parametrize("Cs", [(64, 96, 32, 48), (320, 384, 384, 192), (8, 16)])
+def test_zero_copy_concat_exact(Cs):
+    """concat_channels of LazyBN parts (+ a plain tensor part) == torch.cat of the materialised parts,
+    bit for bit, forward and backward (raw-input gradient and the BN-statistics gradient)."""
+    from distributed_tensorflow_models_amd.ops.fused import bn_apply, concat_channels
+    from distributed_tensorflow_models_amd.ops.lazy import LazyBN
+    torch.manual_seed(0)
+    N, H, W = 3, 9, 7
+    raws = [torch.randn(N, H, W, c, device=DEV).to(torch.bfloat16) for c in Cs]
+    sss = [torch.cat([torch.rand(1, c, device=DEV) + 0.5, torch.randn(1, c, device=DEV) * 0.3,
+                      torch.randn(2, c, device=DEV)]) for c in Cs]
+    plain = torch.randn(N, H, W, 24, device=DEV).to(torch.bfloat16)
+    dout = torch.randn(N, H, W, sum(Cs) + 24, device=DEV).to(torch.bfloat16)
+    outs = []
+    for zero_copy in (True, False):
+        rs = [r.clone().requires_grad_() for r in raws]
+        ss = [x.clone().requires_grad_() for x in sss]
+        pl = plain.clone().requires_grad_()
+        lz = [LazyBN(r, s, True, unscaled=True) for r, s in zip(rs, ss)]
+        if zero_copy:
+            y = concat_channels(lz + [pl])
+        else:
+            y = torch.cat([bn_apply(r, s, True, None, unscaled=True) for r, s in zip(rs, ss)] + [pl], -1)
+        y.backward(dout)
+        outs.append((y.detach(), [r.grad for r in rs], [s.grad for s in ss], pl.grad))
+    (ya, ra, sa, pa), (yb, rb, sb, pb) = outs
+    assert torch.equal(ya, yb) and torch.equal(pa, pb)
+    for a, b in zip(ra, rb):
+        assert torch.equal(a, b)
+    for a, b in zip(sa, sb):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-4)
+
+
+def test_inception_zero_copy_concat_matches_torch_cat(monkeypatch):
+    """Old-slim Inception-v3 with branch outputs BN-applied straight into their concat slices (and
+    their gradients read in place) vs the same model through torch.cat of materialised branches."""
+    from distributed_tensorflow_models_amd.models import inception_v3_slim as iv3
+    from distributed_tensorflow_models_amd.ops import elementwise as E
+    from distributed_tensorflow_models_amd.ops.lazy import as_tensor
+
+    def run(zero_copy):
+        E._seed[0] = 1234  # same dropout masks in both runs
+        if not zero_copy:
+            monkeypatch.setattr(iv3, "concat_channels", lambda parts: torch.cat([as_tensor(p) for p in parts], -1))
+        torch.manual_seed(0)
+        net = nets_factory.build("inception_v3_slim_old", num_classes=11).to(DEV)
+        g = torch.Generator().manual_seed(1)
+        x = torch.randn(2, 299, 299, 3, generator=g).to(DEV, torch.bfloat16)
+        logits, aux = net(x, training=True)
+        (logits.float().square().mean() + 0.4 * aux.float().square().mean()).backward()
+        torch.cuda.synchronize()
+        monkeypatch.undo()
+        grads = torch.cat([p.grad.float().reshape(-1) for p in net.parameters() if p.grad is not None])
+        return logits.float(), grads
+
+    la, ga = run(True)
+    lb, gb = run(False)
+    lc, gc = run(False)  # noise floor: the same path twice (BN statistics use fp32 atomics)
+    assert _rel(la, lb) < max(3 * _rel(lc, lb), 1e-2)
+    assert _rel(ga, gb) < max(3 * _rel(gc, gb), 2e-2)
