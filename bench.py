@@ -52,15 +52,22 @@ def main():
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the step in a hipGraph (1/0); -1 = auto: on for launch-bound models on 1 GPU")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--device", default="cuda", choices=("cuda", "cpu"),
+                    help="cpu: the plumbing config (LeNet over gloo, no GPU; BASELINE.json config 1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = args.device == "cpu"
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
+        if cpu:
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cpu") if cpu else torch.device("cuda", local_rank)
+    sync = (lambda: None) if cpu else torch.cuda.synchronize
 
     from distributed_tensorflow_models_amd.engine import TrainStep
     from distributed_tensorflow_models_amd.models import nets_factory
@@ -68,7 +75,7 @@ def main():
     if args.graph < 0:
         # measured on one MI355X: LeNet 396k -> 875k img/s with the captured step; ResNet-50 and
         # VGG-16 are GPU-bound (same ms/step either way), so they stay eager
-        args.graph = int(args.model == "lenet" and world == 1)
+        args.graph = int(args.model == "lenet" and world == 1 and not cpu)
     torch.manual_seed(1234 + rank)
     S0, ncls, B0, opt, extra = PRESETS[args.model]
     S = args.image_size or S0
@@ -78,18 +85,18 @@ def main():
     step = TrainStep(net, optimizer=opt, lr=0.1 * world if opt == "momentum" else 0.01 * world, momentum=0.9,
                      bucket_mb=args.bucket_mb, use_graph=bool(args.graph), **extra)
     cin = 1 if args.model == "lenet" else 3
-    images = torch.randn(B, S, S, cin, device=dev).to(torch.bfloat16)
+    images = torch.randn(B, S, S, cin, device=dev).to(torch.float32 if cpu else torch.bfloat16)
     labels = torch.randint(0, ncls, (B,), device=dev)
 
     for _ in range(args.warmup):
         step(images, labels)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step(images, labels)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
@@ -102,7 +109,7 @@ def main():
     if rank == 0:
         out = {
             "metric": HEADLINE_METRIC if args.model == "resnet_v1_50" else
-            "images/sec (whole node) %s %dx%d bf16 training" % (args.model, S, S),
+            "images/sec (whole node) %s %dx%d %s training" % (args.model, S, S, "fp32 cpu" if cpu else "bf16"),
             "value": round(value, 2),
             "unit": "images/sec",
             "n_gpus": world,
@@ -112,10 +119,11 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
-            "dtype": "bf16",
-            "data": "synthetic (random %dx%dx%d bf16 images, random labels, random-init weights)" % (S, S, cin),
+            "dtype": "fp32" if cpu else "bf16",
+            "data": "synthetic (random %dx%dx%d %s images, random labels, random-init weights)" % (
+                S, S, cin, "fp32" if cpu else "bf16"),
             "config": {"model": args.model, "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
-                       "image_size": S, "parallelism": "dp%d" % world,
+                       "image_size": S, "parallelism": "dp%d" % world, "device": args.device,
                        "optimizer": {"momentum": "momentum-sgd+wd", "rmsprop": "rmsprop(TF)+wd", "sgd": "sgd+wd"}[opt],
                        "final_loss": round(float(loss), 4)},
         }

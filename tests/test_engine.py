@@ -124,3 +124,23 @@ def test_hipgraph_replay_draws_fresh_dropout_masks():
     assert not torch.equal(a, b)
     want = E.dropout_mask(x.shape, 0.5, E.mix_seed(99, 6)).to(dev)
     assert torch.equal(b != 0, want & (x != 0))
+
+
+def test_bench_cpu_plumbing_json():
+    """bench.py contract on the CPU plumbing config (BASELINE.json config 1: LeNet, no GPU)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--model", "lenet", "--device", "cpu",
+                          "--steps", "2", "--warmup", "1", "--batch", "16"], capture_output=True, text=True,
+                         timeout=300, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    r = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in r
+    assert r["steps"] == 2 and r["n_gpus"] == 1 and r["value"] > 0 and r["config"]["model"] == "lenet"
