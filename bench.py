@@ -49,6 +49,8 @@ def main():
     ap.add_argument("--model", default="resnet_v1_50", choices=sorted(PRESETS))
     ap.add_argument("--image-size", type=int, default=0)
     ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--grad-comm", default="fp32", choices=("fp32", "bf16"),
+                    help="dtype of the gradient all-reduce on the wire (bf16 halves the xGMI bytes)")
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the step in a hipGraph (1/0); -1 = auto: on for launch-bound models on 1 GPU")
     ap.add_argument("--profile-steps", type=int, default=0)
@@ -83,7 +85,8 @@ def main():
     kw = {"fc_conv_padding": "SAME"} if args.model == "vgg_16" else {}
     net = nets_factory.build(args.model, num_classes=ncls, **kw).to(dev)
     step = TrainStep(net, optimizer=opt, lr=0.1 * world if opt == "momentum" else 0.01 * world, momentum=0.9,
-                     bucket_mb=args.bucket_mb, use_graph=bool(args.graph), **extra)
+                     bucket_mb=args.bucket_mb, use_graph=bool(args.graph),
+                     grad_comm_dtype=torch.bfloat16 if args.grad_comm == "bf16" else None, **extra)
     cin = 1 if args.model == "lenet" else 3
     images = torch.randn(B, S, S, cin, device=dev).to(torch.float32 if cpu else torch.bfloat16)
     labels = torch.randint(0, ncls, (B,), device=dev)
@@ -124,6 +127,7 @@ def main():
                 S, S, cin, "fp32" if cpu else "bf16"),
             "config": {"model": args.model, "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
                        "image_size": S, "parallelism": "dp%d" % world, "device": args.device,
+                       "grad_allreduce_dtype": args.grad_comm,
                        "optimizer": {"momentum": "momentum-sgd+wd", "rmsprop": "rmsprop(TF)+wd", "sgd": "sgd+wd"}[opt],
                        "final_loss": round(float(loss), 4)},
         }

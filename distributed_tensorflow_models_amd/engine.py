@@ -24,11 +24,12 @@ def prepare_compute_copies(model):
 class TrainStep:
     def __init__(self, model, optimizer="momentum", lr=0.1, momentum=0.9, rho=0.9, epsilon=1e-10, bucket_mb=32.0,
                  label_smoothing=0.0, aux_weight=0.4, ema_decay=None, lr_schedule=None, use_graph=False,
-                 process_group=None, weight_decay=None, batch_weight=1.0, nan_guard=True, timer=None):
+                 process_group=None, weight_decay=None, batch_weight=1.0, nan_guard=True, timer=None,
+                 grad_comm_dtype=None):
         self.model = model
         prepare_compute_copies(model)
         params = [p for p in model.parameters() if p.requires_grad]
-        self.dp = BSPDataParallel(params, bucket_mb, process_group)
+        self.dp = BSPDataParallel(params, bucket_mb, process_group, comm_dtype=grad_comm_dtype)
         self.opt = FusedOptimizer(params, optimizer, lr, momentum, rho, epsilon, ema_decay, weight_decay)
         self.lr = lr
         self.lr_schedule = lr_schedule

@@ -15,7 +15,11 @@ Design (MI355X-first):
     asynchronously; RCCL's internal stream waits on the compute stream at issue time, so the
     reduction overlaps the rest of backward;
   * averaging (1/W) and the per-rank batch weight (C15, b_r / b_nominal) are folded into the
-    optimizer's grad_scale / the loss scale - no extra pass over the gradients.
+    optimizer's grad_scale / the loss scale - no extra pass over the gradients;
+  * ``comm_dtype=torch.bfloat16`` (opt-in) sends each bucket as bf16: the bucket is cast into a
+    bf16 shadow right before its all-reduce and cast back after the wait - half the bytes on the
+    xGMI links for communication-bound models (VGG-16: 537 MB of fp32 gradient per step), at the
+    cost of bf16 rounding of the per-rank and summed gradients.
 With world_size == 1 no collective is issued.
 """
 import torch
@@ -25,13 +29,18 @@ from ..ops import nn as opsnn
 
 
 class BSPDataParallel:
-    def __init__(self, params, bucket_mb=32.0, process_group=None, device=None, overlap=True, grad_dtype=torch.float32):
+    def __init__(self, params, bucket_mb=32.0, process_group=None, device=None, overlap=True, grad_dtype=torch.float32,
+                 comm_dtype=None):
         self.params = [p for p in params if p.requires_grad]
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
         dev = device or self.params[0].device
         total = sum(p.numel() for p in self.params)
         self.flat = torch.zeros(total, dtype=grad_dtype, device=dev)
+        self.comm_dtype = comm_dtype if comm_dtype is not None else grad_dtype
+        # low-precision shadow of the flat buffer for the wire (only with more than one rank)
+        self.comm = (torch.empty(total, dtype=self.comm_dtype, device=dev)
+                     if (self.comm_dtype != grad_dtype and self.world > 1) else None)
         # backward order ~ reverse of registration order
         order = list(reversed(self.params))
         self.offsets = {}
@@ -108,7 +117,11 @@ class BSPDataParallel:
         if self.world == 1:
             return
         s, e = self.buckets[bi]
-        self._works.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+        buf = self.flat[s:e]
+        if self.comm is not None:
+            buf = self.comm[s:e]
+            buf.copy_(self.flat[s:e])
+        self._works.append((bi, dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)))
 
     def finish(self):
         """Launch any bucket not yet reduced (unused params / no overlap) and make the current
@@ -116,8 +129,11 @@ class BSPDataParallel:
         for bi in range(len(self.buckets)):
             if not self._launched[bi]:
                 self._launch(bi)
-        for w in self._works:
+        for bi, w in self._works:
             w.wait()
+            if self.comm is not None:
+                s, e = self.buckets[bi]
+                self.flat[s:e].copy_(self.comm[s:e])
         self._works = []
 
     @property

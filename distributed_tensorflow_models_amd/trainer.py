@@ -122,6 +122,7 @@ def define_common_flags(flags, preset):
             ("synthetic_data", B, False, "use HBM-resident synthetic batches"),
             ("bucket_mb", Fl, 32.0, "all-reduce bucket size (MB)"),
             ("use_hipgraph", B, False, "capture the BSP training step in a hipGraph (launch-bound models)"),
+            ("grad_comm_dtype", S, "fp32", "gradient all-reduce dtype on the wire: fp32 | bf16"),
             ("trace_steps", S, "", "a:b -> export a Chrome trace of steps [a, b)"),
             ("fresh", B, False, "wipe train_dir before training (the reference always did)"),
             ("log_every", I, 1, "log the per-step line every N steps"),
@@ -244,6 +245,7 @@ def train(preset, flags, default_mode="bsp"):
         step_fn = TrainStep(model, bucket_mb=FLAGS.bucket_mb, label_smoothing=cfg.get("label_smoothing", 0.0),
                             aux_weight=cfg.get("aux_weight", 0.4), ema_decay=cfg.get("ema"), lr_schedule=sched,
                             batch_weight=FLAGS.batch_weight, use_graph=FLAGS.use_hipgraph,
+                            grad_comm_dtype=torch.bfloat16 if FLAGS.grad_comm_dtype == "bf16" else None,
                             timer=StepTimer() if (FLAGS.metrics_file and rank == 0 and not FLAGS.use_hipgraph)
                             else None, **opt_kw)
         vars_ = model_variables(model, step_fn.opt, gstep)

@@ -17,14 +17,15 @@ def _batch():
     return torch.randn(B, S, S, 3, generator=g), torch.randint(0, 10, (B,), generator=g)
 
 
-def _bsp_worker(rank, world, steps=2):
+def _bsp_worker(rank, world, steps=2, comm=None):
     from distributed_tensorflow_models_amd.engine import TrainStep
     from distributed_tensorflow_models_amd.models import nets_factory
     from distributed_tensorflow_models_amd.parallel import process_group as pg
     torch.manual_seed(0)
     model = nets_factory.build("cifar10_cnn", num_classes=10)
     pg.broadcast_tensors(list(model.parameters()))
-    step = TrainStep(model, optimizer="momentum", lr=0.05, momentum=0.9, ema_decay=0.99, bucket_mb=0.25)
+    step = TrainStep(model, optimizer="momentum", lr=0.05, momentum=0.9, ema_decay=0.99, bucket_mb=0.25,
+                     grad_comm_dtype=comm)
     x, y = _batch()
     per = B // world
     xs, ys = x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per]
@@ -45,6 +46,16 @@ def test_bsp_two_ranks_equal_single_rank_full_batch():
         assert torch.equal(two[r]["params"], two[0]["params"])  # replicas stay bit-identical
     for k in ("params", "ema", "mom"):
         torch.testing.assert_close(two[0][k], single[k], rtol=2e-4, atol=2e-6)
+
+
+def test_bsp_bf16_gradient_communication():
+    """bf16 on the wire: replicas stay identical and track the fp32 all-reduce to bf16 precision."""
+    ref_ = run_workers(_bsp_worker, 2)
+    lo = run_workers(_bsp_worker, 2, 2, torch.bfloat16)
+    assert torch.equal(lo[0]["params"], lo[1]["params"])
+    assert not torch.equal(lo[0]["params"], ref_[0]["params"])  # the bf16 path really ran
+    for k in ("params", "mom"):
+        torch.testing.assert_close(lo[0][k], ref_[0][k], rtol=2e-2, atol=2e-3)
 
 
 def test_bsp_deterministic():
@@ -126,14 +137,14 @@ def test_launcher_restart_resumes_after_rank_failure(tmp_path):
 # (gloo reduces device tensors through host staging).  Both ranks see the SAME batch, so the
 # averaged gradient equals the single-rank gradient exactly (x + x then * 1/2) even with BN.
 
-def _bsp_gpu_worker(rank, world, steps=2):
+def _bsp_gpu_worker(rank, world, steps=2, comm=None):
     from distributed_tensorflow_models_amd.engine import TrainStep
     from distributed_tensorflow_models_amd.models import nets_factory
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     torch.manual_seed(0)
     model = nets_factory.build("resnet_v1_50", num_classes=16).to(dev)
-    step = TrainStep(model, optimizer="momentum", lr=0.05, momentum=0.9, bucket_mb=4.0)
+    step = TrainStep(model, optimizer="momentum", lr=0.05, momentum=0.9, bucket_mb=4.0, grad_comm_dtype=comm)
     g = torch.Generator().manual_seed(7)
     x = torch.randn(4, 64, 64, 3, generator=g).to(dev, torch.bfloat16)
     y = torch.randint(0, 16, (4,), generator=g).to(dev)
@@ -189,3 +200,13 @@ def test_heartbeat_staleness(tmp_path):
     assert hb.stale_ranks(d, 2, 10.0, started_at=now - 5, now=now) == []         # rank 1 still starting
     assert hb.stale_ranks(d, 2, 10.0, started_at=now - 30, now=now) == [1]       # rank 1 never beat
     assert hb.stale_ranks(d, 2, 10.0, started_at=now - 30, now=now + 60) == [0, 1]
+
+
+@pytest.mark.gpu
+def test_bsp_gpu_two_ranks_bf16_wire():
+    # one step: params = p0 - lr*g, so the difference is the bf16 rounding of the gradient itself
+    # (over several steps the 2x2-pixel BN of this tiny ResNet amplifies any rounding chaotically)
+    single = _bsp_gpu_worker(0, 1, 1)
+    two = run_workers(_bsp_gpu_worker, 2, 1, torch.bfloat16)
+    assert torch.equal(two[0]["params"], two[1]["params"])
+    assert ((two[0]["params"] - single["params"]).norm() / single["params"].norm()).item() < 1e-3
