@@ -142,10 +142,12 @@ class InceptionV3Slim(Layer):
     @staticmethod
     def _run(branch, x, training):
         for op in branch:
+            # a pooling branch reads the block input alongside the branch convs: it joins their
+            # gradient hand-off (its backward runs first and stashes; the last conv folds the stash)
             if op == "avg3":
-                x = F.avg_pool(x, 3, 1, "SAME")
+                x = F.avg_pool(x, 3, 1, "SAME", grad_handoff=True)
             elif op == "max3s2":
-                x = F.max_pool(x, 3, 2, "VALID")
+                x = F.max_pool(x, 3, 2, "VALID", grad_handoff=True)
             elif isinstance(op, tuple):
                 # a 'split' pair ends the branch with two channel parts
                 return [op[1](x, training), op[2](x, training)]

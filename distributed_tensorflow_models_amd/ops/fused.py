@@ -216,12 +216,15 @@ class _ConvBNFn(torch.autograd.Function):
                                            _lib.ptr(x_raw), _lib.ptr(in_ss), _lib.ptr(d_in), int(ctx.in_unscaled), s),
                        "conv_dgrad_act")
             else:
-                use_add = last and add_src is not None
+                # every conv consumer folds the pending stash into its own dgrad epilogue (free), so
+                # a tensor read by k consumers costs no separate add at all; a non-last consumer
+                # then leaves its (now cumulative) gradient as the new stash
+                use_add = add_src is not None
                 _check(L.dtm_conv_dgrad_ex(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d),
                                            _lib.ptr(add_src) if use_add else None, add_stride if use_add else 1,
                                            None, None, None, 0, s), "conv_dgrad")
                 if not last:
-                    _slot_stash(ctx.slot, dx)
+                    ctx.slot.buf, ctx.slot.stride = dx, 1
                     dx = None
         if ctx.needs_input_grad[2]:
             mg = getattr(w, "main_grad", None)

@@ -428,16 +428,39 @@ def batch_norm(x, gamma, beta, moving_mean, moving_var, training=True, decay=0.9
 
 # ---------------------------------------------------------------------------------------------
 # pooling
+def _pool_slot(x):
+    """Join the gradient hand-off of a tensor shared with fused conv consumers (an Inception block
+    input feeds three 1x1 convs and a pooling branch): see ops.fused._GradSlot."""
+    from .fused import _slot_register
+    return _slot_register(x)
+
+
+def _pool_grad_out(slot, dx):
+    """Pool backward's input gradient under the hand-off: the pool branch is built last in an
+    Inception block, so its backward runs first and stashes; the last conv consumer folds the stash
+    into its dgrad epilogue - no separate add over the block input."""
+    from .fused import _slot_stash, _slot_take, _unstride
+    if slot is None:
+        return dx
+    last, buf, bst = _slot_take(slot)
+    if not last:
+        _slot_stash(slot, dx, 1)
+        return None
+    if buf is not None:
+        dx = dx + _unstride(slot, buf, bst)
+    return dx
+
+
 class _MaxPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, g):
+    def forward(ctx, x, g, slot=None):
         L = _lib.lib()
         x = x.contiguous()
         y = torch.empty((g.N, g.P, g.Q, g.C), device=x.device, dtype=x.dtype)
         arg = torch.empty((g.N, g.P, g.Q, g.C), device=x.device, dtype=torch.uint8)
         a = g.as_args(_lib.PoolArgs)
         L.dtm_maxpool_fwd(_lib.ptr(x), _lib.ptr(y), _lib.ptr(arg), ctypes.byref(a), _lib.stream_ptr())
-        ctx.g = g
+        ctx.g, ctx.slot = g, slot
         ctx.save_for_backward(arg)
         return y
 
@@ -449,7 +472,7 @@ class _MaxPoolFn(torch.autograd.Function):
         dx = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
         a = g.as_args(_lib.PoolArgs)
         L.dtm_maxpool_bwd(_lib.ptr(dy.contiguous()), _lib.ptr(arg), _lib.ptr(dx), ctypes.byref(a), _lib.stream_ptr())
-        return dx, None
+        return _pool_grad_out(ctx.slot, dx), None, None
 
 
 class _MaxPoolBNReluFn(torch.autograd.Function):
@@ -483,7 +506,11 @@ class _MaxPoolBNReluFn(torch.autograd.Function):
         return dx, sums, None, None
 
 
-def max_pool(x, kernel, stride, padding="VALID"):
+def max_pool(x, kernel, stride, padding="VALID", grad_handoff=False):
+    """``grad_handoff``: x is also read by fused conv consumers whose backward is certain to run
+    (an Inception block input); the pool then joins their gradient hand-off instead of leaving an
+    add to autograd.  Off by default: a registered consumer whose backward never runs (an unused
+    branch) would strand the hand-off."""
     if isinstance(x, LazyBN) and x.relu and x.raw.is_cuda and x.raw.dtype == torch.bfloat16 \
             and x.raw.shape[-1] % 8 == 0 and x.raw.is_contiguous():
         g = pool_geom(tuple(x.raw.shape), kernel, stride, padding)
@@ -495,17 +522,19 @@ def max_pool(x, kernel, stride, padding="VALID"):
     g = pool_geom(tuple(x.shape), kernel, stride, padding)
     if g.KH * g.KW > 255:
         raise ValueError("max-pool window too large for the uint8 argmax")
-    return _MaxPoolFn.apply(x.to(torch.bfloat16), g)
+    xb = x.to(torch.bfloat16)
+    share = grad_handoff and xb is x and xb.is_contiguous()
+    return _MaxPoolFn.apply(xb, g, _pool_slot(xb) if share else None)
 
 
 class _AvgPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, g, count_pad):
+    def forward(ctx, x, g, count_pad, slot=None):
         L = _lib.lib()
         y = torch.empty((g.N, g.P, g.Q, g.C), device=x.device, dtype=torch.bfloat16)
         a = g.as_args(_lib.PoolArgs)
         L.dtm_avgpool_fwd(_lib.ptr(x.contiguous()), _lib.ptr(y), ctypes.byref(a), int(count_pad), _lib.stream_ptr())
-        ctx.g, ctx.cp = g, count_pad
+        ctx.g, ctx.cp, ctx.slot = g, count_pad, slot
         return y
 
     @staticmethod
@@ -515,15 +544,19 @@ class _AvgPoolFn(torch.autograd.Function):
         dx = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
         a = g.as_args(_lib.PoolArgs)
         L.dtm_avgpool_bwd(_lib.ptr(dy.contiguous()), _lib.ptr(dx), ctypes.byref(a), int(ctx.cp), _lib.stream_ptr())
-        return dx, None, None
+        return _pool_grad_out(ctx.slot, dx), None, None, None
 
 
-def avg_pool(x, kernel, stride, padding="VALID", count_pad=False):
+def avg_pool(x, kernel, stride, padding="VALID", count_pad=False, grad_handoff=False):
+    """TF avg pool (SAME excludes the padding from the divisor unless count_pad); grad_handoff as in
+    max_pool."""
     x = as_tensor(x)
     if not x.is_cuda:
         return ref.avg_pool(x, kernel, stride, padding, count_pad)
     g = pool_geom(tuple(x.shape), kernel, stride, padding)
-    return _AvgPoolFn.apply(x.to(torch.bfloat16), g, bool(count_pad))
+    xb = x.to(torch.bfloat16)
+    share = grad_handoff and xb is x and xb.is_contiguous()
+    return _AvgPoolFn.apply(xb, g, bool(count_pad), _pool_slot(xb) if share else None)
 
 
 class _GlobalAvgFn(torch.autograd.Function):
