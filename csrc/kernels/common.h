@@ -59,6 +59,7 @@ __host__ static inline FastDiv make_fastdiv(uint32_t d) {
 float* dtm_ws_get(size_t floats);
 void dtm_reduce_rows(const float* ws, int rows, int width, int ld, float* out, hipStream_t st);
 void dtm_reduce_split(int rows, int xblocks, int* rpb, int* ychunks);
+int dtm_reduce_direct_max();  // grids up to this many blocks reduce with atomics in the producer
 int dtm_bn_stats_finalize(const float* ws, int rows, int K, const float* gamma, const float* beta, float* mov_mean,
                           float* mov_var, float* ss, float count, float eps, float decay, int update, int bessel,
                           hipStream_t st);
@@ -67,13 +68,18 @@ int dtm_bn_stats_finalize(const float* ws, int rows, int K, const float* gamma, 
 // row-lane t / cols; with RP = 256 / cols row-lanes, lanes >= RP*cols idle (C/8 need not divide 256).
 // col_reduce8 sums the per-lane [8] partials of the RP row-lanes of each column in LDS and writes
 // the per-block partial row out0[c0..c0+7], out1[...] (plain stores; reduced later by reduce_rows).
+// atomic: add into the final [C] sums instead (small grids: one launch fewer, <= a few hundred
+// adders per address).
 __device__ __forceinline__ void col_reduce8(float (*red)[256][8], const float* s, const float* q, float* out0,
-                                            float* out1, int cols, int c0) {
+                                            float* out1, int cols, int c0, bool atomic = false) {
   const int t = threadIdx.x, RP = 256 / cols;
   if (RP == 1) {
     if (t < cols) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { out0[c0 + e] = s[e]; out1[c0 + e] = q[e]; }
+      for (int e = 0; e < 8; ++e) {
+        if (atomic) { atomicAdd(out0 + c0 + e, s[e]); atomicAdd(out1 + c0 + e, q[e]); }
+        else { out0[c0 + e] = s[e]; out1[c0 + e] = q[e]; }
+      }
     }
     return;
   }
@@ -99,6 +105,9 @@ __device__ __forceinline__ void col_reduce8(float (*red)[256][8], const float* s
   }
   if (t < cols) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { out0[c0 + e] = red[0][t][e]; out1[c0 + e] = red[1][t][e]; }
+    for (int e = 0; e < 8; ++e) {
+      if (atomic) { atomicAdd(out0 + c0 + e, red[0][t][e]); atomicAdd(out1 + c0 + e, red[1][t][e]); }
+      else { out0[c0 + e] = red[0][t][e]; out1[c0 + e] = red[1][t][e]; }
+    }
   }
 }

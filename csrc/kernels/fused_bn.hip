@@ -38,7 +38,8 @@ __global__ __launch_bounds__(256) void bn_apply_bwd_kernel(const bf16_t* __restr
                                                            const bf16_t* __restrict__ r, const float* __restrict__ rss,
                                                            bf16_t* __restrict__ dx, bf16_t* __restrict__ dres,
                                                            float* __restrict__ sx, float* __restrict__ sr, int M, int C,
-                                                           int mode, int res_mode, int unscaled, int rpb, int lddy) {
+                                                           int mode, int res_mode, int unscaled, int rpb, int lddy,
+                                                           int direct) {
   __shared__ float red[2][256][8];
   const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t % cols) * 8, lr0 = t / cols;
   float sc[8], sh[8], rsc[8];
@@ -116,6 +117,11 @@ __global__ __launch_bounds__(256) void bn_apply_bwd_kernel(const bf16_t* __restr
     }
   }
   // partial row per block in the workspace: [Σg·x | Σg | (residual) Σg·r | Σg]
+  if (direct) {  // small grid: atomics straight into the zeroed [Σg·x | Σg] outputs, no reduce launch
+    col_reduce8(red, a1, a0, sx, sx + C, cols, c0, true);
+    if (res_mode == 2) col_reduce8(red, b1, b0, sr, sr + C, cols, c0, true);
+    return;
+  }
   float* row = sx + (size_t)blockIdx.x * 4 * C;
   col_reduce8(red, a1, a0, row, row + C, cols, c0);
   if (res_mode == 2) col_reduce8(red, b1, b0, row + 2 * C, row + 3 * C, cols, c0);
@@ -271,11 +277,17 @@ DTM_API int dtm_bn_apply_bwd(const void* dy, const void* y, const void* ymask, c
   if ((mode == 3 && !ymask) || (mode == 1 && !y)) return -2;
   int blocks, rpb;
   grid2(M, C, &blocks, &rpb);
+  if (blocks <= dtm_reduce_direct_max()) {
+    hipLaunchKernelGGL(bn_apply_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
+                       (const bf16_t*)y, (const uint8_t*)ymask, (const bf16_t*)x, ss, (const bf16_t*)r, rss,
+                       (bf16_t*)dx, (bf16_t*)dres, sx, sr, (int)M, C, mode, res_mode, unscaled, rpb, C, 1);
+    return 0;
+  }
   float* ws = dtm_ws_get((size_t)blocks * 4 * C);
   if (!ws) return -4;
   hipLaunchKernelGGL(bn_apply_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
                      (const bf16_t*)y, (const uint8_t*)ymask, (const bf16_t*)x, ss, (const bf16_t*)r, rss, (bf16_t*)dx,
-                     (bf16_t*)dres, ws, nullptr, (int)M, C, mode, res_mode, unscaled, rpb, C);
+                     (bf16_t*)dres, ws, nullptr, (int)M, C, mode, res_mode, unscaled, rpb, C, 0);
   dtm_reduce_rows(ws, blocks, 2 * C, 4 * C, sx, (hipStream_t)stream);
   if (res_mode == 2) dtm_reduce_rows(ws + 2 * C, blocks, 2 * C, 4 * C, sr, (hipStream_t)stream);
   return 0;
@@ -288,13 +300,14 @@ DTM_API int dtm_bn_apply_bwd_ld(const void* dy, const void* ymask, const void* x
   if (!shape_ok(M, C) || !ymask || lddy < C || lddy % 8 || ((uintptr_t)dy & 15)) return -1;
   int blocks, rpb;
   grid2(M, C, &blocks, &rpb);
-  float* ws = dtm_ws_get((size_t)blocks * 4 * C);
+  const int direct = blocks <= dtm_reduce_direct_max();
+  float* ws = direct ? sx : dtm_ws_get((size_t)blocks * 4 * C);
   if (!ws) return -4;
   hipLaunchKernelGGL(bn_apply_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
                      (const bf16_t*)nullptr, (const uint8_t*)ymask, (const bf16_t*)x, ss, (const bf16_t*)nullptr,
                      (const float*)nullptr, (bf16_t*)dx, (bf16_t*)nullptr, ws, nullptr, (int)M, C, 3, 0, unscaled & 1,
-                     rpb, lddy);
-  dtm_reduce_rows(ws, blocks, 2 * C, 4 * C, sx, (hipStream_t)stream);
+                     rpb, lddy, direct);
+  if (!direct) dtm_reduce_rows(ws, blocks, 2 * C, 4 * C, sx, (hipStream_t)stream);
   return 0;
 }
 

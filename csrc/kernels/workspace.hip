@@ -80,11 +80,13 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
 // more row chunks mean more atomics per output column.  Policy (A/B-able at run time):
 // g_red_target = total blocks wanted (0 = legacy fixed 256 rows per block), g_red_maxy = cap on row
 // chunks (= atomics per output column).
-static int g_red_target = 0, g_red_maxy = 64;
-DTM_API void dtm_set_reduce_policy(int target_blocks, int max_chunks) {
+static int g_red_target = 0, g_red_maxy = 64, g_red_direct = 0;  // direct: A/B neutral on ResNet-50, -1.6..-7 % on Inception at 256..512
+DTM_API void dtm_set_reduce_policy(int target_blocks, int max_chunks, int direct_max) {
   g_red_target = target_blocks;
   g_red_maxy = max_chunks > 0 ? max_chunks : 1;
+  g_red_direct = direct_max;
 }
+int dtm_reduce_direct_max() { return g_red_direct; }
 
 void dtm_reduce_split(int rows, int xblocks, int* rpb, int* ychunks) {
   if (g_red_target <= 0) {

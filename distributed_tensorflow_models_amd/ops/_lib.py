@@ -76,7 +76,7 @@ _SIGS = {
     "dtm_depthwise_fwd": (_I, [_P, _P, _P, _P, _P]),
     "dtm_depthwise_dgrad": (_I, [_P, _P, _P, _P, _P]),
     "dtm_depthwise_wgrad": (_I, [_P, _P, _P, _P, _P]),
-    "dtm_set_reduce_policy": (None, [_I, _I]),
+    "dtm_set_reduce_policy": (None, [_I, _I, _I]),
     "dtm_bn_apply_ld": (_I, [_P, _P, _P, _P, _L, _I, _I, _I, _P]),
     "dtm_bn_apply_bwd_ld": (_I, [_P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _P]),
     "dtm_dropout": (_I, [_P, _P, _L, _I, _F, ctypes.c_ulonglong, _P, _P]),

@@ -4,8 +4,9 @@ median ms/step per variant; one device, one process: MI355X_MICROARCH 'DVFS give
 
 VARIANTS="base=;noW=wtile:-3;noT=tile:-3;fused=prologue:fused" python tools/ab_step.py
 keys: tile (conv_nt tile id), wtile[:occ] (wgrad tile id / blocks-per-CU target), prologue (DTM_PROLOGUE),
-stem (DTM_STEM: 1 = packed-row stem path), red (target_blocks:max_chunks of the partial-sum
-reductions; 0 = legacy 256 rows per block)."""
+stem (DTM_STEM: 1 = packed-row stem path), red (target_blocks:max_chunks[:direct_max] of the
+partial-sum reductions; 0 = legacy 256 rows per block; direct_max = largest BN-backward grid that
+reduces with atomics in the producer instead of a reduce launch)."""
 import os
 import statistics
 import sys
@@ -24,8 +25,8 @@ def apply(cfg):
     L.dtm_conv_set_tile(int(cfg.get("tile", -1)))
     wt = cfg.get("wtile", "-1").split(":")
     L.dtm_conv_set_wgrad_tile(int(wt[0]), int(wt[1]) if len(wt) > 1 else 0)
-    red = cfg.get("red", "0:64").split(":")
-    L.dtm_set_reduce_policy(int(red[0]), int(red[1]))
+    red = cfg.get("red", "0:64:0").split(":")
+    L.dtm_set_reduce_policy(int(red[0]), int(red[1]), int(red[2]) if len(red) > 2 else 0)
     os.environ["DTM_PROLOGUE"] = cfg.get("prologue", "auto")
     os.environ["DTM_STEM"] = cfg.get("stem", "1")
 
@@ -36,14 +37,18 @@ def main():
         name, _, spec = item.partition("=")
         cfg = dict(kv.split(":", 1) for kv in spec.split(",") if kv)
         variants.append((name, cfg))
-    B = int(os.environ.get("B", "256"))
+    B = int(os.environ.get("B", "0"))
     steps, rounds = int(os.environ.get("STEPS", "6")), int(os.environ.get("ROUNDS", "4"))
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    net = nets_factory.build("resnet_v1_50", num_classes=1000).to(dev)
-    step = TrainStep(net, optimizer="momentum", lr=0.1, momentum=0.9)
-    x = torch.randn(B, 224, 224, 3, device=dev).to(torch.bfloat16)
-    y = torch.randint(0, 1000, (B,), device=dev)
+    model = os.environ.get("MODEL", "resnet_v1_50")
+    from bench import PRESETS
+    S, ncls, B0, opt, extra = PRESETS[model]
+    net = nets_factory.build(model, num_classes=ncls).to(dev)
+    B = B or B0
+    step = TrainStep(net, optimizer=opt, lr=0.01, momentum=0.9, **extra)
+    x = torch.randn(B, S, S, 1 if model == "lenet" else 3, device=dev).to(torch.bfloat16)
+    y = torch.randint(0, ncls, (B,), device=dev)
     res = {n: [] for n, _ in variants}
     for n, cfg in variants:  # warm every variant (workspace growth, first-touch)
         apply(cfg)
