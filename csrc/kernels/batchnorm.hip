@@ -330,6 +330,17 @@ __global__ __launch_bounds__(256) void bn_stats_fast(const bf16_t* __restrict__ 
 
 // mask (optional, relu only): one bit per output element, bit e of byte (row*C + c0)/8 = [y > 0] for
 // channel c0+e -- the ReLU mask the backward needs, 1/16 of the bytes of y.
+typedef unsigned int v4u_bn_t __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ uint4 ld16_bn(const bf16_t* p) {
+  if (NT) {
+    v4u_bn_t v = __builtin_nontemporal_load((const v4u_bn_t*)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+  return *(const uint4*)p;
+}
+
+template <bool NT>
 __global__ __launch_bounds__(256) void bn_apply_fast(const bf16_t* __restrict__ x, const float* __restrict__ ss,
                                                      const bf16_t* __restrict__ res, const float* __restrict__ rss,
                                                      bf16_t* __restrict__ y, uint8_t* __restrict__ mask, int M, int C,
@@ -349,8 +360,8 @@ __global__ __launch_bounds__(256) void bn_apply_fast(const bf16_t* __restrict__ 
     for (int u = 0; u < FU; ++u) {
       int rr = r + u * RP;
       bool ok = rr < r1;
-      v[u] = ok ? *(const uint4*)(x + (size_t)rr * C + c0) : make_uint4(0, 0, 0, 0);
-      if (res_mode) w[u] = ok ? *(const uint4*)(res + (size_t)rr * C + c0) : make_uint4(0, 0, 0, 0);
+      v[u] = ok ? ld16_bn<NT>(x + (size_t)rr * C + c0) : make_uint4(0, 0, 0, 0);
+      if (res_mode) w[u] = ok ? ld16_bn<NT>(res + (size_t)rr * C + c0) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < FU; ++u) {
@@ -650,7 +661,7 @@ DTM_API int dtm_bn_apply2(const void* x, const float* ss, const void* res, const
                           int C, int res_mode, int relu, void* stream) {
   if (fast_ok(M, C)) {
     int blocks, rpb; fast_grid(M, C, &blocks, &rpb);
-    hipLaunchKernelGGL(bn_apply_fast, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ss,
+    hipLaunchKernelGGL((dtm_ntld_bits() & 1) ? bn_apply_fast<true> : bn_apply_fast<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ss,
                        (const bf16_t*)res, rss, (bf16_t*)y, (uint8_t*)mask, (int)M, C, res_mode, relu, rpb, C);
     return 0;
   }
@@ -671,7 +682,7 @@ DTM_API int dtm_bn_apply_ld(const void* x, const float* ss, void* y, void* mask,
                             void* stream) {
   if (!fast_ok(M, C) || ldy < C || ldy % 8 || ((uintptr_t)y & 15) || M * (long)ldy >= (1l << 40)) return -1;
   int blocks, rpb; fast_grid(M, C, &blocks, &rpb);
-  hipLaunchKernelGGL(bn_apply_fast, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ss,
+  hipLaunchKernelGGL((dtm_ntld_bits() & 1) ? bn_apply_fast<true> : bn_apply_fast<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ss,
                      (const bf16_t*)nullptr, (const float*)nullptr, (bf16_t*)y, (uint8_t*)mask, (int)M, C, 0, relu, rpb,
                      ldy);
   return 0;

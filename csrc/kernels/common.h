@@ -59,7 +59,8 @@ __host__ static inline FastDiv make_fastdiv(uint32_t d) {
 float* dtm_ws_get(size_t floats);
 void dtm_reduce_rows(const float* ws, int rows, int width, int ld, float* out, hipStream_t st);
 void dtm_reduce_split(int rows, int xblocks, int* rpb, int* ychunks);
-int dtm_reduce_direct_max();  // grids up to this many blocks reduce with atomics in the producer
+int dtm_reduce_direct_max();
+int dtm_ntld_bits();  // non-temporal input-load policy of the BN-apply kernels (fused_bn.hip)  // grids up to this many blocks reduce with atomics in the producer
 int dtm_bn_stats_finalize(const float* ws, int rows, int K, const float* gamma, const float* beta, float* mov_mean,
                           float* mov_var, float* ss, float count, float eps, float decay, int update, int bessel,
                           hipStream_t st);

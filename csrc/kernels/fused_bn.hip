@@ -25,6 +25,25 @@ __device__ __forceinline__ uint4 pk8(const float* f) {
 }
 
 
+typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ uint4 ld16(const bf16_t* p) {
+  if (NT) {
+    v4u_t v = __builtin_nontemporal_load((const v4u_t*)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+  return *(const uint4*)p;
+}
+template <bool NT>
+__device__ __forceinline__ void st16(bf16_t* p, uint4 u) {
+  if (NT) {
+    v4u_t v = {u.x, u.y, u.z, u.w};
+    __builtin_nontemporal_store(v, (v4u_t*)p);
+  } else {
+    *(uint4*)p = u;
+  }
+}
+
 // y = act(x) path backward.  mode: 0 = plain BN (no relu), 1 = relu with mask from y, 2 = relu with
 // mask recomputed from x*scale+shift.  res_mode 0/1/2 as in bn_apply.
 // sx: [2][C] += (Σ g·x, Σ g)  (the dss of x's BN);  sr: same for a BN'd residual.
@@ -32,6 +51,7 @@ __device__ __forceinline__ uint4 pk8(const float* f) {
 // (BN'd residual): that input's producer is a training conv+BN whose backward applies the BN scale
 // itself (stats_combine_fin prescale), so the gradient handed to it is g, not g*scale; when dx and
 // dres are both g, only dx is written and the caller aliases dres to it.
+template <bool NT>
 __global__ __launch_bounds__(256) void bn_apply_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
                                                            const uint8_t* __restrict__ ymask,
                                                            const bf16_t* __restrict__ x, const float* __restrict__ ss,
@@ -62,11 +82,11 @@ __global__ __launch_bounds__(256) void bn_apply_bwd_kernel(const bf16_t* __restr
       bool ok = rr < r1;
       size_t o = (size_t)rr * C + c0;
       uint4 z = make_uint4(0, 0, 0, 0);
-      vdy[u] = ok ? *(const uint4*)(dy + (size_t)rr * lddy + c0) : z;  // lddy > C: a concat slice
-      vx[u] = ok ? *(const uint4*)(x + o) : z;
-      if (mode == 1) vy[u] = ok ? *(const uint4*)(y + o) : z;
+      vdy[u] = ok ? ld16<NT>(dy + (size_t)rr * lddy + c0) : z;  // lddy > C: a concat slice
+      vx[u] = ok ? ld16<NT>(x + o) : z;
+      if (mode == 1) vy[u] = ok ? ld16<NT>(y + o) : z;
       if (mode == 3) mb[u] = ok ? (uint32_t)ymask[o >> 3] : 0u;
-      if (res_mode == 2) vr[u] = ok ? *(const uint4*)(r + o) : z;
+      if (res_mode == 2) vr[u] = ok ? ld16<NT>(r + o) : z;
     }
 #pragma unroll
     for (int u = 0; u < FU2; ++u) {
@@ -177,6 +197,8 @@ __device__ __forceinline__ void fin_bwd_channel(const float* dss, const float* s
   *db = dsh;
 }
 
+// U rows in flight per lane; NT: non-temporal loads / stores (streamed once, keep L2/MALL for others)
+template <int U, bool NT, bool NTS = NT>
 __global__ __launch_bounds__(256) void stats_combine_fin_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                                 const float* __restrict__ dss, const float* __restrict__ ss,
                                                                 const float* __restrict__ gamma, float count,
@@ -204,25 +226,25 @@ __global__ __launch_bounds__(256) void stats_combine_fin_kernel(const bf16_t* __
     sc[e] = prescale ? ss[c0 + e] : 1.f;  // dy is the unscaled g: the BN-apply gradient is g*scale
   }
   const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
-  for (int row = lr0 < RP ? r0 + lr0 : r1; row < r1; row += RP * FU2) {
-    uint4 vd[FU2], vx[FU2];
+  for (int row = lr0 < RP ? r0 + lr0 : r1; row < r1; row += RP * U) {
+    uint4 vd[U], vx[U];
 #pragma unroll
-    for (int u = 0; u < FU2; ++u) {
+    for (int u = 0; u < U; ++u) {
       int rr = row + u * RP;
       bool ok = rr < r1;
       size_t o = (size_t)rr * C + c0;
-      vd[u] = ok ? *(const uint4*)(dy + o) : make_uint4(0, 0, 0, 0);
-      vx[u] = ok ? *(const uint4*)(x + o) : make_uint4(0, 0, 0, 0);
+      vd[u] = ok ? ld16<NT>(dy + o) : make_uint4(0, 0, 0, 0);
+      vx[u] = ok ? ld16<NT>(x + o) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
-    for (int u = 0; u < FU2; ++u) {
+    for (int u = 0; u < U; ++u) {
       int rr = row + u * RP;
       if (rr >= r1) break;
       float d[8], xv[8];
       up8(vd[u], d); up8(vx[u], xv);
 #pragma unroll
       for (int e = 0; e < 8; ++e) d[e] = fmaf(d[e], sc[e], a[e] + b[e] * xv[e]);
-      *(uint4*)(out + (size_t)rr * C + c0) = pk8(d);
+      st16<NTS>(out + (size_t)rr * C + c0, pk8(d));
     }
   }
 }
@@ -249,12 +271,18 @@ __global__ void bn_finalize_bwd_kernel(const float* __restrict__ dss, const floa
   dstats[C + c] = dvar / count;
 }
 
-static void grid2(long M, int C, int* blocks, int* rpb) {
+// stats-combine stream policy (A/B, tools/ab_step.py sc:): non-temporal loads of the two last-use
+// streams, 4096-block cap: -0.9 % ResNet-50 step vs plain loads / 2048 blocks (nt stores: +0.4 %)
+static int g_sc_var = 5, g_sc_cap = 4096;
+// non-temporal input loads: bit 0 bn_apply_fast (forward), bit 1 bn_apply_bwd
+static int g_ntld = 3;  // A/B (ResNet-50 b256): both on -1.5 % step time on top of the stats-combine policy
+
+static void grid2(long M, int C, int* blocks, int* rpb, int cap = 2048) {
   int cols = C / 8, RP = 256 / cols;
   long chunks = M * cols;
   long b = chunks / (256 * 8);
   if (b < 1) b = 1;
-  if (b > 2048) b = 2048;
+  if (b > cap) b = cap;
   long r = (M + b - 1) / b;
   r = (r + RP - 1) / RP * RP;
   *rpb = (int)r;
@@ -263,6 +291,9 @@ static void grid2(long M, int C, int* blocks, int* rpb) {
 
 }  // namespace dtm
 using namespace dtm;
+
+DTM_API void dtm_set_ntld_policy(int bits) { dtm::g_ntld = bits; }
+int dtm_ntld_bits() { return dtm::g_ntld; }
 
 static int shape_ok(long M, int C) {
   if (C % 8) return 0;
@@ -278,14 +309,14 @@ DTM_API int dtm_bn_apply_bwd(const void* dy, const void* y, const void* ymask, c
   int blocks, rpb;
   grid2(M, C, &blocks, &rpb);
   if (blocks <= dtm_reduce_direct_max()) {
-    hipLaunchKernelGGL(bn_apply_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
+    hipLaunchKernelGGL((g_ntld & 2) ? bn_apply_bwd_kernel<true> : bn_apply_bwd_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
                        (const bf16_t*)y, (const uint8_t*)ymask, (const bf16_t*)x, ss, (const bf16_t*)r, rss,
                        (bf16_t*)dx, (bf16_t*)dres, sx, sr, (int)M, C, mode, res_mode, unscaled, rpb, C, 1);
     return 0;
   }
   float* ws = dtm_ws_get((size_t)blocks * 4 * C);
   if (!ws) return -4;
-  hipLaunchKernelGGL(bn_apply_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
+  hipLaunchKernelGGL((g_ntld & 2) ? bn_apply_bwd_kernel<true> : bn_apply_bwd_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
                      (const bf16_t*)y, (const uint8_t*)ymask, (const bf16_t*)x, ss, (const bf16_t*)r, rss, (bf16_t*)dx,
                      (bf16_t*)dres, ws, nullptr, (int)M, C, mode, res_mode, unscaled, rpb, C, 0);
   dtm_reduce_rows(ws, blocks, 2 * C, 4 * C, sx, (hipStream_t)stream);
@@ -303,7 +334,7 @@ DTM_API int dtm_bn_apply_bwd_ld(const void* dy, const void* ymask, const void* x
   const int direct = blocks <= dtm_reduce_direct_max();
   float* ws = direct ? sx : dtm_ws_get((size_t)blocks * 4 * C);
   if (!ws) return -4;
-  hipLaunchKernelGGL(bn_apply_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
+  hipLaunchKernelGGL((g_ntld & 2) ? bn_apply_bwd_kernel<true> : bn_apply_bwd_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
                      (const bf16_t*)nullptr, (const uint8_t*)ymask, (const bf16_t*)x, ss, (const bf16_t*)nullptr,
                      (const float*)nullptr, (bf16_t*)dx, (bf16_t*)nullptr, ws, nullptr, (int)M, C, 3, 0, unscaled & 1,
                      rpb, lddy, direct);
@@ -332,8 +363,27 @@ DTM_API int dtm_stats_combine_fin(const void* dy, const void* x, const float* ds
                                   void* stream) {
   if (!shape_ok(M, C) || C > 2048) return -1;
   int blocks, rpb;
-  grid2(M, C, &blocks, &rpb);
-  hipLaunchKernelGGL(stats_combine_fin_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
-                     (const bf16_t*)x, dss, ss, gamma, count, dgamma, dbeta, (bf16_t*)out, (int)M, C, prescale, rpb);
+  grid2(M, C, &blocks, &rpb, g_sc_cap);
+#define SCF_LAUNCH(U, NT, NTS)                                                                                    \
+  hipLaunchKernelGGL((stats_combine_fin_kernel<U, NT, NTS>), dim3(blocks), dim3(256), 0, (hipStream_t)stream,          \
+                     (const bf16_t*)dy, (const bf16_t*)x, dss, ss, gamma, count, dgamma, dbeta, (bf16_t*)out, (int)M, \
+                     C, prescale, rpb)
+  switch (g_sc_var) {
+    case 1: SCF_LAUNCH(8, false, false); break;
+    case 2: SCF_LAUNCH(4, true, true); break;
+    case 3: SCF_LAUNCH(8, true, true); break;
+    case 4: SCF_LAUNCH(2, false, false); break;
+    case 5: SCF_LAUNCH(4, true, false); break;
+    case 6: SCF_LAUNCH(4, false, true); break;
+    default: SCF_LAUNCH(4, false, false); break;
+  }
+#undef SCF_LAUNCH
   return 0;
+}
+
+// A/B policy of the stats-combine stream: variant (0 U4, 1 U8, 2 U4 nt, 3 U8 nt, 4 U2, 5 U4 nt loads,
+// 6 U4 nt stores) and block cap
+DTM_API void dtm_set_sc_policy(int variant, int cap) {
+  g_sc_var = variant;
+  g_sc_cap = cap > 0 ? cap : 2048;
 }

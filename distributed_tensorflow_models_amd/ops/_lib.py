@@ -79,6 +79,8 @@ _SIGS = {
     "dtm_set_reduce_policy": (None, [_I, _I, _I]),
     "dtm_bn_apply_ld": (_I, [_P, _P, _P, _P, _L, _I, _I, _I, _P]),
     "dtm_bn_apply_bwd_ld": (_I, [_P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _P]),
+    "dtm_set_sc_policy": (None, [_I, _I]),
+    "dtm_set_ntld_policy": (None, [_I]),
     "dtm_dropout": (_I, [_P, _P, _L, _I, _F, ctypes.c_ulonglong, _P, _P]),
     "dtm_in_top_k": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
 }
