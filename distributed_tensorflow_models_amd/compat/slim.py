@@ -44,6 +44,7 @@ class VariableStore:
         self.name_counts = [{}]
         self.arg_stack = [{}]
         self.training = True
+        self.quant = None  # compat.quantize.QuantConfig: fake-quant training/eval graph
 
     def reset(self):
         self.__init__()
@@ -336,6 +337,25 @@ class VariableDeviceChooser:
 # layers
 
 
+def _qvar(name, init):
+    """State variable of a fake quantiser inside the current layer scope (checkpointed)."""
+    return variable(name, (), initializer=("constant", float(init)), trainable=False, buffer=True)
+
+
+def _qw(w):
+    if _store.quant is None:
+        return w
+    from . import quantize as Q
+    return Q.quantize_weights(w, _qvar, _store.quant)
+
+
+def _qa(y):
+    if _store.quant is None:
+        return y
+    from . import quantize as Q
+    return Q.quantize_activations(as_tensor(y), _qvar, _store.quant, _store.training)
+
+
 def _act(x, fn):
     if fn is None:
         return x
@@ -429,11 +449,12 @@ def conv2d(inputs, num_outputs, kernel_size, stride=1, padding="SAME", data_form
             b = variable("biases", (num_outputs,), initializer=biases_initializer, regularizer=biases_regularizer,
                          trainable=trainable)
         fuse = normalizer_fn is None and activation_fn in (torch.relu, E.relu, "relu")
-        y = F.conv2d(x, w, b, stride, padding, relu=fuse, dilation=rate)
+        y = F.conv2d(x, _qw(w), b, stride, padding, relu=fuse, dilation=rate)
         if normalizer_fn is not None:
             y = normalizer_fn(y, activation_fn=activation_fn, **(normalizer_params or {}))
-            return y
-    return y if fuse else _act(y, activation_fn)
+        elif not fuse:
+            y = _act(y, activation_fn)
+        return _qa(y)
 
 
 convolution2d = conv2d
@@ -478,19 +499,24 @@ def separable_conv2d(inputs, num_outputs, kernel_size, depth_multiplier=1, strid
     with variable_scope(scope, "SeparableConv2d", reuse=reuse):
         dw = variable("depthwise_weights", (kh, kw, cin, depth_multiplier), initializer=weights_initializer,
                       regularizer=weights_regularizer, trainable=trainable)
-        y = depthwise_conv2d(x, dw, stride, padding, rate)
+        if _store.quant is not None:
+            with variable_scope("depthwise_weights_q"):
+                dwq = _qw(dw)
+        else:
+            dwq = dw
+        y = depthwise_conv2d(x, dwq, stride, padding, rate)
         if num_outputs is not None:
             pw = variable("pointwise_weights", (num_outputs, 1, 1, cin * depth_multiplier),
                           initializer=weights_initializer, regularizer=weights_regularizer, trainable=trainable,
                           tf_layout="KRSC->HWIO")
-            y = F.conv2d(y, pw, None, 1, "SAME")
+            y = F.conv2d(y, _qw(pw), None, 1, "SAME")
         nout = y.shape[-1]
         if normalizer_fn is not None:
-            return normalizer_fn(y, activation_fn=activation_fn, **(normalizer_params or {}))
+            return _qa(normalizer_fn(y, activation_fn=activation_fn, **(normalizer_params or {})))
         if biases_initializer is not None:
             b = variable("biases", (nout,), initializer=biases_initializer, trainable=trainable)
             y = y + b.to(y.dtype)
-    return _act(y, activation_fn)
+        return _qa(_act(y, activation_fn))
 
 
 @add_arg_scope
@@ -508,12 +534,12 @@ def fully_connected(inputs, num_outputs, activation_fn=torch.relu, normalizer_fn
             b = variable("biases", (num_outputs,), initializer=biases_initializer, regularizer=biases_regularizer,
                          trainable=trainable)
         fuse = normalizer_fn is None and activation_fn in (torch.relu, E.relu, "relu")
-        y = F.linear(x, w, b, relu=fuse)
+        y = F.linear(x, _qw(w), b, relu=fuse)
         if normalizer_fn is not None:
             y = normalizer_fn(y.reshape(y.shape[0], 1, 1, -1), activation_fn=activation_fn,
                               **(normalizer_params or {}))
-            return as_tensor(y).reshape(x.shape[0], -1)
-    return y if fuse else _act(y, activation_fn)
+            return _qa(as_tensor(y).reshape(x.shape[0], -1))
+        return _qa(y if fuse else _act(y, activation_fn))
 
 
 fc = fully_connected

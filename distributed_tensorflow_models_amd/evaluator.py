@@ -113,6 +113,9 @@ def evaluate(preset, flags):
     kw = {"resnet_size": F.resnet_size} if cfg["model"] == "cifar10_resnet_v2" else {}
     if cfg["model"].startswith("mobilenet") and "depth_multiplier" in F and F.depth_multiplier != 1.0:
         kw["depth_multiplier"] = F.depth_multiplier
+    if "quantize" in F and F.quantize:  # create_eval_graph (mobilenet_v1_eval.py:126-127)
+        from .compat.quantize import QuantConfig
+        kw["quantize"] = QuantConfig(is_training=False)
     model = trainer.build_model_for_eval(preset, **kw).to(device)
     model.eval()
     if os.path.isdir(F.eval_dir):

@@ -211,6 +211,11 @@ def train(preset, flags, default_mode="bsp"):
         mkw["resnet_size"] = FLAGS.resnet_size
     if cfg["model"].startswith("mobilenet") and FLAGS.depth_multiplier != 1.0:
         mkw["depth_multiplier"] = FLAGS.depth_multiplier
+    if "quantize" in FLAGS and FLAGS.quantize:
+        # tf.contrib.quantize.create_training_graph(quant_delay=get_quant_delay())
+        # (reference vgg/nets/mobilenet_v1_train.py:66-73,138-139): quantise at once when fine-tuning
+        from .compat.quantize import QuantConfig
+        mkw["quantize"] = QuantConfig(quant_delay=0 if FLAGS.fine_tune_checkpoint else FLAGS.quant_delay)
     model = nets_factory.build(cfg["model"], num_classes=cfg["num_classes"], **mkw).to(device)
     if cfg.get("wd_all") is not None:  # loss += wd * sum(l2_loss(v) for v in trainable_variables())
         for p in model.parameters():

@@ -6,6 +6,7 @@ from .. import evaluator
 evaluator.define_eval_flags(flags, "mobilenet_v1")
 flags.DEFINE_float("depth_multiplier", 1.0, "Depth multiplier for mobilenet")
 flags.DEFINE_string("dataset_dir", "", "Location of dataset (alias of --data_dir)")
+flags.DEFINE_boolean("quantize", False, "Quantize training (evaluate the fake-quantised graph)")
 
 
 def main(_argv=None):

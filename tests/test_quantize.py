@@ -1,0 +1,105 @@
+"""Fake-quantised training (tf.contrib.quantize behind mobilenet_v1_train.py --quantize):
+quantiser numerics, delayed start, checkpointed range variables, eval graph, entry scripts."""
+import os
+
+import torch
+
+from distributed_tensorflow_models_amd.compat import quantize as Q
+from distributed_tensorflow_models_amd.models import nets_factory
+
+
+def test_fake_quant_grid_zero_exact_and_ste():
+    x = torch.linspace(-1.3, 2.7, 1001, requires_grad=True)
+    y = Q.fake_quant(x, torch.tensor(-1.0), torch.tensor(2.0), 8)
+    scale = 3.0 / 255
+    k = (y.detach() / scale)
+    # nudged zero point: 0.0 is a grid point and every output is an integer multiple of the scale
+    assert torch.allclose(k, k.round(), atol=1e-3)
+    assert float(Q.fake_quant(torch.zeros(3), torch.tensor(-1.0), torch.tensor(2.0))[0]) == 0.0
+    assert y.detach().min() >= -1.0 - 1e-6 and y.detach().max() <= 2.0 + scale
+    y.sum().backward()
+    inside = (x.detach() >= -1.0) & (x.detach() <= 2.0)
+    outside = (x.detach() < -1.0 - scale) | (x.detach() > 2.0 + scale)  # half-step rounding band aside
+    assert torch.all(x.grad[inside] == 1) and torch.all(x.grad[outside] == 0)  # straight-through
+    # narrow range (weights): 254 steps, the lowest code unused
+    w = Q.fake_quant(torch.tensor([-1.0, 1.0]), torch.tensor(-1.0), torch.tensor(1.0), 8, narrow=True)
+    torch.testing.assert_close(w, torch.tensor([-1.0, 1.0]))
+
+
+def _mobilenet(cfg):
+    torch.manual_seed(0)
+    return nets_factory.build("mobilenet_v1_025", num_classes=11, quantize=cfg)
+
+
+def test_mobilenet_quant_delay_ranges_and_eval_graph():
+    cfg = Q.QuantConfig(quant_delay=2)
+    net = _mobilenet(cfg)
+    ref = _mobilenet(None)
+    ref.load_state_dict({k: v for k, v in net.state_dict().items() if k in ref.state_dict()})
+    names = set(net.store.vars)
+    assert any(n.endswith("act_quant/min") for n in names) and any(n.endswith("weights_quant/max") for n in names)
+    assert not any("quant" in n for n in ref.store.vars)
+    from distributed_tensorflow_models_amd.ops import elementwise as E
+    x = torch.randn(2, 64, 64, 3)
+    with torch.no_grad():
+        E._seed[0] = 7  # same dropout masks for both models
+        a = net(x, training=True)
+        E._seed[0] = 7
+        b = ref(x, training=True)
+    torch.testing.assert_close(a, b)            # step 0 < quant_delay: identity quantisers
+    amax = [v for n, v in net.store.vars.items() if n.endswith("act_quant/max")][0]
+    assert float(amax) != 6.0                   # ...but the activation ranges are tracked
+    with torch.no_grad():
+        net(x, training=True)
+        E._seed[0] = 9
+        c = net(x, training=True)               # step 2: quantised
+        E._seed[0] = 9
+        d = ref(x, training=True)
+    assert not torch.allclose(c, d)
+    # gradients flow through the straight-through quantisers to the fp32 masters
+    out = net(x, training=True)
+    out.float().square().mean().backward()
+    w = [v for n, v in net.store.vars.items() if n.endswith("Conv2d_0/weights")][0]
+    assert w.grad is not None and float(w.grad.abs().sum()) > 0
+    # eval graph: stored ranges, no update
+    Q.create_eval_graph(net)
+    before = float(amax)
+    with torch.no_grad():
+        net(x, training=False)
+    assert float(amax) == before
+
+
+def test_mobilenet_train_quantize_entry_and_checkpoint(tmp_path):
+    from distributed_tensorflow_models_amd.ckpt.bundle import BundleReader
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    d = str(tmp_path / "train")
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, "-m", "distributed_tensorflow_models_amd.trainers.mobilenet_v1_train",
+                        "--quantize", "--quant_delay=1", "--max_steps=2", "--batch_size=2", "--train_dir=" + d,
+                        "--data_dir=/nonexistent", "--synthetic_data", "--depth_multiplier=0.25"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, (p.stdout + p.stderr)[-3000:]
+    names = set(BundleReader(os.path.join(d, "model.ckpt-2")).names())
+    assert any(n.endswith("act_quant/min") for n in names)
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_mobilenet_quantized_train_step_gpu():
+    """Fake-quant MobileNet through the engine on the GPU (HIP depthwise/pointwise kernels under
+    the quantisers; torch fake-quant ops with device-side ranges, no host sync)."""
+    from distributed_tensorflow_models_amd.engine import TrainStep
+    dev = torch.device("cuda", 0)
+    cfg = Q.QuantConfig(quant_delay=1)
+    net = _mobilenet(cfg).to(dev)
+    step = TrainStep(net, optimizer="momentum", lr=0.01, momentum=0.9)
+    x = torch.randn(4, 96, 96, 3, device=dev).to(torch.bfloat16)
+    y = torch.randint(0, 11, (4,), device=dev)
+    losses = [float(step(x, y)) for _ in range(3)]
+    step.dp.close()
+    assert cfg.step == 3 and all(l == l and abs(l) < 1e3 for l in losses)
