@@ -189,21 +189,24 @@ def test_zero_copy_concat_exact(Cs):
 
 def test_inception_zero_copy_concat_matches_torch_cat(monkeypatch):
     """Old-slim Inception-v3 with branch outputs BN-applied straight into their concat slices (and
-    their gradients read in place) vs the same model through torch.cat of materialised branches."""
+    their gradients read in place) vs the same model through torch.cat of materialised branches.
+    Inference-mode BN (moving statistics) keeps the comparison deterministic: in training mode the
+    fp32-atomic batch statistics differ in the last bit between any two runs with different
+    allocation histories (even torch.cat vs torch.cat + clone), and a batch-2 BN network amplifies
+    that chaotically (tools/diag_concat.py); the training-mode concat itself is checked bit for bit
+    by test_zero_copy_concat_exact."""
     from distributed_tensorflow_models_amd.models import inception_v3_slim as iv3
-    from distributed_tensorflow_models_amd.ops import elementwise as E
     from distributed_tensorflow_models_amd.ops.lazy import as_tensor
 
     def run(zero_copy):
-        E._seed[0] = 1234  # same dropout masks in both runs
         if not zero_copy:
             monkeypatch.setattr(iv3, "concat_channels", lambda parts: torch.cat([as_tensor(p) for p in parts], -1))
         torch.manual_seed(0)
         net = nets_factory.build("inception_v3_slim_old", num_classes=11).to(DEV)
         g = torch.Generator().manual_seed(1)
         x = torch.randn(2, 299, 299, 3, generator=g).to(DEV, torch.bfloat16)
-        logits, aux = net(x, training=True)
-        (logits.float().square().mean() + 0.4 * aux.float().square().mean()).backward()
+        logits = net(x, training=False)
+        logits.float().square().mean().backward()
         torch.cuda.synchronize()
         monkeypatch.undo()
         grads = torch.cat([p.grad.float().reshape(-1) for p in net.parameters() if p.grad is not None])
@@ -211,9 +214,8 @@ def test_inception_zero_copy_concat_matches_torch_cat(monkeypatch):
 
     la, ga = run(True)
     lb, gb = run(False)
-    lc, gc = run(False)  # noise floor: the same path twice (BN statistics use fp32 atomics)
-    assert _rel(la, lb) < max(3 * _rel(lc, lb), 1e-2)
-    assert _rel(ga, gb) < max(3 * _rel(gc, gb), 2e-2)
+    assert torch.equal(la, lb)
+    assert _rel(ga, gb) < 1e-3
 
 
 @pytest.mark.parametrize("pool", ["avg", "max"])
