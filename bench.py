@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the step in a hipGraph (1/0); -1 = auto: on for launch-bound models on 1 GPU")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--dist-backend", default="", help="override the process-group backend (default: nccl = "
+                    "RCCL on GPUs, gloo on CPU); gloo on GPUs lets several ranks share one device for rehearsals")
     ap.add_argument("--device", default="cuda", choices=("cuda", "cpu"),
                     help="cpu: the plumbing config (LeNet over gloo, no GPU; BASELINE.json config 1)")
     args = ap.parse_args()
@@ -62,13 +64,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     cpu = args.device == "cpu"
+    ndev = 0 if cpu else max(torch.cuda.device_count(), 1)
+    gpu_index = local_rank % ndev if ndev else 0  # ranks > devices only in shared-GPU gloo rehearsals
     if world > 1:
-        if cpu:
+        backend = args.dist_backend or ("gloo" if cpu else "nccl")
+        if cpu or backend == "gloo":
+            if not cpu:
+                torch.cuda.set_device(gpu_index)
             dist.init_process_group("gloo")
         else:
             torch.cuda.set_device(local_rank)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cpu") if cpu else torch.device("cuda", local_rank)
+            dist.init_process_group(backend, device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cpu") if cpu else torch.device("cuda", gpu_index)
     sync = (lambda: None) if cpu else torch.cuda.synchronize
 
     from distributed_tensorflow_models_amd.engine import TrainStep
