@@ -86,9 +86,21 @@ DTM_API void dtm_set_reduce_policy(int target_blocks, int max_chunks, int direct
   g_red_maxy = max_chunks > 0 ? max_chunks : 1;
   g_red_direct = direct_max;
 }
-int dtm_reduce_direct_max() { return g_red_direct; }
+static int g_red_det = 0;
+int dtm_reduce_direct_max() { return g_red_det ? 0 : g_red_direct; }
+
+// Deterministic mode: one row chunk per column group, so every output column is summed by one
+// block in a fixed order (no fp32 atomics across blocks) - bit-reproducible BN statistics and
+// reductions regardless of scheduling / allocation history, at some latency on tall slabs.
+DTM_API void dtm_set_deterministic(int on) { g_red_det = on != 0; }
+DTM_API int dtm_get_deterministic() { return g_red_det; }
 
 void dtm_reduce_split(int rows, int xblocks, int* rpb, int* ychunks) {
+  if (g_red_det) {
+    *rpb = rows < 16 ? 16 : (rows + 15) / 16 * 16;
+    *ychunks = 1;
+    return;
+  }
   if (g_red_target <= 0) {
     *rpb = 256;
     *ychunks = (rows + 255) / 256;
@@ -113,7 +125,7 @@ void dtm_reduce_rows(const float* ws, int rows, int width, int ld, float* out, h
                        out, rpb);
     return;
   }
-  int chunks = rows >= 512 ? 32 : (rows >= 64 ? 8 : 1);
+  int chunks = g_red_det ? 1 : (rows >= 512 ? 32 : (rows >= 64 ? 8 : 1));
   hipLaunchKernelGGL(reduce_rows_kernel, dim3((width + 255) / 256, chunks), dim3(256), 0, st, ws, rows, width, ld, out,
                      chunks);
 }

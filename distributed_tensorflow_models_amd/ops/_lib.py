@@ -81,6 +81,8 @@ _SIGS = {
     "dtm_bn_apply_bwd_ld": (_I, [_P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _P]),
     "dtm_set_sc_policy": (None, [_I, _I]),
     "dtm_set_ntld_policy": (None, [_I]),
+    "dtm_set_deterministic": (None, [_I]),
+    "dtm_get_deterministic": (_I, []),
     "dtm_dropout": (_I, [_P, _P, _L, _I, _F, ctypes.c_ulonglong, _P, _P]),
     "dtm_in_top_k": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
 }
@@ -107,7 +109,16 @@ def lib():
             fn.restype = res
             fn.argtypes = args
         _lib = L
+        if os.environ.get("DTM_DETERMINISTIC", "0") not in ("", "0"):
+            L.dtm_set_deterministic(1)
     return _lib
+
+
+def set_deterministic(on=True):
+    """Bit-reproducible GPU reductions (BN statistics, BN-gradient sums, split-K wgrad): every
+    output column summed by one block in a fixed order instead of fp32 atomics across blocks.
+    Also enabled by DTM_DETERMINISTIC=1.  Costs a little latency on tall partial-sum slabs."""
+    lib().dtm_set_deterministic(int(bool(on)))
 
 
 def available():

@@ -123,6 +123,7 @@ def define_common_flags(flags, preset):
             ("bucket_mb", Fl, 32.0, "all-reduce bucket size (MB)"),
             ("use_hipgraph", B, False, "capture the BSP training step in a hipGraph (launch-bound models)"),
             ("grad_comm_dtype", S, "fp32", "gradient all-reduce dtype on the wire: fp32 | bf16"),
+            ("deterministic", B, False, "bit-reproducible GPU reductions (no cross-block fp32 atomics)"),
             ("trace_steps", S, "", "a:b -> export a Chrome trace of steps [a, b)"),
             ("fresh", B, False, "wipe train_dir before training (the reference always did)"),
             ("log_every", I, 1, "log the per-step line every N steps"),
@@ -204,6 +205,9 @@ def train(preset, flags, default_mode="bsp"):
     rank, world = pg.rank(), pg.world_size()
     device = _device()
     torch.manual_seed(FLAGS.seed + (rank if mode != "bsp" else 0))
+    if FLAGS.deterministic and device.type == "cuda":
+        from .ops import _lib
+        _lib.set_deterministic(True)
 
     # ---- model ---------------------------------------------------------------------------------
     mkw = dict(cfg.get("model_kw", {}))

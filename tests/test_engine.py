@@ -144,3 +144,23 @@ def test_bench_cpu_plumbing_json():
               "vs_baseline", "dtype", "data", "config"):
         assert k in r
     assert r["steps"] == 2 and r["n_gpus"] == 1 and r["value"] > 0 and r["config"]["model"] == "lenet"
+
+
+@pytest.mark.gpu
+def test_deterministic_mode_bit_reproducible_across_allocation_histories():
+    """DTM_DETERMINISTIC / ops._lib.set_deterministic: two ResNet training runs whose allocation
+    histories differ (a dummy allocation shifts every buffer) end bit-identical; BN statistics and
+    gradient sums are summed in a fixed order instead of cross-block fp32 atomics."""
+    from distributed_tensorflow_models_amd.ops import _lib
+    _lib.set_deterministic(True)
+    try:
+        outs = []
+        for pad in (0, 3 << 20):
+            junk = torch.empty(pad + 1, device="cuda", dtype=torch.uint8)
+            losses, params, _, st = _run_steps("resnet_v1_50", False, 3, 64, 16)
+            outs.append((losses, params))
+            del junk
+        assert outs[0][0] == outs[1][0]
+        assert torch.equal(outs[0][1], outs[1][1])
+    finally:
+        _lib.set_deterministic(False)
