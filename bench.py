@@ -85,12 +85,16 @@ def main():
         # measured on one MI355X: LeNet 396k -> 875k img/s with the captured step; ResNet-50 and
         # VGG-16 are GPU-bound (same ms/step either way), so they stay eager
         args.graph = int(args.model == "lenet" and world == 1 and not cpu)
-    torch.manual_seed(1234 + rank)
+    torch.manual_seed(1234)  # identical replicas: every rank builds the same initial weights
     S0, ncls, B0, opt, extra = PRESETS[args.model]
     S = args.image_size or S0
     B = args.batch or B0
     kw = {"fc_conv_padding": "SAME"} if args.model == "vgg_16" else {}
     net = nets_factory.build(args.model, num_classes=ncls, **kw).to(dev)
+    if world > 1:  # and make it explicit (the reference's chief-initialises-then-workers-wait contract)
+        from distributed_tensorflow_models_amd.parallel import process_group as pg
+        pg.broadcast_tensors(list(net.parameters()) + list(net.buffers()))
+    torch.manual_seed(1234 + rank)  # each rank its own synthetic batch
     step = TrainStep(net, optimizer=opt, lr=0.1 * world if opt == "momentum" else 0.01 * world, momentum=0.9,
                      bucket_mb=args.bucket_mb, use_graph=bool(args.graph),
                      grad_comm_dtype=torch.bfloat16 if args.grad_comm == "bf16" else None, **extra)

@@ -1494,6 +1494,8 @@ struct TileCfg {
   int id, PT, NWP;
 };
 static int g_tile_env = -2;
+static int g_k64_tile = 3;  // tile of the 64-output-channel layers (A/B knob: dtm_conv_set_k64_tile)
+DTM_API void dtm_conv_set_k64_tile(int id) { g_k64_tile = id; }
 static TileCfg pick_tile(const ConvNTArgs& a) {
   if (g_tile_env == -2) {
     const char* e = getenv("DTM_CONV_TILE");
@@ -1510,7 +1512,7 @@ static TileCfg pick_tile(const ConvNTArgs& a) {
   // (the persistent streaming 1x1 kernel: the 64-deep 56x56 expand / reduce layers and their dgrads are
   // HBM streams: -20..-33 % (tools/conv_tile_sweep.py); at Kg 128 its 1 block/CU loses)
   if (id == -1 && !a.in_scale && a.Kg >= 1024) id = 21;  // (-3: the policy without it, for A/B runs)
-  if (id < 0) id = a.K <= 64 ? 3 : ((a.M <= 16384 && a.Kg >= 2048) ? 0 : 4);
+  if (id < 0) id = a.K <= 64 ? g_k64_tile : ((a.M <= 16384 && a.Kg >= 2048) ? 0 : 4);
   // LDS-DMA variants (10-12, opt-in) need an operand without the prologue affine
   if (id >= 10 && id < 20 && a.in_scale) id = a.K <= 64 ? 3 : 4;
   // pipelined LDS-DMA variants (20-23) stage the prologue affine in LDS: C <= 512

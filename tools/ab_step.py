@@ -29,6 +29,7 @@ def apply(cfg):
     L.dtm_set_reduce_policy(int(red[0]), int(red[1]), int(red[2]) if len(red) > 2 else 0)
     L.dtm_set_ntld_policy(int(cfg.get("ntld", "3")))
     L.dtm_set_deterministic(int(cfg.get("det", "0")))
+    L.dtm_conv_set_k64_tile(int(cfg.get("k64", "3")))
     sc = cfg.get("sc", "5:4096").split(":")
     L.dtm_set_sc_policy(int(sc[0]), int(sc[1]))
     os.environ["DTM_PROLOGUE"] = cfg.get("prologue", "auto")
