@@ -11,6 +11,8 @@ data-parallel engine can launch a bucket's all-reduce while backward continues.
 """
 import ctypes
 
+import os
+
 import torch
 
 from . import _lib
@@ -146,7 +148,12 @@ class _Conv2dFn(torch.autograd.Function):
         x, w, y = ctx.saved_tensors
         g = ctx.geom
         dy = dy.contiguous()
-        if ctx.relu:
+        gb = None
+        if ctx.relu and _relu_bias_bwd_ok(dy):
+            # one pass: ReLU mask from y and the bias-gradient column sums (the BN-apply backward
+            # kernel with unit scale), instead of compare + where + cast + reduce torch ops
+            dy, gb = _relu_bias_bwd(dy, y)
+        elif ctx.relu:
             dy = torch.where(y > 0, dy, torch.zeros((), dtype=dy.dtype, device=dy.device))
         d = g.as_desc(_lib.ConvDesc)
         s = _lib.stream_ptr()
@@ -167,9 +174,35 @@ class _Conv2dFn(torch.autograd.Function):
                 dw = target
         db = None
         if ctx.has_b and ctx.needs_input_grad[2]:
-            gb = dy.reshape(-1, g.K).float().sum(0)
+            if gb is None:
+                gb = dy.reshape(-1, g.K).float().sum(0)
             db = _accum_param_grad(ctx.bias_param, gb)
         return dx, dw, db, None, None
+
+
+_UNIT_SS = {}
+_RELU_BIAS_FUSE = os.environ.get("DTM_RELU_BIAS_FUSE", "1") != "0"  # A/B knob (tools/ab_step.py)
+
+
+def _relu_bias_bwd_ok(dy):
+    K = dy.shape[-1]
+    return _RELU_BIAS_FUSE and dy.dtype == torch.bfloat16 and K % 8 == 0 and K // 8 <= 256 and dy.numel() // K < (1 << 31)
+
+
+def _relu_bias_bwd(dy, y):
+    """g = dy * [y > 0] and sum_rows(g) (fp32) in one HIP pass (dtm_bn_apply_bwd, mode 1, unscaled)."""
+    L = _lib.lib()
+    K = dy.shape[-1]
+    M = dy.numel() // K
+    key = (dy.device, K)
+    ss = _UNIT_SS.get(key)
+    if ss is None:
+        ss = _UNIT_SS[key] = torch.ones((4, K), device=dy.device, dtype=torch.float32)
+    g = torch.empty_like(dy)
+    sums = torch.zeros((4, K), device=dy.device, dtype=torch.float32)
+    _check(L.dtm_bn_apply_bwd(_lib.ptr(dy), _lib.ptr(y), None, _lib.ptr(y), _lib.ptr(ss), None, None, _lib.ptr(g),
+                              None, _lib.ptr(sums), None, M, K, 1, 0, 1, _lib.stream_ptr()), "relu_bias_bwd")
+    return g, sums[1]
 
 
 def conv2d(x, w, bias=None, stride=1, padding="SAME", relu=False, dilation=1):

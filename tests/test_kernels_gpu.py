@@ -345,3 +345,27 @@ def test_conv_dead_taps_cropped(H, R, K, C, use_main_grad):
     c = R // 2
     if H == 1:
         assert float(dw.abs().sum() - dw[:, c, c].abs().sum()) == 0.0  # only the centre tap is live
+
+
+@pytest.mark.parametrize("K,H", [(64, 16), (200, 7), (512, 2)])
+def test_conv_relu_bias_backward_fused(K, H):
+    """conv + bias + ReLU backward: mask and bias-gradient sums from one HIP pass, vs fp32 torch.
+
+    The fp32 reference back-propagates through the GPU's own ReLU mask (y > 0 of the bf16 output):
+    elements within bf16 rounding of zero would otherwise flip and dominate the bias-sum error."""
+    torch.manual_seed(0)
+    x = torch.randn(8, H, H, 32).bfloat16().float()
+    w = torch.randn(K, 3, 3, 32) * 0.1
+    b = torch.randn(K) * 0.1
+    dy = torch.randn(8, H, H, K).bfloat16().float()
+    xg = x.to(DEV, torch.bfloat16).requires_grad_()
+    wg = torch.nn.Parameter(w.to(DEV))
+    bg = torch.nn.Parameter(b.to(DEV))
+    y = dnn.conv2d(xg, wg, bg, 1, "SAME", relu=True)
+    y.backward(dy.to(DEV, torch.bfloat16))
+    mask = (y.detach().float().cpu() > 0).float()
+    xr, wr, br = (t.clone().requires_grad_() for t in (x, w, b))
+    ref.conv2d(xr, wr, br, 1, "SAME", False, 1).backward(dy * mask)
+    assert _rel(bg.grad.cpu(), br.grad) < 5e-3
+    assert _rel(wg.grad.cpu(), wr.grad) < 2e-2
+    assert _rel(xg.grad.float().cpu(), xr.grad) < 2e-2
