@@ -204,6 +204,7 @@ def train(preset, flags, default_mode="bsp"):
         pg.init()
     rank, world = pg.rank(), pg.world_size()
     device = _device()
+    logging.info("replica %d of world %d (%s, %s)", rank, world, mode, device)
     torch.manual_seed(FLAGS.seed + (rank if mode != "bsp" else 0))
     if FLAGS.deterministic and device.type == "cuda":
         from .ops import _lib
