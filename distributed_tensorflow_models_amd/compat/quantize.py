@@ -16,15 +16,22 @@ registered and checkpointed like every other variable):
   still tracked), exactly the reference's delayed start;
 * gradients use the straight-through estimator, zero outside the clamp range.
 
-Deviation (documented): TF additionally folds BatchNorm into the preceding conv weights in the
-quantised training graph; here BN stays a separate fused op and only weights and activations are
-quantised.  Quantisation runs in fp32 torch ops (the model is small; not a hot path).
+* BatchNorm after a conv2d / separable_conv2d is folded into that conv's weights, as TF's
+  ``fold_batch_norms`` does (``compat/slim.py::_folded_bn``): in training the plain conv gives the
+  batch moments (moving averages updated from them) and the layer computes
+  ``conv(x, Q(w * gamma/sqrt(var+eps))) + beta - mean * gamma/sqrt(var+eps)``; in evaluation the
+  moving moments replace the batch ones.  ``QuantConfig(fold_bn=False)`` keeps BN a separate op.
+
+Deviation (documented): TF's optional ``freeze_bn_delay`` (switch to moving moments with the
+correction factors after N steps) is not implemented -- the reference's scripts never set it.
+Quantisation runs in fp32 torch ops (the model is small; not a hot path).
 """
 import torch
 
 
 class QuantConfig:
-    def __init__(self, quant_delay=0, num_bits=8, ema_decay=0.999, is_training=True):
+    def __init__(self, quant_delay=0, num_bits=8, ema_decay=0.999, is_training=True, fold_bn=True):
+        self.fold_bn = bool(fold_bn)  # fold slim.batch_norm into the producing conv's weights (TF default)
         self.quant_delay = int(quant_delay or 0)
         self.num_bits = int(num_bits)
         self.ema_decay = float(ema_decay)

@@ -376,10 +376,13 @@ def _pair(v):
 def batch_norm(inputs, decay=0.999, center=True, scale=False, epsilon=0.001, activation_fn=None,
                is_training=None, trainable=True, scope=None, reuse=None, updates_collections=None,
                param_initializers=None, fused=None, outputs_collections=None, bessel=None, data_format=None,
-               zero_debias_moving_mean=False):
+               zero_debias_moving_mean=False, _fold=None):
+    """slim batch_norm.  ``_fold`` (internal, set by conv2d / separable_conv2d under a fake-quant
+    config with ``fold_bn``): (conv_fn, weights, scale_fn) -- BatchNorm is folded into the producing
+    conv's weights instead of normalising ``inputs`` (``inputs`` is then the number of channels)."""
     is_training = _store.training if is_training is None else is_training
-    x = as_tensor(inputs)
-    C = x.shape[-1]
+    x = None if _fold is not None else as_tensor(inputs)
+    C = inputs if _fold is not None else x.shape[-1]
     pi = param_initializers or {}
     with variable_scope(scope, "BatchNorm", reuse=reuse):
         beta = variable("beta", (C,), initializer=pi.get("beta", ("constant", 0.0)), trainable=trainable) \
@@ -390,10 +393,55 @@ def batch_norm(inputs, decay=0.999, center=True, scale=False, epsilon=0.001, act
                       collections=[GraphKeys.MOVING_AVERAGE_VARIABLES])
         mv = variable("moving_variance", (C,), initializer=("constant", 1.0), trainable=False, buffer=True,
                       collections=[GraphKeys.MOVING_AVERAGE_VARIABLES])
+    if _fold is not None:  # outside the BatchNorm scope: the weight quantiser lives in the conv's scope
+        return _folded_bn(_fold, gamma, beta, mm, mv, is_training, decay, epsilon, activation_fn,
+                          True if bessel is None else bessel)
     relu_fused = activation_fn in (torch.relu, E.relu, "relu")
     y = F.batch_norm(x, gamma, beta, mm.data, mv.data, is_training, decay, epsilon, relu_fused, None,
                      True if bessel is None else bessel)
     return y if relu_fused else _act(y, activation_fn)
+
+
+def _folded_bn(fold, gamma, beta, mm, mv, is_training, decay, epsilon, activation_fn, bessel):
+    """tf.contrib.quantize fold_batch_norms (training graph without BN freeze, eval graph):
+    training: the plain conv y0 = conv(x, w) gives the batch moments (gradients flow through them, as
+    TF keeps that conv), the moving averages are updated from them, and the output is
+    conv(x, Q(w * m)) + (beta - mean * m) with m = gamma / sqrt(var + eps) -- exactly BN(y0) when
+    quantisation is off; eval: the same with the moving mean / variance."""
+    conv_fn, w, scale_fn = fold[:3]
+    qscope = fold[3] if len(fold) > 3 else None
+    if is_training:
+        y0 = as_tensor(conv_fn(w)).float()
+        dims = tuple(range(y0.dim() - 1))
+        mean = y0.mean(dims)
+        var = y0.var(dims, unbiased=False)
+        with torch.no_grad():
+            n = y0.numel() // y0.shape[-1]
+            uv = var * (n / max(n - 1, 1)) if bessel else var
+            mm.data.sub_((mm.data - mean.detach()) * (1.0 - decay))
+            mv.data.sub_((mv.data - uv.detach()) * (1.0 - decay))
+    else:
+        mean, var = mm.detach(), mv.detach()
+    mult = torch.rsqrt(var + epsilon)
+    if gamma is not None:
+        mult = mult * gamma
+    bias = -mean * mult
+    if beta is not None:
+        bias = bias + beta
+    wf = scale_fn(w, mult)
+    if qscope:
+        with variable_scope(qscope):
+            wq = _qw(wf)
+    else:
+        wq = _qw(wf)
+    y = as_tensor(conv_fn(wq))
+    y = (y.float() + bias).to(y.dtype)
+    return _act(y, activation_fn)
+
+
+def _fold_ok(normalizer_fn):
+    q = _store.quant
+    return q is not None and getattr(q, "fold_bn", False) and normalizer_fn is batch_norm
 
 
 @add_arg_scope
@@ -448,6 +496,11 @@ def conv2d(inputs, num_outputs, kernel_size, stride=1, padding="SAME", data_form
         if normalizer_fn is None and biases_initializer is not None:
             b = variable("biases", (num_outputs,), initializer=biases_initializer, regularizer=biases_regularizer,
                          trainable=trainable)
+        if normalizer_fn is not None and _fold_ok(normalizer_fn):
+            fold = (lambda wt: F.conv2d(x, wt, None, stride, padding, dilation=rate), w,
+                    lambda wt, m: wt * m.reshape(-1, 1, 1, 1))
+            return _qa(normalizer_fn(num_outputs, activation_fn=activation_fn, _fold=fold,
+                                     **(normalizer_params or {})))
         fuse = normalizer_fn is None and activation_fn in (torch.relu, E.relu, "relu")
         y = F.conv2d(x, _qw(w), b, stride, padding, relu=fuse, dilation=rate)
         if normalizer_fn is not None:
@@ -499,12 +552,25 @@ def separable_conv2d(inputs, num_outputs, kernel_size, depth_multiplier=1, strid
     with variable_scope(scope, "SeparableConv2d", reuse=reuse):
         dw = variable("depthwise_weights", (kh, kw, cin, depth_multiplier), initializer=weights_initializer,
                       regularizer=weights_regularizer, trainable=trainable)
+        if num_outputs is None and normalizer_fn is not None and _fold_ok(normalizer_fn):
+            # depthwise-only layer (MobileNet v1): BN folded into the depthwise weights per channel
+            fold = (lambda wt: depthwise_conv2d(x, wt, stride, padding, rate), dw,
+                    lambda wt, m: wt * m.reshape(1, 1, cin, depth_multiplier), "depthwise_weights_q")
+            return _qa(normalizer_fn(cin * depth_multiplier, activation_fn=activation_fn, _fold=fold,
+                                     **(normalizer_params or {})))
         if _store.quant is not None:
             with variable_scope("depthwise_weights_q"):
                 dwq = _qw(dw)
         else:
             dwq = dw
         y = depthwise_conv2d(x, dwq, stride, padding, rate)
+        if num_outputs is not None and normalizer_fn is not None and _fold_ok(normalizer_fn):
+            pw = variable("pointwise_weights", (num_outputs, 1, 1, cin * depth_multiplier),
+                          initializer=weights_initializer, regularizer=weights_regularizer, trainable=trainable,
+                          tf_layout="KRSC->HWIO")
+            fold = (lambda wt: F.conv2d(y, wt, None, 1, "SAME"), pw, lambda wt, m: wt * m.reshape(-1, 1, 1, 1))
+            return _qa(normalizer_fn(num_outputs, activation_fn=activation_fn, _fold=fold,
+                                     **(normalizer_params or {})))
         if num_outputs is not None:
             pw = variable("pointwise_weights", (num_outputs, 1, 1, cin * depth_multiplier),
                           initializer=weights_initializer, regularizer=weights_regularizer, trainable=trainable,
