@@ -659,9 +659,10 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, w, b, relu):
         w16 = weight_bf16(w)
         x16 = x.to(torch.bfloat16)
-        y = x16 @ w16  # w stored TF-style [in, out]
-        if b is not None:
-            y = y + b.to(torch.bfloat16)
+        if b is not None:  # bias in the GEMM epilogue (w stored TF-style [in, out])
+            y = torch.addmm(b.to(torch.bfloat16), x16, w16)
+        else:
+            y = x16 @ w16
         if relu:
             y = torch.relu(y)
         ctx.save_for_backward(x16, w, y if relu else None)
@@ -671,7 +672,11 @@ class _LinearFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x16, w, y = ctx.saved_tensors
-        if ctx.relu:
+        gb = None
+        dy = dy.contiguous()
+        if ctx.relu and ctx.b is not None and _relu_bias_bwd_ok(dy):
+            dy, gb = _relu_bias_bwd(dy, y)  # mask + bias-gradient sums in one HIP pass
+        elif ctx.relu:
             dy = torch.where(y > 0, dy, torch.zeros((), dtype=dy.dtype, device=dy.device))
         dy16 = dy.to(torch.bfloat16)
         dx = dy16 @ weight_bf16(w).t() if ctx.needs_input_grad[0] else None
@@ -681,7 +686,7 @@ class _LinearFn(torch.autograd.Function):
             dw = _accum_param_grad(w, gw)
         db = None
         if ctx.b is not None and ctx.needs_input_grad[2]:
-            db = _accum_param_grad(ctx.b, dy16.float().sum(0))
+            db = _accum_param_grad(ctx.b, gb if gb is not None else dy16.float().sum(0))
         return dx, dw, db, None
 
 

@@ -369,3 +369,27 @@ def test_conv_relu_bias_backward_fused(K, H):
     assert _rel(bg.grad.cpu(), br.grad) < 5e-3
     assert _rel(wg.grad.cpu(), wr.grad) < 2e-2
     assert _rel(xg.grad.float().cpu(), xr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("B,N,relu", [(64, 384, True), (37, 192, True), (16, 1000, False), (8, 24, True)])
+def test_linear_bias_relu_fused(B, N, relu):
+    """FC layer: bias in the GEMM epilogue, ReLU mask + bias sums in one HIP pass, vs fp32 torch
+    through the GPU's own ReLU mask."""
+    torch.manual_seed(0)
+    x = torch.randn(B, 96).bfloat16().float()
+    w = torch.randn(96, N) * 0.1
+    b = torch.randn(N) * 0.1
+    dy = torch.randn(B, N).bfloat16().float()
+    xg = x.to(DEV, torch.bfloat16).requires_grad_()
+    wg = torch.nn.Parameter(w.to(DEV))
+    bg = torch.nn.Parameter(b.to(DEV))
+    y = dnn.linear(xg, wg, bg, relu=relu)
+    y.backward(dy.to(DEV, torch.bfloat16))
+    mask = (y.detach().float().cpu() > 0).float() if relu else torch.ones(B, N)
+    xr, wr, br = (t.clone().requires_grad_() for t in (x, w, b))
+    yr = xr @ wr + br
+    assert _rel(y.float().cpu(), torch.relu(yr) if relu else yr) < 2e-2
+    yr.backward(dy * mask)
+    assert _rel(bg.grad.cpu(), br.grad) < 5e-3
+    assert _rel(wg.grad.cpu(), wr.grad) < 2e-2
+    assert _rel(xg.grad.float().cpu(), xr.grad) < 2e-2
