@@ -13,6 +13,7 @@ momentum-SGD + weight-decay update of every parameter.  Data: synthetic ImageNet
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -95,7 +96,9 @@ def main():
         from distributed_tensorflow_models_amd.parallel import process_group as pg
         pg.broadcast_tensors(list(net.parameters()) + list(net.buffers()))
     torch.manual_seed(1234 + rank)  # each rank its own synthetic batch
-    step = TrainStep(net, optimizer=opt, lr=0.1 * world if opt == "momentum" else 0.01 * world, momentum=0.9,
+    # one learning rate at every N (no linear x W scaling here, unlike the trainers' C16): the same
+    # update math at 1..8 GPUs, and no early divergence of a random-init net at lr 0.8 on random labels
+    step = TrainStep(net, optimizer=opt, lr=0.1 if opt == "momentum" else 0.01, momentum=0.9,
                      bucket_mb=args.bucket_mb, use_graph=bool(args.graph),
                      grad_comm_dtype=torch.bfloat16 if args.grad_comm == "bf16" else None, **extra)
     cin = 1 if args.model == "lenet" else 3
@@ -140,7 +143,7 @@ def main():
                        "image_size": S, "parallelism": "dp%d" % world, "device": args.device,
                        "grad_allreduce_dtype": args.grad_comm,
                        "optimizer": {"momentum": "momentum-sgd+wd", "rmsprop": "rmsprop(TF)+wd", "sgd": "sgd+wd"}[opt],
-                       "final_loss": round(float(loss), 4)},
+                       "final_loss": round(float(loss), 4) if math.isfinite(float(loss)) else None},
         }
         print(json.dumps(out), flush=True)
     if world > 1:
