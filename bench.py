@@ -15,11 +15,10 @@ import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
@@ -61,7 +60,20 @@ def main():
                     help="cpu: the plumbing config (LeNet over gloo, no GPU; BASELINE.json config 1)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # self-launch (mirrors reference train.sh:46-61, one process per worker): the parent never
+        # touches the GPU; it starts N fresh ranks and forwards their output
+        sys.exit(_launch_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        print("bench.py: WORLD_SIZE=%s but --gpus %d; refusing to report a mismatched run" % (env_world, args.gpus),
+              file=sys.stderr, flush=True)
+        sys.exit(2)
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(env_world or "1")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     cpu = args.device == "cpu"
@@ -96,6 +108,8 @@ def main():
         from distributed_tensorflow_models_amd.parallel import process_group as pg
         pg.broadcast_tensors(list(net.parameters()) + list(net.buffers()))
     torch.manual_seed(1234 + rank)  # each rank its own synthetic batch
+    from distributed_tensorflow_models_amd.ops import elementwise as _ew
+    _ew.set_base_seed(1234, rank)  # and its own dropout masks
     # one learning rate at every N (no linear x W scaling here, unlike the trainers' C16): the same
     # update math at 1..8 GPUs, and no early divergence of a random-init net at lr 0.8 on random labels
     step = TrainStep(net, optimizer=opt, lr=0.1 if opt == "momentum" else 0.01, momentum=0.9,
@@ -148,6 +162,28 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _launch_ranks(n):
+    """Start ``n`` ranks of this script under torch.distributed.run (subprocess, never exec) and
+    return the worst child exit code.  Rank 0's JSON line reaches stdout through the child."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this host driver
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    proc = subprocess.Popen(cmd, env=env, start_new_session=True)
+    try:
+        return proc.wait()
+    except KeyboardInterrupt:
+        os.killpg(proc.pid, 15)
+        return proc.wait()
 
 
 if __name__ == "__main__":

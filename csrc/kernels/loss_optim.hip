@@ -106,6 +106,11 @@ __global__ __launch_bounds__(256) void multi_tensor_opt_kernel(const OptTensor* 
   const float lr = (h.dyn ? h.dyn[0] : h.lr) * t.lr_mult;
   const float ema_decay = h.dyn ? h.dyn[1] : h.ema_decay;
   const float grad_scale = h.dyn ? h.dyn[2] : h.grad_scale;
+  if (!t.g) {  // EMA-only row (BN moving statistics): shadow -= (1-d)(shadow - value)
+    if (h.use_ema && t.ema)
+      for (long i = c.start + threadIdx.x; i < end; i += 256) t.ema[i] -= (1.f - ema_decay) * (t.ema[i] - t.p[i]);
+    return;
+  }
   for (long i = c.start + threadIdx.x; i < end; i += 256) {
     float p = t.p[i];
     float g = t.g[i] * grad_scale + t.wd * p;

@@ -68,6 +68,10 @@ def model_variables(model, optimizer=None, global_step=None, include_slots=True,
                 out.append(TFVar(base.name + "/RMSProp_1", st["s1"], base.layout))
             if "ema" in st:
                 out.append(TFVar(base.name + "/ExponentialMovingAverage", st["ema"], base.layout))
+        for b, shadow in getattr(optimizer, "buffer_shadows", lambda: [])():
+            base = by_param.get(id(b))
+            if base is not None:
+                out.append(TFVar(base.name + "/ExponentialMovingAverage", shadow, base.layout))
     if global_step is not None:
         out.append(TFVar("global_step", global_step))
     return out

@@ -21,6 +21,13 @@ def prepare_compute_copies(model):
             p.bf16 = p.detach().to(torch.bfloat16)
 
 
+def moving_average_buffers(model):
+    """The tensors TF puts in moving_average_variables(): every BN moving mean / variance."""
+    from .models.layers import tf_variables
+    return [t for _n, t, _l, trainable in tf_variables(model)
+            if not trainable and t.dtype == torch.float32 and t.is_floating_point()]
+
+
 class TrainStep:
     def __init__(self, model, optimizer="momentum", lr=0.1, momentum=0.9, rho=0.9, epsilon=1e-10, bucket_mb=32.0,
                  label_smoothing=0.0, aux_weight=0.4, ema_decay=None, lr_schedule=None, use_graph=False,
@@ -30,7 +37,8 @@ class TrainStep:
         prepare_compute_copies(model)
         params = [p for p in model.parameters() if p.requires_grad]
         self.dp = BSPDataParallel(params, bucket_mb, process_group, comm_dtype=grad_comm_dtype)
-        self.opt = FusedOptimizer(params, optimizer, lr, momentum, rho, epsilon, ema_decay, weight_decay)
+        self.opt = FusedOptimizer(params, optimizer, lr, momentum, rho, epsilon, ema_decay, weight_decay,
+                                  ema_buffers=moving_average_buffers(model) if ema_decay is not None else ())
         self.lr = lr
         self.lr_schedule = lr_schedule
         self.smoothing = label_smoothing

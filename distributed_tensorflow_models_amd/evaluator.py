@@ -61,13 +61,16 @@ def define_eval_flags(flags, preset):
 
 
 def restore_for_eval(model, path, use_ema):
-    """Trainable variables from their EMA shadow (when present), everything else by name."""
+    """With ``use_ema`` every variable that has a shadow (trainables and BN moving statistics, as
+    tf.train.ExponentialMovingAverage.variables_to_restore maps them; reference
+    cnn/cifar10_eval.py:132-135, inception/inception_eval.py:157-160) is restored from
+    ``<v>/ExponentialMovingAverage``; everything else by name."""
     from .ckpt.bundle import BundleReader
     names = set(BundleReader(path).names()) if use_ema else set()
     vs = []
     for name, t, layout, trainable in tf_variables(model):
         shadow = name + "/ExponentialMovingAverage"
-        vs.append(TFVar(shadow if (use_ema and trainable and shadow in names) else name, t, layout))
+        vs.append(TFVar(shadow if (use_ema and shadow in names) else name, t, layout))
     Saver(vs).restore(path)
     from .ops.nn import invalidate_weight_copies
     invalidate_weight_copies(model.parameters())

@@ -124,6 +124,15 @@ class _DropoutFn(torch.autograd.Function):
 _seed = [1234]
 
 
+def set_base_seed(seed, rank=0):
+    """Reset the dropout seed stream from the run seed and this process's rank, so every replica
+    draws its own masks (each reference worker samples dropout independently) while a fixed
+    (seed, rank) pair stays reproducible.  Called by the trainer and bench at start-up."""
+    x = (int(seed) * 0x9E3779B97F4A7C15 + (int(rank) + 1) * 0xBF58476D1CE4E5B9) % (1 << 64)
+    x ^= x >> 31
+    _seed[0] = (x * 0x94D049BB133111EB) % (1 << 62)
+
+
 def next_seed():
     _seed[0] = (_seed[0] * 6364136223846793005 + 1442695040888963407) % (1 << 62)
     return int(_seed[0])

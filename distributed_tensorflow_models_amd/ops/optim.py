@@ -23,8 +23,13 @@ KINDS = {"sgd": 0, "momentum": 1, "rmsprop": 2}
 
 class FusedOptimizer:
     def __init__(self, params, kind="momentum", lr=0.1, momentum=0.9, rho=0.9, epsilon=1e-10, ema_decay=None,
-                 weight_decay=None, lr_mults=None):
+                 weight_decay=None, lr_mults=None, ema_buffers=()):
         self.params = [p for p in params if p.requires_grad]
+        # non-trainable tensors that also get an EMA shadow (BN moving mean/variance: the reference
+        # averages trainable_variables() + moving_average_variables(), e.g. reference
+        # alexnet/cifar10_alexnet_bsp.py:79-86, inception/imagenet_inception_bsp.py:123-126)
+        self.ema_buffers = [b for b in ema_buffers] if ema_decay is not None else []
+        self.buffer_ema = {id(b): b.detach().clone().float() for b in self.ema_buffers}
         if kind not in KINDS:
             raise ValueError(kind)
         self.kind, self.lr, self.mu, self.rho, self.eps = kind, lr, momentum, rho, epsilon
@@ -69,6 +74,17 @@ class FusedOptimizer:
             tens[i, 7] = np.array([st["wd"], st["lr_mult"]], dtype=np.float32).view(np.uint64)[0]
             for s in range(0, p.numel(), chunk):
                 chunks.append((i, 0, s))
+        # EMA-only rows (grad pointer 0): the kernel just moves the shadow towards the buffer
+        base = len(self.params)
+        if self.ema_buffers:
+            tens = np.concatenate([tens, np.zeros((len(self.ema_buffers), 8), dtype=np.uint64)])
+        for j, b in enumerate(self.ema_buffers):
+            assert b.dtype == torch.float32 and b.is_contiguous(), "EMA buffers must be contiguous fp32"
+            tens[base + j, 0] = b.data_ptr()
+            tens[base + j, 5] = self.buffer_ema[id(b)].data_ptr()
+            tens[base + j, 6] = b.numel()
+            for s in range(0, b.numel(), chunk):
+                chunks.append((base + j, 0, s))
         ct = np.zeros((len(chunks), 2), dtype=np.int64)
         for j, (i, _, s) in enumerate(chunks):
             ct[j, 0] = i  # int t, int pad packed little-endian into first 8 bytes
@@ -161,6 +177,9 @@ class FusedOptimizer:
                 w16.copy_(p)
             if "ema" in st:
                 st["ema"].sub_((1 - d) * (st["ema"] - p))
+        for b in self.ema_buffers:
+            e = self.buffer_ema[id(b)]
+            e.sub_((1 - d) * (e - b.float()))
 
     # ---- state for checkpoints (TF slot names) -------------------------------------------------
     def slot_variables(self):
@@ -180,3 +199,7 @@ class FusedOptimizer:
             if "ema" in st:
                 out.append((name + "/ExponentialMovingAverage", st["ema"]))
         return out
+
+    def buffer_shadows(self):
+        """[(buffer, shadow)] for the EMA-averaged non-trainable tensors (BN moving statistics)."""
+        return [(b, self.buffer_ema[id(b)]) for b in self.ema_buffers]

@@ -206,6 +206,8 @@ def train(preset, flags, default_mode="bsp"):
     device = _device()
     logging.info("replica %d of world %d (%s, %s)", rank, world, mode, device)
     torch.manual_seed(FLAGS.seed + (rank if mode != "bsp" else 0))
+    from .ops import elementwise as _ew
+    _ew.set_base_seed(FLAGS.seed, rank)  # independent dropout masks per replica
     if FLAGS.deterministic and device.type == "cuda":
         from .ops import _lib
         _lib.set_deterministic(True)

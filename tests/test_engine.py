@@ -164,3 +164,33 @@ def test_deterministic_mode_bit_reproducible_across_allocation_histories():
         assert torch.equal(outs[0][1], outs[1][1])
     finally:
         _lib.set_deterministic(False)
+
+
+def _run_bench(args, env_extra=None, timeout=300):
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=timeout, cwd=root, env=env)
+
+
+def test_bench_self_launches_ranks():
+    """``bench.py --gpus 2`` with no WORLD_SIZE starts its own 2 ranks (gloo on CPU here)."""
+    import json
+    out = _run_bench(["--model", "lenet", "--device", "cpu", "--gpus", "2", "--steps", "2", "--warmup", "1",
+                      "--batch", "16"])
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 32
+
+
+def test_bench_refuses_world_size_mismatch():
+    out = _run_bench(["--model", "lenet", "--device", "cpu", "--gpus", "4", "--steps", "1", "--warmup", "0"],
+                     env_extra={"WORLD_SIZE": "2"})
+    assert out.returncode == 2 and "WORLD_SIZE" in out.stderr
