@@ -84,8 +84,9 @@ __device__ __forceinline__ void epi_barrier() {
 // SACC (statistics accumulate, persistent kernels): the BatchNorm sums are not shuffle-reduced per tile;
 // each thread adds the bf16 outputs of its fixed 8-channel chunk column in the staged-store loop to
 // ssum / ssq (registers, across all the block's tiles) and the kernel reduces them once at its end.
+// NT: threads of the block (256 = 4 waves, 512 = the 8-wave big-tile kernel).
 template <int PT, int CT, int WP, int WC, int STG, bool RAWB = false, bool EXACT = false, bool NOBIAS = false,
-          bool SACC = false>
+          bool SACC = false, int NT = 256>
 __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&acc)[WC / 16][WP / 16], char* smem,
                                                  int p0, int c0, int by, float* ssum = nullptr,
                                                  float* ssq = nullptr) {
@@ -127,7 +128,7 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
       } else if (m < a.M && kch < a.K) {
         *(uint2*)(a.y + (size_t)m * a.K + kch) = make_uint2(lo, hi);
       }
-      if (!SACC && a.stats && m < a.M && kch < a.K) {
+      if (!SACC && !staged && a.stats && m < a.M && kch < a.K) {
         float q0 = lo_bf(lo), q1 = hi_bf(lo), q2 = lo_bf(hi), q3 = hi_bf(hi);
         bsum[0] += q0; bsq[0] += q0 * q0;
         bsum[1] += q1; bsq[1] += q1 * q1;
@@ -135,7 +136,7 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
         bsum[3] += q3; bsq[3] += q3 * q3;
       }
     }
-    if (!SACC && a.stats) {
+    if (!SACC && !staged && a.stats) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
 #pragma unroll
@@ -155,10 +156,15 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
   if constexpr (staged) {
     epi_barrier<RAWB>();
     constexpr int CPR = CT / 8;  // 16-B chunks per pixel row of the tile
-    constexpr int NIT = PT * CPR / 256;
-    const int chn = tid % CPR;   // fixed per thread (256 % CPR == 0)
+    constexpr int NIT = PT * CPR / NT;
+    static_assert(NT % CPR == 0 && (PT * CPR) % NT == 0, "staged-store mapping");
+    const int chn = tid % CPR;   // fixed per thread (NT % CPR == 0)
     const int kc = c0 + chn * 8;
     const bool act = a.act_x != nullptr;
+    // BatchNorm statistics of a staged tile: each thread sums its fixed 8-channel chunk column over its
+    // rows (bf16-rounded outputs) and the block reduces them once through LDS below -> ONE partial row
+    // per pixel tile, no per-subtile shuffle trees (those cost up to +100 % on the wide-K 1x1 layers)
+    const bool bstats = !SACC && a.stats != nullptr;
     float sc[8], sh[8], sgx[8], sg[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { sc[e] = 1.f; sh[e] = 0.f; sgx[e] = 0.f; sg[e] = 0.f; }
@@ -168,7 +174,7 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
     }
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
-      const int idx = it * 256 + tid;
+      const int idx = it * NT + tid;
       const int row = idx / CPR;
       const int m = p0 + row;
       const bool inb = m < a.M && kc < a.K;
@@ -181,6 +187,13 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
                                 lo_bf(v.z), hi_bf(v.z), lo_bf(v.w), hi_bf(v.w)};
 #pragma unroll
             for (int e = 0; e < 8; ++e) { ssum[e] += q[e]; ssq[e] = fmaf(q[e], q[e], ssq[e]); }
+          }
+        } else {
+          if (bstats && inb) {  // (sgx / sg double as the statistics accumulators: act is off here)
+            const float q[8] = {lo_bf(v.x), hi_bf(v.x), lo_bf(v.y), hi_bf(v.y),
+                                lo_bf(v.z), hi_bf(v.z), lo_bf(v.w), hi_bf(v.w)};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { sgx[e] += q[e]; sg[e] = fmaf(q[e], q[e], sg[e]); }
           }
         }
         if (inb && (a.add_src || act)) {
@@ -221,25 +234,24 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
         *(uint4*)(inb ? a.y + o : a.dump) = v;
       }
     }
-    if (act) {
+    if (act || bstats) {
       // reduce the per-thread partial sums over the threads sharing this chunk column, one partial
-      // row per pixel tile (reduced over tiles by dtm_reduce_rows)
+      // row per pixel tile (reduced over tiles by dtm_reduce_rows / stats_reduce_finalize)
       epi_barrier<RAWB>();
-      float* red = (float*)smem;  // [256][16]
+      float* red = (float*)smem;  // [NT][16]
 #pragma unroll
       for (int e = 0; e < 8; ++e) { red[tid * 16 + e] = sgx[e]; red[tid * 16 + 8 + e] = sg[e]; }
       epi_barrier<RAWB>();
-      if (tid < CPR && kc < a.K) {
-        float tx[8], tg[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { tx[e] = 0.f; tg[e] = 0.f; }
-        for (int t = tid; t < 256; t += CPR) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) { tx[e] += red[t * 16 + e]; tg[e] += red[t * 16 + 8 + e]; }
-        }
-        float* prow = a.act_sums + (size_t)by * (2 * a.K);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { prow[kc + e] = tx[e]; prow[a.K + kc + e] = tg[e]; }
+      // every thread finishes one (chunk column, value) output: NT/CPR partials each, instead of CPR
+      // threads walking all NT rows of the table serially
+      float* prow = (act ? a.act_sums : a.stats) + (size_t)by * (2 * a.K);
+      for (int o = tid; o < CPR * 16; o += NT) {
+        const int c = o >> 4, e = o & 15;
+        float t = 0.f;
+#pragma unroll 4
+        for (int k = 0; k < NT / CPR; ++k) t += red[((c + k * CPR) << 4) + e];
+        const int kk = c0 + c * 8 + (e & 7);
+        if (kk < a.K) prow[(e < 8 ? 0 : a.K) + kk] = t;
       }
     }
   }
@@ -758,6 +770,145 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
   __syncthreads();  // the epilogue reuses the ring
   if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1>(a, acc, smem, p0, c0, by);
   else conv_nt_epilogue<PT, CT, WP, WC, 2>(a, acc, smem, p0, c0, by);
+}
+
+// 8-wave big-tile variant of the pipelined kernel: PT = 256 pixels x CT (128 | 256) channels per
+// 512-thread block, waves NWP (pixels) x 8/NWP (channels), each wave a (PT/NWP) x (CT*NWP/8) tile of
+// 16x16x32 MFMAs.  Why a bigger tile: the 4-wave 128x128 block (2 per CU) pulls one 32 KiB operand
+// k-tile from L2 per 128 MFMAs, i.e. ~64 B/clk/CU at the MFMA rate - more than the L2 delivers
+// (MI355X_MICROARCH: ~34.5 TB/s chip-wide); a 256x256 block halves the L2 bytes per MFMA (256x128: 0.75x).
+// Same LDS image / source-side swizzle / counted-vmcnt ring as conv_nt_pipe_kernel (no input prologue);
+// one 8-row x 128-B LDS-DMA group per wave-instruction, AI + WI of them per wave per k-tile.
+template <int PT, int CT, int NWP, int NS, int UD>
+__global__ __launch_bounds__(512) void conv_nt_w8_kernel(ConvNTArgs a) {
+  constexpr int NT = 512, NW = 8;
+  constexpr int BK = 64;
+  constexpr int NWC = NW / NWP;
+  constexpr int WP = PT / NWP, WC = CT / NWC;
+  constexpr int TP = WP / 16, TC = WC / 16;
+  constexpr int AI = PT / 64, WI = CT / 64;  // 8-row DMA groups per wave per k-tile
+  constexpr int G = AI + WI;                 // DMA instructions per wave per k-tile
+  constexpr int BUF = (PT + CT) * 128;
+  constexpr int OROW = CT * 2 + 16;
+  constexpr int RING = NS * BUF > PT * OROW ? NS * BUF : PT * OROW;
+  static_assert(RING <= 160 * 1024, "LDS budget");
+  static_assert(G <= 31 && NS >= 2 && NS <= 3, "vmcnt range");
+  __shared__ __attribute__((aligned(16))) char smem[RING];
+  typedef __attribute__((address_space(1))) const void gvoid;
+  typedef __attribute__((address_space(3))) void lvoid;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tile = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const int bx = tile % gridDim.x, by = tile / gridDim.x;
+  const int p0 = by * PT, c0 = bx * CT;
+  const int lr = lane >> 3;
+  const int ch = (lane & 7) ^ lr;  // logical 16-B chunk this lane moves (source-side swizzle)
+
+  int ih0[AI], iw0[AI], pixbase[AI];
+#pragma unroll
+  for (int j = 0; j < AI; ++j) {
+    const int m = p0 + 8 * (wave + NW * j) + lr;
+    if (m < a.M) {
+      uint32_t n = fdiv((uint32_t)m, a.fd_PQ);
+      uint32_t rem = m - n * (a.P * a.Q);
+      uint32_t p = fdiv(rem, a.fd_Q);
+      uint32_t q = rem - p * a.Q;
+      ih0[j] = (int)p * a.stride - a.pad_h;
+      iw0[j] = (int)q * a.stride - a.pad_w;
+      pixbase[j] = (int)n * a.Hin * a.Win;
+    } else {
+      ih0[j] = -(1 << 28);
+      iw0[j] = -(1 << 28);
+      pixbase[j] = 0;
+    }
+  }
+  int cc = (ch * 8) % a.C, tap = (ch * 8) / a.C;
+  int rr = tap / a.S, ss = tap - (tap / a.S) * a.S;
+  const char* xg = (const char*)a.x;
+  const char* wg = (const char*)a.w;
+  const char* zg = (const char*)a.zero;
+
+  auto issue = [&](int kt, int slot) {
+    char* base = smem + slot * BUF;
+    const int k = kt * BK + ch * 8;
+    const bool kin = k < a.Kg;
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+      const int ihv = ih0[j] + rr, iwv = iw0[j] + ss;
+      bool v = kin & ((unsigned)ihv < (unsigned)a.Hv) & ((unsigned)iwv < (unsigned)a.Wv);
+      if (UD > 1) v = v & (((ihv | iwv) & (UD - 1)) == 0);
+      const int ih = UD > 1 ? ihv / UD : ihv, iw = UD > 1 ? iwv / UD : iwv;
+      const char* src = xg + (size_t)(uint32_t)((pixbase[j] + ih * a.Win + iw) * a.pix_bytes + cc * 2);
+      __builtin_amdgcn_global_load_lds((gvoid*)(v ? src : zg), (lvoid*)(base + (wave + NW * j) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < WI; ++j) {
+      const int row = c0 + 8 * (wave + NW * j) + lr;
+      const bool v = kin & (row < a.K);
+      const char* src = wg + (size_t)(uint32_t)((row * a.Kg + k) * 2);
+      __builtin_amdgcn_global_load_lds((gvoid*)(v ? src : zg), (lvoid*)(base + PT * 128 + (wave + NW * j) * 1024),
+                                       16, 0, 0);
+    }
+    cc += BK;
+    while (cc >= a.C) {
+      cc -= a.C;
+      if (++ss == a.S) { ss = 0; ++rr; }
+    }
+  };
+
+  f32x4 acc[TC][TP];
+#pragma unroll
+  for (int i = 0; i < TC; ++i)
+#pragma unroll
+    for (int j = 0; j < TP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int wp = wave % NWP, wc = wave / NWP;
+  const int fr = lane & 15, fk = lane >> 4;
+  auto compute = [&](int slot) {
+    const char* base = smem + slot * BUF;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int chn = ks * 4 + fk;
+      short8 bf[TP], af[TC];
+#pragma unroll
+      for (int j = 0; j < TP; ++j) {
+        const int row = wp * WP + j * 16 + fr;
+        bf[j] = *(const short8*)(base + row * 128 + ((chn ^ (row & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < TC; ++i) {
+        const int row = wc * WC + i * 16 + fr;
+        af[i] = *(const short8*)(base + PT * 128 + row * 128 + ((chn ^ (row & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < TC; ++i)
+#pragma unroll
+        for (int j = 0; j < TP; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  const int nk = (a.Kg + BK - 1) / BK;
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) issue(s, s);
+  int slot = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = min(nk - 1, kt + NS - 2) - kt;
+    if (NS >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // stage kt visible to all waves; stage kt-1 no longer read
+    if (kt + NS - 1 < nk) issue(kt + NS - 1, slot == 0 ? NS - 1 : slot - 1);
+    __builtin_amdgcn_s_setprio(1);
+    compute(slot);
+    __builtin_amdgcn_s_setprio(0);
+    slot = slot == NS - 1 ? 0 : slot + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // the epilogue reuses the ring
+  if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1, false, false, false, false, NT>(a, acc, smem, p0, c0, by);
+  else conv_nt_epilogue<PT, CT, WP, WC, 2, false, false, false, false, NT>(a, acc, smem, p0, c0, by);
 }
 
 // Persistent streaming kernel for the short-reduction 1x1 stride-1 convs (K*R*S*C = 64 * NKT <= 256:
@@ -1409,6 +1560,12 @@ static void launch_nt_dma(const ConvNTArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((conv_nt_dma_kernel<PT, CT, WP, WC, UD>), grid, dim3(256), 0, st, a);
 }
 
+template <int PT, int CT, int NWP, int NS, int UD>
+static void launch_w8(const ConvNTArgs& a, hipStream_t st) {
+  dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT);
+  hipLaunchKernelGGL((conv_nt_w8_kernel<PT, CT, NWP, NS, UD>), grid, dim3(512), 0, st, a);
+}
+
 template <int PT, int CT, int NS, int UD>
 static void launch_pipe(const ConvNTArgs& a, hipStream_t st) {
   dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT);
@@ -1494,9 +1651,11 @@ struct TileCfg {
   int id, PT, NWP;
 };
 static int g_tile_env = -2;
+static int g_tile_w8 = 1;  // A/B knob: the 8-wave tile in the shape policy (dtm_conv_set_w8)
+DTM_API void dtm_conv_set_w8(int on) { g_tile_w8 = on; }
 static int g_k64_tile = 3;  // tile of the 64-output-channel layers (A/B knob: dtm_conv_set_k64_tile)
 DTM_API void dtm_conv_set_k64_tile(int id) { g_k64_tile = id; }
-static TileCfg pick_tile(const ConvNTArgs& a) {
+static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
   if (g_tile_env == -2) {
     const char* e = getenv("DTM_CONV_TILE");
     g_tile_env = e ? atoi(e) : -1;
@@ -1511,6 +1670,14 @@ static TileCfg pick_tile(const ConvNTArgs& a) {
   else if (id == -1 && a.Kg == 64 && stream_ok(a)) id = a.K >= 128 ? 30 : 31;
   // (the persistent streaming 1x1 kernel: the 64-deep 56x56 expand / reduce layers and their dgrads are
   // HBM streams: -20..-33 % (tools/conv_tile_sweep.py); at Kg 128 its 1 block/CU loses)
+  // the 8-wave 256x256 tile (id 40) where it fills the chip: >= ~150 tiles (one round, 58-100 % of the
+  // CUs), and not on the many-tile short-reduction layers without statistics (their 4-wave tiles stream
+  // better).  Measured per ResNet-50 layer (tools/conv_tile_sweep.py STATS=1, profiles/r2_conv_tiles_w8.txt):
+  // 14x14 3x3 fwd/dgrad -16 %, 7x7 1024->2048 -12 %, 28x28 256->512 fwd+stats -17 %; loses at <= 98 tiles.
+  if (id == -1 && !a.in_scale && a.K >= 256 && g_tile_w8) {
+    const long tiles = (long)((a.M + 255) / 256) * ((a.K + 255) / 256);
+    if (tiles >= 150 && !(tiles > 600 && a.Kg <= 256 && !stats)) id = 40;
+  }
   if (id == -1 && !a.in_scale && a.Kg >= 1024) id = 21;  // (-3: the policy without it, for A/B runs)
   if (id < 0) id = a.K <= 64 ? g_k64_tile : ((a.M <= 16384 && a.Kg >= 2048) ? 0 : 4);
   // LDS-DMA variants (10-12, opt-in) need an operand without the prologue affine
@@ -1518,6 +1685,11 @@ static TileCfg pick_tile(const ConvNTArgs& a) {
   // pipelined LDS-DMA variants (20-23) stage the prologue affine in LDS: C <= 512
   if (id >= 20 && a.in_scale && a.C > 512) id = 0;
   if (id >= 20 && id <= 23) return {id, 128, 2};
+  // 8-wave 256-pixel tiles (no prologue): 40 = 256x256 (waves 2x4), 41 = 256x128 3-slot (4x2),
+  // 42 = 256x128 2-slot, 43 = 256x256 (waves 4x2)
+  if (id >= 40 && id <= 43 && a.in_scale) id = 0;
+  if (id == 40) return {id, 256, 2};
+  if (id == 41 || id == 42 || id == 43) return {id, 256, 4};
   if (id == 30 || id == 31) {
     if (stream_ok(a)) return {id, 64, 2};
     id = a.K <= 64 ? 3 : 4;
@@ -1549,6 +1721,10 @@ static void dispatch_ud(const ConvNTArgs& a, const TileCfg& t, hipStream_t st) {
   else if (t.id == 21) launch_pipe<128, 128, 2, UD>(a, st);
   else if (t.id == 22) launch_pipe<128, 128, 4, UD>(a, st);
   else if (t.id == 23) launch_pipe<128, 64, 3, UD>(a, st);
+  else if (t.id == 40) launch_w8<256, 256, 2, 2, UD>(a, st);
+  else if (t.id == 41) launch_w8<256, 128, 4, 3, UD>(a, st);
+  else if (t.id == 42) launch_w8<256, 128, 4, 2, UD>(a, st);
+  else if (t.id == 43) launch_w8<256, 256, 4, 2, UD>(a, st);
   else launch_nt<128, 128, 64, 64, UD>(a, st);
 }
 
@@ -1582,10 +1758,11 @@ static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, cons
   a.M = d->N * d->P * d->Q; a.Kg = d->R * d->S * d->C; a.relu = relu;
   a.fd_PQ = make_fastdiv(d->P * d->Q); a.fd_Q = make_fastdiv(d->Q);
   int rows = 0;
-  const TileCfg tc = pick_tile(a);
+  const TileCfg tc = pick_tile(a, stats);
   if (stats) {
-    rows = (tc.id == 30 || tc.id == 31) ? stream_rows(a, tc.id)    // one per streaming worker
-                                         : ((a.M + tc.PT - 1) / tc.PT) * tc.NWP;  // per (pixel tile, pixel wave)
+    // one per streaming worker; one per pixel tile (staged epilogue, K % 8 == 0); else per (pixel tile, pixel wave)
+    rows = (tc.id == 30 || tc.id == 31) ? stream_rows(a, tc.id)
+                                         : ((a.M + tc.PT - 1) / tc.PT) * ((a.K & 7) == 0 ? 1 : tc.NWP);
     float* ws = dtm_ws_get((size_t)rows * 2 * d->K);
     if (!ws) return -4;
     a.stats = ws;

@@ -8,8 +8,14 @@
 // SSTable: data blocks with prefix-compressed entries + restart array, 5-byte trailer
 // (compression type 0 + masked crc32c), empty meta-index block, index block (restart interval 1),
 // 48-byte footer ending in magic 0xdb4775248b80fb57.
-// The reader parses any such table (multiple data shards via shard_id supported).  Partitioned
-// (sliced) variables are reported with dtype -1 (their slices are not reassembled here).
+// The reader parses any such table (multiple data shards via shard_id supported).
+// Partitioned variables (tf.fixed_size_partitioner under a partitioned variable_scope, e.g. the
+// reference's 'partitioned_space' / 'root' trainers) are stored the way TF's BundleWriter::AddSlice
+// lays them out: a data-less full-tensor entry {dtype, full shape, slices: [TensorSliceProto]} plus
+// one ordinary entry per slice whose key is checkpoint::EncodeTensorNameSlice(name, slice) - an
+// OrderedCode string (0, name, rank, (start, length) per dim; binary, so it sorts before every
+// plain name).  The writer emits that layout (dtm_bundle_writer_add_slice) and the reader
+// reassembles a sliced variable into its full tensor (dtm_bundle_reader_read).
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -67,6 +73,9 @@ void pb_fixed32(std::string* s, int field, uint32_t v) {
   put_fixed32(s, v);
 }
 
+// one TensorSliceProto: per dim (start, length); length -1 = the full extent
+typedef std::vector<std::pair<int64_t, int64_t>> Slice;
+
 struct Entry {
   std::string name;
   int dtype = 0;
@@ -75,7 +84,60 @@ struct Entry {
   int64_t offset = 0, size = 0;
   uint32_t crc = 0;  // masked
   bool sliced = false;
+  std::vector<Slice> slices;  // full-tensor entry of a partitioned variable
 };
+
+// ---- tensorflow::strings::OrderedCode (the slice-entry key encoding) ------------------------
+void oc_num_increasing(std::string* s, uint64_t v) {
+  unsigned char buf[8];
+  int len = 0;
+  while (v) {
+    buf[7 - len] = (unsigned char)(v & 0xff);
+    v >>= 8;
+    ++len;
+  }
+  s->push_back((char)len);
+  s->append((const char*)buf + 8 - len, (size_t)len);
+}
+void oc_string(std::string* s, const std::string& str) {
+  for (unsigned char c : str) {
+    if (c == 0x00) { s->push_back('\x00'); s->push_back('\xff'); }
+    else if (c == 0xff) { s->push_back('\xff'); s->push_back('\x00'); }
+    else s->push_back((char)c);
+  }
+  s->push_back('\x00');
+  s->push_back('\x01');
+}
+void oc_signed_num_increasing(std::string* s, int64_t val) {
+  const uint64_t x = val < 0 ? ~(uint64_t)val : (uint64_t)val;
+  if (x < 64) {
+    s->push_back((char)(0x80 ^ (uint8_t)val));
+    return;
+  }
+  static const uint8_t hdr[11][2] = {{0, 0},    {0x80, 0}, {0xc0, 0}, {0xe0, 0},    {0xf0, 0},   {0xf8, 0},
+                                     {0xfc, 0}, {0xfe, 0}, {0xff, 0}, {0xff, 0x80}, {0xff, 0xc0}};
+  const int bits = 64 - __builtin_clzll(x);
+  const int len = bits / 7 + 1;
+  uint8_t buf[10];
+  buf[0] = buf[1] = val < 0 ? 0xff : 0x00;
+  for (int i = 0; i < 8; ++i) buf[2 + i] = (uint8_t)((uint64_t)val >> (56 - 8 * i));
+  uint8_t* b = buf + 10 - len;
+  b[0] ^= hdr[len][0];
+  b[1] ^= hdr[len][1];
+  s->append((const char*)b, (size_t)len);
+}
+// checkpoint::EncodeTensorNameSlice
+std::string slice_key(const std::string& name, const Slice& sl) {
+  std::string k;
+  oc_num_increasing(&k, 0);
+  oc_string(&k, name);
+  oc_num_increasing(&k, sl.size());
+  for (const auto& e : sl) {
+    oc_signed_num_increasing(&k, e.first);
+    oc_signed_num_increasing(&k, e.second);
+  }
+  return k;
+}
 
 std::string encode_entry(const Entry& e) {
   std::string s, shp;
@@ -86,11 +148,57 @@ std::string encode_entry(const Entry& e) {
     pb_bytes(&shp, 2, dim);
   }
   pb_bytes(&s, 2, shp);  // TensorShapeProto (present even for scalars)
+  if (!e.slices.empty()) {
+    // full-tensor entry of a partitioned variable: no shard / offset / size / crc (BundleWriter::AddSlice)
+    for (const Slice& sl : e.slices) {
+      std::string sp;
+      for (const auto& ext : sl) {
+        std::string ex;  // TensorSliceProto.Extent: a full extent is an empty message
+        if (ext.second >= 0) {
+          if (ext.first) pb_varint(&ex, 1, (uint64_t)ext.first);
+          pb_varint(&ex, 2, (uint64_t)ext.second);
+        }
+        pb_bytes(&sp, 1, ex);
+      }
+      pb_bytes(&s, 7, sp);
+    }
+    return s;
+  }
   if (e.shard) pb_varint(&s, 3, (uint64_t)e.shard);
   if (e.offset) pb_varint(&s, 4, (uint64_t)e.offset);
   if (e.size) pb_varint(&s, 5, (uint64_t)e.size);
   pb_fixed32(&s, 6, e.crc);
   return s;
+}
+
+bool skip_field(const char*& p, const char* end, int wt);
+
+bool decode_slice(const char* p, const char* end, Slice* sl) {
+  while (p < end) {
+    uint64_t key, len;
+    if (!get_varint(p, end, &key)) return false;
+    if ((key >> 3) == 1 && (key & 7) == 2) {
+      if (!get_varint(p, end, &len) || p + len > end) return false;
+      const char* q = p, *qe = p + len;
+      int64_t start = 0, length = -1;
+      while (q < qe) {
+        uint64_t k2, v2;
+        if (!get_varint(q, qe, &k2)) return false;
+        if ((k2 & 7) == 0) {
+          if (!get_varint(q, qe, &v2)) return false;
+          if ((k2 >> 3) == 1) start = (int64_t)v2;
+          else if ((k2 >> 3) == 2) length = (int64_t)v2;
+        } else if (!skip_field(q, qe, (int)(k2 & 7))) {
+          return false;
+        }
+      }
+      sl->emplace_back(start, length);
+      p = qe;
+    } else if (!skip_field(p, end, (int)(key & 7))) {
+      return false;
+    }
+  }
+  return true;
 }
 
 std::string encode_header(int num_shards) {
@@ -164,6 +272,9 @@ bool decode_entry(const std::string& val, Entry* e) {
         if (!decode_shape(p, p + v, &e->shape)) return false;
       } else if (f == 7) {
         e->sliced = true;
+        Slice sl;
+        if (!decode_slice(p, p + v, &sl)) return false;
+        e->slices.push_back(sl);
       }
       p += v;
     } else if (!skip_field(p, end, wt)) {
@@ -329,12 +440,14 @@ struct Writer {
   FILE* data = nullptr;
   int64_t off = 0;
   std::vector<Entry> entries;
+  std::map<std::string, Entry> full;  // partitioned variables: name -> full-tensor entry
 };
 
 struct Reader {
   std::string prefix;
   int num_shards = 1;
-  std::vector<Entry> entries;
+  std::vector<Entry> entries;               // plain tensors + full entries of partitioned ones
+  std::map<std::string, Entry> slice_entries;  // encoded slice key -> entry
   std::map<int, FILE*> shards;
   ~Reader() {
     for (auto& s : shards) std::fclose(s.second);
@@ -362,9 +475,9 @@ API void* dtm_bundle_writer_new(const char* prefix) {
   return w;
 }
 
-API int dtm_bundle_writer_add(void* h, const char* name, int dtype, const int64_t* shape, int ndim, const void* data,
-                              int64_t nbytes) {
-  Writer* w = (Writer*)h;
+// (the key is a std::string: an encoded slice key contains NUL bytes)
+static int writer_add(Writer* w, const std::string& name, int dtype, const int64_t* shape, int ndim, const void* data,
+                      int64_t nbytes) {
   Entry e;
   e.name = name;
   e.dtype = dtype;
@@ -378,9 +491,40 @@ API int dtm_bundle_writer_add(void* h, const char* name, int dtype, const int64_
   return 0;
 }
 
+API int dtm_bundle_writer_add(void* h, const char* name, int dtype, const int64_t* shape, int ndim, const void* data,
+                              int64_t nbytes) {
+  return writer_add((Writer*)h, name, dtype, shape, ndim, data, nbytes);
+}
+
+// One slice of a partitioned variable: starts/lengths per dim of the FULL tensor (length -1 = full
+// extent), data = the slice's values (C order, shape = the lengths).
+API int dtm_bundle_writer_add_slice(void* h, const char* name, int dtype, const int64_t* full_shape, int ndim,
+                                    const int64_t* starts, const int64_t* lengths, const void* data, int64_t nbytes) {
+  Writer* w = (Writer*)h;
+  Slice sl;
+  std::vector<int64_t> sshape;
+  for (int d = 0; d < ndim; ++d) {
+    if (starts[d] < 0 || (lengths[d] >= 0 && starts[d] + lengths[d] > full_shape[d])) return -4;
+    sl.emplace_back(starts[d], lengths[d]);
+    sshape.push_back(lengths[d] < 0 ? full_shape[d] : lengths[d]);
+  }
+  Entry& f = w->full[name];
+  if (f.name.empty()) {
+    f.name = name;
+    f.dtype = dtype;
+    f.shape.assign(full_shape, full_shape + ndim);
+  } else if (f.dtype != dtype || f.shape != std::vector<int64_t>(full_shape, full_shape + ndim)) {
+    return -5;
+  }
+  f.slices.push_back(sl);
+  const std::string key = slice_key(name, sl);
+  return writer_add(w, key, dtype, sshape.data(), ndim, data, nbytes) == 0 ? 0 : -1;
+}
+
 API int dtm_bundle_writer_finish(void* h) {
   Writer* w = (Writer*)h;
   int rc = 0;
+  for (auto& kv : w->full) w->entries.push_back(kv.second);
   if (std::fclose(w->data) != 0) rc = -1;
   std::sort(w->entries.begin(), w->entries.end(), [](const Entry& a, const Entry& b) { return a.name < b.name; });
   for (size_t i = 1; i < w->entries.size(); ++i)
@@ -441,7 +585,8 @@ API void* dtm_bundle_reader_open(const char* prefix) {
       delete r;
       return nullptr;
     }
-    r->entries.push_back(e);
+    if (e.name[0] == '\0') r->slice_entries[e.name] = e;  // an EncodeTensorNameSlice key
+    else r->entries.push_back(e);
   }
   return r;
 }
@@ -449,21 +594,94 @@ API void* dtm_bundle_reader_open(const char* prefix) {
 API int dtm_bundle_reader_num(void* h) { return (int)((Reader*)h)->entries.size(); }
 API const char* dtm_bundle_reader_name(void* h, int i) { return ((Reader*)h)->entries[i].name.c_str(); }
 
-API int dtm_bundle_reader_info(void* h, int i, int* dtype, int64_t* shape, int* ndim, int64_t* nbytes) {
+static int dtype_size(int dt) {
+  switch (dt) {
+    case 1: case 3: return 4;          // float, int32
+    case 2: case 9: return 8;          // double, int64
+    case 4: case 6: case 10: return 1; // uint8, int8, bool
+    case 5: case 14: case 17: case 19: return 2;  // int16, bfloat16, uint16, half
+    default: return 0;
+  }
+}
+
+static int64_t full_bytes(const Entry& e) {
+  int64_t n = dtype_size(e.dtype);
+  for (int64_t d : e.shape) n *= d;
+  return n;
+}
+
+// sliced: 1 when the entry is a partitioned variable (read reassembles its slices), nbytes = full size
+API int dtm_bundle_reader_info2(void* h, int i, int* dtype, int64_t* shape, int* ndim, int64_t* nbytes, int* sliced) {
   Reader* r = (Reader*)h;
   if (i < 0 || i >= (int)r->entries.size()) return -1;
   const Entry& e = r->entries[i];
-  *dtype = e.sliced ? -1 : e.dtype;
+  *dtype = e.dtype;
   *ndim = (int)std::min<size_t>(e.shape.size(), 8);
   for (int d = 0; d < *ndim; ++d) shape[d] = e.shape[d];
-  *nbytes = e.size;
+  *nbytes = e.sliced ? full_bytes(e) : e.size;
+  *sliced = e.sliced ? 1 : 0;
   return 0;
+}
+
+API int dtm_bundle_reader_info(void* h, int i, int* dtype, int64_t* shape, int* ndim, int64_t* nbytes) {
+  int sliced = 0;
+  return dtm_bundle_reader_info2(h, i, dtype, shape, ndim, nbytes, &sliced);
+}
+
+static int read_entry(Reader* r, const Entry& e, void* dst, int64_t nbytes);
+
+// reassemble a partitioned variable: every slice's data is copied into its box of the full tensor
+static int read_sliced(Reader* r, const Entry& e, void* dst, int64_t nbytes) {
+  const int es = dtype_size(e.dtype), nd = (int)e.shape.size();
+  if (!es || nbytes != full_bytes(e)) return -1;
+  std::vector<int64_t> fstride(nd + 1, 1);
+  for (int d = nd - 1; d >= 0; --d) fstride[d] = fstride[d + 1] * e.shape[d];
+  int64_t covered = 0;
+  for (const Slice& sl : e.slices) {
+    if ((int)sl.size() != nd) return -4;
+    std::vector<int64_t> st(nd), ln(nd);
+    int64_t cnt = 1;
+    for (int d = 0; d < nd; ++d) {
+      st[d] = sl[d].first;
+      ln[d] = sl[d].second < 0 ? e.shape[d] : sl[d].second;
+      if (st[d] < 0 || st[d] + ln[d] > e.shape[d]) return -4;
+      cnt *= ln[d];
+    }
+    auto it = r->slice_entries.find(slice_key(e.name, sl));
+    if (it == r->slice_entries.end() || it->second.size != cnt * es) return -4;
+    std::vector<char> buf((size_t)(cnt * es));
+    int rc = read_entry(r, it->second, buf.data(), (int64_t)buf.size());
+    if (rc) return rc;
+    covered += cnt;
+    if (cnt == 0) continue;
+    // copy rows of the innermost dim: iterate the outer index tuple of the slice box
+    const int64_t row = (nd ? ln[nd - 1] : 1) * es;
+    const int64_t rows = nd ? cnt / ln[nd - 1] : 1;
+    std::vector<int64_t> idx(nd, 0);
+    for (int64_t rrow = 0; rrow < rows; ++rrow) {
+      int64_t off = 0;
+      for (int d = 0; d < nd; ++d) off += (st[d] + idx[d]) * fstride[d + 1];
+      std::memcpy((char*)dst + off * es, buf.data() + rrow * row, (size_t)row);
+      for (int d = nd - 2; d >= 0; --d) {  // odometer over the outer dims
+        if (++idx[d] < ln[d]) break;
+        idx[d] = 0;
+      }
+    }
+  }
+  int64_t total = 1;
+  for (int64_t d : e.shape) total *= d;
+  return covered == total ? 0 : -4;  // slices must tile the tensor (TF partitions do, disjointly)
 }
 
 API int dtm_bundle_reader_read(void* h, int i, void* dst, int64_t nbytes) {
   Reader* r = (Reader*)h;
   if (i < 0 || i >= (int)r->entries.size()) return -1;
   const Entry& e = r->entries[i];
+  if (e.sliced) return read_sliced(r, e, dst, nbytes);
+  return read_entry(r, e, dst, nbytes);
+}
+
+static int read_entry(Reader* r, const Entry& e, void* dst, int64_t nbytes) {
   if (nbytes != e.size) return -1;
   FILE*& f = r->shards[e.shard];
   if (!f) {

@@ -12,7 +12,11 @@ _SIGS = {
     "dtm_crc32c_masked": (ctypes.c_uint32, [_P, ctypes.c_size_t]),
     "dtm_bundle_writer_new": (_P, [_C]),
     "dtm_bundle_writer_add": (_I, [_P, _C, _I, ctypes.POINTER(ctypes.c_int64), _I, _P, _L]),
+    "dtm_bundle_writer_add_slice": (_I, [_P, _C, _I, ctypes.POINTER(ctypes.c_int64), _I,
+                                        ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), _P, _L]),
     "dtm_bundle_writer_finish": (_I, [_P]),
+    "dtm_bundle_reader_info2": (_I, [_P, _I, ctypes.POINTER(_I), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(_I),
+                                     ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(_I)]),
     "dtm_bundle_reader_open": (_P, [_C]),
     "dtm_bundle_reader_num": (_I, [_P]),
     "dtm_bundle_reader_name": (_C, [_P, _I]),

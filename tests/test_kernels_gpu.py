@@ -16,25 +16,31 @@ def _rel(a, b):
 
 
 CONV_CASES = [
-    # N, H, W, C, K, R, stride, padding
-    (2, 14, 14, 64, 64, 3, 1, "SAME"),
-    (2, 14, 14, 64, 128, 1, 1, "SAME"),
-    (2, 15, 15, 32, 64, 3, 2, "SAME"),      # asymmetric SAME
-    (2, 16, 16, 64, 64, 3, 2, (1, 1)),       # conv2d_same style explicit pad
-    (2, 9, 9, 128, 256, 3, 1, "VALID"),
-    (2, 32, 32, 3, 64, 7, 2, (3, 3)),        # stem (C=3 -> padded)
-    (3, 7, 7, 512, 512, 3, 1, "SAME"),
-    (2, 8, 8, 256, 1000, 1, 1, "SAME"),      # K not a multiple of the tile
-    (1, 17, 17, 192, 160, (1, 7)[0], 1, "SAME"),
+    # N, H, W, C, K, (R, S), stride, padding
+    (2, 14, 14, 64, 64, (3, 3), 1, "SAME"),
+    (2, 14, 14, 64, 128, (1, 1), 1, "SAME"),
+    (2, 15, 15, 32, 64, (3, 3), 2, "SAME"),      # asymmetric SAME
+    (2, 16, 16, 64, 64, (3, 3), 2, (1, 1)),       # conv2d_same style explicit pad
+    (2, 9, 9, 128, 256, (3, 3), 1, "VALID"),
+    (2, 32, 32, 3, 64, (7, 7), 2, (3, 3)),        # stem (C=3 -> padded)
+    (3, 7, 7, 512, 512, (3, 3), 1, "SAME"),
+    (2, 8, 8, 256, 1000, (1, 1), 1, "SAME"),      # K not a multiple of the tile
+    # Inception-v3 factorised convs (reference inception/slim/inception_model.py:127-317)
+    (2, 17, 17, 128, 128, (1, 7), 1, "SAME"),
+    (2, 17, 17, 160, 192, (7, 1), 1, "SAME"),
+    (2, 8, 8, 384, 384, (1, 3), 1, "SAME"),
+    (2, 8, 8, 448, 384, (3, 1), 1, "SAME"),
+    (2, 35, 35, 288, 384, (3, 3), 2, "VALID"),    # mixed_17x17x768a 3x3/2 VALID
+    (2, 17, 17, 192, 320, (3, 3), 2, "VALID"),    # mixed_8x8x1280a
 ]
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_fwd_bwd(case):
     torch.manual_seed(0)
-    N, H, W, C, K, R, st, pad = case
+    N, H, W, C, K, (R, S), st, pad = case
     x = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16).float()
-    w = (torch.randn(K, R, R, C, device=DEV) * (1.0 / (R * R * C) ** 0.5)).to(torch.bfloat16).float()
+    w = (torch.randn(K, R, S, C, device=DEV) * (1.0 / (R * S * C) ** 0.5)).to(torch.bfloat16).float()
     xr = x.clone().requires_grad_()
     wr = w.clone().requires_grad_()
     yr = ref.conv2d(xr, wr, None, st, pad)
@@ -154,11 +160,11 @@ def test_image_augment_kernel_matches_oracle(distort, size):
     assert got.is_cuda and _rel(got.cpu(), ref_out) < 1e-4
 
 
-@pytest.mark.parametrize("tile", [20, 21, 22, 23, 30, 31])
+@pytest.mark.parametrize("tile", [20, 21, 22, 23, 30, 31, 40, 41, 42, 43])
 @pytest.mark.parametrize("prologue", [False, True])
 @pytest.mark.parametrize("case", [(4, 15, 15, 64, 96, 3, 2), (2, 14, 14, 128, 256, 3, 1), (3, 7, 7, 512, 200, 1, 1),
                                   (2, 9, 9, 24, 40, 3, 1), (4, 12, 12, 64, 256, 1, 1), (3, 7, 7, 128, 96, 1, 1),
-                                  (2, 9, 9, 64, 64, 1, 1), (2, 30, 30, 128, 64, 1, 1)])
+                                  (2, 9, 9, 64, 64, 1, 1), (2, 30, 30, 128, 64, 1, 1), (4, 16, 16, 256, 512, 3, 1)])
 def test_conv_pipelined_tiles_match_reference(tile, prologue, case):
     """The pipelined LDS-DMA conv kernels (DTM_CONV_TILE=20..23; ring of k-tiles, counted vmcnt, the
     BatchNorm-apply prologue transformed in LDS) against the fp32 reference: forward (with and without
