@@ -1329,24 +1329,29 @@ __device__ __forceinline__ void tr_inv(int q, int& k, int& m) {
   m = (b % MB) * 16 + (q & 1) * 8;
 }
 
-template <int MT, int NT, int NS>
-__global__ __launch_bounds__(256) void conv_wgrad_pipe_kernel(ConvWgradArgs a) {
+// NTH threads (256 = 4 waves 2x2; 512 = the 8-wave 256x256 variant, waves NWM x 8/NWM): the bigger tile
+// halves the L2 operand bytes per MFMA (same reasoning as conv_nt_w8_kernel)
+template <int MT, int NT, int NS, int NWM = 2, int NTH = 256>
+__global__ __launch_bounds__(NTH) void conv_wgrad_pipe_kernel(ConvWgradArgs a) {
   constexpr int BK = 64;
-  constexpr int WM = MT / 2, WN = NT / 2;
+  constexpr int NW = NTH / 64;
+  constexpr int NWN = NW / NWM;
+  constexpr int WM = MT / NWM, WN = NT / NWN;
   constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int AI = MT / 32, BI = NT / 32;  // 1-KiB DMA pieces per wave per k-tile
+  constexpr int AI = MT / (8 * NW), BI = NT / (8 * NW);  // 1-KiB DMA pieces per wave per k-tile
   constexpr int G = AI + BI;
   constexpr int BUF = BK * (MT + NT) * 2;
   __shared__ __attribute__((aligned(16))) char smem[NS * BUF];
   typedef __attribute__((address_space(1))) const void gvoid;
   typedef __attribute__((address_space(3))) void lvoid;
   static_assert(G <= 31 && NS >= 2 && NS <= 3, "vmcnt range");
+  static_assert(AI * 8 * NW == MT && BI * 8 * NW == NT, "DMA piece mapping");
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int gxy = gridDim.x * gridDim.y;
   const int tile = xcd_remap((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x, gxy * gridDim.z);
   const int bz = tile / gxy, by = (tile % gxy) / gridDim.x, bx = tile % gridDim.x;
-  const int wm = wave % 2, wn = wave / 2;
+  const int wm = wave % NWM, wn = wave / NWM;
   const int n0 = bx * NT, m0 = by * MT;
   const int pix_lo = bz * a.pix_per_split;
   const int pix_hi = min(a.Mpix, pix_lo + a.pix_per_split);
@@ -1357,7 +1362,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_pipe_kernel(ConvWgradArgs a) {
 #pragma unroll
   for (int j = 0; j < AI; ++j) {
     int k, m;
-    tr_inv<MT>((wave + 4 * j) * 64 + lane, k, m);
+    tr_inv<MT>((wave + NW * j) * 64 + lane, k, m);
     a_k[j] = k;
     a_colv[j] = m0 + m < a.K;
     a_off[j] = m0 + m;
@@ -1367,7 +1372,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_pipe_kernel(ConvWgradArgs a) {
 #pragma unroll
   for (int j = 0; j < BI; ++j) {
     int k, m;
-    tr_inv<NT>((wave + 4 * j) * 64 + lane, k, m);
+    tr_inv<NT>((wave + NW * j) * 64 + lane, k, m);
     b_k[j] = k;
     const int col = n0 + m;
     b_colv[j] = col < a.Kg;
@@ -1387,7 +1392,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_pipe_kernel(ConvWgradArgs a) {
       const int pix = pbase + a_k[j];
       const bool v = (pix < pix_hi) & a_colv[j];
       const char* src = dg + (size_t)(uint32_t)((pix * a.K + a_off[j]) * 2);
-      __builtin_amdgcn_global_load_lds((gvoid*)(v ? src : zg), (lvoid*)(base + (wave + 4 * j) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gvoid*)(v ? src : zg), (lvoid*)(base + (wave + NW * j) * 1024), 16, 0, 0);
     }
 #pragma unroll
     for (int j = 0; j < BI; ++j) {
@@ -1400,7 +1405,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_pipe_kernel(ConvWgradArgs a) {
       const int iw = (int)q * a.stride - a.pad_w + b_s[j];
       const bool v = (pix < pix_hi) & b_colv[j] & ((unsigned)ih < (unsigned)a.H) & ((unsigned)iw < (unsigned)a.W);
       const char* src = xg + (size_t)(uint32_t)((((int)n * a.H + ih) * a.W + iw) * a.pix_bytes + b_c[j] * 2);
-      __builtin_amdgcn_global_load_lds((gvoid*)(v ? src : zg), (lvoid*)(base + BK * MT * 2 + (wave + 4 * j) * 1024),
+      __builtin_amdgcn_global_load_lds((gvoid*)(v ? src : zg), (lvoid*)(base + BK * MT * 2 + (wave + NW * j) * 1024),
                                        16, 0, 0);
     }
   };
@@ -1892,10 +1897,15 @@ DTM_API int dtm_conv_wgrad(const void* x, const void* dy, float* dw, const float
   if (wenv == -1 && !in_scale && d->K > 64) {  // (-3: the policy without it, for A/B runs)
     wt = 10;
     occ = (d->R * d->S > 1 && a.Mpix <= 16384) ? 4 : 2;
+    // the 8-wave 256x256 tile on the wide deep-reduction layers (profiles/r2_wgrad_tiles_w8.txt:
+    // 14x14 / 7x7 3x3 -8..-13 %, 7x7 1024->2048 -7 %; it loses on every K < 256 or short-RSC layer)
+    if (g_tile_w8 && d->K >= 256 && a.Kg >= 1024 && (d->R * d->S > 1 || d->K >= 1024)) wt = 12;
   }
   if (wt >= 10 && in_scale) wt = d->K <= 64 ? 1 : 0;  // the pipelined kernels have no input prologue
   const bool small_m = (wt == 1 || wt == 2);
-  const int MT = small_m ? 64 : 128, NT = 128;
+  const bool big = wt == 12;  // 8-wave 256x256 (one block per CU)
+  const int MT = small_m ? 64 : (big ? 256 : 128), NT = big ? 256 : 128;
+  if (big) occ = (wenv == 12 && g_wgrad_occ != 4) ? g_wgrad_occ : 1;  // (sweeps: WTILES=12:<occ>)
   long tiles = (long)((a.Kg + NT - 1) / NT) * ((a.K + MT - 1) / MT);
   long target = (long)num_cus * (wt >= 10 ? occ : 3);
   long ksteps = (a.Mpix + 63) / 64;
@@ -1913,7 +1923,9 @@ DTM_API int dtm_conv_wgrad(const void* x, const void* dy, float* dw, const float
   if (wt >= 10) {
     a.in_shift = (const float*)zero_chunk();  // the zero DMA source
     dim3 grid((a.Kg + NT - 1) / NT, (a.K + MT - 1) / MT, splits);
-    if (wt == 11)
+    if (wt == 12)
+      hipLaunchKernelGGL((conv_wgrad_pipe_kernel<256, 256, 2, 2, 512>), grid, dim3(512), 0, (hipStream_t)stream, a);
+    else if (wt == 11)
       hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 128, 3>), grid, dim3(256), 0, (hipStream_t)stream, a);
     else
       hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 128, 2>), grid, dim3(256), 0, (hipStream_t)stream, a);

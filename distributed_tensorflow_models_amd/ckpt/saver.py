@@ -16,22 +16,30 @@ import threading
 import numpy as np
 import torch
 
-from .bundle import DT_BFLOAT16, BundleReader, write_bundle
+from .bundle import DT_BFLOAT16, BundleReader, partition_axis0, write_bundle
 
 
 class TFVar:
-    __slots__ = ("name", "tensor", "layout")
+    """One checkpoint variable.  ``partitions``: the variable lives under a partitioned variable_scope
+    (tf.fixed_size_partitioner(P, axis=0), reference alexnet/cifar10_alexnet_bsp.py:50-51,
+    vgg/cifar10_vgg_bsp.py:52-53) and is written as P axis-0 slices of its TF-layout tensor."""
+    __slots__ = ("name", "tensor", "layout", "partitions")
 
-    def __init__(self, name, tensor, layout=None):
-        self.name, self.tensor, self.layout = name, tensor, layout
+    def __init__(self, name, tensor, layout=None, partitions=None):
+        self.name, self.tensor, self.layout, self.partitions = name, tensor, layout, partitions
+
+    def _wrap(self, arr, tf_dtype=None):
+        if self.partitions and arr.ndim >= 1:
+            return partition_axis0(arr, self.partitions, tf_dtype)
+        return (arr, tf_dtype) if tf_dtype is not None else arr
 
     def export(self):
         t = self.tensor.detach()
         if self.layout == "KRSC->HWIO":
             t = t.permute(1, 2, 3, 0)
         if t.dtype == torch.bfloat16:
-            return (t.contiguous().view(torch.int16).cpu().numpy().view(np.uint16), DT_BFLOAT16)
-        return t.contiguous().cpu().numpy()
+            return self._wrap(t.contiguous().view(torch.int16).cpu().numpy().view(np.uint16), DT_BFLOAT16)
+        return self._wrap(t.contiguous().cpu().numpy())
 
     def load(self, arr):
         t = torch.from_numpy(np.require(arr, requirements="C"))
@@ -46,13 +54,18 @@ class TFVar:
             self.tensor.copy_(t.to(self.tensor.dtype))
 
 
-def model_variables(model, optimizer=None, global_step=None, include_slots=True, prefix=""):
-    """Collect TFVar records for a model built from models.layers (+ optimizer slots / EMA)."""
+def model_variables(model, optimizer=None, global_step=None, include_slots=True, prefix="", partitions=None,
+                    store=None):
+    """Collect TFVar records for a model built from models.layers (+ optimizer slots / EMA).
+
+    prefix: the trainer's variable_scope ('partitioned_space/', 'root/'); partitions: P of its
+    fixed_size_partitioner (slots of a partitioned variable are partitioned like it, as TF's
+    slot_creator does); store: an ASP/SSP ParamStore whose owner shards hold the optimizer slots."""
     from ..models.layers import tf_variables
     out = []
     by_param = {}
     for name, t, layout, _trainable in tf_variables(model):
-        v = TFVar(prefix + name, t, layout)
+        v = TFVar(prefix + name, t, layout, partitions)
         out.append(v)
         by_param[id(t)] = v
     if optimizer is not None and include_slots:
@@ -62,16 +75,28 @@ def model_variables(model, optimizer=None, global_step=None, include_slots=True,
                 continue
             st = optimizer.state[p]
             if optimizer.kind == "momentum":
-                out.append(TFVar(base.name + "/Momentum", st["s1"], base.layout))
+                out.append(TFVar(base.name + "/Momentum", st["s1"], base.layout, partitions))
             elif optimizer.kind == "rmsprop":
-                out.append(TFVar(base.name + "/RMSProp", st["s2"], base.layout))
-                out.append(TFVar(base.name + "/RMSProp_1", st["s1"], base.layout))
+                out.append(TFVar(base.name + "/RMSProp", st["s2"], base.layout, partitions))
+                out.append(TFVar(base.name + "/RMSProp_1", st["s1"], base.layout, partitions))
             if "ema" in st:
-                out.append(TFVar(base.name + "/ExponentialMovingAverage", st["ema"], base.layout))
+                out.append(TFVar(base.name + "/ExponentialMovingAverage", st["ema"], base.layout, partitions))
         for b, shadow in getattr(optimizer, "buffer_shadows", lambda: [])():
             base = by_param.get(id(b))
             if base is not None:
-                out.append(TFVar(base.name + "/ExponentialMovingAverage", shadow, base.layout))
+                out.append(TFVar(base.name + "/ExponentialMovingAverage", shadow, base.layout, partitions))
+    if store is not None and include_slots:
+        # ASP / SSP: the slots live in the owner shards (every rank maps every shard)
+        for i, p in enumerate(store.params):
+            base = by_param.get(id(p))
+            if base is None:
+                continue
+            sh = store.shards[i]
+            if store.kind == "momentum":
+                out.append(TFVar(base.name + "/Momentum", sh["s1"], base.layout, partitions))
+            elif store.kind == "rmsprop":
+                out.append(TFVar(base.name + "/RMSProp", sh["s2"], base.layout, partitions))
+                out.append(TFVar(base.name + "/RMSProp_1", sh["s1"], base.layout, partitions))
     if global_step is not None:
         out.append(TFVar("global_step", global_step))
     return out
@@ -177,11 +202,11 @@ class Saver:
         def arrays():
             from .bundle import DT_BFLOAT16
             out = {}
-            for name, h in host:
+            for v, (name, h) in zip(self.vars, host):
                 if h.dtype == torch.bfloat16:
-                    out[name] = (h.view(torch.int16).numpy().view(np.uint16), DT_BFLOAT16)
+                    out[name] = v._wrap(h.view(torch.int16).numpy().view(np.uint16), DT_BFLOAT16)
                 else:
-                    out[name] = h.numpy()
+                    out[name] = v._wrap(h.numpy())
             return out
         return arrays, ev
 

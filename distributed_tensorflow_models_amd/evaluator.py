@@ -60,15 +60,18 @@ def define_eval_flags(flags, preset):
         F.reset(name)
 
 
-def restore_for_eval(model, path, use_ema):
+def restore_for_eval(model, path, use_ema, prefix=""):
     """With ``use_ema`` every variable that has a shadow (trainables and BN moving statistics, as
     tf.train.ExponentialMovingAverage.variables_to_restore maps them; reference
     cnn/cifar10_eval.py:132-135, inception/inception_eval.py:157-160) is restored from
-    ``<v>/ExponentialMovingAverage``; everything else by name."""
+    ``<v>/ExponentialMovingAverage``; everything else by name.  ``prefix``: the trainer's variable
+    scope (the reference evals rebuild the net under it: alexnet/cifar10_alexnet_eval.py:125,
+    resnet/cifar10_resnet_eval.py:107); partitioned (sliced) checkpoint entries are reassembled."""
     from .ckpt.bundle import BundleReader
     names = set(BundleReader(path).names()) if use_ema else set()
     vs = []
     for name, t, layout, trainable in tf_variables(model):
+        name = prefix + name
         shadow = name + "/ExponentialMovingAverage"
         vs.append(TFVar(shadow if (use_ema and shadow in names) else name, t, layout))
     Saver(vs).restore(path)
@@ -135,7 +138,7 @@ def evaluate(preset, flags):
         if not path:
             print("No checkpoint file found", flush=True)
         elif path != last:
-            restore_for_eval(model, path, F.use_ema)
+            restore_for_eval(model, path, F.use_ema, prefix=cfg.get("scope_prefix", ""))
             gs = step_from_path(path)
             t0 = time.time()
             p1, r5 = eval_once(model, data, F.num_examples, F.batch_size, top5)

@@ -42,29 +42,36 @@ PRESETS = {
     "alexnet": dict(model="alexnet_v2", num_classes=10, dataset="cifar10", image_size=32, batch_size=128, lr=0.01,
                     lr_scale_workers=True, decay_epochs=350.0, decay_factor=0.1, optimizer="sgd", ema=0.9999,
                     wd_all=2e-4, max_steps=2000000, save_secs=60, log_style="standard", max_to_keep=5,
+                    scope_prefix="partitioned_space/", partitioned=True,
+                    global_step_name="partitioned_space/Variable",
                     train_dir="/home/ubuntu/cifar10/train", data_dir="/home/ubuntu/cifar10/data"),
     # vgg/cifar10_vgg_bsp.py:19-30,57-95 (factory vgg_16, 10 classes, is_training=False -> no dropout)
     "vgg": dict(model="vgg_16", num_classes=10, dataset="cifar10", image_size=32, batch_size=72, lr=0.01,
                 lr_scale_workers=True, decay_epochs=350.0, decay_factor=0.1, optimizer="sgd", ema=None,
                 wd_all=2e-4, max_steps=20000, save_secs=60, log_style="standard", max_to_keep=5,
                 model_kw=dict(fc_conv_padding="SAME", dropout_keep_prob=1.0, weight_decay=0.0),
+                scope_prefix="root/", partitioned=True, global_step_name="root/Variable",
                 train_dir="/home/ubuntu/cifar10_train", data_dir="/home/ubuntu/cifar10_data"),
     # vgg/cifar10_vgg_asp.py:20-31 + vgg/cifar10.py:338-391 (lr not scaled, var EMA)
     "vgg_asp": dict(model="vgg_16", num_classes=10, dataset="cifar10", image_size=32, batch_size=72, lr=0.01,
                     lr_scale_workers=False, decay_epochs=350.0, decay_factor=0.1, optimizer="sgd", ema=0.9999,
                     wd_all=2e-4, max_steps=20000, save_secs=60, log_style="standard", max_to_keep=5,
                     model_kw=dict(fc_conv_padding="SAME", dropout_keep_prob=1.0, weight_decay=0.0),
+                    scope_prefix="root/", partitioned=True, global_step_name="root/Variable",
                     train_dir="/home/ubuntu/cifar10_train", data_dir="/home/ubuntu/cifar10_data"),
     # resnet/cifar10_resnet_bsp.py:19-29,57-106 (CIFAR ResNet v2, resnet_size 32)
     "resnet": dict(model="cifar10_resnet_v2", num_classes=10, dataset="cifar10", image_size=32, batch_size=128,
                    lr=0.08, lr_scale_workers=True, decay_epochs=32.0, decay_factor=0.1, optimizer="sgd",
                    ema=0.9999, wd_all=2e-3, max_steps=10000000, save_secs=60, log_style="short", max_to_keep=1,
-                   train_accuracy_every=200, train_dir="/home/ubuntu/cifar10/train",
+                   train_accuracy_every=200, scope_prefix="root/", partitioned=True, global_step_name="Variable",
+                   train_dir="/home/ubuntu/cifar10/train",
                    data_dir="/home/ubuntu/cifar10/data"),
     # cifarnet/cifar10_cifarnet_bsp.py:20-32,56-91
     "cifarnet": dict(model="cifarnet", num_classes=10, dataset="cifar10", image_size=32, batch_size=512, lr=0.1,
                      lr_scale_workers=True, decay_epochs=20.0, decay_factor=0.1, optimizer="sgd", ema=0.9999,
                      wd_all=2e-4, max_steps=2000000, save_secs=60, log_style="standard", max_to_keep=5,
+                     scope_prefix="partitioned_space/", partitioned=True,
+                     global_step_name="partitioned_space/Variable",
                      train_dir="/home/ubuntu/cifar10/train", data_dir="/home/ubuntu/cifar10/data"),
     # inception/imagenet_inception_bsp.py:54-72,104-157 (old-slim Inception-v3, RMSProp, label smoothing)
     "inception": dict(model="inception_v3_slim_old", num_classes=1001, dataset="imagenet", image_size=299,
@@ -250,6 +257,10 @@ def train(preset, flags, default_mode="bsp"):
         shutil.rmtree(FLAGS.train_dir)
     pg.barrier()
     path = latest_checkpoint(FLAGS.train_dir) if os.path.isdir(FLAGS.train_dir) else None
+    # TF variable layout of the trainer: its variable_scope prefix and, for the
+    # partitioned scopes, P = len(ps_hosts) axis-0 slices per variable (tf.fixed_size_partitioner)
+    ckpt_kw = dict(prefix=cfg.get("scope_prefix", ""),
+                   partitions=max(1, len(ps_hosts)) if cfg.get("partitioned") else None)
     gstep = torch.zeros((), dtype=torch.int64)
     loss_fn = make_loss_fn(cfg.get("label_smoothing", 0.0), cfg.get("aux_weight", 0.4), FLAGS.batch_weight)
     store = clock = None
@@ -260,7 +271,7 @@ def train(preset, flags, default_mode="bsp"):
                             grad_comm_dtype=torch.bfloat16 if FLAGS.grad_comm_dtype == "bf16" else None,
                             timer=StepTimer() if (FLAGS.metrics_file and rank == 0 and not FLAGS.use_hipgraph)
                             else None, **opt_kw)
-        vars_ = model_variables(model, step_fn.opt, gstep)
+        vars_ = model_variables(model, step_fn.opt, gstep, **ckpt_kw)
         vars_[-1].name = cfg.get("global_step_name", "global_step")
         if path:
             Saver(vars_).restore(path)
@@ -275,7 +286,7 @@ def train(preset, flags, default_mode="bsp"):
         from .engine import prepare_compute_copies
         from .parallel.asp import ASPTrainStep, ParamStore
         from .parallel.ssp import StalenessClock
-        vars_ = model_variables(model, None, gstep)
+        vars_ = model_variables(model, None, gstep, **ckpt_kw)
         vars_[-1].name = cfg.get("global_step_name", "global_step")
         if path:  # owners initialise their shards from the restored replica
             Saver(vars_).restore(path)
@@ -284,6 +295,12 @@ def train(preset, flags, default_mode="bsp"):
                            opt_kw["epsilon"], run_id=os.environ.get("DTM_RUN_ID", "0"))
         if is_chief and int(gstep):
             store.set_global_step(int(gstep))
+        # optimizer slots live in the owner shards: checkpointed from there, restored into them
+        slot_vars = [v for v in model_variables(model, None, None, store=store, **ckpt_kw)
+                     if v.name.endswith(("/Momentum", "/RMSProp", "/RMSProp_1"))]
+        if path and is_chief and slot_vars:
+            Saver(slot_vars).restore(path, strict=False)
+        vars_ = vars_[:-1] + slot_vars + vars_[-1:]
         pg.barrier()
         if mode == "ssp":
             clock = StalenessClock(FLAGS.max_staleness, log_fn=logging.info)
@@ -295,7 +312,7 @@ def train(preset, flags, default_mode="bsp"):
     elif FLAGS.fine_tune_checkpoint:
         # model variables only (no slots, no global step: the schedule restarts), missing ones keep
         # their initialisation (e.g. a new logits layer)
-        ft = [v for v in model_variables(model, None, None)]
+        ft = [v for v in model_variables(model, None, None, prefix=ckpt_kw["prefix"])]
         missing = Saver(ft).restore(FLAGS.fine_tune_checkpoint, strict=False)
         logging.info("fine-tuning from %s (%d variables not in the checkpoint)", FLAGS.fine_tune_checkpoint,
                      len(missing or []))

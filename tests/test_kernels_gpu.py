@@ -210,9 +210,9 @@ def test_conv_pipelined_tiles_match_reference(tile, prologue, case):
     assert _rel(stats[0], yf.sum(0)) < 1e-3 and _rel(stats[1], yf.square().sum(0)) < 1e-3
 
 
-@pytest.mark.parametrize("tile", [10, 11])
+@pytest.mark.parametrize("tile", [10, 11, 12])
 @pytest.mark.parametrize("case", [(4, 15, 15, 64, 96, 3, 2), (2, 14, 14, 128, 256, 3, 1), (3, 7, 7, 512, 200, 1, 1),
-                                  (2, 9, 9, 24, 40, 3, 1), (5, 8, 8, 64, 64, 1, 1)])
+                                  (2, 9, 9, 24, 40, 3, 1), (5, 8, 8, 64, 64, 1, 1), (4, 9, 9, 256, 512, 3, 1)])
 def test_conv_wgrad_pipelined_tiles_match_reference(tile, case):
     """The pipelined LDS-DMA wgrad kernels (inverse transposed-read image mapping for the DMA slots,
     split-K slabs) against the fp32 reference, including K / R*S*C tails and empty splits."""

@@ -85,3 +85,46 @@ def test_launcher_dry_run():
     assert ev[1][2].endswith("imagenet_inception_eval")
     mod, extra = launcher.resolve("resnet", "asp")  # any model in any mode via --sync_mode
     assert mod == "cifar10_resnet_bsp" and extra == ["--sync_mode=asp"]
+
+
+@pytest.mark.parametrize("mod,scope,gs,probe", [
+    ("cifar10_alexnet_bsp", "partitioned_space/", "partitioned_space/Variable", "alexnet_v2/conv1/weights"),
+    ("cifar10_cifarnet_bsp", "partitioned_space/", "partitioned_space/Variable", "CifarNet/conv1/weights"),
+    ("cifar10_vgg_bsp", "root/", "root/Variable", "vgg_16/conv1/conv1_1/weights"),
+    ("cifar10_resnet_bsp", "root/", "Variable", None),
+])
+def test_trainer_scopes_and_partitioned_layout(tmp_path, mod, scope, gs, probe):
+    """SURVEY.md §5.4 name layout of the partitioned trainers: every variable under the trainer's
+    variable_scope, saved as fixed_size_partitioner(len(ps_hosts)) slices; eval restores it."""
+    from distributed_tensorflow_models_amd.ckpt.bundle import BundleReader
+    d = str(tmp_path / "train")
+    _run(mod, "--max_steps=1", "--batch_size=2", "--train_dir=" + d, "--data_dir=/nonexistent", "--synthetic_data",
+         "--ps_hosts=127.0.0.1:1,127.0.0.1:2")
+    r = BundleReader(os.path.join(d, "model.ckpt-1"))
+    names = r.names()
+    assert gs in names and int(r.get_tensor(gs)) == 1
+    assert all(n.startswith(scope) or n == gs for n in names), names[:5]
+    trainables = [n for n in names if n != gs and not n.endswith("ExponentialMovingAverage")]
+    assert trainables and all(n in r.sliced for n in trainables if r.get_variable_to_shape_map()[n])
+    if probe:
+        assert scope + probe in names
+        assert r.get_tensor(scope + probe).shape == tuple(r.get_variable_to_shape_map()[scope + probe])
+    else:  # tf.layers auto-names under root/ (resnet/resnet_model.py)
+        assert any(n.startswith("root/") and "batch_normalization" in n and "moving_mean" in n for n in names), names
+    evm = mod.replace("_bsp", "_eval")
+    ev = _run(evm, "--checkpoint_dir=" + d, "--eval_dir=" + str(tmp_path / "eval"), "--run_once",
+              "--num_examples=4", "--batch_size=2", "--data_dir=/nonexistent", "--synthetic_data")
+    assert "precision @ 1" in ev
+
+
+def test_asp_checkpoint_keeps_optimizer_slots(tmp_path):
+    """ASP: the momentum / RMSProp slots live in the owner shards and are checkpointed from there."""
+    from distributed_tensorflow_models_amd.ckpt.bundle import BundleReader
+    d = str(tmp_path / "train")
+    _run("imagenet_inception_asp", "--max_steps=1", "--batch_size=1", "--train_dir=" + d, "--data_dir=/nonexistent",
+         "--synthetic_data")
+    r = BundleReader(os.path.join(d, "model.ckpt-1"))
+    names = r.names()
+    assert "conv0/weights/RMSProp" in names and "conv0/weights/RMSProp_1" in names
+    ms = r.get_tensor("conv0/weights/RMSProp")
+    assert not np.allclose(ms, 1.0)  # ms slot (init 1.0) was updated by the push, and saved from the shard
