@@ -1684,12 +1684,17 @@ static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
     if (tiles >= 150 && !(tiles > 600 && a.Kg <= 256 && !stats)) id = 40;
   }
   if (id == -1 && !a.in_scale && a.Kg >= 1024) id = 21;  // (-3: the policy without it, for A/B runs)
+  // 64-output-channel 3x3 layers (56x56 bottleneck conv2, fwd and dgrad): the 2-slot pipelined 128x64 tile
+  // (profiles/r2_conv_tiles_k64.txt: -4 % vs the register-staged single-buffer tile)
+  if (id == -1 && !a.in_scale && a.K <= 64 && a.R * a.S > 1 && a.K % 64 == 0) id = 26;
   if (id < 0) id = a.K <= 64 ? g_k64_tile : ((a.M <= 16384 && a.Kg >= 2048) ? 0 : 4);
   // LDS-DMA variants (10-12, opt-in) need an operand without the prologue affine
   if (id >= 10 && id < 20 && a.in_scale) id = a.K <= 64 ? 3 : 4;
   // pipelined LDS-DMA variants (20-23) stage the prologue affine in LDS: C <= 512
-  if (id >= 20 && a.in_scale && a.C > 512) id = 0;
+  if (id >= 20 && id < 30 && a.in_scale && a.C > 512) id = 0;
   if (id >= 20 && id <= 23) return {id, 128, 2};
+  if (id == 24 || id == 25) return {id, 256, 2};  // 256 x 64 pipelined (waves 2x2 of 128x32), 2 / 3 slots
+  if (id == 26) return {id, 128, 2};              // 128 x 64 pipelined, 2 slots
   // 8-wave 256-pixel tiles (no prologue): 40 = 256x256 (waves 2x4), 41 = 256x128 3-slot (4x2),
   // 42 = 256x128 2-slot, 43 = 256x256 (waves 4x2)
   if (id >= 40 && id <= 43 && a.in_scale) id = 0;
@@ -1726,6 +1731,9 @@ static void dispatch_ud(const ConvNTArgs& a, const TileCfg& t, hipStream_t st) {
   else if (t.id == 21) launch_pipe<128, 128, 2, UD>(a, st);
   else if (t.id == 22) launch_pipe<128, 128, 4, UD>(a, st);
   else if (t.id == 23) launch_pipe<128, 64, 3, UD>(a, st);
+  else if (t.id == 24) launch_pipe<256, 64, 2, UD>(a, st);
+  else if (t.id == 25) launch_pipe<256, 64, 3, UD>(a, st);
+  else if (t.id == 26) launch_pipe<128, 64, 2, UD>(a, st);
   else if (t.id == 40) launch_w8<256, 256, 2, 2, UD>(a, st);
   else if (t.id == 41) launch_w8<256, 128, 4, 3, UD>(a, st);
   else if (t.id == 42) launch_w8<256, 128, 4, 2, UD>(a, st);
@@ -1902,9 +1910,9 @@ DTM_API int dtm_conv_wgrad(const void* x, const void* dy, float* dw, const float
     if (g_tile_w8 && d->K >= 256 && a.Kg >= 1024 && (d->R * d->S > 1 || d->K >= 1024)) wt = 12;
   }
   if (wt >= 10 && in_scale) wt = d->K <= 64 ? 1 : 0;  // the pipelined kernels have no input prologue
-  const bool small_m = (wt == 1 || wt == 2);
+  const bool small_m = (wt == 1 || wt == 2 || wt == 13 || wt == 14 || wt == 15);
   const bool big = wt == 12;  // 8-wave 256x256 (one block per CU)
-  const int MT = small_m ? 64 : (big ? 256 : 128), NT = big ? 256 : 128;
+  const int MT = small_m ? 64 : (big ? 256 : 128), NT = (big || wt == 13 || wt == 14) ? 256 : 128;
   if (big) occ = (wenv == 12 && g_wgrad_occ != 4) ? g_wgrad_occ : 1;  // (sweeps: WTILES=12:<occ>)
   long tiles = (long)((a.Kg + NT - 1) / NT) * ((a.K + MT - 1) / MT);
   long target = (long)num_cus * (wt >= 10 ? occ : 3);
@@ -1925,6 +1933,12 @@ DTM_API int dtm_conv_wgrad(const void* x, const void* dy, float* dw, const float
     dim3 grid((a.Kg + NT - 1) / NT, (a.K + MT - 1) / MT, splits);
     if (wt == 12)
       hipLaunchKernelGGL((conv_wgrad_pipe_kernel<256, 256, 2, 2, 512>), grid, dim3(512), 0, (hipStream_t)stream, a);
+    else if (wt == 13)
+      hipLaunchKernelGGL((conv_wgrad_pipe_kernel<64, 256, 2, 1, 256>), grid, dim3(256), 0, (hipStream_t)stream, a);
+    else if (wt == 14)
+      hipLaunchKernelGGL((conv_wgrad_pipe_kernel<64, 256, 3, 1, 256>), grid, dim3(256), 0, (hipStream_t)stream, a);
+    else if (wt == 15)
+      hipLaunchKernelGGL((conv_wgrad_pipe_kernel<64, 128, 2>), grid, dim3(256), 0, (hipStream_t)stream, a);
     else if (wt == 11)
       hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 128, 3>), grid, dim3(256), 0, (hipStream_t)stream, a);
     else

@@ -160,7 +160,7 @@ def test_image_augment_kernel_matches_oracle(distort, size):
     assert got.is_cuda and _rel(got.cpu(), ref_out) < 1e-4
 
 
-@pytest.mark.parametrize("tile", [20, 21, 22, 23, 30, 31, 40, 41, 42, 43])
+@pytest.mark.parametrize("tile", [20, 21, 22, 23, 24, 25, 26, 30, 31, 40, 41, 42, 43])
 @pytest.mark.parametrize("prologue", [False, True])
 @pytest.mark.parametrize("case", [(4, 15, 15, 64, 96, 3, 2), (2, 14, 14, 128, 256, 3, 1), (3, 7, 7, 512, 200, 1, 1),
                                   (2, 9, 9, 24, 40, 3, 1), (4, 12, 12, 64, 256, 1, 1), (3, 7, 7, 128, 96, 1, 1),
@@ -210,7 +210,7 @@ def test_conv_pipelined_tiles_match_reference(tile, prologue, case):
     assert _rel(stats[0], yf.sum(0)) < 1e-3 and _rel(stats[1], yf.square().sum(0)) < 1e-3
 
 
-@pytest.mark.parametrize("tile", [10, 11, 12])
+@pytest.mark.parametrize("tile", [10, 11, 12, 13, 14, 15])
 @pytest.mark.parametrize("case", [(4, 15, 15, 64, 96, 3, 2), (2, 14, 14, 128, 256, 3, 1), (3, 7, 7, 512, 200, 1, 1),
                                   (2, 9, 9, 24, 40, 3, 1), (5, 8, 8, 64, 64, 1, 1), (4, 9, 9, 256, 512, 3, 1)])
 def test_conv_wgrad_pipelined_tiles_match_reference(tile, case):
@@ -243,7 +243,7 @@ def test_conv_wgrad_pipelined_tiles_match_reference(tile, case):
     assert _rel(dw, wr.grad) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [10, 11, 12])
+@pytest.mark.parametrize("tile", [10, 11, 12, 13, 14, 15])
 def test_conv_lds_dma_tiles_match_default(tile):
     """The opt-in LDS-DMA conv kernels (DTM_CONV_TILE=10..12) give the default kernel's results
     (fwd with padding, stride-2 dgrad through the dilated path)."""
