@@ -12,6 +12,7 @@ from .ops import fused as _fused
 from .ops import nn as F
 from .ops.optim import FusedOptimizer
 from .parallel.bsp import BSPDataParallel
+from .utils.profiler import range_pop, range_push, roctx
 
 
 def prepare_compute_copies(model):
@@ -80,14 +81,18 @@ class TrainStep:
             _fused.arena.begin_step(images.device)
             _elementwise.advance_seed_offset(images.device)  # fresh dropout masks, replay included
         try:
-            out = self.model(images, training=True)
-            loss = self.loss_fn(out, labels)
+            with roctx("forward"):
+                out = self.model(images, training=True)
+            with roctx("loss"):
+                loss = self.loss_fn(out, labels)
             self._mark("fwd")
-            loss.backward()
+            with roctx("backward"):  # bucket all-reduces are issued (own ranges) from the grad hooks
+                loss.backward()
             self._mark("bwd")
         finally:
             _fused.arena.end_step()
-        self.dp.finish()
+        with roctx("allreduce_wait"):
+            self.dp.finish()
         self._mark("allreduce")
         skip = None
         if self.nan_guard:
@@ -96,7 +101,8 @@ class TrainStep:
             flat = self.dp.flat
             if flat.is_cuda:
                 skip = torch.zeros(1, device=flat.device, dtype=torch.int32)
-                _lib.lib().dtm_check_finite(_lib.ptr(flat), flat.numel(), _lib.ptr(skip), _lib.stream_ptr())
+                with roctx("nan_guard"):
+                    _lib.lib().dtm_check_finite(_lib.ptr(flat), flat.numel(), _lib.ptr(skip), _lib.stream_ptr())
             else:
                 skip = torch.tensor([0 if bool(torch.isfinite(flat).all()) else 1], dtype=torch.int32)
             self.last_skip = skip
@@ -105,12 +111,13 @@ class TrainStep:
     def __call__(self, images, labels):
         if self.use_graph and images.is_cuda:
             return self._graph_step(images, labels)
-        rng = _range_push("train_step")
+        rng = range_push("train_step")
         loss, skip = self._forward_backward(images, labels)
-        self.opt.step(self.current_lr(), grad_scale=self.dp.grad_scale, skip_flag=skip)
+        with roctx("optimizer"):
+            self.opt.step(self.current_lr(), grad_scale=self.dp.grad_scale, skip_flag=skip)
         self._mark("optimizer")
         self.global_step += 1
-        _range_pop(rng)
+        range_pop(rng)
         return loss
 
     # ---- hipGraph path -----------------------------------------------------------------------
@@ -164,22 +171,3 @@ class TrainStep:
             self.skipped += 1
             return True
         return False
-
-
-def _range_push(name):
-    """roctx range (torch.cuda.nvtx maps to roctx on ROCm builds); no-op when unavailable."""
-    try:
-        if torch.cuda.is_available():
-            torch.cuda.nvtx.range_push(name)
-            return True
-    except Exception:
-        pass
-    return False
-
-
-def _range_pop(active):
-    if active:
-        try:
-            torch.cuda.nvtx.range_pop()
-        except Exception:
-            pass

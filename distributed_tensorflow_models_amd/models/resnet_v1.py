@@ -35,14 +35,17 @@ def subsample(x, factor, lazy=False):
 
 
 def conv2d_same_padding(kernel, stride, rate=1):
+    """resnet_utils.conv2d_same (reference vgg/nets/resnet_utils.py:77-122): stride 1 -> 'SAME';
+    else explicit [pad_beg, pad_end] (pad_end = pad_beg + 1 for an even effective kernel) + VALID."""
     if stride == 1:
         return "SAME"
     keff = kernel + (kernel - 1) * (rate - 1)
     total = keff - 1
     beg = total // 2
-    if total - beg != beg:
-        raise NotImplementedError("even kernel conv2d_same")
-    return (beg, beg)
+    end = total - beg
+    if end == beg:
+        return (beg, beg)
+    return ((beg, end), (beg, end))
 
 
 class BottleneckV1(Layer):

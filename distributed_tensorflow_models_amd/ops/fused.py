@@ -430,7 +430,8 @@ def _stem_eligible(x, w, stride, padding):
         return False
     K, R, S, C = w.shape
     st = stride if isinstance(stride, int) else stride[0]
-    if isinstance(padding, str) or not isinstance(padding, (tuple, list)) or padding[0] != padding[1]:
+    if isinstance(padding, str) or not isinstance(padding, (tuple, list)) or padding[0] != padding[1] or \
+            isinstance(padding[0], (tuple, list)):
         return False
     return C <= 4 and x.shape[-1] == C and st == 2 and S <= 7 and K % 4 == 0
 

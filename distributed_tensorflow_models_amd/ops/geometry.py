@@ -42,8 +42,21 @@ def same_pads(size, k, stride, dilation=1):
     return out, total // 2, total - total // 2
 
 
+def explicit_pads(padding):
+    """int | (ph, pw) symmetric | ((top, bottom), (left, right)) -> (top, bottom, left, right).
+    The asymmetric form is resnet_utils.conv2d_same with an even kernel (tf.pad [beg, end] then VALID;
+    reference vgg/nets/resnet_utils.py:77-122): the extra row / column goes bottom / right."""
+    if isinstance(padding, (tuple, list)) and len(padding) == 2 and isinstance(padding[0], (tuple, list)):
+        (pt, pb), (pl, pr) = padding
+        return int(pt), int(pb), int(pl), int(pr)
+    ph, pw = _pair(padding)
+    return ph, ph, pw, pw
+
+
 def conv_geom(x_shape, k_shape, stride=1, padding="SAME", dilation=1):
-    """x_shape NHWC, k_shape (K, R, S, C). padding: 'SAME' | 'VALID' | int | (ph, pw) symmetric."""
+    """x_shape NHWC, k_shape (K, R, S, C). padding: 'SAME' | 'VALID' | int | (ph, pw) symmetric |
+    ((top, bottom), (left, right)) explicit.  The kernels take the top/left pad and the output size;
+    bottom/right padding is the zero fill of out-of-range taps."""
     N, H, W, C = x_shape
     K, R, S, C2 = k_shape
     if C2 != C:
@@ -63,11 +76,9 @@ def conv_geom(x_shape, k_shape, stride=1, padding="SAME", dilation=1):
         else:
             raise ValueError(padding)
     else:
-        ph, pw = _pair(padding)
-        pt = pb = ph
-        pl = pr = pw
-        P = (H + 2 * ph - ((R - 1) * dilation + 1)) // sh + 1
-        Q = (W + 2 * pw - ((S - 1) * dilation + 1)) // sw + 1
+        pt, pb, pl, pr = explicit_pads(padding)
+        P = (H + pt + pb - ((R - 1) * dilation + 1)) // sh + 1
+        Q = (W + pl + pr - ((S - 1) * dilation + 1)) // sw + 1
     if P <= 0 or Q <= 0:
         raise ValueError("non-positive conv output %dx%d for input %dx%d kernel %dx%d" % (P, Q, H, W, R, S))
     return ConvGeom(N, H, W, C, K, R, S, P, Q, sh, pt, pl, pb, pr, dilation)

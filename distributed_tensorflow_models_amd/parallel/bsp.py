@@ -26,6 +26,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import nn as opsnn
+from ..utils.profiler import roctx
 
 
 class BSPDataParallel:
@@ -118,10 +119,11 @@ class BSPDataParallel:
             return
         s, e = self.buckets[bi]
         buf = self.flat[s:e]
-        if self.comm is not None:
-            buf = self.comm[s:e]
-            buf.copy_(self.flat[s:e])
-        self._works.append((bi, dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)))
+        with roctx("allreduce_bucket_%d" % bi):
+            if self.comm is not None:
+                buf = self.comm[s:e]
+                buf.copy_(self.flat[s:e])
+            self._works.append((bi, dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)))
 
     def finish(self):
         """Launch any bucket not yet reduced (unused params / no overlap) and make the current

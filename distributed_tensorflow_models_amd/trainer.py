@@ -119,7 +119,7 @@ def define_common_flags(flags, preset):
             ("protocol", S, "grpc", "accepted for compatibility; transport is RCCL/gloo"),
             ("save_interval_secs", I, p["save_secs"], "Save interval seconds."),
             ("save_every_steps", I, 0, "also checkpoint every N global steps (0 = time-based only)"),
-            ("save_summaries_secs", I, 180, "(unused, as in the reference)"),
+            ("save_summaries_secs", I, 180, "train-side TensorBoard scalars at most this often (0 = off)"),
             ("initial_learning_rate", Fl, p["lr"], "Initial learning rate."),
             ("num_epochs_per_decay", Fl, p["decay_epochs"], "Epochs after which learning rate decays."),
             ("learning_rate_decay_factor", Fl, p["decay_factor"], "Learning rate decay factor."),
@@ -331,9 +331,17 @@ def train(preset, flags, default_mode="bsp"):
         fault = (int(parts[0]), int(parts[1]), parts[2] if len(parts) > 2 else "exit")
     heartbeat = Heartbeat(rank)
 
+    # training-side TensorBoard scalars (the graph-side summaries the reference defines, e.g.
+    # cnn/cifar10.py:309-335,361: learning_rate, total_loss (raw) and its 0.9 moving average), written
+    # to train_dir by the chief at most every --save_summaries_secs
+    from .utils.tb import SummaryWriter
+    tbw = SummaryWriter(FLAGS.train_dir) if (is_chief and FLAGS.save_summaries_secs > 0) else None
+    loss_avg, t_summary = None, None
+
     # ---- loop (reference hot loop) ------------------------------------------------
     step = start if mode == "bsp" else 0
     loss_v = float("nan")
+    t_log, n_since = time.time(), 0
     while step < FLAGS.max_steps:
         if fault and fault[0] == rank and fault[1] == step:
             if fault[2] == "hang":
@@ -344,25 +352,40 @@ def train(preset, flags, default_mode="bsp"):
             os._exit(17)
         tracer.step(step)
         images, labels = data.next_batch()
-        t0 = time.time()
         if mode == "bsp":
             loss = step_fn(images, labels)
             gs = step_fn.global_step
         else:
             loss, gs = step_fn(images, labels)
-        need_log = (step % max(FLAGS.log_every, 1) == 0) or cfg.get("nan_guard")
+        n_since += 1
+        log_now = step % max(FLAGS.log_every, 1) == 0
+        need_log = log_now or cfg.get("nan_guard")
         if need_log:
             loss_v = float(loss)
-        if device.type == "cuda":
-            torch.cuda.synchronize()
-        dt = time.time() - t0
+        dt = 0.0
+        if log_now:
+            # the device is drained only on logged steps (the time is averaged over the steps since the
+            # last log line); the other steps leave the host free to run ahead of the GPU
+            if device.type == "cuda":
+                torch.cuda.synchronize()
+            now = time.time()
+            dt = (now - t_log) / n_since
+            t_log, n_since = now, 0
         if cfg.get("nan_guard") and math.isnan(loss_v):  # imagenet_inception_bsp.py:191
             raise FloatingPointError("Model diverged with loss = NaN")
         if mode == "bsp" and need_log and step_fn.poll_skipped():
             logging.warning("step %d: non-finite gradients, update skipped (%d so far)", step, step_fn.skipped)
         gstep.fill_(gs)
-        if step % max(FLAGS.log_every, 1) == 0:
+        if log_now:
             print(format_step(cfg["log_style"], step, gs, loss_v, B / max(dt, 1e-9), dt), flush=True)
+            if tbw is not None and loss_v == loss_v:
+                loss_avg = loss_v if loss_avg is None else 0.9 * loss_avg + 0.1 * loss_v
+                if t_summary is None or time.time() - t_summary >= FLAGS.save_summaries_secs:
+                    t_summary = time.time()
+                    tbw.add_scalar("learning_rate", float(sched(gs)), gs)
+                    tbw.add_scalar("total_loss (raw)", loss_v, gs)
+                    tbw.add_scalar("total_loss", loss_avg, gs)
+                    tbw.add_scalar("images_per_sec", world * B / max(dt, 1e-9), gs)
             extra = step_fn.timer.sections() if (mode == "bsp" and step_fn.timer is not None) else {}
             if device.type == "cuda" and metrics.f is not None:
                 extra["max_mem_gb"] = torch.cuda.max_memory_allocated(device) / 2 ** 30
@@ -384,6 +407,8 @@ def train(preset, flags, default_mode="bsp"):
         store.pull()
     sv.maybe_save(int(gstep), force=True)
     metrics.close()
+    if tbw is not None:
+        tbw.close()
     if store is not None:  # owners keep their shards alive until every worker is done with them
         from .parallel.asp import wait_all_done
         wait_all_done(store.store, world, store.run_id)

@@ -1,8 +1,39 @@
 """--trace_steps a:b -> torch.profiler (roctracer on ROCm) Chrome trace per rank; the reference
 collected FULL_TRACE RunMetadata every step and never exported it."""
+import contextlib
 import os
 
 import torch
+
+
+def range_push(name):
+    """roctx range push (torch.cuda.nvtx maps to roctx on ROCm builds); False when unavailable.
+    Shows up in rocprofv3 --marker-trace and in the torch profiler timeline."""
+    try:
+        if torch.cuda.is_available():
+            torch.cuda.nvtx.range_push(name)
+            return True
+    except Exception:
+        pass
+    return False
+
+
+def range_pop(active):
+    if active:
+        try:
+            torch.cuda.nvtx.range_pop()
+        except Exception:
+            pass
+
+
+@contextlib.contextmanager
+def roctx(name):
+    """Per-phase roctx range (fwd, loss, bwd, allreduce bucket issue / wait, nan guard, optimizer)."""
+    a = range_push(name)
+    try:
+        yield
+    finally:
+        range_pop(a)
 
 
 class StepTracer:

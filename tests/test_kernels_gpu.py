@@ -32,6 +32,7 @@ CONV_CASES = [
     (2, 8, 8, 448, 384, (3, 1), 1, "SAME"),
     (2, 35, 35, 288, 384, (3, 3), 2, "VALID"),    # mixed_17x17x768a 3x3/2 VALID
     (2, 17, 17, 192, 320, (3, 3), 2, "VALID"),    # mixed_8x8x1280a
+    (2, 9, 9, 64, 64, (4, 4), 2, ((1, 2), (1, 2))),  # even-kernel conv2d_same (resnet_utils.py:77-122)
 ]
 
 

@@ -228,3 +228,24 @@ def test_resnet_v1_50_output_stride_16_shapes():
     assert list(out.shape) == [1, 21, 21, 2048]
     assert [list(ep["resnet_v1_50/block%d" % i].shape)[1:3] for i in range(1, 5)] == [[41, 41], [21, 21],
                                                                                      [21, 21], [21, 21]]
+
+
+@pytest.mark.parametrize("kernel,stride,rate,H", [(4, 2, 1, 9), (2, 2, 1, 8), (4, 2, 2, 11), (3, 2, 1, 10)])
+def test_conv2d_same_even_kernel(kernel, stride, rate, H):
+    """resnet_utils.conv2d_same for an even effective kernel: tf.pad [beg, end] (end = beg + 1) then
+    VALID (reference vgg/nets/resnet_utils.py:77-122, ResnetUtilsTest.testConv2DSameEven's point)."""
+    import torch.nn.functional as tF
+    from distributed_tensorflow_models_amd.models.resnet_v1 import conv2d_same_padding
+    from distributed_tensorflow_models_amd.ops import reference as ref
+    torch.manual_seed(0)
+    x = torch.randn(2, H, H, 8)
+    w = torch.randn(16, kernel, kernel, 8)
+    pad = conv2d_same_padding(kernel, stride, rate)
+    keff = kernel + (kernel - 1) * (rate - 1)
+    beg = (keff - 1) // 2
+    end = keff - 1 - beg
+    got = ref.conv2d(x, w, None, stride, pad, False, rate)
+    xp = tF.pad(x, (0, 0, beg, end, beg, end))
+    want = ref.conv2d(xp, w, None, stride, "VALID", False, rate)
+    assert got.shape == want.shape
+    torch.testing.assert_close(got, want)

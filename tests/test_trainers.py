@@ -128,3 +128,16 @@ def test_asp_checkpoint_keeps_optimizer_slots(tmp_path):
     assert "conv0/weights/RMSProp" in names and "conv0/weights/RMSProp_1" in names
     ms = r.get_tensor("conv0/weights/RMSProp")
     assert not np.allclose(ms, 1.0)  # ms slot (init 1.0) was updated by the push, and saved from the shard
+
+
+def test_training_tb_scalars(tmp_path):
+    """The chief writes train-side TensorBoard scalars (learning_rate, total_loss (raw), its 0.9
+    moving average total_loss) into train_dir (reference cnn/cifar10.py:309-335,361)."""
+    d = str(tmp_path / "train")
+    _run("cifar10_cnn_bsp", "--max_steps=3", "--batch_size=8", "--train_dir=" + d, "--data_dir=/nonexistent",
+         "--synthetic_data")
+    ev = [f for f in os.listdir(d) if f.startswith("events.out.tfevents")]
+    assert ev
+    blob = open(os.path.join(d, ev[0]), "rb").read()
+    for tag in (b"learning_rate", b"total_loss (raw)", b"total_loss", b"images_per_sec"):
+        assert tag in blob
