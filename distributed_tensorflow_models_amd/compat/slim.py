@@ -457,27 +457,21 @@ def instance_norm(inputs, center=True, scale=True, epsilon=1e-6, activation_fn=N
             if center else None
         gamma = variable("gamma", (C,), initializer=pi.get("gamma", ("constant", 1.0)), trainable=trainable) \
             if scale else None
-    xf = x.float()
-    mean = xf.mean(dim=(1, 2), keepdim=True)
-    var = xf.var(dim=(1, 2), keepdim=True, unbiased=False)
-    y = (xf - mean) * torch.rsqrt(var + epsilon)
-    if gamma is not None:
-        y = y * gamma
-    if beta is not None:
-        y = y + beta
-    return _act(y.to(x.dtype), activation_fn)
+    from ..ops.activation import instance_norm as _inorm
+    fuse_relu = activation_fn in (torch.relu, E.relu, "relu")
+    y = _inorm(x, gamma, beta, epsilon, relu=fuse_relu)  # HIP kernel on CUDA (activation.hip)
+    return y if fuse_relu else _act(y, activation_fn)
 
 
 def leaky_relu(x, alpha=0.2):
-    x = as_tensor(x)
-    return torch.nn.functional.leaky_relu(x, alpha)
+    from ..ops.activation import leaky_relu as _lrelu
+    return _lrelu(as_tensor(x), alpha)
 
 
 def reflect_pad(x, top, bottom, left, right):
-    """tf.pad(..., 'REFLECT') on NHWC."""
-    x = as_tensor(x)
-    y = torch.nn.functional.pad(x.permute(0, 3, 1, 2), (left, right, top, bottom), mode="reflect")
-    return y.permute(0, 2, 3, 1).contiguous()
+    """tf.pad(..., 'REFLECT') on NHWC (HIP gather kernel on CUDA, deterministic gather backward)."""
+    from ..ops.activation import reflect_pad as _rpad
+    return _rpad(as_tensor(x), top, bottom, left, right)
 
 
 @add_arg_scope

@@ -112,13 +112,15 @@ def apply_activation(x, act):
     if act == "relu6":
         return E.relu6(x)
     if act == "leaky_relu":
-        return torch.nn.functional.leaky_relu(x, 0.2)
+        from ..ops.activation import leaky_relu
+        return leaky_relu(x, 0.2)
     if act == "tanh":
         return torch.tanh(x)
     if act == "sigmoid":
         return torch.sigmoid(x)
     if act == "elu":
-        return torch.nn.functional.elu(x)
+        from ..ops.activation import elu
+        return elu(x)
     raise ValueError(act)
 
 

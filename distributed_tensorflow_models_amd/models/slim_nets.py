@@ -17,7 +17,8 @@ relu = torch.relu
 
 
 def _relu6(x):
-    return torch.clamp(as_tensor(x), 0.0, 6.0)
+    from ..ops.activation import relu6
+    return relu6(as_tensor(x))
 
 
 def _cat(ts):

@@ -33,6 +33,12 @@ _F = ctypes.c_float
 
 _SIGS = {
     "dtm_conv_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, ctypes.POINTER(ConvDesc), _P]),
+    "dtm_act_fwd": (_I, [_P, _P, _L, _I, _F, _I, _P]),
+    "dtm_act_bwd": (_I, [_P, _P, _P, _L, _I, _F, _I, _P]),
+    "dtm_instnorm_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _I, _P]),
+    "dtm_instnorm_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "dtm_reflect_pad": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "dtm_reflect_pad_bwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "dtm_conv_dgrad": (_I, [_P, _P, _P, ctypes.POINTER(ConvDesc), _P]),
     "dtm_conv_dgrad_ex": (_I, [_P, _P, _P, ctypes.POINTER(ConvDesc), _P, _I, _P, _P, _P, _I, _P]),
     "dtm_conv_wgrad": (_I, [_P, _P, _P, _P, _P, ctypes.POINTER(ConvDesc), _I, _P]),
