@@ -653,8 +653,102 @@ def softmax_cross_entropy(logits, labels, smoothing=0.0, row_weight=None):
 
 
 # ---------------------------------------------------------------------------------------------
-# fully connected (plain library GEMM on hipBLASLt; fp32 master + bf16 compute copy)
+# fully connected (reference cnn/cifar10.py:262-279 local3/local4,
+# inception/slim/ops.py:305,317 logits / aux FC).  An FC layer IS a 1x1 convolution over a 1x1
+# image, so it runs on the hand-written MFMA implicit-GEMM kernels (conv_igemm.hip) with the bias and
+# ReLU in the GEMM epilogue:  forward  y[B][N]  = conv(x [B,1,1,Kin], W^T [N][Kin])  (the dgrad copy of
+#                            the [Kin][N] TF-layout weight, refreshed with the conv weights);
+#                            dgrad    dx[B][Kin] = conv(dy [B,1,1,N], W [Kin][N]);
+#                            wgrad    dW[Kin][N] = conv_wgrad with the roles of x / dy swapped.
+# Output widths that are not a multiple of 8 (logits: 10, 1001) run on zero-padded copies.
+def _pad8(n):
+    return (n + 7) // 8 * 8
+
+
+def _fc_desc(B, C, K):
+    return _lib.ConvDesc(B, 1, 1, C, K, 1, 1, 1, 1, 1, 0, 0, 0)
+
+
+class _LinearHipFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, relu):
+        L = _lib.lib()
+        s = _lib.stream_ptr()
+        Kin, N = w.shape
+        Np = _pad8(N)
+        B = x.shape[0]
+        x16 = x.to(torch.bfloat16).contiguous()
+        if Np == N:
+            wt = weight_flipped(w, Kin, 1, 1, N).view(N, Kin)
+            bias = b.float().contiguous() if b is not None else None
+        else:
+            wt = torch.zeros((Np, Kin), device=x.device, dtype=torch.bfloat16)
+            wt[:N].copy_(weight_bf16(w).t())
+            bias = None
+            if b is not None:
+                bias = torch.zeros(Np, device=x.device, dtype=torch.float32)
+                bias[:N].copy_(b)
+        y = torch.empty((B, Np), device=x.device, dtype=torch.bfloat16)
+        d = _fc_desc(B, Kin, Np)
+        _check(L.dtm_conv_fwd(_lib.ptr(x16), _lib.ptr(wt), _lib.ptr(y), None, _lib.ptr(bias), None, None, int(relu),
+                              ctypes.byref(d), s), "fc_fwd")
+        if Np != N:
+            y = y[:, :N].contiguous()
+        ctx.save_for_backward(x16, w, y if relu else None)
+        ctx.b, ctx.relu = b, relu
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L = _lib.lib()
+        s = _lib.stream_ptr()
+        x16, w, y = ctx.saved_tensors
+        Kin, N = w.shape
+        Np = _pad8(N)
+        B = x16.shape[0]
+        gb = None
+        dy = dy.contiguous()
+        if ctx.relu and ctx.b is not None and _relu_bias_bwd_ok(dy):
+            dy, gb = _relu_bias_bwd(dy, y)  # mask + bias-gradient sums in one HIP pass
+        elif ctx.relu:
+            dy = torch.where(y > 0, dy, torch.zeros((), dtype=dy.dtype, device=dy.device))
+        dy16 = dy.to(torch.bfloat16).contiguous()
+        if Np != N:
+            dyp = torch.zeros((B, Np), device=dy.device, dtype=torch.bfloat16)
+            dyp[:, :N].copy_(dy16)
+        else:
+            dyp = dy16
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if Np == N:
+                w16 = weight_bf16(w)
+            else:
+                w16 = torch.zeros((Kin, Np), device=dy.device, dtype=torch.bfloat16)
+                w16[:, :N].copy_(weight_bf16(w))
+            dx = torch.empty((B, Kin), device=dy.device, dtype=torch.bfloat16)
+            d = _fc_desc(B, Np, Kin)
+            _check(L.dtm_conv_fwd(_lib.ptr(dyp), _lib.ptr(w16), _lib.ptr(dx), None, None, None, None, 0,
+                                  ctypes.byref(d), s), "fc_dgrad")
+        dw = None
+        if ctx.needs_input_grad[1]:
+            mg = getattr(w, "main_grad", None)
+            direct = mg is not None and Np == N
+            target = mg if direct else torch.zeros((Kin, Np), device=dy.device, dtype=torch.float32)
+            d = _fc_desc(B, Np, Kin)  # "input" dy (C = Np), "output gradient" x (K = Kin): dW[Kin][Np]
+            _check(L.dtm_conv_wgrad(_lib.ptr(dyp), _lib.ptr(x16), _lib.ptr(target), None, None, ctypes.byref(d),
+                                    _lib.num_cus(), s), "fc_wgrad")
+            if direct:
+                _notify(w)
+            else:
+                dw = _accum_param_grad(w, target[:, :N] if Np != N else target)
+        db = None
+        if ctx.b is not None and ctx.needs_input_grad[2]:
+            db = _accum_param_grad(ctx.b, gb if gb is not None else dy16.float().sum(0))
+        return dx, dw, db, None
+
+
 class _LinearFn(torch.autograd.Function):
+    """hipBLASLt fallback (input width not a multiple of 8, or DTM_FC_BLAS=1 for A/B runs)."""
     @staticmethod
     def forward(ctx, x, w, b, relu):
         w16 = weight_bf16(w)
@@ -698,4 +792,7 @@ def linear(x, w, b=None, relu=False):
         if b is not None:
             y = y + b
         return torch.relu(y) if relu else y
+    import os
+    if w.shape[0] % 8 == 0 and x.dim() == 2 and os.environ.get("DTM_FC_BLAS", "0") != "1":
+        return _LinearHipFn.apply(x, w, b, bool(relu))
     return _LinearFn.apply(x, w, b, bool(relu))

@@ -378,7 +378,7 @@ def test_conv_relu_bias_backward_fused(K, H):
     assert _rel(xg.grad.float().cpu(), xr.grad) < 2e-2
 
 
-@pytest.mark.parametrize("B,N,relu", [(64, 384, True), (37, 192, True), (16, 1000, False), (8, 24, True)])
+@pytest.mark.parametrize("B,N,relu", [(64, 384, True), (37, 192, True), (16, 1000, False), (8, 24, True), (32, 10, False), (5, 1001, True)])
 def test_linear_bias_relu_fused(B, N, relu):
     """FC layer: bias in the GEMM epilogue, ReLU mask + bias sums in one HIP pass, vs fp32 torch
     through the GPU's own ReLU mask."""
