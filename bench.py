@@ -156,6 +156,10 @@ def main():
             "config": {"model": args.model, "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
                        "image_size": S, "parallelism": "dp%d" % world, "device": args.device,
                        "grad_allreduce_dtype": args.grad_comm,
+                       # bytes each rank contributes to the gradient all-reduce per step (dead-tap windows
+                       # excluded: parallel/bsp.py compact buckets)
+                       "grad_wire_mb": round(step.dp.wire_elements() * (2 if args.grad_comm == "bf16" else 4) / 1e6,
+                                             1),
                        "optimizer": {"momentum": "momentum-sgd+wd", "rmsprop": "rmsprop(TF)+wd", "sgd": "sgd+wd"}[opt],
                        "final_loss": round(float(loss), 4) if math.isfinite(float(loss)) else None},
         }

@@ -38,6 +38,34 @@ def _notify(p):
         h(p)
 
 
+# live-tap windows: a conv whose outer taps only ever read zero padding has a provably-zero weight
+# gradient outside its live window (VGG-16 fc6 on a 1x1 map: 48 of 49 taps).  The window is announced
+# during the forward (geometry only, identical on every rank) so the data-parallel layer can leave the
+# dead part of the gradient out of the all-reduce (parallel/bsp.py).
+_live_window_hooks = []
+
+
+def add_live_window_hook(fn):
+    _live_window_hooks.append(fn)
+    return fn
+
+
+def remove_live_window_hook(fn):
+    if fn in _live_window_hooks:
+        _live_window_hooks.remove(fn)
+
+
+def _note_live_window(w, win):
+    if getattr(w, "_live_win", None) == win:
+        return
+    try:
+        w._live_win = win
+    except Exception:
+        return
+    for h in _live_window_hooks:
+        h(w, win)
+
+
 def _accum_param_grad(p, g):
     """Route a computed fp32 grad for parameter p; returns what autograd should receive."""
     mg = getattr(p, "main_grad", None)
@@ -208,6 +236,11 @@ def _relu_bias_bwd(dy, y):
 def conv2d(x, w, bias=None, stride=1, padding="SAME", relu=False, dilation=1):
     """NHWC conv. x [N,H,W,C]; w fp32 master [K,R,S,C]; bias [K] or None."""
     x = as_tensor(x)
+    if dilation == 1 and isinstance(w, torch.nn.Parameter) and w.requires_grad and torch.is_grad_enabled():
+        gl = conv_geom(tuple(x.shape), tuple(w.shape), stride, padding, dilation)
+        win = live_taps(gl)
+        if (win[1] - win[0], win[3] - win[2]) != (gl.R, gl.S):
+            _note_live_window(w, win)
     if not x.is_cuda:
         return ref.conv2d(x, w, bias, stride, padding, relu, dilation)
     if dilation != 1:
