@@ -101,65 +101,161 @@ def sample_distorted_bounding_box(h, w, bboxes, rng, min_object_covered=0.1, asp
     return 0, 0, h, w
 
 
-def _resize(img, size, method):
-    from PIL import Image
-    methods = [Image.BILINEAR, Image.NEAREST, Image.BICUBIC, Image.BOX]  # thread_id % 4 (image_processing.py)
-    return np.asarray(Image.fromarray(img).resize((size, size), methods[method % 4]))
+# ---- TF 1.x image semantics on float [0, 1] images (the host oracle of the GPU pipeline) -----------
+# resize_images(method=thread_id % 4) without align_corners / half-pixel centres (the TF 1 "legacy"
+# sampling: source coordinate = dst * in / out).  Every method is separable, so the resize is
+# Wy @ img @ Wx^T with per-axis weight matrices (the GPU kernel evaluates the same taps directly).
+RESIZE_METHODS = ("bilinear", "nearest", "bicubic", "area")
+_CUBIC_A = -0.75
+_CUBIC_TABLE = 1024  # TF's legacy bicubic quantises the fractional offset to 1/1024
 
 
-def distort_color(img, rng, thread_id=0):
+def _cubic_weights(delta):
+    """TF legacy resize_bicubic taps for offsets -1, 0, 1, 2 (its coefficient table, Keys a = -0.75)."""
+    a = _CUBIC_A
+    off = int(np.rint(delta * _CUBIC_TABLE))
+
+    def near(x):  # |x| <= 1
+        return ((a + 2) * x - (a + 3)) * x * x + 1
+
+    def far(x):  # 1 < |x| < 2
+        return ((a * x - 5 * a) * x + 8 * a) * x - 4 * a
+    x = off / _CUBIC_TABLE
+    y = (_CUBIC_TABLE - off) / _CUBIC_TABLE
+    return far(x + 1.0), near(x), near(y), far(y + 1.0)
+
+
+def resize_weights(n, out, method):
+    """[out, n] float64 weight matrix of one axis."""
+    W = np.zeros((out, n), np.float64)
+    scale = np.float32(n) / np.float32(out)  # float32 coordinates, as TF's resize kernels compute them
+    for o in range(out):
+        f = float(np.float32(o) * scale)
+        scale_f = float(scale)
+        if method == "bilinear":
+            i0 = int(np.floor(f))
+            i1 = min(i0 + 1, n - 1)
+            d = f - i0
+            W[o, i0] += 1.0 - d
+            W[o, i1] += d
+        elif method == "nearest":
+            W[o, min(int(np.floor(f)), n - 1)] = 1.0
+        elif method == "bicubic":
+            i = int(np.floor(f))
+            for k, wk in zip((-1, 0, 1, 2), _cubic_weights(f - i)):
+                W[o, min(max(i + k, 0), n - 1)] += wk
+        else:  # area: fractional box [o*scale, (o+1)*scale)
+            f1 = float(np.float32(o + 1) * scale)
+            i = int(np.floor(f))
+            while i < f1:
+                lo, hi = max(f, i), min(f1, i + 1)
+                if hi > lo:
+                    W[o, min(i, n - 1)] += (hi - lo) / scale_f
+                i += 1
+    return W
+
+
+def resize(img, size, method="bilinear"):
+    """img [h, w, 3] float -> [size, size, 3] float32 (TF 1 legacy resize_images semantics)."""
+    h, w = img.shape[:2]
+    wy, wx = resize_weights(h, size, method), resize_weights(w, size, method)
+    t = np.tensordot(wy, img.astype(np.float64), axes=(1, 0))            # [size, w, 3]
+    return np.tensordot(t, wx, axes=(1, 1)).transpose(0, 2, 1).astype(np.float32)  # [size, size, 3]
+
+
+def rgb_to_hsv(x):
+    r, g, b = x[..., 0], x[..., 1], x[..., 2]
+    v = np.max(x, -1)
+    rng_ = v - np.min(x, -1)
+    s = np.where(v > 0, rng_ / np.where(v > 0, v, 1), 0.0)
+    safe = np.where(rng_ > 0, rng_, 1)
+    h = np.where(r == v, (g - b) / safe, np.where(g == v, (b - r) / safe + 2.0, (r - g) / safe + 4.0)) / 6.0
+    h = np.where(rng_ > 0, h, 0.0)
+    h = np.where(h < 0, h + 1.0, h)
+    return np.stack([h, s, v], -1)
+
+
+def hsv_to_rgb(x):
+    h, s, v = x[..., 0], x[..., 1], x[..., 2]
+    c = s * v
+    m = v - c
+    dh = h * 6.0
+    xx = c * (1.0 - np.abs(np.fmod(dh, 2.0) - 1.0))
+    k = np.floor(dh).astype(np.int64) % 6
+    z = np.zeros_like(c)
+    rgb = np.select([k[..., None] == i for i in range(6)],
+                    [np.stack(t, -1) for t in ((c, xx, z), (xx, c, z), (z, c, xx), (z, xx, c), (xx, z, c), (c, z, xx))])
+    return rgb + m[..., None]
+
+
+def adjust_saturation(x, f):
+    hsv = rgb_to_hsv(x)
+    hsv[..., 1] = np.clip(hsv[..., 1] * f, 0.0, 1.0)
+    return hsv_to_rgb(hsv)
+
+
+def adjust_hue(x, delta):
+    hsv = rgb_to_hsv(x)
+    h = hsv[..., 0] + delta
+    hsv[..., 0] = np.where(h < 0, h + 1.0, np.where(h >= 1.0, h - 1.0, h))
+    return hsv_to_rgb(hsv)
+
+
+def adjust_contrast(x, f):
+    m = x.mean((0, 1), keepdims=True)
+    return (x - m) * f + m
+
+
+def sample_params(h, w, bbox, rng, thread_id, train):
+    """Per-image random parameters of image_preprocessing (shared by the host oracle and the GPU
+    pipeline): crop window, resize method (thread_id % 4), flip, colour factors, colour ordering."""
+    if not train:
+        # tf.image.central_crop(0.875): start = int((h - h * 0.875) / 2), size = h - 2 * start
+        y0, x0 = int((h - h * 0.875) / 2), int((w - w * 0.875) / 2)
+        return dict(y0=y0, x0=x0, ch=h - 2 * y0, cw=w - 2 * x0, method=0, flip=0, color=0, ordering=0,
+                    bright=0.0, sat=1.0, hue=0.0, contrast=1.0)
+    y0, x0, ch, cw = sample_distorted_bounding_box(h, w, bbox, rng)
+    return dict(y0=y0, x0=x0, ch=ch, cw=cw, method=thread_id % 4, flip=int(rng.randint(2)), color=1,
+                ordering=thread_id % 2, bright=float(rng.uniform(-32.0 / 255, 32.0 / 255)),
+                sat=float(rng.uniform(0.5, 1.5)), hue=float(rng.uniform(-0.2, 0.2)),
+                contrast=float(rng.uniform(0.5, 1.5)))
+
+
+def preprocess_with_params(img, size, p):
+    """uint8 [h, w, 3] -> float32 [size, size, 3] in [-1, 1] (reference inception/image_processing.py:
+    decode -> convert_image_dtype -> distort_image / eval_image -> (x - 0.5) * 2)."""
     x = img.astype(np.float32) / 255.0
-    ops = [lambda v: v + rng.uniform(-32.0 / 255, 32.0 / 255),
-           lambda v: _saturation(v, rng.uniform(0.5, 1.5)),
-           lambda v: _hue(v, rng.uniform(-0.2, 0.2)),
-           lambda v: (v - v.mean((0, 1), keepdims=True)) * rng.uniform(0.5, 1.5) + v.mean((0, 1), keepdims=True)]
-    order = [0, 1, 2, 3] if thread_id % 2 == 0 else [0, 2, 1, 3]  # the two orderings of distort_color
-    if thread_id % 2 == 0:
-        order = [0, 1, 2, 3]
-    else:
-        order = [0, 1, 3, 2]
-    for k in order:
-        x = ops[k](x)
-    return np.clip(x, 0.0, 1.0)
-
-
-def _saturation(x, f):
-    gray = x.mean(-1, keepdims=True)
-    return gray + (x - gray) * f
-
-
-def _hue(x, delta):
-    # rotate in YIQ space (approximation of tf.image.adjust_hue)
-    t = delta * 2 * np.pi
-    c, s = np.cos(t), np.sin(t)
-    yiq = np.array([[0.299, 0.587, 0.114], [0.596, -0.274, -0.322], [0.211, -0.523, 0.312]], np.float32)
-    rot = np.array([[1, 0, 0], [0, c, -s], [0, s, c]], np.float32)
-    m = np.linalg.inv(yiq) @ rot @ yiq
-    return x @ m.T.astype(np.float32)
+    x = x[p["y0"]:p["y0"] + p["ch"], p["x0"]:p["x0"] + p["cw"]]
+    x = resize(x, size, RESIZE_METHODS[p["method"]]).astype(np.float64)
+    if p["flip"]:
+        x = x[:, ::-1]
+    if p["color"]:
+        # distort_color: ordering 0 = brightness, saturation, hue, contrast; 1 = brightness, contrast,
+        # saturation, hue (reference image_processing.py:180-193); then clip to [0, 1]
+        x = x + p["bright"]
+        if p["ordering"] == 0:
+            x = adjust_contrast(adjust_hue(adjust_saturation(x, p["sat"]), p["hue"]), p["contrast"])
+        else:
+            x = adjust_hue(adjust_saturation(adjust_contrast(x, p["contrast"]), p["sat"]), p["hue"])
+        x = np.clip(x, 0.0, 1.0)
+    return ((x - 0.5) * 2.0).astype(np.float32)
 
 
 def distort_image(img, size, bbox, rng, thread_id=0):
     h, w = img.shape[:2]
-    y0, x0, ch, cw = sample_distorted_bounding_box(h, w, bbox, rng)
-    crop = img[y0:y0 + ch, x0:x0 + cw]
-    out = _resize(crop, size, thread_id)
-    if rng.randint(2):
-        out = out[:, ::-1]
-    return distort_color(out, rng, thread_id)
+    return preprocess_with_params(img, size, sample_params(h, w, bbox, rng, thread_id, True))
 
 
-def eval_image(img, size, central_fraction=0.875):
+def eval_image(img, size):
     h, w = img.shape[:2]
-    ch, cw = int(h * central_fraction), int(w * central_fraction)
-    y0, x0 = (h - ch) // 2, (w - cw) // 2
-    return _resize(img[y0:y0 + ch, x0:x0 + cw], size, 0).astype(np.float32) / 255.0
+    return preprocess_with_params(img, size, sample_params(h, w, None, None, 0, False))
 
 
 def image_preprocessing(record, train, size, rng, thread_id=0):
     data, label, bbox, _ = parse_example_proto(record)
     img = _decode_jpeg(data)
     x = distort_image(img, size, bbox, rng, thread_id) if train else eval_image(img, size)
-    return (x * 2.0 - 1.0).astype(np.float32), label  # [-1, 1]
+    return x, label  # [-1, 1]
 
 
 class BatchInputs:

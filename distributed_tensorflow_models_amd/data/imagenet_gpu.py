@@ -1,0 +1,159 @@
+"""GPU ImageNet input pipeline (reference inception/image_processing.py:
+batch_inputs / image_preprocessing with num_readers reader threads and num_preprocess_threads
+preprocessing threads).
+
+MI355X-native split of the work:
+  * host: TFRecord readers (threads) -> JPEG decode on a thread pool (PIL releases the GIL while it
+    decodes) -> per-image random parameters (``imagenet.sample_params``: distorted bounding box,
+    resize method = thread id % 4, flip, colour factors and ordering = thread id % 2, with thread id =
+    the example's slot % num_preprocess_threads) -> a background assembler packs each batch into a
+    pinned ragged uint8 buffer + a parameter table (two batches ahead);
+  * device: one H2D copy per batch and two HIP kernels (``dtm_imagenet_prep``, csrc/kernels/image.hip):
+    crop + TF-1 legacy resample + flip + colour distortion + clip + [-1, 1], written straight into
+    the bf16 NHWC batch the model consumes.  The host oracle of the same math is
+    ``imagenet.preprocess_with_params`` (tests/test_data_gpu.py).
+"""
+import ctypes
+import queue
+import random
+import threading
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import torch
+
+from ..ops import _lib
+from . import imagenet
+from .tfrecord import tf_record_iterator
+
+PARAM_FIELDS = ("src_off", "h", "w", "y0", "x0", "ch", "cw", "method", "flip", "color", "ordering",
+                "bright", "sat", "hue", "contrast")
+_PARAM_DT = np.dtype([("src_off", "<i8"), ("h", "<i4"), ("w", "<i4"), ("y0", "<i4"), ("x0", "<i4"),
+                      ("ch", "<i4"), ("cw", "<i4"), ("method", "<i4"), ("flip", "<i4"), ("color", "<i4"),
+                      ("ordering", "<i4"), ("bright", "<f4"), ("sat", "<f4"), ("hue", "<f4"),
+                      ("contrast", "<f4")])
+
+
+def pack_batch(images, params):
+    """-> (uint8 ragged buffer, structured parameter table) for a list of HxWx3 uint8 images."""
+    offs = np.cumsum([0] + [im.nbytes for im in images])
+    buf = np.empty(int(offs[-1]), np.uint8)
+    tab = np.zeros(len(images), _PARAM_DT)
+    for i, (im, p) in enumerate(zip(images, params)):
+        buf[offs[i]:offs[i + 1]] = np.ascontiguousarray(im, np.uint8).reshape(-1)
+        tab[i]["src_off"] = offs[i]
+        tab[i]["h"], tab[i]["w"] = im.shape[0], im.shape[1]
+        for k in PARAM_FIELDS[3:]:
+            tab[i][k] = p[k]
+    return buf, tab
+
+
+def gpu_preprocess(images, params, size, device, out_dtype=torch.bfloat16):
+    """Run the HIP preprocessing on host-decoded images with given parameters -> [B, size, size, 3]."""
+    L = _lib.lib()
+    assert L.dtm_prep_params_bytes() == _PARAM_DT.itemsize
+    buf, tab = pack_batch(images, params)
+    return _launch(torch.from_numpy(buf), torch.from_numpy(tab.view(np.uint8)), len(images), size, device,
+                   out_dtype)
+
+
+def _launch(buf_cpu, tab_cpu, B, size, device, out_dtype, stage=None):
+    L = _lib.lib()
+    src = buf_cpu.to(device, non_blocking=True)
+    tab = tab_cpu.to(device, non_blocking=True)
+    if stage is None or stage.numel() < B * size * size * 3:
+        stage = torch.empty(B * size * size * 3, device=device, dtype=torch.float32)
+    sums = torch.empty(B * 3, device=device, dtype=torch.float32)
+    out = torch.empty((B, size, size, 3), device=device, dtype=out_dtype)
+    rc = L.dtm_imagenet_prep(_lib.ptr(src), _lib.ptr(tab), _lib.ptr(stage), _lib.ptr(sums), _lib.ptr(out),
+                             int(out_dtype == torch.bfloat16), B, size, _lib.stream_ptr())
+    if rc != 0:
+        raise RuntimeError("dtm_imagenet_prep failed (%d)" % rc)
+    return out, stage
+
+
+class GPUBatchInputs:
+    """Drop-in for ``imagenet.BatchInputs`` producing device batches ([B,S,S,3] bf16, [B] int64)."""
+
+    def __init__(self, dataset, batch_size, train=True, image_size=299, num_preprocess_threads=4, num_readers=4,
+                 num_decoders=8, seed=0, device="cuda", shuffle_buffer=1024, prefetch=2):
+        self.files = dataset.data_files()
+        self.B, self.S, self.train = batch_size, image_size, train
+        self.device = torch.device(device)
+        self.nthreads = max(1, num_preprocess_threads)
+        self.records = queue.Queue(maxsize=shuffle_buffer)
+        self.ready = queue.Queue(maxsize=max(1, prefetch))
+        self.stop = threading.Event()
+        self.pool = ThreadPoolExecutor(max_workers=max(1, num_decoders))
+        self.rng = np.random.RandomState(seed)
+        self.slot = 0
+        self.threads = []
+        for r in range(num_readers):
+            t = threading.Thread(target=self._read, args=(r, num_readers, seed + r), daemon=True)
+            t.start()
+            self.threads.append(t)
+        t = threading.Thread(target=self._assemble, daemon=True)
+        t.start()
+        self.threads.append(t)
+        self._stage = None
+        self.images_done = 0
+
+    def _read(self, rid, n, seed):
+        rng = random.Random(seed)
+        files = self.files[rid::n] or self.files
+        while not self.stop.is_set():
+            if self.train:
+                rng.shuffle(files)
+            for f in files:
+                for rec in tf_record_iterator(f):
+                    if self.stop.is_set():
+                        return
+                    self.records.put(rec)
+            if not self.train:
+                break
+
+    @staticmethod
+    def _decode(rec):
+        data, label, bbox, _ = imagenet.parse_example_proto(rec)
+        return imagenet._decode_jpeg(data), label, bbox
+
+    def _assemble(self):
+        while not self.stop.is_set():
+            recs = []
+            while len(recs) < self.B and not self.stop.is_set():
+                try:
+                    recs.append(self.records.get(timeout=0.5))
+                except queue.Empty:
+                    continue
+            if self.stop.is_set():
+                return
+            dec = list(self.pool.map(self._decode, recs))
+            imgs, params, labels = [], [], []
+            for img, label, bbox in dec:
+                tid = self.slot % self.nthreads  # the reference's per-thread method / colour ordering
+                self.slot += 1
+                params.append(imagenet.sample_params(img.shape[0], img.shape[1], bbox, self.rng, tid, self.train))
+                imgs.append(img)
+                labels.append(label)
+            buf, tab = pack_batch(imgs, params)
+            bt = torch.from_numpy(buf).pin_memory()
+            tt = torch.from_numpy(tab.view(np.uint8)).pin_memory()
+            self.ready.put((bt, tt, torch.tensor(labels, dtype=torch.int64).pin_memory()))
+
+    def next_batch(self):
+        bt, tt, lab = self.ready.get()
+        x, self._stage = _launch(bt, tt, self.B, self.S, self.device, torch.bfloat16, self._stage)
+        self.images_done += self.B
+        return x, lab.to(self.device, non_blocking=True)
+
+    def close(self):
+        self.stop.set()
+        self.pool.shutdown(wait=False)
+
+
+def distorted_inputs(dataset, batch_size, num_preprocess_threads=4, image_size=299, **kw):
+    return GPUBatchInputs(dataset, batch_size, True, image_size, num_preprocess_threads, **kw)
+
+
+def inputs(dataset, batch_size, num_preprocess_threads=4, image_size=299, **kw):
+    return GPUBatchInputs(dataset, batch_size, False, image_size, num_preprocess_threads, num_readers=1, **kw)

@@ -88,6 +88,10 @@ def _inputs(preset, flags, device):
         return cifar10.inputs(F.eval_data == "test", F.data_dir, F.batch_size, S, device=device)
     if cfg["dataset"] == "imagenet" and not F.synthetic_data:
         from .data import imagenet
+        if torch.device(device).type == "cuda":
+            from .data import imagenet_gpu
+            return imagenet_gpu.inputs(imagenet.ImagenetData(F.subset, F.data_dir), F.batch_size, image_size=S,
+                                       device=device)
         return imagenet.inputs(imagenet.ImagenetData(F.subset, F.data_dir), F.batch_size, image_size=S,
                                device=device)
     from .data.synthetic import SyntheticImages

@@ -34,6 +34,8 @@ _F = ctypes.c_float
 _SIGS = {
     "dtm_conv_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, ctypes.POINTER(ConvDesc), _P]),
     "dtm_act_fwd": (_I, [_P, _P, _L, _I, _F, _I, _P]),
+    "dtm_prep_params_bytes": (_I, []),
+    "dtm_imagenet_prep": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P]),
     "dtm_act_bwd": (_I, [_P, _P, _P, _L, _I, _F, _I, _P]),
     "dtm_instnorm_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _I, _P]),
     "dtm_instnorm_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),

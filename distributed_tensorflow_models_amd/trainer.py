@@ -172,6 +172,11 @@ def make_input(cfg, batch_size, device, flags, rank):
         return _M()
     if ds == "imagenet":
         from .data import imagenet
+        if torch.device(device).type == "cuda":
+            # decode on host threads, crop / resize / flip / colour on the GPU (data/imagenet_gpu.py)
+            from .data import imagenet_gpu
+            return imagenet_gpu.distorted_inputs(imagenet.ImagenetData("train", flags.data_dir), batch_size,
+                                                 image_size=S, device=device, seed=flags.seed + rank)
         return imagenet.distorted_inputs(imagenet.ImagenetData("train", flags.data_dir), batch_size, image_size=S,
                                          device=device, seed=flags.seed + rank)
     from .data.synthetic import SyntheticImages

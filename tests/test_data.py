@@ -167,3 +167,25 @@ def test_in_top_k_tf_semantics():
     assert E.in_top_k(p, t, 3).tolist() == [True, False, False, True]
     assert E.in_top_k(p, t, 4).tolist() == [True, True, False, True]
     assert E.in_top_k(p, torch.tensor([5, -1, 1, 0]), 4).tolist() == [False, False, True, True]
+
+
+def test_imagenet_oracle_tf_semantics():
+    """Host oracle of the ImageNet preprocessing: TF-1 legacy resize weights (rows sum to 1; nearest /
+    bilinear at known points), HSV round trip, and the reference's two distort_color orderings."""
+    x = np.random.RandomState(0).rand(9, 7, 3)
+    np.testing.assert_allclose(imagenet.hsv_to_rgb(imagenet.rgb_to_hsv(x)), x, atol=1e-12)
+    for m in imagenet.RESIZE_METHODS:
+        W = imagenet.resize_weights(13, 5, m)
+        np.testing.assert_allclose(W.sum(1), 1.0, atol=1e-5)
+    Wb = imagenet.resize_weights(4, 8, "bilinear")  # legacy: src = dst * 0.5, no half-pixel offset
+    np.testing.assert_allclose(Wb[1], [0.5, 0.5, 0, 0])
+    np.testing.assert_allclose(Wb[7], [0, 0, 0, 1])
+    assert np.argmax(imagenet.resize_weights(10, 4, "nearest"), 1).tolist() == [0, 2, 5, 7]
+    # ordering 1 = brightness, contrast, saturation, hue (reference image_processing.py:187-192)
+    img = (np.random.RandomState(1).rand(16, 16, 3) * 255).astype(np.uint8)
+    p = dict(y0=0, x0=0, ch=16, cw=16, method=0, flip=0, color=1, ordering=1, bright=0.05, sat=1.3, hue=0.1,
+             contrast=0.7)
+    got = imagenet.preprocess_with_params(img, 16, p)
+    v = imagenet.resize(img.astype(np.float32) / 255.0, 16, "bilinear").astype(np.float64) + 0.05
+    v = imagenet.adjust_hue(imagenet.adjust_saturation(imagenet.adjust_contrast(v, 0.7), 1.3), 0.1)
+    np.testing.assert_allclose(got, ((np.clip(v, 0, 1) - 0.5) * 2).astype(np.float32), atol=1e-6)
