@@ -134,10 +134,85 @@ class ParamStore:
                 w16.copy_(p)
         WEIGHT_VERSION[0] += 1
 
+    # ---- fused GPU push: one multi-tensor optimizer launch on the owner shards -----------------
+    def _fused_tables(self):
+        """Static part of the multi-tensor table (shard / slot pointers, sizes, wd) + the chunk list."""
+        import numpy as np
+
+        from ..ops import _lib
+        L = _lib.lib()
+        tb, chunk = L.dtm_opt_tensor_bytes(), L.dtm_opt_chunk_size()
+        assert tb == 64, tb
+        tens = np.zeros((len(self.params), 8), dtype=np.uint64)
+        chunks = []
+        for i, p in enumerate(self.params):
+            sh = self.shards[i]
+            tens[i, 0] = sh["param"].data_ptr()
+            tens[i, 2] = sh["s1"].data_ptr() if "s1" in sh else 0
+            tens[i, 3] = sh["s2"].data_ptr() if "s2" in sh else 0
+            tens[i, 6] = p.numel()
+            tens[i, 7] = np.array([self.wd[i], 1.0], dtype=np.float32).view(np.uint64)[0]
+            for st in range(0, p.numel(), chunk):
+                chunks.append((i, st))
+        ct = np.zeros((len(chunks), 2), dtype=np.int64)
+        for j, (i, st) in enumerate(chunks):
+            ct[j, 0], ct[j, 1] = i, st
+        dev = self.params[0].device
+        self._ftens = tens
+        self._fchunks = torch.from_numpy(ct.view(np.uint8).reshape(-1).copy()).to(dev)
+        self._fnchunks = len(chunks)
+        self._fring = [(torch.empty(tens.nbytes, dtype=torch.uint8).pin_memory(),
+                        torch.zeros(3, dtype=torch.float32).pin_memory(), None) for _ in range(4)]
+        self._fi = 0
+        self._fdev_tens = torch.empty(tens.nbytes, dtype=torch.uint8, device=dev)
+        self._fdyn = torch.zeros(3, dtype=torch.float32, device=dev)
+
     @torch.no_grad()
-    def push(self, grads, lr=None, grad_scale=1.0):
-        """Apply this worker's gradients to the owner shards with the TF rule (M2)."""
+    def _push_fused(self, grads, lr, grad_scale, sync):
+        """GPU mode: every shard updated by ONE dtm_multi_tensor_opt launch on this rank's stream; the
+        kernel writes the owners' HBM directly through the IPC mappings (xGMI peer access).  The grad
+        pointers change per step, so the per-step table row is staged through a pinned ring."""
+        import numpy as np
+
+        from ..ops import _lib
+        from ..ops.optim import KINDS
+        if getattr(self, "_ftens", None) is None:
+            self._fused_tables()
+        keep = []
+        tens = self._ftens.copy()
+        for i, g in enumerate(grads):
+            if g is None:
+                tens[i, 6] = 0  # no gradient this step: the rows of this tensor do nothing
+                continue
+            g = g.detach().float().contiguous()
+            keep.append(g)
+            tens[i, 1] = g.data_ptr()
+        host, dyn, ev = self._fring[self._fi]
+        if ev is not None:
+            ev.synchronize()  # the copy that last read this ring slot has executed
+        host.numpy()[:] = tens.view(np.uint8).reshape(-1)
+        dyn[0], dyn[1], dyn[2] = float(lr), 0.0, float(grad_scale)
+        self._fdev_tens.copy_(host, non_blocking=True)
+        self._fdyn.copy_(dyn, non_blocking=True)
+        L = _lib.lib()
+        L.dtm_multi_tensor_opt(_lib.ptr(self._fdev_tens), _lib.ptr(self._fchunks), self._fnchunks, KINDS[self.kind],
+                               float(lr), float(self.mu), float(self.rho), float(self.eps), float(grad_scale), 0.0, 0,
+                               None, _lib.ptr(self._fdyn), _lib.stream_ptr())
+        ev = torch.cuda.Event()
+        ev.record()
+        self._fring[self._fi] = (host, dyn, ev)
+        self._fi = (self._fi + 1) % len(self._fring)
+        if sync:
+            ev.synchronize()
+
+    @torch.no_grad()
+    def push(self, grads, lr=None, grad_scale=1.0, sync=True):
+        """Apply this worker's gradients to the owner shards with the TF rule (M2).  GPU shards: one
+        fused multi-tensor launch (``sync``: wait for it, e.g. before an SSP clock tick); host shards
+        (shm mode): per-tensor torch ops."""
         lr = self.lr if lr is None else lr
+        if self.params[0].is_cuda and self.mode == "ipc":
+            return self._push_fused(grads, lr, grad_scale, sync)
         for i, p in enumerate(self.params):
             g = grads[i]
             if g is None:
@@ -227,8 +302,10 @@ class ASPTrainStep:
         loss.backward()
         gs = self.store.global_step()
         lr = self.lr_schedule(gs) if self.lr_schedule else None
+        # ASP: nothing waits for the update (Hogwild: the next pull on this stream sees it); SSP ticks
+        # the staleness clock only after the update has landed
         self.store.push([getattr(p, "main_grad", None) if p.grad is None else p.grad for p in self.store.params],
-                        lr=lr)
+                        lr=lr, sync=self.ssp is not None)
         gstep = self.store.increment_global_step()
         self.local_step += 1
         if self.ssp is not None:

@@ -273,3 +273,49 @@ def test_bsp_dead_tap_gradients_left_out_of_the_allreduce():
     assert full[0]["wire"] - comp[0]["wire"] == 32 * 16 * 48  # the 48 dead taps of w6
     assert torch.equal(comp[0]["params"], comp[1]["params"])
     assert torch.equal(comp[0]["params"], full[0]["params"])
+
+
+def _asp_ipc_worker(rank, world, kind="sgd", lr=0.5):
+    """Two ranks sharing cuda:0: owner shards in HBM opened through HIP IPC by the other rank; every
+    push is ONE fused multi-tensor optimizer launch writing the owners' memory directly."""
+    from distributed_tensorflow_models_amd.parallel.asp import ParamStore, wait_all_done
+    dev = torch.device("cuda", 0)
+    params = [torch.nn.Parameter(torch.full((5,), 1.0, device=dev)),
+              torch.nn.Parameter(torch.full((3, 20000), 2.0, device=dev)),  # several optimizer chunks
+              torch.nn.Parameter(torch.zeros(4, device=dev))]
+    store = ParamStore(params, kind, lr, momentum=0.9, mode="ipc", run_id="aspipc%s%d" % (kind, world))
+    from distributed_tensorflow_models_amd.parallel import process_group as pg
+    for step in range(2):
+        g = [torch.full_like(p, float(rank + 1)) for p in params]
+        for r in range(world):  # one pusher at a time: this test checks the update math, not Hogwild races
+            if r == rank:
+                store.push(g, sync=True)
+                store.increment_global_step()
+            pg.barrier()
+    wait_all_done(store.store, world, store.run_id)
+    store.pull()
+    torch.cuda.synchronize()
+    out = {"params": [p.detach().cpu().clone() for p in params], "gs": store.global_step(),
+           "fused": getattr(store, "_ftens", None) is not None}
+    store.close()
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["sgd", "momentum"])
+def test_asp_gpu_ipc_fused_push(kind):
+    res = run_workers(_asp_ipc_worker, 2, kind)
+    # pushes land in the order rank 0, rank 1, rank 0, rank 1 with g = 1, 2, 1, 2 (lr 0.5)
+    gs_seq = [1.0, 2.0, 1.0, 2.0]
+    dec, a = 0.0, 0.0
+    for g in gs_seq:
+        if kind == "sgd":
+            dec += 0.5 * g
+        else:  # TF Momentum: a <- 0.9 a + g ; w -= lr a  (the accumulator lives in the owner shard)
+            a = 0.9 * a + g
+            dec += 0.5 * a
+    for r in res:
+        assert r["gs"] == 4 and r["fused"]
+        torch.testing.assert_close(r["params"][1], torch.full((3, 20000), 2.0 - dec))
+        torch.testing.assert_close(r["params"][2], torch.full((4,), -dec))
+        torch.testing.assert_close(r["params"][0], torch.full((5,), 1.0 - dec))
