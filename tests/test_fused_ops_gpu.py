@@ -36,24 +36,26 @@ def test_conv_bn_single(C, K, R, stride, relu):
     x = torch.randn(2, 12, 12, C, device=DEV).to(torch.bfloat16).float()
     w = (torch.randn(K, R, R, C, device=DEV) / (R * R * C) ** 0.5).to(torch.bfloat16).float()
     bn = _bn(K)
-    xr, wr = x.clone().requires_grad_(), w.clone().requires_grad_()
-    gr, br = bn.gamma.detach().clone().requires_grad_(), bn.beta.detach().clone().requires_grad_()
-    yr = ref.batch_norm(ref.conv2d(xr, wr, None, stride, "SAME"), gr, br, None, None, True, 0.9, 1e-3, relu)
-    gy = torch.randn_like(yr).to(torch.bfloat16).float()
-    yr.backward(gy)
     xk = x.to(torch.bfloat16).requires_grad_()
     wk = w.clone().requires_grad_()
     lz = fused.conv_bn(xk, wk, bn, stride, "SAME", True, relu)
     yk = lz.materialize()
+    # the fp32 reference back-propagates through the KERNEL's ReLU mask (otherwise bf16-rounded outputs
+    # within rounding of zero flip the mask and dominate the per-channel gradient error)
+    mask = (yk.detach().float() > 0).float() if relu else None
+    xr, wr = x.clone().requires_grad_(), w.clone().requires_grad_()
+    gr, br = bn.gamma.detach().clone().requires_grad_(), bn.beta.detach().clone().requires_grad_()
+    yr = ref.batch_norm(ref.conv2d(xr, wr, None, stride, "SAME"), gr, br, None, None, True, 0.9, 1e-3, False)
+    if relu:
+        yr = yr * mask
+    gy = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(gy)
     yk.backward(gy.to(torch.bfloat16))
     torch.cuda.synchronize()
     errs = dict(y=_rel(yk, yr), dx=_rel(xk.grad, xr.grad), dw=_rel(wk.grad, wr.grad),
                 dgamma=_rel(bn.gamma.grad, gr.grad), dbeta=_rel(bn.beta.grad, br.grad))
-    # K=8 channels over 288 pixels: per-channel BN statistics of so few bf16 values carry ~3 % noise.
-    # With relu, the bf16-rounded y flips the mask of near-zero outputs vs. the fp32 oracle: dgamma /
-    # dbeta then differ by 2-4 % although the reductions themselves are exact (tools/diag_bn.py shows
-    # dbeta == sum(g * own_mask) to fp32 precision for every C, incl. C/8 not dividing 256).
-    tol = 5e-2 if (K < 16 or relu) else 2e-2
+    # K=8 channels over 288 pixels: per-channel BN statistics of so few bf16 values carry ~3 % noise
+    tol = 5e-2 if K < 16 else 2e-2
     assert all(v < tol for v in errs.values()), errs
 
 
@@ -68,29 +70,33 @@ def test_conv_bn_chain_prologue(C, relu):
     w1 = (torch.randn(C, 1, 1, C, device=DEV) / C ** 0.5).to(torch.bfloat16).float()
     w2 = (torch.randn(C, 3, 3, C, device=DEV) / (9 * C) ** 0.5).to(torch.bfloat16).float()
     bn1, bn2 = _bn(C), _bn(C)
-    xr, w1r, w2r = (t.clone().requires_grad_() for t in (x, w1, w2))
-    g1, b1 = bn1.gamma.detach().clone().requires_grad_(), bn1.beta.detach().clone().requires_grad_()
-    g2, b2 = bn2.gamma.detach().clone().requires_grad_(), bn2.beta.detach().clone().requires_grad_()
-    a1 = ref.batch_norm(ref.conv2d(xr, w1r), g1, b1, None, None, True, 0.9, 1e-3, relu)
-    yr = ref.batch_norm(ref.conv2d(a1, w2r), g2, b2, None, None, True, 0.9, 1e-3, relu)
-    gy = torch.randn_like(yr).to(torch.bfloat16).float()
-    yr.backward(gy)
     xk = x.to(torch.bfloat16).requires_grad_()
     w1k, w2k = w1.clone().requires_grad_(), w2.clone().requires_grad_()
     l1 = fused.conv_bn(xk, w1k, bn1, 1, "SAME", True, relu)
+    # the kernels' own ReLU masks: the prologue / act epilogue decide relu(raw * scale + shift) from the
+    # bf16 raw conv output and the fp32 scale/shift; the output BN-apply from its own value
+    m1 = ((l1.raw.detach().float() * l1.ss[0] + l1.ss[1]) > 0).float() if relu else None
     l2 = fused.conv_bn(l1, w2k, bn2, 1, "SAME", True, relu)
     yk = l2.materialize()
+    m2 = (yk.detach().float() > 0).float() if relu else None
+    xr, w1r, w2r = (t.clone().requires_grad_() for t in (x, w1, w2))
+    g1, b1 = bn1.gamma.detach().clone().requires_grad_(), bn1.beta.detach().clone().requires_grad_()
+    g2, b2 = bn2.gamma.detach().clone().requires_grad_(), bn2.beta.detach().clone().requires_grad_()
+    a1 = ref.batch_norm(ref.conv2d(xr, w1r), g1, b1, None, None, True, 0.9, 1e-3, False)
+    if relu:
+        a1 = a1 * m1
+    yr = ref.batch_norm(ref.conv2d(a1, w2r), g2, b2, None, None, True, 0.9, 1e-3, False)
+    if relu:
+        yr = yr * m2
+    gy = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(gy)
     yk.backward(gy.to(torch.bfloat16))
     torch.cuda.synchronize()
     errs = dict(y=_rel(yk, yr), dx=_rel(xk.grad, xr.grad), dw1=_rel(w1k.grad, w1r.grad),
                 dw2=_rel(w2k.grad, w2r.grad), dg1=_rel(bn1.gamma.grad, g1.grad), db1=_rel(bn1.beta.grad, b1.grad),
                 dg2=_rel(bn2.gamma.grad, g2.grad), db2=_rel(bn2.beta.grad, b2.grad))
     msg = " ".join("%s=%.4f" % kv for kv in errs.items())
-    if relu:
-        # flip noise ~ sqrt(flipped / active elements): ~6 % on these 200-pixel channels
-        assert all(v < 1.2e-1 for v in errs.values()) and errs["y"] < 1e-2, msg
-    else:
-        assert all(v < 1.5e-2 for v in errs.values()), msg
+    assert all(v < 2e-2 for v in errs.values()), msg
 
 
 @pytest.mark.parametrize("proj,C,act", [(False, 64, "relu"), (True, 64, "relu"), (True, 96, None), (False, 320, None),
@@ -101,17 +107,20 @@ def test_bn_apply_residual(proj, C, act):
     w = (torch.randn(C, 1, 1, C, device=DEV) / C ** 0.5).to(torch.bfloat16).float()
     ws = (torch.randn(C, 1, 1, C, device=DEV) / C ** 0.5).to(torch.bfloat16).float()
     bn, bns = _bn(C), _bn(C)
-    xr, wr, wsr = (t.clone().requires_grad_() for t in (x, w, ws))
-    g, b = bn.gamma.detach().clone().requires_grad_(), bn.beta.detach().clone().requires_grad_()
-    gs, bs = bns.gamma.detach().clone().requires_grad_(), bns.beta.detach().clone().requires_grad_()
-    sc = ref.batch_norm(ref.conv2d(xr, wsr), gs, bs, None, None, True, 0.9, 1e-3, False) if proj else xr
-    yr = ref.batch_norm(ref.conv2d(xr, wr), g, b, None, None, True, 0.9, 1e-3, act == "relu", residual=sc)
-    gy = torch.randn_like(yr).to(torch.bfloat16).float()
-    yr.backward(gy)
     xk = x.to(torch.bfloat16).requires_grad_()
     wk, wsk = w.clone().requires_grad_(), ws.clone().requires_grad_()
     sck = fused.conv_bn(xk, wsk, bns, 1, "SAME", True, False) if proj else xk
     yk = fused.conv_bn(xk, wk, bn, 1, "SAME", True, False).materialize(residual=sck, residual_act=act)
+    mask = (yk.detach().float() > 0).float() if act == "relu" else None  # the kernel's own ReLU mask
+    xr, wr, wsr = (t.clone().requires_grad_() for t in (x, w, ws))
+    g, b = bn.gamma.detach().clone().requires_grad_(), bn.beta.detach().clone().requires_grad_()
+    gs, bs = bns.gamma.detach().clone().requires_grad_(), bns.beta.detach().clone().requires_grad_()
+    sc = ref.batch_norm(ref.conv2d(xr, wsr), gs, bs, None, None, True, 0.9, 1e-3, False) if proj else xr
+    yr = ref.batch_norm(ref.conv2d(xr, wr), g, b, None, None, True, 0.9, 1e-3, False, residual=sc)
+    if mask is not None:
+        yr = yr * mask
+    gy = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(gy)
     yk.backward(gy.to(torch.bfloat16))
     torch.cuda.synchronize()
     errs = dict(y=_rel(yk, yr), dx=_rel(xk.grad, xr.grad), dw=_rel(wk.grad, wr.grad),
@@ -119,10 +128,7 @@ def test_bn_apply_residual(proj, C, act):
     if proj:
         errs.update(dws=_rel(wsk.grad, wsr.grad), dgs=_rel(bns.gamma.grad, gs.grad), dbs=_rel(bns.beta.grad, bs.grad))
     msg = " ".join("%s=%.4f" % kv for kv in errs.items())
-    if act == "relu":  # relu-mask flip noise, see test_conv_bn_chain_prologue
-        assert all(v < 1.2e-1 for v in errs.values()) and errs["y"] < 1e-2, msg
-    else:
-        assert all(v < 1.5e-2 for v in errs.values()), msg
+    assert all(v < 2e-2 for v in errs.values()), msg
 
 
 @pytest.mark.parametrize("H,act", [(8, None), (9, None), (15, "relu")])
