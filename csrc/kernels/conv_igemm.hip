@@ -1657,6 +1657,8 @@ struct TileCfg {
 };
 static int g_tile_env = -2;
 static int g_tile_w8 = 1;  // A/B knob: the 8-wave tile in the shape policy (dtm_conv_set_w8)
+static int g_kwide = 1;    // A/B knob: 64-channel tiles for K % 128 in (0, 64] (dtm_conv_set_kwide)
+DTM_API void dtm_conv_set_kwide(int on) { g_kwide = on; }
 DTM_API void dtm_conv_set_w8(int on) { g_tile_w8 = on; }
 static int g_k64_tile = 3;  // tile of the 64-output-channel layers (A/B knob: dtm_conv_set_k64_tile)
 DTM_API void dtm_conv_set_k64_tile(int id) { g_k64_tile = id; }
@@ -1683,6 +1685,10 @@ static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
     const long tiles = (long)((a.M + 255) / 256) * ((a.K + 255) / 256);
     if (tiles >= 150 && !(tiles > 600 && a.Kg <= 256 && !stats)) id = 40;
   }
+  // output widths that leave the last 128-channel tile at most half full (Inception's 192 / 320 / 96 /
+  // 160 ...): 64-channel tiles (A/B knob dtm_conv_set_kwide)
+  if (id == -1 && g_kwide && a.K > 64 && a.K % 128 != 0 && (a.K % 128) <= 64 && a.K % 8 == 0)
+    id = a.in_scale ? 3 : 26;
   if (id == -1 && !a.in_scale && a.Kg >= 1024) id = 21;  // (-3: the policy without it, for A/B runs)
   // 64-output-channel 3x3 layers (56x56 bottleneck conv2, fwd and dgrad): the 2-slot pipelined 128x64 tile
   // (profiles/r2_conv_tiles_k64.txt: -4 % vs the register-staged single-buffer tile)
