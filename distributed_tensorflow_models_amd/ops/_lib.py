@@ -94,6 +94,7 @@ _SIGS = {
     "dtm_conv_set_k64_tile": (None, [_I]),
     "dtm_conv_set_w8": (None, [_I]),
     "dtm_conv_set_kwide": (None, [_I]),
+    "dtm_set_reduce_few": (None, [_I]),
     "dtm_dropout": (_I, [_P, _P, _L, _I, _F, ctypes.c_ulonglong, _P, _P]),
     "dtm_in_top_k": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
 }
