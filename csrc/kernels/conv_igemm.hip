@@ -60,6 +60,9 @@ struct ConvNTArgs {
   float* act_sums;        //   partial rows per pixel tile: [sum g*act_x (K) | sum g (K)]
   const bf16_t* zero;     // >= 16 B of zeros: the LDS-DMA source of padding / out-of-range chunks
   int act_unscaled;       // act path: out <- g (not g*scale); the producer's conv+BN backward scales it
+  const uint8_t* act_mask;  // act path, block-output form: the ReLU mask is the forward's bitmask (1 bit per
+                            //   element) of relu(bn(act_x) + residual) instead of act_x*scale+shift > 0
+  const bf16_t* act_r;      //   + a BN'd residual: also sum g*act_r -> rows [g*x | g | g*r | g] (4K wide)
   int pix_bytes;          // byte pitch of one input pixel (C*2, or less for the packed-row stem view)
   bf16_t* dump;           // >= 16 B scratch: target of the out-of-range stores of the exact-count epilogue
 };
@@ -168,70 +171,129 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
     float sc[8], sh[8], sgx[8], sg[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { sc[e] = 1.f; sh[e] = 0.f; sgx[e] = 0.f; sg[e] = 0.f; }
-    if (act && kc < a.K) {
+    const bool amask = act && a.act_mask != nullptr;
+    float sgr[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sgr[e] = 0.f;
+    if (act && !amask && kc < a.K) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) { sc[e] = a.act_ss[kc + e]; sh[e] = a.act_ss[a.K + kc + e]; }
     }
+    // side inputs of the dgrad post-ops (add_src, act_x, act_r, mask bytes) are loaded for a group of
+    // GRP rows before any of them is used, so their latencies overlap instead of serialising per row
+    constexpr int GRP = NIT < 4 ? NIT : 4;
+    static_assert(NIT % GRP == 0, "epilogue row groups");
+    const bool side = a.add_src != nullptr || act;
 #pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int idx = it * NT + tid;
-      const int row = idx / CPR;
-      const int m = p0 + row;
-      const bool inb = m < a.M && kc < a.K;
-      if (EXACT || inb) {
-        uint4 v = *(const uint4*)(smem + row * OROW + chn * 16);
-        const size_t o = (size_t)m * a.K + kc;
-        if constexpr (SACC) {
-          if (inb) {
-            const float q[8] = {lo_bf(v.x), hi_bf(v.x), lo_bf(v.y), hi_bf(v.y),
-                                lo_bf(v.z), hi_bf(v.z), lo_bf(v.w), hi_bf(v.w)};
+    for (int g0 = 0; g0 < NIT; g0 += GRP) {
+      uint4 pa[GRP], px[GRP], pr[GRP];
+      uint32_t pm[GRP];
+      bool ph[GRP];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) { ssum[e] += q[e]; ssq[e] = fmaf(q[e], q[e], ssq[e]); }
-          }
-        } else {
-          if (bstats && inb) {  // (sgx / sg double as the statistics accumulators: act is off here)
-            const float q[8] = {lo_bf(v.x), hi_bf(v.x), lo_bf(v.y), hi_bf(v.y),
-                                lo_bf(v.z), hi_bf(v.z), lo_bf(v.w), hi_bf(v.w)};
+      for (int j = 0; j < GRP; ++j) {
+        pa[j] = px[j] = pr[j] = make_uint4(0, 0, 0, 0);
+        pm[j] = 0u;
+        ph[j] = false;
+      }
+      if (side) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) { sgx[e] += q[e]; sg[e] = fmaf(q[e], q[e], sg[e]); }
+        for (int j = 0; j < GRP; ++j) {
+          const int row = ((g0 + j) * NT + tid) / CPR;
+          const int m = p0 + row;
+          if (m < a.M && kc < a.K) {
+            const size_t o = (size_t)m * a.K + kc;
+            if (a.add_src) {
+              const bf16_t* src = a.add_src + o;
+              if (a.add_stride > 1) {
+                const uint32_t n = fdiv((uint32_t)m, a.fd_PQ), rem = m - n * (a.P * a.Q);
+                const uint32_t h = fdiv(rem, a.fd_Q), w = rem - h * a.Q;
+                const int s = a.add_stride;
+                src = (h % s == 0 && w % s == 0)
+                          ? a.add_src + ((size_t)((int)n * a.add_H + (int)h / s) * a.add_W + (int)w / s) * a.K + kc
+                          : nullptr;
+              }
+              if (src) {
+                pa[j] = *(const uint4*)src;
+                ph[j] = true;
+              }
+            }
+            if (act) {
+              px[j] = *(const uint4*)(a.act_x + o);
+              if (amask) {
+                pm[j] = a.act_mask[o >> 3];
+                if (a.act_r) pr[j] = *(const uint4*)(a.act_r + o);
+              }
+            }
           }
         }
-        if (inb && (a.add_src || act)) {
-          float f[8];
-          f[0] = lo_bf(v.x); f[1] = hi_bf(v.x); f[2] = lo_bf(v.y); f[3] = hi_bf(v.y);
-          f[4] = lo_bf(v.z); f[5] = hi_bf(v.z); f[6] = lo_bf(v.w); f[7] = hi_bf(v.w);
-          if (a.add_src) {
-            const bf16_t* src = a.add_src + o;
-            if (a.add_stride > 1) {
-              const uint32_t n = fdiv((uint32_t)m, a.fd_PQ), rem = m - n * (a.P * a.Q);
-              const uint32_t h = fdiv(rem, a.fd_Q), w = rem - h * a.Q;
-              const int s = a.add_stride;
-              src = (h % s == 0 && w % s == 0)
-                        ? a.add_src + ((size_t)((int)n * a.add_H + (int)h / s) * a.add_W + (int)w / s) * a.K + kc
-                        : nullptr;
+      }
+#pragma unroll
+      for (int j = 0; j < GRP; ++j) {
+        const int idx = (g0 + j) * NT + tid;
+        const int row = idx / CPR;
+        const int m = p0 + row;
+        const bool inb = m < a.M && kc < a.K;
+        if (EXACT || inb) {
+          uint4 v = *(const uint4*)(smem + row * OROW + chn * 16);
+          const size_t o = (size_t)m * a.K + kc;
+          if constexpr (SACC) {
+            if (inb) {
+              const float q[8] = {lo_bf(v.x), hi_bf(v.x), lo_bf(v.y), hi_bf(v.y),
+                                  lo_bf(v.z), hi_bf(v.z), lo_bf(v.w), hi_bf(v.w)};
+#pragma unroll
+              for (int e = 0; e < 8; ++e) { ssum[e] += q[e]; ssq[e] = fmaf(q[e], q[e], ssq[e]); }
             }
-            if (src) {
-              const uint4 r = *(const uint4*)src;
+          } else {
+            if (bstats && inb) {  // (sgx / sg double as the statistics accumulators: act is off here)
+              const float q[8] = {lo_bf(v.x), hi_bf(v.x), lo_bf(v.y), hi_bf(v.y),
+                                  lo_bf(v.z), hi_bf(v.z), lo_bf(v.w), hi_bf(v.w)};
+#pragma unroll
+              for (int e = 0; e < 8; ++e) { sgx[e] += q[e]; sg[e] = fmaf(q[e], q[e], sg[e]); }
+            }
+          }
+          if (inb && side) {
+            float f[8];
+            f[0] = lo_bf(v.x); f[1] = hi_bf(v.x); f[2] = lo_bf(v.y); f[3] = hi_bf(v.y);
+            f[4] = lo_bf(v.z); f[5] = hi_bf(v.z); f[6] = lo_bf(v.w); f[7] = hi_bf(v.w);
+            if (ph[j]) {
+              const uint4 r = pa[j];
               f[0] += lo_bf(r.x); f[1] += hi_bf(r.x); f[2] += lo_bf(r.y); f[3] += hi_bf(r.y);
               f[4] += lo_bf(r.z); f[5] += hi_bf(r.z); f[6] += lo_bf(r.w); f[7] += hi_bf(r.w);
             }
-          }
-          if (act) {
-            const uint4 xu = *(const uint4*)(a.act_x + o);
-            float xv[8];
-            xv[0] = lo_bf(xu.x); xv[1] = hi_bf(xu.x); xv[2] = lo_bf(xu.y); xv[3] = hi_bf(xu.y);
-            xv[4] = lo_bf(xu.z); xv[5] = hi_bf(xu.z); xv[6] = lo_bf(xu.w); xv[7] = hi_bf(xu.w);
+            if (act) {
+              const uint4 xu = px[j];
+              float xv[8];
+              xv[0] = lo_bf(xu.x); xv[1] = hi_bf(xu.x); xv[2] = lo_bf(xu.y); xv[3] = hi_bf(xu.y);
+              xv[4] = lo_bf(xu.z); xv[5] = hi_bf(xu.z); xv[6] = lo_bf(xu.w); xv[7] = hi_bf(xu.w);
+              if (amask) {
+                // block-output form: g = d(out) * bit, sums against the raw conv output (and the raw
+                // BN'd residual); out <- g (the producers' conv+BN backwards apply their scales)
+                const uint32_t mb = pm[j];
+                const uint4 ru = pr[j];
+                const float rv[8] = {lo_bf(ru.x), hi_bf(ru.x), lo_bf(ru.y), hi_bf(ru.y),
+                                     lo_bf(ru.z), hi_bf(ru.z), lo_bf(ru.w), hi_bf(ru.w)};
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float g = fmaf(xv[e], sc[e], sh[e]) > 0.f ? f[e] : 0.f;
-              sgx[e] += g * xv[e];
-              sg[e] += g;
-              f[e] = a.act_unscaled ? g : g * sc[e];
+                for (int e = 0; e < 8; ++e) {
+                  const float g = (mb >> e) & 1u ? f[e] : 0.f;
+                  sgx[e] += g * xv[e];
+                  sg[e] += g;
+                  sgr[e] += g * rv[e];  // (rv = 0 without a BN'd residual)
+                  f[e] = g;
+                }
+              } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                  const float g = fmaf(xv[e], sc[e], sh[e]) > 0.f ? f[e] : 0.f;
+                  sgx[e] += g * xv[e];
+                  sg[e] += g;
+                  f[e] = a.act_unscaled ? g : g * sc[e];
+                }
+              }
             }
+            v = make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
           }
-          v = make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
+          *(uint4*)(inb ? a.y + o : a.dump) = v;
         }
-        *(uint4*)(inb ? a.y + o : a.dump) = v;
       }
     }
     if (act || bstats) {
@@ -244,7 +306,8 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
       epi_barrier<RAWB>();
       // every thread finishes one (chunk column, value) output: NT/CPR partials each, instead of CPR
       // threads walking all NT rows of the table serially
-      float* prow = (act ? a.act_sums : a.stats) + (size_t)by * (2 * a.K);
+      const int rw = (act && a.act_r) ? 4 : 2;  // row width in K units
+      float* prow = (act ? a.act_sums : a.stats) + (size_t)by * (rw * a.K);
       for (int o = tid; o < CPR * 16; o += NT) {
         const int c = o >> 4, e = o & 15;
         float t = 0.f;
@@ -252,6 +315,20 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
         for (int k = 0; k < NT / CPR; ++k) t += red[((c + k * CPR) << 4) + e];
         const int kk = c0 + c * 8 + (e & 7);
         if (kk < a.K) prow[(e < 8 ? 0 : a.K) + kk] = t;
+      }
+      if (act && a.act_r) {  // second round: [sum g*r | sum g] of the BN'd residual
+        epi_barrier<RAWB>();
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { red[tid * 16 + e] = sgr[e]; red[tid * 16 + 8 + e] = sg[e]; }
+        epi_barrier<RAWB>();
+        for (int o = tid; o < CPR * 16; o += NT) {
+          const int c = o >> 4, e = o & 15;
+          float t = 0.f;
+#pragma unroll 4
+          for (int k = 0; k < NT / CPR; ++k) t += red[((c + k * CPR) << 4) + e];
+          const int kk = c0 + c * 8 + (e & 7);
+          if (kk < a.K) prow[2 * a.K + (e < 8 ? 0 : a.K) + kk] = t;
+        }
       }
     }
   }
@@ -1657,6 +1734,8 @@ struct TileCfg {
 };
 static int g_tile_env = -2;
 static int g_tile_w8 = 1;  // A/B knob: the 8-wave tile in the shape policy (dtm_conv_set_w8)
+static int g_stream_act = 1;  // A/B knob: the persistent streaming kernel also for act / block-output dgrads
+DTM_API void dtm_conv_set_stream_act(int on) { g_stream_act = on; }
 static int g_kwide = 1;    // A/B knob: 64-channel tiles for K % 128 in (0, 64] (dtm_conv_set_kwide)
 DTM_API void dtm_conv_set_kwide(int on) { g_kwide = on; }
 DTM_API void dtm_conv_set_w8(int on) { g_tile_w8 = on; }
@@ -1674,7 +1753,7 @@ static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
   // the pipelined LDS-DMA 128x128 tile (2 slots, 2 blocks/CU) wins every deep-reduction layer without the
   // prologue (tools/conv_tile_sweep.py: 3x3 at 14x14 / 7x7 -13..-18 %, deep 1x1 -5..-16 %)
   if (id == -4) id = -1;  // (-4: the policy without the streaming kernel, for A/B runs)
-  else if (id == -1 && a.Kg == 64 && stream_ok(a)) id = a.K >= 128 ? 30 : 31;
+  else if (id == -1 && a.Kg == 64 && stream_ok(a) && (g_stream_act || !a.act_x)) id = a.K >= 128 ? 30 : 31;
   // (the persistent streaming 1x1 kernel: the 64-deep 56x56 expand / reduce layers and their dgrads are
   // HBM streams: -20..-33 % (tools/conv_tile_sweep.py); at Kg 128 its 1 block/CU loses)
   // the 8-wave 256x256 tile (id 40) where it fills the chip: >= ~150 tiles (one round, 58-100 % of the
@@ -1763,6 +1842,7 @@ static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, cons
   a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.y = (bf16_t*)y;
   a.stats = nullptr; a.bias = bias; a.in_scale = in_scale; a.in_shift = in_shift;
   a.add_src = nullptr; a.act_x = nullptr; a.act_ss = nullptr; a.act_sums = nullptr;
+  a.act_mask = nullptr; a.act_r = nullptr;
   a.add_stride = 1; a.add_H = a.add_W = 0;
   a.act_unscaled = 0;
   a.zero = zero_chunk();
@@ -1826,9 +1906,32 @@ DTM_API int dtm_conv_fwd_bn(const void* x, const void* w, void* y, const float* 
 //   act_x [N][H][W][C] + act_ss [4][C] (scale, shift, ...): the input was relu(act_x*scale+shift)
 //   (BatchNorm+ReLU fused into this conv's forward prologue); dx <- [act_x*scale+shift>0]*dx*scale and
 //   act_sums[2][C] += (sum g*act_x, sum g) with g the masked gradient (the BN scale/shift grads).
+// Block-output form (dtm_conv_dgrad_bnout): the input of this conv was y = relu(bn(act_x) [+ bn(act_r) |
+// + identity]) with the ReLU mask kept as a bitmask; the epilogue applies that BN-apply's backward to
+// the total input gradient (dgrad + add_src): dx <- g = (dgrad + add_src) * bit, act_sums[4][C] +=
+// (sum g*act_x, sum g, sum g*act_r, sum g) - the separate bn_apply_bwd pass over the block output (read
+// d(out), mask and act_x, write g) disappears.
+static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvDesc* d, const void* add_src,
+                           int add_stride, const void* act_x, const float* act_ss, float* act_sums, int act_unscaled,
+                           const void* act_mask, const void* act_r, void* stream);
+
+DTM_API int dtm_conv_dgrad_bnout(const void* dy, const void* wt, void* dx, const ConvDesc* d, const void* add_src,
+                                 int add_stride, const void* mask, const void* x_raw, const void* r_raw, float* sums,
+                                 void* stream) {
+  if (!mask || !x_raw || !sums) return -7;
+  return conv_dgrad_impl(dy, wt, dx, d, add_src, add_stride, x_raw, nullptr, sums, 1, mask, r_raw, stream);
+}
+
 DTM_API int dtm_conv_dgrad_ex(const void* dy, const void* wt, void* dx, const ConvDesc* d, const void* add_src,
                               int add_stride, const void* act_x, const float* act_ss, float* act_sums,
                               int act_unscaled, void* stream) {
+  return conv_dgrad_impl(dy, wt, dx, d, add_src, add_stride, act_x, act_ss, act_sums, act_unscaled, nullptr, nullptr,
+                         stream);
+}
+
+static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvDesc* d, const void* add_src,
+                           int add_stride, const void* act_x, const float* act_ss, float* act_sums, int act_unscaled,
+                           const void* act_mask, const void* act_r, void* stream) {
   if (d->K % 8 || d->C % 4) return -1;
   if (add_stride < 1 || (add_stride > 1 && !add_src)) return -6;
   if (d->stride > 2) return -3;
@@ -1837,6 +1940,7 @@ DTM_API int dtm_conv_dgrad_ex(const void* dy, const void* wt, void* dx, const Co
   a.x = (const bf16_t*)dy; a.w = (const bf16_t*)wt; a.y = (bf16_t*)dx;
   a.stats = nullptr; a.bias = nullptr; a.in_scale = nullptr; a.in_shift = nullptr;
   a.add_src = (const bf16_t*)add_src; a.act_x = (const bf16_t*)act_x; a.act_ss = act_ss; a.act_sums = nullptr;
+  a.act_mask = (const uint8_t*)act_mask; a.act_r = (const bf16_t*)act_r;
   a.add_stride = add_stride;
   a.act_unscaled = act_unscaled;
   a.zero = zero_chunk();
@@ -1854,13 +1958,14 @@ DTM_API int dtm_conv_dgrad_ex(const void* dy, const void* wt, void* dx, const Co
   a.fd_PQ = make_fastdiv(d->H * d->W); a.fd_Q = make_fastdiv(d->W);
   const TileCfg tc = pick_tile(a);
   const int rows = (a.M + tc.PT - 1) / tc.PT;  // pixel tiles
+  const int rw = act_r ? 4 : 2;
   if (act_x) {
-    float* ws = dtm_ws_get((size_t)rows * 2 * d->C);
+    float* ws = dtm_ws_get((size_t)rows * rw * d->C);
     if (!ws) return -4;
     a.act_sums = ws;
   }
   dispatch_nt(a, d->stride, tc, (hipStream_t)stream);
-  if (act_x) dtm_reduce_rows(a.act_sums, rows, 2 * d->C, 2 * d->C, act_sums, (hipStream_t)stream);
+  if (act_x) dtm_reduce_rows(a.act_sums, rows, rw * d->C, rw * d->C, act_sums, (hipStream_t)stream);
   return 0;
 }
 

@@ -43,6 +43,7 @@ _SIGS = {
     "dtm_reflect_pad_bwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "dtm_conv_dgrad": (_I, [_P, _P, _P, ctypes.POINTER(ConvDesc), _P]),
     "dtm_conv_dgrad_ex": (_I, [_P, _P, _P, ctypes.POINTER(ConvDesc), _P, _I, _P, _P, _P, _I, _P]),
+    "dtm_conv_dgrad_bnout": (_I, [_P, _P, _P, ctypes.POINTER(ConvDesc), _P, _I, _P, _P, _P, _P, _P]),
     "dtm_conv_wgrad": (_I, [_P, _P, _P, _P, _P, ctypes.POINTER(ConvDesc), _I, _P]),
     "dtm_weight_flip_transpose": (None, [_P, _P, _I, _I, _I, _I, _P]),
     "dtm_weight_flip_transpose_batched": (None, [_P, _I, _P]),
@@ -95,6 +96,7 @@ _SIGS = {
     "dtm_conv_set_w8": (None, [_I]),
     "dtm_conv_set_kwide": (None, [_I]),
     "dtm_set_reduce_few": (None, [_I]),
+    "dtm_conv_set_stream_act": (None, [_I]),
     "dtm_dropout": (_I, [_P, _P, _L, _I, _F, ctypes.c_ulonglong, _P, _P]),
     "dtm_in_top_k": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
 }

@@ -78,6 +78,26 @@ class _GradSlot:
         self.shape = tuple(shape)
 
 
+class _BNOutInfo:
+    """Block-output BN-apply y = relu(x*scale+shift [+ res]) whose backward can run inside the dgrad
+    epilogue of the conv that consumes y last (dtm_conv_dgrad_bnout): that conv writes g = d(y) * mask
+    and the scale/shift gradient sums; the BN-apply's own backward then only hands them on."""
+    __slots__ = ("mask", "x", "r", "sums", "g")
+
+    def __init__(self, mask, x, r):
+        self.mask, self.x, self.r = mask, x, r
+        self.sums = None  # [4, C]: sum g*x, sum g, sum g*r, sum g  (set by the fusing dgrad)
+        self.g = None     # the tensor the fusing dgrad returned
+
+
+BNOUT_FUSED = [0]  # count of block-output BN backwards absorbed by a dgrad epilogue (tests / diagnostics)
+
+
+def _bnout_enabled():
+    import os
+    return os.environ.get("DTM_BNOUT_FUSE", "1") != "0"
+
+
 def _slot_register(x):
     if not (torch.is_grad_enabled() and x.requires_grad and x.is_cuda):
         return None
@@ -161,6 +181,9 @@ class _ConvBNFn(torch.autograd.Function):
         ctx.geom = geom
         ctx.slot = slot
         ctx.in_unscaled = bool(in_unscaled)
+        # the input is a block output whose BN-apply backward this conv's dgrad can absorb (if it turns
+        # out to be the input's last consumer)
+        ctx.bnout = getattr(x, "_dtm_bnout", None) if (in_ss is None and x_mat is None) else None
         ctx.has_gamma, ctx.has_beta = gamma is not None, beta is not None
         ctx.save_for_backward(x, in_ss, w, y, ss, gamma, beta, x_raw)
         if ss is None:
@@ -220,9 +243,22 @@ class _ConvBNFn(torch.autograd.Function):
                 # a tensor read by k consumers costs no separate add at all; a non-last consumer
                 # then leaves its (now cumulative) gradient as the new stash
                 use_add = add_src is not None
-                _check(L.dtm_conv_dgrad_ex(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d),
-                                           _lib.ptr(add_src) if use_add else None, add_stride if use_add else 1,
-                                           None, None, None, 0, s), "conv_dgrad")
+                info = ctx.bnout
+                if last and info is not None and info.sums is None and tuple(info.x.shape) == tuple(dx.shape):
+                    # last consumer of a block output: the BN-apply backward (mask, scale/shift sums)
+                    # runs in this dgrad's epilogue; the BN-apply node just hands the results on
+                    sums = arena.zeros((4, g.C), dy.device)
+                    _check(L.dtm_conv_dgrad_bnout(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d),
+                                                  _lib.ptr(add_src) if use_add else None,
+                                                  add_stride if use_add else 1, _lib.ptr(info.mask),
+                                                  _lib.ptr(info.x), _lib.ptr(info.r), _lib.ptr(sums), s),
+                           "conv_dgrad_bnout")
+                    info.sums, info.g = sums, dx
+                    BNOUT_FUSED[0] += 1
+                else:
+                    _check(L.dtm_conv_dgrad_ex(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d),
+                                               _lib.ptr(add_src) if use_add else None, add_stride if use_add else 1,
+                                               None, None, None, 0, s), "conv_dgrad")
                 if not last:
                     ctx.slot.buf, ctx.slot.stride = dx, 1
                     dx = None
@@ -285,7 +321,8 @@ class _BNApplyFn(torch.autograd.Function):
         M = x.numel() // C
         y = torch.empty_like(x)
         res_mode = 0 if res is None else (2 if res_ss is not None else 1)
-        want_mask = relu and torch.is_grad_enabled() and C % 8 == 0
+        # (grad mode is off inside Function.forward: whether a backward will run is needs_input_grad)
+        want_mask = relu and any(ctx.needs_input_grad) and C % 8 == 0
         mask = torch.empty(M * C // 8, device=x.device, dtype=torch.uint8) if want_mask else None
         if res_stride > 1:
             N, Ho, Wo, _ = x.shape
@@ -301,6 +338,16 @@ class _BNApplyFn(torch.autograd.Function):
                                 res_mode, int(relu), _lib.stream_ptr())
         ctx.relu, ctx.res_mode, ctx.res_slot, ctx.res_stride = relu, res_mode, res_slot, res_stride
         ctx.unscaled = int(unscaled) if res_mode == 2 else int(unscaled) & 1
+        # eligible for the dgrad-epilogue backward: bitmask ReLU, unstrided residual, and every gradient
+        # this backward hands out equal to g itself (unscaled producers)
+        ctx.bnout = None
+        if (mask is not None and relu and res_stride == 1 and (ctx.unscaled & 1) and
+                (res_mode != 2 or (ctx.unscaled & 2)) and C % 8 == 0 and _bnout_enabled()):
+            ctx.bnout = _BNOutInfo(mask, x, res if res_mode == 2 else None)
+            try:
+                y._dtm_bnout = ctx.bnout
+            except Exception:
+                ctx.bnout = None
         ctx.res_shape = None if res is None else tuple(res.shape)
         # the residual itself is only read back for a BN'd residual (res_mode 2)
         ctx.save_for_backward(x, ss, res if res_mode == 2 else None, res_ss,
@@ -314,16 +361,45 @@ class _BNApplyFn(torch.autograd.Function):
         C = x.shape[-1]
         M = x.numel() // C
         ux, ur = bool(ctx.unscaled & 1), bool(ctx.unscaled & 2)
-        dx = torch.empty_like(x)
         # dres aliases dx when both are g (identity residual with an unscaled x, or both BN'd unscaled)
         alias = (ctx.res_mode == 1 and ux) or (ctx.res_mode == 2 and ux and ur)
-        dres = None if not ctx.res_mode else (dx if alias else torch.empty_like(x))
-        sx = arena.zeros((4, C), x.device)
-        sr = arena.zeros((4, C), x.device) if ctx.res_mode == 2 else None
-        mode = 3 if mask is not None else (1 if ctx.relu else 0)
-        _check(L.dtm_bn_apply_bwd(_lib.ptr(dy.contiguous()), _lib.ptr(y), _lib.ptr(mask), _lib.ptr(x), _lib.ptr(ss),
-                                  _lib.ptr(res), _lib.ptr(rss), _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(sx), _lib.ptr(sr),
-                                  M, C, mode, ctx.res_mode, ctx.unscaled, _lib.stream_ptr()), "bn_apply_bwd")
+        info = ctx.bnout
+        if info is not None and info.sums is not None:
+            # the consuming conv's dgrad epilogue already applied this backward: dy is g (= d(y) * mask)
+            sx = arena.zeros((4, C), x.device)
+            sx[:2].copy_(info.sums[:2])
+            sr = None
+            if ctx.res_mode == 2:
+                sr = arena.zeros((4, C), x.device)
+                sr[:2].copy_(info.sums[2:])
+            dx = info.g
+            if dy.data_ptr() != dx.data_ptr():
+                # another (non-hand-off) consumer of y added its gradient: push the remainder through
+                # the regular kernel (masking is linear) and add it
+                rest = (dy.float() - dx.float()).to(dx.dtype).contiguous()
+                dx2 = torch.empty_like(x)
+                sx2 = arena.zeros((4, C), x.device)
+                sr2 = arena.zeros((4, C), x.device) if ctx.res_mode == 2 else None
+                _check(L.dtm_bn_apply_bwd(_lib.ptr(rest), None, _lib.ptr(mask), _lib.ptr(x), _lib.ptr(ss),
+                                          _lib.ptr(res), _lib.ptr(rss), _lib.ptr(dx2), _lib.ptr(dx2), _lib.ptr(sx2),
+                                          _lib.ptr(sr2), M, C, 3, ctx.res_mode, ctx.unscaled, _lib.stream_ptr()),
+                       "bn_apply_bwd")
+                dx = dx + dx2
+                sx = sx + sx2
+                if sr is not None:
+                    sr = sr + sr2
+            info.g = info.sums = None
+            dres = None if not ctx.res_mode else dx
+        else:
+            dx = torch.empty_like(x)
+            dres = None if not ctx.res_mode else (dx if alias else torch.empty_like(x))
+            sx = arena.zeros((4, C), x.device)
+            sr = arena.zeros((4, C), x.device) if ctx.res_mode == 2 else None
+            mode = 3 if mask is not None else (1 if ctx.relu else 0)
+            _check(L.dtm_bn_apply_bwd(_lib.ptr(dy.contiguous()), _lib.ptr(y), _lib.ptr(mask), _lib.ptr(x),
+                                      _lib.ptr(ss), _lib.ptr(res), _lib.ptr(rss), _lib.ptr(dx), _lib.ptr(dres),
+                                      _lib.ptr(sx), _lib.ptr(sr), M, C, mode, ctx.res_mode, ctx.unscaled,
+                                      _lib.stream_ptr()), "bn_apply_bwd")
         st = ctx.res_stride
         if ctx.res_slot is not None:
             last, buf, bst = _slot_take(ctx.res_slot)

@@ -221,3 +221,38 @@ def test_stem_packed_row_conv_bn(H, W, C, N):
                 mv=_rel(bn.moving_variance, bn_r.moving_variance))
     # same bf16 ReLU-mask flip noise on dgamma / dbeta / dw as test_conv_bn_single (tol 5e-2 with relu)
     assert all(v < 5e-2 for v in errs.values()), errs
+
+
+def test_block_output_bn_backward_in_dgrad_epilogue(monkeypatch):
+    """ResNet-50 v1: the block-output BN-apply backward (mask, d(scale)/d(shift) sums, the residual's
+    share) runs inside the dgrad epilogue of the conv that consumes the block output last; every
+    gradient matches the separate bn_apply_bwd pass."""
+    from distributed_tensorflow_models_amd.models import nets_factory
+    torch.manual_seed(0)
+    net = nets_factory.build("resnet_v1_50", num_classes=10).to(DEV)
+    x = torch.randn(4, 64, 64, 3, device=DEV).to(torch.bfloat16)
+    y = torch.randint(0, 10, (4,), device=DEV)
+    from distributed_tensorflow_models_amd.ops import nn as F
+    grads = {}
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("DTM_BNOUT_FUSE", fuse)
+        for p in net.parameters():
+            p.grad = None
+        n0 = fused.BNOUT_FUSED[0]
+        loss = F.softmax_cross_entropy(net(x, training=True), y).mean()
+        loss.backward()
+        torch.cuda.synchronize()
+        grads[fuse] = {n: p.grad.detach().float().clone() for n, p in net.named_parameters() if p.grad is not None}
+        if fuse == "1":
+            assert fused.BNOUT_FUSED[0] - n0 >= 12  # every block output consumed by a conv (16 units - 4)
+    assert grads["0"].keys() == grads["1"].keys()
+    # The two paths differ only in rounding: the separate pass rounds d(out) to bf16 before masking and sums
+    # the bf16 g, the epilogue masks and sums the fp32 value.  The difference is ~0.4 % at the first fused
+    # unit and accumulates ~0.15 % per unit towards the stem (tools/diag_bnout.py; an indexing or mask bug
+    # shows up at full size at the first fused unit).  The stem BN's beta gradient (a cancelling sum over
+    # the whole image) is excluded.
+    errs = {k: _rel(grads["1"][k], grads["0"][k]) for k in grads["0"] if k.startswith("units.")}
+    assert max(v for k, v in errs.items() if k.startswith(("units.14.", "units.13."))) < 1e-2, errs
+    worst = max((v, k) for k, v in errs.items())
+    assert worst[0] < 3.5e-2, worst
+    assert sorted(errs.values())[len(errs) // 2] < 1.5e-2
