@@ -135,6 +135,23 @@ def main():
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    phases = {}
+    if world > 1 and not cpu and not args.graph:
+        # after (outside) the timed region: 3 steps with HIP events on the compute stream.  The
+        # "allreduce" section runs from the last backward kernel to the moment the compute stream
+        # may proceed past every bucket's collective = the exposed (non-overlapped) all-reduce time.
+        from distributed_tensorflow_models_amd.utils.metrics import StepTimer
+        step.timer, acc = StepTimer(cuda=True), {}
+        for _ in range(3):
+            step(images, labels)
+            for k, v in step.timer.sections().items():
+                acc[k] = acc.get(k, 0.0) + v / 3
+        step.timer = None
+        t = torch.tensor([acc.get(k, 0.0) for k in ("fwd_ms", "bwd_ms", "allreduce_ms", "optimizer_ms")],
+                         device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        phases = dict(zip(("fwd_ms", "bwd_ms", "allreduce_exposed_ms", "optimizer_ms"),
+                          [round(float(v), 3) for v in t.tolist()]))
     ms = dt / args.steps * 1000.0
     value = world * B * args.steps / dt
     if rank == 0:
@@ -160,6 +177,8 @@ def main():
                        # excluded: parallel/bsp.py compact buckets)
                        "grad_wire_mb": round(step.dp.wire_elements() * (2 if args.grad_comm == "bf16" else 4) / 1e6,
                                              1),
+                       # max over ranks, measured after the timed steps (N > 1 only)
+                       "phases_ms": phases or None,
                        "optimizer": {"momentum": "momentum-sgd+wd", "rmsprop": "rmsprop(TF)+wd", "sgd": "sgd+wd"}[opt],
                        "final_loss": round(float(loss), 4) if math.isfinite(float(loss)) else None},
         }
