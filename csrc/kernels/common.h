@@ -112,3 +112,23 @@ __device__ __forceinline__ void col_reduce8(float (*red)[256][8], const float* s
     }
   }
 }
+
+namespace dtm {
+// BatchNorm finalize backward of one channel (bn_finalize_bwd_kernel's algebra): from dss = [dscale;
+// dshift; dmean; drstd], ss = [scale; shift; mean; rstd] and gamma -> the statistics gradient
+// (ds = d/dsum, dq = d/dsumsq, divided by the count) and the parameter gradients dg, db.
+__device__ __forceinline__ void fin_bwd_channel(const float* dss, const float* ss, const float* gamma, int C, int c,
+                                                float count, float* ds, float* dq, float* dg, float* db) {
+  const float scale = ss[c], mean = ss[2 * C + c], rstd = ss[3 * C + c];
+  const float g = gamma ? gamma[c] : 1.f;
+  const float dsc = dss[c], dsh = dss[C + c];
+  const float dscale_tot = dsc - dsh * mean;
+  const float dmean = dss[2 * C + c] - dsh * scale;
+  const float drstd = dss[3 * C + c] + dscale_tot * g;
+  const float dvar = drstd * (-0.5f) * rstd * rstd * rstd;
+  *ds = dmean / count - dvar * 2.f * mean / count;
+  *dq = dvar / count;
+  *dg = dscale_tot * rstd;
+  *db = dsh;
+}
+}  // namespace dtm

@@ -179,24 +179,8 @@ __global__ __launch_bounds__(256) void stats_combine_kernel(const bf16_t* __rest
   }
 }
 
-// stats_combine with the finalize backward folded in: the per-channel (dsum, dsumsq) are computed
-// from dss = [dscale; dshift; dmean; drstd], ss = [scale; shift; mean; rstd] and gamma in registers
-// (bn_finalize_bwd_kernel's algebra), and block 0 accumulates dgamma / dbeta.
-__device__ __forceinline__ void fin_bwd_channel(const float* dss, const float* ss, const float* gamma, int C, int c,
-                                                float count, float* ds, float* dq, float* dg, float* db) {
-  const float scale = ss[c], mean = ss[2 * C + c], rstd = ss[3 * C + c];
-  const float g = gamma ? gamma[c] : 1.f;
-  const float dsc = dss[c], dsh = dss[C + c];
-  const float dscale_tot = dsc - dsh * mean;
-  const float dmean = dss[2 * C + c] - dsh * scale;
-  const float drstd = dss[3 * C + c] + dscale_tot * g;
-  const float dvar = drstd * (-0.5f) * rstd * rstd * rstd;
-  *ds = dmean / count - dvar * 2.f * mean / count;
-  *dq = dvar / count;
-  *dg = dscale_tot * rstd;
-  *db = dsh;
-}
-
+// stats_combine with the finalize backward folded in: the per-channel (dsum, dsumsq) come from
+// fin_bwd_channel (common.h) in registers, and block 0 accumulates dgamma / dbeta.
 // U rows in flight per lane; NT: non-temporal loads / stores (streamed once, keep L2/MALL for others)
 template <int U, bool NT, bool NTS = NT>
 __global__ __launch_bounds__(256) void stats_combine_fin_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,

@@ -201,6 +201,10 @@ class _ConvBNFn(torch.autograd.Function):
         M_out = g.N * g.P * g.Q
         dy = dy.contiguous()
         dgamma = dbeta = None
+        if ss is not None and dss is not None and in_ss is not None and _bwd1x1_ok(ctx, g):
+            out = _ConvBNFn._backward_1x1_fused(ctx, dy, dss, x_raw, in_ss, w, y, ss, gamma, beta)
+            if out is not None:
+                return out
         if ss is not None and dss is not None:
             gmg = getattr(gamma, "main_grad", None) if gamma is not None else None
             bmg = getattr(beta, "main_grad", None) if beta is not None else None
@@ -275,6 +279,49 @@ class _ConvBNFn(torch.autograd.Function):
         else:
             dw = None
         return dx, d_in, dw, dgamma, dbeta, None, None, None, None, None
+
+
+    @staticmethod
+    def _backward_1x1_fused(ctx, dy, dss, x_raw, in_ss, w, y, ss, gamma, beta):
+        """Stats-combine + dgrad (input BN+ReLU backward) + wgrad of a 1x1 conv+BN in one pass over
+        dy / y (dtm_conv1x1_bnbwd).  Returns the backward's outputs, or None if the kernel declines."""
+        L = _lib.lib()
+        s = _lib.stream_ptr()
+        g = ctx.geom
+        gmg = getattr(gamma, "main_grad", None) if gamma is not None else None
+        bmg = getattr(beta, "main_grad", None) if beta is not None else None
+        dgamma = torch.zeros(g.K, device=dy.device) if (gamma is not None and gmg is None) else None
+        dbeta = torch.zeros(g.K, device=dy.device) if (beta is not None and bmg is None) else None
+        wt = weight_flipped(w, g.K, g.R, g.S, g.C)  # 1x1: [C][K] = W transposed
+        dx = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
+        d_in = arena.zeros((4, g.C), dy.device)
+        mg = getattr(w, "main_grad", None)
+        target = mg if mg is not None else torch.zeros(w.shape, device=dy.device, dtype=torch.float32)
+        rc = L.dtm_conv1x1_bnbwd(_lib.ptr(dy), _lib.ptr(y), _lib.ptr(dss.contiguous()), _lib.ptr(ss),
+                                 _lib.ptr(gamma), ctx.count, _lib.ptr(gmg if gmg is not None else dgamma),
+                                 _lib.ptr(bmg if bmg is not None else dbeta), _lib.ptr(wt), _lib.ptr(x_raw),
+                                 _lib.ptr(in_ss), int(ctx.in_unscaled), _lib.ptr(dx), _lib.ptr(d_in),
+                                 _lib.ptr(target), g.N * g.P * g.Q, g.K, g.C, s)
+        if rc == -1:
+            return None
+        _check(rc, "conv1x1_bnbwd")
+        _slot_take(ctx.slot)  # (the activation-input path takes no stashed gradient)
+        BWD1X1_FUSED[0] += 1
+        for p, m in ((gamma, gmg), (beta, bmg), (w, mg)):
+            if m is not None:
+                _notify(p)
+        return dx, d_in, (None if mg is not None else target), dgamma, dbeta, None, None, None, None, None
+
+
+BWD1X1_FUSED = [0]  # count of 1x1 conv+BN backwards done by the one-pass kernel (tests / diagnostics)
+
+
+def _bwd1x1_ok(ctx, g):
+    """The one-pass 1x1 backward covers the ResNet bottleneck expansion shape (64 -> 256 channels)."""
+    import os
+    return (os.environ.get("DTM_BWD1X1_FUSE", "1") != "0" and g.R == 1 and g.S == 1 and g.stride == 1 and
+            g.pad_h == 0 and g.pad_w == 0 and g.P == g.H and g.Q == g.W and g.K == 256 and g.C == 64 and
+            ctx.needs_input_grad[0] and ctx.needs_input_grad[2])
 
 
 class _BNFinalizeFn(torch.autograd.Function):

@@ -256,3 +256,54 @@ def test_block_output_bn_backward_in_dgrad_epilogue(monkeypatch):
     worst = max((v, k) for k, v in errs.items())
     assert worst[0] < 3.5e-2, worst
     assert sorted(errs.values())[len(errs) // 2] < 1.5e-2
+
+
+@pytest.mark.parametrize("N,H,relu", [(2, 14, True), (4, 8, True), (2, 9, True)])
+def test_conv1x1_bn_backward_one_pass(monkeypatch, N, H, relu):
+    """The bottleneck expansion backward (BN stats-combine + dgrad with the input BN+ReLU backward +
+    wgrad of a 1x1 64->256 conv+BN) in one pass over d(out) and the raw conv output
+    (dtm_conv1x1_bnbwd) against the fp32 reference through the kernels' own masks, and against the
+    three-kernel path.  M = N*H*H covers a partial last 64-pixel tile."""
+    torch.manual_seed(3)
+    C, K = 64, 256
+    x = torch.randn(N, H, H, C, device=DEV).to(torch.bfloat16).float()
+    w1 = (torch.randn(C, 3, 3, C, device=DEV) / (9 * C) ** 0.5).to(torch.bfloat16).float()
+    w2 = (torch.randn(K, 1, 1, C, device=DEV) / C ** 0.5).to(torch.bfloat16).float()
+    bn1, bn2 = _bn(C), _bn(K)
+    gy = None
+    res = {}
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("DTM_BWD1X1_FUSE", fuse)
+        for b in (bn1, bn2):
+            for p in b.parameters():
+                p.grad = None
+        xk = x.to(torch.bfloat16).requires_grad_()
+        w1k, w2k = w1.clone().requires_grad_(), w2.clone().requires_grad_()
+        l1 = fused.conv_bn(xk, w1k, bn1, 1, "SAME", True, relu)
+        m1 = ((l1.raw.detach().float() * l1.ss[0] + l1.ss[1]) > 0).float() if relu else None
+        l2 = fused.conv_bn(l1, w2k, bn2, 1, "SAME", True, False)
+        yk = l2.materialize()
+        if gy is None:
+            gy = torch.randn_like(yk.float()).to(torch.bfloat16)
+        n0 = fused.BWD1X1_FUSED[0]
+        yk.backward(gy)
+        torch.cuda.synchronize()
+        # (a linear input BN is materialised, not an activation input: that conv keeps the 3-kernel path)
+        assert fused.BWD1X1_FUSED[0] - n0 == (1 if (fuse == "1" and relu) else 0)
+        res[fuse] = dict(dx=xk.grad.float(), dw1=w1k.grad.float(), dw2=w2k.grad.float(),
+                         dg1=bn1.gamma.grad.float().clone(), db1=bn1.beta.grad.float().clone(),
+                         dg2=bn2.gamma.grad.float().clone(), db2=bn2.beta.grad.float().clone())
+    xr, w1r, w2r = (t.clone().requires_grad_() for t in (x, w1, w2))
+    g1, b1 = bn1.gamma.detach().clone().requires_grad_(), bn1.beta.detach().clone().requires_grad_()
+    g2, b2 = bn2.gamma.detach().clone().requires_grad_(), bn2.beta.detach().clone().requires_grad_()
+    a1 = ref.batch_norm(ref.conv2d(xr, w1r), g1, b1, None, None, True, 0.9, 1e-3, False)
+    if relu:
+        a1 = a1 * m1
+    yr = ref.batch_norm(ref.conv2d(a1, w2r), g2, b2, None, None, True, 0.9, 1e-3, False)
+    yr.backward(gy.float())
+    refs = dict(dx=xr.grad, dw1=w1r.grad, dw2=w2r.grad, dg1=g1.grad, db1=b1.grad, dg2=g2.grad, db2=b2.grad)
+    e_ref = {k: _rel(res["1"][k], refs[k]) for k in refs}
+    e_pair = {k: _rel(res["1"][k], res["0"][k]) for k in refs}
+    assert all(v < 2e-2 for v in e_ref.values()), e_ref
+    # same math, different summation order / one bf16 rounding fewer
+    assert all(v < 1e-2 for v in e_pair.values()), e_pair
