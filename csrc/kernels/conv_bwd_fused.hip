@@ -40,6 +40,7 @@ struct Bwd1x1Args {
   const bf16_t* x;       // [M][CI] raw input of the conv's input BatchNorm+ReLU
   const float* xss;      // [4][CI] its scale, shift
   int x_unscaled;        // the input gradient is g2 (1) or g2*scale (0)
+  const bf16_t* add_src; // plain mode: [M][CI] gradient of x from its other consumer, added (or nullptr)
   bf16_t* dx;            // [M][CI] out
   float* sums;           // [blocks][2][CI] partial (sum g2*x, sum g2)
   float* slab;           // [blocks][KO][CI] weight-gradient partials
@@ -73,7 +74,9 @@ struct Bwd1x1Smem {
   static constexpr int BYTES = XS + 2 * CI * 4;
 };
 
-template <int KO, int CI>
+// ACT: the conv input is relu(x*xs+xt) (recomputed; its backward in the dgrad epilogue); else the conv
+// input is x itself (plain mode: the dgrad epilogue adds add_src)
+template <int KO, int CI, bool ACT>
 __global__ __launch_bounds__(512) void conv1x1_bnbwd_kernel(Bwd1x1Args a) {
   using L = Bwd1x1Smem<KO, CI>;
   constexpr int PT = L::PT;
@@ -109,8 +112,8 @@ __global__ __launch_bounds__(512) void conv1x1_bnbwd_kernel(Bwd1x1Args a) {
     }
   }
   for (int c = tid; c < CI; c += 512) {
-    s_xs[c] = a.xss[c];
-    s_xh[c] = a.xss[CI + c];
+    s_xs[c] = ACT ? a.xss[c] : 1.f;
+    s_xh[c] = ACT ? a.xss[CI + c] : 0.f;
   }
   for (int q = tid; q < CI * KCH; q += 512) {
     const int c = q / KCH, k = (q % KCH) * 8;
@@ -185,7 +188,7 @@ __global__ __launch_bounds__(512) void conv1x1_bnbwd_kernel(Bwd1x1Args a) {
     {
       float av[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) av[e] = pb + xp < a.M ? fmaxf(fmaf(xv[e], xs[e], xh[e]), 0.f) : 0.f;
+      for (int e = 0; e < 8; ++e) av[e] = pb + xp < a.M ? (ACT ? fmaxf(fmaf(xv[e], xs[e], xh[e]), 0.f) : xv[e]) : 0.f;
       *(uint4*)(s_xa + img_off<CI>(xp, xc)) =
           make_uint4(pack2bf(av[0], av[1]), pack2bf(av[2], av[3]), pack2bf(av[4], av[5]), pack2bf(av[6], av[7]));
     }
@@ -244,7 +247,16 @@ __global__ __launch_bounds__(512) void conv1x1_bnbwd_kernel(Bwd1x1Args a) {
       float f[8];
       f[0] = lo_bf(v.x); f[1] = hi_bf(v.x); f[2] = lo_bf(v.y); f[3] = hi_bf(v.y);
       f[4] = lo_bf(v.z); f[5] = hi_bf(v.z); f[6] = lo_bf(v.w); f[7] = hi_bf(v.w);
-      if (pb + xp < a.M) {
+      if (!ACT && pb + xp < a.M) {
+        if (a.add_src) {
+          const uint4 r = *(const uint4*)(a.add_src + (size_t)(pb + xp) * CI + xc);
+          f[0] += lo_bf(r.x); f[1] += hi_bf(r.x); f[2] += lo_bf(r.y); f[3] += hi_bf(r.y);
+          f[4] += lo_bf(r.z); f[5] += hi_bf(r.z); f[6] += lo_bf(r.w); f[7] += hi_bf(r.w);
+        }
+        *(uint4*)(a.dx + (size_t)(pb + xp) * CI + xc) =
+            make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
+      }
+      if (ACT && pb + xp < a.M) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float gg = fmaf(xv[e], xs[e], xh[e]) > 0.f ? f[e] : 0.f;
@@ -268,6 +280,7 @@ __global__ __launch_bounds__(512) void conv1x1_bnbwd_kernel(Bwd1x1Args a) {
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) slab[(size_t)(wave * 32 + i * 16 + 4 * g + r) * CI + j * 16 + li] = accw[i][j][r];
+  if constexpr (!ACT) return;
   __syncthreads();  // s_dy free
   float* red = (float*)s_dy;  // [512][16]
 #pragma unroll
@@ -290,7 +303,7 @@ static int bwd1x1_blocks(int ntiles) {
   static int cap = 0;
   if (!cap) {
     int occ = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv1x1_bnbwd_kernel<256, 64>, 512, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv1x1_bnbwd_kernel<256, 64, true>, 512, 0) != hipSuccess ||
         occ <= 0)
       occ = 1;
     hipGetDevice(&dev);
@@ -304,25 +317,28 @@ static int bwd1x1_blocks(int ntiles) {
 // g: gradient of the BN output (unscaled), y: raw conv output, dss/ss/gamma: the BN's ss gradient and
 // forward ss, wt: [C][K] transposed weight, x/xss: the input BN's raw input and ss.  Outputs: dx
 // ([M][C] input gradient, masked), sums[2][C] += (sum dx*x, sum dx) (unscaled form), dw[K][C] +=,
-// dgamma/dbeta +=.  Returns -1 for a shape this kernel does not cover (the caller falls back).
+// dgamma/dbeta +=.  xss == nullptr: plain mode, the conv input is x itself; dx = dgrad (+ add_src) and
+// sums is untouched.  Returns -1 for a shape this kernel does not cover (the caller falls back).
 DTM_API int dtm_conv1x1_bnbwd(const void* g, const void* y, const float* dss, const float* ss, const float* gamma,
                               float count, float* dgamma, float* dbeta, const void* wt, const void* x,
-                              const float* xss, int x_unscaled, void* dx, float* sums, float* dw, long M, int K, int C,
-                              void* stream) {
+                              const float* xss, int x_unscaled, const void* add_src, void* dx, float* sums, float* dw,
+                              long M, int K, int C, void* stream) {
   if (K != 256 || C != 64 || M <= 0 || M * (long)K >= (1l << 31)) return -1;
-  if (((uintptr_t)g | (uintptr_t)y | (uintptr_t)wt | (uintptr_t)x | (uintptr_t)dx) & 15) return -1;
+  if (((uintptr_t)g | (uintptr_t)y | (uintptr_t)wt | (uintptr_t)x | (uintptr_t)dx | (uintptr_t)add_src) & 15) return -1;
+  if (xss && !sums) return -1;
   Bwd1x1Args a;
   a.g = (const bf16_t*)g; a.y = (const bf16_t*)y; a.dss = dss; a.ss = ss; a.gamma = gamma; a.count = count;
   a.dgamma = dgamma; a.dbeta = dbeta; a.wt = (const bf16_t*)wt; a.x = (const bf16_t*)x; a.xss = xss;
-  a.x_unscaled = x_unscaled; a.dx = (bf16_t*)dx; a.M = (int)M;
+  a.x_unscaled = x_unscaled; a.dx = (bf16_t*)dx; a.M = (int)M; a.add_src = (const bf16_t*)add_src;
   a.ntiles = (int)((M + 63) / 64);
   const int blocks = bwd1x1_blocks(a.ntiles);
   float* ws = dtm_ws_get((size_t)blocks * (K * C + 2 * C));
   if (!ws) return -4;
   a.slab = ws;
   a.sums = ws + (size_t)blocks * K * C;
-  hipLaunchKernelGGL((conv1x1_bnbwd_kernel<256, 64>), dim3(blocks), dim3(512), 0, (hipStream_t)stream, a);
+  if (xss) hipLaunchKernelGGL((conv1x1_bnbwd_kernel<256, 64, true>), dim3(blocks), dim3(512), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL((conv1x1_bnbwd_kernel<256, 64, false>), dim3(blocks), dim3(512), 0, (hipStream_t)stream, a);
   dtm_reduce_rows(a.slab, blocks, K * C, K * C, dw, (hipStream_t)stream);
-  dtm_reduce_rows(a.sums, blocks, 2 * C, 2 * C, sums, (hipStream_t)stream);
+  if (xss) dtm_reduce_rows(a.sums, blocks, 2 * C, 2 * C, sums, (hipStream_t)stream);
   return 0;
 }

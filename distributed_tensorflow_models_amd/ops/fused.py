@@ -201,7 +201,7 @@ class _ConvBNFn(torch.autograd.Function):
         M_out = g.N * g.P * g.Q
         dy = dy.contiguous()
         dgamma = dbeta = None
-        if ss is not None and dss is not None and in_ss is not None and _bwd1x1_ok(ctx, g):
+        if ss is not None and dss is not None and _bwd1x1_ok(ctx, g):
             out = _ConvBNFn._backward_1x1_fused(ctx, dy, dss, x_raw, in_ss, w, y, ss, gamma, beta)
             if out is not None:
                 return out
@@ -283,29 +283,45 @@ class _ConvBNFn(torch.autograd.Function):
 
     @staticmethod
     def _backward_1x1_fused(ctx, dy, dss, x_raw, in_ss, w, y, ss, gamma, beta):
-        """Stats-combine + dgrad (input BN+ReLU backward) + wgrad of a 1x1 conv+BN in one pass over
-        dy / y (dtm_conv1x1_bnbwd).  Returns the backward's outputs, or None if the kernel declines."""
+        """Stats-combine + dgrad + wgrad of a 1x1 conv+BN in one pass over dy / y (dtm_conv1x1_bnbwd).
+        With an activation input (in_ss) the dgrad epilogue does that BN+ReLU backward; with a plain
+        input it adds the input's stashed gradient (_GradSlot) instead.  Returns the backward's
+        outputs, or None if the kernel declines (the caller runs the three-kernel path)."""
+        g = ctx.geom
+        act = in_ss is not None
+        add_src = None
+        if not act:
+            sl = ctx.slot
+            if ctx.bnout is not None or (sl is not None and sl.buf is not None and sl.stride != 1):
+                return None  # (block-output input: the dgrad-epilogue BN-apply backward wins)
         L = _lib.lib()
         s = _lib.stream_ptr()
-        g = ctx.geom
         gmg = getattr(gamma, "main_grad", None) if gamma is not None else None
         bmg = getattr(beta, "main_grad", None) if beta is not None else None
         dgamma = torch.zeros(g.K, device=dy.device) if (gamma is not None and gmg is None) else None
         dbeta = torch.zeros(g.K, device=dy.device) if (beta is not None and bmg is None) else None
         wt = weight_flipped(w, g.K, g.R, g.S, g.C)  # 1x1: [C][K] = W transposed
         dx = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
-        d_in = arena.zeros((4, g.C), dy.device)
+        d_in = arena.zeros((4, g.C), dy.device) if act else None
         mg = getattr(w, "main_grad", None)
         target = mg if mg is not None else torch.zeros(w.shape, device=dy.device, dtype=torch.float32)
+        last = True
+        if not act:
+            sl = ctx.slot
+            add_src = sl.buf if sl is not None else None
         rc = L.dtm_conv1x1_bnbwd(_lib.ptr(dy), _lib.ptr(y), _lib.ptr(dss.contiguous()), _lib.ptr(ss),
                                  _lib.ptr(gamma), ctx.count, _lib.ptr(gmg if gmg is not None else dgamma),
                                  _lib.ptr(bmg if bmg is not None else dbeta), _lib.ptr(wt), _lib.ptr(x_raw),
-                                 _lib.ptr(in_ss), int(ctx.in_unscaled), _lib.ptr(dx), _lib.ptr(d_in),
-                                 _lib.ptr(target), g.N * g.P * g.Q, g.K, g.C, s)
+                                 _lib.ptr(in_ss), int(ctx.in_unscaled), _lib.ptr(add_src), _lib.ptr(dx),
+                                 _lib.ptr(d_in), _lib.ptr(target), g.N * g.P * g.Q, g.K, g.C, s)
         if rc == -1:
             return None
         _check(rc, "conv1x1_bnbwd")
-        _slot_take(ctx.slot)  # (the activation-input path takes no stashed gradient)
+        last, _buf, _st = _slot_take(ctx.slot)
+        if not act and not last:
+            # (the kernel already folded the pending stash in: dx is the cumulative gradient)
+            ctx.slot.buf, ctx.slot.stride = dx, 1
+            dx = None
         BWD1X1_FUSED[0] += 1
         for p, m in ((gamma, gmg), (beta, bmg), (w, mg)):
             if m is not None:
@@ -317,7 +333,8 @@ BWD1X1_FUSED = [0]  # count of 1x1 conv+BN backwards done by the one-pass kernel
 
 
 def _bwd1x1_ok(ctx, g):
-    """The one-pass 1x1 backward covers the ResNet bottleneck expansion shape (64 -> 256 channels)."""
+    """The one-pass 1x1 backward covers the ResNet 64 -> 256 channel shape (stage-1 expansion conv and
+    projection shortcut)."""
     import os
     return (os.environ.get("DTM_BWD1X1_FUSE", "1") != "0" and g.R == 1 and g.S == 1 and g.stride == 1 and
             g.pad_h == 0 and g.pad_w == 0 and g.P == g.H and g.Q == g.W and g.K == 256 and g.C == 64 and

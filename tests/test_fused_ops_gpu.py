@@ -307,3 +307,30 @@ def test_conv1x1_bn_backward_one_pass(monkeypatch, N, H, relu):
     assert all(v < 2e-2 for v in e_ref.values()), e_ref
     # same math, different summation order / one bf16 rounding fewer
     assert all(v < 1e-2 for v in e_pair.values()), e_pair
+
+
+def test_conv1x1_bn_backward_one_pass_plain_input(monkeypatch):
+    """Plain-input form of the one-pass 1x1 backward (the stage-1 projection shortcut: its input is the
+    pool output, also read by the unit's first conv, whose gradient arrives as the stash and is added
+    in the epilogue): whole ResNet-50 gradients with and without the one-pass kernel."""
+    from distributed_tensorflow_models_amd.models import nets_factory
+    from distributed_tensorflow_models_amd.ops import nn as F
+    torch.manual_seed(0)
+    net = nets_factory.build("resnet_v1_50", num_classes=10).to(DEV)
+    x = torch.randn(4, 64, 64, 3, device=DEV).to(torch.bfloat16)
+    y = torch.randint(0, 10, (4,), device=DEV)
+    grads, counts = {}, {}
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("DTM_BWD1X1_FUSE", fuse)
+        for p in net.parameters():
+            p.grad = None
+        n0 = fused.BWD1X1_FUSED[0]
+        loss = F.softmax_cross_entropy(net(x, training=True), y).mean()
+        loss.backward()
+        torch.cuda.synchronize()
+        counts[fuse] = fused.BWD1X1_FUSED[0] - n0
+        grads[fuse] = {n: p.grad.detach().float().clone() for n, p in net.named_parameters() if p.grad is not None}
+    assert counts["0"] == 0 and counts["1"] == 4, counts  # 3 expansion convs + the projection shortcut
+    errs = {k: _rel(grads["1"][k], grads["0"][k]) for k in grads["0"]}
+    worst = max((v, k) for k, v in errs.items() if "beta" not in k or not k.startswith("conv1"))
+    assert worst[0] < 2e-2, worst
