@@ -1908,9 +1908,9 @@ DTM_API int dtm_conv_fwd_bn(const void* x, const void* w, void* y, const float* 
 //   act_sums[2][C] += (sum g*act_x, sum g) with g the masked gradient (the BN scale/shift grads).
 // Block-output form (dtm_conv_dgrad_bnout): the input of this conv was y = relu(bn(act_x) [+ bn(act_r) |
 // + identity]) with the ReLU mask kept as a bitmask; the epilogue applies that BN-apply's backward to
-// the total input gradient (dgrad + add_src): dx <- g = (dgrad + add_src) * bit, act_sums[4][C] +=
-// (sum g*act_x, sum g, sum g*act_r, sum g) - the separate bn_apply_bwd pass over the block output (read
-// d(out), mask and act_x, write g) disappears.
+// the total input gradient (dgrad + add_src): dx <- g = (dgrad + add_src) * bit, act_sums[0..1][C] +=
+// (sum g*act_x, sum g) and, with act_r, act_sums[4..5][C] += (sum g*act_r, sum g) - the separate
+// bn_apply_bwd pass over the block output (read d(out), mask and act_x, write g) disappears.
 static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvDesc* d, const void* add_src,
                            int add_stride, const void* act_x, const float* act_ss, float* act_sums, int act_unscaled,
                            const void* act_mask, const void* act_r, void* stream);
@@ -1965,7 +1965,14 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvD
     a.act_sums = ws;
   }
   dispatch_nt(a, d->stride, tc, (hipStream_t)stream);
-  if (act_x) dtm_reduce_rows(a.act_sums, rows, rw * d->C, rw * d->C, act_sums, (hipStream_t)stream);
+  if (act_x && act_r) {
+    // [sum g*x | sum g] -> act_sums rows 0-1, [sum g*r | sum g] -> rows 4-5 of an [8][C] buffer: rows 0-3
+    // and 4-7 are then directly the ss gradients of the two BatchNorms (no copies)
+    dtm_reduce_rows(a.act_sums, rows, 2 * d->C, rw * d->C, act_sums, (hipStream_t)stream);
+    dtm_reduce_rows(a.act_sums + 2 * d->C, rows, 2 * d->C, rw * d->C, act_sums + 4 * d->C, (hipStream_t)stream);
+  } else if (act_x) {
+    dtm_reduce_rows(a.act_sums, rows, rw * d->C, rw * d->C, act_sums, (hipStream_t)stream);
+  }
   return 0;
 }
 

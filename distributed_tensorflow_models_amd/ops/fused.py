@@ -86,7 +86,7 @@ class _BNOutInfo:
 
     def __init__(self, mask, x, r):
         self.mask, self.x, self.r = mask, x, r
-        self.sums = None  # [4, C]: sum g*x, sum g, sum g*r, sum g  (set by the fusing dgrad)
+        self.sums = None  # [4 or 8, C]: sum g*x, sum g, 0, 0 (, sum g*r, sum g, 0, 0)  (set by the fusing dgrad)
         self.g = None     # the tensor the fusing dgrad returned
 
 
@@ -251,7 +251,8 @@ class _ConvBNFn(torch.autograd.Function):
                 if last and info is not None and info.sums is None and tuple(info.x.shape) == tuple(dx.shape):
                     # last consumer of a block output: the BN-apply backward (mask, scale/shift sums)
                     # runs in this dgrad's epilogue; the BN-apply node just hands the results on
-                    sums = arena.zeros((4, g.C), dy.device)
+                    # [8][C]: rows 0-3 / 4-7 = the ss gradients of bn(x) / bn(r) (rows 2-3, 6-7 stay 0)
+                    sums = arena.zeros((8 if info.r is not None else 4, g.C), dy.device)
                     _check(L.dtm_conv_dgrad_bnout(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d),
                                                   _lib.ptr(add_src) if use_add else None,
                                                   add_stride if use_add else 1, _lib.ptr(info.mask),
@@ -430,12 +431,8 @@ class _BNApplyFn(torch.autograd.Function):
         info = ctx.bnout
         if info is not None and info.sums is not None:
             # the consuming conv's dgrad epilogue already applied this backward: dy is g (= d(y) * mask)
-            sx = arena.zeros((4, C), x.device)
-            sx[:2].copy_(info.sums[:2])
-            sr = None
-            if ctx.res_mode == 2:
-                sr = arena.zeros((4, C), x.device)
-                sr[:2].copy_(info.sums[2:])
+            sx = info.sums[:4]
+            sr = info.sums[4:8] if ctx.res_mode == 2 else None
             dx = info.g
             if dy.data_ptr() != dx.data_ptr():
                 # another (non-hand-off) consumer of y added its gradient: push the remainder through

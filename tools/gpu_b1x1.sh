@@ -6,5 +6,5 @@ timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method threa
 grep -E "passed|failed" gpurun_out/t_b1x1.log | tail -3
 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_trajectory_gpu.py tests/test_fused_gpu.py > gpurun_out/t_b1x1_net.log 2>&1 || { echo "net tests failed"; tail -40 gpurun_out/t_b1x1_net.log; exit 1; }
 tail -2 gpurun_out/t_b1x1_net.log
-VARIANTS="fused=;off=b1x1:0" ROUNDS=5 timeout -k 10 300 python tools/ab_step.py > gpurun_out/ab_b1x1.log 2>&1 || { tail -20 gpurun_out/ab_b1x1.log; exit 1; }
+VARIANTS="${VARIANTS:-fused=;off=b1x1:0}" ROUNDS=5 timeout -k 10 300 python tools/ab_step.py > gpurun_out/ab_b1x1.log 2>&1 || { tail -20 gpurun_out/ab_b1x1.log; exit 1; }
 tail -3 gpurun_out/ab_b1x1.log
