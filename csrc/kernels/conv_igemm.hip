@@ -1188,6 +1188,17 @@ struct ConvWgradArgs {
   int pix_per_split;
   FastDiv fd_PQ, fd_Q;
   int pix_bytes;  // byte pitch of one x pixel (C*2, or less for the packed-row stem view)
+  // optional BatchNorm backward of dy (register-staged kernels only): dy is the unscaled gradient g of
+  // the BN output and the A operand is comb = g*scale + dsum + 2*dsumsq*ay (stats_combine_fin's algebra,
+  // coefficients from dss / ss / gamma per block); the blocks of pixel split 0 / column tile 0 also
+  // accumulate dgamma / dbeta.  Saves writing comb and reading it back when nothing else reads it.
+  const bf16_t* ay;  // [N][P][Q][K] raw BN input, or nullptr
+  const float* dss;
+  const float* ss;
+  const float* gamma;
+  float count;
+  float* dgamma;
+  float* dbeta;
 };
 
 // byte offset of element (k, m) in a [64 k][ROWS] tile stored as [k/4][m/16][4][16] blocks,
@@ -1209,9 +1220,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
   constexpr int ACH = MT / 32;  // BK*MT/8 chunks / 256 threads
   constexpr int BCH = NT / 32;
   constexpr int BUF = BK * (MT + NT) * 2;
-  __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF + NT * 8];
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF + NT * 8 + MT * 12];
   float* s_scale = (float*)(smem + NBUF * BUF);  // prologue scale/shift of this block's NT columns
   float* s_shift = s_scale + NT;
+  float* s_cs = s_shift + NT;  // BN-backward coefficients of this block's MT rows (a.ay)
+  float* s_ca = s_cs + MT;
+  float* s_cb = s_ca + MT;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int gxy = gridDim.x * gridDim.y;
@@ -1231,9 +1245,28 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
   const int pix_lo = bz * a.pix_per_split;
   const int pix_hi = min(a.Mpix, pix_lo + a.pix_per_split);
   // (an empty split still runs: it stores a zero slab, which the reduction relies on)
+  if (a.ay) {
+    for (int j = tid; j < MT; j += 256) {
+      const int ko = m0 + j;
+      float ds = 0.f, dq = 0.f, dg, db, sc = 0.f;
+      if (ko < a.K) {
+        fin_bwd_channel(a.dss, a.ss, a.gamma, a.K, ko, a.count, &ds, &dq, &dg, &db);
+        sc = a.ss[ko];
+        if (bx == 0 && bz == 0) {
+          if (a.dgamma) a.dgamma[ko] += dg;
+          if (a.dbeta) a.dbeta[ko] += db;
+        }
+      }
+      s_cs[j] = sc;
+      s_ca[j] = ds;
+      s_cb[j] = 2.f * dq;
+    }
+    __syncthreads();
+  }
 
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
   const __amdgpu_buffer_rsrc_t dr = make_rsrc(a.dy, a.dy_bytes);
+  const __amdgpu_buffer_rsrc_t yr = make_rsrc(a.ay ? a.ay : a.dy, a.dy_bytes);
 
   const int sub = tid & 7, kk = sub >> 1, half = sub & 1, grp = tid >> 3;
   // A (dy) chunk coordinates
@@ -1260,8 +1293,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
     b_s[i] = tap - b_r[i] * a.S;
   }
 
-  uint4 areg[ACH], breg[BCH];
-  bool bval[BCH];
+  uint4 areg[ACH], breg[BCH], yreg[ACH];
+  bool aval[ACH], bval[BCH];
   int bcc[BCH];
   auto gload = [&](int pbase) {
 #pragma unroll
@@ -1271,6 +1304,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
       bool v = pix < pix_hi && ko < a.K;
       uint32_t off = v ? (uint32_t)(((size_t)pix * a.K + ko) * 2) : OOB_OFFSET;
       areg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(dr, off, 0, 0));
+      aval[i] = v;
+      if (a.ay) yreg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yr, off, 0, 0));
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
@@ -1291,6 +1326,22 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
   };
   auto swrite = [&](int buf) {
     char* base = smem + buf * BUF;
+    if (a.ay) {
+#pragma unroll
+      for (int i = 0; i < ACH; ++i) {
+        uint32_t u[4] = {areg[i].x, areg[i].y, areg[i].z, areg[i].w};
+        const uint32_t yu[4] = {yreg[i].x, yreg[i].y, yreg[i].z, yreg[i].w};
+        const int m = a_m[i];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c0 = m + 2 * e, c1 = c0 + 1;
+          const float lo = aval[i] ? fmaf(lo_bf(u[e]), s_cs[c0], s_ca[c0] + s_cb[c0] * lo_bf(yu[e])) : 0.f;
+          const float hi = aval[i] ? fmaf(hi_bf(u[e]), s_cs[c1], s_ca[c1] + s_cb[c1] * hi_bf(yu[e])) : 0.f;
+          u[e] = pack2bf(lo, hi);
+        }
+        areg[i] = make_uint4(u[0], u[1], u[2], u[3]);
+      }
+    }
     if (a.in_scale) {
 #pragma unroll
       for (int i = 0; i < BCH; ++i) {
@@ -1995,12 +2046,40 @@ DTM_API void dtm_conv_set_wgrad_tile(int id, int occ) {
   if (occ > 0) g_wgrad_occ = occ;
 }
 
+struct WgradBN {
+  const void* y;
+  const float *dss, *ss, *gamma;
+  float count;
+  float *dgamma, *dbeta;
+};
+
+static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float* in_scale, const float* in_shift,
+                           const ConvDesc* d, int num_cus, const WgradBN* bn, void* stream);
+
 DTM_API int dtm_conv_wgrad(const void* x, const void* dy, float* dw, const float* in_scale,
                            const float* in_shift, const ConvDesc* d, int num_cus, void* stream) {
+  return conv_wgrad_impl(x, dy, dw, in_scale, in_shift, d, num_cus, nullptr, stream);
+}
+
+// Weight gradient of a conv followed by a training BatchNorm whose stats-combine output (comb) has no
+// other reader (the stem: no input gradient): comb is formed in the A-operand staging from g = the
+// BN output's unscaled gradient and y = the raw conv output, and dgamma / dbeta are accumulated.
+DTM_API int dtm_conv_wgrad_bnbwd(const void* x, const void* g, const void* y, const float* dss, const float* ss,
+                                 const float* gamma, float count, float* dgamma, float* dbeta, float* dw,
+                                 const ConvDesc* d, int num_cus, void* stream) {
+  WgradBN bn{y, dss, ss, gamma, count, dgamma, dbeta};
+  return conv_wgrad_impl(x, g, dw, nullptr, nullptr, d, num_cus, &bn, stream);
+}
+
+static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float* in_scale, const float* in_shift,
+                           const ConvDesc* d, int num_cus, const WgradBN* bn, void* stream) {
   if (d->C % 8 || d->K % 8) return -1;
   ConvWgradArgs a;
   a.x = (const bf16_t*)x; a.dy = (const bf16_t*)dy; a.dw = dw;
   a.in_scale = in_scale; a.in_shift = in_shift;
+  a.ay = bn ? (const bf16_t*)bn->y : nullptr;
+  a.dss = bn ? bn->dss : nullptr; a.ss = bn ? bn->ss : nullptr; a.gamma = bn ? bn->gamma : nullptr;
+  a.count = bn ? bn->count : 0.f; a.dgamma = bn ? bn->dgamma : nullptr; a.dbeta = bn ? bn->dbeta : nullptr;
   a.pix_bytes = d->pix_bytes > 0 ? d->pix_bytes : d->C * 2;
   size_t xb = (size_t)d->N * d->H * d->W * a.pix_bytes, yb = (size_t)d->N * d->P * d->Q * d->K * 2;
   if (xb >= (1ull << 31) || yb >= (1ull << 31)) return -2;
@@ -2027,7 +2106,7 @@ DTM_API int dtm_conv_wgrad(const void* x, const void* dy, float* dw, const float
     // 14x14 / 7x7 3x3 -8..-13 %, 7x7 1024->2048 -7 %; it loses on every K < 256 or short-RSC layer)
     if (g_tile_w8 && d->K >= 256 && a.Kg >= 1024 && (d->R * d->S > 1 || d->K >= 1024)) wt = 12;
   }
-  if (wt >= 10 && in_scale) wt = d->K <= 64 ? 1 : 0;  // the pipelined kernels have no input prologue
+  if (wt >= 10 && (in_scale || bn)) wt = d->K <= 64 ? 1 : 0;  // the pipelined kernels have no operand prologues
   const bool small_m = (wt == 1 || wt == 2 || wt == 13 || wt == 14 || wt == 15);
   const bool big = wt == 12;  // 8-wave 256x256 (one block per CU)
   const int MT = small_m ? 64 : (big ? 256 : 128), NT = (big || wt == 13 || wt == 14) ? 256 : 128;

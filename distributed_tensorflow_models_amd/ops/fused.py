@@ -527,6 +527,27 @@ class _StemConvBNFn(torch.autograd.Function):
         N, Hp, Wp, K, R, S, C, P, Q, st = ctx.d
         dy = dy.contiguous()
         dgamma = dbeta = None
+        import os
+        if (ss is not None and dss is not None and ctx.needs_input_grad[1] and
+                os.environ.get("DTM_STEM_WGRAD_FUSE", "1") != "0"):
+            # no input gradient: comb (the BN backward of dy) has the wgrad as its only reader, so it is
+            # formed in the wgrad's operand staging instead of being written and read back
+            gmg = getattr(gamma, "main_grad", None) if gamma is not None else None
+            bmg = getattr(beta, "main_grad", None) if beta is not None else None
+            dgamma = torch.zeros(K, device=dy.device) if (gamma is not None and gmg is None) else None
+            dbeta = torch.zeros(K, device=dy.device) if (beta is not None and bmg is None) else None
+            d = _lib.ConvDesc(N, Hp, Wp, 32, K, R, 1, P, Q, st, 0, 0, 8)
+            tv = torch.zeros((K, R, 8, 4), device=dy.device, dtype=torch.float32)
+            _check(L.dtm_conv_wgrad_bnbwd(_lib.ptr(xp), _lib.ptr(dy), _lib.ptr(y), _lib.ptr(dss.contiguous()),
+                                          _lib.ptr(ss), _lib.ptr(gamma), ctx.count,
+                                          _lib.ptr(gmg if gmg is not None else dgamma),
+                                          _lib.ptr(bmg if bmg is not None else dbeta), _lib.ptr(tv), ctypes.byref(d),
+                                          _lib.num_cus(), s), "stem_conv_wgrad_bnbwd")
+            for p, m in ((gamma, gmg), (beta, bmg)):
+                if m is not None:
+                    _notify(p)
+            dw = _accum_param_grad(w, tv[:, :, :S, :C])
+            return None, dw, dgamma, dbeta, None, None, None
         if ss is not None and dss is not None:
             gmg = getattr(gamma, "main_grad", None) if gamma is not None else None
             bmg = getattr(beta, "main_grad", None) if beta is not None else None

@@ -191,10 +191,13 @@ def test_bn_relu_maxpool_fused(H, pool, pad, st):
     assert errs["y"] < 1e-2 and all(v < 1.2e-1 for v in errs.values()), msg
 
 
+@pytest.mark.parametrize("stemw", ["0", "1"])
 @pytest.mark.parametrize("H,W,C,N", [(32, 32, 3, 4), (36, 30, 3, 2), (224, 224, 3, 2), (17, 23, 1, 3)])
-def test_stem_packed_row_conv_bn(H, W, C, N):
+def test_stem_packed_row_conv_bn(monkeypatch, H, W, C, N, stemw):
     """The packed-row stem path (7x7/2, explicit pad 3, C <= 4: an R x 1 conv over 32 'channels' with an
-    8-byte pixel pitch) against torch fp32: output, BN moving statistics, weight/gamma/beta grads."""
+    8-byte pixel pitch) against torch fp32: output, BN moving statistics, weight/gamma/beta grads; the
+    BN backward either as a stats-combine pass or inside the wgrad operand staging (stemw=1)."""
+    monkeypatch.setenv("DTM_STEM_WGRAD_FUSE", stemw)
     torch.manual_seed(0)
     x = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16)
     w = (torch.randn(64, 7, 7, C, device=DEV) / (49 * C) ** 0.5).to(torch.bfloat16).float()

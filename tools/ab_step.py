@@ -3,7 +3,7 @@
 median ms/step per variant; one device, one process: MI355X_MICROARCH 'DVFS give-back' / rule 24).
 
 VARIANTS="base=;noW=wtile:-3;noT=tile:-3;fused=prologue:fused" python tools/ab_step.py
-keys: tile (conv_nt tile id), w8 (0/1: the 8-wave 256x256 conv tile in the shape policy), kwide (0/1: 64-channel tiles for K % 128 <= 64), few (0/1: streaming few-row slab reduction), bnout (0/1: block-output BN backward in the consuming dgrad's epilogue), b1x1 (0/1: one-pass 1x1 conv+BN backward), sact (0/1: streaming 1x1 kernel for act dgrads), wtile[:occ] (wgrad tile id / blocks-per-CU target), prologue (DTM_PROLOGUE),
+keys: tile (conv_nt tile id), w8 (0/1: the 8-wave 256x256 conv tile in the shape policy), kwide (0/1: 64-channel tiles for K % 128 <= 64), few (0/1: streaming few-row slab reduction), bnout (0/1: block-output BN backward in the consuming dgrad's epilogue), b1x1 (0/1: one-pass 1x1 conv+BN backward), stemw (0/1: stem BN backward in the wgrad operand staging), sact (0/1: streaming 1x1 kernel for act dgrads), wtile[:occ] (wgrad tile id / blocks-per-CU target), prologue (DTM_PROLOGUE),
 stem (DTM_STEM: 1 = packed-row stem path), red (target_blocks:max_chunks[:direct_max] of the
 partial-sum reductions; 0 = legacy 256 rows per block; direct_max = largest BN-backward grid that
 reduces with atomics in the producer instead of a reduce launch)."""
@@ -40,6 +40,7 @@ def apply(cfg):
     os.environ["DTM_STEM"] = cfg.get("stem", "1")
     os.environ["DTM_BNOUT_FUSE"] = cfg.get("bnout", "1")
     os.environ["DTM_BWD1X1_FUSE"] = cfg.get("b1x1", "1")
+    os.environ["DTM_STEM_WGRAD_FUSE"] = cfg.get("stemw", "1")
 
 
 def main():
