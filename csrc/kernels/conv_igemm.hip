@@ -65,7 +65,26 @@ struct ConvNTArgs {
   const bf16_t* act_r;      //   + a BN'd residual: also sum g*act_r -> rows [g*x | g | g*r | g] (4K wide)
   int pix_bytes;          // byte pitch of one input pixel (C*2, or less for the packed-row stem view)
   bf16_t* dump;           // >= 16 B scratch: target of the out-of-range stores of the exact-count epilogue
+  // output remap of a stride-decomposed dgrad (ostr > 1): output pixel (n, i, j) of this launch's P x Q
+  // grid is pixel (n, i*ostr + oa, j*ostr + ob) of the OH x OW tensor that y and every epilogue side
+  // input (add_src, act_x, act_r, act_mask) index.  ostr == 1: identity (OH = P, OW = Q, oa = ob = 0)
+  int ostr, oa, ob, OH, OW;
 };
+
+// full-resolution coordinates / row of output pixel m (see ConvNTArgs::ostr)
+__device__ __forceinline__ void out_nhw(const ConvNTArgs& a, int m, int& n, int& h, int& w) {
+  const uint32_t nn = fdiv((uint32_t)m, a.fd_PQ), rem = m - nn * (a.P * a.Q);
+  const uint32_t i = fdiv(rem, a.fd_Q), j = rem - i * a.Q;
+  n = (int)nn;
+  h = (int)i * a.ostr + a.oa;
+  w = (int)j * a.ostr + a.ob;
+}
+__device__ __forceinline__ int out_row(const ConvNTArgs& a, int m) {
+  if (a.ostr == 1) return m;
+  int n, h, w;
+  out_nhw(a, m, n, h, w);
+  return (n * a.OH + h) * a.OW + w;
+}
 
 // Shared epilogue of the conv_nt kernels (register-staged and LDS-DMA): acc[TC][TP] of wave (wp, wc)
 // for the tile at pixel p0 / channel c0; smem must hold PT * (2*CT + 16) bytes and be free.
@@ -129,7 +148,7 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
       if constexpr (staged) {
         *(uint2*)(smem + mloc * OROW + kloc * 2) = make_uint2(lo, hi);
       } else if (m < a.M && kch < a.K) {
-        *(uint2*)(a.y + (size_t)m * a.K + kch) = make_uint2(lo, hi);
+        *(uint2*)(a.y + (size_t)out_row(a, m) * a.K + kch) = make_uint2(lo, hi);
       }
       if (!SACC && !staged && a.stats && m < a.M && kch < a.K) {
         float q0 = lo_bf(lo), q1 = hi_bf(lo), q2 = lo_bf(hi), q3 = hi_bf(hi);
@@ -201,15 +220,15 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
           const int row = ((g0 + j) * NT + tid) / CPR;
           const int m = p0 + row;
           if (m < a.M && kc < a.K) {
-            const size_t o = (size_t)m * a.K + kc;
+            const size_t o = (size_t)out_row(a, m) * a.K + kc;
             if (a.add_src) {
               const bf16_t* src = a.add_src + o;
               if (a.add_stride > 1) {
-                const uint32_t n = fdiv((uint32_t)m, a.fd_PQ), rem = m - n * (a.P * a.Q);
-                const uint32_t h = fdiv(rem, a.fd_Q), w = rem - h * a.Q;
+                int n, h, w;
+                out_nhw(a, m, n, h, w);
                 const int s = a.add_stride;
                 src = (h % s == 0 && w % s == 0)
-                          ? a.add_src + ((size_t)((int)n * a.add_H + (int)h / s) * a.add_W + (int)w / s) * a.K + kc
+                          ? a.add_src + ((size_t)(n * a.add_H + h / s) * a.add_W + w / s) * a.K + kc
                           : nullptr;
               }
               if (src) {
@@ -235,7 +254,7 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
         const bool inb = m < a.M && kc < a.K;
         if (EXACT || inb) {
           uint4 v = *(const uint4*)(smem + row * OROW + chn * 16);
-          const size_t o = (size_t)m * a.K + kc;
+          const size_t o = (size_t)(inb ? out_row(a, m) : m) * a.K + kc;
           if constexpr (SACC) {
             if (inb) {
               const float q[8] = {lo_bf(v.x), hi_bf(v.x), lo_bf(v.y), hi_bf(v.y),
@@ -1617,7 +1636,31 @@ struct FlipDesc {
   const bf16_t* w;
   bf16_t* wt;
   int K, R, S, C;
+  int st, ph, pw, pad_;  // st > 1: the stride-decomposed layout for a stride-st conv with top/left pads ph/pw
 };
+
+// Stride decomposition of a stride-st dgrad along one dimension (kernel extent R, forward pad `pad`):
+// the input pixels h = st*i + a (class a) receive exactly the taps r = r0 + st*t, t < T, from dy rows
+// p = i + off - t.  So class a is a stride-1 correlation of dy with those T taps (flipped) and pad
+// T-1-off, no zero-dilated input (the plain dgrad multiplies st^2 - 1 of every st^2 gathered rows by 0).
+__host__ __device__ __forceinline__ void dec_dim(int R, int st, int pad, int a, int& r0, int& T, int& off) {
+  r0 = ((a + pad) % st + st) % st;
+  T = r0 < R ? (R - r0 + st - 1) / st : 0;
+  off = (a + pad - r0) / st;
+}
+// element offset of class (a, b)'s block [C][Tr][Tu][K] in the decomposed layout (classes a-major)
+__host__ __device__ __forceinline__ size_t dec_block(int R, int S, int C, int K, int st, int ph, int pw, int a, int b) {
+  size_t off = 0;
+  for (int a2 = 0; a2 < st; ++a2)
+    for (int b2 = 0; b2 < st; ++b2) {
+      if (a2 == a && b2 == b) return off;
+      int r0, Tr, o1, s0, Tu, o2;
+      dec_dim(R, st, ph, a2, r0, Tr, o1);
+      dec_dim(S, st, pw, b2, s0, Tu, o2);
+      off += (size_t)C * K * Tr * Tu;
+    }
+  return off;
+}
 // One 64(k) x 64(c) tile of one tap through LDS: the source rows are read along c and the flipped
 // destination rows written along k, both coalesced (the old per-element gather read with a stride
 // of R*S*C elements: 0.17 TB/s, 2.9 ms per VGG-16 step for its 103 M-element fc6 kernel).
@@ -1631,6 +1674,18 @@ __device__ __forceinline__ void flip_tile(const FlipDesc& f, int tile, uint16_t 
   const uint16_t* w = (const uint16_t*)f.w;
   uint16_t* wt = (uint16_t*)f.wt;
   const size_t RS = (size_t)f.R * f.S;
+  // destination of element (c, k): wt[(c * dRS + drs) * K + k] (+ the class block offset)
+  size_t dRS = RS, drs = rs2;
+  if (f.st > 1) {
+    const int a = ((r - f.ph) % f.st + f.st) % f.st, b = ((s - f.pw) % f.st + f.st) % f.st;
+    int r0, Tr, o1, s0, Tu, o2;
+    dec_dim(f.R, f.st, f.ph, a, r0, Tr, o1);
+    dec_dim(f.S, f.st, f.pw, b, s0, Tu, o2);
+    const int tq = Tr - 1 - (r - r0) / f.st, uq = Tu - 1 - (s - s0) / f.st;
+    wt += dec_block(f.R, f.S, f.C, f.K, f.st, f.ph, f.pw, a, b);
+    dRS = (size_t)Tr * Tu;
+    drs = (size_t)tq * Tu + uq;
+  }
 #pragma unroll 4
   for (int i = threadIdx.x; i < FLIP_T * FLIP_T; i += 256) {
     const int kk = i / FLIP_T, cc = i % FLIP_T;
@@ -1642,7 +1697,7 @@ __device__ __forceinline__ void flip_tile(const FlipDesc& f, int tile, uint16_t 
   for (int i = threadIdx.x; i < FLIP_T * FLIP_T; i += 256) {
     const int cc = i / FLIP_T, kk = i % FLIP_T;
     const int k = k0 + kk, c = c0 + cc;
-    if (k < f.K && c < f.C) wt[((size_t)c * RS + rs2) * f.K + k] = lds[kk][cc];
+    if (k < f.K && c < f.C) wt[((size_t)c * dRS + drs) * f.K + k] = lds[kk][cc];
   }
   __syncthreads();
 }
@@ -1675,6 +1730,7 @@ using namespace dtm;
 struct ConvDesc {
   int N, H, W, C, K, R, S, P, Q, stride, pad_h, pad_w;
   int pix_bytes;  // 0 = C*2 (dense NHWC); else the input pixel pitch in bytes (packed-row stem view)
+  int dec;        // dgrad only: the weight is in the stride-decomposed flipped layout (see dec_dim)
 };
 
 static const bf16_t* zero_chunk() {
@@ -1768,7 +1824,7 @@ static int stream_rows(const ConvNTArgs& a, int id) {
 static bool stream_ok(const ConvNTArgs& a) {
   return !a.bias && !a.relu && a.R == 1 && a.S == 1 && a.stride == 1 && a.pad_h == 0 && a.pad_w == 0 && a.Hv == a.Hin && a.Wv == a.Win &&
          a.P == a.Hin && a.Q == a.Win && a.Kg % 64 == 0 && a.Kg <= 128 && a.K % 8 == 0 &&
-         (!a.in_scale || a.C <= 512) && a.dump != nullptr;
+         (!a.in_scale || a.C <= 512) && a.dump != nullptr && a.ostr == 1;
 }
 
 template <int PT, int CT, int WP, int WC, int UD, int NBUF = 2>
@@ -1792,6 +1848,8 @@ DTM_API void dtm_conv_set_kwide(int on) { g_kwide = on; }
 DTM_API void dtm_conv_set_w8(int on) { g_tile_w8 = on; }
 static int g_k64_tile = 3;  // tile of the 64-output-channel layers (A/B knob: dtm_conv_set_k64_tile)
 DTM_API void dtm_conv_set_k64_tile(int id) { g_k64_tile = id; }
+static int g_act_tile = -1;  // A/B knob: tile of the dgrads with a fused activation-backward epilogue (-1 = policy)
+DTM_API void dtm_conv_set_act_tile(int id) { g_act_tile = id; }
 static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
   if (g_tile_env == -2) {
     const char* e = getenv("DTM_CONV_TILE");
@@ -1801,6 +1859,7 @@ static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
   // variants win almost everywhere (more resident blocks hide the short-K latency); the 2-buffer
   // 128x128 tile keeps the small-M / deep-K layers (7x7 maps, K-reduction >= 2048)
   int id = g_tile_env;
+  if (id == -1 && a.act_x && g_act_tile >= 0) id = g_act_tile;
   // the pipelined LDS-DMA 128x128 tile (2 slots, 2 blocks/CU) wins every deep-reduction layer without the
   // prologue (tools/conv_tile_sweep.py: 3x3 at 14x14 / 7x7 -13..-18 %, deep 1x1 -5..-16 %)
   if (id == -4) id = -1;  // (-4: the policy without the streaming kernel, for A/B runs)
@@ -1907,6 +1966,7 @@ static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, cons
   a.Hv = d->H; a.Wv = d->W;
   a.M = d->N * d->P * d->Q; a.Kg = d->R * d->S * d->C; a.relu = relu;
   a.fd_PQ = make_fastdiv(d->P * d->Q); a.fd_Q = make_fastdiv(d->Q);
+  a.ostr = 1; a.oa = a.ob = 0; a.OH = a.P; a.OW = a.Q;
   int rows = 0;
   const TileCfg tc = pick_tile(a, stats);
   if (stats) {
@@ -1985,7 +2045,6 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvD
                            const void* act_mask, const void* act_r, void* stream) {
   if (d->K % 8 || d->C % 4) return -1;
   if (add_stride < 1 || (add_stride > 1 && !add_src)) return -6;
-  if (d->stride > 2) return -3;
   if ((add_src || act_x) && d->C % 8) return -5;
   ConvNTArgs a;
   a.x = (const bf16_t*)dy; a.w = (const bf16_t*)wt; a.y = (bf16_t*)dx;
@@ -2001,28 +2060,65 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvD
   size_t xb = (size_t)d->N * d->P * d->Q * d->K * 2, wb = (size_t)d->K * d->R * d->S * d->C * 2;
   if (xb >= (1ull << 31) || wb >= (1ull << 31)) return -2;
   a.x_bytes = (uint32_t)xb; a.w_bytes = (uint32_t)wb;
-  a.N = d->N; a.Hin = d->P; a.Win = d->Q; a.C = d->K; a.K = d->C; a.R = d->R; a.S = d->S;
-  a.P = d->H; a.Q = d->W; a.stride = 1;
-  a.pad_h = d->R - 1 - d->pad_h; a.pad_w = d->S - 1 - d->pad_w;
-  a.Hv = (d->P - 1) * d->stride + 1; a.Wv = (d->Q - 1) * d->stride + 1;
-  a.M = d->N * d->H * d->W; a.Kg = d->R * d->S * d->K; a.relu = 0;
-  a.fd_PQ = make_fastdiv(d->H * d->W); a.fd_Q = make_fastdiv(d->W);
-  const TileCfg tc = pick_tile(a);
-  const int rows = (a.M + tc.PT - 1) / tc.PT;  // pixel tiles
+  a.N = d->N; a.Hin = d->P; a.Win = d->Q; a.C = d->K; a.K = d->C; a.relu = 0;
+  a.stride = 1;
+  a.Hv = d->P; a.Wv = d->Q;
+  a.OH = d->H; a.OW = d->W;
   const int rw = act_r ? 4 : 2;
+  // launches: one plain dgrad over the zero-dilated dy (UD = stride), or (d->dec, stride > 1) one stride-1
+  // conv per output parity class (a, b) with that class's taps of the decomposed weight (dec_dim)
+  const int st = d->stride;
+  const bool dec = d->dec && st > 1;
+  if (!dec && st > 2) return -3;
+  if (dec && (d->R < st || d->S < st)) return -8;  // a class without taps (1x1 strided): caller falls back
+  ConvNTArgs la[16];
+  TileCfg lt[16];
+  int lrows[16], nl = 0, rows = 0;
+  for (int ca = 0; ca < (dec ? st : 1); ++ca)
+    for (int cb = 0; cb < (dec ? st : 1); ++cb) {
+      ConvNTArgs b = a;
+      if (dec) {
+        int r0, Tr, offa, s0, Tu, offb;
+        dec_dim(d->R, st, d->pad_h, ca, r0, Tr, offa);
+        dec_dim(d->S, st, d->pad_w, cb, s0, Tu, offb);
+        const int Hc = (d->H - ca + st - 1) / st, Wc = (d->W - cb + st - 1) / st;
+        if (Hc <= 0 || Wc <= 0) continue;
+        b.w = (const bf16_t*)wt + dec_block(d->R, d->S, d->C, d->K, st, d->pad_h, d->pad_w, ca, cb);
+        b.R = Tr; b.S = Tu;
+        b.P = Hc; b.Q = Wc;
+        b.pad_h = Tr - 1 - offa; b.pad_w = Tu - 1 - offb;
+        b.ostr = st; b.oa = ca; b.ob = cb;
+      } else {
+        b.R = d->R; b.S = d->S;
+        b.P = d->H; b.Q = d->W;
+        b.pad_h = d->R - 1 - d->pad_h; b.pad_w = d->S - 1 - d->pad_w;
+        b.Hv = (d->P - 1) * st + 1; b.Wv = (d->Q - 1) * st + 1;
+        b.ostr = 1; b.oa = b.ob = 0;
+      }
+      b.M = d->N * b.P * b.Q; b.Kg = b.R * b.S * d->K;
+      b.fd_PQ = make_fastdiv(b.P * b.Q); b.fd_Q = make_fastdiv(b.Q);
+      lt[nl] = pick_tile(b);
+      lrows[nl] = (b.M + lt[nl].PT - 1) / lt[nl].PT;  // pixel tiles
+      rows += lrows[nl];
+      la[nl++] = b;
+    }
+  float* ws = nullptr;
   if (act_x) {
-    float* ws = dtm_ws_get((size_t)rows * rw * d->C);
+    ws = dtm_ws_get((size_t)rows * rw * d->C);
     if (!ws) return -4;
-    a.act_sums = ws;
   }
-  dispatch_nt(a, d->stride, tc, (hipStream_t)stream);
+  for (int i = 0, r = 0; i < nl; r += lrows[i], ++i) {
+    // every launch's partial-sum rows go to its own slice of one table, reduced together below
+    if (act_x) la[i].act_sums = ws + (size_t)r * rw * d->C;
+    dispatch_nt(la[i], dec ? 1 : st, lt[i], (hipStream_t)stream);
+  }
   if (act_x && act_r) {
     // [sum g*x | sum g] -> act_sums rows 0-1, [sum g*r | sum g] -> rows 4-5 of an [8][C] buffer: rows 0-3
     // and 4-7 are then directly the ss gradients of the two BatchNorms (no copies)
-    dtm_reduce_rows(a.act_sums, rows, 2 * d->C, rw * d->C, act_sums, (hipStream_t)stream);
-    dtm_reduce_rows(a.act_sums + 2 * d->C, rows, 2 * d->C, rw * d->C, act_sums + 4 * d->C, (hipStream_t)stream);
+    dtm_reduce_rows(ws, rows, 2 * d->C, rw * d->C, act_sums, (hipStream_t)stream);
+    dtm_reduce_rows(ws + 2 * d->C, rows, 2 * d->C, rw * d->C, act_sums + 4 * d->C, (hipStream_t)stream);
   } else if (act_x) {
-    dtm_reduce_rows(a.act_sums, rows, rw * d->C, rw * d->C, act_sums, (hipStream_t)stream);
+    dtm_reduce_rows(ws, rows, rw * d->C, rw * d->C, act_sums, (hipStream_t)stream);
   }
   return 0;
 }
@@ -2159,8 +2255,17 @@ DTM_API void dtm_weight_flip_transpose_batched(const void* descs, int n, void* s
                      (const FlipDesc*)descs);
 }
 
+// the stride-decomposed flipped layout for a stride-st dgrad with forward pads ph / pw (ConvDesc::dec)
+DTM_API void dtm_weight_flip_transpose_dec(const void* w, void* wt, int K, int R, int S, int C, int st, int ph, int pw,
+                                           void* stream) {
+  FlipDesc f{(const bf16_t*)w, (bf16_t*)wt, K, R, S, C, st, ph, pw, 0};
+  int tiles = ((K + FLIP_T - 1) / FLIP_T) * ((C + FLIP_T - 1) / FLIP_T) * R * S;
+  int blocks = tiles < 2048 ? tiles : 2048;
+  hipLaunchKernelGGL(weight_flip_tiled_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, f);
+}
+
 DTM_API void dtm_weight_flip_transpose(const void* w, void* wt, int K, int R, int S, int C, void* stream) {
-  FlipDesc f{(const bf16_t*)w, (bf16_t*)wt, K, R, S, C};
+  FlipDesc f{(const bf16_t*)w, (bf16_t*)wt, K, R, S, C, 1, 0, 0, 0};
   int tiles = ((K + FLIP_T - 1) / FLIP_T) * ((C + FLIP_T - 1) / FLIP_T) * R * S;
   int blocks = tiles < 2048 ? tiles : 2048;
   hipLaunchKernelGGL(weight_flip_tiled_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, f);

@@ -18,7 +18,7 @@ _lib = None
 
 class ConvDesc(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in
-                ("N", "H", "W", "C", "K", "R", "S", "P", "Q", "stride", "pad_h", "pad_w", "pix_bytes")]
+                ("N", "H", "W", "C", "K", "R", "S", "P", "Q", "stride", "pad_h", "pad_w", "pix_bytes", "dec")]
 
 
 class PoolArgs(ctypes.Structure):
@@ -49,6 +49,7 @@ _SIGS = {
     "dtm_conv_wgrad": (_I, [_P, _P, _P, _P, _P, ctypes.POINTER(ConvDesc), _I, _P]),
     "dtm_weight_flip_transpose": (None, [_P, _P, _I, _I, _I, _I, _P]),
     "dtm_weight_flip_transpose_batched": (None, [_P, _I, _P]),
+    "dtm_weight_flip_transpose_dec": (None, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "dtm_flip_desc_bytes": (_I, []),
     "dtm_bn_stats": (None, [_P, _P, _L, _I, _P]),
     "dtm_bn_finalize": (None, [_P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _I, _I, _P]),
@@ -99,6 +100,7 @@ _SIGS = {
     "dtm_conv_set_kwide": (None, [_I]),
     "dtm_set_reduce_few": (None, [_I]),
     "dtm_conv_set_stream_act": (None, [_I]),
+    "dtm_conv_set_act_tile": (None, [_I]),
     "dtm_dropout": (_I, [_P, _P, _L, _I, _F, ctypes.c_ulonglong, _P, _P]),
     "dtm_in_top_k": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
 }

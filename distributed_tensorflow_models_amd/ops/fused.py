@@ -17,7 +17,7 @@ import torch
 from . import _lib
 from .geometry import conv_geom
 from .lazy import LazyBN, Subsampled, as_tensor  # noqa: F401
-from .nn import _accum_param_grad, _check, _notify, weight_bf16, weight_flipped
+from .nn import _accum_param_grad, _check, _notify, dgrad_decomposable, weight_bf16, weight_flipped
 
 
 class ZeroArena:
@@ -233,7 +233,10 @@ class _ConvBNFn(torch.autograd.Function):
         dx = d_in = None
         if ctx.needs_input_grad[0] or (in_ss is not None and ctx.needs_input_grad[1]):
             last, add_src, add_stride = _slot_take(ctx.slot)
-            wt = weight_flipped(w, g.K, g.R, g.S, g.C)
+            # stride > 1: one stride-1 conv per output parity class instead of the zero-dilated dgrad
+            dec = (g.stride, g.pad_h, g.pad_w) if dgrad_decomposable(g) else None
+            wt = weight_flipped(w, g.K, g.R, g.S, g.C, dec)
+            d.dec = int(dec is not None)
             dx = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
             if in_ss is not None:
                 # BN+ReLU of the input was fused into the forward prologue: mask, scale and the BN
@@ -267,6 +270,7 @@ class _ConvBNFn(torch.autograd.Function):
                 if not last:
                     ctx.slot.buf, ctx.slot.stride = dx, 1
                     dx = None
+            d.dec = 0
         if ctx.needs_input_grad[2]:
             mg = getattr(w, "main_grad", None)
             target = mg if mg is not None else torch.zeros(w.shape, device=dy.device, dtype=torch.float32)

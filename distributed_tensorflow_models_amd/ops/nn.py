@@ -97,21 +97,36 @@ def weight_bf16(w):
 # for one weights version; FusedOptimizer bumps the version and refreshes every registered copy in
 # one batched launch right after its update, so backward normally finds them ready.
 WEIGHT_VERSION = [0]
-FLIP_REGISTRY = {}   # id(param) -> (param, wt buffer)
+FLIP_REGISTRY = {}   # (id(param), dec) -> (param, wt buffer, dec)
 
 
-def weight_flipped(w, K, R, S, C):
-    c = getattr(w, "_flip", None)
-    if c is not None and c[0] == WEIGHT_VERSION[0] and c[1].shape == (C, R, S, K):
+def dgrad_decomposable(g):
+    """A stride > 1 dgrad runs as one stride-1 conv per output parity class (ConvDesc.dec, the
+    decomposed flipped weight) when every class has taps (R, S >= stride).  DTM_DGRAD_DEC=0: off."""
+    import os
+    return g.stride > 1 and g.R >= g.stride and g.S >= g.stride and os.environ.get("DTM_DGRAD_DEC", "1") != "0"
+
+
+def weight_flipped(w, K, R, S, C, dec=None):
+    """Flipped / transposed bf16 dgrad copy [C][R][S][K] of w [K][R][S][C]; with dec = (stride, pad_h,
+    pad_w) the same elements in the stride-decomposed layout (per output parity class (a, b) a block
+    [C][Tr][Tu][K] of that class's taps, conv_igemm.hip dec_dim)."""
+    attr = "_flip" if dec is None else "_flipdec"
+    c = getattr(w, attr, None)
+    if c is not None and c[0] == WEIGHT_VERSION[0] and c[1].shape == (C, R, S, K) and c[2] == dec:
         return c[1]
     L = _lib.lib()
     wt = c[1] if (c is not None and c[1].shape == (C, R, S, K)) else \
         torch.empty((C, R, S, K), device=w.device, dtype=torch.bfloat16)
-    L.dtm_weight_flip_transpose(_lib.ptr(weight_bf16(w)), _lib.ptr(wt), K, R, S, C, _lib.stream_ptr())
+    if dec is None:
+        L.dtm_weight_flip_transpose(_lib.ptr(weight_bf16(w)), _lib.ptr(wt), K, R, S, C, _lib.stream_ptr())
+    else:
+        L.dtm_weight_flip_transpose_dec(_lib.ptr(weight_bf16(w)), _lib.ptr(wt), K, R, S, C, int(dec[0]), int(dec[1]),
+                                        int(dec[2]), _lib.stream_ptr())
     if isinstance(w, torch.nn.Parameter):
         try:
-            w._flip = (WEIGHT_VERSION[0], wt)
-            FLIP_REGISTRY[id(w)] = (w, wt)
+            setattr(w, attr, (WEIGHT_VERSION[0], wt, dec))
+            FLIP_REGISTRY[(id(w), dec)] = (w, wt, dec)
         except Exception:
             pass
     return wt
@@ -124,22 +139,24 @@ def refresh_flipped(stream=None):
         return
     L = _lib.lib()
     entries = list(FLIP_REGISTRY.values())
-    key = tuple(id(w) for w, _ in entries)
+    key = tuple((id(w), d) for w, _, d in entries)
     cache = refresh_flipped.__dict__.get("table")
     if cache is None or cache[0] != key:
         nb = L.dtm_flip_desc_bytes()
         import numpy as np
         tab = np.zeros((len(entries), nb // 8), dtype=np.int64)
-        for i, (w, wt) in enumerate(entries):
+        for i, (w, wt, d) in enumerate(entries):
             C, R, S, K = wt.shape
             tab[i, 0] = weight_bf16(w).data_ptr()
             tab[i, 1] = wt.data_ptr()
             tab[i, 2:4] = np.array([K, R, S, C], dtype=np.int32).view(np.int64)
+            st, ph, pw = d if d is not None else (1, 0, 0)
+            tab[i, 4:6] = np.array([st, ph, pw, 0], dtype=np.int32).view(np.int64)
         dev_tab = torch.from_numpy(tab.view(np.uint8).reshape(-1).copy()).to(entries[0][0].device)
         refresh_flipped.table = cache = (key, dev_tab, len(entries))
     L.dtm_weight_flip_transpose_batched(_lib.ptr(cache[1]), cache[2], stream or _lib.stream_ptr())
-    for w, wt in entries:
-        w._flip = (WEIGHT_VERSION[0], wt)
+    for w, wt, d in entries:
+        setattr(w, "_flip" if d is None else "_flipdec", (WEIGHT_VERSION[0], wt, d))
 
 
 def invalidate_weight_copies(params):
@@ -187,9 +204,12 @@ class _Conv2dFn(torch.autograd.Function):
         s = _lib.stream_ptr()
         dx = None
         if ctx.needs_input_grad[0]:
-            wt = weight_flipped(w, g.K, g.R, g.S, g.C)
+            dec = (g.stride, g.pad_h, g.pad_w) if dgrad_decomposable(g) else None
+            wt = weight_flipped(w, g.K, g.R, g.S, g.C, dec)
             dx = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
+            d.dec = int(dec is not None)
             _check(L.dtm_conv_dgrad(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), s), "conv_dgrad")
+            d.dec = 0
         dw = None
         if ctx.needs_input_grad[1]:
             mg = getattr(w, "main_grad", None)

@@ -40,8 +40,10 @@ def main():
     L = _lib.lib()
     s = _lib.stream_ptr()
     only = os.environ.get("ONLY")
-    tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0, "miopen_fwd": 0.0, "miopen_bwd": 0.0}
-    print("%-28s %9s %9s %9s | %9s %9s" % ("shape", "fwd", "dgrad", "wgrad", "mio_fwd", "mio_bwd"))
+    tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0, "miopen_fwd": 0.0, "miopen_bwd": 0.0, "miopen_dgrad": 0.0,
+           "miopen_wgrad": 0.0}
+    print("%-24s %14s %14s %14s | %14s %14s %14s | %s" % ("shape", "fwd", "dgrad", "wgrad", "mio_fwd", "mio_dgrad",
+                                                           "mio_wgrad", "ours/miopen f d w"))
     for (H, C, K, R, st, pad, cnt) in SHAPES:
         if only and only not in "%d_%d_%d_%d" % (H, C, K, R):
             continue
@@ -52,16 +54,22 @@ def main():
         y = torch.empty(B, g.P, g.Q, K, device="cuda", dtype=torch.bfloat16)
         dy = torch.randn_like(y)
         wt = torch.empty(C, R, R, K, device="cuda", dtype=torch.bfloat16)
-        L.dtm_weight_flip_transpose(_lib.ptr(w), _lib.ptr(wt), K, R, R, C, s)
+        if st > 1 and R >= st and not os.environ.get("NODEC"):
+            # strided dgrad: the stride-decomposed form the training path uses (ConvDesc.dec)
+            L.dtm_weight_flip_transpose_dec(_lib.ptr(w), _lib.ptr(wt), K, R, R, C, st, pad, pad, s)
+            d.dec = 1
+        else:
+            L.dtm_weight_flip_transpose(_lib.ptr(w), _lib.ptr(wt), K, R, R, C, s)
         dx = torch.empty_like(x)
         dw = torch.zeros(K, R, R, C, device="cuda")
         fl = 2.0 * B * g.P * g.Q * K * R * R * C
         tf = timeit(lambda: L.dtm_conv_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(y), None, None, None, None, 0,
                                            ctypes.byref(d), s))
         td = timeit(lambda: L.dtm_conv_dgrad(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), s))
+        d.dec = 0
         tw = timeit(lambda: L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(dw), None, None, ctypes.byref(d),
                                              _lib.num_cus(), s))
-        mf = mb = 0.0
+        mf = mb = md = mw = 0.0
         if not os.environ.get("NOMIO"):
             xc = x.permute(0, 3, 1, 2)
             wc = w.permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
@@ -70,16 +78,26 @@ def main():
             mf = timeit(lambda: torch.nn.functional.conv2d(xc, wc, None, st, pad))
             yy = torch.nn.functional.conv2d(xg, wg, None, st, pad)
             gy = torch.randn_like(yy)
-            mb = timeit(lambda: torch.autograd.grad(torch.nn.functional.conv2d(xg, wg, None, st, pad), (xg, wg),
-                                                    gy)) - mf
-        for k, v in (("fwd", tf), ("dgrad", td), ("wgrad", tw), ("miopen_fwd", mf), ("miopen_bwd", mb)):
+            cb = torch.ops.aten.convolution_backward
+            md = timeit(lambda: cb(gy, xc, wc, None, (st, st), (pad, pad), (1, 1), False, (0, 0), 1,
+                                   (True, False, False)))
+            mw = timeit(lambda: cb(gy, xc, wc, None, (st, st), (pad, pad), (1, 1), False, (0, 0), 1,
+                                   (False, True, False)))
+            mb = md + mw
+        for k, v in (("fwd", tf), ("dgrad", td), ("wgrad", tw), ("miopen_fwd", mf), ("miopen_bwd", mb),
+                     ("miopen_dgrad", md), ("miopen_wgrad", mw)):
             tot[k] += v * cnt
         name = "H%d C%d K%d R%d s%d x%d" % (H, C, K, R, st, cnt)
-        print("%-28s %6.0fus %4.0fT %6.0fus %4.0fT %6.0fus %4.0fT | %6.0fus %6.0fus" % (
-            name, tf * 1e6, fl / tf / 1e12, td * 1e6, fl / td / 1e12, tw * 1e6, fl / tw / 1e12, mf * 1e6, mb * 1e6),
-            flush=True)
-    print("TOTAL per step (weighted): fwd %.2f ms  dgrad %.2f ms  wgrad %.2f ms  | miopen fwd %.2f ms bwd %.2f ms" % (
-        tot["fwd"] * 1e3, tot["dgrad"] * 1e3, tot["wgrad"] * 1e3, tot["miopen_fwd"] * 1e3, tot["miopen_bwd"] * 1e3))
+        tfl = lambda t: fl / t / 1e12 if t > 0 else 0.0  # noqa: E731
+        rat = lambda a, b: b / a if (a > 0 and b > 0) else 0.0  # noqa: E731
+        print("%-24s %6.0fus %5.0fT %6.0fus %5.0fT %6.0fus %5.0fT | %6.0fus %5.0fT %6.0fus %5.0fT %6.0fus %5.0fT |"
+              " %4.2f %4.2f %4.2f" % (
+                  name, tf * 1e6, tfl(tf), td * 1e6, tfl(td), tw * 1e6, tfl(tw), mf * 1e6, tfl(mf), md * 1e6, tfl(md),
+                  mw * 1e6, tfl(mw), rat(tf, mf), rat(td, md), rat(tw, mw)), flush=True)
+    print("TOTAL per step (weighted): fwd %.2f ms  dgrad %.2f ms  wgrad %.2f ms  | miopen fwd %.2f ms dgrad %.2f ms "
+          "wgrad %.2f ms" % (tot["fwd"] * 1e3, tot["dgrad"] * 1e3, tot["wgrad"] * 1e3, tot["miopen_fwd"] * 1e3,
+                             tot["miopen_dgrad"] * 1e3, tot["miopen_wgrad"] * 1e3))
+    print("(speed ratio columns: MIOpen time / ours; > 1 = ours faster)")
 
 
 if __name__ == "__main__":
