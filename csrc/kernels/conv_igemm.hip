@@ -684,10 +684,12 @@ __global__ __launch_bounds__(256) void conv_nt_dma_kernel(ConvNTArgs a) {
 // barrier that publishes the stage; padding / out-of-range chunks (from the zero buffer) are left at
 // zero, their validity recomputed from a lagging copy of the k iterator.  All LDS is ONE __shared__
 // array (a second object makes hipcc drain vmcnt before the fragment reads).
-template <int PT, int CT, int NS, int UD, bool PRO>
+// NWP: waves along the pixel dimension (4 / NWP along channels); NWP = 4 with PT = 512, CT = 64 gives every
+// wave a 128 x 64 tile (the 64-channel 3x3 layers: 2x the MFMAs per LDS byte of the 2x2 layout's 64x32)
+template <int PT, int CT, int NS, int UD, bool PRO, int NWP = 2>
 __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
   constexpr int BK = 64;
-  constexpr int WP = PT / 2, WC = CT / 2;
+  constexpr int WP = PT / NWP, WC = CT / (4 / NWP);
   constexpr int TP = WP / 16, TC = WC / 16;
   constexpr int AI = PT / 32, WI = CT / 32;  // 8-row DMA groups per wave per k-tile
   constexpr int G = AI + WI;                 // DMA instructions per wave per k-tile
@@ -814,7 +816,7 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
 #pragma unroll
     for (int j = 0; j < TP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const int wp = wave % 2, wc = wave / 2;
+  const int wp = wave % NWP, wc = wave / NWP;
   const int fr = lane & 15, fk = lane >> 4;
   auto compute = [&](int slot) {
     // all 2 x (TP + TC) fragment reads of the k-tile first: the ks = 1 reads are in flight under the
@@ -1755,11 +1757,11 @@ static void launch_w8(const ConvNTArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((conv_nt_w8_kernel<PT, CT, NWP, NS, UD>), grid, dim3(512), 0, st, a);
 }
 
-template <int PT, int CT, int NS, int UD>
+template <int PT, int CT, int NS, int UD, int NWP = 2>
 static void launch_pipe(const ConvNTArgs& a, hipStream_t st) {
   dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT);
-  if (a.in_scale) hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, true>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, false>), grid, dim3(256), 0, st, a);
+  if (a.in_scale) hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, true, NWP>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, false, NWP>), grid, dim3(256), 0, st, a);
 }
 
 static int device_cus() {
@@ -1890,6 +1892,9 @@ static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
   if (id >= 20 && id <= 23) return {id, 128, 2};
   if (id == 24 || id == 25) return {id, 256, 2};  // 256 x 64 pipelined (waves 2x2 of 128x32), 2 / 3 slots
   if (id == 26) return {id, 128, 2};              // 128 x 64 pipelined, 2 slots
+  if (id == 27) return {id, 256, 2};              // 256 x 128 pipelined, waves 2x2 of 128x64
+  if (id == 28) return {id, 512, 4};              // 512 x 64 pipelined, waves 4x1 of 128x64
+  if (id == 29) return {id, 256, 4};              // 256 x 64 pipelined, waves 4x1 of 64x64
   // 8-wave 256-pixel tiles (no prologue): 40 = 256x256 (waves 2x4), 41 = 256x128 3-slot (4x2),
   // 42 = 256x128 2-slot, 43 = 256x256 (waves 4x2)
   if (id >= 40 && id <= 43 && a.in_scale) id = 0;
@@ -1929,6 +1934,9 @@ static void dispatch_ud(const ConvNTArgs& a, const TileCfg& t, hipStream_t st) {
   else if (t.id == 24) launch_pipe<256, 64, 2, UD>(a, st);
   else if (t.id == 25) launch_pipe<256, 64, 3, UD>(a, st);
   else if (t.id == 26) launch_pipe<128, 64, 2, UD>(a, st);
+  else if (t.id == 27) launch_pipe<256, 128, 2, UD>(a, st);     // waves 2x2 of 128x64
+  else if (t.id == 28) launch_pipe<512, 64, 2, UD, 4>(a, st);   // waves 4x1 of 128x64
+  else if (t.id == 29) launch_pipe<256, 64, 2, UD, 4>(a, st);   // waves 4x1 of 64x64
   else if (t.id == 40) launch_w8<256, 256, 2, 2, UD>(a, st);
   else if (t.id == 41) launch_w8<256, 128, 4, 3, UD>(a, st);
   else if (t.id == 42) launch_w8<256, 128, 4, 2, UD>(a, st);
@@ -2136,6 +2144,8 @@ static void launch_wgrad(const ConvWgradArgs& a, int splits, hipStream_t st) {
 // wgrad tile override (-1 = policy) and the blocks-per-CU target of the split count for the pipelined
 // kernels (A/B sweeps: tools/conv_tile_sweep.py)
 static int g_wgrad_env = -2;
+static int g_wgrad_n256 = 0;  // A/B knob: 256-column register-staged wgrad tiles for K <= 64, Kg > 128 (see policy)
+DTM_API void dtm_conv_set_wgrad_n256(int on) { g_wgrad_n256 = on; }
 static int g_wgrad_occ = 4;
 DTM_API void dtm_conv_set_wgrad_tile(int id, int occ) {
   g_wgrad_env = id;
@@ -2192,6 +2202,11 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   }
   const int wenv = g_wgrad_env;
   int wt = wenv >= 0 ? wenv : (d->K <= 64 ? 1 : 0);
+  // K <= 64 with a reduction width over one 128-column tile (the stem's 224, 56x56 256->64, 3x3 64->64):
+  // 256-column tiles read (and BN-backward-transform) the dy operand half as many times (A/B knob
+  // dtm_conv_set_wgrad_n256)
+  // (knob 1: only with the BN-backward operand transform, i.e. the stem; 2: every such layer)
+  if (wenv == -1 && wt == 1 && a.Kg > 128 && (g_wgrad_n256 == 2 || (g_wgrad_n256 == 1 && bn))) wt = 4;
   int occ = g_wgrad_occ;
   // policy (tools/conv_tile_sweep.py WTILES sweep, ResNet-50 shapes): the pipelined kernel at 2 blocks
   // per CU wins every layer with K > 64 (-10..-25 %); 4 blocks' worth of splits for the deep 3x3 7x7s
@@ -2203,9 +2218,10 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
     if (g_tile_w8 && d->K >= 256 && a.Kg >= 1024 && (d->R * d->S > 1 || d->K >= 1024)) wt = 12;
   }
   if (wt >= 10 && (in_scale || bn)) wt = d->K <= 64 ? 1 : 0;  // the pipelined kernels have no operand prologues
-  const bool small_m = (wt == 1 || wt == 2 || wt == 13 || wt == 14 || wt == 15);
+  const bool small_m = (wt == 1 || wt == 2 || wt == 4 || wt == 5 || wt == 13 || wt == 14 || wt == 15);
   const bool big = wt == 12;  // 8-wave 256x256 (one block per CU)
-  const int MT = small_m ? 64 : (big ? 256 : 128), NT = (big || wt == 13 || wt == 14) ? 256 : 128;
+  const int MT = small_m ? 64 : (big ? 256 : 128),
+            NT = (big || wt == 4 || wt == 5 || wt == 13 || wt == 14) ? 256 : 128;
   if (big) occ = (wenv == 12 && g_wgrad_occ != 4) ? g_wgrad_occ : 1;  // (sweeps: WTILES=12:<occ>)
   long tiles = (long)((a.Kg + NT - 1) / NT) * ((a.K + MT - 1) / MT);
   long target = (long)num_cus * (wt >= 10 ? occ : 3);
@@ -2237,6 +2253,8 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
     else
       hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 128, 2>), grid, dim3(256), 0, (hipStream_t)stream, a);
   } else if (wt == 1) launch_wgrad<64, 128, 32, 64>(a, (int)splits, (hipStream_t)stream);
+  else if (wt == 4) launch_wgrad<64, 256, 32, 128>(a, (int)splits, (hipStream_t)stream);
+  else if (wt == 5) launch_wgrad<64, 256, 32, 128, 1>(a, (int)splits, (hipStream_t)stream);
   else if (wt == 2) launch_wgrad<64, 128, 32, 64, 1>(a, (int)splits, (hipStream_t)stream);
   else if (wt == 3) launch_wgrad<128, 128, 64, 64, 1>(a, (int)splits, (hipStream_t)stream);
   else launch_wgrad<128, 128, 64, 64>(a, (int)splits, (hipStream_t)stream);

@@ -102,9 +102,52 @@ __global__ __launch_bounds__(256) void in_top_k_kernel(const void* __restrict__ 
   if (lane == 0) out[row] = (valid && isfinite(xt) && cnt < k) ? 1 : 0;
 }
 
+// Packed-row stem input (fused.py _StemConvBNFn): xp[n][h][w][0..3] = x[n][h-pad][w-pad][c] (c < C, else 0),
+// zero outside the image, as bf16 -- the zero border, the channel padding to 4 and the dtype conversion
+// in one pass (one thread = two 8-byte output pixels = one 16-B store) instead of a fill + a pad copy.
+template <bool F32>
+__global__ __launch_bounds__(256) void stem_pack_kernel(const void* __restrict__ x, bf16_t* __restrict__ xp, int N,
+                                                        int H, int W, int C, int Hp, int Wp, int pad) {
+  const long npair = (long)N * Hp * (Wp / 2);
+  for (long t = blockIdx.x * 256L + threadIdx.x; t < npair; t += (long)gridDim.x * 256) {
+    const int w0 = (int)(t % (Wp / 2)) * 2;
+    const long nh = t / (Wp / 2);
+    const int h = (int)(nh % Hp), n = (int)(nh / Hp);
+    const int ih = h - pad;
+    uint32_t o[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int iw = w0 + k - pad;
+      if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
+        const long base = (((long)n * H + ih) * W + iw) * C;
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int c = 0; c < C; ++c)
+          v[c] = F32 ? ((const float*)x)[base + c] : __uint_as_float((uint32_t)((const uint16_t*)x)[base + c] << 16);
+        o[2 * k] = pack2bf(v[0], v[1]);
+        o[2 * k + 1] = pack2bf(v[2], v[3]);
+      }
+    }
+    *(uint4*)(xp + (nh * Wp + w0) * 4) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 }  // namespace dtm
 
 using namespace dtm;
+
+// dtype: 0 = fp32, 1 = bf16 input; Wp even, C <= 4
+DTM_API int dtm_stem_pack(const void* x, int dtype, void* xp, int N, int H, int W, int C, int Hp, int Wp, int pad,
+                          hipStream_t st) {
+  if (C < 1 || C > 4 || (Wp & 1) || ((uintptr_t)xp & 15)) return -1;
+  const long npair = (long)N * Hp * (Wp / 2);
+  long blocks = (npair + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  if (dtype == 0)
+    stem_pack_kernel<true><<<(unsigned)blocks, 256, 0, st>>>(x, (bf16_t*)xp, N, H, W, C, Hp, Wp, pad);
+  else
+    stem_pack_kernel<false><<<(unsigned)blocks, 256, 0, st>>>(x, (bf16_t*)xp, N, H, W, C, Hp, Wp, pad);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
 
 // dtype: 0 = fp32, 1 = bf16.  Same seed => same mask (backward passes the upstream gradient).
 DTM_API int dtm_dropout(const void* x, void* y, long n, int dtype, float keep_prob, unsigned long long seed,

@@ -501,7 +501,13 @@ class _StemConvBNFn(torch.autograd.Function):
         Hp = max(H + 2 * pad, st * (P - 1) + R)
         Wp = max(W + 2 * pad, st * (Q - 1) + 8)
         Wp += Wp % 2  # 16-B aligned rows (the 64-B runs start at 16*q bytes)
-        xp = torch.nn.functional.pad(x.to(torch.bfloat16), (0, 4 - C, pad, Wp - W - pad, pad, Hp - H - pad))
+        if x.dtype in (torch.float32, torch.bfloat16) and x.is_contiguous():
+            # zero border + channel pad + bf16 in one pass
+            xp = torch.empty((N, Hp, Wp, 4), device=x.device, dtype=torch.bfloat16)
+            _check(L.dtm_stem_pack(_lib.ptr(x), 0 if x.dtype == torch.float32 else 1, _lib.ptr(xp), N, H, W, C, Hp,
+                                   Wp, pad, s), "stem_pack")
+        else:
+            xp = torch.nn.functional.pad(x.to(torch.bfloat16), (0, 4 - C, pad, Wp - W - pad, pad, Hp - H - pad))
         wv = torch.zeros((K, R, 8, 4), device=x.device, dtype=torch.bfloat16)
         wv[:, :, :S, :C] = weight_bf16(w)
         d = _lib.ConvDesc(N, Hp, Wp, 32, K, R, 1, P, Q, st, 0, 0, 8)

@@ -161,7 +161,7 @@ def test_image_augment_kernel_matches_oracle(distort, size):
     assert got.is_cuda and _rel(got.cpu(), ref_out) < 1e-4
 
 
-@pytest.mark.parametrize("tile", [20, 21, 22, 23, 24, 25, 26, 30, 31, 40, 41, 42, 43])
+@pytest.mark.parametrize("tile", [20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 40, 41, 42, 43])
 @pytest.mark.parametrize("prologue", [False, True])
 @pytest.mark.parametrize("case", [(4, 15, 15, 64, 96, 3, 2), (2, 14, 14, 128, 256, 3, 1), (3, 7, 7, 512, 200, 1, 1),
                                   (2, 9, 9, 24, 40, 3, 1), (4, 12, 12, 64, 256, 1, 1), (3, 7, 7, 128, 96, 1, 1),
@@ -211,12 +211,13 @@ def test_conv_pipelined_tiles_match_reference(tile, prologue, case):
     assert _rel(stats[0], yf.sum(0)) < 1e-3 and _rel(stats[1], yf.square().sum(0)) < 1e-3
 
 
-@pytest.mark.parametrize("tile", [10, 11, 12, 13, 14, 15])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 10, 11, 12, 13, 14, 15])
 @pytest.mark.parametrize("case", [(4, 15, 15, 64, 96, 3, 2), (2, 14, 14, 128, 256, 3, 1), (3, 7, 7, 512, 200, 1, 1),
                                   (2, 9, 9, 24, 40, 3, 1), (5, 8, 8, 64, 64, 1, 1), (4, 9, 9, 256, 512, 3, 1)])
 def test_conv_wgrad_pipelined_tiles_match_reference(tile, case):
-    """The pipelined LDS-DMA wgrad kernels (inverse transposed-read image mapping for the DMA slots,
-    split-K slabs) against the fp32 reference, including K / R*S*C tails and empty splits."""
+    """The wgrad kernels - register-staged tiles 0-5 (64 / 128 rows x 128 / 256 columns) and the pipelined
+    LDS-DMA ones (inverse transposed-read image mapping for the DMA slots) - with split-K slabs against the
+    fp32 reference, including K / R*S*C tails and empty splits."""
     import ctypes
 
     from distributed_tensorflow_models_amd.ops import _lib
@@ -400,3 +401,19 @@ def test_linear_bias_relu_fused(B, N, relu):
     assert _rel(bg.grad.cpu(), br.grad) < 5e-3
     assert _rel(wg.grad.cpu(), wr.grad) < 2e-2
     assert _rel(xg.grad.float().cpu(), xr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(2, 17, 13, 3, 3, 26, 20), (3, 8, 8, 1, 2, 14, 14), (1, 5, 7, 4, 0, 6, 8)])
+def test_stem_pack_kernel(dtype, shape):
+    """dtm_stem_pack (zero border + channel pad to 4 + bf16 in one pass) = torch pad of the bf16 input."""
+    from distributed_tensorflow_models_amd.ops import _lib
+    N, H, W, C, pad, Hp, Wp = shape
+    x = torch.randn(N, H, W, C, device=DEV).to(dtype)
+    xp = torch.full((N, Hp, Wp, 4), 7.0, device=DEV, dtype=torch.bfloat16)
+    rc = _lib.lib().dtm_stem_pack(_lib.ptr(x), 0 if dtype == torch.float32 else 1, _lib.ptr(xp), N, H, W, C, Hp, Wp,
+                                  pad, _lib.stream_ptr())
+    assert rc == 0
+    ref_p = torch.nn.functional.pad(x.to(torch.bfloat16), (0, 4 - C, pad, Wp - W - pad, pad, Hp - H - pad))
+    torch.cuda.synchronize()
+    assert torch.equal(xp, ref_p)
