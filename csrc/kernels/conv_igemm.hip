@@ -69,6 +69,7 @@ struct ConvNTArgs {
   // grid is pixel (n, i*ostr + oa, j*ostr + ob) of the OH x OW tensor that y and every epilogue side
   // input (add_src, act_x, act_r, act_mask) index.  ostr == 1: identity (OH = P, OW = Q, oa = ob = 0)
   int ostr, oa, ob, OH, OW;
+  int pre_side;  // conv_nt_kernel: load the dgrad epilogue's side inputs before the last k-tile (A/B knob)
 };
 
 // full-resolution coordinates / row of output pixel m (see ConvNTArgs::ostr)
@@ -101,6 +102,54 @@ __device__ __forceinline__ void epi_barrier() {
   }
 }
 
+// Side inputs of the staged dgrad epilogue (add_src / act_x / act_r chunks, ReLU-mask bytes) for the NIT
+// rows one thread stores; epi_side_load issues them (e.g. before a kernel's last k-tile, so their HBM
+// latency overlaps MFMAs instead of following them) and conv_nt_epilogue consumes them (a.pre_side).
+template <int NIT>
+struct EpiSide {
+  uint4 pa[NIT], px[NIT], pr[NIT];
+  uint32_t pm[NIT];
+  bool ph[NIT];
+};
+template <int PT, int CT, int NT>
+__device__ __forceinline__ void epi_side_load(const ConvNTArgs& a, int p0, int c0, EpiSide<PT * (CT / 8) / NT>& sd) {
+  constexpr int CPR = CT / 8, NIT = PT * CPR / NT;
+  const int tid = threadIdx.x;
+  const int kc = c0 + (tid % CPR) * 8;
+  const bool act = a.act_x != nullptr, amask = act && a.act_mask != nullptr;
+#pragma unroll
+  for (int j = 0; j < NIT; ++j) {
+    sd.pa[j] = sd.px[j] = sd.pr[j] = make_uint4(0, 0, 0, 0);
+    sd.pm[j] = 0u;
+    sd.ph[j] = false;
+    const int m = p0 + (j * NT + tid) / CPR;
+    if (m < a.M && kc < a.K) {
+      const size_t o = (size_t)out_row(a, m) * a.K + kc;
+      if (a.add_src) {
+        const bf16_t* src = a.add_src + o;
+        if (a.add_stride > 1) {
+          int n, h, w;
+          out_nhw(a, m, n, h, w);
+          const int s = a.add_stride;
+          src = (h % s == 0 && w % s == 0) ? a.add_src + ((size_t)(n * a.add_H + h / s) * a.add_W + w / s) * a.K + kc
+                                           : nullptr;
+        }
+        if (src) {
+          sd.pa[j] = *(const uint4*)src;
+          sd.ph[j] = true;
+        }
+      }
+      if (act) {
+        sd.px[j] = *(const uint4*)(a.act_x + o);
+        if (amask) {
+          sd.pm[j] = a.act_mask[o >> 3];
+          if (a.act_r) sd.pr[j] = *(const uint4*)(a.act_r + o);
+        }
+      }
+    }
+  }
+}
+
 // STG: 1 = LDS-staged stores (K % 8 == 0), 2 = direct 8-B stores.  Kept compile-time: a runtime choice
 // between an LDS and a global pointer makes hipcc emit flat stores, which wait on both counters.
 // SACC (statistics accumulate, persistent kernels): the BatchNorm sums are not shuffle-reduced per tile;
@@ -111,7 +160,8 @@ template <int PT, int CT, int WP, int WC, int STG, bool RAWB = false, bool EXACT
           bool SACC = false, int NT = 256>
 __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&acc)[WC / 16][WP / 16], char* smem,
                                                  int p0, int c0, int by, float* ssum = nullptr,
-                                                 float* ssq = nullptr) {
+                                                 float* ssq = nullptr,
+                                                 const EpiSide<PT * (CT / 8) / NT>* pre = nullptr) {
   constexpr int NWP = PT / WP;
   constexpr int TP = WP / 16, TC = WC / 16;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -214,7 +264,13 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
         pm[j] = 0u;
         ph[j] = false;
       }
-      if (side) {
+      if (side && pre) {
+#pragma unroll
+        for (int j = 0; j < GRP; ++j) {
+          pa[j] = pre->pa[g0 + j]; px[j] = pre->px[g0 + j]; pr[j] = pre->pr[g0 + j];
+          pm[j] = pre->pm[g0 + j]; ph[j] = pre->ph[g0 + j];
+        }
+      } else if (side) {
 #pragma unroll
         for (int j = 0; j < GRP; ++j) {
           const int row = ((g0 + j) * NT + tid) / CPR;
@@ -353,7 +409,7 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
   }
 }
 
-template <int PT, int CT, int WP, int WC, int UD, int NBUF>
+template <int PT, int CT, int WP, int WC, int UD, int NBUF, bool PRE = false>
 __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
   constexpr int BK = 64;
   constexpr int NWP = PT / WP;
@@ -521,7 +577,13 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
   gload(0, st);
   swrite(0, st);
   __syncthreads();
+  // dgrad epilogue side inputs issued before the last k-tile's MFMAs (a.pre_side, staged stores only)
+  constexpr int NIT = PT * (CT / 8) / 256;
+  EpiSide<PRE ? NIT : 1> sd;
   for (int kt = 0; kt < nk; ++kt) {
+    if constexpr (PRE) {
+      if (kt == nk - 1) epi_side_load<PT, CT, 256>(a, p0, c0, sd);
+    }
     if constexpr (NBUF == 2) {
       const int cur = kt & 1;
       if (kt + 1 < nk) gload(kt + 1, st);
@@ -542,7 +604,8 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
   }
 
   static_assert(PT * (CT * 2 + 16) <= NBUF * BUF, "output staging fits in the operand buffers");
-  if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1>(a, acc, smem, p0, c0, by);
+  if constexpr (PRE) conv_nt_epilogue<PT, CT, WP, WC, 1>(a, acc, smem, p0, c0, by, nullptr, nullptr, &sd);
+  else if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1>(a, acc, smem, p0, c0, by);
   else conv_nt_epilogue<PT, CT, WP, WC, 2>(a, acc, smem, p0, c0, by);
 }
 
@@ -1832,7 +1895,11 @@ static bool stream_ok(const ConvNTArgs& a) {
 template <int PT, int CT, int WP, int WC, int UD, int NBUF = 2>
 static void launch_nt(const ConvNTArgs& a, hipStream_t st) {
   dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT);
-  hipLaunchKernelGGL((conv_nt_kernel<PT, CT, WP, WC, UD, NBUF>), grid, dim3(256), 0, st, a);
+  // dgrads with epilogue side inputs: the variant that loads them before the last k-tile (a.pre_side)
+  if (a.pre_side && (a.K & 7) == 0 && (a.add_src || a.act_x))
+    hipLaunchKernelGGL((conv_nt_kernel<PT, CT, WP, WC, UD, NBUF, true>), grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_nt_kernel<PT, CT, WP, WC, UD, NBUF>), grid, dim3(256), 0, st, a);
 }
 
 // tile variants: 0 = 128 pix x 128 ch (4 waves 2x2 of 64x64), 1 = 128 x 64 (4x1 of 32x64),
@@ -1850,6 +1917,8 @@ DTM_API void dtm_conv_set_kwide(int on) { g_kwide = on; }
 DTM_API void dtm_conv_set_w8(int on) { g_tile_w8 = on; }
 static int g_k64_tile = 3;  // tile of the 64-output-channel layers (A/B knob: dtm_conv_set_k64_tile)
 DTM_API void dtm_conv_set_k64_tile(int id) { g_k64_tile = id; }
+static int g_pre_side = 0;  // A/B knob: early side-input loads in the register-staged dgrad epilogue
+DTM_API void dtm_conv_set_pre_side(int on) { g_pre_side = on; }
 static int g_act_tile = -1;  // A/B knob: tile of the dgrads with a fused activation-backward epilogue (-1 = policy)
 DTM_API void dtm_conv_set_act_tile(int id) { g_act_tile = id; }
 static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
@@ -1861,11 +1930,11 @@ static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
   // variants win almost everywhere (more resident blocks hide the short-K latency); the 2-buffer
   // 128x128 tile keeps the small-M / deep-K layers (7x7 maps, K-reduction >= 2048)
   int id = g_tile_env;
-  if (id == -1 && a.act_x && g_act_tile >= 0) id = g_act_tile;
   // the pipelined LDS-DMA 128x128 tile (2 slots, 2 blocks/CU) wins every deep-reduction layer without the
   // prologue (tools/conv_tile_sweep.py: 3x3 at 14x14 / 7x7 -13..-18 %, deep 1x1 -5..-16 %)
   if (id == -4) id = -1;  // (-4: the policy without the streaming kernel, for A/B runs)
   else if (id == -1 && a.Kg == 64 && stream_ok(a) && (g_stream_act || !a.act_x)) id = a.K >= 128 ? 30 : 31;
+  if (id == -1 && a.act_x && g_act_tile >= 0) id = g_act_tile;  // (A/B: the non-streaming act dgrads)
   // (the persistent streaming 1x1 kernel: the 64-deep 56x56 expand / reduce layers and their dgrads are
   // HBM streams: -20..-33 % (tools/conv_tile_sweep.py); at Kg 128 its 1 block/CU loses)
   // the 8-wave 256x256 tile (id 40) where it fills the chip: >= ~150 tiles (one round, 58-100 % of the
@@ -1975,6 +2044,7 @@ static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, cons
   a.M = d->N * d->P * d->Q; a.Kg = d->R * d->S * d->C; a.relu = relu;
   a.fd_PQ = make_fastdiv(d->P * d->Q); a.fd_Q = make_fastdiv(d->Q);
   a.ostr = 1; a.oa = a.ob = 0; a.OH = a.P; a.OW = a.Q;
+  a.pre_side = 0;
   int rows = 0;
   const TileCfg tc = pick_tile(a, stats);
   if (stats) {
@@ -2072,6 +2142,7 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvD
   a.stride = 1;
   a.Hv = d->P; a.Wv = d->Q;
   a.OH = d->H; a.OW = d->W;
+  a.pre_side = g_pre_side;
   const int rw = act_r ? 4 : 2;
   // launches: one plain dgrad over the zero-dilated dy (UD = stride), or (d->dec, stride > 1) one stride-1
   // conv per output parity class (a, b) with that class's taps of the decomposed weight (dec_dim)

@@ -102,6 +102,7 @@ _SIGS = {
     "dtm_conv_set_stream_act": (None, [_I]),
     "dtm_conv_set_act_tile": (None, [_I]),
     "dtm_conv_set_wgrad_n256": (None, [_I]),
+    "dtm_conv_set_pre_side": (None, [_I]),
     "dtm_stem_pack": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "dtm_dropout": (_I, [_P, _P, _L, _I, _F, ctypes.c_ulonglong, _P, _P]),
     "dtm_in_top_k": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),

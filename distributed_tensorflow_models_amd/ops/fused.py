@@ -659,7 +659,7 @@ def _prologue_mode(x_shape, w_shape, stride):
     Measured per ResNet-50 layer (tools/conv_tile_sweep.py with WGRAD=1, batch 256): the prologue
     costs fwd +13..+66 us and wgrad +12..+68 us per layer, a materialising pass 6..35 us -> 'mat' wins
     every conv except the stride-2 3x3 at 56x56, where it is neutral.
-    DTM_PROLOGUE = auto (default) | fused | mat | apply | legacy."""
+    DTM_PROLOGUE = auto (default) | auto0 (auto without the expansion-1x1 rule) | fused | mat | apply | legacy."""
     import os
     mode = os.environ.get("DTM_PROLOGUE", "auto")
     if mode in ("fused", "apply", "mat"):
@@ -670,6 +670,11 @@ def _prologue_mode(x_shape, w_shape, stride):
     if mode == "legacy":  # the previous policy: autograd apply for the stride-1 3x3 convs at <= 14x14
         return "apply" if (R * S > 1 and st == 1 and H * W <= 14 * 14) else "fused"
     if st > 1 and H * W >= 56 * 56:
+        return "fused"
+    K, C = w_shape[0], w_shape[3]
+    if mode == "auto" and R * S == 1 and st == 1 and C == 64 and K == 256:
+        # the stage-1 expansion 1x1: its backward (dtm_conv1x1_bnbwd) recomputes relu(bn(x)) from the raw x
+        # anyway, so the materialised copy would only feed this forward (streaming kernel, prologue in LDS)
         return "fused"
     return "mat"
 
