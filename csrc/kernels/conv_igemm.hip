@@ -2231,11 +2231,18 @@ struct WgradBN {
 };
 
 static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float* in_scale, const float* in_shift,
-                           const ConvDesc* d, int num_cus, const WgradBN* bn, void* stream);
+                           const ConvDesc* d, int num_cus, const WgradBN* bn, void* stream, bool side = false);
 
 DTM_API int dtm_conv_wgrad(const void* x, const void* dy, float* dw, const float* in_scale,
                            const float* in_shift, const ConvDesc* d, int num_cus, void* stream) {
   return conv_wgrad_impl(x, dy, dw, in_scale, in_shift, d, num_cus, nullptr, stream);
+}
+
+// dw is a persistent gradient buffer that nothing reads before dtm_side_join: the split-K slab reduction
+// runs on the side stream (workspace.hip)
+DTM_API int dtm_conv_wgrad_side(const void* x, const void* dy, float* dw, const float* in_scale,
+                                const float* in_shift, const ConvDesc* d, int num_cus, void* stream) {
+  return conv_wgrad_impl(x, dy, dw, in_scale, in_shift, d, num_cus, nullptr, stream, true);
 }
 
 // Weight gradient of a conv followed by a training BatchNorm whose stats-combine output (comb) has no
@@ -2249,7 +2256,7 @@ DTM_API int dtm_conv_wgrad_bnbwd(const void* x, const void* g, const void* y, co
 }
 
 static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float* in_scale, const float* in_shift,
-                           const ConvDesc* d, int num_cus, const WgradBN* bn, void* stream) {
+                           const ConvDesc* d, int num_cus, const WgradBN* bn, void* stream, bool side) {
   if (d->C % 8 || d->K % 8) return -1;
   ConvWgradArgs a;
   a.x = (const bf16_t*)x; a.dy = (const bf16_t*)dy; a.dw = dw;
@@ -2305,7 +2312,9 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   long steps_per = (ksteps + splits - 1) / splits;
   a.pix_per_split = (int)(steps_per * 64);
   splits = (a.Mpix + a.pix_per_split - 1) / a.pix_per_split;
-  float* ws = dtm_ws_get((size_t)splits * a.K * a.Kg);
+  int slot = -1;
+  float* ws = side ? dtm_side_slab((size_t)splits * a.K * a.Kg, (hipStream_t)stream, &slot) : nullptr;
+  if (!ws) ws = dtm_ws_get((size_t)splits * a.K * a.Kg);
   if (!ws) return -4;
   a.dw = ws;
   if (wt >= 10) {
@@ -2330,7 +2339,8 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   else if (wt == 3) launch_wgrad<128, 128, 64, 64, 1>(a, (int)splits, (hipStream_t)stream);
   else launch_wgrad<128, 128, 64, 64>(a, (int)splits, (hipStream_t)stream);
   // dW += sum over the split slabs (every slab element is written: tiles cover [K][Kg] exactly)
-  dtm_reduce_rows(ws, (int)splits, a.K * a.Kg, a.K * a.Kg, dw, (hipStream_t)stream);
+  if (slot >= 0) dtm_side_reduce(slot, (int)splits, a.K * a.Kg, a.K * a.Kg, dw, (hipStream_t)stream);
+  else dtm_reduce_rows(ws, (int)splits, a.K * a.Kg, a.K * a.Kg, dw, (hipStream_t)stream);
   return 0;
 }
 

@@ -162,3 +162,86 @@ void dtm_reduce_rows(const float* ws, int rows, int width, int ld, float* out, h
 }
 
 DTM_API int dtm_ws_reserve(long floats) { return dtm_ws_get((size_t)floats) ? 0 : -1; }
+
+// ---- side-stream reductions --------------------------------------------------------------------
+// The split-K weight-gradient slabs are summed into the fp32 gradient buffer, which nothing reads
+// before the end of backward (bucket all-reduce, NaN guard, optimizer).  So that reduction -- a short,
+// latency-bound launch per conv -- runs on a low-priority side stream forked from the caller's stream
+// by an event, overlapping the next layers' kernels instead of sitting between them.  Its slab comes
+// from a ring of NRING buffers (never the shared dtm_ws arena, which the next kernel reuses at once);
+// a ring slot is handed out again only after the caller's stream waits for its previous reduction.
+// dtm_side_join(stream) makes a stream wait for every side reduction issued so far: the engine calls it
+// after backward and before any collective.  Under hipGraph capture the caller reduces inline.
+namespace {
+constexpr int NRING = 4;
+hipStream_t g_side = nullptr;
+hipEvent_t g_fork[NRING], g_done[NRING], g_join;
+bool g_used[NRING] = {false, false, false, false};
+float* g_ring[NRING] = {nullptr, nullptr, nullptr, nullptr};
+size_t g_ring_floats[NRING] = {0, 0, 0, 0};
+int g_ring_i = 0;
+bool g_pending = false;
+int g_side_on = 0;
+
+bool side_init() {
+  if (g_side) return true;
+  int least = 0, greatest = 0;
+  hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (hipStreamCreateWithPriority(&g_side, hipStreamNonBlocking, least) != hipSuccess) {
+    g_side = nullptr;
+    return false;
+  }
+  for (int i = 0; i < NRING; ++i) {
+    hipEventCreateWithFlags(&g_fork[i], hipEventDisableTiming);
+    hipEventCreateWithFlags(&g_done[i], hipEventDisableTiming);
+  }
+  hipEventCreateWithFlags(&g_join, hipEventDisableTiming);
+  return true;
+}
+}  // namespace
+
+DTM_API void dtm_set_side_reduce(int on) { g_side_on = on; }
+
+// returns a slab buffer and its ring slot (slot -1: use the inline path -- capture, disabled, no memory)
+float* dtm_side_slab(size_t floats, hipStream_t st, int* slot) {
+  *slot = -1;
+  if (!g_side_on || !side_init()) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  const int i = g_ring_i;
+  if (floats > g_ring_floats[i]) {
+    if (g_ring[i]) {
+      hipEventSynchronize(g_done[i]);
+      hipFree(g_ring[i]);
+    }
+    size_t n = floats < (4u << 20) ? (4u << 20) : floats;
+    if (hipMalloc(&g_ring[i], n * sizeof(float)) != hipSuccess) {
+      g_ring[i] = nullptr;
+      g_ring_floats[i] = 0;
+      return nullptr;
+    }
+    g_ring_floats[i] = n;
+    g_used[i] = false;
+  }
+  // the slot's previous reduction must have read its slab before this stream's kernel overwrites it
+  if (g_used[i]) hipStreamWaitEvent(st, g_done[i], 0);
+  g_ring_i = (i + 1) % NRING;
+  *slot = i;
+  return g_ring[i];
+}
+
+void dtm_side_reduce(int slot, int rows, int width, int ld, float* out, hipStream_t st) {
+  hipEventRecord(g_fork[slot], st);
+  hipStreamWaitEvent(g_side, g_fork[slot], 0);
+  dtm_reduce_rows(g_ring[slot], rows, width, ld, out, g_side);
+  hipEventRecord(g_done[slot], g_side);
+  g_used[slot] = true;
+  g_pending = true;
+}
+
+DTM_API void dtm_side_join(void* stream) {
+  if (!g_pending || !g_side) return;
+  hipEventRecord(g_join, g_side);
+  hipStreamWaitEvent((hipStream_t)stream, g_join, 0);
+  g_pending = false;
+}

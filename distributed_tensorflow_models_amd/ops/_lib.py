@@ -47,6 +47,9 @@ _SIGS = {
     "dtm_conv1x1_bnbwd": (_I, [_P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _L, _I, _I, _P]),
     "dtm_conv_wgrad_bnbwd": (_I, [_P, _P, _P, _P, _P, _P, _F, _P, _P, _P, ctypes.POINTER(ConvDesc), _I, _P]),
     "dtm_conv_wgrad": (_I, [_P, _P, _P, _P, _P, ctypes.POINTER(ConvDesc), _I, _P]),
+    "dtm_conv_wgrad_side": (_I, [_P, _P, _P, _P, _P, ctypes.POINTER(ConvDesc), _I, _P]),
+    "dtm_side_join": (None, [_P]),
+    "dtm_set_side_reduce": (None, [_I]),
     "dtm_weight_flip_transpose": (None, [_P, _P, _I, _I, _I, _I, _P]),
     "dtm_weight_flip_transpose_batched": (None, [_P, _I, _P]),
     "dtm_weight_flip_transpose_dec": (None, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),

@@ -300,6 +300,9 @@ class ASPTrainStep:
         out = self.model(images, training=True)
         loss = self.loss_fn(out, labels)
         loss.backward()
+        if images.is_cuda:
+            from ..ops.nn import side_join
+            side_join()  # side-stream weight-gradient reductions land before the push reads them
         gs = self.store.global_step()
         lr = self.lr_schedule(gs) if self.lr_schedule else None
         # ASP: nothing waits for the update (Hogwild: the next pull on this stream sees it); SSP ticks

@@ -180,6 +180,8 @@ class BSPDataParallel:
         self._launched[bi] = True
         if self.world == 1:
             return
+        if self.flat.is_cuda:
+            opsnn.side_join()  # the collective's stream syncs with this stream at issue
         with roctx("allreduce_bucket_%d" % bi):
             if bi in self.compact:
                 p, (r0, r1, s0, s1), buf, low = self.compact[bi]
@@ -198,6 +200,8 @@ class BSPDataParallel:
     def finish(self):
         """Launch any bucket not yet reduced (unused params / no overlap) and make the current
         stream wait for every reduction."""
+        if self.flat.is_cuda:
+            opsnn.side_join()
         for bi in range(len(self.buckets)):
             if not self._launched[bi]:
                 self._launch(bi)
