@@ -594,20 +594,7 @@ __global__ __launch_bounds__(256) void stats_reduce_finalize_kernel(
     for (int i = 0; i < 8; ++i) {
     const int c = cb + i * 256 + threadIdx.x;
     if (c >= K) break;
-    const float sum = sv[i], sq = qv[i];
-    const float mean = sum / count;
-    const float var = fmaxf(sq / count - mean * mean, 0.f);
-    const float rstd = rsqrtf(var + eps);
-    const float sc = (gamma ? gamma[c] : 1.f) * rstd;
-    out[c] = sc;
-    out[K + c] = (beta ? beta[c] : 0.f) - mean * sc;
-    out[2 * K + c] = mean;
-    out[3 * K + c] = rstd;
-    if (update) {
-      const float uvar = (bessel && count > 1.f) ? var * count / (count - 1.f) : var;
-      mov_mean[c] -= (mov_mean[c] - mean) * (1.f - decay);
-      mov_var[c] -= (mov_var[c] - uvar) * (1.f - decay);
-    }
+    bn_fin_channel(sv[i], qv[i], c, K, gamma, beta, mov_mean, mov_var, out, count, eps, decay, update, bessel);
     }
   }
   if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -120,6 +120,26 @@ namespace dtm {
 // BatchNorm finalize backward of one channel (bn_finalize_bwd_kernel's algebra): from dss = [dscale;
 // dshift; dmean; drstd], ss = [scale; shift; mean; rstd] and gamma -> the statistics gradient
 // (ds = d/dsum, dq = d/dsumsq, divided by the count) and the parameter gradients dg, db.
+// training BatchNorm finalize of one channel from the batch sums: ss = [scale; shift; mean; rstd] (out[c],
+// out[K+c], ...) and the moving averages (shared by stats_reduce_finalize and the conv epilogue's hand-off)
+__device__ __forceinline__ void bn_fin_channel(float sum, float sq, int c, int K, const float* gamma, const float* beta,
+                                               float* mov_mean, float* mov_var, float* out, float count, float eps,
+                                               float decay, int update, int bessel) {
+  const float mean = sum / count;
+  const float var = fmaxf(sq / count - mean * mean, 0.f);
+  const float rstd = rsqrtf(var + eps);
+  const float sc = (gamma ? gamma[c] : 1.f) * rstd;
+  out[c] = sc;
+  out[K + c] = (beta ? beta[c] : 0.f) - mean * sc;
+  out[2 * K + c] = mean;
+  out[3 * K + c] = rstd;
+  if (update) {
+    const float uvar = (bessel && count > 1.f) ? var * count / (count - 1.f) : var;
+    mov_mean[c] -= (mov_mean[c] - mean) * (1.f - decay);
+    mov_var[c] -= (mov_var[c] - uvar) * (1.f - decay);
+  }
+}
+
 __device__ __forceinline__ void fin_bwd_channel(const float* dss, const float* ss, const float* gamma, int C, int c,
                                                 float count, float* ds, float* dq, float* dg, float* db) {
   const float scale = ss[c], mean = ss[2 * C + c], rstd = ss[3 * C + c];

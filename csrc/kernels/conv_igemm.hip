@@ -70,6 +70,19 @@ struct ConvNTArgs {
   // input (add_src, act_x, act_r, act_mask) index.  ostr == 1: identity (OH = P, OW = Q, oa = ob = 0)
   int ostr, oa, ob, OH, OW;
   int pre_side;  // conv_nt_kernel: load the dgrad epilogue's side inputs before the last k-tile (A/B knob)
+  // BatchNorm finalize hand-off in the statistics epilogue (fin_acc != nullptr): each block adds its tile's
+  // column sums into replica (by % fin_G) of a self-cleaning [fin_G][2K] accumulator with memory-side
+  // atomics; the last block (fin_counter) folds the replicas (atomic exchanges re-zero them) and writes
+  // ss = [scale; shift; mean; rstd] + the moving averages: no separate reduce/finalize launch
+  float* fin_acc;
+  unsigned* fin_counter;
+  int fin_G, fin_update, fin_bessel;
+  const float* fin_gamma;
+  const float* fin_beta;
+  float* fin_mm;
+  float* fin_mv;
+  float* fin_ss;
+  float fin_count, fin_eps, fin_decay;
 };
 
 // full-resolution coordinates / row of output pixel m (see ConvNTArgs::ostr)
@@ -382,14 +395,44 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
       // every thread finishes one (chunk column, value) output: NT/CPR partials each, instead of CPR
       // threads walking all NT rows of the table serially
       const int rw = (act && a.act_r) ? 4 : 2;  // row width in K units
-      float* prow = (act ? a.act_sums : a.stats) + (size_t)by * (rw * a.K);
+      const bool fin = !act && a.fin_acc != nullptr;
+      float* prow = fin ? a.fin_acc + (size_t)(by % a.fin_G) * (2 * a.K)
+                        : (act ? a.act_sums : a.stats) + (size_t)by * (rw * a.K);
       for (int o = tid; o < CPR * 16; o += NT) {
         const int c = o >> 4, e = o & 15;
         float t = 0.f;
 #pragma unroll 4
         for (int k = 0; k < NT / CPR; ++k) t += red[((c + k * CPR) << 4) + e];
         const int kk = c0 + c * 8 + (e & 7);
-        if (kk < a.K) prow[(e < 8 ? 0 : a.K) + kk] = t;
+        if (kk < a.K) {
+          if (fin) atomicAdd(prow + (e < 8 ? 0 : a.K) + kk, t);
+          else prow[(e < 8 ? 0 : a.K) + kk] = t;
+        }
+      }
+      if (fin) {
+        // hand-off: every wave's atomics are performed (its own vmcnt drained) before the block's count;
+        // the totals are read back with memory-side atomics (never a stale L2 line of another XCD)
+        __builtin_amdgcn_s_waitcnt(0);
+        epi_barrier<RAWB>();
+        // (the flag lives in the kernel's one LDS array: a second __shared__ object would make hipcc add
+        //  vmcnt drains to the LDS-DMA main loops)
+        int* fin_last = (int*)smem;
+        if (tid == 0)
+          *fin_last = __hip_atomic_fetch_add(a.fin_counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                      gridDim.x * gridDim.y - 1;
+        epi_barrier<RAWB>();
+        if (*fin_last) {
+          for (int c = tid; c < a.K; c += NT) {
+            float sum = 0.f, sq = 0.f;
+            for (int g = 0; g < a.fin_G; ++g) {
+              sum += atomicExch(a.fin_acc + (size_t)g * 2 * a.K + c, 0.f);
+              sq += atomicExch(a.fin_acc + (size_t)g * 2 * a.K + a.K + c, 0.f);
+            }
+            bn_fin_channel(sum, sq, c, a.K, a.fin_gamma, a.fin_beta, a.fin_mm, a.fin_mv, a.fin_ss, a.fin_count,
+                           a.fin_eps, a.fin_decay, a.fin_update, a.fin_bessel);
+          }
+          if (tid == 0) __hip_atomic_store(a.fin_counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
       if (act && a.act_r) {  // second round: [sum g*r | sum g] of the BN'd residual
         epi_barrier<RAWB>();
@@ -2021,9 +2064,29 @@ static void dispatch_nt(const ConvNTArgs& a, int ud, const TileCfg& t, hipStream
   else dispatch_ud<2>(a, t, st);
 }
 
+DTM_API int dtm_get_deterministic();
+
+// BatchNorm finalize parameters for the statistics epilogue's hand-off (ConvNTArgs::fin_acc)
+struct FinArgs {
+  float* acc;
+  unsigned* counter;
+  int G, update, bessel;
+  const float* gamma;
+  const float* beta;
+  float* mm;
+  float* mv;
+  float* ss;
+  float count, eps, decay;
+};
+static int g_fin_fuse = 0;  // A/B knob: BN finalize in the conv statistics epilogue (dtm_conv_set_fin_fuse)
+DTM_API void dtm_conv_set_fin_fuse(int on) { g_fin_fuse = on; }
+static float* g_cfin_acc = nullptr;
+static unsigned* g_cfin_counter = nullptr;
+static size_t g_cfin_floats = 0;
+
 static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, const float* bias, const float* in_scale,
                          const float* in_shift, int relu, const ConvDesc* d, hipStream_t stream, float** rows_ws,
-                         int* nrows) {
+                         int* nrows, const FinArgs* fin = nullptr, bool* fused = nullptr) {
   if (d->C % 8 || d->K % 4) return -1;
   ConvNTArgs a;
   a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.y = (bf16_t*)y;
@@ -2045,8 +2108,18 @@ static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, cons
   a.fd_PQ = make_fastdiv(d->P * d->Q); a.fd_Q = make_fastdiv(d->Q);
   a.ostr = 1; a.oa = a.ob = 0; a.OH = a.P; a.OW = a.Q;
   a.pre_side = 0;
+  a.fin_acc = nullptr; a.fin_counter = nullptr;
+  if (fin && stats) {
+    a.fin_acc = fin->acc; a.fin_counter = fin->counter; a.fin_G = fin->G;
+    a.fin_gamma = fin->gamma; a.fin_beta = fin->beta; a.fin_mm = fin->mm; a.fin_mv = fin->mv; a.fin_ss = fin->ss;
+    a.fin_count = fin->count; a.fin_eps = fin->eps; a.fin_decay = fin->decay;
+    a.fin_update = fin->update; a.fin_bessel = fin->bessel;
+  }
   int rows = 0;
   const TileCfg tc = pick_tile(a, stats);
+  // the hand-off needs the staged epilogue's per-tile statistics (not the streaming kernel's per-worker rows)
+  if (a.fin_acc && (tc.id == 30 || tc.id == 31 || (a.K & 7) != 0)) a.fin_acc = nullptr;
+  if (fused) *fused = a.fin_acc != nullptr;
   if (stats) {
     // one per streaming worker; one per pixel tile (staged epilogue, K % 8 == 0); else per (pixel tile, pixel wave)
     rows = (tc.id == 30 || tc.id == 31) ? stream_rows(a, tc.id)
@@ -2081,8 +2154,29 @@ DTM_API int dtm_conv_fwd_bn(const void* x, const void* w, void* y, const float* 
                             void* stream) {
   float* ws = nullptr;
   int rows = 0;
-  int rc = conv_fwd_impl(x, w, y, true, nullptr, in_scale, in_shift, 0, d, (hipStream_t)stream, &ws, &rows);
+  FinArgs fa{};
+  const FinArgs* fp = nullptr;
+  if (g_fin_fuse && !dtm_get_deterministic()) {
+    // replicas spread the per-tile atomics (fewer blocks per address), at most 8 K floats in all
+    const int G = d->K >= 4096 ? 1 : (8192 / (2 * d->K) < 16 ? 8192 / (2 * d->K) : 16);
+    const size_t need = (size_t)G * 2 * d->K;
+    if (need > g_cfin_floats) {
+      hipDeviceSynchronize();
+      if (g_cfin_acc) hipFree(g_cfin_acc);
+      if (!g_cfin_counter && hipMalloc(&g_cfin_counter, 64) != hipSuccess) return -4;
+      if (hipMalloc(&g_cfin_acc, need * sizeof(float)) != hipSuccess) { g_cfin_acc = nullptr; g_cfin_floats = 0; return -4; }
+      hipMemset(g_cfin_acc, 0, need * sizeof(float));
+      hipMemset(g_cfin_counter, 0, 64);
+      hipDeviceSynchronize();
+      g_cfin_floats = need;
+    }
+    fa = FinArgs{g_cfin_acc, g_cfin_counter, G, update, bessel, gamma, beta, mov_mean, mov_var, ss, count, eps, decay};
+    fp = &fa;
+  }
+  bool fused = false;
+  int rc = conv_fwd_impl(x, w, y, true, nullptr, in_scale, in_shift, 0, d, (hipStream_t)stream, &ws, &rows, fp, &fused);
   if (rc) return rc;
+  if (fused) return 0;
   return dtm_bn_stats_finalize(ws, rows, d->K, gamma, beta, mov_mean, mov_var, ss, count, eps, decay, update, bessel,
                                (hipStream_t)stream);
 }
@@ -2143,6 +2237,7 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvD
   a.Hv = d->P; a.Wv = d->Q;
   a.OH = d->H; a.OW = d->W;
   a.pre_side = g_pre_side;
+  a.fin_acc = nullptr; a.fin_counter = nullptr;
   const int rw = act_r ? 4 : 2;
   // launches: one plain dgrad over the zero-dilated dy (UD = stride), or (d->dec, stride > 1) one stride-1
   // conv per output parity class (a, b) with that class's taps of the decomposed weight (dec_dim)
