@@ -589,9 +589,10 @@ class _StemConvBNFn(torch.autograd.Function):
         return None, dw, dgamma, dbeta, None, None, None
 
 
-def _stem_eligible(x, w, stride, padding):
+def _stem_eligible(x, w, stride, g):
     """The packed-row stem path: a plain (non-lazy) input without gradient, <= 4 channels, stride 2,
-    S <= 7 taps per kernel row (S x 4 channels fit one 64-byte run), symmetric explicit padding."""
+    S <= 7 taps per kernel row (S x 4 channels fit one 64-byte run), equal top / left pads (explicit,
+    'VALID', or TF 'SAME'; the bottom / right zero fill comes from the packed buffer's extent)."""
     import os
     if os.environ.get("DTM_STEM", "1") == "0" or isinstance(x, (LazyBN, Subsampled)):
         return False
@@ -599,10 +600,8 @@ def _stem_eligible(x, w, stride, padding):
         return False
     K, R, S, C = w.shape
     st = stride if isinstance(stride, int) else stride[0]
-    if isinstance(padding, str) or not isinstance(padding, (tuple, list)) or padding[0] != padding[1] or \
-            isinstance(padding[0], (tuple, list)):
-        return False
-    return C <= 4 and x.shape[-1] == C and st == 2 and S <= 7 and K % 4 == 0
+    return (C <= 4 and x.shape[-1] == C and st == 2 and S <= 7 and K % 4 == 0 and g.pad_h == g.pad_w and
+            g.pad_h >= 0 and g.dilation == 1)
 
 
 def bn_apply(raw, ss, relu, residual=None, unscaled=False):
@@ -694,11 +693,11 @@ def conv_bn(x, w, bn, stride, padding, training, relu):
             if mode == "mat":
                 x_mat = bn_apply_nograd(x, in_ss)
     g = conv_geom(tuple(x.shape), tuple(w.shape), stride, padding)
-    if in_ss is None and _stem_eligible(x, w, stride, padding):
+    if in_ss is None and _stem_eligible(x, w, stride, g):
         if training:
-            y, ss = _StemConvBNFn.apply(x, w, bn.gamma, bn.beta, g, bn, int(padding[0]))
+            y, ss = _StemConvBNFn.apply(x, w, bn.gamma, bn.beta, g, bn, int(g.pad_h))
         else:
-            y = _StemConvBNFn.apply(x, w, None, None, g, None, int(padding[0]))
+            y = _StemConvBNFn.apply(x, w, None, None, g, None, int(g.pad_h))
             ss = bn_inference_ss(bn)
         return LazyBN(y, ss, relu, unscaled=training)
     if g.C % 8 != 0:

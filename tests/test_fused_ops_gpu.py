@@ -192,29 +192,34 @@ def test_bn_relu_maxpool_fused(H, pool, pad, st):
 
 
 @pytest.mark.parametrize("stemw", ["0", "1"])
-@pytest.mark.parametrize("H,W,C,N", [(32, 32, 3, 4), (36, 30, 3, 2), (224, 224, 3, 2), (17, 23, 1, 3)])
-def test_stem_packed_row_conv_bn(monkeypatch, H, W, C, N, stemw):
-    """The packed-row stem path (7x7/2, explicit pad 3, C <= 4: an R x 1 conv over 32 'channels' with an
-    8-byte pixel pitch) against torch fp32: output, BN moving statistics, weight/gamma/beta grads; the
-    BN backward either as a stats-combine pass or inside the wgrad operand staging (stemw=1)."""
+@pytest.mark.parametrize("H,W,C,N,R,pad", [(32, 32, 3, 4, 7, (3, 3)), (36, 30, 3, 2, 7, (3, 3)), (224, 224, 3, 2, 7, (3, 3)),
+                                            (17, 23, 1, 3, 7, (3, 3)),
+                                            (41, 41, 3, 2, 3, "VALID"),   # Inception-v3 conv0 3x3/2 VALID
+                                            (31, 31, 3, 2, 3, "SAME")])
+def test_stem_packed_row_conv_bn(monkeypatch, H, W, C, N, R, pad, stemw):
+    """The packed-row stem path (7x7/2 pad 3, or Inception's 3x3/2 VALID; C <= 4: an R x 1 conv over 32
+    'channels' with an 8-byte pixel pitch) against torch fp32: output, BN moving statistics,
+    weight/gamma/beta grads; the BN backward either as a stats-combine pass or inside the wgrad operand
+    staging (stemw=1)."""
+    from distributed_tensorflow_models_amd.ops.geometry import conv_geom
     monkeypatch.setenv("DTM_STEM_WGRAD_FUSE", stemw)
     torch.manual_seed(0)
     x = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16)
-    w = (torch.randn(64, 7, 7, C, device=DEV) / (49 * C) ** 0.5).to(torch.bfloat16).float()
+    w = (torch.randn(64, R, R, C, device=DEV) / (R * R * C) ** 0.5).to(torch.bfloat16).float()
     bn = _bn(64)
     bn_r = _bn(64)
     with torch.no_grad():
         bn_r.gamma.copy_(bn.gamma)
         bn_r.beta.copy_(bn.beta)
-    assert fused._stem_eligible(x, w, 2, (3, 3))
+    assert fused._stem_eligible(x, w, 2, conv_geom(tuple(x.shape), tuple(w.shape), 2, pad))
     wr = w.clone().requires_grad_()
     gr, br = bn.gamma.detach().clone().requires_grad_(), bn.beta.detach().clone().requires_grad_()
-    yr = ref.batch_norm(ref.conv2d(x.float(), wr, None, 2, (3, 3)), gr, br, bn_r.moving_mean, bn_r.moving_variance,
+    yr = ref.batch_norm(ref.conv2d(x.float(), wr, None, 2, pad), gr, br, bn_r.moving_mean, bn_r.moving_variance,
                         True, 0.9, 1e-3, True)
     gy = torch.randn_like(yr).to(torch.bfloat16).float()
     yr.backward(gy)
     wk = w.clone().requires_grad_()
-    lz = fused.conv_bn(x, wk, bn, 2, (3, 3), True, True)
+    lz = fused.conv_bn(x, wk, bn, 2, pad, True, True)
     yk = lz.materialize()
     assert yk.shape == yr.shape
     yk.backward(gy.to(torch.bfloat16))
