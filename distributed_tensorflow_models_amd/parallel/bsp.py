@@ -9,7 +9,9 @@ Design (MI355X-first):
     order; every parameter gets ``param.main_grad`` = its view.  Conv wgrad kernels add into it
     directly with fp32 atomics, so there is no per-parameter grad copy or bucket pack kernel;
   * the buffer is cut into ~``bucket_mb`` contiguous buckets (a tensor larger than a bucket - e.g.
-    VGG-16's 411 MB fc6 gradient - is split across several buckets so its all-reduce pipelines);
+    VGG-16's 411 MB fc6 gradient - is split across several buckets so its all-reduce pipelines); the
+    last bucket of backward (the first layers, whose gradients come last and whose collective nothing
+    can hide) is cut at ``tail_mb`` (ResNet-50: stem + stage 1 ~ 1 MB instead of a 6 MB remainder);
   * when the last gradient of a bucket is produced (``grad_ready`` fired by the ops, or autograd
     post-accumulate hooks for plain torch ops), the bucket's all_reduce(SUM) is issued
     asynchronously; RCCL's internal stream waits on the compute stream at issue time, so the
@@ -36,7 +38,7 @@ from ..utils.profiler import roctx
 
 class BSPDataParallel:
     def __init__(self, params, bucket_mb=32.0, process_group=None, device=None, overlap=True, grad_dtype=torch.float32,
-                 comm_dtype=None):
+                 comm_dtype=None, tail_mb=1.0):
         self.params = [p for p in params if p.requires_grad]
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
@@ -56,6 +58,8 @@ class BSPDataParallel:
             p.main_grad = self.flat[off:off + p.numel()].view(p.shape)
             off += p.numel()
         self.cap = max(1, int(bucket_mb * (1 << 20) / self.flat.element_size()))
+        # the LAST bucket of backward is the exposed one (nothing is left to overlap it): keep it small
+        self.tail = max(0, int(tail_mb * (1 << 20) / self.flat.element_size()))
         # param -> live-tap window (r0, r1, s0, s1): compact bucket (windows announced to an earlier
         # instance are remembered on the parameter).  DTM_BSP_COMPACT=0 turns compaction off (A/B).
         import os
@@ -91,10 +95,15 @@ class BSPDataParallel:
         if cur is not None:
             segs.append(cur)
         self.buckets = []  # (start, end) of the flat buffer, or (param, window) for a compact bucket
-        for s, e in segs:
-            while s < e:
-                self.buckets.append((s, min(e, s + self.cap)))
+        for i, (s, e) in enumerate(segs):
+            # the final segment ends with a tail bucket of at most `tail` elements (the first layers'
+            # gradients, produced last), so the collective left exposed after backward is short
+            cut = e - self.tail if (i == len(segs) - 1 and 0 < self.tail < e - s) else e
+            while s < cut:
+                self.buckets.append((s, min(cut, s + self.cap)))
                 s += self.cap
+            if cut < e:
+                self.buckets.append((cut, e))
         self.compact = {}  # bucket index -> (param, window, fp32 buffer, comm-dtype buffer or None)
         for p in self.order:
             if p in self.windows:

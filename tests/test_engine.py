@@ -194,3 +194,21 @@ def test_bench_refuses_world_size_mismatch():
     out = _run_bench(["--model", "lenet", "--device", "cpu", "--gpus", "4", "--steps", "1", "--warmup", "0"],
                      env_extra={"WORLD_SIZE": "2"})
     assert out.returncode == 2 and "WORLD_SIZE" in out.stderr
+
+
+def test_bsp_bucket_layout_small_tail():
+    """Buckets cover the flat gradient buffer exactly, at most bucket_mb each, and the last one of
+    backward (the first layers' gradients) is cut at tail_mb so the exposed collective is short."""
+    from distributed_tensorflow_models_amd.parallel.bsp import BSPDataParallel
+    params = [torch.nn.Parameter(torch.zeros(n)) for n in (1000, 300_000, 50_000, 700_000, 20_000, 5_000)]
+    dp = BSPDataParallel(params, bucket_mb=1.0, tail_mb=0.1)
+    try:
+        spans = [b for b in dp.buckets if isinstance(b[0], int)]
+        assert spans[0][0] == 0 and spans[-1][1] == dp.flat.numel()
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+        assert all(e - s <= (1 << 20) // 4 for s, e in spans)
+        assert spans[-1][1] - spans[-1][0] <= int(0.1 * (1 << 20)) // 4
+        # every parameter's elements are accounted for exactly once
+        assert sum(n for p in dp.params for _, n in dp.contrib[p]) == dp.flat.numel()
+    finally:
+        dp.close()
