@@ -1952,6 +1952,9 @@ struct TileCfg {
   int id, PT, NWP;
 };
 static int g_tile_env = -2;
+static int device_cus();
+static int g_policy2 = 1;  // A/B knob: the v2 shape-policy rules (dtm_conv_set_policy2)
+DTM_API void dtm_conv_set_policy2(int on) { g_policy2 = on; }
 static int g_tile_w8 = 1;  // A/B knob: the 8-wave tile in the shape policy (dtm_conv_set_w8)
 static int g_stream_act = 1;  // A/B knob: the persistent streaming kernel also for act / block-output dgrads
 DTM_API void dtm_conv_set_stream_act(int on) { g_stream_act = on; }
@@ -1984,15 +1987,31 @@ static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
   // CUs), and not on the many-tile short-reduction layers without statistics (their 4-wave tiles stream
   // better).  Measured per ResNet-50 layer (tools/conv_tile_sweep.py STATS=1, profiles/r2_conv_tiles_w8.txt):
   // 14x14 3x3 fwd/dgrad -16 %, 7x7 1024->2048 -12 %, 28x28 256->512 fwd+stats -17 %; loses at <= 98 tiles.
-  if (id == -1 && !a.in_scale && a.K >= 256 && g_tile_w8) {
+  // (policy v2: the w8 tile only for whole 256-channel tiles - Inception's 384 = 256 + a half-empty tile ran
+  //  147 us vs 91 on 128x128)
+  if (id == -1 && !a.in_scale && a.K >= 256 && g_tile_w8 && (!g_policy2 || a.K % 256 == 0)) {
     const long tiles = (long)((a.M + 255) / 256) * ((a.K + 255) / 256);
     if (tiles >= 150 && !(tiles > 600 && a.Kg <= 256 && !stats)) id = 40;
   }
+  // policy v2 (A/B knob dtm_conv_set_policy2), from the Inception-v3 shape sweep
+  // (profiles/r2/r2_sweep_inception.log, batch 128):
+  //  * <= 64 output channels with a spatial kernel: the 2-slot pipelined 128x64 tile whatever the reduction
+  //    depth (5x5 48->64: 38.5 us vs 63.6 on the 128x128 tile the Kg >= 1024 rule picked; 3x3 -> 32: -10 %)
+  //  * 64 < K <= 128 with a spatial kernel: the pipelined 128x128 tile (35x35 3x3 ->96: -11 %)
+  if (id == -1 && g_policy2 && !a.in_scale && a.K % 8 == 0 && a.R * a.S > 1) {
+    if (a.K <= 64) id = 26;
+    else if (a.K <= 128) id = 21;
+  }
   // output widths that leave the last 128-channel tile at most half full (Inception's 192 / 320 / 96 /
-  // 160 ...): 64-channel tiles (A/B knob dtm_conv_set_kwide)
+  // 160 ...): 64-channel tiles (A/B knob dtm_conv_set_kwide); v2: 256-pixel tiles on mid-size maps
+  // (17x17 at batch 128: 1x7 / 7x1 / 1x1 -> 160 / 192 -19 %), not on small ones (8x8: +33 %)
   if (id == -1 && g_kwide && a.K > 64 && a.K % 128 != 0 && (a.K % 128) <= 64 && a.K % 8 == 0)
-    id = a.in_scale ? 3 : 26;
-  if (id == -1 && !a.in_scale && a.Kg >= 1024) id = 21;  // (-3: the policy without it, for A/B runs)
+    id = a.in_scale ? 3 : ((g_policy2 && a.M >= 16384 && a.M <= 65536) ? 24 : 26);
+  if (id == -1 && !a.in_scale && a.Kg >= 1024) {
+    id = 21;  // (-3: the policy without it, for A/B runs)
+    // v2: fewer 128x128 tiles than CUs (8x8 maps at batch 128): 128x64 tiles fill the chip (-13 %)
+    if (g_policy2 && (long)((a.M + 127) / 128) * ((a.K + 127) / 128) < device_cus()) id = 26;
+  }
   // 64-output-channel 3x3 layers (56x56 bottleneck conv2, fwd and dgrad): the 2-slot pipelined 128x64 tile
   // (profiles/r2_conv_tiles_k64.txt: -4 % vs the register-staged single-buffer tile)
   if (id == -1 && !a.in_scale && a.K <= 64 && a.R * a.S > 1 && a.K % 64 == 0) id = 26;

@@ -51,6 +51,7 @@ _SIGS = {
     "dtm_side_join": (None, [_P]),
     "dtm_set_side_reduce": (None, [_I]),
     "dtm_conv_set_fin_fuse": (None, [_I]),
+    "dtm_conv_set_policy2": (None, [_I]),
     "dtm_weight_flip_transpose": (None, [_P, _P, _I, _I, _I, _I, _P]),
     "dtm_weight_flip_transpose_batched": (None, [_P, _I, _P]),
     "dtm_weight_flip_transpose_dec": (None, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),

@@ -31,23 +31,42 @@ def timed(fn, n=10):
     return s.elapsed_time(e) / n * 1e3  # us
 
 
+# Inception-v3 (old slim) training shapes at batch 128 (reference inception/slim/inception_model.py:54-332):
+# (H, C, K, R, S, stride, padding, count per step)
+INCEPTION = [
+    (149, 32, 32, 3, 3, 1, "VALID", 1), (147, 32, 64, 3, 3, 1, "SAME", 1), (73, 64, 80, 1, 1, 1, "VALID", 1),
+    (73, 80, 192, 3, 3, 1, "VALID", 1),
+    (35, 288, 64, 1, 1, 1, "SAME", 9), (35, 288, 48, 1, 1, 1, "SAME", 3), (35, 48, 64, 5, 5, 1, "SAME", 3),
+    (35, 64, 96, 3, 3, 1, "SAME", 4), (35, 96, 96, 3, 3, 1, "SAME", 3),
+    (35, 288, 384, 3, 3, 2, "VALID", 1), (35, 96, 96, 3, 3, 2, "VALID", 1),
+    (17, 768, 192, 1, 1, 1, "SAME", 10), (17, 768, 160, 1, 1, 1, "SAME", 8),
+    (17, 160, 160, 1, 7, 1, "SAME", 8), (17, 160, 160, 7, 1, 1, "SAME", 8), (17, 160, 192, 1, 7, 1, "SAME", 4),
+    (17, 160, 192, 7, 1, 1, "SAME", 4), (17, 192, 320, 3, 3, 2, "VALID", 1), (17, 192, 192, 3, 3, 2, "VALID", 1),
+    (8, 2048, 320, 1, 1, 1, "SAME", 2), (8, 2048, 384, 1, 1, 1, "SAME", 2), (8, 2048, 448, 1, 1, 1, "SAME", 2),
+    (8, 2048, 192, 1, 1, 1, "SAME", 2), (8, 384, 384, 1, 3, 1, "SAME", 4), (8, 384, 384, 3, 1, 1, "SAME", 4),
+    (8, 448, 384, 3, 3, 1, "SAME", 2),
+]
+
+
 def main():
     L = _lib.lib()
     st = _lib.stream_ptr()
     print("%-24s %-6s " % ("shape", "pass") + " ".join("%8s" % ("t%d" % t) for t in TILES) + "   best", flush=True)
     tot = {t: 0.0 for t in TILES}
     wtot = {}
-    for (H, C, K, R, stride, pad, cnt) in SHAPES[1:]:
+    shapes = ([(H, C, K, R, R, s_, (p_, p_), n) for (H, C, K, R, s_, p_, n) in SHAPES[1:]]
+              if os.environ.get("SET", "resnet") == "resnet" else INCEPTION)
+    for (H, C, K, R, S, stride, pad, cnt) in shapes:
         if ONLY and ONLY not in "%d_%d_%d_%d" % (H, C, K, R):
             continue
         x = torch.randn(B, H, H, C, device="cuda").to(torch.bfloat16)
-        w = (torch.randn(K, R, R, C, device="cuda") * 0.05).to(torch.bfloat16)
-        g = conv_geom(tuple(x.shape), tuple(w.shape), stride, (pad, pad))
+        w = (torch.randn(K, R, S, C, device="cuda") * 0.05).to(torch.bfloat16)
+        g = conv_geom(tuple(x.shape), tuple(w.shape), stride, pad)
         d = g.as_desc(_lib.ConvDesc)
         y = torch.empty(B, g.P, g.Q, K, device="cuda", dtype=torch.bfloat16)
         dy = torch.randn_like(y)
-        wt = torch.empty(C, R, R, K, device="cuda", dtype=torch.bfloat16)
-        L.dtm_weight_flip_transpose(_lib.ptr(w), _lib.ptr(wt), K, R, R, C, st)
+        wt = torch.empty(C, R, S, K, device="cuda", dtype=torch.bfloat16)
+        L.dtm_weight_flip_transpose(_lib.ptr(w), _lib.ptr(wt), K, R, S, C, st)
         dx = torch.empty_like(x)
         sc = torch.rand(C, device="cuda") + 0.5
         sh = torch.randn(C, device="cuda") * 0.1
@@ -65,7 +84,7 @@ def main():
             passes["fwd+s"] = lambda: L.dtm_conv_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(y), _lib.ptr(stats), None,
                                                      None, None, 0, ctypes.byref(d), st)
         if os.environ.get("WGRAD"):
-            dw = torch.zeros(K, R, R, C, device="cuda")
+            dw = torch.zeros(K, R, S, C, device="cuda")
             ss4 = torch.stack([sc, sh, sh, sc]).contiguous()
             mask = torch.empty(x.numel() // 8, device="cuda", dtype=torch.uint8)
             xa = torch.empty_like(x)
@@ -82,7 +101,7 @@ def main():
                 print("H%-3d C%-4d K%-4d R%d s%d x%d %-7s %8.1f" % (H, C, K, R, stride, cnt, pname, v), flush=True)
         if os.environ.get("WTILES"):
             wts = [tuple(int(u) for u in t.split(":")) for t in os.environ["WTILES"].split(",")]
-            dw = torch.zeros(K, R, R, C, device="cuda")
+            dw = torch.zeros(K, R, S, C, device="cuda")
             fn = lambda: L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(dw), None, None, ctypes.byref(d),  # noqa
                                           _lib.num_cus(), st)
             res = {t: [] for t in wts}
@@ -109,7 +128,7 @@ def main():
             for t in TILES:
                 tot[t] += med[t] * cnt
             best = min(med, key=med.get)
-            print("H%-3d C%-4d K%-4d R%d s%d x%d %-6s " % (H, C, K, R, stride, cnt, pname) +
+            print("H%-3d C%-4d K%-4d R%dx%d s%d x%d %-6s " % (H, C, K, R, S, stride, cnt, pname) +
                   " ".join("%8.1f" % med[t] for t in TILES) + "   t%d" % best, flush=True)
     print("weighted total (us): " + " ".join("t%d=%.0f" % (t, v) for t, v in tot.items()), flush=True)
     if wtot:
