@@ -1979,7 +1979,9 @@ static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
   // the pipelined LDS-DMA 128x128 tile (2 slots, 2 blocks/CU) wins every deep-reduction layer without the
   // prologue (tools/conv_tile_sweep.py: 3x3 at 14x14 / 7x7 -13..-18 %, deep 1x1 -5..-16 %)
   if (id == -4) id = -1;  // (-4: the policy without the streaming kernel, for A/B runs)
-  else if (id == -1 && a.Kg == 64 && stream_ok(a) && (g_stream_act || !a.act_x)) id = a.K >= 128 ? 30 : 31;
+  else if (id == -1 && a.Kg == 64 && stream_ok(a) && (g_stream_act || !a.act_x) &&
+           (!g_policy2 || a.K % 128 == 0 || a.K <= 64))  // (v2: no partial channel tiles: 35x35 ->288 -33 %)
+    id = a.K >= 128 ? 30 : 31;
   if (id == -1 && a.act_x && g_act_tile >= 0) id = g_act_tile;  // (A/B: the non-streaming act dgrads)
   // (the persistent streaming 1x1 kernel: the 64-deep 56x56 expand / reduce layers and their dgrads are
   // HBM streams: -20..-33 % (tools/conv_tile_sweep.py); at Kg 128 its 1 block/CU loses)
