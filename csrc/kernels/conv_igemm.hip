@@ -2011,8 +2011,9 @@ static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
     id = a.in_scale ? 3 : ((g_policy2 && a.M >= 16384 && a.M <= 65536) ? 24 : 26);
   if (id == -1 && !a.in_scale && a.Kg >= 1024) {
     id = 21;  // (-3: the policy without it, for A/B runs)
-    // v2: fewer 128x128 tiles than CUs (8x8 maps at batch 128): 128x64 tiles fill the chip (-13 %)
-    if (g_policy2 && (long)((a.M + 127) / 128) * ((a.K + 127) / 128) < device_cus()) id = 26;
+    // v2: no more 128x128 tiles than CUs (8x8 maps at batch 128, VGG's 4x4 at 512): 128x64 tiles fill the
+    // chip (-13 %; profiles/r2/r2_sweep_vgg.log)
+    if (g_policy2 && (long)((a.M + 127) / 128) * ((a.K + 127) / 128) <= device_cus()) id = 26;
   }
   // 64-output-channel 3x3 layers (56x56 bottleneck conv2, fwd and dgrad): the 2-slot pipelined 128x64 tile
   // (profiles/r2_conv_tiles_k64.txt: -4 % vs the register-staged single-buffer tile)

@@ -64,7 +64,8 @@ def main():
     model = os.environ.get("MODEL", "resnet_v1_50")
     from bench import PRESETS
     S, ncls, B0, opt, extra = PRESETS[model]
-    net = nets_factory.build(model, num_classes=ncls).to(dev)
+    kw = {"fc_conv_padding": "SAME"} if model == "vgg_16" else {}  # (bench.py's CIFAR geometry)
+    net = nets_factory.build(model, num_classes=ncls, **kw).to(dev)
     B = B or B0
     step = TrainStep(net, optimizer=opt, lr=0.01, momentum=0.9, **extra)
     x = torch.randn(B, S, S, 1 if model == "lenet" else 3, device=dev).to(torch.bfloat16)

@@ -48,14 +48,25 @@ INCEPTION = [
 ]
 
 
+# VGG-16 in the reference's CIFAR geometry (reference vgg/cifar10_vgg_bsp.py:64, vgg/nets/vgg.py:144-222) at batch
+# 512; fc6 runs as its live centre tap (1x1), fc7 as a 1x1 conv over a 1x1 map
+VGG = [
+    (32, 64, 64, 3, 3, 1, "SAME", 1), (16, 64, 128, 3, 3, 1, "SAME", 1), (16, 128, 128, 3, 3, 1, "SAME", 1),
+    (8, 128, 256, 3, 3, 1, "SAME", 1), (8, 256, 256, 3, 3, 1, "SAME", 2), (4, 256, 512, 3, 3, 1, "SAME", 1),
+    (4, 512, 512, 3, 3, 1, "SAME", 2), (2, 512, 512, 3, 3, 1, "SAME", 3), (1, 512, 4096, 1, 1, 1, "SAME", 1),
+    (1, 4096, 4096, 1, 1, 1, "SAME", 1),
+]
+
+
 def main():
     L = _lib.lib()
     st = _lib.stream_ptr()
     print("%-24s %-6s " % ("shape", "pass") + " ".join("%8s" % ("t%d" % t) for t in TILES) + "   best", flush=True)
     tot = {t: 0.0 for t in TILES}
     wtot = {}
+    which = os.environ.get("SET", "resnet")
     shapes = ([(H, C, K, R, R, s_, (p_, p_), n) for (H, C, K, R, s_, p_, n) in SHAPES[1:]]
-              if os.environ.get("SET", "resnet") == "resnet" else INCEPTION)
+              if which == "resnet" else (INCEPTION if which == "inception" else VGG))
     for (H, C, K, R, S, stride, pad, cnt) in shapes:
         if ONLY and ONLY not in "%d_%d_%d_%d" % (H, C, K, R):
             continue
