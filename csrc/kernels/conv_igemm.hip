@@ -1971,6 +1971,8 @@ static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
   if (g_tile_env == -2) {
     const char* e = getenv("DTM_CONV_TILE");
     g_tile_env = e ? atoi(e) : -1;
+    const char* p2 = getenv("DTM_CONV_POLICY2");  // (0: the round-1 shape policy, for A/B runs)
+    if (p2) g_policy2 = atoi(p2);
   }
   // measured per ResNet-50 shape (tools/conv_microbench.py, DTM_CONV_TILE sweep): the single-buffer
   // variants win almost everywhere (more resident blocks hide the short-K latency); the 2-buffer
