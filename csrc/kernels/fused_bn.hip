@@ -10,6 +10,8 @@
 //   stats_combine: dx_total = dx + dsum + 2*x*dsumsq   (the gradient through the statistics)
 // Together these equal the textbook BN backward dx = scale*(g - mean(g) - xhat*mean(g*xhat)).
 // Lane mapping: one fixed 8-channel column per lane (parameters in registers), 16-B accesses.
+#include <cstring>
+
 #include "common.h"
 
 namespace dtm {
@@ -261,6 +263,123 @@ static int g_sc_var = 5, g_sc_cap = 4096;
 // non-temporal input loads: bit 0 bn_apply_fast (forward), bit 1 bn_apply_bwd
 static int g_ntld = 3;  // A/B (ResNet-50 b256): both on -1.5 % step time on top of the stats-combine policy
 
+// ---- zero-copy concat, all parts in one launch (Inception mixed blocks: 3-4 BN'd branches per block) --------
+// Part k owns channels [off, off + C) of the [M][Ct] concat; its BN-apply input raw / ss / mask are its own
+// [M][C] tensors.  Each lane keeps one fixed 8-channel column of the CONCAT row (so it belongs to one part),
+// so the whole block output is written / its gradient read in full coalesced rows, and the per-part
+// launches (and, backward, their reduce launches) collapse into one.
+constexpr int CAT_MAXP = 8;
+struct CatPart {
+  const bf16_t* raw;
+  const float* ss;
+  uint8_t* mask;
+  bf16_t* dx;       // backward: the part's input gradient [M][C]
+  int C, off, flags;  // flags bit 0: relu (forward) / unscaled (backward)
+};
+struct CatArgs {
+  CatPart p[CAT_MAXP];
+  int np, Ct, M, rpb;
+};
+__device__ __forceinline__ int cat_part(const CatArgs& a, int gc) {
+  int k = 0;
+#pragma unroll
+  for (int i = 1; i < CAT_MAXP; ++i)
+    if (i < a.np && gc >= a.p[i].off) k = i;
+  return k;
+}
+
+__global__ __launch_bounds__(256) void cat_bn_apply_kernel(CatArgs a, bf16_t* __restrict__ out) {
+  const int cols = a.Ct >> 3, t = threadIdx.x, RP = 256 / cols, gc = (t % cols) * 8, lr0 = t / cols;
+  if (lr0 >= RP) return;
+  const int k = cat_part(a, gc);
+  const CatPart& P = a.p[k];
+  const int cl = gc - P.off;
+  const bool relu = P.flags & 1;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { sc[e] = P.ss[cl + e]; sh[e] = P.ss[P.C + cl + e]; }
+  const int r0 = blockIdx.x * a.rpb, r1 = min(a.M, r0 + a.rpb);
+  for (int row = r0 + lr0; row < r1; row += RP * FU2) {
+    uint4 v[FU2];
+#pragma unroll
+    for (int u = 0; u < FU2; ++u) {
+      const int rr = row + u * RP;
+      v[u] = rr < r1 ? ld16<true>(P.raw + (size_t)rr * P.C + cl) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < FU2; ++u) {
+      const int rr = row + u * RP;
+      if (rr >= r1) break;
+      float f[8];
+      up8(v[u], f);
+      uint32_t bits = 0u;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        f[e] = fmaf(f[e], sc[e], sh[e]);
+        if (relu) f[e] = fmaxf(f[e], 0.f);
+        bits |= (f[e] > 0.f ? 1u : 0u) << e;
+      }
+      *(uint4*)(out + (size_t)rr * a.Ct + gc) = pk8(f);
+      if (P.mask) P.mask[((size_t)rr * P.C + cl) >> 3] = (uint8_t)bits;
+    }
+  }
+}
+
+// backward: g = d(concat slice) * mask bit; dx = g (unscaled producer) or g*scale; per block a partial row of
+// width 4*Ct laid out as every part's [4][C] (Σg·x | Σg | 0 | 0), so ONE reduction yields the parts' dss
+// buffers back to back
+__global__ __launch_bounds__(256) void cat_bn_apply_bwd_kernel(CatArgs a, const bf16_t* __restrict__ dout,
+                                                               float* __restrict__ ws) {
+  __shared__ float red[2][256][8];
+  const int cols = a.Ct >> 3, t = threadIdx.x, RP = 256 / cols, gc = (t % cols) * 8, lr0 = t / cols;
+  const int k = cat_part(a, gc);
+  const CatPart& P = a.p[k];
+  const int cl = gc - P.off;
+  const bool ux = P.flags & 1;
+  float sc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sc[e] = P.ss[cl + e];
+  float a1[8], a0[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a1[e] = a0[e] = 0.f;
+  const int r0 = blockIdx.x * a.rpb, r1 = min(a.M, r0 + a.rpb);
+  for (int row = lr0 < RP ? r0 + lr0 : r1; row < r1; row += RP * FU2) {
+    uint4 vd[FU2], vx[FU2];
+    uint32_t mb[FU2];
+#pragma unroll
+    for (int u = 0; u < FU2; ++u) {
+      const int rr = row + u * RP;
+      const bool ok = rr < r1;
+      const size_t o = (size_t)rr * P.C + cl;
+      vd[u] = ok ? ld16<true>(dout + (size_t)rr * a.Ct + gc) : make_uint4(0, 0, 0, 0);
+      vx[u] = ok ? ld16<true>(P.raw + o) : make_uint4(0, 0, 0, 0);
+      mb[u] = ok ? (uint32_t)P.mask[o >> 3] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < FU2; ++u) {
+      const int rr = row + u * RP;
+      if (rr >= r1) break;
+      float g[8], xv[8];
+      up8(vd[u], g);
+      up8(vx[u], xv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        g[e] = (mb[u] >> e) & 1u ? g[e] : 0.f;
+        a1[e] += g[e] * xv[e];
+        a0[e] += g[e];
+        if (!ux) g[e] *= sc[e];
+      }
+      *(uint4*)(P.dx + (size_t)rr * P.C + cl) = pk8(g);
+    }
+  }
+  float* row = ws + (size_t)blockIdx.x * 4 * a.Ct + 4 * P.off;  // this part's [4][C] image in the row
+  col_reduce8(red, a1, a0, row - P.off, row + P.C - P.off, cols, gc);
+  if (t < cols) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { row[2 * P.C + cl + e] = 0.f; row[3 * P.C + cl + e] = 0.f; }
+  }
+}
+
 static void grid2(long M, int C, int* blocks, int* rpb, int cap = 2048) {
   int cols = C / 8, RP = 256 / cols;
   long chunks = M * cols;
@@ -323,6 +442,46 @@ DTM_API int dtm_bn_apply_bwd_ld(const void* dy, const void* ymask, const void* x
                      (const float*)nullptr, (bf16_t*)dx, (bf16_t*)nullptr, ws, nullptr, (int)M, C, 3, 0, unscaled & 1,
                      rpb, lddy, direct);
   if (!direct) dtm_reduce_rows(ws, blocks, 2 * C, 4 * C, sx, (hipStream_t)stream);
+  return 0;
+}
+
+// Zero-copy concat of np BN'd parts in one launch: descs[np] = {raw, ss, mask, dx, C, off, flags}, from the
+// host as a packed table (dtm_cat_desc_bytes per part).  Forward writes out [M][Ct] and the masks.
+DTM_API int dtm_cat_desc_bytes() { return (int)sizeof(CatPart); }
+static int cat_args(const void* descs, int np, long M, int Ct, CatArgs* a) {
+  if (np < 1 || np > CAT_MAXP || Ct % 8 || Ct / 8 > 256 || M >= (1l << 31)) return -1;
+  memcpy(a->p, descs, np * sizeof(CatPart));
+  int off = 0;
+  for (int i = 0; i < np; ++i) {
+    if (a->p[i].off != off || a->p[i].C % 8 || !a->p[i].raw || !a->p[i].ss) return -1;
+    off += a->p[i].C;
+  }
+  if (off != Ct) return -1;
+  a->np = np; a->Ct = Ct; a->M = (int)M;
+  return 0;
+}
+DTM_API int dtm_cat_bn_apply(const void* descs, int np, void* out, long M, int Ct, void* stream) {
+  CatArgs a;
+  if (cat_args(descs, np, M, Ct, &a) || ((uintptr_t)out & 15)) return -1;
+  int blocks;
+  grid2(M, Ct, &blocks, &a.rpb);
+  hipLaunchKernelGGL(cat_bn_apply_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a, (bf16_t*)out);
+  return 0;
+}
+// Backward: dout [M][Ct]; every part's dx gets g (or g*scale), and sums [4*Ct] (zeroed by the caller) +=
+// the parts' [4][C] ss gradients back to back (rows 0-1: Σg·x, Σg; rows 2-3 stay zero).
+DTM_API int dtm_cat_bn_apply_bwd(const void* descs, int np, const void* dout, float* sums, long M, int Ct, void* stream) {
+  CatArgs a;
+  if (cat_args(descs, np, M, Ct, &a) || ((uintptr_t)dout & 15)) return -1;
+  for (int i = 0; i < np; ++i)
+    if (!a.p[i].mask || !a.p[i].dx) return -1;
+  int blocks;
+  grid2(M, Ct, &blocks, &a.rpb);
+  float* ws = dtm_ws_get((size_t)blocks * 4 * Ct);
+  if (!ws) return -4;
+  hipLaunchKernelGGL(cat_bn_apply_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a,
+                     (const bf16_t*)dout, ws);
+  dtm_reduce_rows(ws, blocks, 4 * Ct, 4 * Ct, sums, (hipStream_t)stream);
   return 0;
 }
 

@@ -730,6 +730,20 @@ class _ConcatBNApplyFn(torch.autograd.Function):
     are copied into their slice.  meta: per part ('bn', C, relu, unscaled) or ('t', C)."""
 
     @staticmethod
+    def _descs(parts):
+        """Host table of CatPart (fused_bn.hip) for dtm_cat_bn_apply(_bwd): per part (raw, ss, mask, dx, C,
+        channel offset, flags)."""
+        import numpy as np
+        nb = _lib.lib().dtm_cat_desc_bytes()
+        tab = np.zeros((len(parts), nb // 8), dtype=np.int64)
+        off = 0
+        for i, (raw, ss, mask, dx, C, flags) in enumerate(parts):
+            tab[i, 0:4] = [t.data_ptr() if t is not None else 0 for t in (raw, ss, mask, dx)]
+            tab[i, 4:6] = np.array([C, off, flags, 0], dtype=np.int32).view(np.int64)
+            off += C
+        return tab
+
+    @staticmethod
     def forward(ctx, meta, *ts):
         L = _lib.lib()
         first = ts[0]
@@ -739,6 +753,21 @@ class _ConcatBNApplyFn(torch.autograd.Function):
         out = torch.empty((N, H, W, Ct), device=first.device, dtype=torch.bfloat16)
         saved, off, i = [], 0, 0
         s = _lib.stream_ptr()
+        ctx.multi = _cat_multi() and all(m[0] == "bn" for m in meta) and len(meta) <= 8
+        if ctx.multi:
+            # every part's BN-apply in one launch (fused_bn.hip cat_bn_apply_kernel)
+            parts = []
+            for k, m in enumerate(meta):
+                raw, ss = ts[2 * k], ts[2 * k + 1]
+                mask = torch.empty(M * m[1] // 8, device=raw.device, dtype=torch.uint8)
+                parts.append((raw, ss, mask, None, m[1], int(m[2])))
+                saved += [raw, ss, mask]
+            tab = _ConcatBNApplyFn._descs(parts)
+            _check(L.dtm_cat_bn_apply(ctypes.c_void_p(tab.ctypes.data), len(parts), _lib.ptr(out), M, Ct, s),
+                   "cat_bn_apply")
+            ctx.meta = meta
+            ctx.save_for_backward(*saved)
+            return out
         for m in meta:
             C = m[1]
             if m[0] == "bn":
@@ -764,6 +793,21 @@ class _ConcatBNApplyFn(torch.autograd.Function):
         Ct = dout.shape[-1]
         M = dout.numel() // Ct
         s = _lib.stream_ptr()
+        if ctx.multi:
+            # every part's BN-apply backward and ONE reduction: sums holds the parts' [4][C] dss back to back
+            parts, grads = [], []
+            sums = arena.zeros((4 * Ct,), dout.device)
+            off = 0
+            for k, m in enumerate(ctx.meta):
+                raw, ss, mask = saved[3 * k:3 * k + 3]
+                dx = torch.empty_like(raw)
+                parts.append((raw, ss, mask, dx, m[1], int(m[3])))
+                grads += [dx, sums[4 * off:4 * (off + m[1])].view(4, m[1])]
+                off += m[1]
+            tab = _ConcatBNApplyFn._descs(parts)
+            _check(L.dtm_cat_bn_apply_bwd(ctypes.c_void_p(tab.ctypes.data), len(parts), _lib.ptr(dout), _lib.ptr(sums),
+                                          M, Ct, s), "cat_bn_apply_bwd")
+            return (None,) + tuple(grads)
         grads, off, j = [], 0, 0
         for m in ctx.meta:
             C = m[1]
@@ -780,6 +824,12 @@ class _ConcatBNApplyFn(torch.autograd.Function):
                 grads.append(dout[..., off:off + C])
             off += C
         return (None,) + tuple(grads)
+
+
+def _cat_multi():
+    """A/B knob DTM_CAT_MULTI (default on): the one-launch multi-part concat BN-apply."""
+    import os
+    return os.environ.get("DTM_CAT_MULTI", "1") != "0"
 
 
 def concat_channels(parts):

@@ -187,6 +187,42 @@ def test_zero_copy_concat_exact(Cs):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize("Cs", [(64, 96, 32, 48), (320, 384, 384, 192), (192, 192, 192, 192), (8, 16)])
+def test_zero_copy_concat_one_launch(monkeypatch, Cs):
+    """All-BN concats take the one-launch multi-part kernels (every part's BN-apply, then every part's
+    backward + one reduction of the dss rows): bit-identical output / masks / input gradients to the
+    per-part launches and torch.cat, the statistics gradients equal up to summation order."""
+    from distributed_tensorflow_models_amd.ops.fused import bn_apply, concat_channels
+    from distributed_tensorflow_models_amd.ops.lazy import LazyBN
+    torch.manual_seed(0)
+    N, H, W = 4, 9, 7
+    raws = [torch.randn(N, H, W, c, device=DEV).to(torch.bfloat16) for c in Cs]
+    sss = [torch.cat([torch.rand(1, c, device=DEV) + 0.5, torch.randn(1, c, device=DEV) * 0.3,
+                      torch.randn(2, c, device=DEV)]) for c in Cs]
+    dout = torch.randn(N, H, W, sum(Cs), device=DEV).to(torch.bfloat16)
+    outs = []
+    for mode in ("multi", "parts", "cat"):
+        monkeypatch.setenv("DTM_CAT_MULTI", "0" if mode == "parts" else "1")
+        rs = [r.clone().requires_grad_() for r in raws]
+        ss = [x.clone().requires_grad_() for x in sss]
+        lz = [LazyBN(r, s, True, unscaled=(i % 2 == 0)) for i, (r, s) in enumerate(zip(rs, ss))]
+        if mode == "cat":
+            y = torch.cat([bn_apply(r, s, True, None, unscaled=(i % 2 == 0)) for i, (r, s) in enumerate(zip(rs, ss))],
+                          -1)
+        else:
+            y = concat_channels(lz)
+        y.backward(dout)
+        torch.cuda.synchronize()
+        outs.append((y.detach(), [r.grad for r in rs], [s.grad for s in ss]))
+    (ya, ra, sa), (yb, rb, sb), (yc, rc, sc) = outs
+    assert torch.equal(ya, yb) and torch.equal(ya, yc)
+    for a, b, c in zip(ra, rb, rc):
+        assert torch.equal(a, b) and torch.equal(a, c)
+    for a, b, c in zip(sa, sb, sc):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-4)
+        torch.testing.assert_close(a, c, rtol=1e-5, atol=1e-4)
+
+
 def test_inception_zero_copy_concat_matches_torch_cat(monkeypatch):
     """Old-slim Inception-v3 with branch outputs BN-applied straight into their concat slices (and
     their gradients read in place) vs the same model through torch.cat of materialised branches.
