@@ -2357,8 +2357,9 @@ DTM_API int dtm_conv_wgrad(const void* x, const void* dy, float* dw, const float
   return conv_wgrad_impl(x, dy, dw, in_scale, in_shift, d, num_cus, nullptr, stream);
 }
 
-// dw is a persistent gradient buffer that nothing reads before dtm_side_join: the split-K slab reduction
-// runs on the side stream (workspace.hip)
+// dw is a persistent gradient buffer that nothing reads before ops.nn.side_join: the split-K slab
+// reduction runs on the side stream (opt-in) or is queued for the next dtm_def_flush (default;
+// workspace.hip)
 DTM_API int dtm_conv_wgrad_side(const void* x, const void* dy, float* dw, const float* in_scale,
                                 const float* in_shift, const ConvDesc* d, int num_cus, void* stream) {
   return conv_wgrad_impl(x, dy, dw, in_scale, in_shift, d, num_cus, nullptr, stream, true);
@@ -2432,8 +2433,13 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   a.pix_per_split = (int)(steps_per * 64);
   splits = (a.Mpix + a.pix_per_split - 1) / a.pix_per_split;
   int slot = -1;
-  float* ws = side ? dtm_side_slab((size_t)splits * a.K * a.Kg, (hipStream_t)stream, &slot) : nullptr;
-  if (!ws) ws = dtm_ws_get((size_t)splits * a.K * a.Kg);
+  const size_t slab = (size_t)splits * a.K * a.Kg;
+  float* ws = side ? dtm_side_slab(slab, (hipStream_t)stream, &slot) : nullptr;
+  // deferred: one segmented reduction for many convs at the next flush (needs float4 columns)
+  float* dws = (side && !ws && (a.K * a.Kg) % 4 == 0 && ((uintptr_t)dw & 15) == 0)
+                   ? dtm_def_slab(slab, (hipStream_t)stream) : nullptr;
+  if (dws) ws = dws;
+  if (!ws) ws = dtm_ws_get(slab);
   if (!ws) return -4;
   a.dw = ws;
   if (wt >= 10) {
@@ -2459,6 +2465,7 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   else launch_wgrad<128, 128, 64, 64>(a, (int)splits, (hipStream_t)stream);
   // dW += sum over the split slabs (every slab element is written: tiles cover [K][Kg] exactly)
   if (slot >= 0) dtm_side_reduce(slot, (int)splits, a.K * a.Kg, a.K * a.Kg, dw, (hipStream_t)stream);
+  else if (dws) dtm_def_push(ws, (int)splits, a.K * a.Kg, dw);
   else dtm_reduce_rows(ws, (int)splits, a.K * a.Kg, a.K * a.Kg, dw, (hipStream_t)stream);
   return 0;
 }

@@ -245,3 +245,104 @@ DTM_API void dtm_side_join(void* stream) {
   hipStreamWaitEvent((hipStream_t)stream, g_join, 0);
   g_pending = false;
 }
+
+// ---- deferred weight-gradient reductions ---------------------------------------------------------
+// The split-K slabs of the convs whose gradient target is a persistent buffer (main_grad) are not reduced
+// one launch per conv: each slab goes to a bump arena and its (slab, rows, width, out) is queued; the
+// queue is flushed - ONE segmented reduction launch (per 64 entries) - when a reader needs the gradients
+// (bucket all-reduce, end of backward: dtm_def_flush via ops.nn.side_join) or when the arena is full.
+// Same stream throughout, so no event is needed; each output column is summed by one thread over the
+// slab rows in order (deterministic).
+namespace {
+struct DefEntry {
+  const float* ws;
+  float* out;
+  int rows, width;  // width in floats, % 4 == 0
+};
+constexpr int DEF_TAB = 64;
+struct DefTab {
+  DefEntry e[DEF_TAB];
+  int start[DEF_TAB + 1];  // first block of each entry
+  int n;
+};
+DefEntry g_def[4096];
+int g_def_n = 0;
+float* g_def_buf = nullptr;
+size_t g_def_cap = 0, g_def_used = 0;
+int g_def_on = 0;
+}  // namespace
+
+__global__ __launch_bounds__(256) void def_reduce_kernel(DefTab t) {
+  int i = 0;
+  while (i + 1 < t.n && (int)blockIdx.x >= t.start[i + 1]) ++i;
+  const DefEntry e = t.e[i];
+  const int col = ((int)blockIdx.x - t.start[i]) * 1024 + threadIdx.x * 4;
+  if (col >= e.width) return;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int r = 0;
+  for (; r + 4 <= e.rows; r += 4) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *(const float4*)(e.ws + (size_t)(r + u) * e.width + col);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
+  }
+  for (; r < e.rows; ++r) {
+    const float4 v = *(const float4*)(e.ws + (size_t)r * e.width + col);
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  float4* o = (float4*)(e.out + col);
+  const float4 c = *o;
+  *o = make_float4(c.x + acc.x, c.y + acc.y, c.z + acc.z, c.w + acc.w);
+}
+
+DTM_API void dtm_set_def_reduce(int on) { g_def_on = on; }
+
+DTM_API void dtm_def_flush(void* stream) {
+  for (int b = 0; b < g_def_n; b += DEF_TAB) {
+    DefTab t;
+    t.n = g_def_n - b < DEF_TAB ? g_def_n - b : DEF_TAB;
+    int blocks = 0;
+    for (int i = 0; i < t.n; ++i) {
+      t.e[i] = g_def[b + i];
+      t.start[i] = blocks;
+      blocks += (t.e[i].width + 1023) / 1024;
+    }
+    t.start[t.n] = blocks;
+    hipLaunchKernelGGL(def_reduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, t);
+  }
+  g_def_n = 0;
+  g_def_used = 0;
+}
+
+// a slab of `floats` for a deferred reduction (nullptr: reduce in place - knob off, shape, no memory)
+float* dtm_def_slab(size_t floats, hipStream_t st) {
+  if (!g_def_on || g_def_n >= 4096) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) return nullptr;
+  const size_t need = (floats + 63) / 64 * 64;
+  if (g_def_used + need > g_def_cap) {
+    dtm_def_flush(st);  // (stream-ordered: the queued reductions read the arena before anything reuses it)
+    if (need > g_def_cap) {
+      if (cs != hipStreamCaptureStatusNone) return nullptr;  // no allocation inside a capture
+      if (g_def_buf) {
+        hipStreamSynchronize(st);
+        hipFree(g_def_buf);
+      }
+      size_t n = need < (64u << 20) ? (64u << 20) : need;  // >= 256 MB
+      if (hipMalloc(&g_def_buf, n * sizeof(float)) != hipSuccess) {
+        g_def_buf = nullptr;
+        g_def_cap = 0;
+        return nullptr;
+      }
+      g_def_cap = n;
+    }
+  }
+  float* p = g_def_buf + g_def_used;
+  g_def_used += need;
+  return p;
+}
+
+void dtm_def_push(const float* ws, int rows, int width, float* out) {
+  g_def[g_def_n++] = DefEntry{ws, out, rows, width};
+}

@@ -49,6 +49,8 @@ _SIGS = {
     "dtm_conv_wgrad": (_I, [_P, _P, _P, _P, _P, ctypes.POINTER(ConvDesc), _I, _P]),
     "dtm_conv_wgrad_side": (_I, [_P, _P, _P, _P, _P, ctypes.POINTER(ConvDesc), _I, _P]),
     "dtm_side_join": (None, [_P]),
+    "dtm_def_flush": (None, [_P]),
+    "dtm_set_def_reduce": (None, [_I]),
     "dtm_set_side_reduce": (None, [_I]),
     "dtm_conv_set_fin_fuse": (None, [_I]),
     "dtm_conv_set_policy2": (None, [_I]),

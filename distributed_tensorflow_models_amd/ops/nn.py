@@ -67,15 +67,20 @@ def _note_live_window(w, win):
 
 
 def side_join():
-    """Make the current stream wait for every weight-gradient reduction issued on the kernel library's
-    side stream (dtm_conv_wgrad_side): call before anything reads the fp32 gradient buffers."""
+    """Complete every weight-gradient reduction that dtm_conv_wgrad_side left pending: flush the queue of
+    deferred slab reductions (one segmented launch) and make the current stream wait for the side
+    stream (if that opt-in path is on).  Call before anything reads the fp32 gradient buffers."""
     if torch.cuda.is_available() and torch.cuda.is_initialized():
-        _lib.lib().dtm_side_join(_lib.stream_ptr())
+        L = _lib.lib()
+        s = _lib.stream_ptr()
+        L.dtm_def_flush(s)
+        L.dtm_side_join(s)
 
 
 def wgrad_into(L, target, is_main_grad):
     """The wgrad entry for a target buffer: a persistent main_grad (read only after side_join) lets the
-    split-K slab reduction run on the side stream; a temporary takes the in-stream reduction."""
+    split-K slab reduction be deferred and batched with other convs' (or run on the side stream); a
+    temporary takes the immediate in-stream reduction."""
     return L.dtm_conv_wgrad_side if is_main_grad else L.dtm_conv_wgrad
 
 
