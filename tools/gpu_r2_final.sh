@@ -12,4 +12,6 @@ timeout -k 10 300 python bench.py --gpus 2 --dist-backend gloo --steps 5 --warmu
 grep '"value"' gpurun_out/bench_gloo2_final.log | cut -c1-400
 rm -rf gpurun_out/prof
 bash tools/gpu_session.sh prof > gpurun_out/prof_session_final.log 2>&1 || { tail -20 gpurun_out/prof_session_final.log; exit 1; }
+rm -rf gpurun_out/prof_inception_v3_slim_old gpurun_out/prof_vgg_16
+MODELS="inception_v3_slim_old vgg_16" bash tools/gpu_prof_models.sh > gpurun_out/prof_models_final.log 2>&1 || { tail -20 gpurun_out/prof_models_final.log; exit 1; }
 python3 tools/prof_summary.py $(find gpurun_out/prof -name "*kernel_stats.csv" | head -1) 5 12
