@@ -627,18 +627,30 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
     if constexpr (PRE) {
       if (kt == nk - 1) epi_side_load<PT, CT, 256>(a, p0, c0, sd);
     }
+    // (PRE, last k-tile: a raw barrier - __syncthreads() would also drain the side-input loads just issued)
+    const bool raw_last = PRE && kt == nk - 1;
     if constexpr (NBUF == 2) {
       const int cur = kt & 1;
       if (kt + 1 < nk) gload(kt + 1, st);
       compute(cur);
       if (kt + 1 < nk) swrite(cur ^ 1, st);
-      __syncthreads();
+      if (raw_last) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      } else {
+        __syncthreads();
+      }
     } else {
       // single LDS buffer (less LDS -> more resident blocks for short-K layers): the next tile's
       // global loads still overlap the MFMAs; the LDS write waits for every wave's reads
       if (kt + 1 < nk) gload(kt + 1, st);
       compute(0);
-      __syncthreads();
+      if (raw_last) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      } else {
+        __syncthreads();
+      }
       if (kt + 1 < nk) {
         swrite(0, st);
         __syncthreads();
@@ -647,7 +659,8 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
   }
 
   static_assert(PT * (CT * 2 + 16) <= NBUF * BUF, "output staging fits in the operand buffers");
-  if constexpr (PRE) conv_nt_epilogue<PT, CT, WP, WC, 1>(a, acc, smem, p0, c0, by, nullptr, nullptr, &sd);
+  // (PRE: raw-barrier epilogue, so the side loads stay in flight until their registers are used)
+  if constexpr (PRE) conv_nt_epilogue<PT, CT, WP, WC, 1, true>(a, acc, smem, p0, c0, by, nullptr, nullptr, &sd);
   else if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1>(a, acc, smem, p0, c0, by);
   else conv_nt_epilogue<PT, CT, WP, WC, 2>(a, acc, smem, p0, c0, by);
 }

@@ -12,8 +12,9 @@ Returns (logits, aux_logits) in training mode; the trainer weights the aux loss 
 import torch
 
 from ..ops import nn as F
+from ..ops import fused as _fused
 from ..ops.fused import concat_channels
-from .layers import BatchNorm, Conv2d, Dropout, FullyConnected, Layer
+from .layers import BatchNorm, Conv2d, Dropout, FullyConnected, Layer, fused_enabled
 
 
 class _Scope:
@@ -141,10 +142,22 @@ class InceptionV3Slim(Layer):
     # ---- forward --------------------------------------------------------------------------------
     @staticmethod
     def _run(branch, x, training):
-        for op in branch:
+        skip = False
+        for i, op in enumerate(branch):
+            if skip:
+                skip = False
+                continue
             # a pooling branch reads the block input alongside the branch convs: it joins their
             # gradient hand-off (its backward runs first and stashes; the last conv folds the stash)
             if op == "avg3":
+                nxt = branch[i + 1] if i + 1 < len(branch) else None
+                if (isinstance(nxt, Conv2d) and nxt.kh == 1 and nxt.kw == 1 and nxt.stride == 1 and
+                        nxt.bn is not None and nxt.activation == "relu" and _fused.pool_commute_enabled() and
+                        getattr(x, "is_cuda", False) and fused_enabled()):
+                    # conv -> pool -> BN: the pool runs over the conv's output channels (ops.fused)
+                    x = _fused.conv_avgpool_bn(x, nxt.weights, nxt.bn, training, relu=True)
+                    skip = True
+                    continue
                 x = F.avg_pool(x, 3, 1, "SAME", grad_handoff=True)
             elif op == "max3s2":
                 x = F.max_pool(x, 3, 2, "VALID", grad_handoff=True)

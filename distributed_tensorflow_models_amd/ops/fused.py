@@ -720,6 +720,52 @@ def conv_bn(x, w, bn, stride, padding, training, relu):
     return LazyBN(y, ss, relu, unscaled=training)
 
 
+class _BNStatsFn(torch.autograd.Function):
+    """stats = [sum y; sum y^2] per channel (HIP reduction); backward: dy = dsum + 2*y*dsumsq."""
+
+    @staticmethod
+    def forward(ctx, y):
+        C = y.shape[-1]
+        stats = torch.zeros((2, C), device=y.device, dtype=torch.float32)
+        _lib.lib().dtm_bn_stats(_lib.ptr(y), _lib.ptr(stats), y.numel() // C, C, _lib.stream_ptr())
+        ctx.save_for_backward(y)
+        return stats
+
+    @staticmethod
+    def backward(ctx, dstats):
+        (y,) = ctx.saved_tensors
+        return (dstats[0] + 2.0 * y.float() * dstats[1]).to(y.dtype)
+
+
+def pool_commute_enabled():
+    """A/B knob DTM_POOL_COMMUTE (default on): Inception pool branches as conv -> avg_pool -> BN."""
+    import os
+    return os.environ.get("DTM_POOL_COMMUTE", "1") != "0"
+
+
+def conv_avgpool_bn(x, w, bn, training, relu=True):
+    """An Inception pool branch - avg_pool 3x3/1 'SAME' -> 1x1 conv -> BatchNorm (+ReLU), reference
+    inception/slim/inception_model.py:88-92 etc. - computed as 1x1 conv -> avg_pool -> BatchNorm.  The two
+    linear maps commute exactly (the pool mixes pixels per channel, the 1x1 conv channels per pixel, and
+    TF's 'SAME' divisor depends on the pixel only), so the pool runs over the conv's K output channels
+    instead of the block input's C (Inception: 288 -> 64, 768 -> 192, 2048 -> 192), forward and backward.
+    The conv keeps the block input's gradient hand-off; the BatchNorm statistics come from the pooled
+    tensor.  Returns a LazyBN like conv_bn."""
+    from .nn import avg_pool
+    xb = as_tensor(x).to(torch.bfloat16).contiguous()
+    g = conv_geom(tuple(xb.shape), tuple(w.shape), 1, "SAME")
+    slot = _slot_register(xb) if xb is x else None
+    z = _ConvBNFn.apply(xb, None, w, None, None, g, None, slot)
+    y = avg_pool(z, 3, 1, "SAME")
+    if training:
+        stats = _BNStatsFn.apply(y)
+        ss = _BNFinalizeFn.apply(stats, bn.gamma, bn.beta, bn.moving_mean, bn.moving_variance,
+                                 float(y.numel() // y.shape[-1]), float(bn.eps), float(bn.decay), bool(bn.bessel), True)
+    else:
+        ss = bn_inference_ss(bn)
+    return LazyBN(y, ss, relu, unscaled=False)
+
+
 # ---------------------------------------------------------------------------------------------
 class _ConcatBNApplyFn(torch.autograd.Function):
     """Zero-copy channel concat (Inception mixed blocks, reference

@@ -276,3 +276,47 @@ def test_pool_joins_shared_input_grad_handoff(pool):
         loss.backward()
         grads.append(x.grad.float())
     assert _rel(grads[0], grads[1]) < 1e-2
+
+
+@pytest.mark.parametrize("C,K,H", [(288, 64, 35), (768, 192, 17), (2048, 192, 8)])
+def test_pool_branch_commuted(C, K, H):
+    """Inception pool branch avg_pool(3x3/1 SAME) -> 1x1 conv -> BN+ReLU computed as 1x1 conv -> avg_pool ->
+    BN (fused.conv_avgpool_bn): output, input / weight / BN-parameter gradients and moving statistics are
+    as close to the fp32 reference (original order) as the bf16 original-order path is (training-mode
+    batch statistics; the residual difference is bf16 rounding of different intermediates and the ReLU
+    mask flips it causes)."""
+    from distributed_tensorflow_models_amd.models.layers import Conv2d
+    from distributed_tensorflow_models_amd.ops import fused
+    from distributed_tensorflow_models_amd.ops import nn as F
+    from distributed_tensorflow_models_amd.ops import reference as ref
+    bn = dict(decay=0.9997, epsilon=1e-3, scale=False, bessel=False)
+    torch.manual_seed(0)
+    x0 = torch.randn(8, H, H, C, device=DEV).to(torch.bfloat16)
+    gy0 = torch.randn(8, H, H, K, device=DEV).to(torch.bfloat16)
+    res = []
+    for mode in ("ref", "orig", "commute"):
+        torch.manual_seed(0)
+        conv = Conv2d("pool_conv", C, K, 1, 1, "SAME", "relu", dict(bn), False, 0.0, ("truncated_normal", 0.1)).to(DEV)
+        if mode == "ref":
+            x = x0.float().requires_grad_()
+            w = conv.weights.detach().float().requires_grad_()
+            beta = conv.bn.beta.detach().clone().requires_grad_()
+            mm, mv = conv.bn.moving_mean.clone(), conv.bn.moving_variance.clone()
+            y = ref.batch_norm(ref.conv2d(ref.avg_pool(x, 3, 1, "SAME"), w, None, 1, "SAME"), None, beta, mm, mv,
+                               True, 0.9997, 1e-3, True, None, False)
+            y.backward(gy0.float())
+            res.append((y, x.grad, w.grad, beta.grad, mm, mv))
+            continue
+        x = x0.clone().requires_grad_()
+        if mode == "commute":
+            lz = fused.conv_avgpool_bn(x, conv.weights, conv.bn, True, relu=True)
+        else:
+            lz = conv(F.avg_pool(x, 3, 1, "SAME"), True)
+        y = lz.materialize()
+        y.backward(gy0)
+        torch.cuda.synchronize()
+        res.append((y.float(), x.grad.float(), conv.weights.grad.float(), conv.bn.beta.grad.float(),
+                    conv.bn.moving_mean.clone(), conv.bn.moving_variance.clone()))
+    for r, o, c in zip(*res):
+        eo, ec = _rel(o, r), _rel(c, r)
+        assert ec < max(1.5 * eo, 2e-2), (eo, ec)
