@@ -1978,6 +1978,8 @@ static int g_k64_tile = 3;  // tile of the 64-output-channel layers (A/B knob: d
 DTM_API void dtm_conv_set_k64_tile(int id) { g_k64_tile = id; }
 static int g_pre_side = 0;  // A/B knob: early side-input loads in the register-staged dgrad epilogue
 DTM_API void dtm_conv_set_pre_side(int on) { g_pre_side = on; }
+static int g_stream128_act = 0;  // A/B knob (dtm_conv_set_stream128_act)
+DTM_API void dtm_conv_set_stream128_act(int on) { g_stream128_act = on; }
 static int g_act_tile = -1;  // A/B knob: tile of the dgrads with a fused activation-backward epilogue (-1 = policy)
 DTM_API void dtm_conv_set_act_tile(int id) { g_act_tile = id; }
 static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
@@ -1997,6 +1999,9 @@ static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
   else if (id == -1 && a.Kg == 64 && stream_ok(a) && (g_stream_act || !a.act_x) &&
            (!g_policy2 || a.K % 128 == 0 || a.K <= 64))  // (v2: no partial channel tiles: 35x35 ->288 -33 %)
     id = a.K >= 128 ? 30 : 31;
+  // A/B knob: the persistent streaming kernel also for the 128-deep dgrads with a fused epilogue (ResNet
+  // stage-2 block-output dgrads: epilogue-dominated HBM streams)
+  else if (id == -1 && g_stream128_act && a.Kg == 128 && a.act_x && stream_ok(a) && a.K % 128 == 0) id = 30;
   if (id == -1 && a.act_x && g_act_tile >= 0) id = g_act_tile;  // (A/B: the non-streaming act dgrads)
   // (the persistent streaming 1x1 kernel: the 64-deep 56x56 expand / reduce layers and their dgrads are
   // HBM streams: -20..-33 % (tools/conv_tile_sweep.py); at Kg 128 its 1 block/CU loses)
