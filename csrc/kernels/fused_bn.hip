@@ -380,10 +380,12 @@ __global__ __launch_bounds__(256) void cat_bn_apply_bwd_kernel(CatArgs a, const 
   }
 }
 
+static int g_cpt = 8;  // A/B knob: 16-B chunks per thread the BN-stream grids aim for (dtm_set_grid_cpt)
+DTM_API void dtm_set_grid_cpt(int n) { g_cpt = n > 0 ? n : 8; }
 static void grid2(long M, int C, int* blocks, int* rpb, int cap = 2048) {
   int cols = C / 8, RP = 256 / cols;
   long chunks = M * cols;
-  long b = chunks / (256 * 8);
+  long b = chunks / (256 * g_cpt);
   if (b < 1) b = 1;
   if (b > cap) b = cap;
   long r = (M + b - 1) / b;
