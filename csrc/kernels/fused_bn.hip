@@ -274,7 +274,8 @@ struct CatPart {
   const float* ss;
   uint8_t* mask;
   bf16_t* dx;       // backward: the part's input gradient [M][C]
-  int C, off, flags;  // flags bit 0: relu (forward) / unscaled (backward)
+  int C, off, flags;  // flags bit 0: relu (forward) / unscaled (backward); bit 1: a plain tensor part (copied
+                      // forward, no BN; its gradient is the caller's view of the concat gradient)
 };
 struct CatArgs {
   CatPart p[CAT_MAXP];
@@ -294,10 +295,13 @@ __global__ __launch_bounds__(256) void cat_bn_apply_kernel(CatArgs a, bf16_t* __
   const int k = cat_part(a, gc);
   const CatPart& P = a.p[k];
   const int cl = gc - P.off;
-  const bool relu = P.flags & 1;
+  const bool relu = P.flags & 1, plain = P.flags & 2;
   float sc[8], sh[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) { sc[e] = P.ss[cl + e]; sh[e] = P.ss[P.C + cl + e]; }
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = plain ? 1.f : P.ss[cl + e];
+    sh[e] = plain ? 0.f : P.ss[P.C + cl + e];
+  }
   const int r0 = blockIdx.x * a.rpb, r1 = min(a.M, r0 + a.rpb);
   for (int row = r0 + lr0; row < r1; row += RP * FU2) {
     uint4 v[FU2];
@@ -310,6 +314,10 @@ __global__ __launch_bounds__(256) void cat_bn_apply_kernel(CatArgs a, bf16_t* __
     for (int u = 0; u < FU2; ++u) {
       const int rr = row + u * RP;
       if (rr >= r1) break;
+      if (plain) {  // a plain part is copied bit for bit
+        *(uint4*)(out + (size_t)rr * a.Ct + gc) = v[u];
+        continue;
+      }
       float f[8];
       up8(v[u], f);
       uint32_t bits = 0u;
@@ -335,15 +343,16 @@ __global__ __launch_bounds__(256) void cat_bn_apply_bwd_kernel(CatArgs a, const 
   const int k = cat_part(a, gc);
   const CatPart& P = a.p[k];
   const int cl = gc - P.off;
-  const bool ux = P.flags & 1;
+  const bool ux = P.flags & 1, plain = P.flags & 2;
   float sc[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) sc[e] = P.ss[cl + e];
+  for (int e = 0; e < 8; ++e) sc[e] = plain ? 1.f : P.ss[cl + e];
   float a1[8], a0[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) a1[e] = a0[e] = 0.f;
   const int r0 = blockIdx.x * a.rpb, r1 = min(a.M, r0 + a.rpb);
-  for (int row = lr0 < RP ? r0 + lr0 : r1; row < r1; row += RP * FU2) {
+  // (a plain part's lanes only join the block reduction below, with zeros)
+  for (int row = (lr0 < RP && !plain) ? r0 + lr0 : r1; row < r1; row += RP * FU2) {
     uint4 vd[FU2], vx[FU2];
     uint32_t mb[FU2];
 #pragma unroll
@@ -455,7 +464,7 @@ static int cat_args(const void* descs, int np, long M, int Ct, CatArgs* a) {
   memcpy(a->p, descs, np * sizeof(CatPart));
   int off = 0;
   for (int i = 0; i < np; ++i) {
-    if (a->p[i].off != off || a->p[i].C % 8 || !a->p[i].raw || !a->p[i].ss) return -1;
+    if (a->p[i].off != off || a->p[i].C % 8 || !a->p[i].raw || (!a->p[i].ss && !(a->p[i].flags & 2))) return -1;
     off += a->p[i].C;
   }
   if (off != Ct) return -1;
@@ -476,7 +485,7 @@ DTM_API int dtm_cat_bn_apply_bwd(const void* descs, int np, const void* dout, fl
   CatArgs a;
   if (cat_args(descs, np, M, Ct, &a) || ((uintptr_t)dout & 15)) return -1;
   for (int i = 0; i < np; ++i)
-    if (!a.p[i].mask || !a.p[i].dx) return -1;
+    if (!(a.p[i].flags & 2) && (!a.p[i].mask || !a.p[i].dx)) return -1;
   int blocks;
   grid2(M, Ct, &blocks, &a.rpb);
   float* ws = dtm_ws_get((size_t)blocks * 4 * Ct);

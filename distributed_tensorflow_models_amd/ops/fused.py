@@ -799,15 +799,21 @@ class _ConcatBNApplyFn(torch.autograd.Function):
         out = torch.empty((N, H, W, Ct), device=first.device, dtype=torch.bfloat16)
         saved, off, i = [], 0, 0
         s = _lib.stream_ptr()
-        ctx.multi = _cat_multi() and all(m[0] == "bn" for m in meta) and len(meta) <= 8
+        cm = _cat_multi()
+        ctx.multi = (cm and any(m[0] == "bn" for m in meta) and len(meta) <= 8 and
+                     all(m[0] == "bn" or (cm == 1 and ts[i].dtype == torch.bfloat16 and ts[i].is_contiguous())
+                         for m, i in zip(meta, _part_index(meta))))
         if ctx.multi:
-            # every part's BN-apply in one launch (fused_bn.hip cat_bn_apply_kernel)
+            # every part's BN-apply (plain parts: a copy) in one launch (fused_bn.hip cat_bn_apply_kernel)
             parts = []
-            for k, m in enumerate(meta):
-                raw, ss = ts[2 * k], ts[2 * k + 1]
-                mask = torch.empty(M * m[1] // 8, device=raw.device, dtype=torch.uint8)
-                parts.append((raw, ss, mask, None, m[1], int(m[2])))
-                saved += [raw, ss, mask]
+            for m, i in zip(meta, _part_index(meta)):
+                if m[0] == "bn":
+                    raw, ss = ts[i], ts[i + 1]
+                    mask = torch.empty(M * m[1] // 8, device=raw.device, dtype=torch.uint8)
+                    parts.append((raw, ss, mask, None, m[1], int(m[2])))
+                    saved += [raw, ss, mask]
+                else:
+                    parts.append((ts[i], None, None, None, m[1], 2))
             tab = _ConcatBNApplyFn._descs(parts)
             _check(L.dtm_cat_bn_apply(ctypes.c_void_p(tab.ctypes.data), len(parts), _lib.ptr(out), M, Ct, s),
                    "cat_bn_apply")
@@ -841,14 +847,20 @@ class _ConcatBNApplyFn(torch.autograd.Function):
         s = _lib.stream_ptr()
         if ctx.multi:
             # every part's BN-apply backward and ONE reduction: sums holds the parts' [4][C] dss back to back
+            # (a plain part's gradient is its view of dout; its sums slots stay zero)
             parts, grads = [], []
             sums = arena.zeros((4 * Ct,), dout.device)
-            off = 0
-            for k, m in enumerate(ctx.meta):
-                raw, ss, mask = saved[3 * k:3 * k + 3]
-                dx = torch.empty_like(raw)
-                parts.append((raw, ss, mask, dx, m[1], int(m[3])))
-                grads += [dx, sums[4 * off:4 * (off + m[1])].view(4, m[1])]
+            off, j = 0, 0
+            for m in ctx.meta:
+                if m[0] == "bn":
+                    raw, ss, mask = saved[j:j + 3]
+                    j += 3
+                    dx = torch.empty_like(raw)
+                    parts.append((raw, ss, mask, dx, m[1], int(m[3])))
+                    grads += [dx, sums[4 * off:4 * (off + m[1])].view(4, m[1])]
+                else:
+                    parts.append((dout, None, None, None, m[1], 2))
+                    grads.append(dout[..., off:off + m[1]])
                 off += m[1]
             tab = _ConcatBNApplyFn._descs(parts)
             _check(L.dtm_cat_bn_apply_bwd(ctypes.c_void_p(tab.ctypes.data), len(parts), _lib.ptr(dout), _lib.ptr(sums),
@@ -872,10 +884,21 @@ class _ConcatBNApplyFn(torch.autograd.Function):
         return (None,) + tuple(grads)
 
 
+def _part_index(meta):
+    """Index of each concat part's first tensor in the flat (raw, ss | tensor) argument list."""
+    idx, i = [], 0
+    for m in meta:
+        idx.append(i)
+        i += 2 if m[0] == "bn" else 1
+    return idx
+
+
 def _cat_multi():
-    """A/B knob DTM_CAT_MULTI (default on): the one-launch multi-part concat BN-apply."""
+    """A/B knob DTM_CAT_MULTI: 1 (default) = the one-launch multi-part concat BN-apply, plain tensor parts
+    included; 2 = only for concats of BN'd parts; 0 = one launch per part."""
     import os
-    return os.environ.get("DTM_CAT_MULTI", "1") != "0"
+    v = os.environ.get("DTM_CAT_MULTI", "1")
+    return int(v) if v in ("0", "1", "2") else 1
 
 
 def concat_channels(parts):
