@@ -1978,6 +1978,8 @@ static int g_k64_tile = 3;  // tile of the 64-output-channel layers (A/B knob: d
 DTM_API void dtm_conv_set_k64_tile(int id) { g_k64_tile = id; }
 static int g_pre_side = 0;  // A/B knob: early side-input loads in the register-staged dgrad epilogue
 DTM_API void dtm_conv_set_pre_side(int on) { g_pre_side = on; }
+static int g_k32_tile = 1;  // A/B knob: the 256x32 tile for <= 32-channel spatial convs (dtm_conv_set_k32)
+DTM_API void dtm_conv_set_k32(int on) { g_k32_tile = on; }
 static int g_stream128_act = 0;  // A/B knob (dtm_conv_set_stream128_act)
 DTM_API void dtm_conv_set_stream128_act(int on) { g_stream128_act = on; }
 static int g_act_tile = -1;  // A/B knob: tile of the dgrads with a fused activation-backward epilogue (-1 = policy)
@@ -2021,7 +2023,8 @@ static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
   //    depth (5x5 48->64: 38.5 us vs 63.6 on the 128x128 tile the Kg >= 1024 rule picked; 3x3 -> 32: -10 %)
   //  * 64 < K <= 128 with a spatial kernel: the pipelined 128x128 tile (35x35 3x3 ->96: -11 %)
   if (id == -1 && g_policy2 && !a.in_scale && a.K % 8 == 0 && a.R * a.S > 1) {
-    if (a.K <= 64) id = 26;
+    if (a.K <= 32 && g_k32_tile) id = 32;  // (Inception's 32-channel stem 3x3s: no half-empty 64-wide tile)
+    else if (a.K <= 64) id = 26;
     else if (a.K <= 128) id = 21;
   }
   // output widths that leave the last 128-channel tile at most half full (Inception's 192 / 320 / 96 /
@@ -2049,6 +2052,7 @@ static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
   if (id == 27) return {id, 256, 2};              // 256 x 128 pipelined, waves 2x2 of 128x64
   if (id == 28) return {id, 512, 4};              // 512 x 64 pipelined, waves 4x1 of 128x64
   if (id == 29) return {id, 256, 4};              // 256 x 64 pipelined, waves 4x1 of 64x64
+  if (id == 32) return {id, 256, 4};              // 256 x 32 pipelined, waves 4x1 of 64x32
   // 8-wave 256-pixel tiles (no prologue): 40 = 256x256 (waves 2x4), 41 = 256x128 3-slot (4x2),
   // 42 = 256x128 2-slot, 43 = 256x256 (waves 4x2)
   if (id >= 40 && id <= 43 && a.in_scale) id = 0;
@@ -2091,6 +2095,7 @@ static void dispatch_ud(const ConvNTArgs& a, const TileCfg& t, hipStream_t st) {
   else if (t.id == 27) launch_pipe<256, 128, 2, UD>(a, st);     // waves 2x2 of 128x64
   else if (t.id == 28) launch_pipe<512, 64, 2, UD, 4>(a, st);   // waves 4x1 of 128x64
   else if (t.id == 29) launch_pipe<256, 64, 2, UD, 4>(a, st);   // waves 4x1 of 64x64
+  else if (t.id == 32) launch_pipe<256, 32, 2, UD, 4>(a, st);   // waves 4x1 of 64x32 (32-channel outputs)
   else if (t.id == 40) launch_w8<256, 256, 2, 2, UD>(a, st);
   else if (t.id == 41) launch_w8<256, 128, 4, 3, UD>(a, st);
   else if (t.id == 42) launch_w8<256, 128, 4, 2, UD>(a, st);

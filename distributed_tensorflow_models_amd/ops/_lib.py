@@ -56,6 +56,7 @@ _SIGS = {
     "dtm_conv_set_policy2": (None, [_I]),
     "dtm_conv_set_stream128_act": (None, [_I]),
     "dtm_set_grid_cpt": (None, [_I]),
+    "dtm_conv_set_k32": (None, [_I]),
     "dtm_cat_desc_bytes": (_I, []),
     "dtm_cat_bn_apply": (_I, [_P, _I, _P, _L, _I, _P]),
     "dtm_cat_bn_apply_bwd": (_I, [_P, _I, _P, _P, _L, _I, _P]),

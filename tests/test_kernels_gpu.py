@@ -161,11 +161,12 @@ def test_image_augment_kernel_matches_oracle(distort, size):
     assert got.is_cuda and _rel(got.cpu(), ref_out) < 1e-4
 
 
-@pytest.mark.parametrize("tile", [20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 40, 41, 42, 43])
+@pytest.mark.parametrize("tile", [20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 40, 41, 42, 43])
 @pytest.mark.parametrize("prologue", [False, True])
 @pytest.mark.parametrize("case", [(4, 15, 15, 64, 96, 3, 2), (2, 14, 14, 128, 256, 3, 1), (3, 7, 7, 512, 200, 1, 1),
                                   (2, 9, 9, 24, 40, 3, 1), (4, 12, 12, 64, 256, 1, 1), (3, 7, 7, 128, 96, 1, 1),
-                                  (2, 9, 9, 64, 64, 1, 1), (2, 30, 30, 128, 64, 1, 1), (4, 16, 16, 256, 512, 3, 1)])
+                                  (2, 9, 9, 64, 64, 1, 1), (2, 30, 30, 128, 64, 1, 1), (4, 16, 16, 256, 512, 3, 1),
+                                  (2, 19, 19, 32, 32, 3, 1), (2, 17, 17, 32, 24, 3, 2)])
 def test_conv_pipelined_tiles_match_reference(tile, prologue, case):
     """The pipelined LDS-DMA conv kernels (DTM_CONV_TILE=20..23; ring of k-tiles, counted vmcnt, the
     BatchNorm-apply prologue transformed in LDS) against the fp32 reference: forward (with and without
