@@ -2428,6 +2428,8 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   // dtm_conv_set_wgrad_n256)
   // (knob 1: only with the BN-backward operand transform, i.e. the stem; 2: every such layer)
   if (wenv == -1 && wt == 1 && a.Kg > 128 && (g_wgrad_n256 == 2 || (g_wgrad_n256 == 1 && bn))) wt = 4;
+  // <= 32 output channels: 32-row tiles (no half-empty 64-row tile; A/B knob dtm_conv_set_k32)
+  if (wenv == -1 && wt == 1 && d->K <= 32 && g_k32_tile) wt = 6;
   int occ = g_wgrad_occ;
   // policy (tools/conv_tile_sweep.py WTILES sweep, ResNet-50 shapes): the pipelined kernel at 2 blocks
   // per CU wins every layer with K > 64 (-10..-25 %); 4 blocks' worth of splits for the deep 3x3 7x7s
@@ -2441,7 +2443,7 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   if (wt >= 10 && (in_scale || bn)) wt = d->K <= 64 ? 1 : 0;  // the pipelined kernels have no operand prologues
   const bool small_m = (wt == 1 || wt == 2 || wt == 4 || wt == 5 || wt == 13 || wt == 14 || wt == 15);
   const bool big = wt == 12;  // 8-wave 256x256 (one block per CU)
-  const int MT = small_m ? 64 : (big ? 256 : 128),
+  const int MT = wt == 6 ? 32 : (small_m ? 64 : (big ? 256 : 128)),
             NT = (big || wt == 4 || wt == 5 || wt == 13 || wt == 14) ? 256 : 128;
   if (big) occ = (wenv == 12 && g_wgrad_occ != 4) ? g_wgrad_occ : 1;  // (sweeps: WTILES=12:<occ>)
   long tiles = (long)((a.Kg + NT - 1) / NT) * ((a.K + MT - 1) / MT);
@@ -2482,6 +2484,7 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
       hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 128, 2>), grid, dim3(256), 0, (hipStream_t)stream, a);
   } else if (wt == 1) launch_wgrad<64, 128, 32, 64>(a, (int)splits, (hipStream_t)stream);
   else if (wt == 4) launch_wgrad<64, 256, 32, 128>(a, (int)splits, (hipStream_t)stream);
+  else if (wt == 6) launch_wgrad<32, 128, 16, 64>(a, (int)splits, (hipStream_t)stream);
   else if (wt == 5) launch_wgrad<64, 256, 32, 128, 1>(a, (int)splits, (hipStream_t)stream);
   else if (wt == 2) launch_wgrad<64, 128, 32, 64, 1>(a, (int)splits, (hipStream_t)stream);
   else if (wt == 3) launch_wgrad<128, 128, 64, 64, 1>(a, (int)splits, (hipStream_t)stream);
