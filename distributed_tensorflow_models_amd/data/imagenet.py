@@ -75,7 +75,10 @@ def _decode_jpeg(data):
     from io import BytesIO
 
     from PIL import Image
-    return np.asarray(Image.open(BytesIO(data)).convert("RGB"))
+    im = Image.open(BytesIO(data))
+    if im.mode != "RGB":  # (grayscale / CMYK JPEGs; RGB ones skip the extra copy)
+        im = im.convert("RGB")
+    return np.asarray(im)
 
 
 def sample_distorted_bounding_box(h, w, bboxes, rng, min_object_covered=0.1, aspect_ratio_range=(0.75, 1.33),

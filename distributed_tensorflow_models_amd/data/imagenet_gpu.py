@@ -17,7 +17,7 @@ import ctypes
 import queue
 import random
 import threading
-from concurrent.futures import ThreadPoolExecutor
+from concurrent.futures import CancelledError, ThreadPoolExecutor
 
 import numpy as np
 import torch
@@ -34,17 +34,32 @@ _PARAM_DT = np.dtype([("src_off", "<i8"), ("h", "<i4"), ("w", "<i4"), ("y0", "<i
                       ("contrast", "<f4")])
 
 
-def pack_batch(images, params):
-    """-> (uint8 ragged buffer, structured parameter table) for a list of HxWx3 uint8 images."""
+def _decode_chunk(recs):
+    """Decode worker (thread or spawned process): serialized Examples -> [(HxWx3 uint8, label, bbox)]."""
+    out = []
+    for rec in recs:
+        data, label, bbox, _ = imagenet.parse_example_proto(rec)
+        out.append((imagenet._decode_jpeg(data), label, bbox))
+    return out
+
+
+def param_table(images, params):
+    """-> structured parameter table (src_off from the images' byte sizes), built in one numpy call."""
     offs = np.cumsum([0] + [im.nbytes for im in images])
-    buf = np.empty(int(offs[-1]), np.uint8)
-    tab = np.zeros(len(images), _PARAM_DT)
-    for i, (im, p) in enumerate(zip(images, params)):
-        buf[offs[i]:offs[i + 1]] = np.ascontiguousarray(im, np.uint8).reshape(-1)
-        tab[i]["src_off"] = offs[i]
-        tab[i]["h"], tab[i]["w"] = im.shape[0], im.shape[1]
-        for k in PARAM_FIELDS[3:]:
-            tab[i][k] = p[k]
+    rows = [(int(offs[i]), im.shape[0], im.shape[1]) + tuple(p[k] for k in PARAM_FIELDS[3:])
+            for i, (im, p) in enumerate(zip(images, params))]
+    return np.array(rows, _PARAM_DT), int(offs[-1])
+
+
+def pack_batch(images, params, out=None):
+    """-> (uint8 ragged buffer, structured parameter table) for a list of HxWx3 uint8 images.  ``out``
+    (optional) = a uint8 array of at least the total size to pack into (e.g. a pinned host tensor's
+    numpy view): the copies are plain contiguous numpy copies, which run without the GIL."""
+    tab, total = param_table(images, params)
+    buf = out[:total] if out is not None else np.empty(total, np.uint8)
+    for i, im in enumerate(images):
+        o = int(tab[i]["src_off"])
+        np.copyto(buf[o:o + im.nbytes], np.ascontiguousarray(im, np.uint8).reshape(-1))
     return buf, tab
 
 
@@ -76,7 +91,7 @@ class GPUBatchInputs:
     """Drop-in for ``imagenet.BatchInputs`` producing device batches ([B,S,S,3] bf16, [B] int64)."""
 
     def __init__(self, dataset, batch_size, train=True, image_size=299, num_preprocess_threads=4, num_readers=4,
-                 num_decoders=8, seed=0, device="cuda", shuffle_buffer=1024, prefetch=2):
+                 num_decoders=8, seed=0, device="cuda", shuffle_buffer=1024, prefetch=2, decode_processes=None):
         self.files = dataset.data_files()
         self.B, self.S, self.train = batch_size, image_size, train
         self.device = torch.device(device)
@@ -84,9 +99,23 @@ class GPUBatchInputs:
         self.records = queue.Queue(maxsize=shuffle_buffer)
         self.ready = queue.Queue(maxsize=max(1, prefetch))
         self.stop = threading.Event()
-        self.pool = ThreadPoolExecutor(max_workers=max(1, num_decoders))
+        self.ndec = max(1, num_decoders)
+        # decoders: processes (spawned - never forked from a process holding a HIP context) by default;
+        # a thread pool is GIL-bound in PIL's Python-level JPEG header parsing and the Example parse
+        # (DTM_DECODE_PROCESSES=0 or decode_processes=False selects threads)
+        if decode_processes is None:
+            import os
+            decode_processes = os.environ.get("DTM_DECODE_PROCESSES", "1") != "0" and self.ndec > 1
+        self.chunk = 8 if decode_processes else 1  # records per task (fewer IPC round trips)
+        if decode_processes:
+            import multiprocessing
+            from concurrent.futures import ProcessPoolExecutor
+            self.pool = ProcessPoolExecutor(max_workers=self.ndec, mp_context=multiprocessing.get_context("spawn"))
+        else:
+            self.pool = ThreadPoolExecutor(max_workers=self.ndec)
         self.rng = np.random.RandomState(seed)
         self.slot = 0
+        self.pin = self.device.type == "cuda" and torch.cuda.is_available()
         self.threads = []
         for r in range(num_readers):
             t = threading.Thread(target=self._read, args=(r, num_readers, seed + r), daemon=True)
@@ -106,28 +135,53 @@ class GPUBatchInputs:
                 rng.shuffle(files)
             for f in files:
                 for rec in tf_record_iterator(f):
+                    while not self.stop.is_set():
+                        try:
+                            self.records.put(rec, timeout=0.5)
+                            break
+                        except queue.Full:
+                            continue
                     if self.stop.is_set():
                         return
-                    self.records.put(rec)
             if not self.train:
                 break
 
     @staticmethod
     def _decode(rec):
-        data, label, bbox, _ = imagenet.parse_example_proto(rec)
-        return imagenet._decode_jpeg(data), label, bbox
+        return _decode_chunk([rec])[0]
+
+    def _host_buffer(self, nbytes):
+        """Pinned (device runs) host staging buffer of at least ``nbytes``, as (tensor, numpy view)."""
+        t = torch.empty(max(nbytes, 1), dtype=torch.uint8, pin_memory=self.pin)
+        return t, t.numpy()
 
     def _assemble(self):
+        """Decodes stream through the pool (the next batch's JPEGs decode while this one is packed);
+        this thread only samples the per-image parameters (one RNG, deterministic order), builds the
+        parameter table in one numpy call and copies the pixels straight into a fresh pinned buffer
+        (GIL-free numpy copies) - no per-batch pool barrier, no pin_memory() copy."""
+        from collections import deque
+        pending, done = deque(), deque()
+        depth = (self.B + 2 * self.ndec * self.chunk) // self.chunk + 1  # tasks in flight: a batch + look-ahead
         while not self.stop.is_set():
-            recs = []
-            while len(recs) < self.B and not self.stop.is_set():
+            while len(pending) < depth and not self.stop.is_set():
+                recs = []
+                while len(recs) < self.chunk and not self.stop.is_set():
+                    try:
+                        recs.append(self.records.get(timeout=0.5))
+                    except queue.Empty:
+                        break
+                if not recs:
+                    break
+                pending.append(self.pool.submit(_decode_chunk, recs))
+            while pending and len(done) < self.B:
                 try:
-                    recs.append(self.records.get(timeout=0.5))
-                except queue.Empty:
-                    continue
-            if self.stop.is_set():
-                return
-            dec = list(self.pool.map(self._decode, recs))
+                    done.extend(pending.popleft().result())
+                except CancelledError:  # close() cancelled the queued decodes
+                    return
+            if len(done) < self.B:
+                continue
+            dec = [done.popleft() for _ in range(self.B)]
             imgs, params, labels = [], [], []
             for img, label, bbox in dec:
                 tid = self.slot % self.nthreads  # the reference's per-thread method / colour ordering
@@ -135,10 +189,21 @@ class GPUBatchInputs:
                 params.append(imagenet.sample_params(img.shape[0], img.shape[1], bbox, self.rng, tid, self.train))
                 imgs.append(img)
                 labels.append(label)
-            buf, tab = pack_batch(imgs, params)
-            bt = torch.from_numpy(buf).pin_memory()
-            tt = torch.from_numpy(tab.view(np.uint8)).pin_memory()
-            self.ready.put((bt, tt, torch.tensor(labels, dtype=torch.int64).pin_memory()))
+            tab, total = param_table(imgs, params)
+            bt, view = self._host_buffer(total)
+            for i, im in enumerate(imgs):
+                o = int(tab[i]["src_off"])
+                np.copyto(view[o:o + im.nbytes], im.reshape(-1))
+            tt = torch.from_numpy(tab.view(np.uint8))
+            lab = torch.tensor(labels, dtype=torch.int64)
+            if self.pin:
+                tt, lab = tt.pin_memory(), lab.pin_memory()
+            while not self.stop.is_set():
+                try:
+                    self.ready.put((bt, tt, lab), timeout=0.5)
+                    break
+                except queue.Full:
+                    continue
 
     def next_batch(self):
         bt, tt, lab = self.ready.get()
@@ -148,7 +213,7 @@ class GPUBatchInputs:
 
     def close(self):
         self.stop.set()
-        self.pool.shutdown(wait=False)
+        self.pool.shutdown(wait=False, cancel_futures=True)
 
 
 def distorted_inputs(dataset, batch_size, num_preprocess_threads=4, image_size=299, **kw):

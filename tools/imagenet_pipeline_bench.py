@@ -64,8 +64,9 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t
     bi.close()
-    print("gpu pipeline: %.0f img/s sustained (batch %d, %d decoder threads, %dx%d bf16 out)" % (
-        args.batches * args.batch / dt, args.batch, args.decoders, args.size, args.size), flush=True)
+    print("gpu pipeline: %.0f img/s sustained (batch %d, %d decoder %s, %dx%d bf16 out)" % (
+        args.batches * args.batch / dt, args.batch, args.decoders,
+        "threads" if os.environ.get("DTM_DECODE_PROCESSES") == "0" else "processes", args.size, args.size), flush=True)
     # device-side cost alone: the two kernels on a resident batch
     from distributed_tensorflow_models_amd.data.imagenet_gpu import gpu_preprocess
     rng = np.random.RandomState(0)
