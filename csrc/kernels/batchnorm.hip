@@ -614,6 +614,32 @@ static long rows_per_block_for(long M, int C) {
   return r;
 }
 
+// Backward of stats = [sum y; sum y^2] (per channel): dy = dstats[0] + 2 * y * dstats[1], bf16 out,
+// one pass over y (8 channels per lane; C % 8 == 0).  Replaces five torch elementwise launches
+// (float copy, two muls, add, bf16 copy) over the activation per call (Inception pool branches).
+__global__ __launch_bounds__(256) void bn_stats_bwd_kernel(const bf16_t* __restrict__ y, const float* __restrict__ dstats,
+                                                           bf16_t* __restrict__ dy, long n8, int C8) {
+  const int C = C8 * 8;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % C8) * 8;
+    float f[8];
+    unpack8(((const uint4*)y)[i], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = dstats[c + j] + 2.0f * f[j] * dstats[C + c + j];
+    ((uint4*)dy)[i] = pack8(f);
+  }
+}
+
+DTM_API int dtm_bn_stats_bwd(const void* y, const float* dstats, void* dy, long M, int C, void* stream) {
+  if (C % 8) return -1;
+  const long n8 = M * (C / 8);
+  long blocks = (n8 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(bn_stats_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)y,
+                     dstats, (bf16_t*)dy, n8, C / 8);
+  return 0;
+}
+
 DTM_API void dtm_bn_stats(const void* x, float* stats, long M, int C, void* stream) {
   if (fast_ok(M, C)) {
     int blocks, rpb; fast_grid(M, C, &blocks, &rpb);

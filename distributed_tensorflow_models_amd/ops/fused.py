@@ -734,6 +734,14 @@ class _BNStatsFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dstats):
         (y,) = ctx.saved_tensors
+        C = y.shape[-1]
+        import os
+        if (y.is_cuda and y.dtype == torch.bfloat16 and C % 8 == 0 and y.is_contiguous() and
+                os.environ.get("DTM_STATS_BWD", "1") != "0"):  # (A/B knob: 0 = the torch expression)
+            dy = torch.empty_like(y)
+            _check(_lib.lib().dtm_bn_stats_bwd(_lib.ptr(y), _lib.ptr(dstats.float().contiguous()), _lib.ptr(dy),
+                                               y.numel() // C, C, _lib.stream_ptr()), "dtm_bn_stats_bwd")
+            return dy
         return (dstats[0] + 2.0 * y.float() * dstats[1]).to(y.dtype)
 
 

@@ -3,7 +3,7 @@
 median ms/step per variant; one device, one process: MI355X_MICROARCH 'DVFS give-back' / rule 24).
 
 VARIANTS="base=;noW=wtile:-3;noT=tile:-3;fused=prologue:fused" python tools/ab_step.py
-keys: tile (conv_nt tile id), w8 (0/1: the 8-wave 256x256 conv tile in the shape policy), kwide (0/1: 64-channel tiles for K % 128 <= 64), few (0/1: streaming few-row slab reduction), bnout (0/1: block-output BN backward in the consuming dgrad's epilogue), b1x1 (0/1: one-pass 1x1 conv+BN backward), stemw (0/1: stem BN backward in the wgrad operand staging), sact (0/1: streaming 1x1 kernel for act dgrads), pcom (0/1: Inception pool branches as conv -> pool -> BN), catm (0/1: one-launch multi-part concat BN-apply), dec (0/1: stride-decomposed strided dgrads), k32 (0/1: 256x32 tile for <=32-channel spatial convs), cpt (16-B chunks per thread of the BN-stream grids), s128 (0/1: streaming kernel for 128-deep act dgrads), pol2 (0/1: v2 conv tile-policy rules), fin (0/1: BN finalize hand-off in the conv statistics epilogue), defr (0/1: deferred batched weight-gradient slab reductions), side (0/1: weight-gradient slab reductions on the side stream), pre (0/1: early dgrad-epilogue side-input loads), wn256 (0/1: 256-column wgrad tiles for K <= 64), atile (tile id of the dgrads with a fused
+keys: tile (conv_nt tile id), w8 (0/1: the 8-wave 256x256 conv tile in the shape policy), kwide (0/1: 64-channel tiles for K % 128 <= 64), few (0/1: streaming few-row slab reduction), bnout (0/1: block-output BN backward in the consuming dgrad's epilogue), b1x1 (0/1: one-pass 1x1 conv+BN backward), stemw (0/1: stem BN backward in the wgrad operand staging), sact (0/1: streaming 1x1 kernel for act dgrads), pcom (0/1: Inception pool branches as conv -> pool -> BN), sbwd (0/1: HIP backward of the pooled-BN statistics), catm (0/1: one-launch multi-part concat BN-apply), dec (0/1: stride-decomposed strided dgrads), k32 (0/1: 256x32 tile for <=32-channel spatial convs), cpt (16-B chunks per thread of the BN-stream grids), s128 (0/1: streaming kernel for 128-deep act dgrads), pol2 (0/1: v2 conv tile-policy rules), fin (0/1: BN finalize hand-off in the conv statistics epilogue), defr (0/1: deferred batched weight-gradient slab reductions), side (0/1: weight-gradient slab reductions on the side stream), pre (0/1: early dgrad-epilogue side-input loads), wn256 (0/1: 256-column wgrad tiles for K <= 64), atile (tile id of the dgrads with a fused
 activation-backward epilogue, -1 = policy), wtile[:occ] (wgrad tile id / blocks-per-CU target), prologue (DTM_PROLOGUE),
 stem (DTM_STEM: 1 = packed-row stem path), red (target_blocks:max_chunks[:direct_max] of the
 partial-sum reductions; 0 = legacy 256 rows per block; direct_max = largest BN-backward grid that
@@ -55,6 +55,7 @@ def apply(cfg):
     os.environ["DTM_DGRAD_DEC"] = cfg.get("dec", "1")
     os.environ["DTM_CAT_MULTI"] = cfg.get("catm", "1")
     os.environ["DTM_POOL_COMMUTE"] = cfg.get("pcom", "1")
+    os.environ["DTM_STATS_BWD"] = cfg.get("sbwd", "1")
 
 
 def main():

@@ -19,6 +19,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="inception_v3_slim_old")
     ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--dispatch", action="store_true",
+                    help="attribute ops with a TorchDispatchMode + Python traceback (works in custom backward)")
     args = ap.parse_args()
     import torch
     from torch.profiler import ProfilerActivity, profile
@@ -40,6 +42,8 @@ def main():
     for _ in range(3):
         step(x, y)
     torch.cuda.synchronize()
+    if args.dispatch:
+        return dispatch_sites(step, x, y)
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
         step(x, y)
         torch.cuda.synchronize()
@@ -68,6 +72,40 @@ def main():
     for key, n in sorted(sites.items(), key=lambda kv: -dev_us[kv[0]]):
         print("%-28s %5d %9.1f  %s" % (key[0], n, dev_us[key], key[1]))
     print("total aten device us/step: %.1f" % sum(dev_us.values()))
+
+
+def dispatch_sites(step, x, y):
+    """Every aten op of one step whose outputs live on the GPU, keyed by the innermost package frame."""
+    import traceback
+
+    import torch
+    from torch.utils._python_dispatch import TorchDispatchMode
+    skip = ("aten::empty", "aten::view", "aten::_to_copy", "aten::as_strided", "aten::detach", "aten::alias",
+            "aten::_unsafe_view", "aten::t", "aten::reshape", "aten::slice", "aten::select", "aten::expand",
+            "aten::permute", "aten::unsqueeze", "aten::squeeze", "aten::empty_strided", "aten::lift_fresh",
+            "aten::set_", "aten::resize_", "aten::split", "aten::is_same_size")
+    pkg = "distributed_tensorflow_models_amd"
+    sites = Counter()
+
+    class Mode(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            out = func(*args, **(kwargs or {}))
+            name = "aten::" + func.__name__.split(".")[0]
+            if name not in skip:
+                outs = out if isinstance(out, (tuple, list)) else [out]
+                if any(isinstance(o, torch.Tensor) and o.is_cuda for o in outs):
+                    fr = [f for f in traceback.extract_stack()[:-1] if pkg in f.filename or "bench" in f.filename]
+                    site = ("%s:%d %s" % (fr[-1].filename.split(pkg + "/")[-1], fr[-1].lineno, fr[-1].name)
+                            if fr else "(autograd engine)")
+                    sites[(func.__name__, site)] += 1
+            return out
+
+    with Mode():
+        step(x, y)
+    torch.cuda.synchronize()
+    print("%-34s %5s  %s" % ("aten op", "calls", "innermost package frame"))
+    for (op, site), n in sorted(sites.items(), key=lambda kv: -kv[1]):
+        print("%-34s %5d  %s" % (op, n, site))
 
 
 if __name__ == "__main__":
