@@ -614,11 +614,11 @@ static long rows_per_block_for(long M, int C) {
   return r;
 }
 
-// Backward of stats = [sum y; sum y^2] (per channel): dy = dstats[0] + 2 * y * dstats[1], bf16 out,
+// Backward of stats = [sum y; sum y^2] (per channel): dy = [g +] dstats[0] + 2 * y * dstats[1], bf16 out,
 // one pass over y (8 channels per lane; C % 8 == 0).  Replaces five torch elementwise launches
 // (float copy, two muls, add, bf16 copy) over the activation per call (Inception pool branches).
 __global__ __launch_bounds__(256) void bn_stats_bwd_kernel(const bf16_t* __restrict__ y, const float* __restrict__ dstats,
-                                                           bf16_t* __restrict__ dy, long n8, int C8) {
+                                                           const bf16_t* g, bf16_t* dy, long n8, int C8) {
   const int C = C8 * 8;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
     const int c = (int)(i % C8) * 8;
@@ -626,17 +626,23 @@ __global__ __launch_bounds__(256) void bn_stats_bwd_kernel(const bf16_t* __restr
     unpack8(((const uint4*)y)[i], f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = dstats[c + j] + 2.0f * f[j] * dstats[C + c + j];
+    if (g) {  // the tensor's other gradient (may alias dy: each lane reads its chunk before writing it)
+      float h[8];
+      unpack8(((const uint4*)g)[i], h);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += h[j];
+    }
     ((uint4*)dy)[i] = pack8(f);
   }
 }
 
-DTM_API int dtm_bn_stats_bwd(const void* y, const float* dstats, void* dy, long M, int C, void* stream) {
+DTM_API int dtm_bn_stats_bwd(const void* y, const float* dstats, const void* g, void* dy, long M, int C, void* stream) {
   if (C % 8) return -1;
   const long n8 = M * (C / 8);
   long blocks = (n8 + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(bn_stats_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)y,
-                     dstats, (bf16_t*)dy, n8, C / 8);
+                     dstats, (const bf16_t*)g, (bf16_t*)dy, n8, C / 8);
   return 0;
 }
 

@@ -721,7 +721,9 @@ def conv_bn(x, w, bn, stride, padding, training, relu):
 
 
 class _BNStatsFn(torch.autograd.Function):
-    """stats = [sum y; sum y^2] per channel (HIP reduction); backward: dy = dsum + 2*y*dsumsq."""
+    """stats = [sum y; sum y^2] per channel (HIP reduction), returned with an alias of y that the
+    consumers use instead of y: backward then receives both of y's gradients at once and forms
+    dy = d(alias) + dsum + 2*y*dsumsq in one HIP pass (no separate autograd accumulation launch)."""
 
     @staticmethod
     def forward(ctx, y):
@@ -729,20 +731,27 @@ class _BNStatsFn(torch.autograd.Function):
         stats = torch.zeros((2, C), device=y.device, dtype=torch.float32)
         _lib.lib().dtm_bn_stats(_lib.ptr(y), _lib.ptr(stats), y.numel() // C, C, _lib.stream_ptr())
         ctx.save_for_backward(y)
-        return stats
+        return stats, y.view_as(y)
 
     @staticmethod
-    def backward(ctx, dstats):
+    def backward(ctx, dstats, dalias):
         (y,) = ctx.saved_tensors
         C = y.shape[-1]
+        if dstats is None:
+            return dalias
         import os
         if (y.is_cuda and y.dtype == torch.bfloat16 and C % 8 == 0 and y.is_contiguous() and
                 os.environ.get("DTM_STATS_BWD", "1") != "0"):  # (A/B knob: 0 = the torch expression)
-            dy = torch.empty_like(y)
-            _check(_lib.lib().dtm_bn_stats_bwd(_lib.ptr(y), _lib.ptr(dstats.float().contiguous()), _lib.ptr(dy),
+            g = None
+            if dalias is not None:
+                g = dalias.to(torch.bfloat16).contiguous()
+            dy = torch.empty_like(y) if g is None or g.data_ptr() == y.data_ptr() else g  # in place into g
+            _check(_lib.lib().dtm_bn_stats_bwd(_lib.ptr(y), _lib.ptr(dstats.float().contiguous()),
+                                               _lib.ptr(g) if g is not None else None, _lib.ptr(dy),
                                                y.numel() // C, C, _lib.stream_ptr()), "dtm_bn_stats_bwd")
             return dy
-        return (dstats[0] + 2.0 * y.float() * dstats[1]).to(y.dtype)
+        dy = (dstats[0] + 2.0 * y.float() * dstats[1]).to(y.dtype)
+        return dy if dalias is None else dy + dalias
 
 
 def pool_commute_enabled():
@@ -766,7 +775,7 @@ def conv_avgpool_bn(x, w, bn, training, relu=True):
     z = _ConvBNFn.apply(xb, None, w, None, None, g, None, slot)
     y = avg_pool(z, 3, 1, "SAME")
     if training:
-        stats = _BNStatsFn.apply(y)
+        stats, y = _BNStatsFn.apply(y)  # (y: the alias whose gradient the statistics backward folds in)
         ss = _BNFinalizeFn.apply(stats, bn.gamma, bn.beta, bn.moving_mean, bn.moving_variance,
                                  float(y.numel() // y.shape[-1]), float(bn.eps), float(bn.decay), bool(bn.bessel), True)
     else:
