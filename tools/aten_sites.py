@@ -80,7 +80,7 @@ def dispatch_sites(step, x, y):
 
     import torch
     from torch.utils._python_dispatch import TorchDispatchMode
-    skip = ("aten::empty", "aten::view", "aten::_to_copy", "aten::as_strided", "aten::detach", "aten::alias",
+    skip = ("aten::empty", "aten::view", "aten::as_strided", "aten::detach", "aten::alias",
             "aten::_unsafe_view", "aten::t", "aten::reshape", "aten::slice", "aten::select", "aten::expand",
             "aten::permute", "aten::unsqueeze", "aten::squeeze", "aten::empty_strided", "aten::lift_fresh",
             "aten::set_", "aten::resize_", "aten::split", "aten::is_same_size")
