@@ -95,9 +95,10 @@ def main():
     from distributed_tensorflow_models_amd.models import nets_factory
 
     if args.graph < 0:
-        # measured on one MI355X: LeNet 396k -> 875k img/s with the captured step; ResNet-50 and
-        # VGG-16 are GPU-bound (same ms/step either way), so they stay eager
-        args.graph = int(args.model == "lenet" and world == 1 and not cpu)
+        # measured on one MI355X (profiles/ab/r2_ab_graph_bench.log): LeNet 396k -> 875k img/s with the
+        # captured step, Inception-v3 +0.5 % (885 launches per step), VGG-16 +0.2 %; ResNet-50 is
+        # GPU-bound (+0.1 %, within noise) and stays eager
+        args.graph = int(args.model in ("lenet", "inception_v3_slim_old", "vgg_16") and world == 1 and not cpu)
     torch.manual_seed(1234)  # identical replicas: every rank builds the same initial weights
     S0, ncls, B0, opt, extra = PRESETS[args.model]
     S = args.image_size or S0
