@@ -34,12 +34,17 @@ _PARAM_DT = np.dtype([("src_off", "<i8"), ("h", "<i4"), ("w", "<i4"), ("y0", "<i
                       ("contrast", "<f4")])
 
 
-def _decode_chunk(recs):
-    """Decode worker (thread or spawned process): serialized Examples -> [(HxWx3 uint8, label, bbox)]."""
+def _decode_chunk(tasks):
+    """Decode worker (thread or spawned process): [(serialized Example, thread id, seed, train)] ->
+    [(HxWx3 uint8, label, preprocessing parameters)].  The parameters are drawn here, from a per-image
+    seed the assembler assigned in submission order, so the stream is reproducible for a given seed
+    and the assembler thread does no per-image sampling."""
     out = []
-    for rec in recs:
+    for rec, tid, seed, train in tasks:
         data, label, bbox, _ = imagenet.parse_example_proto(rec)
-        out.append((imagenet._decode_jpeg(data), label, bbox))
+        img = imagenet._decode_jpeg(data)
+        p = imagenet.sample_params(img.shape[0], img.shape[1], bbox, np.random.RandomState(seed), tid, train)
+        out.append((img, label, p))
     return out
 
 
@@ -148,7 +153,8 @@ class GPUBatchInputs:
 
     @staticmethod
     def _decode(rec):
-        return _decode_chunk([rec])[0]
+        img, label, _p = _decode_chunk([(rec, 0, 0, False)])[0]
+        return img, label
 
     def _host_buffer(self, nbytes):
         """Pinned (device runs) host staging buffer of at least ``nbytes``, as (tensor, numpy view)."""
@@ -165,15 +171,18 @@ class GPUBatchInputs:
         depth = (self.B + 2 * self.ndec * self.chunk) // self.chunk + 1  # tasks in flight: a batch + look-ahead
         while not self.stop.is_set():
             while len(pending) < depth and not self.stop.is_set():
-                recs = []
-                while len(recs) < self.chunk and not self.stop.is_set():
+                tasks = []
+                while len(tasks) < self.chunk and not self.stop.is_set():
                     try:
-                        recs.append(self.records.get(timeout=0.5))
+                        rec = self.records.get(timeout=0.5)
                     except queue.Empty:
                         break
-                if not recs:
+                    # the reference's per-thread resize method / colour ordering: thread id = slot % threads
+                    tasks.append((rec, self.slot % self.nthreads, int(self.rng.randint(2 ** 31 - 1)), self.train))
+                    self.slot += 1
+                if not tasks:
                     break
-                pending.append(self.pool.submit(_decode_chunk, recs))
+                pending.append(self.pool.submit(_decode_chunk, tasks))
             while pending and len(done) < self.B:
                 try:
                     done.extend(pending.popleft().result())
@@ -182,13 +191,9 @@ class GPUBatchInputs:
             if len(done) < self.B:
                 continue
             dec = [done.popleft() for _ in range(self.B)]
-            imgs, params, labels = [], [], []
-            for img, label, bbox in dec:
-                tid = self.slot % self.nthreads  # the reference's per-thread method / colour ordering
-                self.slot += 1
-                params.append(imagenet.sample_params(img.shape[0], img.shape[1], bbox, self.rng, tid, self.train))
-                imgs.append(img)
-                labels.append(label)
+            imgs = [d[0] for d in dec]
+            labels = [d[1] for d in dec]
+            params = [d[2] for d in dec]
             tab, total = param_table(imgs, params)
             bt, view = self._host_buffer(total)
             for i, im in enumerate(imgs):

@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--size", type=int, default=299)
     ap.add_argument("--decoders", type=int, default=16)
     ap.add_argument("--batches", type=int, default=12)
+    ap.add_argument("--warm-batches", type=int, default=4)
     ap.add_argument("--host", action="store_true", help="also time the host (numpy) pipeline")
     args = ap.parse_args()
     import torch
@@ -56,7 +57,8 @@ def main():
     ds = imagenet.ImagenetData("train", d)
     bi = imagenet_gpu.distorted_inputs(ds, args.batch, num_preprocess_threads=4, image_size=args.size,
                                        num_readers=4, num_decoders=args.decoders)
-    x, _ = bi.next_batch()  # warm-up (first batch includes thread start-up)
+    for _ in range(args.warm_batches):  # warm-up (decoder start-up: spawned processes import the package)
+        x, _ = bi.next_batch()
     torch.cuda.synchronize()
     t = time.perf_counter()
     for _ in range(args.batches):
