@@ -189,3 +189,45 @@ def test_imagenet_oracle_tf_semantics():
     v = imagenet.resize(img.astype(np.float32) / 255.0, 16, "bilinear").astype(np.float64) + 0.05
     v = imagenet.adjust_hue(imagenet.adjust_saturation(imagenet.adjust_contrast(v, 0.7), 1.3), 0.1)
     np.testing.assert_allclose(got, ((np.clip(v, 0, 1) - 0.5) * 2).astype(np.float32), atol=1e-6)
+
+
+def _assembled(ds, procs, decoders, nbatch=2):
+    from distributed_tensorflow_models_amd.data import imagenet_gpu
+    bi = imagenet_gpu.GPUBatchInputs(ds, 4, train=True, image_size=32, num_readers=1, num_decoders=decoders, seed=7,
+                                     device="cpu", decode_processes=procs, shuffle_buffer=64)
+    try:
+        out = [bi.ready.get(timeout=120) for _ in range(nbatch)]
+    finally:
+        bi.close()
+    return out
+
+
+def test_gpu_pipeline_assembler_host_side(tmp_path):
+    """Host side of data/imagenet_gpu.py (no GPU needed): decoder processes and threads give the same
+    packed pixels, labels and per-image parameters for a fixed seed (parameters are drawn in the
+    workers from per-image seeds assigned in submission order), and the table's offsets tile the
+    ragged pixel buffer."""
+    from PIL import Image
+
+    from distributed_tensorflow_models_amd.data import imagenet_gpu
+    out = tmp_path / "d"
+    out.mkdir()
+    rng = np.random.RandomState(0)
+    with TFRecordWriter(str(out / "train-00000-of-00001")) as w:
+        for i in range(12):
+            b = io.BytesIO()
+            Image.fromarray((rng.rand(20 + i, 30, 3) * 255).astype(np.uint8)).save(b, format="JPEG")
+            w.write(encode_example({"image/encoded": b.getvalue(), "image/class/label": i + 1,
+                                    "image/object/bbox/xmin": [0.1], "image/object/bbox/ymin": [0.1],
+                                    "image/object/bbox/xmax": [0.9], "image/object/bbox/ymax": [0.9]}))
+    ds = imagenet.ImagenetData("train", str(out))
+    a = _assembled(ds, True, 2)
+    b = _assembled(ds, False, 3)
+    for (bt, tt, lab), (bt2, tt2, lab2) in zip(a, b):
+        tab = tt.numpy().view(imagenet_gpu._PARAM_DT)
+        assert torch.equal(lab, lab2) and torch.equal(tt, tt2)
+        total = int(tab["src_off"][-1] + tab["h"][-1] * tab["w"][-1] * 3)
+        assert torch.equal(bt[:total], bt2[:total])
+        assert list(tab["src_off"][1:]) == list(np.cumsum(tab["h"] * tab["w"] * 3)[:-1])
+        assert (tab["y0"] + tab["ch"] <= tab["h"]).all() and (tab["x0"] + tab["cw"] <= tab["w"]).all()
+        assert list(tab["method"]) == [0, 1, 2, 3] and set(lab.tolist()) <= set(range(1, 13))
