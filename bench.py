@@ -99,6 +99,10 @@ def main():
         # captured step, Inception-v3 +0.5 % (885 launches per step), VGG-16 +0.2 %; ResNet-50 is
         # GPU-bound (+0.1 %, within noise) and stays eager
         args.graph = int(args.model in ("lenet", "inception_v3_slim_old", "vgg_16") and world == 1 and not cpu)
+    if args.graph and world > 1:
+        print("bench.py: --graph 1 is single-rank only (hipGraph capture of RCCL collectives is not "
+              "supported here); use --graph 0 or -1 with --gpus %d" % world, file=sys.stderr, flush=True)
+        sys.exit(2)
     torch.manual_seed(1234)  # identical replicas: every rank builds the same initial weights
     S0, ncls, B0, opt, extra = PRESETS[args.model]
     S = args.image_size or S0

@@ -261,6 +261,19 @@ def image_preprocessing(record, train, size, rng, thread_id=0):
     return x, label  # [-1, 1]
 
 
+class _PipelineError:
+    """Sentinel a pipeline thread queues when it dies; next_batch re-raises it (no silent hang)."""
+
+    def __init__(self, msg):
+        self.msg = msg
+
+
+def _log_bad_record(e, n):
+    import logging
+    if n <= 10 or n % 1000 == 0:
+        logging.getLogger(__name__).warning("skipping undecodable ImageNet record (%d so far): %r", n, e)
+
+
 class BatchInputs:
     """num_readers x num_preprocess_threads pipeline producing (images [B,S,S,3], labels [B])."""
 
@@ -271,6 +284,7 @@ class BatchInputs:
         self.records = queue.Queue(maxsize=shuffle_buffer)
         self.examples = queue.Queue(maxsize=batch_size * queue_batches)
         self.stop = threading.Event()
+        self.bad_records = 0
         self.threads = []
         for r in range(num_readers):
             t = threading.Thread(target=self._read, args=(r, num_readers, seed + r), daemon=True)
@@ -288,12 +302,16 @@ class BatchInputs:
             if self.train:
                 rng.shuffle(files)
             for f in files:
-                for rec in tf_record_iterator(f):
-                    if self.stop.is_set():
-                        return
-                    self.records.put(rec)
-            if not self.train:
-                break
+                try:
+                    for rec in tf_record_iterator(f):
+                        if self.stop.is_set():
+                            return
+                        self.records.put(rec)
+                except Exception as e:  # unreadable / corrupt record file: surface it in next_batch
+                    self.examples.put(_PipelineError("reading %s: %r" % (f, e)))
+                    return
+            # train AND eval loop over the files forever, as string_input_producer without num_epochs
+            # does (reference image_processing.py:444-452): repeated eval_once calls never starve
 
     def _prep(self, tid, seed):
         rng = np.random.RandomState(seed)
@@ -302,10 +320,22 @@ class BatchInputs:
                 rec = self.records.get(timeout=0.5)
             except queue.Empty:
                 continue
-            self.examples.put(image_preprocessing(rec, self.train, self.S, rng, tid))
+            try:
+                ex = image_preprocessing(rec, self.train, self.S, rng, tid)
+            except Exception as e:  # one undecodable record is skipped (and counted), not fatal
+                self.bad_records += 1
+                _log_bad_record(e, self.bad_records)
+                continue
+            self.examples.put(ex)
 
     def next_batch(self):
-        xs, ys = zip(*[self.examples.get() for _ in range(self.B)])
+        got = []
+        while len(got) < self.B:
+            ex = self.examples.get()
+            if isinstance(ex, _PipelineError):
+                raise RuntimeError("ImageNet input pipeline failed: %s" % ex.msg)
+            got.append(ex)
+        xs, ys = zip(*got)
         x = torch.from_numpy(np.stack(xs))
         y = torch.tensor(ys, dtype=torch.int64)
         if self.device.type == "cuda":

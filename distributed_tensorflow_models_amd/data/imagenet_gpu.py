@@ -41,9 +41,13 @@ def _decode_chunk(tasks):
     and the assembler thread does no per-image sampling."""
     out = []
     for rec, tid, seed, train in tasks:
-        data, label, bbox, _ = imagenet.parse_example_proto(rec)
-        img = imagenet._decode_jpeg(data)
-        p = imagenet.sample_params(img.shape[0], img.shape[1], bbox, np.random.RandomState(seed), tid, train)
+        try:
+            data, label, bbox, _ = imagenet.parse_example_proto(rec)
+            img = imagenet._decode_jpeg(data)
+            p = imagenet.sample_params(img.shape[0], img.shape[1], bbox, np.random.RandomState(seed), tid, train)
+        except Exception as e:  # corrupt / undecodable record: skipped (and counted) by the assembler
+            out.append((None, repr(e), None))
+            continue
         out.append((img, label, p))
     return out
 
@@ -104,6 +108,7 @@ class GPUBatchInputs:
         self.records = queue.Queue(maxsize=shuffle_buffer)
         self.ready = queue.Queue(maxsize=max(1, prefetch))
         self.stop = threading.Event()
+        self.bad_records = 0
         self.ndec = max(1, num_decoders)
         # decoders: processes (spawned - never forked from a process holding a HIP context) by default;
         # a thread pool is GIL-bound in PIL's Python-level JPEG header parsing and the Example parse
@@ -139,17 +144,21 @@ class GPUBatchInputs:
             if self.train:
                 rng.shuffle(files)
             for f in files:
-                for rec in tf_record_iterator(f):
-                    while not self.stop.is_set():
-                        try:
-                            self.records.put(rec, timeout=0.5)
-                            break
-                        except queue.Full:
-                            continue
-                    if self.stop.is_set():
-                        return
-            if not self.train:
-                break
+                try:
+                    for rec in tf_record_iterator(f):
+                        while not self.stop.is_set():
+                            try:
+                                self.records.put(rec, timeout=0.5)
+                                break
+                            except queue.Full:
+                                continue
+                        if self.stop.is_set():
+                            return
+                except Exception as e:  # unreadable record file: next_batch raises it
+                    self._fail("reading %s: %r" % (f, e))
+                    return
+            # eval loops too (string_input_producer without num_epochs, reference
+            # image_processing.py:444-452): repeated eval_once calls on one pipeline never starve
 
     @staticmethod
     def _decode(rec):
@@ -185,8 +194,16 @@ class GPUBatchInputs:
                 pending.append(self.pool.submit(_decode_chunk, tasks))
             while pending and len(done) < self.B:
                 try:
-                    done.extend(pending.popleft().result())
+                    for d in pending.popleft().result():
+                        if d[0] is None:
+                            self.bad_records += 1
+                            imagenet._log_bad_record(d[1], self.bad_records)
+                        else:
+                            done.append(d)
                 except CancelledError:  # close() cancelled the queued decodes
+                    return
+                except Exception as e:  # e.g. BrokenProcessPool: a decoder process died
+                    self._fail("decoder: %r" % (e,))
                     return
             if len(done) < self.B:
                 continue
@@ -210,8 +227,21 @@ class GPUBatchInputs:
                 except queue.Full:
                     continue
 
+    def _fail(self, msg):
+        """A pipeline thread died: hand the error to the consumer (no silent hang in next_batch)."""
+        while not self.stop.is_set():
+            try:
+                self.ready.put(imagenet._PipelineError(msg), timeout=0.5)
+                return
+            except queue.Full:
+                continue
+
     def next_batch(self):
-        bt, tt, lab = self.ready.get()
+        item = self.ready.get()
+        if isinstance(item, imagenet._PipelineError):
+            self.ready.put(item)  # every later call fails the same way
+            raise RuntimeError("ImageNet input pipeline failed: %s" % item.msg)
+        bt, tt, lab = item
         x, self._stage = _launch(bt, tt, self.B, self.S, self.device, torch.bfloat16, self._stage)
         self.images_done += self.B
         return x, lab.to(self.device, non_blocking=True)

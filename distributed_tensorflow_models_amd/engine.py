@@ -11,7 +11,7 @@ from .ops import elementwise as _elementwise
 from .ops import fused as _fused
 from .ops import nn as F
 from .ops.optim import FusedOptimizer
-from .parallel.bsp import BSPDataParallel
+from .parallel.bsp import BSPDataParallel, BufferSync
 from .utils.profiler import range_pop, range_push, roctx
 
 
@@ -33,13 +33,24 @@ class TrainStep:
     def __init__(self, model, optimizer="momentum", lr=0.1, momentum=0.9, rho=0.9, epsilon=1e-10, bucket_mb=32.0,
                  label_smoothing=0.0, aux_weight=0.4, ema_decay=None, lr_schedule=None, use_graph=False,
                  process_group=None, weight_decay=None, batch_weight=1.0, nan_guard=True, timer=None,
-                 grad_comm_dtype=None):
+                 grad_comm_dtype=None, ema_buffers=True, bn_sync_every=1):
         self.model = model
         prepare_compute_copies(model)
         params = [p for p in model.parameters() if p.requires_grad]
         self.dp = BSPDataParallel(params, bucket_mb, process_group, comm_dtype=grad_comm_dtype)
+        if use_graph and self.dp.world > 1:
+            # a captured step would hold the bucket collectives (and their waits) inside the graph;
+            # RCCL-in-hipGraph has never been validated here, so multi-rank runs stay eager
+            raise ValueError("use_graph (hipGraph step capture) is single-rank only; world size is %d"
+                             % self.dp.world)
+        # BN moving statistics: one flat buffer, averaged over the replicas every step (reference
+        # keeps ONE PS-resident copy that every worker updates); must precede the optimizer tables
+        self.bufsync = BufferSync(moving_average_buffers(model), process_group, every=bn_sync_every)
+        # ema_buffers: whether the statistics also get EMA shadows (slim BN lists them in
+        # moving_average_variables(); tf.layers BN - the CIFAR ResNet preset - does not)
         self.opt = FusedOptimizer(params, optimizer, lr, momentum, rho, epsilon, ema_decay, weight_decay,
-                                  ema_buffers=moving_average_buffers(model) if ema_decay is not None else ())
+                                  ema_buffers=moving_average_buffers(model)
+                                  if (ema_decay is not None and ema_buffers) else ())
         self.lr = lr
         self.lr_schedule = lr_schedule
         self.smoothing = label_smoothing
@@ -53,6 +64,8 @@ class TrainStep:
         self.timer = timer      # utils.metrics.StepTimer for fwd/bwd/allreduce/optimizer HIP-event sections
         self._graph = None
         self._eager_steps = 0
+        self._skip_total = None  # device int32: number of skipped (non-finite) steps so far
+        self._skip_seen = 0
 
     def loss_fn(self, out, labels):
         aux = None
@@ -86,6 +99,7 @@ class TrainStep:
             with roctx("loss"):
                 loss = self.loss_fn(out, labels)
             self._mark("fwd")
+            self.bufsync.issue()  # forward has finished every moving-statistics update
             with roctx("backward"):  # bucket all-reduces are issued (own ranges) from the grad hooks
                 loss.backward()
             if images.is_cuda:
@@ -95,6 +109,7 @@ class TrainStep:
             _fused.arena.end_step()
         with roctx("allreduce_wait"):
             self.dp.finish()
+            self.bufsync.finish()
         self._mark("allreduce")
         skip = None
         if self.nan_guard:
@@ -108,6 +123,9 @@ class TrainStep:
             else:
                 skip = torch.tensor([0 if bool(torch.isfinite(flat).all()) else 1], dtype=torch.int32)
             self.last_skip = skip
+            if self._skip_total is None:
+                self._skip_total = torch.zeros(1, device=flat.device, dtype=torch.int32)
+            self._skip_total.add_(skip)  # sticky device count: read on log steps only, no per-step sync
         return loss.detach(), skip
 
     def __call__(self, images, labels):
@@ -168,8 +186,12 @@ class TrainStep:
         return self._static_loss.clone()
 
     def poll_skipped(self):
-        """Host-side check of the last step's guard (one small sync; call when logging)."""
-        if self.last_skip is not None and int(self.last_skip.item()) != 0:
-            self.skipped += 1
-            return True
-        return False
+        """Host-side check (one small sync; call on log steps): True if any step since the last poll
+        had non-finite gradients and skipped its update.  ``self.skipped`` = total so far."""
+        if self._skip_total is None:
+            return False
+        n = int(self._skip_total.item())
+        new = n - self._skip_seen
+        self._skip_seen = n
+        self.skipped = n
+        return new > 0

@@ -275,7 +275,7 @@ def tf_variables(module):
         for pname, p in m.named_parameters(recurse=False):
             if p is None:
                 continue
-            out.append((p.tf_name, p, getattr(p, "tf_layout", None), p.requires_grad))
+            out.append((getattr(p, "tf_name", pname), p, getattr(p, "tf_layout", None), p.requires_grad))
         names = getattr(m, "tf_buffer_names", None)
         if names:
             for b, n in names.items():

@@ -745,7 +745,11 @@ class _BNStatsFn(torch.autograd.Function):
             g = None
             if dalias is not None:
                 g = dalias.to(torch.bfloat16).contiguous()
-            dy = torch.empty_like(y) if g is None or g.data_ptr() == y.data_ptr() else g  # in place into g
+            # write dy into g only when nobody else can see g: a copy made just above, or a gradient its
+            # producer marked private (the concat BN-apply backward's fresh dx).  A gradient autograd
+            # shares between several inputs (or a view of a shared one) gets a fresh dy instead.
+            private = g is not None and (g is not dalias or getattr(dalias, "_dtm_private_grad", False))
+            dy = g if (private and g.data_ptr() != y.data_ptr()) else torch.empty_like(y)
             _check(_lib.lib().dtm_bn_stats_bwd(_lib.ptr(y), _lib.ptr(dstats.float().contiguous()),
                                                _lib.ptr(g) if g is not None else None, _lib.ptr(dy),
                                                y.numel() // C, C, _lib.stream_ptr()), "dtm_bn_stats_bwd")
@@ -873,6 +877,7 @@ class _ConcatBNApplyFn(torch.autograd.Function):
                     raw, ss, mask = saved[j:j + 3]
                     j += 3
                     dx = torch.empty_like(raw)
+                    dx._dtm_private_grad = True  # fresh, single-owner: _BNStatsFn may write into it
                     parts.append((raw, ss, mask, dx, m[1], int(m[3])))
                     grads += [dx, sums[4 * off:4 * (off + m[1])].view(4, m[1])]
                 else:
@@ -890,6 +895,7 @@ class _ConcatBNApplyFn(torch.autograd.Function):
                 raw, ss, mask = saved[j:j + 3]
                 j += 3
                 dx = torch.empty_like(raw)
+                dx._dtm_private_grad = True
                 sx = arena.zeros((4, C), raw.device)
                 _check(L.dtm_bn_apply_bwd_ld(ctypes.c_void_p(dout.data_ptr() + 2 * off), _lib.ptr(mask), _lib.ptr(raw),
                                              _lib.ptr(ss), _lib.ptr(dx), _lib.ptr(sx), M, C, int(m[3]), Ct, s),

@@ -37,8 +37,17 @@ def owner_map(params, world):
 
 class ParamStore:
     def __init__(self, params, optimizer="sgd", lr=0.01, momentum=0.9, rho=0.9, epsilon=1e-10, mode=None,
-                 store=None, run_id="0", weight_decays=None):
+                 store=None, run_id="0", weight_decays=None, buffers=()):
         self.params = [p for p in params if p.requires_grad]
+        # non-trainable state every worker's forward updates in place (BN moving statistics): in the
+        # reference they are PS variables too, written by each worker's AssignMovingAvg ops
+        # (inception/imagenet_inception_asp.py:119-145 runs the UPDATE_OPS with the train op).  They
+        # live in one flat region of owner 0's shard; a worker pulls them with the parameters and
+        # pushes the delta its forward made (shared += local - pulled), Hogwild-style.
+        from .bsp import flatten_tensors
+        self.buffers = [b for b in buffers]
+        self._buf_local = flatten_tensors(self.buffers) if self.buffers else None
+        self._buf_snap = self._buf_local.clone() if self._buf_local is not None else None
         self.rank, self.world = pg.rank(), pg.world_size()
         self.owner = owner_map(self.params, self.world)
         self.kind, self.lr, self.mu, self.rho, self.eps = optimizer, lr, momentum, rho, epsilon
@@ -48,6 +57,8 @@ class ParamStore:
         self.run_id = run_id
         gpu = self.params[0].is_cuda
         self.mode = mode or ("ipc" if gpu else "shm")
+        if self.mode == "ipc" and self.world > 1:
+            self.mode = self._negotiate_ipc()
         self.shards = {}   # param index -> dict(param=..., s1=..., s2=...) views into owner memory
         self._build()
 
@@ -66,8 +77,10 @@ class ParamStore:
                 off += self.params[i].numel()
             per_owner[k] = (idxs, off)
         self.flat = {}
+        nbuf = self._buf_local.numel() if self._buf_local is not None else 0
+        self._nslot = {k: n for k, (idxs, n) in per_owner.items()}
         for k, (idxs, n) in per_owner.items():
-            total = n * (1 + nslots)
+            total = n * (1 + nslots) + (nbuf if k == 0 else 0)
             self.flat[k] = self._open_flat(k, total, init_from=(idxs, n) if k == self.rank or self.mode == "shm"
                                            else None)
         if self.mode == "shm" and self.rank == 0:
@@ -83,7 +96,39 @@ class ParamStore:
             if nslots >= 2:
                 sh["s2"] = buf[2 * n_owner + off:2 * n_owner + off + p.numel()].view(p.shape)
             self.shards[i] = sh
+        if nbuf:
+            base = self._nslot[0] * (1 + nslots)
+            self.buf_shard = self.flat[0][base:base + nbuf]
 
+    def _negotiate_ipc(self):
+        """Owner shards are written from other GPUs over xGMI: every rank checks that its device can
+        access every other rank's device; if any pair cannot, ALL ranks fall back to the host
+        (/dev/shm) store - the decision is collective, since the owners' allocations depend on it."""
+        me = self.params[0].device.index
+        ndev = torch.cuda.device_count()
+        ok = True
+        for d in range(ndev):
+            if d != me and not torch.cuda.can_device_access_peer(me, d):
+                ok = False
+        if ok:
+            for d in range(ndev):  # enable peer access now (torch turns it on with a first P2P copy)
+                if d != me:
+                    torch.empty(1, device=d).copy_(torch.zeros(1, device=me))
+        key = "%s/%s/p2p" % (STORE_PREFIX, self.run_id)
+        self.store.add(key + "_n", 1)
+        if not ok:
+            self.store.add(key + "_bad", 1)
+        t0 = time.time()
+        while int(self.store.add(key + "_n", 0)) < self.world:
+            if time.time() - t0 > 300:
+                raise TimeoutError("ASP peer-access negotiation")
+            time.sleep(0.005)
+        if int(self.store.add(key + "_bad", 0)):
+            import logging
+            logging.getLogger(__name__).warning(
+                "ASP: peer access between the ranks' GPUs is unavailable; using the host (/dev/shm) store")
+            return "shm"
+        return "ipc"
     def _open_flat(self, k, total, init_from):
         if self.mode == "shm":
             path = "/dev/shm/%s_%s_owner%d" % (STORE_PREFIX, self.run_id, k)
@@ -121,6 +166,10 @@ class ParamStore:
                     buf[off:off + p.numel()].copy_(p.detach().reshape(-1).to(buf.device))
             if self.kind == "rmsprop":
                 buf[2 * n_owner:3 * n_owner].fill_(1.0)  # TF RMSProp ms slot init 1.0
+            if k == 0 and self._buf_local is not None:
+                nsl = {"sgd": 0, "momentum": 1, "rmsprop": 2}[self.kind]
+                base = n_owner * (1 + nsl)
+                buf[base:base + self._buf_local.numel()].copy_(self._buf_local.to(buf.device))
 
     # -----------------------------------------------------------------------------------------
     @torch.no_grad()
@@ -132,7 +181,18 @@ class ParamStore:
             w16 = getattr(p, "bf16", None)
             if w16 is not None:
                 w16.copy_(p)
+        if self._buf_local is not None:
+            self._buf_local.copy_(self.buf_shard.to(self._buf_local.device, non_blocking=True))
+            self._buf_snap.copy_(self._buf_local)
         WEIGHT_VERSION[0] += 1
+
+    @torch.no_grad()
+    def push_buffers(self):
+        """Apply this worker's forward-time buffer updates to the shared copy (delta since the pull)."""
+        if self._buf_local is None:
+            return
+        delta = self._buf_local - self._buf_snap
+        self.buf_shard.add_(delta.to(self.buf_shard.device, non_blocking=True))
 
     # ---- fused GPU push: one multi-tensor optimizer launch on the owner shards -----------------
     def _fused_tables(self):
@@ -305,6 +365,7 @@ class ASPTrainStep:
             side_join()  # side-stream weight-gradient reductions land before the push reads them
         gs = self.store.global_step()
         lr = self.lr_schedule(gs) if self.lr_schedule else None
+        self.store.push_buffers()
         # ASP: nothing waits for the update (Hogwild: the next pull on this stream sees it); SSP ticks
         # the staleness clock only after the update has landed
         self.store.push([getattr(p, "main_grad", None) if p.grad is None else p.grad for p in self.store.params],

@@ -227,3 +227,74 @@ class BSPDataParallel:
     @property
     def grad_scale(self):
         return 1.0 / self.world
+
+
+def flatten_tensors(tensors):
+    """Re-home ``tensors`` (same dtype and device) into ONE contiguous buffer and return it.
+
+    Object identity is kept - every tensor's ``.data`` is re-pointed at its view of the buffer - so
+    module buffers, slim variable stores and checkpoint variable lists that already hold the
+    tensors keep working, while one collective / one copy now covers all of them.  Must run before
+    anything caches raw device pointers of the tensors (FusedOptimizer tables)."""
+    tensors = list(tensors)
+    if not tensors:
+        return None
+    dt, dev = tensors[0].dtype, tensors[0].device
+    assert all(t.dtype == dt and t.device == dev for t in tensors), "flatten_tensors: mixed dtype/device"
+    flat = torch.empty(sum(t.numel() for t in tensors), dtype=dt, device=dev)
+    off = 0
+    with torch.no_grad():
+        for t in tensors:
+            n = t.numel()
+            v = flat[off:off + n].view(t.shape)
+            v.copy_(t.detach())
+            t.data = v
+            off += n
+    return flat
+
+
+class BufferSync:
+    """Replica-consistent BN moving statistics under BSP.
+
+    In the reference every worker's BN update op writes the ONE PS-resident ``moving_mean`` /
+    ``moving_variance`` (inception/imagenet_inception_bsp.py:145-149; slim BN puts them in
+    UPDATE_OPS, inception/slim/ops.py:117-131), so there is a single set of moving statistics for
+    the whole job, and it is what the checkpoint and eval see.  Here each replica updates its own
+    copy from its local batch in forward; this class keeps the replicas identical: the statistics
+    live in one flat fp32 buffer (``flatten_tensors``), whose SUM all-reduce is issued right after
+    forward (they are final then; backward never reads them), so the collective runs on the comm
+    stream underneath the whole backward, and ``finish`` waits and scales by 1/W.  The result is
+    ``m <- d*m + (1-d)*mean_r(batch_stat_r)`` on every rank - the reference's update with the
+    average of the workers' batch statistics.  EMA shadows of the statistics are updated by the
+    optimizer from the averaged values, so they stay replica-identical without a collective of
+    their own.  ``every`` > 1 syncs only every k-th step (cheaper; replicas drift in between)."""
+
+    def __init__(self, buffers, process_group=None, every=1):
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        self.buffers = [b for b in buffers]
+        self.every = max(1, int(every))
+        self.flat = flatten_tensors(self.buffers) if (self.world > 1 and self.buffers) else None
+        self._work = None
+        self._n = 0
+
+    def issue(self):
+        if self.flat is None:
+            return
+        self._n += 1
+        if (self._n - 1) % self.every:
+            return
+        if self.flat.is_cuda:
+            opsnn.side_join()
+        with roctx("bn_stats_allreduce"):
+            self._work = dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+
+    def finish(self):
+        if self._work is None:
+            return
+        self._work.wait()
+        self._work = None
+        self.flat.mul_(1.0 / self.world)
+
+    def numel(self):
+        return 0 if self.flat is None else self.flat.numel()

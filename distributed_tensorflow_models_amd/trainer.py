@@ -63,6 +63,9 @@ PRESETS = {
     "resnet": dict(model="cifar10_resnet_v2", num_classes=10, dataset="cifar10", image_size=32, batch_size=128,
                    lr=0.08, lr_scale_workers=True, decay_epochs=32.0, decay_factor=0.1, optimizer="sgd",
                    ema=0.9999, wd_all=2e-3, max_steps=10000000, save_secs=60, log_style="short", max_to_keep=1,
+                   # tf.layers.batch_normalization (resnet_model.py:45) keeps its moving statistics out of
+                   # tf.moving_average_variables(): the EMA covers trainables only
+                   ema_buffers=False,
                    train_accuracy_every=200, scope_prefix="root/", partitioned=True, global_step_name="Variable",
                    train_dir="/home/ubuntu/cifar10/train",
                    data_dir="/home/ubuntu/cifar10/data"),
@@ -128,7 +131,9 @@ def define_common_flags(flags, preset):
             ("max_staleness", I, 5, "SSP staleness bound in local steps"),
             ("synthetic_data", B, False, "use HBM-resident synthetic batches"),
             ("bucket_mb", Fl, 32.0, "all-reduce bucket size (MB)"),
-            ("use_hipgraph", B, False, "capture the BSP training step in a hipGraph (launch-bound models)"),
+            ("use_hipgraph", B, False, "capture the BSP training step in a hipGraph (launch-bound models; "
+             "single-rank only, ignored with a warning when world > 1)"),
+            ("bn_sync_every", I, 1, "BSP: average the BN moving statistics over the replicas every N steps"),
             ("grad_comm_dtype", S, "fp32", "gradient all-reduce dtype on the wire: fp32 | bf16"),
             ("deterministic", B, False, "bit-reproducible GPU reductions (no cross-block fp32 atomics)"),
             ("trace_steps", S, "", "a:b -> export a Chrome trace of steps [a, b)"),
@@ -270,9 +275,12 @@ def train(preset, flags, default_mode="bsp"):
     loss_fn = make_loss_fn(cfg.get("label_smoothing", 0.0), cfg.get("aux_weight", 0.4), FLAGS.batch_weight)
     store = clock = None
     if mode == "bsp":
+        if FLAGS.use_hipgraph and world > 1:
+            logging.warning("--use_hipgraph ignored: step capture is single-rank only (world size %d)", world)
         step_fn = TrainStep(model, bucket_mb=FLAGS.bucket_mb, label_smoothing=cfg.get("label_smoothing", 0.0),
                             aux_weight=cfg.get("aux_weight", 0.4), ema_decay=cfg.get("ema"), lr_schedule=sched,
-                            batch_weight=FLAGS.batch_weight, use_graph=FLAGS.use_hipgraph,
+                            batch_weight=FLAGS.batch_weight, use_graph=FLAGS.use_hipgraph and world == 1,
+                            ema_buffers=cfg.get("ema_buffers", True), bn_sync_every=FLAGS.bn_sync_every,
                             grad_comm_dtype=torch.bfloat16 if FLAGS.grad_comm_dtype == "bf16" else None,
                             timer=StepTimer() if (FLAGS.metrics_file and rank == 0 and not FLAGS.use_hipgraph)
                             else None, **opt_kw)
@@ -288,7 +296,7 @@ def train(preset, flags, default_mode="bsp"):
         step_fn.global_step = int(gstep)
         step_fn.opt.num_updates = int(gstep)
     elif mode in ("asp", "ssp"):
-        from .engine import prepare_compute_copies
+        from .engine import moving_average_buffers, prepare_compute_copies
         from .parallel.asp import ASPTrainStep, ParamStore
         from .parallel.ssp import StalenessClock
         vars_ = model_variables(model, None, gstep, **ckpt_kw)
@@ -297,7 +305,8 @@ def train(preset, flags, default_mode="bsp"):
             Saver(vars_).restore(path)
         prepare_compute_copies(model)
         store = ParamStore(list(model.parameters()), cfg["optimizer"], sched(0), opt_kw["momentum"], opt_kw["rho"],
-                           opt_kw["epsilon"], run_id=os.environ.get("DTM_RUN_ID", "0"))
+                           opt_kw["epsilon"], run_id=os.environ.get("DTM_RUN_ID", "0"),
+                           buffers=moving_average_buffers(model))
         if is_chief and int(gstep):
             store.set_global_step(int(gstep))
         # optimizer slots live in the owner shards: checkpointed from there, restored into them
@@ -363,8 +372,11 @@ def train(preset, flags, default_mode="bsp"):
         else:
             loss, gs = step_fn(images, labels)
         n_since += 1
-        log_now = step % max(FLAGS.log_every, 1) == 0
-        need_log = log_now or cfg.get("nan_guard")
+        log_now = step % max(FLAGS.log_every, 1) == 0 or step + 1 >= FLAGS.max_steps
+        # the loss is read (a device sync) on log steps only; the NaN assertion of the reference
+        # (imagenet_inception_bsp.py:191, every step) is checked there, and non-finite steps in
+        # between are caught by the engine's device-side guard (update skipped, counted, reported)
+        need_log = log_now
         if need_log:
             loss_v = float(loss)
         dt = 0.0
@@ -379,7 +391,8 @@ def train(preset, flags, default_mode="bsp"):
         if cfg.get("nan_guard") and math.isnan(loss_v):  # imagenet_inception_bsp.py:191
             raise FloatingPointError("Model diverged with loss = NaN")
         if mode == "bsp" and need_log and step_fn.poll_skipped():
-            logging.warning("step %d: non-finite gradients, update skipped (%d so far)", step, step_fn.skipped)
+            logging.warning("step %d: non-finite gradients since the last log line, update(s) skipped (%d so far)",
+                            step, step_fn.skipped)
         gstep.fill_(gs)
         if log_now:
             print(format_step(cfg["log_style"], step, gs, loss_v, B / max(dt, 1e-9), dt), flush=True)

@@ -231,3 +231,61 @@ def test_gpu_pipeline_assembler_host_side(tmp_path):
         assert list(tab["src_off"][1:]) == list(np.cumsum(tab["h"] * tab["w"] * 3)[:-1])
         assert (tab["y0"] + tab["ch"] <= tab["h"]).all() and (tab["x0"] + tab["cw"] <= tab["w"]).all()
         assert list(tab["method"]) == [0, 1, 2, 3] and set(lab.tolist()) <= set(range(1, 13))
+
+
+@pytest.mark.timeout(120)
+def test_imagenet_eval_pipeline_loops_and_skips_corrupt_records(tmp_path):
+    """Eval readers loop over the files like string_input_producer (no num_epochs): more batches than
+    records never starve (two eval_once passes on one pipeline); a corrupt JPEG is skipped and counted,
+    not a dead preprocessing thread and a hung next_batch."""
+    out = tmp_path / "data"
+    out.mkdir()
+    with TFRecordWriter(str(out / "validation-00000-of-00001")) as w:
+        for i in range(5):
+            w.write(encode_example({"image/encoded": _jpeg(40, 40, (i * 30, 0, 0)), "image/class/label": i + 1}))
+        w.write(encode_example({"image/encoded": b"\xff\xd8 definitely not a jpeg", "image/class/label": 9}))
+    ds = imagenet.ImagenetData("validation", str(out))
+    bi = imagenet.inputs(ds, 4, num_preprocess_threads=2, image_size=32)
+    try:
+        labels = []
+        for _ in range(4):  # 16 images from 5 good records
+            x, y = bi.next_batch()
+            labels += y.tolist()
+    finally:
+        bi.close()
+    assert set(labels) <= set(range(1, 6)) and bi.bad_records >= 1
+
+
+@pytest.mark.timeout(180)
+def test_gpu_pipeline_assembler_skips_corrupt_record(tmp_path):
+    from distributed_tensorflow_models_amd.data import imagenet_gpu
+    out = tmp_path / "d"
+    out.mkdir()
+    with TFRecordWriter(str(out / "train-00000-of-00001")) as w:
+        for i in range(6):
+            w.write(encode_example({"image/encoded": _jpeg(24, 24, (0, i * 30, 0)), "image/class/label": i + 1}))
+        w.write(encode_example({"image/encoded": b"garbage", "image/class/label": 99}))
+    ds = imagenet.ImagenetData("train", str(out))
+    bi = imagenet_gpu.GPUBatchInputs(ds, 4, train=True, image_size=16, num_readers=1, num_decoders=2, seed=1,
+                                     device="cpu", decode_processes=False, shuffle_buffer=16)
+    try:
+        got = [bi.ready.get(timeout=120) for _ in range(3)]
+    finally:
+        bi.close()
+    for _bt, _tt, lab in got:
+        assert 99 not in lab.tolist()
+    assert bi.bad_records >= 1
+
+
+def test_gpu_pipeline_error_surfaces_in_next_batch(tmp_path):
+    from distributed_tensorflow_models_amd.data import imagenet_gpu
+    out = tmp_path / "d"
+    out.mkdir()
+    (out / "train-00000-of-00001").write_bytes(b"\x07" * 64)  # not a TFRecord file: the reader dies
+    bi = imagenet_gpu.GPUBatchInputs(imagenet.ImagenetData("train", str(out)), 2, train=True, image_size=16,
+                                     num_readers=1, num_decoders=1, device="cpu", decode_processes=False)
+    try:
+        with pytest.raises(RuntimeError, match="pipeline failed"):
+            bi.next_batch()
+    finally:
+        bi.close()

@@ -319,3 +319,96 @@ def test_asp_gpu_ipc_fused_push(kind):
         torch.testing.assert_close(r["params"][1], torch.full((3, 20000), 2.0 - dec))
         torch.testing.assert_close(r["params"][2], torch.full((4,), -dec))
         torch.testing.assert_close(r["params"][0], torch.full((5,), 1.0 - dec))
+
+
+# ---------------------------------------------------------------------------------------------
+# BN moving statistics under BSP: the reference keeps ONE PS-resident copy that every worker's
+# update op writes (inception/imagenet_inception_bsp.py:145-149); here every replica must end each
+# step with the same statistics = the average of what the replicas computed from their own batches.
+
+def _bn_sync_worker(rank, world, steps=3):
+    import copy
+
+    from distributed_tensorflow_models_amd.engine import TrainStep, moving_average_buffers
+    from distributed_tensorflow_models_amd.models import nets_factory
+    torch.manual_seed(0)
+    model = nets_factory.build("cifar10_resnet_v2", num_classes=10, resnet_size=8)
+    step = TrainStep(model, optimizer="momentum", lr=0.05, momentum=0.9, ema_decay=0.99, bucket_mb=0.05)
+    g = torch.Generator().manual_seed(100 + rank)  # a DIFFERENT batch on every rank
+    local, synced = [], []
+    for _ in range(steps):
+        x, y = torch.randn(4, 32, 32, 3, generator=g) * (1 + rank), torch.randint(0, 10, (4,), generator=g)
+        shadow = copy.deepcopy(model)  # what this replica's forward alone makes of the statistics
+        with torch.no_grad():
+            shadow(x, training=True)
+        local.append(torch.cat([b.reshape(-1) for b in moving_average_buffers(shadow)]))
+        step(x, y)
+        synced.append(torch.cat([b.reshape(-1) for b in moving_average_buffers(model)]).clone())
+    shadows = torch.cat([s.reshape(-1) for _b, s in step.opt.buffer_shadows()])
+    return {"local": torch.stack(local), "synced": torch.stack(synced), "shadows": shadows,
+            "flat": step.bufsync.numel(), "nbuf": len(moving_average_buffers(model))}
+
+
+def test_bsp_bn_moving_statistics_replica_consistent():
+    res = run_workers(_bn_sync_worker, 2)
+    assert res[0]["nbuf"] > 0 and res[0]["flat"] > 0
+    # bit-identical replicas after every step (and so are the EMA shadows of the statistics)
+    assert torch.equal(res[0]["synced"], res[1]["synced"])
+    assert torch.equal(res[0]["shadows"], res[1]["shadows"])
+    # the ranks saw different data, so their own statistics differ ...
+    assert not torch.allclose(res[0]["local"][0], res[1]["local"][0])
+    # ... and the synced value is their average (from the same pre-step state on both ranks)
+    mean = (res[0]["local"] + res[1]["local"]) / 2
+    torch.testing.assert_close(res[0]["synced"], mean, rtol=1e-5, atol=1e-6)
+
+
+def test_bsp_single_rank_keeps_buffers_unflattened():
+    from distributed_tensorflow_models_amd.engine import TrainStep
+    from distributed_tensorflow_models_amd.models import nets_factory
+    model = nets_factory.build("cifar10_resnet_v2", num_classes=10, resnet_size=8)
+    step = TrainStep(model, optimizer="sgd", lr=0.01)
+    assert step.bufsync.flat is None  # world 1: no collective, no re-homing
+
+
+def _graph_refusal_worker(rank, world):
+    from distributed_tensorflow_models_amd.engine import TrainStep
+    from distributed_tensorflow_models_amd.models import nets_factory
+    model = nets_factory.build("cifar10_cnn", num_classes=10)
+    try:
+        TrainStep(model, optimizer="sgd", lr=0.01, use_graph=True)
+    except ValueError as e:
+        return {"refused": "single-rank" in str(e)}
+    return {"refused": False}
+
+
+def test_hipgraph_capture_refused_with_more_than_one_rank():
+    assert all(r["refused"] for r in run_workers(_graph_refusal_worker, 2))
+
+
+def _asp_buffer_worker(rank, world):
+    """ASP: BN moving statistics live in the shared store; each worker pushes its forward's delta."""
+    from distributed_tensorflow_models_amd.parallel import process_group as pg
+    from distributed_tensorflow_models_amd.parallel.asp import ParamStore, wait_all_done
+    p = torch.nn.Parameter(torch.ones(3))
+    mm, mv = torch.zeros(4), torch.ones(4)
+    store = ParamStore([p], "sgd", 0.1, mode="shm", run_id="aspbuf%d" % world, buffers=[mm, mv])
+    for r in range(world):  # one worker at a time (this checks the bookkeeping, not the race)
+        if r == rank:
+            store.pull()
+            mm.sub_((mm - float(rank + 1)) * 0.5)  # the forward's moving-average update, decay 0.5
+            mv.mul_(0.5)
+            store.push_buffers()
+        pg.barrier()
+    wait_all_done(store.store, world, store.run_id)
+    store.pull()
+    out = {"mm": mm.clone(), "mv": mv.clone()}
+    store.close()
+    return out
+
+
+def test_asp_shared_bn_statistics():
+    res = run_workers(_asp_buffer_worker, 2)
+    # rank 0: mm 0 -> 0.5 ; rank 1 (sees 0.5): 0.5 -> 1.25 ; mv 1 -> 0.5 -> 0.25
+    for r in res:
+        torch.testing.assert_close(r["mm"], torch.full((4,), 1.25))
+        torch.testing.assert_close(r["mv"], torch.full((4,), 0.25))

@@ -342,3 +342,22 @@ def test_conv1x1_bn_backward_one_pass_plain_input(monkeypatch):
     errs = {k: _rel(grads["1"][k], grads["0"][k]) for k in grads["0"]}
     worst = max((v, k) for k, v in errs.items() if "beta" not in k or not k.startswith("conv1"))
     assert worst[0] < 2e-2, worst
+
+
+@pytest.mark.gpu
+def test_pooled_bn_stats_backward_leaves_shared_gradient_alone():
+    """The pooled-BN statistics backward may write dy into its incoming gradient only when that gradient
+    is private; here the alias feeds an add whose backward hands ONE gradient tensor to both inputs, so
+    the sibling input's gradient must come out untouched (fused.py _BNStatsFn)."""
+    torch.manual_seed(0)
+    x = torch.randn(2, 8, 8, 16, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(16, 1, 1, 16, device=DEV) * 0.2).requires_grad_()
+    bn = _bn(16, scale=False)
+    out = fused.conv_avgpool_bn(x, w, bn, training=True)
+    r = out.raw
+    t = torch.zeros_like(r, requires_grad=True)
+    G = torch.randn(r.shape, device=DEV).to(torch.bfloat16)
+    H = torch.randn(out.ss.shape, device=DEV)
+    loss = ((r + t).float() * G.float()).sum() + (out.ss.float() * H).sum()
+    loss.backward()
+    torch.testing.assert_close(t.grad.float(), G.float(), rtol=0, atol=0)

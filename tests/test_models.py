@@ -283,3 +283,20 @@ def test_pix2pix_discriminator_four_layers(pad):
             return gans.pix2pix_discriminator(x, [64, 128, 256, 512], padding=pad)
     (logits, ep), _ = _run(fn, torch.ones(2, 256, 256, 3))
     assert list(logits.shape) == [2, o, o, 1] and list(ep["predictions"].shape) == [2, o, o, 1]
+
+
+def test_mobilenet_v1_base_model_variable_count():
+    # reference vgg/nets/mobilenet_v1_test.py:344-353 (testModelHasExpectedNumberOfParameters):
+    # mobilenet_v1_base under arg_scope(conv2d / separable_conv2d, normalizer_fn=slim.batch_norm) -
+    # weights + BN beta / moving_mean / moving_variance (slim BN default scale=False) = 3,217,920
+    from distributed_tensorflow_models_amd.compat import slim as S
+
+    def base(images, is_training=True, num_classes=None):
+        ep = {}
+        with S.arg_scope([S.conv2d, S.separable_conv2d], normalizer_fn=S.batch_norm):
+            with S.variable_scope("MobilenetV1"):
+                return slim_nets.mobilenet_v1_base(images, ep), ep
+
+    m = SlimModel(base, 224)
+    n = sum(p.numel() for p in m.parameters()) + sum(b.numel() for b in m.buffers())
+    assert n == 3217920
