@@ -56,6 +56,8 @@ def main():
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--dist-backend", default="", help="override the process-group backend (default: nccl = "
                     "RCCL on GPUs, gloo on CPU); gloo on GPUs lets several ranks share one device for rehearsals")
+    ap.add_argument("--rccl-channels", type=int, default=0,
+                    help="pin the RCCL channel count (NCCL_MIN/MAX_NCHANNELS); 0 = RCCL's own choice")
     ap.add_argument("--device", default="cuda", choices=("cuda", "cpu"),
                     help="cpu: the plumbing config (LeNet over gloo, no GPU; BASELINE.json config 1)")
     args = ap.parse_args()
@@ -86,8 +88,13 @@ def main():
                 torch.cuda.set_device(gpu_index)
             dist.init_process_group("gloo")
         else:
+            from distributed_tensorflow_models_amd.parallel import process_group as pg
+            # per-bucket collective timing (read after the timed steps) + optional channel pinning
+            pg.rccl_env(args.rccl_channels, timing=True)
             torch.cuda.set_device(local_rank)
-            dist.init_process_group(backend, device_id=torch.device("cuda", local_rank))
+            opts = pg.nccl_options(high_priority=True)  # comm stream ahead of queued backward kernels
+            kw = {"pg_options": opts} if opts is not None else {}
+            dist.init_process_group(backend, device_id=torch.device("cuda", local_rank), **kw)
     dev = torch.device("cpu") if cpu else torch.device("cuda", gpu_index)
     sync = (lambda: None) if cpu else torch.cuda.synchronize
 
@@ -157,6 +164,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         phases = dict(zip(("fwd_ms", "bwd_ms", "allreduce_exposed_ms", "optimizer_ms"),
                           [round(float(v), 3) for v in t.tolist()]))
+        bms = step.dp.bucket_ms()  # rank-local durations of each bucket's all-reduce, last step
+        if bms:
+            phases["bucket_allreduce_ms"] = bms
+            phases["bucket_mb"] = [round(n * 4 / 1e6, 2) for n in step.dp.bucket_elements()]
     ms = dt / args.steps * 1000.0
     value = world * B * args.steps / dt
     if rank == 0:

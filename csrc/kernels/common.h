@@ -58,12 +58,6 @@ __host__ static inline FastDiv make_fastdiv(uint32_t d) {
 // workspace arena + two-stage reduction (workspace.hip)
 float* dtm_ws_get(size_t floats);
 void dtm_reduce_rows(const float* ws, int rows, int width, int ld, float* out, hipStream_t st);
-// off-critical-path reductions (workspace.hip): a slab from a ring of side buffers, reduced on a side stream
-float* dtm_side_slab(size_t floats, hipStream_t st, int* slot);
-void dtm_side_reduce(int slot, int rows, int width, int ld, float* out, hipStream_t st);
-// deferred reductions (workspace.hip): a slab from the bump arena, queued, summed at dtm_def_flush
-float* dtm_def_slab(size_t floats, hipStream_t st);
-void dtm_def_push(const float* ws, int rows, int width, float* out);
 void dtm_reduce_split(int rows, int xblocks, int* rpb, int* ychunks);
 int dtm_reduce_direct_max();
 int dtm_ntld_bits();  // non-temporal input-load policy of the BN-apply kernels (fused_bn.hip)  // grids up to this many blocks reduce with atomics in the producer

@@ -69,20 +69,6 @@ struct ConvNTArgs {
   // grid is pixel (n, i*ostr + oa, j*ostr + ob) of the OH x OW tensor that y and every epilogue side
   // input (add_src, act_x, act_r, act_mask) index.  ostr == 1: identity (OH = P, OW = Q, oa = ob = 0)
   int ostr, oa, ob, OH, OW;
-  int pre_side;  // conv_nt_kernel: load the dgrad epilogue's side inputs before the last k-tile (A/B knob)
-  // BatchNorm finalize hand-off in the statistics epilogue (fin_acc != nullptr): each block adds its tile's
-  // column sums into replica (by % fin_G) of a self-cleaning [fin_G][2K] accumulator with memory-side
-  // atomics; the last block (fin_counter) folds the replicas (atomic exchanges re-zero them) and writes
-  // ss = [scale; shift; mean; rstd] + the moving averages: no separate reduce/finalize launch
-  float* fin_acc;
-  unsigned* fin_counter;
-  int fin_G, fin_update, fin_bessel;
-  const float* fin_gamma;
-  const float* fin_beta;
-  float* fin_mm;
-  float* fin_mv;
-  float* fin_ss;
-  float fin_count, fin_eps, fin_decay;
 };
 
 // full-resolution coordinates / row of output pixel m (see ConvNTArgs::ostr)
@@ -115,66 +101,202 @@ __device__ __forceinline__ void epi_barrier() {
   }
 }
 
-// Side inputs of the staged dgrad epilogue (add_src / act_x / act_r chunks, ReLU-mask bytes) for the NIT
-// rows one thread stores; epi_side_load issues them (e.g. before a kernel's last k-tile, so their HBM
-// latency overlaps MFMAs instead of following them) and conv_nt_epilogue consumes them (a.pre_side).
-template <int NIT>
-struct EpiSide {
-  uint4 pa[NIT], px[NIT], pr[NIT];
-  uint32_t pm[NIT];
-  bool ph[NIT];
-};
-template <int PT, int CT, int NT>
-__device__ __forceinline__ void epi_side_load(const ConvNTArgs& a, int p0, int c0, EpiSide<PT * (CT / 8) / NT>& sd) {
-  constexpr int CPR = CT / 8, NIT = PT * CPR / NT;
-  const int tid = threadIdx.x;
-  const int kc = c0 + (tid % CPR) * 8;
-  const bool act = a.act_x != nullptr, amask = act && a.act_mask != nullptr;
-#pragma unroll
-  for (int j = 0; j < NIT; ++j) {
-    sd.pa[j] = sd.px[j] = sd.pr[j] = make_uint4(0, 0, 0, 0);
-    sd.pm[j] = 0u;
-    sd.ph[j] = false;
-    const int m = p0 + (j * NT + tid) / CPR;
-    if (m < a.M && kc < a.K) {
-      const size_t o = (size_t)out_row(a, m) * a.K + kc;
-      if (a.add_src) {
-        const bf16_t* src = a.add_src + o;
-        if (a.add_stride > 1) {
-          int n, h, w;
-          out_nhw(a, m, n, h, w);
-          const int s = a.add_stride;
-          src = (h % s == 0 && w % s == 0) ? a.add_src + ((size_t)(n * a.add_H + h / s) * a.add_W + w / s) * a.K + kc
-                                           : nullptr;
-        }
-        if (src) {
-          sd.pa[j] = *(const uint4*)src;
-          sd.ph[j] = true;
-        }
-      }
-      if (act) {
-        sd.px[j] = *(const uint4*)(a.act_x + o);
-        if (amask) {
-          sd.pm[j] = a.act_mask[o >> 3];
-          if (a.act_r) sd.pr[j] = *(const uint4*)(a.act_r + o);
-        }
-      }
-    }
-  }
-}
-
 // STG: 1 = LDS-staged stores (K % 8 == 0), 2 = direct 8-B stores.  Kept compile-time: a runtime choice
 // between an LDS and a global pointer makes hipcc emit flat stores, which wait on both counters.
 // SACC (statistics accumulate, persistent kernels): the BatchNorm sums are not shuffle-reduced per tile;
 // each thread adds the bf16 outputs of its fixed 8-channel chunk column in the staged-store loop to
 // ssum / ssq (registers, across all the block's tiles) and the kernel reduces them once at its end.
 // NT: threads of the block (256 = 4 waves, 512 = the 8-wave big-tile kernel).
+// Staged-store tail of the conv_nt epilogues: the block's output tile is in LDS as bf16 rows of
+// OROW bytes (pixel-major); each thread stores full 16-B chunks (coalesced NHWC rows) with the dgrad
+// post-ops (add_src, activation backward, block-output BN-apply backward) and the BatchNorm statistics
+// / post-op partial sums.  Shared by the 16x16x32 and the 32x32x16 MFMA register layouts.
+template <int PT, int CT, bool RAWB, bool EXACT, bool SACC, int NT>
+__device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem, int p0, int c0, int by,
+                                                 float* ssum, float* ssq) {
+  constexpr int OROW = CT * 2 + 16;
+  const int tid = threadIdx.x;
+  epi_barrier<RAWB>();
+  constexpr int CPR = CT / 8;  // 16-B chunks per pixel row of the tile
+  constexpr int NIT = PT * CPR / NT;
+  static_assert(NT % CPR == 0 && (PT * CPR) % NT == 0, "staged-store mapping");
+  const int chn = tid % CPR;   // fixed per thread (NT % CPR == 0)
+  const int kc = c0 + chn * 8;
+  const bool act = a.act_x != nullptr;
+  // BatchNorm statistics of a staged tile: each thread sums its fixed 8-channel chunk column over its
+  // rows (bf16-rounded outputs) and the block reduces them once through LDS below -> ONE partial row
+  // per pixel tile, no per-subtile shuffle trees (those cost up to +100 % on the wide-K 1x1 layers)
+  const bool bstats = !SACC && a.stats != nullptr;
+  float sc[8], sh[8], sgx[8], sg[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { sc[e] = 1.f; sh[e] = 0.f; sgx[e] = 0.f; sg[e] = 0.f; }
+  const bool amask = act && a.act_mask != nullptr;
+  float sgr[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sgr[e] = 0.f;
+  if (act && !amask && kc < a.K) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sc[e] = a.act_ss[kc + e]; sh[e] = a.act_ss[a.K + kc + e]; }
+  }
+  // side inputs of the dgrad post-ops (add_src, act_x, act_r, mask bytes) are loaded for a group of
+  // GRP rows before any of them is used, so their latencies overlap instead of serialising per row
+  constexpr int GRP = NIT < 4 ? NIT : 4;
+  static_assert(NIT % GRP == 0, "epilogue row groups");
+  const bool side = a.add_src != nullptr || act;
+#pragma unroll
+  for (int g0 = 0; g0 < NIT; g0 += GRP) {
+    uint4 pa[GRP], px[GRP], pr[GRP];
+    uint32_t pm[GRP];
+    bool ph[GRP];
+#pragma unroll
+    for (int j = 0; j < GRP; ++j) {
+      pa[j] = px[j] = pr[j] = make_uint4(0, 0, 0, 0);
+      pm[j] = 0u;
+      ph[j] = false;
+    }
+    if (side) {
+#pragma unroll
+      for (int j = 0; j < GRP; ++j) {
+        const int row = ((g0 + j) * NT + tid) / CPR;
+        const int m = p0 + row;
+        if (m < a.M && kc < a.K) {
+          const size_t o = (size_t)out_row(a, m) * a.K + kc;
+          if (a.add_src) {
+            const bf16_t* src = a.add_src + o;
+            if (a.add_stride > 1) {
+              int n, h, w;
+              out_nhw(a, m, n, h, w);
+              const int s = a.add_stride;
+              src = (h % s == 0 && w % s == 0)
+                        ? a.add_src + ((size_t)(n * a.add_H + h / s) * a.add_W + w / s) * a.K + kc
+                        : nullptr;
+            }
+            if (src) {
+              pa[j] = *(const uint4*)src;
+              ph[j] = true;
+            }
+          }
+          if (act) {
+            px[j] = *(const uint4*)(a.act_x + o);
+            if (amask) {
+              pm[j] = a.act_mask[o >> 3];
+              if (a.act_r) pr[j] = *(const uint4*)(a.act_r + o);
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < GRP; ++j) {
+      const int idx = (g0 + j) * NT + tid;
+      const int row = idx / CPR;
+      const int m = p0 + row;
+      const bool inb = m < a.M && kc < a.K;
+      if (EXACT || inb) {
+        uint4 v = *(const uint4*)(smem + row * OROW + chn * 16);
+        const size_t o = (size_t)(inb ? out_row(a, m) : m) * a.K + kc;
+        if constexpr (SACC) {
+          if (inb) {
+            const float q[8] = {lo_bf(v.x), hi_bf(v.x), lo_bf(v.y), hi_bf(v.y),
+                                lo_bf(v.z), hi_bf(v.z), lo_bf(v.w), hi_bf(v.w)};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { ssum[e] += q[e]; ssq[e] = fmaf(q[e], q[e], ssq[e]); }
+          }
+        } else {
+          if (bstats && inb) {  // (sgx / sg double as the statistics accumulators: act is off here)
+            const float q[8] = {lo_bf(v.x), hi_bf(v.x), lo_bf(v.y), hi_bf(v.y),
+                                lo_bf(v.z), hi_bf(v.z), lo_bf(v.w), hi_bf(v.w)};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { sgx[e] += q[e]; sg[e] = fmaf(q[e], q[e], sg[e]); }
+          }
+        }
+        if (inb && side) {
+          float f[8];
+          f[0] = lo_bf(v.x); f[1] = hi_bf(v.x); f[2] = lo_bf(v.y); f[3] = hi_bf(v.y);
+          f[4] = lo_bf(v.z); f[5] = hi_bf(v.z); f[6] = lo_bf(v.w); f[7] = hi_bf(v.w);
+          if (ph[j]) {
+            const uint4 r = pa[j];
+            f[0] += lo_bf(r.x); f[1] += hi_bf(r.x); f[2] += lo_bf(r.y); f[3] += hi_bf(r.y);
+            f[4] += lo_bf(r.z); f[5] += hi_bf(r.z); f[6] += lo_bf(r.w); f[7] += hi_bf(r.w);
+          }
+          if (act) {
+            const uint4 xu = px[j];
+            float xv[8];
+            xv[0] = lo_bf(xu.x); xv[1] = hi_bf(xu.x); xv[2] = lo_bf(xu.y); xv[3] = hi_bf(xu.y);
+            xv[4] = lo_bf(xu.z); xv[5] = hi_bf(xu.z); xv[6] = lo_bf(xu.w); xv[7] = hi_bf(xu.w);
+            if (amask) {
+              // block-output form: g = d(out) * bit, sums against the raw conv output (and the raw
+              // BN'd residual); out <- g (the producers' conv+BN backwards apply their scales)
+              const uint32_t mb = pm[j];
+              const uint4 ru = pr[j];
+              const float rv[8] = {lo_bf(ru.x), hi_bf(ru.x), lo_bf(ru.y), hi_bf(ru.y),
+                                   lo_bf(ru.z), hi_bf(ru.z), lo_bf(ru.w), hi_bf(ru.w)};
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                const float g = (mb >> e) & 1u ? f[e] : 0.f;
+                sgx[e] += g * xv[e];
+                sg[e] += g;
+                sgr[e] += g * rv[e];  // (rv = 0 without a BN'd residual)
+                f[e] = g;
+              }
+            } else {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                const float g = fmaf(xv[e], sc[e], sh[e]) > 0.f ? f[e] : 0.f;
+                sgx[e] += g * xv[e];
+                sg[e] += g;
+                f[e] = a.act_unscaled ? g : g * sc[e];
+              }
+            }
+          }
+          v = make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
+        }
+        *(uint4*)(inb ? a.y + o : a.dump) = v;
+      }
+    }
+  }
+  if (act || bstats) {
+    // reduce the per-thread partial sums over the threads sharing this chunk column, one partial
+    // row per pixel tile (reduced over tiles by dtm_reduce_rows / stats_reduce_finalize)
+    epi_barrier<RAWB>();
+    float* red = (float*)smem;  // [NT][16]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { red[tid * 16 + e] = sgx[e]; red[tid * 16 + 8 + e] = sg[e]; }
+    epi_barrier<RAWB>();
+    // every thread finishes one (chunk column, value) output: NT/CPR partials each, instead of CPR
+    // threads walking all NT rows of the table serially
+    const int rw = (act && a.act_r) ? 4 : 2;  // row width in K units
+    float* prow = (act ? a.act_sums : a.stats) + (size_t)by * (rw * a.K);
+    for (int o = tid; o < CPR * 16; o += NT) {
+      const int c = o >> 4, e = o & 15;
+      float t = 0.f;
+#pragma unroll 4
+      for (int k = 0; k < NT / CPR; ++k) t += red[((c + k * CPR) << 4) + e];
+      const int kk = c0 + c * 8 + (e & 7);
+      if (kk < a.K) prow[(e < 8 ? 0 : a.K) + kk] = t;
+    }
+    if (act && a.act_r) {  // second round: [sum g*r | sum g] of the BN'd residual
+      epi_barrier<RAWB>();
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { red[tid * 16 + e] = sgr[e]; red[tid * 16 + 8 + e] = sg[e]; }
+      epi_barrier<RAWB>();
+      for (int o = tid; o < CPR * 16; o += NT) {
+        const int c = o >> 4, e = o & 15;
+        float t = 0.f;
+#pragma unroll 4
+        for (int k = 0; k < NT / CPR; ++k) t += red[((c + k * CPR) << 4) + e];
+        const int kk = c0 + c * 8 + (e & 7);
+        if (kk < a.K) prow[2 * a.K + (e < 8 ? 0 : a.K) + kk] = t;
+      }
+    }
+  }
+}
+
 template <int PT, int CT, int WP, int WC, int STG, bool RAWB = false, bool EXACT = false, bool NOBIAS = false,
           bool SACC = false, int NT = 256>
 __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&acc)[WC / 16][WP / 16], char* smem,
                                                  int p0, int c0, int by, float* ssum = nullptr,
-                                                 float* ssq = nullptr,
-                                                 const EpiSide<PT * (CT / 8) / NT>* pre = nullptr) {
+                                                 float* ssq = nullptr) {
   constexpr int NWP = PT / WP;
   constexpr int TP = WP / 16, TC = WC / 16;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -238,221 +360,48 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
       }
     }
   }
-  if constexpr (staged) {
-    epi_barrier<RAWB>();
-    constexpr int CPR = CT / 8;  // 16-B chunks per pixel row of the tile
-    constexpr int NIT = PT * CPR / NT;
-    static_assert(NT % CPR == 0 && (PT * CPR) % NT == 0, "staged-store mapping");
-    const int chn = tid % CPR;   // fixed per thread (NT % CPR == 0)
-    const int kc = c0 + chn * 8;
-    const bool act = a.act_x != nullptr;
-    // BatchNorm statistics of a staged tile: each thread sums its fixed 8-channel chunk column over its
-    // rows (bf16-rounded outputs) and the block reduces them once through LDS below -> ONE partial row
-    // per pixel tile, no per-subtile shuffle trees (those cost up to +100 % on the wide-K 1x1 layers)
-    const bool bstats = !SACC && a.stats != nullptr;
-    float sc[8], sh[8], sgx[8], sg[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { sc[e] = 1.f; sh[e] = 0.f; sgx[e] = 0.f; sg[e] = 0.f; }
-    const bool amask = act && a.act_mask != nullptr;
-    float sgr[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) sgr[e] = 0.f;
-    if (act && !amask && kc < a.K) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { sc[e] = a.act_ss[kc + e]; sh[e] = a.act_ss[a.K + kc + e]; }
-    }
-    // side inputs of the dgrad post-ops (add_src, act_x, act_r, mask bytes) are loaded for a group of
-    // GRP rows before any of them is used, so their latencies overlap instead of serialising per row
-    constexpr int GRP = NIT < 4 ? NIT : 4;
-    static_assert(NIT % GRP == 0, "epilogue row groups");
-    const bool side = a.add_src != nullptr || act;
-#pragma unroll
-    for (int g0 = 0; g0 < NIT; g0 += GRP) {
-      uint4 pa[GRP], px[GRP], pr[GRP];
-      uint32_t pm[GRP];
-      bool ph[GRP];
-#pragma unroll
-      for (int j = 0; j < GRP; ++j) {
-        pa[j] = px[j] = pr[j] = make_uint4(0, 0, 0, 0);
-        pm[j] = 0u;
-        ph[j] = false;
-      }
-      if (side && pre) {
-#pragma unroll
-        for (int j = 0; j < GRP; ++j) {
-          pa[j] = pre->pa[g0 + j]; px[j] = pre->px[g0 + j]; pr[j] = pre->pr[g0 + j];
-          pm[j] = pre->pm[g0 + j]; ph[j] = pre->ph[g0 + j];
-        }
-      } else if (side) {
-#pragma unroll
-        for (int j = 0; j < GRP; ++j) {
-          const int row = ((g0 + j) * NT + tid) / CPR;
-          const int m = p0 + row;
-          if (m < a.M && kc < a.K) {
-            const size_t o = (size_t)out_row(a, m) * a.K + kc;
-            if (a.add_src) {
-              const bf16_t* src = a.add_src + o;
-              if (a.add_stride > 1) {
-                int n, h, w;
-                out_nhw(a, m, n, h, w);
-                const int s = a.add_stride;
-                src = (h % s == 0 && w % s == 0)
-                          ? a.add_src + ((size_t)(n * a.add_H + h / s) * a.add_W + w / s) * a.K + kc
-                          : nullptr;
-              }
-              if (src) {
-                pa[j] = *(const uint4*)src;
-                ph[j] = true;
-              }
-            }
-            if (act) {
-              px[j] = *(const uint4*)(a.act_x + o);
-              if (amask) {
-                pm[j] = a.act_mask[o >> 3];
-                if (a.act_r) pr[j] = *(const uint4*)(a.act_r + o);
-              }
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < GRP; ++j) {
-        const int idx = (g0 + j) * NT + tid;
-        const int row = idx / CPR;
-        const int m = p0 + row;
-        const bool inb = m < a.M && kc < a.K;
-        if (EXACT || inb) {
-          uint4 v = *(const uint4*)(smem + row * OROW + chn * 16);
-          const size_t o = (size_t)(inb ? out_row(a, m) : m) * a.K + kc;
-          if constexpr (SACC) {
-            if (inb) {
-              const float q[8] = {lo_bf(v.x), hi_bf(v.x), lo_bf(v.y), hi_bf(v.y),
-                                  lo_bf(v.z), hi_bf(v.z), lo_bf(v.w), hi_bf(v.w)};
-#pragma unroll
-              for (int e = 0; e < 8; ++e) { ssum[e] += q[e]; ssq[e] = fmaf(q[e], q[e], ssq[e]); }
-            }
-          } else {
-            if (bstats && inb) {  // (sgx / sg double as the statistics accumulators: act is off here)
-              const float q[8] = {lo_bf(v.x), hi_bf(v.x), lo_bf(v.y), hi_bf(v.y),
-                                  lo_bf(v.z), hi_bf(v.z), lo_bf(v.w), hi_bf(v.w)};
-#pragma unroll
-              for (int e = 0; e < 8; ++e) { sgx[e] += q[e]; sg[e] = fmaf(q[e], q[e], sg[e]); }
-            }
-          }
-          if (inb && side) {
-            float f[8];
-            f[0] = lo_bf(v.x); f[1] = hi_bf(v.x); f[2] = lo_bf(v.y); f[3] = hi_bf(v.y);
-            f[4] = lo_bf(v.z); f[5] = hi_bf(v.z); f[6] = lo_bf(v.w); f[7] = hi_bf(v.w);
-            if (ph[j]) {
-              const uint4 r = pa[j];
-              f[0] += lo_bf(r.x); f[1] += hi_bf(r.x); f[2] += lo_bf(r.y); f[3] += hi_bf(r.y);
-              f[4] += lo_bf(r.z); f[5] += hi_bf(r.z); f[6] += lo_bf(r.w); f[7] += hi_bf(r.w);
-            }
-            if (act) {
-              const uint4 xu = px[j];
-              float xv[8];
-              xv[0] = lo_bf(xu.x); xv[1] = hi_bf(xu.x); xv[2] = lo_bf(xu.y); xv[3] = hi_bf(xu.y);
-              xv[4] = lo_bf(xu.z); xv[5] = hi_bf(xu.z); xv[6] = lo_bf(xu.w); xv[7] = hi_bf(xu.w);
-              if (amask) {
-                // block-output form: g = d(out) * bit, sums against the raw conv output (and the raw
-                // BN'd residual); out <- g (the producers' conv+BN backwards apply their scales)
-                const uint32_t mb = pm[j];
-                const uint4 ru = pr[j];
-                const float rv[8] = {lo_bf(ru.x), hi_bf(ru.x), lo_bf(ru.y), hi_bf(ru.y),
-                                     lo_bf(ru.z), hi_bf(ru.z), lo_bf(ru.w), hi_bf(ru.w)};
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                  const float g = (mb >> e) & 1u ? f[e] : 0.f;
-                  sgx[e] += g * xv[e];
-                  sg[e] += g;
-                  sgr[e] += g * rv[e];  // (rv = 0 without a BN'd residual)
-                  f[e] = g;
-                }
-              } else {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                  const float g = fmaf(xv[e], sc[e], sh[e]) > 0.f ? f[e] : 0.f;
-                  sgx[e] += g * xv[e];
-                  sg[e] += g;
-                  f[e] = a.act_unscaled ? g : g * sc[e];
-                }
-              }
-            }
-            v = make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
-          }
-          *(uint4*)(inb ? a.y + o : a.dump) = v;
-        }
-      }
-    }
-    if (act || bstats) {
-      // reduce the per-thread partial sums over the threads sharing this chunk column, one partial
-      // row per pixel tile (reduced over tiles by dtm_reduce_rows / stats_reduce_finalize)
-      epi_barrier<RAWB>();
-      float* red = (float*)smem;  // [NT][16]
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { red[tid * 16 + e] = sgx[e]; red[tid * 16 + 8 + e] = sg[e]; }
-      epi_barrier<RAWB>();
-      // every thread finishes one (chunk column, value) output: NT/CPR partials each, instead of CPR
-      // threads walking all NT rows of the table serially
-      const int rw = (act && a.act_r) ? 4 : 2;  // row width in K units
-      const bool fin = !act && a.fin_acc != nullptr;
-      float* prow = fin ? a.fin_acc + (size_t)(by % a.fin_G) * (2 * a.K)
-                        : (act ? a.act_sums : a.stats) + (size_t)by * (rw * a.K);
-      for (int o = tid; o < CPR * 16; o += NT) {
-        const int c = o >> 4, e = o & 15;
-        float t = 0.f;
-#pragma unroll 4
-        for (int k = 0; k < NT / CPR; ++k) t += red[((c + k * CPR) << 4) + e];
-        const int kk = c0 + c * 8 + (e & 7);
-        if (kk < a.K) {
-          if (fin) atomicAdd(prow + (e < 8 ? 0 : a.K) + kk, t);
-          else prow[(e < 8 ? 0 : a.K) + kk] = t;
-        }
-      }
-      if (fin) {
-        // hand-off: every wave's atomics are performed (its own vmcnt drained) before the block's count;
-        // the totals are read back with memory-side atomics (never a stale L2 line of another XCD)
-        __builtin_amdgcn_s_waitcnt(0);
-        epi_barrier<RAWB>();
-        // (the flag lives in the kernel's one LDS array: a second __shared__ object would make hipcc add
-        //  vmcnt drains to the LDS-DMA main loops)
-        int* fin_last = (int*)smem;
-        if (tid == 0)
-          *fin_last = __hip_atomic_fetch_add(a.fin_counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                      gridDim.x * gridDim.y - 1;
-        epi_barrier<RAWB>();
-        if (*fin_last) {
-          for (int c = tid; c < a.K; c += NT) {
-            float sum = 0.f, sq = 0.f;
-            for (int g = 0; g < a.fin_G; ++g) {
-              sum += atomicExch(a.fin_acc + (size_t)g * 2 * a.K + c, 0.f);
-              sq += atomicExch(a.fin_acc + (size_t)g * 2 * a.K + a.K + c, 0.f);
-            }
-            bn_fin_channel(sum, sq, c, a.K, a.fin_gamma, a.fin_beta, a.fin_mm, a.fin_mv, a.fin_ss, a.fin_count,
-                           a.fin_eps, a.fin_decay, a.fin_update, a.fin_bessel);
-          }
-          if (tid == 0) __hip_atomic_store(a.fin_counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-      if (act && a.act_r) {  // second round: [sum g*r | sum g] of the BN'd residual
-        epi_barrier<RAWB>();
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { red[tid * 16 + e] = sgr[e]; red[tid * 16 + 8 + e] = sg[e]; }
-        epi_barrier<RAWB>();
-        for (int o = tid; o < CPR * 16; o += NT) {
-          const int c = o >> 4, e = o & 15;
-          float t = 0.f;
-#pragma unroll 4
-          for (int k = 0; k < NT / CPR; ++k) t += red[((c + k * CPR) << 4) + e];
-          const int kk = c0 + c * 8 + (e & 7);
-          if (kk < a.K) prow[2 * a.K + (e < 8 ? 0 : a.K) + kk] = t;
-        }
-      }
-    }
-  }
+  if constexpr (staged) conv_nt_epi_tail<PT, CT, RAWB, EXACT, SACC, NT>(a, smem, p0, c0, by, ssum, ssq);
 }
 
-template <int PT, int CT, int WP, int WC, int UD, int NBUF, bool PRE = false>
+// Epilogue of the 32x32x16-MFMA kernels (staged stores only: K % 8 == 0).  Register layout of a 32x32
+// accumulator: lane holds pixel (lane & 31) and, in register quad q, the 4 consecutive channels
+// 8q + 4 (lane >> 5) .. +3 - so each quad is staged like one 16x16 subtile's 8-B lane write.
+template <int PT, int CT, int WP, int WC, int NT = 256>
+__device__ __forceinline__ void conv_nt_epilogue32(const ConvNTArgs& a, f32x16 (&acc)[WC / 32][WP / 32], char* smem,
+                                                   int p0, int c0, int by) {
+  constexpr int NWP = PT / WP;
+  constexpr int TP = WP / 32, TC = WC / 32;
+  constexpr int OROW = CT * 2 + 16;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wp = wave % NWP, wc = wave / NWP;
+  const int fr = lane & 31, fh = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < TC; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int kloc = wc * WC + i * 32 + 8 * q + 4 * fh;
+      const int kch = c0 + kloc;
+      float bia[4] = {0.f, 0.f, 0.f, 0.f};
+      if (a.bias && kch < a.K) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bia[r] = a.bias[kch + r];
+      }
+#pragma unroll
+      for (int j = 0; j < TP; ++j) {
+        const int mloc = wp * WP + j * 32 + fr;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[i][j][4 * q + r] + bia[r];
+          if (a.relu) v[r] = fmaxf(v[r], 0.f);
+        }
+        *(uint2*)(smem + mloc * OROW + kloc * 2) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+      }
+    }
+  conv_nt_epi_tail<PT, CT, false, false, false, NT>(a, smem, p0, c0, by, nullptr, nullptr);
+}
+
+template <int PT, int CT, int WP, int WC, int UD, int NBUF>
 __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
   constexpr int BK = 64;
   constexpr int NWP = PT / WP;
@@ -620,37 +569,19 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
   gload(0, st);
   swrite(0, st);
   __syncthreads();
-  // dgrad epilogue side inputs issued before the last k-tile's MFMAs (a.pre_side, staged stores only)
-  constexpr int NIT = PT * (CT / 8) / 256;
-  EpiSide<PRE ? NIT : 1> sd;
   for (int kt = 0; kt < nk; ++kt) {
-    if constexpr (PRE) {
-      if (kt == nk - 1) epi_side_load<PT, CT, 256>(a, p0, c0, sd);
-    }
-    // (PRE, last k-tile: a raw barrier - __syncthreads() would also drain the side-input loads just issued)
-    const bool raw_last = PRE && kt == nk - 1;
     if constexpr (NBUF == 2) {
       const int cur = kt & 1;
       if (kt + 1 < nk) gload(kt + 1, st);
       compute(cur);
       if (kt + 1 < nk) swrite(cur ^ 1, st);
-      if (raw_last) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-      } else {
-        __syncthreads();
-      }
+      __syncthreads();
     } else {
       // single LDS buffer (less LDS -> more resident blocks for short-K layers): the next tile's
       // global loads still overlap the MFMAs; the LDS write waits for every wave's reads
       if (kt + 1 < nk) gload(kt + 1, st);
       compute(0);
-      if (raw_last) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-      } else {
-        __syncthreads();
-      }
+      __syncthreads();
       if (kt + 1 < nk) {
         swrite(0, st);
         __syncthreads();
@@ -659,141 +590,10 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
   }
 
   static_assert(PT * (CT * 2 + 16) <= NBUF * BUF, "output staging fits in the operand buffers");
-  // (PRE: raw-barrier epilogue, so the side loads stay in flight until their registers are used)
-  if constexpr (PRE) conv_nt_epilogue<PT, CT, WP, WC, 1, true>(a, acc, smem, p0, c0, by, nullptr, nullptr, &sd);
-  else if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1>(a, acc, smem, p0, c0, by);
-  else conv_nt_epilogue<PT, CT, WP, WC, 2>(a, acc, smem, p0, c0, by);
-}
-
-
-// LDS-DMA variant (no input prologue): both operand tiles go global -> LDS with
-// global_load_lds_dwordx4 (no VGPR round trip, no ds_write pass).  One wave-instruction writes 1 KiB
-// = 8 rows x 128 B contiguously (lane i at +16 i), so the XOR swizzle of the LDS image (chunk ^ row&7)
-// is applied on the SOURCE side: lane i loads logical chunk (i&7) ^ (i>>3) of row i>>3 of its group,
-// a chunk index that is fixed per lane for every group and k-tile.  Padding / out-of-range chunks
-// are loaded from a zero buffer.  Two LDS buffers; the DMA of k-tile t+1 is in flight during the
-// MFMAs of tile t; one barrier per k-tile (each wave drains its own DMA, vmcnt(0), before it).
-// Measured (tools/conv_microbench.py, DTM_CONV_TILE=10..12): 5-10 % faster than the register-staged
-// kernel on isolated deep-reduction layers, neutral inside the ResNet-50 step -> opt-in only.
-template <int PT, int CT, int WP, int WC, int UD>
-__global__ __launch_bounds__(256) void conv_nt_dma_kernel(ConvNTArgs a) {
-  constexpr int BK = 64;
-  constexpr int NWP = PT / WP;
-  constexpr int NWC = CT / WC;
-  static_assert(NWP * NWC == 4, "4 waves");
-  constexpr int TP = WP / 16, TC = WC / 16;
-  constexpr int AI = PT / 32, WI = CT / 32;  // 8-row DMA groups per wave per k-tile
-  constexpr int BUF = (PT + CT) * 128;
-  constexpr int OROW = CT * 2 + 16;
-  constexpr int SM = 2 * BUF > PT * OROW ? 2 * BUF : PT * OROW;
-  __shared__ __attribute__((aligned(16))) char smem[SM];
-  typedef __attribute__((address_space(1))) const void gvoid;
-  typedef __attribute__((address_space(3))) void lvoid;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tile = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
-  const int bx = tile % gridDim.x, by = tile / gridDim.x;
-  const int p0 = by * PT, c0 = bx * CT;
-  const int lr = lane >> 3;
-  const int ch = (lane & 7) ^ lr;
-
-  int ih0[AI], iw0[AI], pixbase[AI];
-#pragma unroll
-  for (int j = 0; j < AI; ++j) {
-    const int m = p0 + 8 * (wave + 4 * j) + lr;
-    if (m < a.M) {
-      uint32_t n = fdiv((uint32_t)m, a.fd_PQ);
-      uint32_t rem = m - n * (a.P * a.Q);
-      uint32_t p = fdiv(rem, a.fd_Q);
-      uint32_t q = rem - p * a.Q;
-      ih0[j] = (int)p * a.stride - a.pad_h;
-      iw0[j] = (int)q * a.stride - a.pad_w;
-      pixbase[j] = (int)n * a.Hin * a.Win;
-    } else {
-      ih0[j] = -(1 << 28);
-      iw0[j] = -(1 << 28);
-      pixbase[j] = 0;
-    }
-  }
-  int cc = (ch * 8) % a.C;
-  int tap = (ch * 8) / a.C;
-  int rr = tap / a.S, ss = tap - (tap / a.S) * a.S;
-  const char* xg = (const char*)a.x;
-  const char* wg = (const char*)a.w;
-  const char* zg = (const char*)a.zero;
-
-  auto issue = [&](int kt, int buf) {
-    char* base = smem + buf * BUF;
-    const int k = kt * BK + ch * 8;
-    const bool kin = k < a.Kg;
-#pragma unroll
-    for (int j = 0; j < AI; ++j) {
-      const int ihv = ih0[j] + rr, iwv = iw0[j] + ss;
-      bool v = kin && ihv >= 0 && ihv < a.Hv && iwv >= 0 && iwv < a.Wv;
-      if (UD > 1) v = v && ((ihv % UD) == 0) && ((iwv % UD) == 0);
-      const int ih = UD > 1 ? ihv / UD : ihv, iw = UD > 1 ? iwv / UD : iwv;
-      const char* src = v ? xg + (size_t)((pixbase[j] + ih * a.Win + iw) * a.pix_bytes + cc * 2) : zg;
-      __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(base + (wave + 4 * j) * 1024), 16, 0, 0);
-    }
-#pragma unroll
-    for (int j = 0; j < WI; ++j) {
-      const int row = c0 + 8 * (wave + 4 * j) + lr;
-      const bool v = kin && row < a.K;
-      const char* src = v ? wg + ((size_t)row * a.Kg + k) * 2 : zg;
-      __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(base + PT * 128 + (wave + 4 * j) * 1024), 16, 0, 0);
-    }
-    cc += BK;
-    while (cc >= a.C) {
-      cc -= a.C;
-      if (++ss == a.S) { ss = 0; ++rr; }
-    }
-  };
-
-  f32x4 acc[TC][TP];
-#pragma unroll
-  for (int i = 0; i < TC; ++i)
-#pragma unroll
-    for (int j = 0; j < TP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  const int wp = wave % NWP, wc = wave / NWP;
-  const int fr = lane & 15, fk = lane >> 4;
-  auto compute = [&](int cur) {
-    const char* base = smem + cur * BUF;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      short8 bf[TP], af[TC];
-#pragma unroll
-      for (int j = 0; j < TP; ++j) {
-        int row = wp * WP + j * 16 + fr;
-        int chn = ks * 4 + fk;
-        bf[j] = *(const short8*)(base + row * 128 + ((chn ^ (row & 7)) << 4));
-      }
-#pragma unroll
-      for (int i = 0; i < TC; ++i) {
-        int row = wc * WC + i * 16 + fr;
-        int chn = ks * 4 + fk;
-        af[i] = *(const short8*)(base + PT * 128 + row * 128 + ((chn ^ (row & 7)) << 4));
-      }
-#pragma unroll
-      for (int i = 0; i < TC; ++i)
-#pragma unroll
-        for (int j = 0; j < TP; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
-    }
-  };
-
-  const int nk = (a.Kg + BK - 1) / BK;
-  issue(0, 0);
-  for (int kt = 0; kt < nk; ++kt) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // tile kt landed for every wave; buffer (kt+1)&1 is no longer read
-    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
-    compute(kt & 1);
-  }
-  __syncthreads();  // the epilogue reuses the operand buffers
   if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1>(a, acc, smem, p0, c0, by);
   else conv_nt_epilogue<PT, CT, WP, WC, 2>(a, acc, smem, p0, c0, by);
 }
+
 
 // Deep-K pipelined variant: both operand tiles go global -> LDS by LDS-DMA into an NS-slot ring with
 // ONE raw s_barrier per k-tile and a counted vmcnt, so NS-2 k-tiles stay in flight across the
@@ -805,7 +605,7 @@ __global__ __launch_bounds__(256) void conv_nt_dma_kernel(ConvNTArgs a) {
 // array (a second object makes hipcc drain vmcnt before the fragment reads).
 // NWP: waves along the pixel dimension (4 / NWP along channels); NWP = 4 with PT = 512, CT = 64 gives every
 // wave a 128 x 64 tile (the 64-channel 3x3 layers: 2x the MFMAs per LDS byte of the 2x2 layout's 64x32)
-template <int PT, int CT, int NS, int UD, bool PRO, int NWP = 2>
+template <int PT, int CT, int NS, int UD, bool PRO, int NWP = 2, bool M32 = false>
 __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
   constexpr int BK = 64;
   constexpr int WP = PT / NWP, WC = CT / (4 / NWP);
@@ -929,18 +729,53 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
     }
   };
 
-  f32x4 acc[TC][TP];
+  constexpr int TP32 = M32 ? WP / 32 : 1, TC32 = M32 ? WC / 32 : 1;
+  f32x4 acc[M32 ? 1 : TC][M32 ? 1 : TP];
+  f32x16 acc32[TC32][TP32];
+  if constexpr (M32) {
 #pragma unroll
-  for (int i = 0; i < TC; ++i)
+    for (int i = 0; i < TC32; ++i)
 #pragma unroll
-    for (int j = 0; j < TP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < TP32; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc32[i][j][r] = 0.f;
+  } else {
+#pragma unroll
+    for (int i = 0; i < TC; ++i)
+#pragma unroll
+      for (int j = 0; j < TP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
 
   const int wp = wave % NWP, wc = wave / NWP;
   const int fr = lane & 15, fk = lane >> 4;
   auto compute = [&](int slot) {
+    const char* base = smem + slot * BUF;
+    if constexpr (M32) {  // 32x32x16 (see conv_nt_w8_kernel)
+      const int f32r = lane & 31, fh = lane >> 5;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int chn = ks * 2 + fh;
+        short8 bf[TP32], af[TC32];
+#pragma unroll
+        for (int j = 0; j < TP32; ++j) {
+          const int row = wp * WP + j * 32 + f32r;
+          bf[j] = *(const short8*)(base + row * 128 + ((chn ^ (row & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < TC32; ++i) {
+          const int row = wc * WC + i * 32 + f32r;
+          af[i] = *(const short8*)(base + PT * 128 + row * 128 + ((chn ^ (row & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < TC32; ++i)
+#pragma unroll
+          for (int j = 0; j < TP32; ++j)
+            acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc32[i][j], 0, 0, 0);
+      }
+      return;
+    }
     // all 2 x (TP + TC) fragment reads of the k-tile first: the ks = 1 reads are in flight under the
     // ks = 0 MFMAs (counted lgkmcnt) instead of a full LDS round trip between the two halves
-    const char* base = smem + slot * BUF;
     short8 bf[2][TP], af[2][TC];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -985,7 +820,8 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // the epilogue reuses the ring
-  if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1>(a, acc, smem, p0, c0, by);
+  if constexpr (M32) conv_nt_epilogue32<PT, CT, WP, WC>(a, acc32, smem, p0, c0, by);
+  else if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1>(a, acc, smem, p0, c0, by);
   else conv_nt_epilogue<PT, CT, WP, WC, 2>(a, acc, smem, p0, c0, by);
 }
 
@@ -996,7 +832,10 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
 // (MI355X_MICROARCH: ~34.5 TB/s chip-wide); a 256x256 block halves the L2 bytes per MFMA (256x128: 0.75x).
 // Same LDS image / source-side swizzle / counted-vmcnt ring as conv_nt_pipe_kernel (no input prologue);
 // one 8-row x 128-B LDS-DMA group per wave-instruction, AI + WI of them per wave per k-tile.
-template <int PT, int CT, int NWP, int NS, int UD>
+// M32: v_mfma_f32_32x32x16_bf16 instead of 16x16x32 (same LDS image, same FLOPs per k-tile, half the MFMA
+// instructions and half the operand-register reads per FLOP; tools/mfma_ab.hip measures it 16-60 % faster
+// on this inner-loop pattern); needs K % 8 == 0 (staged epilogue).
+template <int PT, int CT, int NWP, int NS, int UD, bool M32 = false>
 __global__ __launch_bounds__(512) void conv_nt_w8_kernel(ConvNTArgs a) {
   constexpr int NT = 512, NW = 8;
   constexpr int BK = 64;
@@ -1073,16 +912,52 @@ __global__ __launch_bounds__(512) void conv_nt_w8_kernel(ConvNTArgs a) {
     }
   };
 
-  f32x4 acc[TC][TP];
+  constexpr int TP32 = M32 ? WP / 32 : 1, TC32 = M32 ? WC / 32 : 1;
+  f32x4 acc[M32 ? 1 : TC][M32 ? 1 : TP];
+  f32x16 acc32[TC32][TP32];
+  if constexpr (M32) {
 #pragma unroll
-  for (int i = 0; i < TC; ++i)
+    for (int i = 0; i < TC32; ++i)
 #pragma unroll
-    for (int j = 0; j < TP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < TP32; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc32[i][j][r] = 0.f;
+  } else {
+#pragma unroll
+    for (int i = 0; i < TC; ++i)
+#pragma unroll
+      for (int j = 0; j < TP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
 
   const int wp = wave % NWP, wc = wave / NWP;
   const int fr = lane & 15, fk = lane >> 4;
   auto compute = [&](int slot) {
     const char* base = smem + slot * BUF;
+    if constexpr (M32) {
+      // k16 steps; lane: row lane & 31, 16-B chunk 2 ks + (lane >> 5) of the swizzled 128-B row
+      const int f32r = lane & 31, fh = lane >> 5;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int chn = ks * 2 + fh;
+        short8 bf[TP32], af[TC32];
+#pragma unroll
+        for (int j = 0; j < TP32; ++j) {
+          const int row = wp * WP + j * 32 + f32r;
+          bf[j] = *(const short8*)(base + row * 128 + ((chn ^ (row & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < TC32; ++i) {
+          const int row = wc * WC + i * 32 + f32r;
+          af[i] = *(const short8*)(base + PT * 128 + row * 128 + ((chn ^ (row & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < TC32; ++i)
+#pragma unroll
+          for (int j = 0; j < TP32; ++j)
+            acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc32[i][j], 0, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int chn = ks * 4 + fk;
@@ -1124,7 +999,8 @@ __global__ __launch_bounds__(512) void conv_nt_w8_kernel(ConvNTArgs a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // the epilogue reuses the ring
-  if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1, false, false, false, false, NT>(a, acc, smem, p0, c0, by);
+  if constexpr (M32) conv_nt_epilogue32<PT, CT, WP, WC, NT>(a, acc32, smem, p0, c0, by);
+  else if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1, false, false, false, false, NT>(a, acc, smem, p0, c0, by);
   else conv_nt_epilogue<PT, CT, WP, WC, 2, false, false, false, false, NT>(a, acc, smem, p0, c0, by);
 }
 
@@ -1864,23 +1740,17 @@ static const bf16_t* zero_chunk() {
   return (const bf16_t*)z;
 }
 
-template <int PT, int CT, int WP, int WC, int UD>
-static void launch_nt_dma(const ConvNTArgs& a, hipStream_t st) {
-  dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT);
-  hipLaunchKernelGGL((conv_nt_dma_kernel<PT, CT, WP, WC, UD>), grid, dim3(256), 0, st, a);
-}
-
-template <int PT, int CT, int NWP, int NS, int UD>
+template <int PT, int CT, int NWP, int NS, int UD, bool M32 = false>
 static void launch_w8(const ConvNTArgs& a, hipStream_t st) {
   dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT);
-  hipLaunchKernelGGL((conv_nt_w8_kernel<PT, CT, NWP, NS, UD>), grid, dim3(512), 0, st, a);
+  hipLaunchKernelGGL((conv_nt_w8_kernel<PT, CT, NWP, NS, UD, M32>), grid, dim3(512), 0, st, a);
 }
 
-template <int PT, int CT, int NS, int UD, int NWP = 2>
+template <int PT, int CT, int NS, int UD, int NWP = 2, bool M32 = false>
 static void launch_pipe(const ConvNTArgs& a, hipStream_t st) {
   dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT);
-  if (a.in_scale) hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, true, NWP>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, false, NWP>), grid, dim3(256), 0, st, a);
+  if (a.in_scale) hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, true, NWP, M32>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, false, NWP, M32>), grid, dim3(256), 0, st, a);
 }
 
 static int device_cus() {
@@ -1951,16 +1821,14 @@ static bool stream_ok(const ConvNTArgs& a) {
 template <int PT, int CT, int WP, int WC, int UD, int NBUF = 2>
 static void launch_nt(const ConvNTArgs& a, hipStream_t st) {
   dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT);
-  // dgrads with epilogue side inputs: the variant that loads them before the last k-tile (a.pre_side)
-  if (a.pre_side && (a.K & 7) == 0 && (a.add_src || a.act_x))
-    hipLaunchKernelGGL((conv_nt_kernel<PT, CT, WP, WC, UD, NBUF, true>), grid, dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((conv_nt_kernel<PT, CT, WP, WC, UD, NBUF>), grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((conv_nt_kernel<PT, CT, WP, WC, UD, NBUF>), grid, dim3(256), 0, st, a);
 }
 
-// tile variants: 0 = 128 pix x 128 ch (4 waves 2x2 of 64x64), 1 = 128 x 64 (4x1 of 32x64),
-// 2 = 64 x 128 (2x2 of 32x64; 3 blocks/CU by LDS), 3 / 4 = 1 / 2 with a single LDS buffer
-// (more resident blocks); 10-12 = LDS-DMA 128x128 / 64x128 / 128x64 (opt-in).  DTM_CONV_TILE forces one.
+// tile variants (the ones the shape policy uses; the rejected ones and their A/B logs are listed in
+// profiles/ab/README.md): 0 = 128 pix x 128 ch register-staged (4 waves 2x2 of 64x64), 3 / 4 = 128 x 64 /
+// 64 x 128 register-staged with a single LDS buffer (more resident blocks), 21 / 24 / 26 / 32 = LDS-DMA
+// pipelined 128x128 / 256x64 / 128x64 / 256x32, 30 / 31 = the persistent streaming 1x1 kernel (128 / 64
+// channels), 40 = the 8-wave 256x256 tile.  DTM_CONV_TILE forces one (sweeps: tools/conv_tile_sweep.py).
 struct TileCfg {
   int id, PT, NWP;
 };
@@ -1976,15 +1844,17 @@ DTM_API void dtm_conv_set_kwide(int on) { g_kwide = on; }
 DTM_API void dtm_conv_set_w8(int on) { g_tile_w8 = on; }
 static int g_k64_tile = 3;  // tile of the 64-output-channel layers (A/B knob: dtm_conv_set_k64_tile)
 DTM_API void dtm_conv_set_k64_tile(int id) { g_k64_tile = id; }
-static int g_pre_side = 0;  // A/B knob: early side-input loads in the register-staged dgrad epilogue
-DTM_API void dtm_conv_set_pre_side(int on) { g_pre_side = on; }
 static int g_k32_tile = 1;  // A/B knob: the 256x32 tile for <= 32-channel spatial convs (dtm_conv_set_k32)
 DTM_API void dtm_conv_set_k32(int on) { g_k32_tile = on; }
-static int g_stream128_act = 0;  // A/B knob (dtm_conv_set_stream128_act)
-DTM_API void dtm_conv_set_stream128_act(int on) { g_stream128_act = on; }
 static int g_act_tile = -1;  // A/B knob: tile of the dgrads with a fused activation-backward epilogue (-1 = policy)
 DTM_API void dtm_conv_set_act_tile(int id) { g_act_tile = id; }
+static int g_mfma32 = -1;  // -1: DTM_MFMA32 env (default on once measured), 0 / 1: A/B knob
+DTM_API void dtm_conv_set_mfma32(int on) { g_mfma32 = on; }
 static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
+  if (g_mfma32 < 0) {
+    const char* e = getenv("DTM_MFMA32");
+    g_mfma32 = e ? atoi(e) : 0;
+  }
   if (g_tile_env == -2) {
     const char* e = getenv("DTM_CONV_TILE");
     g_tile_env = e ? atoi(e) : -1;
@@ -2001,9 +1871,6 @@ static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
   else if (id == -1 && a.Kg == 64 && stream_ok(a) && (g_stream_act || !a.act_x) &&
            (!g_policy2 || a.K % 128 == 0 || a.K <= 64))  // (v2: no partial channel tiles: 35x35 ->288 -33 %)
     id = a.K >= 128 ? 30 : 31;
-  // A/B knob: the persistent streaming kernel also for the 128-deep dgrads with a fused epilogue (ResNet
-  // stage-2 block-output dgrads: epilogue-dominated HBM streams)
-  else if (id == -1 && g_stream128_act && a.Kg == 128 && a.act_x && stream_ok(a) && a.K % 128 == 0) id = 30;
   if (id == -1 && a.act_x && g_act_tile >= 0) id = g_act_tile;  // (A/B: the non-streaming act dgrads)
   // (the persistent streaming 1x1 kernel: the 64-deep 56x56 expand / reduce layers and their dgrads are
   // HBM streams: -20..-33 % (tools/conv_tile_sweep.py); at Kg 128 its 1 block/CU loses)
@@ -2042,64 +1909,57 @@ static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
   // (profiles/r2_conv_tiles_k64.txt: -4 % vs the register-staged single-buffer tile)
   if (id == -1 && !a.in_scale && a.K <= 64 && a.R * a.S > 1 && a.K % 64 == 0) id = 26;
   if (id < 0) id = a.K <= 64 ? g_k64_tile : ((a.M <= 16384 && a.Kg >= 2048) ? 0 : 4);
-  // LDS-DMA variants (10-12, opt-in) need an operand without the prologue affine
-  if (id >= 10 && id < 20 && a.in_scale) id = a.K <= 64 ? 3 : 4;
-  // pipelined LDS-DMA variants (20-23) stage the prologue affine in LDS: C <= 512
-  if (id >= 20 && id < 30 && a.in_scale && a.C > 512) id = 0;
-  if (id >= 20 && id <= 23) return {id, 128, 2};
-  if (id == 24 || id == 25) return {id, 256, 2};  // 256 x 64 pipelined (waves 2x2 of 128x32), 2 / 3 slots
-  if (id == 26) return {id, 128, 2};              // 128 x 64 pipelined, 2 slots
-  if (id == 27) return {id, 256, 2};              // 256 x 128 pipelined, waves 2x2 of 128x64
-  if (id == 28) return {id, 512, 4};              // 512 x 64 pipelined, waves 4x1 of 128x64
-  if (id == 29) return {id, 256, 4};              // 256 x 64 pipelined, waves 4x1 of 64x64
+  // the 32x32x16-MFMA forms of the LDS-DMA tiles (A/B knob dtm_conv_set_mfma32 / DTM_MFMA32; staged
+  // epilogue only: K % 8 == 0)
+  if (g_mfma32 && (a.K & 7) == 0) {
+    if (id == 40) id = 50;
+    else if (id == 21) id = 51;
+    else if (id == 26) id = 52;
+    else if (id == 24) id = 53;
+    else if (id == 32) id = 54;
+  }
+  if (id >= 50 && id <= 54 && (a.K & 7) != 0) id = 0;
+  if (id >= 51 && id <= 54 && a.in_scale && a.C > 512) id = 0;
+  // pipelined LDS-DMA tiles stage the prologue affine in LDS: C <= 512
+  if ((id == 21 || id == 24 || id == 26 || id == 32) && a.in_scale && a.C > 512) id = 0;
+  if (id == 21 || id == 26) return {id, 128, 2};  // 128 x 128 / 128 x 64 pipelined, 2 slots
+  if (id == 24) return {id, 256, 2};              // 256 x 64 pipelined (waves 2x2 of 128x32)
   if (id == 32) return {id, 256, 4};              // 256 x 32 pipelined, waves 4x1 of 64x32
-  // 8-wave 256-pixel tiles (no prologue): 40 = 256x256 (waves 2x4), 41 = 256x128 3-slot (4x2),
-  // 42 = 256x128 2-slot, 43 = 256x256 (waves 4x2)
-  if (id >= 40 && id <= 43 && a.in_scale) id = 0;
-  if (id == 40) return {id, 256, 2};
-  if (id == 41 || id == 42 || id == 43) return {id, 256, 4};
+  // 8-wave 256x256 tile (waves 2x4), no prologue
+  if ((id == 40 || id == 50) && a.in_scale) id = 0;
+  if (id == 40 || id == 50) return {id, 256, 2};
+  if (id == 51 || id == 52) return {id, 128, 2};
+  if (id == 53) return {id, 256, 2};
+  if (id == 54) return {id, 256, 4};
   if (id == 30 || id == 31) {
     if (stream_ok(a)) return {id, 64, 2};
     id = a.K <= 64 ? 3 : 4;
   }
-  if (id == 1 || id == 3) return {id, 128, 4};
-  if (id == 2 || id == 4) return {id, 64, 2};
-  if (id == 10) return {id, 128, 2};
-  if (id == 11) return {id, 64, 2};
-  if (id == 12) return {id, 128, 4};
+  if (id == 3) return {id, 128, 4};
+  if (id == 4) return {id, 64, 2};
   return {0, 128, 2};
 }
 
 template <int UD>
 static void dispatch_ud(const ConvNTArgs& a, const TileCfg& t, hipStream_t st) {
-  if (t.id == 1) launch_nt<128, 64, 32, 64, UD>(a, st);
-  else if (t.id == 2) launch_nt<64, 128, 32, 64, UD>(a, st);
-  else if (t.id == 3) launch_nt<128, 64, 32, 64, UD, 1>(a, st);
+  if (t.id == 3) launch_nt<128, 64, 32, 64, UD, 1>(a, st);
   else if (t.id == 4) launch_nt<64, 128, 32, 64, UD, 1>(a, st);
-  else if (t.id == 10) launch_nt_dma<128, 128, 64, 64, UD>(a, st);
-  else if (t.id == 11) launch_nt_dma<64, 128, 32, 64, UD>(a, st);
-  else if (t.id == 12) launch_nt_dma<128, 64, 32, 64, UD>(a, st);
   else if (t.id == 30 && UD == 1) {
     if (a.Kg <= 64) launch_stream<128, 1>(a, st);
     else launch_stream<128, 2>(a, st);
   } else if (t.id == 31 && UD == 1) {
     if (a.Kg <= 64) launch_stream<64, 1>(a, st);
     else launch_stream<64, 2>(a, st);
-  } else if (t.id == 20) launch_pipe<128, 128, 3, UD>(a, st);
-  else if (t.id == 21) launch_pipe<128, 128, 2, UD>(a, st);
-  else if (t.id == 22) launch_pipe<128, 128, 4, UD>(a, st);
-  else if (t.id == 23) launch_pipe<128, 64, 3, UD>(a, st);
+  } else if (t.id == 21) launch_pipe<128, 128, 2, UD>(a, st);
   else if (t.id == 24) launch_pipe<256, 64, 2, UD>(a, st);
-  else if (t.id == 25) launch_pipe<256, 64, 3, UD>(a, st);
   else if (t.id == 26) launch_pipe<128, 64, 2, UD>(a, st);
-  else if (t.id == 27) launch_pipe<256, 128, 2, UD>(a, st);     // waves 2x2 of 128x64
-  else if (t.id == 28) launch_pipe<512, 64, 2, UD, 4>(a, st);   // waves 4x1 of 128x64
-  else if (t.id == 29) launch_pipe<256, 64, 2, UD, 4>(a, st);   // waves 4x1 of 64x64
   else if (t.id == 32) launch_pipe<256, 32, 2, UD, 4>(a, st);   // waves 4x1 of 64x32 (32-channel outputs)
   else if (t.id == 40) launch_w8<256, 256, 2, 2, UD>(a, st);
-  else if (t.id == 41) launch_w8<256, 128, 4, 3, UD>(a, st);
-  else if (t.id == 42) launch_w8<256, 128, 4, 2, UD>(a, st);
-  else if (t.id == 43) launch_w8<256, 256, 4, 2, UD>(a, st);
+  else if (t.id == 50) launch_w8<256, 256, 2, 2, UD, true>(a, st);
+  else if (t.id == 51) launch_pipe<128, 128, 2, UD, 2, true>(a, st);
+  else if (t.id == 52) launch_pipe<128, 64, 2, UD, 2, true>(a, st);
+  else if (t.id == 53) launch_pipe<256, 64, 2, UD, 2, true>(a, st);
+  else if (t.id == 54) launch_pipe<256, 32, 2, UD, 4, true>(a, st);
   else launch_nt<128, 128, 64, 64, UD>(a, st);
 }
 
@@ -2113,27 +1973,9 @@ static void dispatch_nt(const ConvNTArgs& a, int ud, const TileCfg& t, hipStream
 
 DTM_API int dtm_get_deterministic();
 
-// BatchNorm finalize parameters for the statistics epilogue's hand-off (ConvNTArgs::fin_acc)
-struct FinArgs {
-  float* acc;
-  unsigned* counter;
-  int G, update, bessel;
-  const float* gamma;
-  const float* beta;
-  float* mm;
-  float* mv;
-  float* ss;
-  float count, eps, decay;
-};
-static int g_fin_fuse = 0;  // A/B knob: BN finalize in the conv statistics epilogue (dtm_conv_set_fin_fuse)
-DTM_API void dtm_conv_set_fin_fuse(int on) { g_fin_fuse = on; }
-static float* g_cfin_acc = nullptr;
-static unsigned* g_cfin_counter = nullptr;
-static size_t g_cfin_floats = 0;
-
 static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, const float* bias, const float* in_scale,
                          const float* in_shift, int relu, const ConvDesc* d, hipStream_t stream, float** rows_ws,
-                         int* nrows, const FinArgs* fin = nullptr, bool* fused = nullptr) {
+                         int* nrows) {
   if (d->C % 8 || d->K % 4) return -1;
   ConvNTArgs a;
   a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.y = (bf16_t*)y;
@@ -2154,19 +1996,8 @@ static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, cons
   a.M = d->N * d->P * d->Q; a.Kg = d->R * d->S * d->C; a.relu = relu;
   a.fd_PQ = make_fastdiv(d->P * d->Q); a.fd_Q = make_fastdiv(d->Q);
   a.ostr = 1; a.oa = a.ob = 0; a.OH = a.P; a.OW = a.Q;
-  a.pre_side = 0;
-  a.fin_acc = nullptr; a.fin_counter = nullptr;
-  if (fin && stats) {
-    a.fin_acc = fin->acc; a.fin_counter = fin->counter; a.fin_G = fin->G;
-    a.fin_gamma = fin->gamma; a.fin_beta = fin->beta; a.fin_mm = fin->mm; a.fin_mv = fin->mv; a.fin_ss = fin->ss;
-    a.fin_count = fin->count; a.fin_eps = fin->eps; a.fin_decay = fin->decay;
-    a.fin_update = fin->update; a.fin_bessel = fin->bessel;
-  }
   int rows = 0;
   const TileCfg tc = pick_tile(a, stats);
-  // the hand-off needs the staged epilogue's per-tile statistics (not the streaming kernel's per-worker rows)
-  if (a.fin_acc && (tc.id == 30 || tc.id == 31 || (a.K & 7) != 0)) a.fin_acc = nullptr;
-  if (fused) *fused = a.fin_acc != nullptr;
   if (stats) {
     // one per streaming worker; one per pixel tile (staged epilogue, K % 8 == 0); else per (pixel tile, pixel wave)
     rows = (tc.id == 30 || tc.id == 31) ? stream_rows(a, tc.id)
@@ -2201,29 +2032,8 @@ DTM_API int dtm_conv_fwd_bn(const void* x, const void* w, void* y, const float* 
                             void* stream) {
   float* ws = nullptr;
   int rows = 0;
-  FinArgs fa{};
-  const FinArgs* fp = nullptr;
-  if (g_fin_fuse && !dtm_get_deterministic()) {
-    // replicas spread the per-tile atomics (fewer blocks per address), at most 8 K floats in all
-    const int G = d->K >= 4096 ? 1 : (8192 / (2 * d->K) < 16 ? 8192 / (2 * d->K) : 16);
-    const size_t need = (size_t)G * 2 * d->K;
-    if (need > g_cfin_floats) {
-      hipDeviceSynchronize();
-      if (g_cfin_acc) hipFree(g_cfin_acc);
-      if (!g_cfin_counter && hipMalloc(&g_cfin_counter, 64) != hipSuccess) return -4;
-      if (hipMalloc(&g_cfin_acc, need * sizeof(float)) != hipSuccess) { g_cfin_acc = nullptr; g_cfin_floats = 0; return -4; }
-      hipMemset(g_cfin_acc, 0, need * sizeof(float));
-      hipMemset(g_cfin_counter, 0, 64);
-      hipDeviceSynchronize();
-      g_cfin_floats = need;
-    }
-    fa = FinArgs{g_cfin_acc, g_cfin_counter, G, update, bessel, gamma, beta, mov_mean, mov_var, ss, count, eps, decay};
-    fp = &fa;
-  }
-  bool fused = false;
-  int rc = conv_fwd_impl(x, w, y, true, nullptr, in_scale, in_shift, 0, d, (hipStream_t)stream, &ws, &rows, fp, &fused);
+  int rc = conv_fwd_impl(x, w, y, true, nullptr, in_scale, in_shift, 0, d, (hipStream_t)stream, &ws, &rows);
   if (rc) return rc;
-  if (fused) return 0;
   return dtm_bn_stats_finalize(ws, rows, d->K, gamma, beta, mov_mean, mov_var, ss, count, eps, decay, update, bessel,
                                (hipStream_t)stream);
 }
@@ -2283,8 +2093,6 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvD
   a.stride = 1;
   a.Hv = d->P; a.Wv = d->Q;
   a.OH = d->H; a.OW = d->W;
-  a.pre_side = g_pre_side;
-  a.fin_acc = nullptr; a.fin_counter = nullptr;
   const int rw = act_r ? 4 : 2;
   // launches: one plain dgrad over the zero-dilated dy (UD = stride), or (d->dec, stride > 1) one stride-1
   // conv per output parity class (a, b) with that class's taps of the decomposed weight (dec_dim)
@@ -2357,8 +2165,6 @@ static void launch_wgrad(const ConvWgradArgs& a, int splits, hipStream_t st) {
 // wgrad tile override (-1 = policy) and the blocks-per-CU target of the split count for the pipelined
 // kernels (A/B sweeps: tools/conv_tile_sweep.py)
 static int g_wgrad_env = -2;
-static int g_wgrad_n256 = 0;  // A/B knob: 256-column register-staged wgrad tiles for K <= 64, Kg > 128 (see policy)
-DTM_API void dtm_conv_set_wgrad_n256(int on) { g_wgrad_n256 = on; }
 static int g_wgrad_occ = 4;
 DTM_API void dtm_conv_set_wgrad_tile(int id, int occ) {
   g_wgrad_env = id;
@@ -2373,19 +2179,11 @@ struct WgradBN {
 };
 
 static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float* in_scale, const float* in_shift,
-                           const ConvDesc* d, int num_cus, const WgradBN* bn, void* stream, bool side = false);
+                           const ConvDesc* d, int num_cus, const WgradBN* bn, void* stream);
 
 DTM_API int dtm_conv_wgrad(const void* x, const void* dy, float* dw, const float* in_scale,
                            const float* in_shift, const ConvDesc* d, int num_cus, void* stream) {
   return conv_wgrad_impl(x, dy, dw, in_scale, in_shift, d, num_cus, nullptr, stream);
-}
-
-// dw is a persistent gradient buffer that nothing reads before ops.nn.side_join: the split-K slab
-// reduction runs on the side stream (opt-in) or is queued for the next dtm_def_flush (default;
-// workspace.hip)
-DTM_API int dtm_conv_wgrad_side(const void* x, const void* dy, float* dw, const float* in_scale,
-                                const float* in_shift, const ConvDesc* d, int num_cus, void* stream) {
-  return conv_wgrad_impl(x, dy, dw, in_scale, in_shift, d, num_cus, nullptr, stream, true);
 }
 
 // Weight gradient of a conv followed by a training BatchNorm whose stats-combine output (comb) has no
@@ -2399,7 +2197,7 @@ DTM_API int dtm_conv_wgrad_bnbwd(const void* x, const void* g, const void* y, co
 }
 
 static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float* in_scale, const float* in_shift,
-                           const ConvDesc* d, int num_cus, const WgradBN* bn, void* stream, bool side) {
+                           const ConvDesc* d, int num_cus, const WgradBN* bn, void* stream) {
   if (d->C % 8 || d->K % 8) return -1;
   ConvWgradArgs a;
   a.x = (const bf16_t*)x; a.dy = (const bf16_t*)dy; a.dw = dw;
@@ -2415,19 +2213,15 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   a.P = d->P; a.Q = d->Q; a.stride = d->stride; a.pad_h = d->pad_h; a.pad_w = d->pad_w;
   a.Mpix = d->N * d->P * d->Q; a.Kg = d->R * d->S * d->C;
   a.fd_PQ = make_fastdiv(d->P * d->Q); a.fd_Q = make_fastdiv(d->Q);
-  // wgrad tile variants: 0 = 128 (K) x 128 (RSC) 2 LDS buffers, 1 = 64 x 128, 2 = 64 x 128 single
-  // buffer, 3 = 128 x 128 single buffer.  DTM_WGRAD_TILE forces one (A/B experiments).
+  // wgrad tile variants: 0 = 128 (K) x 128 (RSC) register-staged, 1 = 64 x 128, 6 = 32 x 128, 10 = the
+  // pipelined LDS-DMA 128 x 128, 12 = the 8-wave pipelined 256 x 256 (the rejected variants and their A/B
+  // logs: profiles/ab/README.md).  DTM_WGRAD_TILE forces one (A/B experiments).
   if (g_wgrad_env == -2) {
     const char* e = getenv("DTM_WGRAD_TILE");
     g_wgrad_env = e ? atoi(e) : -1;
   }
   const int wenv = g_wgrad_env;
   int wt = wenv >= 0 ? wenv : (d->K <= 64 ? 1 : 0);
-  // K <= 64 with a reduction width over one 128-column tile (the stem's 224, 56x56 256->64, 3x3 64->64):
-  // 256-column tiles read (and BN-backward-transform) the dy operand half as many times (A/B knob
-  // dtm_conv_set_wgrad_n256)
-  // (knob 1: only with the BN-backward operand transform, i.e. the stem; 2: every such layer)
-  if (wenv == -1 && wt == 1 && a.Kg > 128 && (g_wgrad_n256 == 2 || (g_wgrad_n256 == 1 && bn))) wt = 4;
   // <= 32 output channels: 32-row tiles (no half-empty 64-row tile; A/B knob dtm_conv_set_k32)
   if (wenv == -1 && wt == 1 && d->K <= 32 && g_k32_tile) wt = 6;
   int occ = g_wgrad_occ;
@@ -2441,10 +2235,9 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
     if (g_tile_w8 && d->K >= 256 && a.Kg >= 1024 && (d->R * d->S > 1 || d->K >= 1024)) wt = 12;
   }
   if (wt >= 10 && (in_scale || bn)) wt = d->K <= 64 ? 1 : 0;  // the pipelined kernels have no operand prologues
-  const bool small_m = (wt == 1 || wt == 2 || wt == 4 || wt == 5 || wt == 13 || wt == 14 || wt == 15);
+  if (wt != 0 && wt != 1 && wt != 6 && wt != 10 && wt != 12) wt = 0;
   const bool big = wt == 12;  // 8-wave 256x256 (one block per CU)
-  const int MT = wt == 6 ? 32 : (small_m ? 64 : (big ? 256 : 128)),
-            NT = (big || wt == 4 || wt == 5 || wt == 13 || wt == 14) ? 256 : 128;
+  const int MT = wt == 6 ? 32 : (wt == 1 ? 64 : (big ? 256 : 128)), NT = big ? 256 : 128;
   if (big) occ = (wenv == 12 && g_wgrad_occ != 4) ? g_wgrad_occ : 1;  // (sweeps: WTILES=12:<occ>)
   long tiles = (long)((a.Kg + NT - 1) / NT) * ((a.K + MT - 1) / MT);
   long target = (long)num_cus * (wt >= 10 ? occ : 3);
@@ -2457,14 +2250,8 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   long steps_per = (ksteps + splits - 1) / splits;
   a.pix_per_split = (int)(steps_per * 64);
   splits = (a.Mpix + a.pix_per_split - 1) / a.pix_per_split;
-  int slot = -1;
   const size_t slab = (size_t)splits * a.K * a.Kg;
-  float* ws = side ? dtm_side_slab(slab, (hipStream_t)stream, &slot) : nullptr;
-  // deferred: one segmented reduction for many convs at the next flush (needs float4 columns)
-  float* dws = (side && !ws && (a.K * a.Kg) % 4 == 0 && ((uintptr_t)dw & 15) == 0)
-                   ? dtm_def_slab(slab, (hipStream_t)stream) : nullptr;
-  if (dws) ws = dws;
-  if (!ws) ws = dtm_ws_get(slab);
+  float* ws = dtm_ws_get(slab);
   if (!ws) return -4;
   a.dw = ws;
   if (wt >= 10) {
@@ -2472,27 +2259,13 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
     dim3 grid((a.Kg + NT - 1) / NT, (a.K + MT - 1) / MT, splits);
     if (wt == 12)
       hipLaunchKernelGGL((conv_wgrad_pipe_kernel<256, 256, 2, 2, 512>), grid, dim3(512), 0, (hipStream_t)stream, a);
-    else if (wt == 13)
-      hipLaunchKernelGGL((conv_wgrad_pipe_kernel<64, 256, 2, 1, 256>), grid, dim3(256), 0, (hipStream_t)stream, a);
-    else if (wt == 14)
-      hipLaunchKernelGGL((conv_wgrad_pipe_kernel<64, 256, 3, 1, 256>), grid, dim3(256), 0, (hipStream_t)stream, a);
-    else if (wt == 15)
-      hipLaunchKernelGGL((conv_wgrad_pipe_kernel<64, 128, 2>), grid, dim3(256), 0, (hipStream_t)stream, a);
-    else if (wt == 11)
-      hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 128, 3>), grid, dim3(256), 0, (hipStream_t)stream, a);
     else
       hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 128, 2>), grid, dim3(256), 0, (hipStream_t)stream, a);
   } else if (wt == 1) launch_wgrad<64, 128, 32, 64>(a, (int)splits, (hipStream_t)stream);
-  else if (wt == 4) launch_wgrad<64, 256, 32, 128>(a, (int)splits, (hipStream_t)stream);
   else if (wt == 6) launch_wgrad<32, 128, 16, 64>(a, (int)splits, (hipStream_t)stream);
-  else if (wt == 5) launch_wgrad<64, 256, 32, 128, 1>(a, (int)splits, (hipStream_t)stream);
-  else if (wt == 2) launch_wgrad<64, 128, 32, 64, 1>(a, (int)splits, (hipStream_t)stream);
-  else if (wt == 3) launch_wgrad<128, 128, 64, 64, 1>(a, (int)splits, (hipStream_t)stream);
   else launch_wgrad<128, 128, 64, 64>(a, (int)splits, (hipStream_t)stream);
   // dW += sum over the split slabs (every slab element is written: tiles cover [K][Kg] exactly)
-  if (slot >= 0) dtm_side_reduce(slot, (int)splits, a.K * a.Kg, a.K * a.Kg, dw, (hipStream_t)stream);
-  else if (dws) dtm_def_push(ws, (int)splits, a.K * a.Kg, dw);
-  else dtm_reduce_rows(ws, (int)splits, a.K * a.Kg, a.K * a.Kg, dw, (hipStream_t)stream);
+  dtm_reduce_rows(ws, (int)splits, a.K * a.Kg, a.K * a.Kg, dw, (hipStream_t)stream);
   return 0;
 }
 

@@ -162,187 +162,3 @@ void dtm_reduce_rows(const float* ws, int rows, int width, int ld, float* out, h
 }
 
 DTM_API int dtm_ws_reserve(long floats) { return dtm_ws_get((size_t)floats) ? 0 : -1; }
-
-// ---- side-stream reductions --------------------------------------------------------------------
-// The split-K weight-gradient slabs are summed into the fp32 gradient buffer, which nothing reads
-// before the end of backward (bucket all-reduce, NaN guard, optimizer).  So that reduction -- a short,
-// latency-bound launch per conv -- runs on a low-priority side stream forked from the caller's stream
-// by an event, overlapping the next layers' kernels instead of sitting between them.  Its slab comes
-// from a ring of NRING buffers (never the shared dtm_ws arena, which the next kernel reuses at once);
-// a ring slot is handed out again only after the caller's stream waits for its previous reduction.
-// dtm_side_join(stream) makes a stream wait for every side reduction issued so far: the engine calls it
-// after backward and before any collective.  Under hipGraph capture the caller reduces inline.
-namespace {
-constexpr int NRING = 4;
-hipStream_t g_side = nullptr;
-hipEvent_t g_fork[NRING], g_done[NRING], g_join;
-bool g_used[NRING] = {false, false, false, false};
-float* g_ring[NRING] = {nullptr, nullptr, nullptr, nullptr};
-size_t g_ring_floats[NRING] = {0, 0, 0, 0};
-int g_ring_i = 0;
-bool g_pending = false;
-int g_side_on = 0;
-
-bool side_init() {
-  if (g_side) return true;
-  int least = 0, greatest = 0;
-  hipDeviceGetStreamPriorityRange(&least, &greatest);
-  if (hipStreamCreateWithPriority(&g_side, hipStreamNonBlocking, least) != hipSuccess) {
-    g_side = nullptr;
-    return false;
-  }
-  for (int i = 0; i < NRING; ++i) {
-    hipEventCreateWithFlags(&g_fork[i], hipEventDisableTiming);
-    hipEventCreateWithFlags(&g_done[i], hipEventDisableTiming);
-  }
-  hipEventCreateWithFlags(&g_join, hipEventDisableTiming);
-  return true;
-}
-}  // namespace
-
-DTM_API void dtm_set_side_reduce(int on) { g_side_on = on; }
-
-// returns a slab buffer and its ring slot (slot -1: use the inline path -- capture, disabled, no memory)
-float* dtm_side_slab(size_t floats, hipStream_t st, int* slot) {
-  *slot = -1;
-  if (!g_side_on || !side_init()) return nullptr;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-  const int i = g_ring_i;
-  if (floats > g_ring_floats[i]) {
-    if (g_ring[i]) {
-      hipEventSynchronize(g_done[i]);
-      hipFree(g_ring[i]);
-    }
-    size_t n = floats < (4u << 20) ? (4u << 20) : floats;
-    if (hipMalloc(&g_ring[i], n * sizeof(float)) != hipSuccess) {
-      g_ring[i] = nullptr;
-      g_ring_floats[i] = 0;
-      return nullptr;
-    }
-    g_ring_floats[i] = n;
-    g_used[i] = false;
-  }
-  // the slot's previous reduction must have read its slab before this stream's kernel overwrites it
-  if (g_used[i]) hipStreamWaitEvent(st, g_done[i], 0);
-  g_ring_i = (i + 1) % NRING;
-  *slot = i;
-  return g_ring[i];
-}
-
-void dtm_side_reduce(int slot, int rows, int width, int ld, float* out, hipStream_t st) {
-  hipEventRecord(g_fork[slot], st);
-  hipStreamWaitEvent(g_side, g_fork[slot], 0);
-  dtm_reduce_rows(g_ring[slot], rows, width, ld, out, g_side);
-  hipEventRecord(g_done[slot], g_side);
-  g_used[slot] = true;
-  g_pending = true;
-}
-
-DTM_API void dtm_side_join(void* stream) {
-  if (!g_pending || !g_side) return;
-  hipEventRecord(g_join, g_side);
-  hipStreamWaitEvent((hipStream_t)stream, g_join, 0);
-  g_pending = false;
-}
-
-// ---- deferred weight-gradient reductions ---------------------------------------------------------
-// The split-K slabs of the convs whose gradient target is a persistent buffer (main_grad) are not reduced
-// one launch per conv: each slab goes to a bump arena and its (slab, rows, width, out) is queued; the
-// queue is flushed - ONE segmented reduction launch (per 64 entries) - when a reader needs the gradients
-// (bucket all-reduce, end of backward: dtm_def_flush via ops.nn.side_join) or when the arena is full.
-// Same stream throughout, so no event is needed; each output column is summed by one thread over the
-// slab rows in order (deterministic).
-namespace {
-struct DefEntry {
-  const float* ws;
-  float* out;
-  int rows, width;  // width in floats, % 4 == 0
-};
-constexpr int DEF_TAB = 64;
-struct DefTab {
-  DefEntry e[DEF_TAB];
-  int start[DEF_TAB + 1];  // first block of each entry
-  int n;
-};
-DefEntry g_def[4096];
-int g_def_n = 0;
-float* g_def_buf = nullptr;
-size_t g_def_cap = 0, g_def_used = 0;
-int g_def_on = 0;
-}  // namespace
-
-__global__ __launch_bounds__(256) void def_reduce_kernel(DefTab t) {
-  int i = 0;
-  while (i + 1 < t.n && (int)blockIdx.x >= t.start[i + 1]) ++i;
-  const DefEntry e = t.e[i];
-  const int col = ((int)blockIdx.x - t.start[i]) * 1024 + threadIdx.x * 4;
-  if (col >= e.width) return;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  int r = 0;
-  for (; r + 4 <= e.rows; r += 4) {
-    float4 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = *(const float4*)(e.ws + (size_t)(r + u) * e.width + col);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
-  }
-  for (; r < e.rows; ++r) {
-    const float4 v = *(const float4*)(e.ws + (size_t)r * e.width + col);
-    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-  }
-  float4* o = (float4*)(e.out + col);
-  const float4 c = *o;
-  *o = make_float4(c.x + acc.x, c.y + acc.y, c.z + acc.z, c.w + acc.w);
-}
-
-DTM_API void dtm_set_def_reduce(int on) { g_def_on = on; }
-
-DTM_API void dtm_def_flush(void* stream) {
-  for (int b = 0; b < g_def_n; b += DEF_TAB) {
-    DefTab t;
-    t.n = g_def_n - b < DEF_TAB ? g_def_n - b : DEF_TAB;
-    int blocks = 0;
-    for (int i = 0; i < t.n; ++i) {
-      t.e[i] = g_def[b + i];
-      t.start[i] = blocks;
-      blocks += (t.e[i].width + 1023) / 1024;
-    }
-    t.start[t.n] = blocks;
-    hipLaunchKernelGGL(def_reduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, t);
-  }
-  g_def_n = 0;
-  g_def_used = 0;
-}
-
-// a slab of `floats` for a deferred reduction (nullptr: reduce in place - knob off, shape, no memory)
-float* dtm_def_slab(size_t floats, hipStream_t st) {
-  if (!g_def_on || g_def_n >= 4096) return nullptr;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess) return nullptr;
-  const size_t need = (floats + 63) / 64 * 64;
-  if (g_def_used + need > g_def_cap) {
-    dtm_def_flush(st);  // (stream-ordered: the queued reductions read the arena before anything reuses it)
-    if (need > g_def_cap) {
-      if (cs != hipStreamCaptureStatusNone) return nullptr;  // no allocation inside a capture
-      if (g_def_buf) {
-        hipStreamSynchronize(st);
-        hipFree(g_def_buf);
-      }
-      size_t n = need < (64u << 20) ? (64u << 20) : need;  // >= 256 MB
-      if (hipMalloc(&g_def_buf, n * sizeof(float)) != hipSuccess) {
-        g_def_buf = nullptr;
-        g_def_cap = 0;
-        return nullptr;
-      }
-      g_def_cap = n;
-    }
-  }
-  float* p = g_def_buf + g_def_used;
-  g_def_used += need;
-  return p;
-}
-
-void dtm_def_push(const float* ws, int rows, int width, float* out) {
-  g_def[g_def_n++] = DefEntry{ws, out, rows, width};
-}

@@ -1,0 +1,73 @@
+"""Split JPEG decoding: host Huffman decode (csrc/runtime/jpeg.cpp) + device IDCT / upsampling / colour
+(csrc/kernels/jpeg.hip), bit-exact with libjpeg(-turbo)'s default decompression (the reference's
+tf.image.decode_jpeg, inception/image_processing.py:339-407, and PIL both use it).
+
+``huffman_decode(data)`` -> (JpegInfo numpy record, int16 coefficients) or None when the file is outside
+the supported subset (progressive, CMYK, ...: decode those with PIL).  ``pixels_cpu`` is the host form of
+the device stage (the oracle of the HIP kernel); ``decode_batch_gpu`` runs the device stage for a batch.
+"""
+import ctypes
+
+import numpy as np
+
+from ..utils import native
+
+# mirror of struct JpegInfo (csrc/runtime/jpeg.cpp)
+INFO_DT = np.dtype([("width", "<i4"), ("height", "<i4"), ("ncomp", "<i4"), ("hmax", "<i4"), ("vmax", "<i4"),
+                    ("mcux", "<i4"), ("mcuy", "<i4"), ("h", "<i4", 3), ("v", "<i4", 3), ("bw", "<i4", 3),
+                    ("bh", "<i4", 3), ("coef_off", "<i4", 3), ("coef_count", "<i4"), ("qt", "<u2", (3, 64))])
+
+UNSUPPORTED, CORRUPT, TOO_SMALL = -2, -1, -3
+
+
+def _rt():
+    L = native.rt()
+    if not getattr(L, "_jpeg_bound", False):
+        L.dtm_jpeg_decode.restype = ctypes.c_int
+        L.dtm_jpeg_decode.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long]
+        L.dtm_jpeg_pixels.restype = ctypes.c_int
+        L.dtm_jpeg_pixels.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.dtm_jpeg_info_bytes.restype = ctypes.c_int
+        assert L.dtm_jpeg_info_bytes() == INFO_DT.itemsize, (L.dtm_jpeg_info_bytes(), INFO_DT.itemsize)
+        L._jpeg_bound = True
+    return L
+
+
+def huffman_decode(data, out=None):
+    """Entropy-decode one JPEG.  ``out``: optional int16 array to decode into (its prefix is used).
+    Returns (info, coefs view) or None if unsupported / corrupt (the caller falls back to PIL)."""
+    L = _rt()
+    info = np.zeros(1, INFO_DT)
+    buf = np.frombuffer(data, np.uint8)
+    if out is None:
+        out = np.empty(1 << 20, np.int16)
+    rc = L.dtm_jpeg_decode(buf.ctypes.data, buf.size, info.ctypes.data, out.ctypes.data, out.size)
+    if rc == TOO_SMALL:
+        out = np.empty(int(info["coef_count"][0]), np.int16)
+        rc = L.dtm_jpeg_decode(buf.ctypes.data, buf.size, info.ctypes.data, out.ctypes.data, out.size)
+    if rc != 0:
+        return None
+    return info[0], out[:int(info["coef_count"][0])]
+
+
+def plane_bytes(info):
+    return int(sum(int(info["bw"][c]) * 8 * int(info["bh"][c]) * 8 for c in range(int(info["ncomp"]))))
+
+
+def pixels_cpu(info, coefs):
+    """Host form of the device stage: islow IDCT + fancy upsampling + YCbCr -> RGB -> HxWx3 uint8."""
+    L = _rt()
+    inf = np.array([info], INFO_DT)
+    scratch = np.empty(plane_bytes(info), np.uint8)
+    rgb = np.empty((int(info["height"]), int(info["width"]), 3), np.uint8)
+    coefs = np.ascontiguousarray(coefs, np.int16)
+    L.dtm_jpeg_pixels(coefs.ctypes.data, inf.ctypes.data, scratch.ctypes.data, rgb.ctypes.data)
+    return rgb
+
+
+def decode_cpu(data):
+    """Full host decode through the split path (None if unsupported)."""
+    r = huffman_decode(data)
+    if r is None:
+        return None
+    return pixels_cpu(*r)

@@ -102,8 +102,6 @@ class TrainStep:
             self.bufsync.issue()  # forward has finished every moving-statistics update
             with roctx("backward"):  # bucket all-reduces are issued (own ranges) from the grad hooks
                 loss.backward()
-            if images.is_cuda:
-                F.side_join()  # side-stream weight-gradient reductions complete before the gradients are read
             self._mark("bwd")
         finally:
             _fused.arena.end_step()

@@ -47,16 +47,10 @@ _SIGS = {
     "dtm_conv1x1_bnbwd": (_I, [_P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _L, _I, _I, _P]),
     "dtm_conv_wgrad_bnbwd": (_I, [_P, _P, _P, _P, _P, _P, _F, _P, _P, _P, ctypes.POINTER(ConvDesc), _I, _P]),
     "dtm_conv_wgrad": (_I, [_P, _P, _P, _P, _P, ctypes.POINTER(ConvDesc), _I, _P]),
-    "dtm_conv_wgrad_side": (_I, [_P, _P, _P, _P, _P, ctypes.POINTER(ConvDesc), _I, _P]),
-    "dtm_side_join": (None, [_P]),
-    "dtm_def_flush": (None, [_P]),
-    "dtm_set_def_reduce": (None, [_I]),
-    "dtm_set_side_reduce": (None, [_I]),
-    "dtm_conv_set_fin_fuse": (None, [_I]),
     "dtm_conv_set_policy2": (None, [_I]),
-    "dtm_conv_set_stream128_act": (None, [_I]),
     "dtm_set_grid_cpt": (None, [_I]),
     "dtm_conv_set_k32": (None, [_I]),
+    "dtm_conv_set_mfma32": (None, [_I]),
     "dtm_cat_desc_bytes": (_I, []),
     "dtm_cat_bn_apply": (_I, [_P, _I, _P, _L, _I, _P]),
     "dtm_cat_bn_apply_bwd": (_I, [_P, _I, _P, _P, _L, _I, _P]),
@@ -115,8 +109,6 @@ _SIGS = {
     "dtm_set_reduce_few": (None, [_I]),
     "dtm_conv_set_stream_act": (None, [_I]),
     "dtm_conv_set_act_tile": (None, [_I]),
-    "dtm_conv_set_wgrad_n256": (None, [_I]),
-    "dtm_conv_set_pre_side": (None, [_I]),
     "dtm_stem_pack": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "dtm_dropout": (_I, [_P, _P, _L, _I, _F, ctypes.c_ulonglong, _P, _P]),
     "dtm_in_top_k": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),

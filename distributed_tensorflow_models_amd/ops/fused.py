@@ -17,7 +17,7 @@ import torch
 from . import _lib
 from .geometry import conv_geom
 from .lazy import LazyBN, Subsampled, as_tensor  # noqa: F401
-from .nn import _accum_param_grad, _check, _notify, dgrad_decomposable, weight_bf16, weight_flipped, wgrad_into
+from .nn import _accum_param_grad, _check, _notify, dgrad_decomposable, weight_bf16, weight_flipped
 
 
 class ZeroArena:
@@ -274,7 +274,7 @@ class _ConvBNFn(torch.autograd.Function):
         if ctx.needs_input_grad[2]:
             mg = getattr(w, "main_grad", None)
             target = mg if mg is not None else torch.zeros(w.shape, device=dy.device, dtype=torch.float32)
-            _check(wgrad_into(L, target, mg is not None)(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(target), _lib.ptr(sc),
+            _check(L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(target), _lib.ptr(sc),
                                                          _lib.ptr(sh), ctypes.byref(d), _lib.num_cus(), s),
                    "conv_wgrad")
             if mg is not None:

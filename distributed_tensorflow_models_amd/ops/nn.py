@@ -66,29 +66,10 @@ def _note_live_window(w, win):
         h(w, win)
 
 
-def side_join():
-    """Complete every weight-gradient reduction that dtm_conv_wgrad_side left pending: flush the queue of
-    deferred slab reductions (one segmented launch) and make the current stream wait for the side
-    stream (if that opt-in path is on).  Call before anything reads the fp32 gradient buffers."""
-    if torch.cuda.is_available() and torch.cuda.is_initialized():
-        L = _lib.lib()
-        s = _lib.stream_ptr()
-        L.dtm_def_flush(s)
-        L.dtm_side_join(s)
-
-
-def wgrad_into(L, target, is_main_grad):
-    """The wgrad entry for a target buffer: a persistent main_grad (read only after side_join) lets the
-    split-K slab reduction be deferred and batched with other convs' (or run on the side stream); a
-    temporary takes the immediate in-stream reduction."""
-    return L.dtm_conv_wgrad_side if is_main_grad else L.dtm_conv_wgrad
-
-
 def _accum_param_grad(p, g):
     """Route a computed fp32 grad for parameter p; returns what autograd should receive."""
     mg = getattr(p, "main_grad", None)
     if mg is not None:
-        side_join()  # (a side-stream reduction may still be adding into this buffer)
         mg.add_(g)
         _notify(p)
         return None
@@ -233,7 +214,7 @@ class _Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             mg = getattr(w, "main_grad", None)
             target = mg if mg is not None else torch.zeros(w.shape, device=dy.device, dtype=torch.float32)
-            _check(wgrad_into(L, target, mg is not None)(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(target), None, None,
+            _check(L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(target), None, None,
                                                          ctypes.byref(d), _lib.num_cus(), s), "conv_wgrad")
             if mg is not None:
                 _notify(w)
@@ -369,7 +350,7 @@ class _Conv2dTransposeFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             mg = getattr(w, "main_grad", None)
             target = mg if mg is not None else torch.zeros(w.shape, device=dy.device, dtype=torch.float32)
-            _check(wgrad_into(L, target, mg is not None)(_lib.ptr(dy), _lib.ptr(x), _lib.ptr(target), None, None,
+            _check(L.dtm_conv_wgrad(_lib.ptr(dy), _lib.ptr(x), _lib.ptr(target), None, None,
                                                          ctypes.byref(d), _lib.num_cus(), s),
                    "conv_transpose_bwd_filter")
             if mg is not None:
@@ -808,7 +789,7 @@ class _LinearHipFn(torch.autograd.Function):
             direct = mg is not None and Np == N
             target = mg if direct else torch.zeros((Kin, Np), device=dy.device, dtype=torch.float32)
             d = _fc_desc(B, Np, Kin)  # "input" dy (C = Np), "output gradient" x (K = Kin): dW[Kin][Np]
-            _check(wgrad_into(L, target, direct)(_lib.ptr(dyp), _lib.ptr(x16), _lib.ptr(target), None, None,
+            _check(L.dtm_conv_wgrad(_lib.ptr(dyp), _lib.ptr(x16), _lib.ptr(target), None, None,
                                                  ctypes.byref(d), _lib.num_cus(), s), "fc_wgrad")
             if direct:
                 _notify(w)

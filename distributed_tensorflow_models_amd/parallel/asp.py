@@ -69,6 +69,11 @@ class ParamStore:
         per_owner = {}
         for i, p in enumerate(self.params):
             per_owner.setdefault(self.owner[i], []).append(i)
+        # within an owner: the tensors with a bf16 compute copy (conv / FC weights) first, so the pull
+        # refreshes those copies with ONE cast over a prefix of the owner's region
+        for k in per_owner:
+            per_owner[k].sort(key=lambda i: (self._bf16(self.params[i]) is None, i))
+        self.owned = {k: list(v) for k, v in per_owner.items()}
         self.layout = {}
         for k, idxs in per_owner.items():
             off = 0
@@ -99,6 +104,28 @@ class ParamStore:
         if nbuf:
             base = self._nslot[0] * (1 + nslots)
             self.buf_shard = self.flat[0][base:base + nbuf]
+        self._flatten_local()
+
+    @staticmethod
+    def _bf16(p):
+        w16 = getattr(p, "bf16", None)
+        return w16 if (w16 is not None and w16.dtype == torch.bfloat16 and w16.shape == p.shape) else None
+
+    def _flatten_local(self):
+        """Re-home the local replica in the owner shards' layout (``flatten_tensors`` keeps every
+        parameter object; only its storage moves): per owner one fp32 region mirroring the shard, and
+        one bf16 region for the compute copies of its leading weights.  The pull is then 2 launches per
+        owner instead of 2 per tensor (ResNet-50: 322)."""
+        from .bsp import flatten_tensors
+        self._local, self._local16 = {}, {}
+        for k, idxs in self.owned.items():
+            ps = [self.params[i] for i in idxs]
+            if len({(p.dtype, p.device) for p in ps}) != 1:
+                self._local = None
+                return
+            self._local[k] = flatten_tensors(ps)
+            w16 = [self._bf16(p) for p in ps if self._bf16(p) is not None]
+            self._local16[k] = flatten_tensors(w16) if w16 else None
 
     def _negotiate_ipc(self):
         """Owner shards are written from other GPUs over xGMI: every rank checks that its device can
@@ -176,11 +203,18 @@ class ParamStore:
     def pull(self):
         """Copy the current shared parameters into the local replica (M1)."""
         from ..ops.nn import WEIGHT_VERSION
-        for i, p in enumerate(self.params):
-            p.copy_(self.shards[i]["param"].to(p.device, non_blocking=True))
-            w16 = getattr(p, "bf16", None)
-            if w16 is not None:
-                w16.copy_(p)
+        if self._local is not None:
+            for k, loc in self._local.items():
+                loc.copy_(self.flat[k][:loc.numel()].to(loc.device, non_blocking=True))
+                l16 = self._local16[k]
+                if l16 is not None:
+                    l16.copy_(loc[:l16.numel()])
+        else:
+            for i, p in enumerate(self.params):
+                p.copy_(self.shards[i]["param"].to(p.device, non_blocking=True))
+                w16 = getattr(p, "bf16", None)
+                if w16 is not None:
+                    w16.copy_(p)
         if self._buf_local is not None:
             self._buf_local.copy_(self.buf_shard.to(self._buf_local.device, non_blocking=True))
             self._buf_snap.copy_(self._buf_local)
@@ -360,9 +394,6 @@ class ASPTrainStep:
         out = self.model(images, training=True)
         loss = self.loss_fn(out, labels)
         loss.backward()
-        if images.is_cuda:
-            from ..ops.nn import side_join
-            side_join()  # side-stream weight-gradient reductions land before the push reads them
         gs = self.store.global_step()
         lr = self.lr_schedule(gs) if self.lr_schedule else None
         self.store.push_buffers()

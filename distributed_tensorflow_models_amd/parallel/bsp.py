@@ -67,6 +67,7 @@ class BSPDataParallel:
         self.windows = {p: p._live_win for p in self.params
                         if self._compact_on and getattr(p, "_live_win", None) is not None and p.dim() == 4}
         self._works = []
+        self._done_works = []
         self._build_buckets()
         self._win_hook = opsnn.add_live_window_hook(self._on_live_window)
         self.overlap = overlap
@@ -189,8 +190,6 @@ class BSPDataParallel:
         self._launched[bi] = True
         if self.world == 1:
             return
-        if self.flat.is_cuda:
-            opsnn.side_join()  # the collective's stream syncs with this stream at issue
         with roctx("allreduce_bucket_%d" % bi):
             if bi in self.compact:
                 p, (r0, r1, s0, s1), buf, low = self.compact[bi]
@@ -209,8 +208,6 @@ class BSPDataParallel:
     def finish(self):
         """Launch any bucket not yet reduced (unused params / no overlap) and make the current
         stream wait for every reduction."""
-        if self.flat.is_cuda:
-            opsnn.side_join()
         for bi in range(len(self.buckets)):
             if not self._launched[bi]:
                 self._launch(bi)
@@ -222,7 +219,25 @@ class BSPDataParallel:
             elif self.comm is not None:
                 s, e = self.buckets[bi]
                 self.flat[s:e].copy_(self.comm[s:e])
+        self._done_works = self._works
         self._works = []
+
+    def bucket_elements(self):
+        """Elements each bucket sends, in bucket order."""
+        return [self.compact[bi][2].numel() if bi in self.compact else b[1] - b[0]
+                for bi, b in enumerate(self.buckets)]
+
+    def bucket_ms(self):
+        """Per-bucket collective durations (ms) of the last step, in issue order - available when the
+        RCCL communicator records timing events (process_group.rccl_env(timing=True)); [] otherwise.
+        Synchronizes with the last collective: call on log steps only."""
+        out = []
+        for _bi, w in self._done_works:
+            try:
+                out.append(round(float(w._get_duration()), 4))
+            except Exception:
+                return []
+        return out
 
     @property
     def grad_scale(self):
@@ -284,8 +299,6 @@ class BufferSync:
         self._n += 1
         if (self._n - 1) % self.every:
             return
-        if self.flat.is_cuda:
-            opsnn.side_join()
         with roctx("bn_stats_allreduce"):
             self._work = dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 

@@ -11,7 +11,32 @@ import torch
 import torch.distributed as dist
 
 
-def init(rank=None, world_size=None, master_addr=None, master_port=None, backend=None, timeout_s=1800):
+def rccl_env(channels=0, timing=False):
+    """RCCL knobs that must be set before the communicator exists.
+
+    channels > 0 pins the number of RCCL channels (NCCL_MIN/MAX_NCHANNELS): each channel is one ring
+    over the xGMI links driven by its own workgroup, so the count trades all-reduce bandwidth against
+    CUs taken from the overlapped backward kernels.  timing: per-collective start/end events
+    (TORCH_NCCL_ENABLE_TIMING) so BSPDataParallel.bucket_ms() can report every bucket's duration."""
+    if channels and channels > 0:
+        os.environ["NCCL_MIN_NCHANNELS"] = str(int(channels))
+        os.environ["NCCL_MAX_NCHANNELS"] = str(int(channels))
+    if timing:
+        os.environ["TORCH_NCCL_ENABLE_TIMING"] = "1"
+
+
+def nccl_options(high_priority=True):
+    """ProcessGroupNCCL options: the collectives' internal stream at high priority, so bucket
+    all-reduces issued mid-backward are scheduled ahead of the compute stream's queued kernels."""
+    try:
+        from torch.distributed import ProcessGroupNCCL
+        return ProcessGroupNCCL.Options(is_high_priority_stream=bool(high_priority))
+    except Exception:  # (a build without the NCCL/RCCL backend)
+        return None
+
+
+def init(rank=None, world_size=None, master_addr=None, master_port=None, backend=None, timeout_s=1800,
+         high_priority=True):
     if dist.is_available() and dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
     rank = int(os.environ.get("RANK", 0) if rank is None else rank)
@@ -27,6 +52,9 @@ def init(rank=None, world_size=None, master_addr=None, master_port=None, backend
         local = int(os.environ.get("LOCAL_RANK", rank % max(torch.cuda.device_count(), 1)))
         torch.cuda.set_device(local)
         kw["device_id"] = torch.device("cuda", local)
+        opts = nccl_options(high_priority)
+        if opts is not None:
+            kw["pg_options"] = opts
     dist.init_process_group(backend, rank=rank, world_size=world_size,
                             timeout=datetime.timedelta(seconds=timeout_s), **kw)
     return rank, world_size

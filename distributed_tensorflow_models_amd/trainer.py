@@ -134,6 +134,7 @@ def define_common_flags(flags, preset):
             ("use_hipgraph", B, False, "capture the BSP training step in a hipGraph (launch-bound models; "
              "single-rank only, ignored with a warning when world > 1)"),
             ("bn_sync_every", I, 1, "BSP: average the BN moving statistics over the replicas every N steps"),
+            ("rccl_channels", I, 0, "pin the RCCL channel count (0 = RCCL's choice)"),
             ("grad_comm_dtype", S, "fp32", "gradient all-reduce dtype on the wire: fp32 | bf16"),
             ("deterministic", B, False, "bit-reproducible GPU reductions (no cross-block fp32 atomics)"),
             ("trace_steps", S, "", "a:b -> export a Chrome trace of steps [a, b)"),
@@ -215,6 +216,8 @@ def train(preset, flags, default_mode="bsp"):
     if FLAGS.job_name == "ps":
         Server({"ps": ps_hosts, "worker": worker_hosts}, "ps", FLAGS.task_id).join()
         return 0
+    # RCCL knobs before the communicator exists: channel count, per-bucket timing for the JSONL metrics
+    pg.rccl_env(FLAGS.rccl_channels, timing=bool(FLAGS.metrics_file))
     if worker_hosts and "WORLD_SIZE" not in os.environ:
         Server({"ps": ps_hosts, "worker": worker_hosts}, "worker", FLAGS.task_id)
     else:
@@ -405,6 +408,10 @@ def train(preset, flags, default_mode="bsp"):
                     tbw.add_scalar("total_loss", loss_avg, gs)
                     tbw.add_scalar("images_per_sec", world * B / max(dt, 1e-9), gs)
             extra = step_fn.timer.sections() if (mode == "bsp" and step_fn.timer is not None) else {}
+            if mode == "bsp" and metrics.f is not None and world > 1:
+                bms = step_fn.dp.bucket_ms()  # per-bucket all-reduce durations (RCCL timing events)
+                if bms:
+                    extra["bucket_allreduce_ms"] = bms
             if device.type == "cuda" and metrics.f is not None:
                 extra["max_mem_gb"] = torch.cuda.max_memory_allocated(device) / 2 ** 30
             metrics.write(step=step, global_step=gs, loss=loss_v, lr=sched(gs), images_per_sec=B / max(dt, 1e-9),

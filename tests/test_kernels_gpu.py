@@ -348,7 +348,6 @@ def test_conv_dead_taps_cropped(H, R, K, C, use_main_grad):
     xg = x.to(DEV, torch.bfloat16).requires_grad_()
     y = F.conv2d(xg, wg, None, 1, "SAME")
     y.backward(dy.to(DEV, torch.bfloat16))
-    F.side_join()  # (a main_grad target's slab reduction runs on the library's side stream)
     dw = wg.main_grad if use_main_grad else wg.grad
     for a, b in ((y, yr), (xg.grad, xr.grad), (dw, wr.grad)):
         a = a.float().cpu()

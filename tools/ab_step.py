@@ -3,7 +3,7 @@
 median ms/step per variant; one device, one process: MI355X_MICROARCH 'DVFS give-back' / rule 24).
 
 VARIANTS="base=;noW=wtile:-3;noT=tile:-3;fused=prologue:fused" python tools/ab_step.py
-keys: tile (conv_nt tile id), w8 (0/1: the 8-wave 256x256 conv tile in the shape policy), kwide (0/1: 64-channel tiles for K % 128 <= 64), few (0/1: streaming few-row slab reduction), bnout (0/1: block-output BN backward in the consuming dgrad's epilogue), b1x1 (0/1: one-pass 1x1 conv+BN backward), stemw (0/1: stem BN backward in the wgrad operand staging), sact (0/1: streaming 1x1 kernel for act dgrads), pcom (0/1: Inception pool branches as conv -> pool -> BN), sbwd (0/1: HIP backward of the pooled-BN statistics), catm (0/1: one-launch multi-part concat BN-apply), dec (0/1: stride-decomposed strided dgrads), k32 (0/1: 256x32 tile for <=32-channel spatial convs), cpt (16-B chunks per thread of the BN-stream grids), s128 (0/1: streaming kernel for 128-deep act dgrads), pol2 (0/1: v2 conv tile-policy rules), fin (0/1: BN finalize hand-off in the conv statistics epilogue), defr (0/1: deferred batched weight-gradient slab reductions), side (0/1: weight-gradient slab reductions on the side stream), pre (0/1: early dgrad-epilogue side-input loads), wn256 (0/1: 256-column wgrad tiles for K <= 64), atile (tile id of the dgrads with a fused
+keys: tile (conv_nt tile id), w8 (0/1: the 8-wave 256x256 conv tile in the shape policy), kwide (0/1: 64-channel tiles for K % 128 <= 64), few (0/1: streaming few-row slab reduction), bnout (0/1: block-output BN backward in the consuming dgrad's epilogue), b1x1 (0/1: one-pass 1x1 conv+BN backward), stemw (0/1: stem BN backward in the wgrad operand staging), sact (0/1: streaming 1x1 kernel for act dgrads), pcom (0/1: Inception pool branches as conv -> pool -> BN), sbwd (0/1: HIP backward of the pooled-BN statistics), catm (0/1: one-launch multi-part concat BN-apply), dec (0/1: stride-decomposed strided dgrads), k32 (0/1: 256x32 tile for <=32-channel spatial convs), cpt (16-B chunks per thread of the BN-stream grids), pol2 (0/1: v2 conv tile-policy rules), m32 (0/1: 32x32x16-MFMA forms of the LDS-DMA conv tiles), atile (tile id of the dgrads with a fused
 activation-backward epilogue, -1 = policy), wtile[:occ] (wgrad tile id / blocks-per-CU target), prologue (DTM_PROLOGUE),
 stem (DTM_STEM: 1 = packed-row stem path), red (target_blocks:max_chunks[:direct_max] of the
 partial-sum reductions; 0 = legacy 256 rows per block; direct_max = largest BN-backward grid that
@@ -36,15 +36,10 @@ def apply(cfg):
     L.dtm_set_reduce_few(int(cfg.get("few", "1")))
     L.dtm_conv_set_stream_act(int(cfg.get("sact", "1")))
     L.dtm_conv_set_act_tile(int(cfg.get("atile", "-1")))
-    L.dtm_conv_set_wgrad_n256(int(cfg.get("wn256", "0")))
-    L.dtm_conv_set_pre_side(int(cfg.get("pre", "0")))
-    L.dtm_set_side_reduce(int(cfg.get("side", "0")))
-    L.dtm_set_def_reduce(int(cfg.get("defr", "0")))
-    L.dtm_conv_set_fin_fuse(int(cfg.get("fin", "0")))
     L.dtm_conv_set_policy2(int(cfg.get("pol2", "1")))
-    L.dtm_conv_set_stream128_act(int(cfg.get("s128", "0")))
     L.dtm_set_grid_cpt(int(cfg.get("cpt", "8")))
     L.dtm_conv_set_k32(int(cfg.get("k32", "1")))
+    L.dtm_conv_set_mfma32(int(cfg.get("m32", os.environ.get("DTM_MFMA32", "0"))))
     sc = cfg.get("sc", "5:4096").split(":")
     L.dtm_set_sc_policy(int(sc[0]), int(sc[1]))
     os.environ["DTM_PROLOGUE"] = cfg.get("prologue", "auto")

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B sweep of the conv_nt tile variants (DTM_CONV_TILE ids) on the ResNet-50 shapes, in ONE process
 with interleaved rounds (per-shape median over rounds): forward, forward with the BatchNorm-apply
-prologue, and dgrad.  Usage: TILES=-1,20,21 python tools/conv_tile_sweep.py"""
+prologue, and dgrad.  Usage: TILES=-1,21,26 python tools/conv_tile_sweep.py"""
 import ctypes
 import os
 import statistics
@@ -15,7 +15,7 @@ from distributed_tensorflow_models_amd.ops.geometry import conv_geom  # noqa: E4
 from tools.conv_microbench import SHAPES  # noqa: E402
 
 B = int(os.environ.get("B", "256"))
-TILES = [int(t) for t in os.environ.get("TILES", "-1,20,21,22,23").split(",")]
+TILES = [int(t) for t in os.environ.get("TILES", "-1,0,21,24,26,40").split(",")]
 ROUNDS = int(os.environ.get("ROUNDS", "3"))
 ONLY = os.environ.get("ONLY")
 

@@ -65,19 +65,47 @@ class bf16_storage:
         self.ref.conv2d, self.ref.batch_norm = self.conv, self.bn
 
 
-def trajectory(bf16):
+def tracked(net):
+    """The tensors whose total 30-step update (w30 - w0) the fixture keeps: every BatchNorm gamma / beta
+    (where a systematic BN-backward error shows first), the stem conv and the logits layer."""
+    from distributed_tensorflow_models_amd.models.layers import tf_variables
+    out = {}
+    for name, t, _l, trainable in tf_variables(net):
+        if trainable and (t.dim() == 1 or "conv1/weights" in name and "block" not in name or "logits" in name):
+            out[name] = t
+    return out
+
+
+def trajectory(bf16, deltas=None):
+    import numpy as np
     from distributed_tensorflow_models_amd.engine import TrainStep
     net = build()
+    tr = tracked(net)
+    w0 = {k: v.detach().clone() for k, v in tr.items()}
     step = TrainStep(net, optimizer="momentum", lr=LR, momentum=0.9)
-    if bf16:
-        with bf16_storage():
-            return [float(step(x, y)) for x, y in batches()]
-    return [float(step(x, y)) for x, y in batches()]
+    losses = []
+    import contextlib
+    with (bf16_storage() if bf16 else contextlib.nullcontext()):
+        for i, (x, y) in enumerate(batches()):
+            losses.append(float(step(x, y)))
+            if i == 0 and deltas is not None:
+                # the first update = -lr * gradient at w0: a whole-backward check before bf16 rounding has
+                # had time to send the trajectories apart (by step 30 the directions are decorrelated)
+                deltas.update({"step1:" + k: (v.detach() - w0[k]).float().numpy() for k, v in tr.items()})
+    if deltas is not None:
+        deltas.update({"norm30:" + k: np.array([float((v.detach() - w0[k]).float().norm())], np.float32)
+                       for k, v in tr.items()})
+    return losses
 
 
 def main():
+    import numpy as np
     torch.set_num_threads(os.cpu_count() or 8)
-    fp32, b16 = trajectory(False), trajectory(True)
+    d32, d16 = {}, {}
+    fp32, b16 = trajectory(False, d32), trajectory(True, d16)
+    fx = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "fixtures")
+    np.savez(os.path.join(fx, "resnet50_112_b32_deltas.npz"),
+             **{"fp32:" + k: v for k, v in d32.items()}, **{"emul:" + k: v for k, v in d16.items()})
     out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "fixtures",
                        "resnet50_112_b32_trajectory.json")
     with open(out, "w") as f:
