@@ -71,3 +71,61 @@ def decode_cpu(data):
     if r is None:
         return None
     return pixels_cpu(*r)
+
+
+# ---- device stage ------------------------------------------------------------------------------------
+# mirror of struct JpegDesc (csrc/kernels/jpeg.hip)
+DESC_DT = np.dtype([("coef_base", "<i8"), ("plane_base", "<i8"), ("rgb_off", "<i8"), ("width", "<i4"),
+                    ("height", "<i4"), ("ncomp", "<i4"), ("hmax", "<i4"), ("vmax", "<i4"), ("h", "<i4", 3),
+                    ("v", "<i4", 3), ("bw", "<i4", 3), ("bh", "<i4", 3), ("coef_off", "<i4", 3), ("nblocks", "<i4"),
+                    ("pad", "<i4"), ("qt", "<u2", (3, 64))])
+
+
+def batch_table(infos):
+    """Descriptor table + buffer sizes for a batch of decoded headers: (descs, coef int16 count, plane bytes,
+    rgb bytes, max blocks, max pixels).  Coefficient bases are 8-int16 aligned, plane bases 8-byte aligned."""
+    n = len(infos)
+    d = np.zeros(n, DESC_DT)
+    coef = plane = rgb = 0
+    maxb = maxp = 0
+    for i, inf in enumerate(infos):
+        for f in ("width", "height", "ncomp", "hmax", "vmax", "h", "v", "bw", "bh", "coef_off"):
+            d[i][f] = inf[f]
+        d[i]["qt"] = inf["qt"]
+        nc = int(inf["ncomp"])
+        nb = int(sum(int(inf["bw"][c]) * int(inf["bh"][c]) for c in range(nc)))
+        d[i]["nblocks"] = nb
+        d[i]["coef_base"] = coef
+        d[i]["plane_base"] = plane
+        d[i]["rgb_off"] = rgb
+        coef += (int(inf["coef_count"]) + 7) // 8 * 8
+        plane += (plane_bytes(inf) + 7) // 8 * 8
+        npx = int(inf["width"]) * int(inf["height"])
+        rgb += npx * 3
+        maxb, maxp = max(maxb, nb), max(maxp, npx)
+    return d, coef, plane, rgb, maxb, maxp
+
+
+def decode_batch_gpu(items, device, stream=None):
+    """[(info, coefs)] -> (device uint8 RGB ragged buffer, descriptor table): image i is the HxWx3 block at
+    descs[i]['rgb_off'].  Coefficients travel as one H2D copy; two HIP launches decode the batch."""
+    import torch
+
+    from ..ops import _lib
+    L = _lib.lib()
+    assert L.dtm_jpeg_desc_bytes() == DESC_DT.itemsize, (L.dtm_jpeg_desc_bytes(), DESC_DT.itemsize)
+    infos = [it[0] for it in items]
+    d, ncoef, nplane, nrgb, maxb, maxp = batch_table(infos)
+    host = torch.empty(max(ncoef, 8), dtype=torch.int16, pin_memory=True)
+    hv = host.numpy()
+    for (inf, cf), base in zip(items, d["coef_base"]):
+        hv[int(base):int(base) + cf.size] = cf
+    coefs = host.to(device, non_blocking=True)
+    descs = torch.from_numpy(d.view(np.uint8)).to(device, non_blocking=True)
+    planes = torch.empty(max(nplane, 8), dtype=torch.uint8, device=device)
+    rgb = torch.empty(max(nrgb, 1), dtype=torch.uint8, device=device)
+    rc = L.dtm_jpeg_decode_gpu(_lib.ptr(coefs), _lib.ptr(descs), len(items), int(maxb), int(maxp), _lib.ptr(planes),
+                               _lib.ptr(rgb), _lib.stream_ptr())
+    if rc != 0:
+        raise RuntimeError("dtm_jpeg_decode_gpu failed (%d)" % rc)
+    return rgb, d

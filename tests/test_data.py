@@ -191,10 +191,10 @@ def test_imagenet_oracle_tf_semantics():
     np.testing.assert_allclose(got, ((np.clip(v, 0, 1) - 0.5) * 2).astype(np.float32), atol=1e-6)
 
 
-def _assembled(ds, procs, decoders, nbatch=2):
+def _assembled(ds, procs, decoders, nbatch=2, split=False):
     from distributed_tensorflow_models_amd.data import imagenet_gpu
     bi = imagenet_gpu.GPUBatchInputs(ds, 4, train=True, image_size=32, num_readers=1, num_decoders=decoders, seed=7,
-                                     device="cpu", decode_processes=procs, shuffle_buffer=64)
+                                     device="cpu", decode_processes=procs, shuffle_buffer=64, split_decode=split)
     try:
         out = [bi.ready.get(timeout=120) for _ in range(nbatch)]
     finally:
@@ -203,34 +203,56 @@ def _assembled(ds, procs, decoders, nbatch=2):
 
 
 def test_gpu_pipeline_assembler_host_side(tmp_path):
-    """Host side of data/imagenet_gpu.py (no GPU needed): decoder processes and threads give the same
-    packed pixels, labels and per-image parameters for a fixed seed (parameters are drawn in the
-    workers from per-image seeds assigned in submission order), and the table's offsets tile the
-    ragged pixel buffer."""
+    """Host side of data/imagenet_gpu.py (no GPU needed).  Thread decoders: the stream is reproducible for
+    a fixed seed (parameters drawn from per-image seeds assigned in submission order).  Decoder processes
+    (reading their own shards, results in shared memory): every record arrives, and the table's offsets tile
+    the ragged pixel buffer whose contents equal the decoded images."""
     from PIL import Image
 
     from distributed_tensorflow_models_amd.data import imagenet_gpu
     out = tmp_path / "d"
     out.mkdir()
     rng = np.random.RandomState(0)
-    with TFRecordWriter(str(out / "train-00000-of-00001")) as w:
-        for i in range(12):
-            b = io.BytesIO()
-            Image.fromarray((rng.rand(20 + i, 30, 3) * 255).astype(np.uint8)).save(b, format="JPEG")
-            w.write(encode_example({"image/encoded": b.getvalue(), "image/class/label": i + 1,
-                                    "image/object/bbox/xmin": [0.1], "image/object/bbox/ymin": [0.1],
-                                    "image/object/bbox/xmax": [0.9], "image/object/bbox/ymax": [0.9]}))
+    pixels = {}
+    for shard in range(2):
+        with TFRecordWriter(str(out / ("train-%05d-of-00002" % shard))) as w:
+            for i in range(6):
+                b = io.BytesIO()
+                lab = shard * 6 + i + 1
+                Image.fromarray((rng.rand(20 + lab, 30, 3) * 255).astype(np.uint8)).save(b, format="JPEG")
+                pixels[lab] = np.asarray(Image.open(io.BytesIO(b.getvalue())).convert("RGB"))
+                w.write(encode_example({"image/encoded": b.getvalue(), "image/class/label": lab,
+                                        "image/object/bbox/xmin": [0.1], "image/object/bbox/ymin": [0.1],
+                                        "image/object/bbox/xmax": [0.9], "image/object/bbox/ymax": [0.9]}))
     ds = imagenet.ImagenetData("train", str(out))
-    a = _assembled(ds, True, 2)
+    a = _assembled(ds, False, 2)
     b = _assembled(ds, False, 3)
-    for (bt, tt, lab), (bt2, tt2, lab2) in zip(a, b):
-        tab = tt.numpy().view(imagenet_gpu._PARAM_DT)
+    for (bt, tt, lab, _s), (bt2, tt2, lab2, _s2) in zip(a, b):
         assert torch.equal(lab, lab2) and torch.equal(tt, tt2)
+        tab = tt.numpy().view(imagenet_gpu._PARAM_DT)
         total = int(tab["src_off"][-1] + tab["h"][-1] * tab["w"][-1] * 3)
         assert torch.equal(bt[:total], bt2[:total])
+        assert list(tab["method"]) == [0, 1, 2, 3]
+    seen = set()
+    bi = imagenet_gpu.GPUBatchInputs(ds, 4, train=True, image_size=32, num_readers=1, num_decoders=2, seed=7,
+                                     device="cpu", decode_processes=True, split_decode=False)
+    got = []
+    try:
+        for _ in range(200):  # until both decoder processes (one shard each) have delivered
+            got.append(bi.ready.get(timeout=120))
+            seen.update(got[-1][2].tolist())
+            if len(seen) == 12:
+                break
+    finally:
+        bi.close()
+    for bt, tt, lab, _s in got:
+        tab = tt.numpy().view(imagenet_gpu._PARAM_DT)
         assert list(tab["src_off"][1:]) == list(np.cumsum(tab["h"] * tab["w"] * 3)[:-1])
         assert (tab["y0"] + tab["ch"] <= tab["h"]).all() and (tab["x0"] + tab["cw"] <= tab["w"]).all()
-        assert list(tab["method"]) == [0, 1, 2, 3] and set(lab.tolist()) <= set(range(1, 13))
+        for i, l in enumerate(lab.tolist()):
+            o, h, w = int(tab["src_off"][i]), int(tab["h"][i]), int(tab["w"][i])
+            np.testing.assert_array_equal(bt.numpy()[o:o + h * w * 3].reshape(h, w, 3), pixels[l])
+    assert seen == set(range(1, 13))  # both decoder processes' shards arrive
 
 
 @pytest.mark.timeout(120)
@@ -272,7 +294,7 @@ def test_gpu_pipeline_assembler_skips_corrupt_record(tmp_path):
         got = [bi.ready.get(timeout=120) for _ in range(3)]
     finally:
         bi.close()
-    for _bt, _tt, lab in got:
+    for _bt, _tt, lab, _split in got:
         assert 99 not in lab.tolist()
     assert bi.bad_records >= 1
 
@@ -289,3 +311,54 @@ def test_gpu_pipeline_error_surfaces_in_next_batch(tmp_path):
             bi.next_batch()
     finally:
         bi.close()
+
+
+def _jpeg_shard(tmp_path, n=10, progressive_every=4):
+    from PIL import Image
+    out = tmp_path / "sd"
+    out.mkdir()
+    rng = np.random.RandomState(3)
+    with TFRecordWriter(str(out / "train-00000-of-00001")) as w:
+        for i in range(n):
+            b = io.BytesIO()
+            img = (rng.rand(20 + 3 * i, 31 + i, 3) * 255).astype(np.uint8)
+            Image.fromarray(img).save(b, format="JPEG", quality=85, progressive=(i % progressive_every == 3))
+            w.write(encode_example({"image/encoded": b.getvalue(), "image/class/label": i + 1,
+                                    "image/object/bbox/xmin": [0.1], "image/object/bbox/ymin": [0.1],
+                                    "image/object/bbox/xmax": [0.9], "image/object/bbox/ymax": [0.9]}))
+    return imagenet.ImagenetData("train", str(out))
+
+
+def test_gpu_pipeline_split_decode_host_side(tmp_path):
+    """Split decode (host Huffman + device IDCT/colour): the assembler packs the coefficients and the
+    JpegDesc table so that each image's device RGB lands at its parameter-table slot; progressive files
+    fall back to PIL pixels.  Rebuilt here with the CPU form of the device stage, every slot equals the
+    full-decode pipeline's pixels (and the parameters / labels are identical)."""
+    from distributed_tensorflow_models_amd.data import imagenet_gpu, jpeg
+    ds = _jpeg_shard(tmp_path)
+    full = _assembled(ds, False, 2, 2, split=False)
+    sp = _assembled(ds, False, 2, 2, split=True)
+    for (bt, tt, lab, _n), (coefs, tt2, lab2, split) in zip(full, sp):
+        assert torch.equal(lab, lab2) and torch.equal(tt, tt2)
+        assert split is not None
+        dt, n, _mb, _mp, _np, total, fb = split
+        tab = tt2.numpy().view(imagenet_gpu._PARAM_DT)
+        descs = dt.numpy().view(jpeg.DESC_DT)
+        rgb = np.zeros(total, np.uint8)
+        cv = coefs.numpy()
+        for d in descs:  # device stage, CPU form
+            info = np.zeros(1, jpeg.INFO_DT)[0]
+            for f in ("width", "height", "ncomp", "hmax", "vmax", "h", "v", "bw", "bh", "coef_off", "qt"):
+                info[f] = d[f]
+            info["coef_count"] = int(sum(int(d["bw"][c]) * int(d["bh"][c]) * 64 for c in range(int(d["ncomp"]))))
+            b = int(d["coef_base"])
+            px = jpeg.pixels_cpu(info, cv[b:b + int(info["coef_count"])])
+            o = int(d["rgb_off"])
+            rgb[o:o + px.size] = px.reshape(-1)
+        if fb is not None:
+            fbt, lst = fb
+            for o, so, nb in lst:
+                rgb[o:o + nb] = fbt.numpy()[so:so + nb]
+        assert n == len(descs) and fb is not None  # both kinds present in these batches
+        np.testing.assert_array_equal(rgb, bt.numpy()[:total])
+        assert int(tab["src_off"][-1] + tab["h"][-1] * tab["w"][-1] * 3) == total

@@ -55,3 +55,40 @@ def test_gpu_batch_inputs_from_tfrecords(tmp_path):
     assert x.is_cuda and x.dtype == torch.bfloat16 and tuple(x.shape) == (8, 64, 64, 3)
     assert float(x.float().min()) >= -1.0 and float(x.float().max()) <= 1.0
     assert set(y.tolist()) <= set(range(1, 6)) and not torch.equal(x, x2)
+
+
+def test_split_decode_pipeline_matches_full_decode(tmp_path):
+    """Device batches through the split JPEG decode (host Huffman + HIP IDCT / upsampling / colour) equal
+    the full host-decode pipeline's (same seeds -> same crops and colour parameters), including a
+    progressive file that takes the PIL fallback inside a split batch.  (The decoded pixels are bit-exact -
+    tests/test_jpeg.py; the preprocessing's per-image contrast mean is an fp32 atomic sum, so the bf16
+    batches agree to rounding.)"""
+    from PIL import Image
+
+    from distributed_tensorflow_models_amd.data.tfrecord import TFRecordWriter, encode_example
+    out = tmp_path / "d"
+    out.mkdir()
+    rng = np.random.RandomState(5)
+    with TFRecordWriter(str(out / "train-00000-of-00001")) as w:
+        for i in range(16):
+            b = io.BytesIO()
+            img = (rng.rand(40 + 7 * i, 60 + 5 * i, 3) * 255).astype(np.uint8)
+            Image.fromarray(img).save(b, format="JPEG", quality=80 + i, progressive=(i == 5),
+                                      subsampling=[0, 1, 2][i % 3])
+            w.write(encode_example({"image/encoded": b.getvalue(), "image/class/label": i + 1,
+                                    "image/object/bbox/xmin": [0.05], "image/object/bbox/ymin": [0.1],
+                                    "image/object/bbox/xmax": [0.9], "image/object/bbox/ymax": [0.95]}))
+    ds = imagenet.ImagenetData("train", str(out))
+    res = []
+    for split in (False, True):
+        bi = G.GPUBatchInputs(ds, 8, train=True, image_size=64, num_readers=1, num_decoders=2, seed=11, device="cuda",
+                              decode_processes=False, shuffle_buffer=32, split_decode=split)
+        try:
+            res.append([bi.next_batch() for _ in range(2)])
+        finally:
+            bi.close()
+    torch.cuda.synchronize()
+    for (x0, y0), (x1, y1) in zip(*res):
+        assert torch.equal(y0, y1)
+        torch.testing.assert_close(x0.float(), x1.float(), rtol=0, atol=1e-2)
+        assert (x0 != x1).float().mean().item() < 0.01

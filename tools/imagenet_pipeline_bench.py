@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--batches", type=int, default=12)
     ap.add_argument("--warm-batches", type=int, default=4)
     ap.add_argument("--host", action="store_true", help="also time the host (numpy) pipeline")
+    ap.add_argument("--mode", default="both", choices=("split", "full", "both"),
+                    help="JPEG decode: split (host Huffman + HIP IDCT/colour), full (host PIL), both (alternating)")
     args = ap.parse_args()
     import torch
 
@@ -55,20 +57,23 @@ def main():
     avg = write_shards(d, args.images)
     print("wrote %d synthetic JPEGs to %s (avg %.0f KB)" % (args.images, d, avg / 1024), flush=True)
     ds = imagenet.ImagenetData("train", d)
-    bi = imagenet_gpu.distorted_inputs(ds, args.batch, num_preprocess_threads=4, image_size=args.size,
-                                       num_readers=4, num_decoders=args.decoders)
-    for _ in range(args.warm_batches):  # warm-up (decoder start-up: spawned processes import the package)
-        x, _ = bi.next_batch()
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    for _ in range(args.batches):
-        x, y = bi.next_batch()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t
-    bi.close()
-    print("gpu pipeline: %.0f img/s sustained (batch %d, %d decoder %s, %dx%d bf16 out)" % (
-        args.batches * args.batch / dt, args.batch, args.decoders,
-        "threads" if os.environ.get("DTM_DECODE_PROCESSES") == "0" else "processes", args.size, args.size), flush=True)
+    modes = {"split": [True], "full": [False], "both": [False, True, False, True]}[args.mode]
+    for split in modes:
+        bi = imagenet_gpu.distorted_inputs(ds, args.batch, num_preprocess_threads=4, image_size=args.size,
+                                           num_readers=4, num_decoders=args.decoders, split_decode=split)
+        for _ in range(args.warm_batches):  # warm-up (decoder start-up: spawned processes import the package)
+            x, _ = bi.next_batch()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(args.batches):
+            x, y = bi.next_batch()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+        bi.close()
+        print("gpu pipeline (%s decode): %.0f img/s sustained (batch %d, %d decoder %s, %dx%d bf16 out)" % (
+            "split host-Huffman + HIP IDCT/colour" if split else "full host PIL", args.batches * args.batch / dt,
+            args.batch, args.decoders, "threads" if os.environ.get("DTM_DECODE_PROCESSES") == "0" else "processes",
+            args.size, args.size), flush=True)
     # device-side cost alone: the two kernels on a resident batch
     from distributed_tensorflow_models_amd.data.imagenet_gpu import gpu_preprocess
     rng = np.random.RandomState(0)
