@@ -58,6 +58,7 @@ __host__ static inline FastDiv make_fastdiv(uint32_t d) {
 // workspace arena + two-stage reduction (workspace.hip)
 float* dtm_ws_get(size_t floats);
 void dtm_reduce_rows(const float* ws, int rows, int width, int ld, float* out, hipStream_t st);
+float* dtm_ws_get_stream(size_t floats, hipStream_t st);  // the side stream's own arena
 void dtm_reduce_split(int rows, int xblocks, int* rpb, int* ychunks);
 int dtm_reduce_direct_max();
 int dtm_ntld_bits();  // non-temporal input-load policy of the BN-apply kernels (fused_bn.hip)  // grids up to this many blocks reduce with atomics in the producer

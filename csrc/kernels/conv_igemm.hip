@@ -111,7 +111,10 @@ __device__ __forceinline__ void epi_barrier() {
 // OROW bytes (pixel-major); each thread stores full 16-B chunks (coalesced NHWC rows) with the dgrad
 // post-ops (add_src, activation backward, block-output BN-apply backward) and the BatchNorm statistics
 // / post-op partial sums.  Shared by the 16x16x32 and the 32x32x16 MFMA register layouts.
-template <int PT, int CT, bool RAWB, bool EXACT, bool SACC, int NT>
+// SIDE = false compiles the dgrad post-ops out: their loads are what the compiler's own vmcnt waits track,
+// and a persistent kernel's loop-carried wait for them (vmcnt(n) with the LDS-DMA prefetch issued after
+// them, which the compiler does not count) would drain the prefetch every tile.
+template <int PT, int CT, bool RAWB, bool EXACT, bool SACC, int NT, bool SIDE = true>
 __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem, int p0, int c0, int by,
                                                  float* ssum, float* ssq) {
   constexpr int OROW = CT * 2 + 16;
@@ -122,7 +125,7 @@ __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem
   static_assert(NT % CPR == 0 && (PT * CPR) % NT == 0, "staged-store mapping");
   const int chn = tid % CPR;   // fixed per thread (NT % CPR == 0)
   const int kc = c0 + chn * 8;
-  const bool act = a.act_x != nullptr;
+  const bool act = SIDE && a.act_x != nullptr;
   // BatchNorm statistics of a staged tile: each thread sums its fixed 8-channel chunk column over its
   // rows (bf16-rounded outputs) and the block reduces them once through LDS below -> ONE partial row
   // per pixel tile, no per-subtile shuffle trees (those cost up to +100 % on the wide-K 1x1 layers)
@@ -142,7 +145,7 @@ __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem
   // GRP rows before any of them is used, so their latencies overlap instead of serialising per row
   constexpr int GRP = NIT < 4 ? NIT : 4;
   static_assert(NIT % GRP == 0, "epilogue row groups");
-  const bool side = a.add_src != nullptr || act;
+  const bool side = SIDE && (a.add_src != nullptr || act);
 #pragma unroll
   for (int g0 = 0; g0 < NIT; g0 += GRP) {
     uint4 pa[GRP], px[GRP], pr[GRP];
@@ -293,7 +296,7 @@ __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem
 }
 
 template <int PT, int CT, int WP, int WC, int STG, bool RAWB = false, bool EXACT = false, bool NOBIAS = false,
-          bool SACC = false, int NT = 256>
+          bool SACC = false, int NT = 256, bool SIDE = true>
 __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&acc)[WC / 16][WP / 16], char* smem,
                                                  int p0, int c0, int by, float* ssum = nullptr,
                                                  float* ssq = nullptr) {
@@ -360,7 +363,7 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
       }
     }
   }
-  if constexpr (staged) conv_nt_epi_tail<PT, CT, RAWB, EXACT, SACC, NT>(a, smem, p0, c0, by, ssum, ssq);
+  if constexpr (staged) conv_nt_epi_tail<PT, CT, RAWB, EXACT, SACC, NT, SIDE>(a, smem, p0, c0, by, ssum, ssq);
 }
 
 // Epilogue of the 32x32x16-MFMA kernels (staged stores only: K % 8 == 0).  Register layout of a 32x32
@@ -1018,7 +1021,12 @@ __device__ __forceinline__ void glds16(const void* gptr, const void* lds) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr), "s"(l) : "memory", "m0");
 }
 
-template <int PT, int CT, int NKT, bool PRO>
+// STEM: the packed-row stem view (ConvDesc.pix_bytes = 8, C = 32 "channels" = 8 taps x 4 input channels,
+// an R x 1 conv with stride): the A chunk of k for output pixel (n, p, q) is the 16 B at input row
+// p*stride + k/32, column q*stride, byte (k % 32) * 2 of the zero-bordered [N][Hp][Wp][4] image -
+// the 7x7/2 ResNet stem as a persistent stream with its 64 x 224 weights resident in LDS.  Its A tiles
+// (28 KiB of L2-resident rows per 64 pixels) ride a 3-slot ring (NBUF = 3): two tiles in flight.
+template <int PT, int CT, int NKT, bool PRO, bool STEM = false, int NBUF = 2, bool SIDE = true>
 __global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int ntiles) {
   constexpr int WP = PT / 2, WC = CT / 2;
   constexpr int TP = WP / 16, TC = WC / 16;
@@ -1029,7 +1037,10 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int n
   constexpr int STG = PT * OROW > 16384 ? PT * OROW : 16384;
   constexpr int NIT = PT * (CT / 8) / 256;      // exact staged stores per thread per tile
   constexpr int MAXC = 512;
-  constexpr int OFF_A = WBUF, OFF_S = WBUF + 2 * ABUF, OFF_P = OFF_S + STG;
+  constexpr int OFF_A = WBUF, OFF_S = WBUF + NBUF * ABUF, OFF_P = OFF_S + STG;
+  constexpr int NDMA = NKT * AI;                // DMA instructions per thread per tile
+  static_assert(NBUF == 2 || NBUF == 3, "ring depth");
+  static_assert(2 * NIT + NDMA <= 63, "vmcnt range");
   __shared__ __attribute__((aligned(16))) char smem[OFF_P + (PRO ? MAXC * 8 : 0)];
   typedef __attribute__((address_space(1))) const void gvoid;
   typedef __attribute__((address_space(3))) void lvoid;
@@ -1069,6 +1080,17 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int n
   const char* srcs[NKT * AI];
   auto issue = [&](int t, int buf) {
     char* base = smem + OFF_A + buf * ABUF;
+    uint32_t pix[AI];  // STEM: byte offset of each of this lane's pixels' first tap
+    if constexpr (STEM) {
+#pragma unroll
+      for (int j = 0; j < AI; ++j) {
+        const int m = t * PT + 8 * (wave + 4 * j) + lr;
+        const uint32_t mm = m < a.M ? (uint32_t)m : 0u;
+        const uint32_t n = fdiv(mm, a.fd_PQ), rem = mm - n * (a.P * a.Q);
+        const uint32_t p = fdiv(rem, a.fd_Q), q = rem - p * a.Q;
+        pix[j] = ((n * a.Hin + p * a.stride) * a.Win + q * a.stride) * 8u;
+      }
+    }
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
       const int k = kt * 64 + ch * 8;
@@ -1076,7 +1098,8 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int n
       for (int j = 0; j < AI; ++j) {
         const int m = t * PT + 8 * (wave + 4 * j) + lr;
         const bool v = (m < a.M) & (k < a.Kg);
-        const char* src = xg + (size_t)(uint32_t)(m * a.pix_bytes + k * 2);
+        const char* src = STEM ? xg + (size_t)(pix[j] + (uint32_t)((k >> 5) * a.Win * 8 + (k & 31) * 2))
+                               : xg + (size_t)(uint32_t)(m * a.pix_bytes + k * 2);
         srcs[kt * AI + j] = v ? src : zg;
         glds16(srcs[kt * AI + j], base + kt * PT * 128 + (wave + 4 * j) * 1024);
       }
@@ -1118,17 +1141,29 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int n
 #pragma unroll
   for (int e = 0; e < 8; ++e) { ssum[e] = 0.f; ssq[e] = 0.f; }
   int t = by0;
+  const int gy = gridDim.y;
   if (t < ntiles) issue(t, 0);
+  if (NBUF == 3 && t + gy < ntiles) issue(t + gy, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // weights (+ prologue affine) resident, tile 0 landed
+  __syncthreads();  // weights (+ prologue affine) resident, tile 0 (and 1) landed
   int buf = 0;
-  for (int it = 0; t < ntiles; ++it, t += gridDim.y) {
-    // this wave's DMA of tile t has landed once at most the previous epilogue's NIT stores are pending
-    if (it > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIT) : "memory");
+  for (int it = 0; t < ntiles; ++it, t += gy) {
+    if constexpr (NBUF == 2) {
+      // this wave's DMA of tile t has landed once at most the previous epilogue's NIT stores are pending
+      if (it > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIT) : "memory");
+    } else if (it >= 2) {
+      // issued after this wave's DMA of tile t: stores(it-2), the DMA of tile t+gy (if any), stores(it-1)
+      if (t + gy < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NIT + NDMA) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NIT) : "memory");
+    }
     if constexpr (PRO) transform(t, buf);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // tile t visible; the other buffer and the stage area are free
-    if (t + (int)gridDim.y < ntiles) issue(t + gridDim.y, buf ^ 1);
+    __builtin_amdgcn_s_barrier();  // tile t visible; the slot read last iteration and the stage area are free
+    if constexpr (NBUF == 2) {
+      if (t + gy < ntiles) issue(t + gy, buf ^ 1);
+    } else {
+      if (t + 2 * gy < ntiles) issue(t + 2 * gy, buf == 0 ? 2 : buf - 1);
+    }
     f32x4 acc[TC][TP];
 #pragma unroll
     for (int i = 0; i < TC; ++i)
@@ -1158,10 +1193,11 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int n
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
       }
     }
-    conv_nt_epilogue<PT, CT, WP, WC, 1, true, true, true, true>(a, acc, smem + OFF_S, t * PT, c0, t, ssum, ssq);
+    conv_nt_epilogue<PT, CT, WP, WC, 1, true, true, true, true, 256, SIDE>(a, acc, smem + OFF_S, t * PT, c0, t, ssum,
+                                                                           ssq);
 #pragma unroll
     for (int i = 0; i < NKT * AI; ++i) asm volatile("" ::"v"(srcs[i]));
-    buf ^= 1;
+    buf = buf + 1 == NBUF ? 0 : buf + 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (a.stats) {
@@ -1771,11 +1807,12 @@ static bf16_t* dump_chunk() {
 
 // persistent streaming 1x1 kernel: blocks = resident capacity (occupancy x CUs), channel tiles x
 // pixel-tile workers
-template <int PT, int CT, int NKT, bool PRO>
+template <int PT, int CT, int NKT, bool PRO, bool STEM = false, int NBUF = 2, bool SIDE = true>
 static int stream_workers_k(const ConvNTArgs& a) {
   static int occ = 0;
   if (!occ) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv1x1_stream_kernel<PT, CT, NKT, PRO>, 256, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv1x1_stream_kernel<PT, CT, NKT, PRO, STEM, NBUF, SIDE>,
+                                                     256, 0) !=
             hipSuccess || occ <= 0)
       occ = 1;
   }
@@ -1787,29 +1824,51 @@ static int stream_workers_k(const ConvNTArgs& a) {
   return workers;
 }
 
-template <int PT, int CT, int NKT, bool PRO>
+template <int PT, int CT, int NKT, bool PRO, bool STEM = false, int NBUF = 2, bool SIDE = true>
 static void launch_stream_k(const ConvNTArgs& a, hipStream_t st) {
   const int ctiles = (a.K + CT - 1) / CT;
   const int ntiles = (a.M + PT - 1) / PT;
-  hipLaunchKernelGGL((conv1x1_stream_kernel<PT, CT, NKT, PRO>), dim3(ctiles, stream_workers_k<PT, CT, NKT, PRO>(a)),
-                     dim3(256), 0, st, a, ntiles);
+  hipLaunchKernelGGL((conv1x1_stream_kernel<PT, CT, NKT, PRO, STEM, NBUF, SIDE>),
+                     dim3(ctiles, stream_workers_k<PT, CT, NKT, PRO, STEM, NBUF, SIDE>(a)), dim3(256), 0, st, a, ntiles);
+}
+
+static bool stem_stream_ok(const ConvNTArgs& a) {
+  // the packed-row stem view, no prologue / bias / relu, whole 64-channel tiles, R <= 8 kernel rows
+  return a.pix_bytes == 8 && a.C == 32 && a.S == 1 && a.pad_h == 0 && a.pad_w == 0 && a.Kg == a.R * 32 &&
+         a.Kg <= 256 && a.K % 64 == 0 && !a.in_scale && !a.bias && !a.relu && a.ostr == 1;
 }
 
 template <int CT, int NKT>
 static void launch_stream(const ConvNTArgs& a, hipStream_t st) {
-  if (a.in_scale) launch_stream_k<64, CT, NKT, true>(a, st);
-  else launch_stream_k<64, CT, NKT, false>(a, st);
+  const bool side = a.add_src || a.act_x;
+  if (a.in_scale) {
+    if (side) launch_stream_k<64, CT, NKT, true, false, 2, true>(a, st);
+    else launch_stream_k<64, CT, NKT, true, false, 2, false>(a, st);
+  } else if (side) launch_stream_k<64, CT, NKT, false, false, 2, true>(a, st);
+  else launch_stream_k<64, CT, NKT, false, false, 2, false>(a, st);
+}
+template <int CT, int NKT>
+static int stream_workers(const ConvNTArgs& a) {
+  const bool side = a.add_src || a.act_x;
+  if (a.in_scale) return side ? stream_workers_k<64, CT, NKT, true, false, 2, true>(a)
+                              : stream_workers_k<64, CT, NKT, true, false, 2, false>(a);
+  if (side) return stream_workers_k<64, CT, NKT, false, false, 2, true>(a);
+  return stream_workers_k<64, CT, NKT, false, false, 2, false>(a);
 }
 
-// statistics partial rows of the streaming kernel (tile id 30 / 31): one per worker
+// the stem forward as a persistent stream: -1: DTM_STEM_STREAM env (default 1), 0 off, 1 on (3-slot ring),
+// 2 on with the 2-slot ring (A/B knob)
+static int g_stem_stream = -1;
+DTM_API void dtm_conv_set_stem_stream(int on) { g_stem_stream = on; }
+// statistics partial rows of the streaming kernel (tile id 30 / 31 / 33): one per worker
 static int stream_rows(const ConvNTArgs& a, int id) {
-  const bool pro = a.in_scale != nullptr, k1 = a.Kg <= 64;
+  if (id == 33) return g_stem_stream == 2 ? stream_workers_k<64, 64, 4, false, true, 2, false>(a)
+                                          : stream_workers_k<64, 64, 4, false, true, 3, false>(a);
+  const bool k1 = a.Kg <= 64;
   if (id == 30) {
-    if (k1) return pro ? stream_workers_k<64, 128, 1, true>(a) : stream_workers_k<64, 128, 1, false>(a);
-    return pro ? stream_workers_k<64, 128, 2, true>(a) : stream_workers_k<64, 128, 2, false>(a);
+    return k1 ? stream_workers<128, 1>(a) : stream_workers<128, 2>(a);
   }
-  if (k1) return pro ? stream_workers_k<64, 64, 1, true>(a) : stream_workers_k<64, 64, 1, false>(a);
-  return pro ? stream_workers_k<64, 64, 2, true>(a) : stream_workers_k<64, 64, 2, false>(a);
+  return k1 ? stream_workers<64, 1>(a) : stream_workers<64, 2>(a);
 }
 
 static bool stream_ok(const ConvNTArgs& a) {
@@ -1865,6 +1924,12 @@ static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
   // variants win almost everywhere (more resident blocks hide the short-K latency); the 2-buffer
   // 128x128 tile keeps the small-M / deep-K layers (7x7 maps, K-reduction >= 2048)
   int id = g_tile_env;
+  if (g_stem_stream < 0) {
+    const char* e = getenv("DTM_STEM_STREAM");
+    g_stem_stream = e ? atoi(e) : 1;
+  }
+  // the packed-row stem as a persistent stream (weights resident, pixel tiles prefetched)
+  if (id == -1 && g_stem_stream && stem_stream_ok(a)) return {33, 64, 2};
   // the pipelined LDS-DMA 128x128 tile (2 slots, 2 blocks/CU) wins every deep-reduction layer without the
   // prologue (tools/conv_tile_sweep.py: 3x3 at 14x14 / 7x7 -13..-18 %, deep 1x1 -5..-16 %)
   if (id == -4) id = -1;  // (-4: the policy without the streaming kernel, for A/B runs)
@@ -1947,6 +2012,9 @@ static void dispatch_ud(const ConvNTArgs& a, const TileCfg& t, hipStream_t st) {
   else if (t.id == 30 && UD == 1) {
     if (a.Kg <= 64) launch_stream<128, 1>(a, st);
     else launch_stream<128, 2>(a, st);
+  } else if (t.id == 33 && UD == 1) {
+    if (g_stem_stream == 2) launch_stream_k<64, 64, 4, false, true, 2, false>(a, st);  // (A/B: 2-slot ring)
+    else launch_stream_k<64, 64, 4, false, true, 3, false>(a, st);
   } else if (t.id == 31 && UD == 1) {
     if (a.Kg <= 64) launch_stream<64, 1>(a, st);
     else launch_stream<64, 2>(a, st);
@@ -2000,7 +2068,7 @@ static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, cons
   const TileCfg tc = pick_tile(a, stats);
   if (stats) {
     // one per streaming worker; one per pixel tile (staged epilogue, K % 8 == 0); else per (pixel tile, pixel wave)
-    rows = (tc.id == 30 || tc.id == 31) ? stream_rows(a, tc.id)
+    rows = (tc.id == 30 || tc.id == 31 || tc.id == 33) ? stream_rows(a, tc.id)
                                          : ((a.M + tc.PT - 1) / tc.PT) * ((a.K & 7) == 0 ? 1 : tc.NWP);
     float* ws = dtm_ws_get((size_t)rows * 2 * d->K);
     if (!ws) return -4;
@@ -2251,7 +2319,7 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   a.pix_per_split = (int)(steps_per * 64);
   splits = (a.Mpix + a.pix_per_split - 1) / a.pix_per_split;
   const size_t slab = (size_t)splits * a.K * a.Kg;
-  float* ws = dtm_ws_get(slab);
+  float* ws = dtm_ws_get_stream(slab, (hipStream_t)stream);
   if (!ws) return -4;
   a.dw = ws;
   if (wt >= 10) {

@@ -162,3 +162,28 @@ void dtm_reduce_rows(const float* ws, int rows, int width, int ld, float* out, h
 }
 
 DTM_API int dtm_ws_reserve(long floats) { return dtm_ws_get((size_t)floats) ? 0 : -1; }
+
+// A second arena for work enqueued on the weight-gradient side stream (ops/_lib.py side_stream): the
+// split-K slabs of a wgrad there must not share scratch with the dgrad / statistics kernels running
+// concurrently on the main stream.
+static hipStream_t g_side_stream = nullptr;
+static float* g_ws_side = nullptr;
+static size_t g_ws_side_floats = 0;
+DTM_API void dtm_ws_set_side_stream(void* s) { g_side_stream = (hipStream_t)s; }
+float* dtm_ws_get_stream(size_t floats, hipStream_t st) {
+  if (st == nullptr || st != g_side_stream) return dtm_ws_get(floats);
+  if (floats > g_ws_side_floats) {
+    size_t n = floats < (16u << 20) ? (16u << 20) : floats;
+    if (g_ws_side) {
+      hipDeviceSynchronize();
+      hipFree(g_ws_side);
+    }
+    if (hipMalloc(&g_ws_side, n * sizeof(float)) != hipSuccess) {
+      g_ws_side = nullptr;
+      g_ws_side_floats = 0;
+      return nullptr;
+    }
+    g_ws_side_floats = n;
+  }
+  return g_ws_side;
+}

@@ -102,6 +102,8 @@ class TrainStep:
             self.bufsync.issue()  # forward has finished every moving-statistics update
             with roctx("backward"):  # bucket all-reduces are issued (own ranges) from the grad hooks
                 loss.backward()
+            if images.is_cuda:
+                _lib.side_join()  # weight gradients enqueued on the side stream (ops/_lib.py)
             self._mark("bwd")
         finally:
             _fused.arena.end_step()

@@ -231,6 +231,18 @@ class _ConvBNFn(torch.autograd.Function):
         sc = in_ss[0] if (in_ss is not None and not ctx.mat) else None
         sh = in_ss[1] if (in_ss is not None and not ctx.mat) else None
         dx = d_in = None
+        # the weight gradient on the side stream (ops/_lib.py side_stream), enqueued BEFORE the dgrad so
+        # the two run concurrently; its bucket all-reduce is launched from that stream (parallel/bsp.py)
+        wg_side = False
+        if ctx.needs_input_grad[2] and getattr(w, "main_grad", None) is not None:
+            st = _lib.side_fork(x, dy, in_ss)
+            if st is not None:
+                with torch.cuda.stream(st):
+                    _check(L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(w.main_grad), _lib.ptr(sc),
+                                            _lib.ptr(sh), ctypes.byref(d), _lib.num_cus(), _lib.stream_ptr()),
+                           "conv_wgrad(side)")
+                    _notify(w)
+                wg_side = True
         if ctx.needs_input_grad[0] or (in_ss is not None and ctx.needs_input_grad[1]):
             last, add_src, add_stride = _slot_take(ctx.slot)
             # stride > 1: one stride-1 conv per output parity class instead of the zero-dilated dgrad
@@ -271,7 +283,9 @@ class _ConvBNFn(torch.autograd.Function):
                     ctx.slot.buf, ctx.slot.stride = dx, 1
                     dx = None
             d.dec = 0
-        if ctx.needs_input_grad[2]:
+        if wg_side:
+            dw = None
+        elif ctx.needs_input_grad[2]:
             mg = getattr(w, "main_grad", None)
             target = mg if mg is not None else torch.zeros(w.shape, device=dy.device, dtype=torch.float32)
             _check(L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(target), _lib.ptr(sc),

@@ -25,6 +25,7 @@ import time
 import torch
 import torch.distributed as dist
 
+from ..ops import _lib
 from . import process_group as pg
 
 STORE_PREFIX = "dtm_asp"
@@ -394,6 +395,8 @@ class ASPTrainStep:
         out = self.model(images, training=True)
         loss = self.loss_fn(out, labels)
         loss.backward()
+        if images.is_cuda:
+            _lib.side_join()  # weight gradients enqueued on the side stream (ops/_lib.py)
         gs = self.store.global_step()
         lr = self.lr_schedule(gs) if self.lr_schedule else None
         self.store.push_buffers()

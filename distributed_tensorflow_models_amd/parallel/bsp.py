@@ -32,6 +32,7 @@ With world_size == 1 no collective is issued.
 import torch
 import torch.distributed as dist
 
+from ..ops import _lib
 from ..ops import nn as opsnn
 from ..utils.profiler import roctx
 
@@ -190,6 +191,17 @@ class BSPDataParallel:
         self._launched[bi] = True
         if self.world == 1:
             return
+        side = _lib.side_active() if self.flat.is_cuda else None
+        if side is not None and torch.cuda.current_stream() != side:
+            # weight gradients run on the side stream (ops/_lib.py): the all-reduce goes after both
+            # streams' work so far without making the main stream wait for the side one
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                self._launch_now(bi)
+        else:
+            self._launch_now(bi)
+
+    def _launch_now(self, bi):
         with roctx("allreduce_bucket_%d" % bi):
             if bi in self.compact:
                 p, (r0, r1, s0, s1), buf, low = self.compact[bi]
@@ -211,6 +223,8 @@ class BSPDataParallel:
         for bi in range(len(self.buckets)):
             if not self._launched[bi]:
                 self._launch(bi)
+        if self.flat.is_cuda:
+            _lib.side_join()
         for bi, w in self._works:
             w.wait()
             if bi in self.compact:

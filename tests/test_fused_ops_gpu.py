@@ -231,6 +231,60 @@ def test_stem_packed_row_conv_bn(monkeypatch, H, W, C, N, R, pad, stemw):
     assert all(v < 5e-2 for v in errs.values()), errs
 
 
+@pytest.mark.parametrize("sstr", [0, 1, 2])
+@pytest.mark.parametrize("H,W,N,R,pad", [(224, 224, 2, 7, (3, 3)), (17, 23, 3, 7, (3, 3)), (41, 41, 2, 3, "VALID")])
+def test_stem_stream_kernel(H, W, N, R, pad, sstr):
+    """The stem forward as a persistent stream (tile id 33: 64 x 224 weights resident in LDS, packed-row
+    pixel tiles prefetched; dtm_conv_set_stem_stream) and the pipelined-tile form both match torch fp32:
+    output and BN statistics (ragged last pixel tile included: 17x23)."""
+    from distributed_tensorflow_models_amd.ops import _lib
+    L = _lib.lib()
+    torch.manual_seed(0)
+    x = torch.randn(N, H, W, 3, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(64, R, R, 3, device=DEV) / (R * R * 3) ** 0.5).to(torch.bfloat16).float()
+    bn, bn_r = _bn(64), _bn(64)
+    with torch.no_grad():
+        bn_r.gamma.copy_(bn.gamma)
+        bn_r.beta.copy_(bn.beta)
+    L.dtm_conv_set_stem_stream(sstr)
+    try:
+        yk = fused.conv_bn(x, w, bn, 2, pad, True, True).materialize()
+        torch.cuda.synchronize()
+    finally:
+        L.dtm_conv_set_stem_stream(1)
+    yr = ref.batch_norm(ref.conv2d(x.float(), w, None, 2, pad), bn_r.gamma.detach(), bn_r.beta.detach(),
+                        bn_r.moving_mean, bn_r.moving_variance, True, 0.9, 1e-3, True)
+    errs = dict(y=_rel(yk, yr), mm=_rel(bn.moving_mean, bn_r.moving_mean),
+                mv=_rel(bn.moving_variance, bn_r.moving_variance))
+    assert all(v < 1e-2 for v in errs.values()), errs
+
+
+def test_wgrad_side_stream_matches_main_stream():
+    """Conv+BN weight gradients enqueued on the side stream (ops/_lib.py side_stream, concurrent with the
+    dgrad chain, own scratch arena) give the same flat gradient as the single-stream backward."""
+    from distributed_tensorflow_models_amd.engine import TrainStep
+    from distributed_tensorflow_models_amd.models import nets_factory
+    from distributed_tensorflow_models_amd.ops import _lib
+    torch.manual_seed(0)
+    net = nets_factory.build("resnet_v1_50", num_classes=10).to(DEV)
+    step = TrainStep(net, optimizer="momentum", lr=0.0, momentum=0.9)
+    x = torch.randn(8, 64, 64, 3, device=DEV).to(torch.bfloat16)
+    y = torch.randint(0, 10, (8,), device=DEV)
+    grads = {}
+    try:
+        for on in (False, True, False):
+            _lib.set_side_enabled(on)
+            step._forward_backward(x, y)
+            torch.cuda.synchronize()
+            grads.setdefault(on, []).append(step.dp.flat.detach().clone())
+    finally:
+        _lib.set_side_enabled(False)
+    ref0, side = grads[False][0], grads[True][0]
+    noise = _rel(grads[False][1], ref0)  # run-to-run (atomics in the reductions)
+    assert _lib.side_active() is None
+    assert _rel(side, ref0) <= max(10 * noise, 1e-5), (_rel(side, ref0), noise)
+
+
 def test_block_output_bn_backward_in_dgrad_epilogue(monkeypatch):
     """ResNet-50 v1: the block-output BN-apply backward (mask, d(scale)/d(shift) sums, the residual's
     share) runs inside the dgrad epilogue of the conv that consumes the block output last; every
