@@ -32,7 +32,7 @@ PRESETS = {
     "resnet_v1_50": (224, 1000, 256, "momentum", {}),
     # config #4: old-slim Inception-v3 as the reference trains it (RMSProp, label smoothing, aux head)
     "inception_v3_slim_old": (299, 1001, 128, "rmsprop", dict(label_smoothing=0.1, aux_weight=0.4, rho=0.9,
-                                                              epsilon=1.0)),
+                                                              epsilon=1.0, wgrad_stream=False)),
     # config #5: VGG-16 with the reference's CIFAR geometry (10 classes, 134.3 M params)
     "vgg_16": (32, 10, 512, "sgd", {}),
     # config #1 plumbing model

@@ -179,8 +179,10 @@ def side_stream():
     """The weight-gradient side stream, or None when off / not on a GPU."""
     if _side["on"] is None:
         _side["on"] = os.environ.get("DTM_WGRAD_STREAM", "1") == "1"
-    if not _side["on"] or not torch.cuda.is_available() or torch.cuda.is_current_stream_capturing():
-        return None  # (hipGraph capture: single stream)
+    if not _side["on"] or not torch.cuda.is_available():
+        return None
+    if torch.cuda.is_current_stream_capturing() and os.environ.get("DTM_WGRAD_STREAM_GRAPH", "0") != "1":
+        return None  # (hipGraph capture: single stream unless DTM_WGRAD_STREAM_GRAPH=1)
     dev = torch.cuda.current_device()
     st = _side["stream"]
     if st is None or st.device.index != dev:

@@ -83,7 +83,7 @@ PRESETS = {
                       rmsprop_epsilon=1.0, ema=0.9999, wd_all=None, label_smoothing=0.1, aux_weight=0.4,
                       max_steps=10000000, save_secs=600, log_style="short", max_to_keep=5, nan_guard=True,
                       train_dir="/home/ubuntu/imagenet/train/", data_dir="/home/ubuntu/imagenet/data/",
-                      wipe=False),
+                      wipe=False, wgrad_stream=False),
     # vgg/nets/mobilenet_v1_train.py:57-160 (SGD 0.045, x0.94 every 2.5 epochs, batch 64)
     "mobilenet_v1": dict(model="mobilenet_v1", num_classes=1001, dataset="imagenet", image_size=224, batch_size=64,
                          lr=0.045, lr_scale_workers=False, decay_epochs=2.5, decay_factor=0.94, optimizer="sgd",
@@ -284,6 +284,7 @@ def train(preset, flags, default_mode="bsp"):
                             aux_weight=cfg.get("aux_weight", 0.4), ema_decay=cfg.get("ema"), lr_schedule=sched,
                             batch_weight=FLAGS.batch_weight, use_graph=FLAGS.use_hipgraph and world == 1,
                             ema_buffers=cfg.get("ema_buffers", True), bn_sync_every=FLAGS.bn_sync_every,
+                            wgrad_stream=cfg.get("wgrad_stream"),
                             grad_comm_dtype=torch.bfloat16 if FLAGS.grad_comm_dtype == "bf16" else None,
                             timer=StepTimer() if (FLAGS.metrics_file and rank == 0 and not FLAGS.use_hipgraph)
                             else None, **opt_kw)

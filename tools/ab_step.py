@@ -21,6 +21,9 @@ from distributed_tensorflow_models_amd.models import nets_factory  # noqa: E402
 from distributed_tensorflow_models_amd.ops import _lib  # noqa: E402
 
 
+WGS_DEFAULT = [os.environ.get("DTM_WGRAD_STREAM", "1")]  # (the model preset's choice, set in main)
+
+
 def apply(cfg):
     L = _lib.lib()
     L.dtm_conv_set_tile(int(cfg.get("tile", -1)))
@@ -41,7 +44,7 @@ def apply(cfg):
     L.dtm_conv_set_k32(int(cfg.get("k32", "1")))
     L.dtm_conv_set_mfma32(int(cfg.get("m32", os.environ.get("DTM_MFMA32", "0"))))
     L.dtm_conv_set_stem_stream(int(cfg.get("sstr", "1")))
-    _lib.set_side_enabled(cfg.get("wgs", os.environ.get("DTM_WGRAD_STREAM", "1")) == "1")
+    _lib.set_side_enabled(cfg.get("wgs", WGS_DEFAULT[0]) == "1")
     sc = cfg.get("sc", "5:4096").split(":")
     L.dtm_set_sc_policy(int(sc[0]), int(sc[1]))
     os.environ["DTM_PROLOGUE"] = cfg.get("prologue", "auto")
@@ -68,6 +71,8 @@ def main():
     model = os.environ.get("MODEL", "resnet_v1_50")
     from bench import PRESETS
     S, ncls, B0, opt, extra = PRESETS[model]
+    if "wgrad_stream" in extra:
+        WGS_DEFAULT[0] = "1" if extra["wgrad_stream"] else "0"
     kw = {"fc_conv_padding": "SAME"} if model == "vgg_16" else {}  # (bench.py's CIFAR geometry)
     net = nets_factory.build(model, num_classes=ncls, **kw).to(dev)
     B = B or B0
