@@ -649,7 +649,7 @@ DTM_API int dtm_bn_stats_bwd(const void* y, const float* dstats, const void* g, 
 DTM_API void dtm_bn_stats(const void* x, float* stats, long M, int C, void* stream) {
   if (fast_ok(M, C)) {
     int blocks, rpb; fast_grid(M, C, &blocks, &rpb);
-    float* ws = dtm_ws_get((size_t)blocks * 2 * C);
+    float* ws = dtm_ws_get_stream((size_t)blocks * 2 * C, (hipStream_t)stream);
     hipLaunchKernelGGL(bn_stats_fast, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ws, (int)M, C, rpb);
     dtm_reduce_rows(ws, blocks, 2 * C, 2 * C, stats, (hipStream_t)stream);
     return;
@@ -730,7 +730,7 @@ DTM_API void dtm_bn_bwd_reduce(const void* dy, const void* x, const void* ymask,
                                int C, int mask_mode, void* stream) {
   if (fast_ok(M, C)) {
     int blocks, rpb; fast_grid(M, C, &blocks, &rpb);
-    float* ws = dtm_ws_get((size_t)blocks * 2 * C);
+    float* ws = dtm_ws_get_stream((size_t)blocks * 2 * C, (hipStream_t)stream);
     hipLaunchKernelGGL(bn_bwd_reduce_fast, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
                        (const bf16_t*)x, (const bf16_t*)ymask, ss, ws, (int)M, C, mask_mode, rpb);
     dtm_reduce_rows(ws, blocks, 2 * C, 2 * C, sums, (hipStream_t)stream);
@@ -770,29 +770,37 @@ DTM_API void dtm_bn_param_grad(const float* sums, float* dgamma, float* dbeta, i
                      dbeta, C);
 }
 
-// self-cleaning accumulator + completion counter for stats_reduce_finalize (stream-ordered use)
-static float* g_fin_acc = nullptr;
-static unsigned* g_fin_counter = nullptr;
-static int g_fin_k = 0;
+// self-cleaning accumulator + completion counter for stats_reduce_finalize (stream-ordered use; one per
+// scratch slot: finalizes on concurrent streams never share them)
+static float* g_fin_acc[DTM_WS_SLOTS] = {};
+static unsigned* g_fin_counter[DTM_WS_SLOTS] = {};
+static int g_fin_k[DTM_WS_SLOTS] = {};
 
 // ss[4][K] (+ moving averages) from the partial statistics rows ws[rows][2K], one launch.
 int dtm_bn_stats_finalize(const float* ws, int rows, int K, const float* gamma, const float* beta, float* mov_mean,
                           float* mov_var, float* ss, float count, float eps, float decay, int update, int bessel,
                           hipStream_t st) {
-  if (K > g_fin_k) {
+  if (!dtm_device_ok()) return -9;
+  const int k = dtm_ws_slot(st);
+  if (K > g_fin_k[k]) {
     hipDeviceSynchronize();
-    if (g_fin_acc) hipFree(g_fin_acc);
-    if (!g_fin_counter && hipMalloc(&g_fin_counter, 64) != hipSuccess) return -4;
-    if (hipMalloc(&g_fin_acc, (size_t)2 * K * sizeof(float)) != hipSuccess) { g_fin_acc = nullptr; g_fin_k = 0; return -4; }
-    hipMemset(g_fin_acc, 0, (size_t)2 * K * sizeof(float));
-    hipMemset(g_fin_counter, 0, 64);
+    if (g_fin_acc[k]) hipFree(g_fin_acc[k]);
+    if (!g_fin_counter[k] && hipMalloc(&g_fin_counter[k], 64) != hipSuccess) return -4;
+    if (hipMalloc(&g_fin_acc[k], (size_t)2 * K * sizeof(float)) != hipSuccess) {
+      g_fin_acc[k] = nullptr;
+      g_fin_k[k] = 0;
+      return -4;
+    }
+    hipMemset(g_fin_acc[k], 0, (size_t)2 * K * sizeof(float));
+    hipMemset(g_fin_counter[k], 0, 64);
     hipDeviceSynchronize();
-    g_fin_k = K;
+    g_fin_k[k] = K;
   }
   if (K % 2) return -1;  // float4 columns over [2K]
   int rpb, ychunks;
   dtm_reduce_split(rows, (2 * K + 63) / 64, &rpb, &ychunks);
   hipLaunchKernelGGL(stats_reduce_finalize_kernel, dim3((2 * K + 63) / 64, ychunks), dim3(256), 0, st, ws, rows, K, rpb,
-                     g_fin_acc, g_fin_counter, gamma, beta, mov_mean, mov_var, ss, count, eps, decay, update, bessel);
+                     g_fin_acc[k], g_fin_counter[k], gamma, beta, mov_mean, mov_var, ss, count, eps, decay, update,
+                     bessel);
   return 0;
 }

@@ -56,9 +56,11 @@ __host__ static inline FastDiv make_fastdiv(uint32_t d) {
 }
 
 // workspace arena + two-stage reduction (workspace.hip)
-float* dtm_ws_get(size_t floats);
 void dtm_reduce_rows(const float* ws, int rows, int width, int ld, float* out, hipStream_t st);
-float* dtm_ws_get_stream(size_t floats, hipStream_t st);  // the side stream's own arena
+constexpr int DTM_WS_SLOTS = 5;
+float* dtm_ws_get_stream(size_t floats, hipStream_t st);  // scratch arena of the stream's slot
+int dtm_ws_slot(hipStream_t st);  // 0 = main, 1.. = registered side streams
+bool dtm_device_ok();  // false when called from another device than the first one used
 void dtm_reduce_split(int rows, int xblocks, int* rpb, int* ychunks);
 int dtm_reduce_direct_max();
 int dtm_ntld_bits();  // non-temporal input-load policy of the BN-apply kernels (fused_bn.hip)  // grids up to this many blocks reduce with atomics in the producer

@@ -332,7 +332,7 @@ DTM_API int dtm_conv1x1_bnbwd(const void* g, const void* y, const float* dss, co
   a.x_unscaled = x_unscaled; a.dx = (bf16_t*)dx; a.M = (int)M; a.add_src = (const bf16_t*)add_src;
   a.ntiles = (int)((M + 63) / 64);
   const int blocks = bwd1x1_blocks(a.ntiles);
-  float* ws = dtm_ws_get((size_t)blocks * (K * C + 2 * C));
+  float* ws = dtm_ws_get_stream((size_t)blocks * (K * C + 2 * C), (hipStream_t)stream);
   if (!ws) return -4;
   a.slab = ws;
   a.sums = ws + (size_t)blocks * K * C;

@@ -2044,6 +2044,7 @@ DTM_API int dtm_get_deterministic();
 static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, const float* bias, const float* in_scale,
                          const float* in_shift, int relu, const ConvDesc* d, hipStream_t stream, float** rows_ws,
                          int* nrows) {
+  if (!dtm_device_ok()) return -9;
   if (d->C % 8 || d->K % 4) return -1;
   ConvNTArgs a;
   a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.y = (bf16_t*)y;
@@ -2070,7 +2071,7 @@ static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, cons
     // one per streaming worker; one per pixel tile (staged epilogue, K % 8 == 0); else per (pixel tile, pixel wave)
     rows = (tc.id == 30 || tc.id == 31 || tc.id == 33) ? stream_rows(a, tc.id)
                                          : ((a.M + tc.PT - 1) / tc.PT) * ((a.K & 7) == 0 ? 1 : tc.NWP);
-    float* ws = dtm_ws_get((size_t)rows * 2 * d->K);
+    float* ws = dtm_ws_get_stream((size_t)rows * 2 * d->K, stream);
     if (!ws) return -4;
     a.stats = ws;
   }
@@ -2140,6 +2141,7 @@ DTM_API int dtm_conv_dgrad_ex(const void* dy, const void* wt, void* dx, const Co
 static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvDesc* d, const void* add_src,
                            int add_stride, const void* act_x, const float* act_ss, float* act_sums, int act_unscaled,
                            const void* act_mask, const void* act_r, void* stream) {
+  if (!dtm_device_ok()) return -9;
   if (d->K % 8 || d->C % 4) return -1;
   if (add_stride < 1 || (add_stride > 1 && !add_src)) return -6;
   if ((add_src || act_x) && d->C % 8) return -5;
@@ -2201,7 +2203,7 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvD
     }
   float* ws = nullptr;
   if (act_x) {
-    ws = dtm_ws_get((size_t)rows * rw * d->C);
+    ws = dtm_ws_get_stream((size_t)rows * rw * d->C, (hipStream_t)stream);
     if (!ws) return -4;
   }
   for (int i = 0, r = 0; i < nl; r += lrows[i], ++i) {
@@ -2266,6 +2268,7 @@ DTM_API int dtm_conv_wgrad_bnbwd(const void* x, const void* g, const void* y, co
 
 static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float* in_scale, const float* in_shift,
                            const ConvDesc* d, int num_cus, const WgradBN* bn, void* stream) {
+  if (!dtm_device_ok()) return -9;
   if (d->C % 8 || d->K % 8) return -1;
   ConvWgradArgs a;
   a.x = (const bf16_t*)x; a.dy = (const bf16_t*)dy; a.dw = dw;

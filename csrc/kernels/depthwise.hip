@@ -239,7 +239,7 @@ DTM_API int dtm_depthwise_wgrad(const void* x, const void* dy, float* dw, const 
     if (blocks > 1024) blocks = 1024;
     int ppb = (int)((M + blocks - 1) / blocks);
     int width = a->R * a->S * a->C;
-    float* ws = dtm_ws_get((size_t)blocks * width);
+    float* ws = dtm_ws_get_stream((size_t)blocks * width, st);
     if (!ws) return -4;
     hipLaunchKernelGGL(dw_wgrad8, dim3(blocks), dim3(256), 256 * 8 * sizeof(float), st, (const bf16_t*)x,
                        (const bf16_t*)dy, ws, *a, ppb);

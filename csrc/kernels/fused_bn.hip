@@ -428,7 +428,7 @@ DTM_API int dtm_bn_apply_bwd(const void* dy, const void* y, const void* ymask, c
                        (bf16_t*)dx, (bf16_t*)dres, sx, sr, (int)M, C, mode, res_mode, unscaled, rpb, C, 1);
     return 0;
   }
-  float* ws = dtm_ws_get((size_t)blocks * 4 * C);
+  float* ws = dtm_ws_get_stream((size_t)blocks * 4 * C, (hipStream_t)stream);
   if (!ws) return -4;
   hipLaunchKernelGGL((g_ntld & 2) ? bn_apply_bwd_kernel<true> : bn_apply_bwd_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
                      (const bf16_t*)y, (const uint8_t*)ymask, (const bf16_t*)x, ss, (const bf16_t*)r, rss, (bf16_t*)dx,
@@ -446,7 +446,7 @@ DTM_API int dtm_bn_apply_bwd_ld(const void* dy, const void* ymask, const void* x
   int blocks, rpb;
   grid2(M, C, &blocks, &rpb);
   const int direct = blocks <= dtm_reduce_direct_max();
-  float* ws = direct ? sx : dtm_ws_get((size_t)blocks * 4 * C);
+  float* ws = direct ? sx : dtm_ws_get_stream((size_t)blocks * 4 * C, (hipStream_t)stream);
   if (!ws) return -4;
   hipLaunchKernelGGL((g_ntld & 2) ? bn_apply_bwd_kernel<true> : bn_apply_bwd_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
                      (const bf16_t*)nullptr, (const uint8_t*)ymask, (const bf16_t*)x, ss, (const bf16_t*)nullptr,
@@ -488,7 +488,7 @@ DTM_API int dtm_cat_bn_apply_bwd(const void* descs, int np, const void* dout, fl
     if (!(a.p[i].flags & 2) && (!a.p[i].mask || !a.p[i].dx)) return -1;
   int blocks;
   grid2(M, Ct, &blocks, &a.rpb);
-  float* ws = dtm_ws_get((size_t)blocks * 4 * Ct);
+  float* ws = dtm_ws_get_stream((size_t)blocks * 4 * Ct, (hipStream_t)stream);
   if (!ws) return -4;
   hipLaunchKernelGGL(cat_bn_apply_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a,
                      (const bf16_t*)dout, ws);

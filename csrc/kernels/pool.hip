@@ -394,7 +394,7 @@ DTM_API int dtm_maxpool_bnrelu_bwd(const void* dy, const void* arg, const void* 
   long rpb = (M + b - 1) / b;
   rpb = (rpb + RP - 1) / RP * RP;
   const int blocks = (int)((M + rpb - 1) / rpb);
-  float* ws = dtm_ws_get((size_t)blocks * 2 * a->C);
+  float* ws = dtm_ws_get_stream((size_t)blocks * 2 * a->C, (hipStream_t)stream);
   if (!ws) return -4;
   const int wm = max((a->KH + a->SH - 1) / a->SH, (a->KW + a->SW - 1) / a->SW);
   if (wm <= 2)

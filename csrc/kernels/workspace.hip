@@ -7,24 +7,52 @@
 // The arena grows on first use (warm-up step, before any hipGraph capture) and is reused.
 #include "common.h"
 
-static float* g_ws = nullptr;
-static size_t g_ws_floats = 0;
+// One arena per stream class: slot 0 serves every stream not registered as a side stream, slots
+// 1..DTM_WS_SLOTS-1 the registered side streams (ops/_lib.py side_stream), so kernels enqueued
+// concurrently on different streams never share scratch.
+static hipStream_t g_slot_stream[DTM_WS_SLOTS] = {};
+static float* g_ws[DTM_WS_SLOTS] = {};
+static size_t g_ws_floats[DTM_WS_SLOTS] = {};
 
-float* dtm_ws_get(size_t floats) {
-  if (floats > g_ws_floats) {
+DTM_API void dtm_ws_set_side_stream(int slot, void* s) {
+  if (slot >= 1 && slot < DTM_WS_SLOTS) g_slot_stream[slot] = (hipStream_t)s;
+}
+int dtm_ws_slot(hipStream_t st) {
+  if (st != nullptr)
+    for (int i = 1; i < DTM_WS_SLOTS; ++i)
+      if (g_slot_stream[i] == st) return i;
+  return 0;
+}
+
+// The library's device state (scratch arenas, finalize accumulators, zero / dump chunks, occupancy caches)
+// belongs to the first device the process uses (one process per GPU).  Entry points that touch it check
+// the caller's current device and fail with -9 instead of handing a kernel memory of another device.
+bool dtm_device_ok() {
+  static int dev0 = -1;
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) return false;
+  if (dev0 < 0) dev0 = d;
+  return d == dev0;
+}
+DTM_API int dtm_device_check() { return dtm_device_ok() ? 0 : -9; }
+
+float* dtm_ws_get_stream(size_t floats, hipStream_t st) {
+  if (!dtm_device_ok()) return nullptr;
+  const int k = dtm_ws_slot(st);
+  if (floats > g_ws_floats[k]) {
     size_t n = floats < (16u << 20) ? (16u << 20) : floats;  // >= 64 MB
-    if (g_ws) {
+    if (g_ws[k]) {
       hipDeviceSynchronize();
-      hipFree(g_ws);
+      hipFree(g_ws[k]);
     }
-    if (hipMalloc(&g_ws, n * sizeof(float)) != hipSuccess) {
-      g_ws = nullptr;
-      g_ws_floats = 0;
+    if (hipMalloc(&g_ws[k], n * sizeof(float)) != hipSuccess) {
+      g_ws[k] = nullptr;
+      g_ws_floats[k] = 0;
       return nullptr;
     }
-    g_ws_floats = n;
+    g_ws_floats[k] = n;
   }
-  return g_ws;
+  return g_ws[k];
 }
 
 // out[j] (+)= sum_r ws[r*ld + j], j < width.  16 column-quads x 16 row-lanes per block, float4 loads,
@@ -161,29 +189,4 @@ void dtm_reduce_rows(const float* ws, int rows, int width, int ld, float* out, h
                      chunks);
 }
 
-DTM_API int dtm_ws_reserve(long floats) { return dtm_ws_get((size_t)floats) ? 0 : -1; }
-
-// A second arena for work enqueued on the weight-gradient side stream (ops/_lib.py side_stream): the
-// split-K slabs of a wgrad there must not share scratch with the dgrad / statistics kernels running
-// concurrently on the main stream.
-static hipStream_t g_side_stream = nullptr;
-static float* g_ws_side = nullptr;
-static size_t g_ws_side_floats = 0;
-DTM_API void dtm_ws_set_side_stream(void* s) { g_side_stream = (hipStream_t)s; }
-float* dtm_ws_get_stream(size_t floats, hipStream_t st) {
-  if (st == nullptr || st != g_side_stream) return dtm_ws_get(floats);
-  if (floats > g_ws_side_floats) {
-    size_t n = floats < (16u << 20) ? (16u << 20) : floats;
-    if (g_ws_side) {
-      hipDeviceSynchronize();
-      hipFree(g_ws_side);
-    }
-    if (hipMalloc(&g_ws_side, n * sizeof(float)) != hipSuccess) {
-      g_ws_side = nullptr;
-      g_ws_side_floats = 0;
-      return nullptr;
-    }
-    g_ws_side_floats = n;
-  }
-  return g_ws_side;
-}
+DTM_API int dtm_ws_reserve(long floats) { return dtm_ws_get_stream((size_t)floats, nullptr) ? 0 : -1; }

@@ -135,6 +135,20 @@ class TrainStep:
     def __call__(self, images, labels):
         if self.use_graph and images.is_cuda:
             return self._graph_step(images, labels)
+        ps = _lib.priority_stream() if images.is_cuda else None
+        if ps is not None:
+            # the step's critical path on a high-priority stream: the side-stream weight gradients only
+            # take the CUs it leaves idle (ops/_lib.py priority_stream)
+            caller = torch.cuda.current_stream()
+            ps.wait_stream(caller)
+            with torch.cuda.stream(ps):
+                loss = self._eager_step(images, labels)
+            caller.wait_stream(ps)
+            loss.record_stream(caller)
+            return loss
+        return self._eager_step(images, labels)
+
+    def _eager_step(self, images, labels):
         rng = range_push("train_step")
         loss, skip = self._forward_backward(images, labels)
         with roctx("optimizer"):

@@ -77,6 +77,9 @@ def _accum_param_grad(p, g):
 
 
 def _check(rc, what):
+    if rc == -9:
+        raise RuntimeError("%s: the kernel library's device state belongs to another device (one process per "
+                           "GPU; csrc/kernels/workspace.hip dtm_device_ok)" % what)
     if rc != 0:
         raise RuntimeError("%s failed with code %d" % (what, rc))
 

@@ -419,3 +419,14 @@ def test_stem_pack_kernel(dtype, shape):
     ref_p = torch.nn.functional.pad(x.to(torch.bfloat16), (0, 4 - C, pad, Wp - W - pad, pad, Hp - H - pad))
     torch.cuda.synchronize()
     assert torch.equal(xp, ref_p)
+
+
+def test_device_state_bound_to_first_device():
+    """The kernel library's device state (scratch arenas, finalize accumulators, zero chunk) belongs to the
+    first device the process uses; from that device the check passes (another device gets -9, which
+    nn._check turns into a clear error - not testable on a one-GPU box)."""
+    from distributed_tensorflow_models_amd.ops import _lib
+    L = _lib.lib()
+    x = torch.zeros(8, device="cuda")  # (initialises the device)
+    assert L.dtm_device_check() == 0
+    assert x.sum().item() == 0

@@ -88,6 +88,13 @@ def main():
                                             _lib.ptr(sh), 0, ctypes.byref(d), st),
             "dgrad": lambda: L.dtm_conv_dgrad(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), st),
         }
+        if stride > 1 and R >= stride and S >= stride:
+            # the stride-decomposed dgrad (ConvDesc.dec: one stride-1 conv per output parity class) as training runs it
+            wtd = torch.empty(C, R, S, K, device="cuda", dtype=torch.bfloat16)
+            L.dtm_weight_flip_transpose_dec(_lib.ptr(w), _lib.ptr(wtd), K, R, S, C, stride, g.pad_h, g.pad_w, st)
+            dd = g.as_desc(_lib.ConvDesc)
+            dd.dec = 1
+            passes["dgdec"] = lambda: L.dtm_conv_dgrad(_lib.ptr(dy), _lib.ptr(wtd), _lib.ptr(dx), ctypes.byref(dd), st)
         if os.environ.get("STATS"):
             stats = torch.zeros(2, K, device="cuda")
             passes["fwd+ps"] = lambda: L.dtm_conv_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(y), _lib.ptr(stats), None,

@@ -16,17 +16,22 @@ def main():
         sys.exit("need >= 2 steps in the trace")
     a, b = opt[-2] + 1, opt[-1] + 1
     tot = 0.0
+    per_stream = {}
     prev_end = int(rows[a - 1]["End_Timestamp"])
     for r in rows[a:b]:
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
         name = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("void ", "").replace("dtm::", "")
         d = (e - s) / 1e3
         tot += d
+        sid = r.get("Stream_Id", "0")
+        per_stream[sid] = per_stream.get(sid, 0.0) + d
         grid = "%sx%s" % (int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]), r["Grid_Size_Y"])
-        print("%8.1f us  gap %6.1f  %-9s %s" % (d, (s - prev_end) / 1e3, grid, name[:90]))
-        prev_end = e
+        # gap: idle time since the latest end of any earlier dispatch (negative = overlapped)
+        print("%8.1f us  gap %6.1f  s%-3s %-9s %s" % (d, (s - prev_end) / 1e3, sid, grid, name[:90]))
+        prev_end = max(prev_end, e)
     span = (int(rows[b - 1]["End_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1e3
-    print("kernels %d, busy %.1f us, span %.1f us" % (b - a, tot, span))
+    print("kernels %d, busy %.1f us, span %.1f us; per stream: %s" % (
+        b - a, tot, span, ", ".join("s%s %.1f us" % kv for kv in sorted(per_stream.items()))))
 
 
 if __name__ == "__main__":
