@@ -69,10 +69,24 @@ struct ConvNTArgs {
   // grid is pixel (n, i*ostr + oa, j*ostr + ob) of the OH x OW tensor that y and every epilogue side
   // input (add_src, act_x, act_r, act_mask) index.  ostr == 1: identity (OH = P, OW = Q, oa = ob = 0)
   int ostr, oa, ob, OH, OW;
+  // spatial output tiles (conv3x3_direct_kernel): sp_tw > 0 -> pixel m of this launch is local pixel m % 128
+  // (row-major 8 x 16) of spatial tile m / 128, tiles ordered [N][tiles_h][sp_tw]; pixels past P / Q are
+  // out of range (M = tiles * 128)
+  int sp_tw, sp_th;
+  FastDiv fd_sp_img, fd_sp_tw;
 };
 
 // full-resolution coordinates / row of output pixel m (see ConvNTArgs::ostr)
 __device__ __forceinline__ void out_nhw(const ConvNTArgs& a, int m, int& n, int& h, int& w) {
+  if (a.sp_tw) {
+    const uint32_t t = (uint32_t)m >> 7, l = (uint32_t)m & 127u;
+    const uint32_t nn = fdiv(t, a.fd_sp_img), rem = t - nn * (a.sp_th * a.sp_tw);
+    const uint32_t th = fdiv(rem, a.fd_sp_tw), tw = rem - th * a.sp_tw;
+    n = (int)nn;
+    h = (int)(th * 8u + (l >> 4));
+    w = (int)(tw * 16u + (l & 15u));
+    return;
+  }
   const uint32_t nn = fdiv((uint32_t)m, a.fd_PQ), rem = m - nn * (a.P * a.Q);
   const uint32_t i = fdiv(rem, a.fd_Q), j = rem - i * a.Q;
   n = (int)nn;
@@ -80,10 +94,18 @@ __device__ __forceinline__ void out_nhw(const ConvNTArgs& a, int m, int& n, int&
   w = (int)j * a.ostr + a.ob;
 }
 __device__ __forceinline__ int out_row(const ConvNTArgs& a, int m) {
-  if (a.ostr == 1) return m;
+  if (a.ostr == 1 && !a.sp_tw) return m;
   int n, h, w;
   out_nhw(a, m, n, h, w);
   return (n * a.OH + h) * a.OW + w;
+}
+
+// spatial-tile launches: pixel m lies inside the P x Q output (always true otherwise)
+__device__ __forceinline__ bool out_valid(const ConvNTArgs& a, int m) {
+  if (!a.sp_tw) return true;
+  int n, h, w;
+  out_nhw(a, m, n, h, w);
+  return h < a.P && w < a.Q;
 }
 
 // Shared epilogue of the conv_nt kernels (register-staged and LDS-DMA): acc[TC][TP] of wave (wp, wc)
@@ -162,7 +184,7 @@ __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem
       for (int j = 0; j < GRP; ++j) {
         const int row = ((g0 + j) * NT + tid) / CPR;
         const int m = p0 + row;
-        if (m < a.M && kc < a.K) {
+        if (m < a.M && kc < a.K && out_valid(a, m)) {
           const size_t o = (size_t)out_row(a, m) * a.K + kc;
           if (a.add_src) {
             const bf16_t* src = a.add_src + o;
@@ -194,7 +216,7 @@ __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem
       const int idx = (g0 + j) * NT + tid;
       const int row = idx / CPR;
       const int m = p0 + row;
-      const bool inb = m < a.M && kc < a.K;
+      const bool inb = m < a.M && kc < a.K && out_valid(a, m);
       if (EXACT || inb) {
         uint4 v = *(const uint4*)(smem + row * OROW + chn * 16);
         const size_t o = (size_t)(inb ? out_row(a, m) : m) * a.K + kc;
@@ -335,10 +357,10 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
       uint32_t lo = pack2bf(v[0], v[1]), hi = pack2bf(v[2], v[3]);
       if constexpr (staged) {
         *(uint2*)(smem + mloc * OROW + kloc * 2) = make_uint2(lo, hi);
-      } else if (m < a.M && kch < a.K) {
+      } else if (m < a.M && kch < a.K && out_valid(a, m)) {
         *(uint2*)(a.y + (size_t)out_row(a, m) * a.K + kch) = make_uint2(lo, hi);
       }
-      if (!SACC && !staged && a.stats && m < a.M && kch < a.K) {
+      if (!SACC && !staged && a.stats && m < a.M && kch < a.K && out_valid(a, m)) {
         float q0 = lo_bf(lo), q1 = hi_bf(lo), q2 = lo_bf(hi), q3 = hi_bf(hi);
         bsum[0] += q0; bsq[0] += q0 * q0;
         bsum[1] += q1; bsq[1] += q1 * q1;
@@ -1226,6 +1248,164 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int n
 }
 
 // ------------------------------------------------------------------------------------------
+// Direct 3x3 stride-1 conv for narrow layers (C in {32, 64} input channels, CT = 32 / 64 output channels per
+// block): the ResNet-50 stage-1 3x3 (64 -> 64) and the Inception-v3 stem 3x3s (32 -> 32 / 64) forward and
+// dgrad.  As an implicit GEMM these re-read every input pixel from L2 once per tap (9x) with a 64-deep
+// reduction per k-step; here a persistent block keeps the 9 x CT x C weights resident in LDS and streams
+// spatial output tiles of 8 x 16 pixels: the tile's (8+2) x (16+2) input halo arrives by LDS-DMA (3-slot ring,
+// two tiles in flight) and all nine taps read their MFMA fragments from it.  16-B chunk swizzle: chunk c of
+// pixel / weight row p sits at slot c ^ ((p >> 1) & 7) (C = 64) or c ^ ((p >> 2) & 3) (C = 32), so the 16
+// consecutive pixels / rows of a fragment read cover all 64 banks.  The finished tile is staged in its own
+// (now free) halo slot for the shared epilogue (spatial output mapping: ConvNTArgs::sp_tw).
+template <int CIN>
+__device__ __forceinline__ int dsw(int p, int c) {
+  return CIN == 64 ? (c ^ ((p >> 1) & 7)) : (c ^ ((p >> 2) & 3));
+}
+
+template <int CIN, int CT, bool SIDE>
+__global__ __launch_bounds__(256) void conv3x3_direct_kernel(ConvNTArgs a, int ntiles) {
+  constexpr int TH = 8, TW = 16, PT = TH * TW, HH = TH + 2, HW = TW + 2;
+  constexpr int CPP = CIN / 8;                    // 16-B chunks per pixel
+  constexpr int HCH = HH * HW * CPP;              // halo chunks
+  constexpr int NDMA = (HCH + 255) / 256;         // halo DMA instructions per thread per tile
+  constexpr int OROW = CT * 2 + 16;
+  constexpr int HDMA = NDMA * 256 * 16;
+  // a slot also holds the staged output tile and the epilogue's [256][16] fp32 post-op reduction table
+  constexpr int HBUF = HDMA > PT * OROW ? (HDMA > 16384 ? HDMA : 16384) : (PT * OROW > 16384 ? PT * OROW : 16384);
+  constexpr int WBUF = 9 * CT * CIN * 2;
+  constexpr int NIT = PT * (CT / 8) / 256;        // exact staged stores per thread per tile
+  constexpr int TC = CT / 16, TP = 2;
+
+  static_assert(2 * NIT + NDMA <= 63, "vmcnt range");
+  __shared__ __attribute__((aligned(16))) char smem[WBUF + 3 * HBUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nb = gridDim.x * gridDim.y;
+  const int bid = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, nb);
+  const int bx = bid % gridDim.x, by0 = bid / gridDim.x;
+  const int c0 = bx * CT;
+  const char* xg = (const char*)a.x;
+  const char* zg = (const char*)a.zero;
+  const int tiles_w = a.sp_tw, tiles_img = a.sp_th * a.sp_tw;
+
+  // resident weights: row (tap, channel) = tap * CT + ch, CIN-deep, swizzled 16-B chunks (plain loads)
+  for (int q = tid; q < 9 * CT * CPP; q += 256) {
+    const int row = q / CPP, c = q % CPP;
+    const int tap = row / CT, ch = row % CT, k = c0 + ch;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (k < a.K) v = *(const uint4*)(a.w + ((size_t)k * 9 + tap) * CIN + c * 8);
+    *(uint4*)(smem + (row * CPP + dsw<CIN>(row, c)) * 16) = v;
+  }
+  // this thread's halo DMA slots (tile-independent part): slot q -> pixel hp, chunk c
+  int hoff[NDMA], hrow[NDMA], hcol[NDMA];
+#pragma unroll
+  for (int j = 0; j < NDMA; ++j) {
+    const int q = (j * 4 + wave) * 64 + lane;
+    const int hp = q / CPP, sc = q % CPP;
+    const int c = dsw<CIN>(hp, sc);
+    const int hh = hp / HW, ww = hp % HW;
+    hrow[j] = q < HCH ? hh : -100000;  // (slots past the halo load zeros)
+    hcol[j] = ww;
+    hoff[j] = (hh * a.Win + ww) * (CIN * 2) + c * 16;
+  }
+  const char* srcs[NDMA];
+  auto issue = [&](int t, int buf) {
+    const uint32_t n = (uint32_t)t / (uint32_t)tiles_img, rem = (uint32_t)t - n * tiles_img;
+    const int th = (int)(rem / (uint32_t)tiles_w), tw = (int)(rem - th * tiles_w);
+    const int h0 = th * TH - a.pad_h, w0 = tw * TW - a.pad_w;
+    const int base = (((int)n * a.Hin + h0) * a.Win + w0) * (CIN * 2);
+    char* dst = smem + WBUF + buf * HBUF;
+#pragma unroll
+    for (int j = 0; j < NDMA; ++j) {
+      const int h = h0 + hrow[j], w = w0 + hcol[j];
+      const bool v = ((unsigned)h < (unsigned)a.Hin) & ((unsigned)w < (unsigned)a.Win);
+      srcs[j] = v ? xg + (size_t)(uint32_t)(base + hoff[j]) : zg;
+      glds16(srcs[j], dst + (j * 4 + wave) * 1024);
+    }
+  };
+
+  const int fr = lane & 15, fk = lane >> 4;
+  float ssum[8], ssq[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { ssum[e] = 0.f; ssq[e] = 0.f; }
+  const int gy = gridDim.y;
+  int t = by0;
+  if (t < ntiles) issue(t, 0);
+  if (t + gy < ntiles) issue(t + gy, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // weights resident, tiles 0 and 1 landed
+  int buf = 0;
+  for (int it = 0; t < ntiles; ++it, t += gy) {
+    if (it >= 2) {
+      // issued after this wave's DMA of tile t: stores(it-2), the DMA of tile t+gy (if any), stores(it-1)
+      if (t + gy < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NIT + NDMA) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NIT) : "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // tile t visible; the slot of tile t-1 (its staging area) is free
+    if (t + 2 * gy < ntiles) issue(t + 2 * gy, buf == 0 ? 2 : buf - 1);
+    f32x4 acc[TC][TP];
+#pragma unroll
+    for (int i = 0; i < TC; ++i)
+#pragma unroll
+      for (int j = 0; j < TP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const char* hb = smem + WBUF + buf * HBUF;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int r = tap / 3, s = tap % 3;
+#pragma unroll
+      for (int kc = 0; kc < CIN / 32; ++kc) {
+        const int c = kc * 4 + fk;
+        short8 bf[TP], af[TC];
+#pragma unroll
+        for (int j = 0; j < TP; ++j) {
+          const int hp = (2 * wave + j + r) * HW + fr + s;
+          bf[j] = *(const short8*)(hb + (hp * CPP + dsw<CIN>(hp, c)) * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < TC; ++i) {
+          const int row = tap * CT + i * 16 + fr;
+          af[i] = *(const short8*)(smem + (row * CPP + dsw<CIN>(row, c)) * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < TC; ++i)
+#pragma unroll
+          for (int j = 0; j < TP; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave is done reading the halo slot: it becomes the staging area
+    conv_nt_epilogue<PT, CT, 32, CT, 1, true, true, true, true, 256, SIDE>(a, acc, (char*)hb, t * PT, c0, t, ssum, ssq);
+#pragma unroll
+    for (int i = 0; i < NDMA; ++i) asm volatile("" ::"v"(srcs[i]));
+    buf = buf == 2 ? 0 : buf + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (a.stats) {
+    // one partial row per worker: [sum(K) | sumsq(K)] of this block's CT channels
+    constexpr int CPR = CT / 8, RPT = 256 / CPR;
+    __syncthreads();
+    float* red = (float*)(smem + WBUF);  // [256][16]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { red[tid * 16 + e] = ssum[e]; red[tid * 16 + 8 + e] = ssq[e]; }
+    __syncthreads();
+    for (int h = RPT / 2; h >= 1; h >>= 1) {
+      if (tid < h * CPR) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) red[tid * 16 + e] += red[(tid + h * CPR) * 16 + e];
+      }
+      __syncthreads();
+    }
+    const int kc = c0 + tid * 8;
+    if (tid < CPR && kc < a.K) {
+      float* row = a.stats + (size_t)by0 * (2 * a.K);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { row[kc + e] = red[tid * 16 + e]; row[a.K + kc + e] = red[tid * 16 + 8 + e]; }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // weight gradient
 struct ConvWgradArgs {
   const bf16_t* x;   // [N][H][W][C] forward input
@@ -1238,6 +1418,7 @@ struct ConvWgradArgs {
   int Mpix;  // N*P*Q
   int Kg;    // R*S*C
   int pix_per_split;
+  int atomic;        // 1: the splits add their partial tiles straight into dw with fp32 atomics (no slabs)
   FastDiv fd_PQ, fd_Q;
   int pix_bytes;  // byte pitch of one x pixel (C*2, or less for the packed-row stem view)
   // optional BatchNorm backward of dy (register-staged kernels only): dy is the unscaled gradient g of
@@ -1489,7 +1670,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
       if (col < a.Kg) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (ko + r < a.K) slab[(size_t)(ko + r) * a.Kg + col] = acc[i][j][r];
+          if (ko + r < a.K) {
+            if (a.atomic) unsafeAtomicAdd(a.dw + (size_t)(ko + r) * a.Kg + col, acc[i][j][r]);
+            else slab[(size_t)(ko + r) * a.Kg + col] = acc[i][j][r];
+          }
       }
     }
   }
@@ -1654,7 +1838,10 @@ __global__ __launch_bounds__(NTH) void conv_wgrad_pipe_kernel(ConvWgradArgs a) {
       if (col < a.Kg) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (ko + r < a.K) slab[(size_t)(ko + r) * a.Kg + col] = acc[i][j][r];
+          if (ko + r < a.K) {
+            if (a.atomic) unsafeAtomicAdd(a.dw + (size_t)(ko + r) * a.Kg + col, acc[i][j][r]);
+            else slab[(size_t)(ko + r) * a.Kg + col] = acc[i][j][r];
+          }
       }
     }
   }
@@ -1888,6 +2075,53 @@ static void launch_nt(const ConvNTArgs& a, hipStream_t st) {
 // 64 x 128 register-staged with a single LDS buffer (more resident blocks), 21 / 24 / 26 / 32 = LDS-DMA
 // pipelined 128x128 / 256x64 / 128x64 / 256x32, 30 / 31 = the persistent streaming 1x1 kernel (128 / 64
 // channels), 40 = the 8-wave 256x256 tile.  DTM_CONV_TILE forces one (sweeps: tools/conv_tile_sweep.py).
+// the direct 3x3 kernel (tile id 60): -1: DTM_DIRECT3X3 env (default 1), 0 / 1: A/B knob
+static int g_direct3 = -1;
+DTM_API void dtm_conv_set_direct3(int on) { g_direct3 = on; }
+// Measured (tools/conv_tile_sweep.py, profiles/r3/r3_sweep_direct3x3.log): 32 output channels win 1.8-2.2x
+// (Inception stem 3x3 32->32 fwd 108 vs 185 us, dgrads 64->32 / 32->32 185 / 100 vs 274 / 182 us); 64 output
+// channels lose ~10 % (ResNet-50 56x56 64->64: 114 vs 103 us): their 1-block/CU tile is LDS-bandwidth bound
+// (6 fragment reads per 8 MFMAs).  The policy takes K == 32; tile id 60 forces it for any K % 32 == 0.
+static bool direct_ok(const ConvNTArgs& a) {
+  return a.R == 3 && a.S == 3 && a.stride == 1 && a.Hv == a.Hin && a.Wv == a.Win && (a.C == 32 || a.C == 64) &&
+         a.K % 32 == 0 && !a.in_scale && !a.bias && !a.relu && a.pix_bytes == a.C * 2 && a.ostr == 1 &&
+         a.pad_h <= 2 && a.pad_w <= 2;
+}
+// spatial 8 x 16 output tiles, M = tiles * 128 (ConvNTArgs::sp_tw)
+static void direct_setup(ConvNTArgs& a) {
+  a.sp_tw = (a.Q + 15) / 16;
+  a.sp_th = (a.P + 7) / 8;
+  a.fd_sp_img = make_fastdiv(a.sp_th * a.sp_tw);
+  a.fd_sp_tw = make_fastdiv(a.sp_tw);
+  a.M = a.N * a.sp_th * a.sp_tw * 128;
+}
+template <int CIN, int CT, bool SIDE>
+static int direct_workers_k(const ConvNTArgs& a) {
+  static int occ = 0;
+  if (!occ) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv3x3_direct_kernel<CIN, CT, SIDE>, 256, 0) != hipSuccess ||
+        occ <= 0)
+      occ = 1;
+  }
+  const int ctiles = a.K / CT, ntiles = a.M / 128;
+  int w = occ * device_cus() / ctiles;
+  if (w < 1) w = 1;
+  return w < ntiles ? w : ntiles;
+}
+template <int CIN, int CT, bool SIDE>
+static void launch_direct_k(const ConvNTArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL((conv3x3_direct_kernel<CIN, CT, SIDE>), dim3(a.K / CT, direct_workers_k<CIN, CT, SIDE>(a)),
+                     dim3(256), 0, st, a, a.M / 128);
+}
+#define DTM_DIRECT_SEL(FN, ...)                                                                     \
+  ((a.add_src || a.act_x)                                                                          \
+       ? (a.C == 64 ? (a.K % 64 == 0 ? FN<64, 64, true>(__VA_ARGS__) : FN<64, 32, true>(__VA_ARGS__)) \
+                    : (a.K % 64 == 0 ? FN<32, 64, true>(__VA_ARGS__) : FN<32, 32, true>(__VA_ARGS__))) \
+       : (a.C == 64 ? (a.K % 64 == 0 ? FN<64, 64, false>(__VA_ARGS__) : FN<64, 32, false>(__VA_ARGS__)) \
+                    : (a.K % 64 == 0 ? FN<32, 64, false>(__VA_ARGS__) : FN<32, 32, false>(__VA_ARGS__))))
+static int direct_workers(const ConvNTArgs& a) { return DTM_DIRECT_SEL(direct_workers_k, a); }
+static void launch_direct(const ConvNTArgs& a, hipStream_t st) { DTM_DIRECT_SEL(launch_direct_k, a, st); }
+
 struct TileCfg {
   int id, PT, NWP;
 };
@@ -1930,6 +2164,13 @@ static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
   }
   // the packed-row stem as a persistent stream (weights resident, pixel tiles prefetched)
   if (id == -1 && g_stem_stream && stem_stream_ok(a)) return {33, 64, 2};
+  if (g_direct3 < 0) {
+    const char* e = getenv("DTM_DIRECT3X3");
+    g_direct3 = e ? atoi(e) : 1;
+  }
+  // narrow 3x3 stride-1 layers: the direct kernel (resident weights, halo tiles; the caller sets the
+  // spatial tiling with direct_setup)
+  if (((id == -1 && a.K == 32) || id == 60) && g_direct3 && direct_ok(a)) return {60, 128, 4};
   // the pipelined LDS-DMA 128x128 tile (2 slots, 2 blocks/CU) wins every deep-reduction layer without the
   // prologue (tools/conv_tile_sweep.py: 3x3 at 14x14 / 7x7 -13..-18 %, deep 1x1 -5..-16 %)
   if (id == -4) id = -1;  // (-4: the policy without the streaming kernel, for A/B runs)
@@ -2012,6 +2253,8 @@ static void dispatch_ud(const ConvNTArgs& a, const TileCfg& t, hipStream_t st) {
   else if (t.id == 30 && UD == 1) {
     if (a.Kg <= 64) launch_stream<128, 1>(a, st);
     else launch_stream<128, 2>(a, st);
+  } else if (t.id == 60 && UD == 1) {
+    launch_direct(a, st);
   } else if (t.id == 33 && UD == 1) {
     if (g_stem_stream == 2) launch_stream_k<64, 64, 4, false, true, 2, false>(a, st);  // (A/B: 2-slot ring)
     else launch_stream_k<64, 64, 4, false, true, 3, false>(a, st);
@@ -2065,12 +2308,16 @@ static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, cons
   a.M = d->N * d->P * d->Q; a.Kg = d->R * d->S * d->C; a.relu = relu;
   a.fd_PQ = make_fastdiv(d->P * d->Q); a.fd_Q = make_fastdiv(d->Q);
   a.ostr = 1; a.oa = a.ob = 0; a.OH = a.P; a.OW = a.Q;
+  a.sp_tw = a.sp_th = 0;
   int rows = 0;
   const TileCfg tc = pick_tile(a, stats);
+  if (tc.id == 60) direct_setup(a);
   if (stats) {
-    // one per streaming worker; one per pixel tile (staged epilogue, K % 8 == 0); else per (pixel tile, pixel wave)
-    rows = (tc.id == 30 || tc.id == 31 || tc.id == 33) ? stream_rows(a, tc.id)
-                                         : ((a.M + tc.PT - 1) / tc.PT) * ((a.K & 7) == 0 ? 1 : tc.NWP);
+    // one per streaming / direct worker; one per pixel tile (staged epilogue, K % 8 == 0); else per (pixel
+    // tile, pixel wave)
+    rows = tc.id == 60 ? direct_workers(a)
+           : (tc.id == 30 || tc.id == 31 || tc.id == 33) ? stream_rows(a, tc.id)
+                                                          : ((a.M + tc.PT - 1) / tc.PT) * ((a.K & 7) == 0 ? 1 : tc.NWP);
     float* ws = dtm_ws_get_stream((size_t)rows * 2 * d->K, stream);
     if (!ws) return -4;
     a.stats = ws;
@@ -2156,6 +2403,7 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvD
   a.dump = dump_chunk();
   a.add_H = (d->H - 1) / add_stride + 1; a.add_W = (d->W - 1) / add_stride + 1;
   a.pix_bytes = d->K * 2;
+  a.sp_tw = a.sp_th = 0;
   size_t xb = (size_t)d->N * d->P * d->Q * d->K * 2, wb = (size_t)d->K * d->R * d->S * d->C * 2;
   if (xb >= (1ull << 31) || wb >= (1ull << 31)) return -2;
   a.x_bytes = (uint32_t)xb; a.w_bytes = (uint32_t)wb;
@@ -2197,6 +2445,7 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvD
       b.M = d->N * b.P * b.Q; b.Kg = b.R * b.S * d->K;
       b.fd_PQ = make_fastdiv(b.P * b.Q); b.fd_Q = make_fastdiv(b.Q);
       lt[nl] = pick_tile(b);
+      if (lt[nl].id == 60) direct_setup(b);
       lrows[nl] = (b.M + lt[nl].PT - 1) / lt[nl].PT;  // pixel tiles
       rows += lrows[nl];
       la[nl++] = b;
@@ -2236,6 +2485,15 @@ static void launch_wgrad(const ConvWgradArgs& a, int splits, hipStream_t st) {
 // kernels (A/B sweeps: tools/conv_tile_sweep.py)
 static int g_wgrad_env = -2;
 static int g_wgrad_occ = 4;
+// split-K weight gradients with at most this many splits accumulate with fp32 atomics straight into dW
+// (no slab workspace, no reduce launch); -1: DTM_WGRAD_ATOMIC env (default 0 = always slabs)
+static int g_wgrad_atomic = -1;
+// A/B knob: the 64 x 256 register-staged wgrad tile (id 7) for K <= 64, Kg > 128: 0 never, 1 always (+3.5 %
+// ResNet-50 step), 2 only with the BN backward in the operand staging (the stem: +1.4 %); its 1 block per CU
+// loses to the 64 x 128 tile's occupancy (profiles/ab/r3_ab_wgrad_wide.log)
+static int g_wgrad_wide = 0;
+DTM_API void dtm_conv_set_wgrad_wide(int on) { g_wgrad_wide = on; }
+DTM_API void dtm_conv_set_wgrad_atomic(int max_splits) { g_wgrad_atomic = max_splits; }
 DTM_API void dtm_conv_set_wgrad_tile(int id, int occ) {
   g_wgrad_env = id;
   if (occ > 0) g_wgrad_occ = occ;
@@ -2295,6 +2553,9 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   int wt = wenv >= 0 ? wenv : (d->K <= 64 ? 1 : 0);
   // <= 32 output channels: 32-row tiles (no half-empty 64-row tile; A/B knob dtm_conv_set_k32)
   if (wenv == -1 && wt == 1 && d->K <= 32 && g_k32_tile) wt = 6;
+  // <= 64 output channels over a wide reduction (Kg > 128): the 64 x 256 tile reads the dy / comb operand
+  // once per 256 columns instead of once per 128 (the stem: 224 columns in one tile, half the g / y reads)
+  if (wenv == -1 && wt == 1 && a.Kg > 128 && (g_wgrad_wide == 1 || (g_wgrad_wide == 2 && bn))) wt = 7;
   int occ = g_wgrad_occ;
   // policy (tools/conv_tile_sweep.py WTILES sweep, ResNet-50 shapes): the pipelined kernel at 2 blocks
   // per CU wins every layer with K > 64 (-10..-25 %); 4 blocks' worth of splits for the deep 3x3 7x7s
@@ -2306,9 +2567,9 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
     if (g_tile_w8 && d->K >= 256 && a.Kg >= 1024 && (d->R * d->S > 1 || d->K >= 1024)) wt = 12;
   }
   if (wt >= 10 && (in_scale || bn)) wt = d->K <= 64 ? 1 : 0;  // the pipelined kernels have no operand prologues
-  if (wt != 0 && wt != 1 && wt != 6 && wt != 10 && wt != 12) wt = 0;
+  if (wt != 0 && wt != 1 && wt != 6 && wt != 7 && wt != 10 && wt != 12) wt = 0;
   const bool big = wt == 12;  // 8-wave 256x256 (one block per CU)
-  const int MT = wt == 6 ? 32 : (wt == 1 ? 64 : (big ? 256 : 128)), NT = big ? 256 : 128;
+  const int MT = wt == 6 ? 32 : ((wt == 1 || wt == 7) ? 64 : (big ? 256 : 128)), NT = (big || wt == 7) ? 256 : 128;
   if (big) occ = (wenv == 12 && g_wgrad_occ != 4) ? g_wgrad_occ : 1;  // (sweeps: WTILES=12:<occ>)
   long tiles = (long)((a.Kg + NT - 1) / NT) * ((a.K + MT - 1) / MT);
   long target = (long)num_cus * (wt >= 10 ? occ : 3);
@@ -2321,9 +2582,16 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   long steps_per = (ksteps + splits - 1) / splits;
   a.pix_per_split = (int)(steps_per * 64);
   splits = (a.Mpix + a.pix_per_split - 1) / a.pix_per_split;
-  const size_t slab = (size_t)splits * a.K * a.Kg;
-  float* ws = dtm_ws_get_stream(slab, (hipStream_t)stream);
-  if (!ws) return -4;
+  if (g_wgrad_atomic < 0) {
+    const char* e = getenv("DTM_WGRAD_ATOMIC");
+    g_wgrad_atomic = e ? atoi(e) : 0;
+  }
+  a.atomic = !dtm_get_deterministic() && splits <= g_wgrad_atomic;
+  float* ws = dw;
+  if (!a.atomic) {
+    ws = dtm_ws_get_stream((size_t)splits * a.K * a.Kg, (hipStream_t)stream);
+    if (!ws) return -4;
+  }
   a.dw = ws;
   if (wt >= 10) {
     a.in_shift = (const float*)zero_chunk();  // the zero DMA source
@@ -2333,10 +2601,11 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
     else
       hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 128, 2>), grid, dim3(256), 0, (hipStream_t)stream, a);
   } else if (wt == 1) launch_wgrad<64, 128, 32, 64>(a, (int)splits, (hipStream_t)stream);
+  else if (wt == 7) launch_wgrad<64, 256, 32, 128>(a, (int)splits, (hipStream_t)stream);
   else if (wt == 6) launch_wgrad<32, 128, 16, 64>(a, (int)splits, (hipStream_t)stream);
   else launch_wgrad<128, 128, 64, 64>(a, (int)splits, (hipStream_t)stream);
   // dW += sum over the split slabs (every slab element is written: tiles cover [K][Kg] exactly)
-  dtm_reduce_rows(ws, (int)splits, a.K * a.Kg, a.K * a.Kg, dw, (hipStream_t)stream);
+  if (!a.atomic) dtm_reduce_rows(ws, (int)splits, a.K * a.Kg, a.K * a.Kg, dw, (hipStream_t)stream);
   return 0;
 }
 

@@ -56,6 +56,9 @@ _SIGS = {
     "dtm_conv_set_stem_stream": (None, [_I]),
     "dtm_ws_set_side_stream": (None, [_I, _P]),
     "dtm_device_check": (_I, []),
+    "dtm_conv_set_wgrad_atomic": (None, [_I]),
+    "dtm_conv_set_wgrad_wide": (None, [_I]),
+    "dtm_conv_set_direct3": (None, [_I]),
     "dtm_cat_desc_bytes": (_I, []),
     "dtm_cat_bn_apply": (_I, [_P, _I, _P, _L, _I, _P]),
     "dtm_cat_bn_apply_bwd": (_I, [_P, _I, _P, _P, _L, _I, _P]),

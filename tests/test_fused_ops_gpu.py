@@ -99,6 +99,76 @@ def test_conv_bn_chain_prologue(C, relu):
     assert all(v < 2e-2 for v in errs.values()), msg
 
 
+@pytest.mark.parametrize("direct", [0, 1])
+@pytest.mark.parametrize("H,W,C,K,pad", [(56, 56, 64, 64, "SAME"), (29, 37, 32, 64, "VALID"), (20, 20, 32, 32, "SAME")])
+def test_direct3x3_conv_bn(H, W, C, K, pad, direct):
+    """conv3x3_direct_kernel (resident weights, 8 x 16 halo tiles, per-worker BN statistics) and the implicit-GEMM
+    tiles give the same conv+BN forward (output, moving statistics) and backward (dx through the direct dgrad,
+    dw, dgamma, dbeta) as torch fp32."""
+    from distributed_tensorflow_models_amd.ops import _lib
+    L = _lib.lib()
+    torch.manual_seed(5)
+    x = torch.randn(2, H, W, C, device=DEV).to(torch.bfloat16).float()
+    w = (torch.randn(K, 3, 3, C, device=DEV) / (9 * C) ** 0.5).to(torch.bfloat16).float()
+    bn, bn_r = _bn(K), _bn(K)
+    with torch.no_grad():
+        bn_r.gamma.copy_(bn.gamma)
+        bn_r.beta.copy_(bn.beta)
+    L.dtm_conv_set_direct3(direct)
+    L.dtm_conv_set_tile(60 if direct else -1)  # (the policy takes the direct kernel for K == 32 only)
+    try:
+        xk = x.to(torch.bfloat16).requires_grad_()
+        wk = w.clone().requires_grad_()
+        yk = fused.conv_bn(xk, wk, bn, 1, pad, True, False).materialize()
+        gy = torch.randn(yk.shape, device=DEV).to(torch.bfloat16)
+        yk.backward(gy)
+        torch.cuda.synchronize()
+    finally:
+        L.dtm_conv_set_direct3(1)
+        L.dtm_conv_set_tile(-1)
+    xr, wr = x.clone().requires_grad_(), w.clone().requires_grad_()
+    gr, br = bn_r.gamma.detach().clone().requires_grad_(), bn_r.beta.detach().clone().requires_grad_()
+    yr = ref.batch_norm(ref.conv2d(xr, wr, None, 1, pad), gr, br, bn_r.moving_mean, bn_r.moving_variance, True, 0.9,
+                        1e-3, False)
+    yr.backward(gy.float())
+    errs = dict(y=_rel(yk, yr), mm=_rel(bn.moving_mean, bn_r.moving_mean), mv=_rel(bn.moving_variance,
+                bn_r.moving_variance), dx=_rel(xk.grad, xr.grad), dw=_rel(wk.grad, wr.grad),
+                dg=_rel(bn.gamma.grad, gr.grad), db=_rel(bn.beta.grad, br.grad))
+    assert all(v < 2e-2 for v in errs.values()), errs
+
+
+def test_full_window_conv_dgrad_gemm():
+    """Inception's aux head: 1x1 conv+BN+ReLU folded into a 5x5 VALID conv over its 5x5 map (1x1 output). The
+    second conv's dgrad runs as a plain GEMM with the act backward in torch (fused._full_window_dgrad_act);
+    every gradient matches torch fp32."""
+    torch.manual_seed(3)
+    C, K = 64, 96
+    x = torch.randn(8, 5, 5, C, device=DEV).to(torch.bfloat16).float()
+    w1 = (torch.randn(C, 1, 1, C, device=DEV) / C ** 0.5).to(torch.bfloat16).float()
+    w2 = (torch.randn(K, 5, 5, C, device=DEV) / (25 * C) ** 0.5).to(torch.bfloat16).float()
+    bn1, bn2 = _bn(C), _bn(K)
+    xk = x.to(torch.bfloat16).requires_grad_()
+    w1k, w2k = w1.clone().requires_grad_(), w2.clone().requires_grad_()
+    l1 = fused.conv_bn(xk, w1k, bn1, 1, "SAME", True, True)
+    m1 = ((l1.raw.detach().float() * l1.ss[0] + l1.ss[1]) > 0).float()
+    l2 = fused.conv_bn(l1, w2k, bn2, 1, "VALID", True, False)
+    from distributed_tensorflow_models_amd.ops.geometry import conv_geom
+    assert fused._full_window(conv_geom((8, 5, 5, C), (K, 5, 5, C), 1, "VALID"))
+    yk = l2.materialize()
+    xr, w1r, w2r = (t.clone().requires_grad_() for t in (x, w1, w2))
+    g1, b1 = bn1.gamma.detach().clone().requires_grad_(), bn1.beta.detach().clone().requires_grad_()
+    g2, b2 = bn2.gamma.detach().clone().requires_grad_(), bn2.beta.detach().clone().requires_grad_()
+    a1 = ref.batch_norm(ref.conv2d(xr, w1r), g1, b1, None, None, True, 0.9, 1e-3, False) * m1
+    yr = ref.batch_norm(ref.conv2d(a1, w2r, None, 1, "VALID"), g2, b2, None, None, True, 0.9, 1e-3, False)
+    gy = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(gy)
+    yk.backward(gy.to(torch.bfloat16))
+    torch.cuda.synchronize()
+    errs = dict(y=_rel(yk, yr), dx=_rel(xk.grad, xr.grad), dw1=_rel(w1k.grad, w1r.grad),
+                dw2=_rel(w2k.grad, w2r.grad), dg1=_rel(bn1.gamma.grad, g1.grad), db1=_rel(bn1.beta.grad, b1.grad))
+    assert all(v < 3e-2 for v in errs.values()), errs
+
+
 @pytest.mark.parametrize("proj,C,act", [(False, 64, "relu"), (True, 64, "relu"), (True, 96, None), (False, 320, None),
                                         (True, 96, "relu")])
 def test_bn_apply_residual(proj, C, act):

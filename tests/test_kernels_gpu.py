@@ -33,6 +33,12 @@ CONV_CASES = [
     (2, 35, 35, 288, 384, (3, 3), 2, "VALID"),    # mixed_17x17x768a 3x3/2 VALID
     (2, 17, 17, 192, 320, (3, 3), 2, "VALID"),    # mixed_8x8x1280a
     (2, 9, 9, 64, 64, (4, 4), 2, ((1, 2), (1, 2))),  # even-kernel conv2d_same (resnet_utils.py:77-122)
+    # the direct 3x3 kernel (C in {32, 64}; ragged 8 x 16 spatial tiles): ResNet stage 1, Inception stem
+    (2, 56, 56, 64, 64, (3, 3), 1, "SAME"),
+    (3, 19, 21, 32, 32, (3, 3), 1, "VALID"),
+    (2, 17, 23, 32, 64, (3, 3), 1, "SAME"),
+    (2, 9, 30, 64, 32, (3, 3), 1, "VALID"),
+    (1, 41, 37, 64, 96, (3, 3), 1, "SAME"),
 ]
 
 
