@@ -2490,7 +2490,7 @@ static int g_wgrad_occ = 4;
 static int g_wgrad_atomic = -1;
 // A/B knob: the 64 x 256 register-staged wgrad tile (id 7) for K <= 64, Kg > 128: 0 never, 1 always (+3.5 %
 // ResNet-50 step), 2 only with the BN backward in the operand staging (the stem: +1.4 %); its 1 block per CU
-// loses to the 64 x 128 tile's occupancy (profiles/ab/r3_ab_wgrad_wide.log)
+// loses to the 64 x 128 tile's occupancy (profiles/ab/r3_ab_wgrad_wide.log); 3 = 2 with a single LDS buffer
 static int g_wgrad_wide = 0;
 DTM_API void dtm_conv_set_wgrad_wide(int on) { g_wgrad_wide = on; }
 DTM_API void dtm_conv_set_wgrad_atomic(int max_splits) { g_wgrad_atomic = max_splits; }
@@ -2555,7 +2555,7 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   if (wenv == -1 && wt == 1 && d->K <= 32 && g_k32_tile) wt = 6;
   // <= 64 output channels over a wide reduction (Kg > 128): the 64 x 256 tile reads the dy / comb operand
   // once per 256 columns instead of once per 128 (the stem: 224 columns in one tile, half the g / y reads)
-  if (wenv == -1 && wt == 1 && a.Kg > 128 && (g_wgrad_wide == 1 || (g_wgrad_wide == 2 && bn))) wt = 7;
+  if (wenv == -1 && wt == 1 && a.Kg > 128 && (g_wgrad_wide == 1 || (g_wgrad_wide >= 2 && bn))) wt = 7;
   int occ = g_wgrad_occ;
   // policy (tools/conv_tile_sweep.py WTILES sweep, ResNet-50 shapes): the pipelined kernel at 2 blocks
   // per CU wins every layer with K > 64 (-10..-25 %); 4 blocks' worth of splits for the deep 3x3 7x7s
@@ -2601,6 +2601,7 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
     else
       hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 128, 2>), grid, dim3(256), 0, (hipStream_t)stream, a);
   } else if (wt == 1) launch_wgrad<64, 128, 32, 64>(a, (int)splits, (hipStream_t)stream);
+  else if (wt == 7 && g_wgrad_wide == 3) launch_wgrad<64, 256, 32, 128, 1>(a, (int)splits, (hipStream_t)stream);
   else if (wt == 7) launch_wgrad<64, 256, 32, 128>(a, (int)splits, (hipStream_t)stream);
   else if (wt == 6) launch_wgrad<32, 128, 16, 64>(a, (int)splits, (hipStream_t)stream);
   else launch_wgrad<128, 128, 64, 64>(a, (int)splits, (hipStream_t)stream);

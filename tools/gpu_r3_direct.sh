@@ -15,3 +15,5 @@ timeout -k 10 300 python bench.py --model inception_v3_slim_old > gpurun_out/ben
 grep '"value"' gpurun_out/bench_inc.log | cut -c1-200
 timeout -k 10 300 python bench.py > gpurun_out/bench_rn.log 2>&1 || { tail -20 gpurun_out/bench_rn.log; exit 1; }
 grep '"value"' gpurun_out/bench_rn.log | cut -c1-200
+VARIANTS="w0=wwide:0;w3=wwide:3" ROUNDS=5 timeout -k 10 400 python -u tools/ab_step.py > gpurun_out/wwide3_rn.log 2>&1 || { tail -30 gpurun_out/wwide3_rn.log; exit 1; }
+tail -3 gpurun_out/wwide3_rn.log
