@@ -136,9 +136,16 @@ __device__ __forceinline__ void epi_barrier() {
 // SIDE = false compiles the dgrad post-ops out: their loads are what the compiler's own vmcnt waits track,
 // and a persistent kernel's loop-carried wait for them (vmcnt(n) with the LDS-DMA prefetch issued after
 // them, which the compiler does not count) would drain the prefetch every tile.
-template <int PT, int CT, bool RAWB, bool EXACT, bool SACC, int NT, bool SIDE = true>
+// PRE: the side inputs were DMA'd to LDS by the kernel (pre: [NIT][NT] 16-B add_src chunks, then [NIT][NT]
+// act_x chunks, slot = thread; pre_ss: the block's act scale / shift [2][CT]) - no global loads here, so no
+// compiler-generated vmcnt waits (add_stride 1, no mask / act_r).
+// aacc (persistent kernels, with SACC): the activation-backward sums [sum g*x | sum g | sum g*r] of this
+// thread's chunk column are added into aacc[24] across all the block's tiles (one partial row per worker at the
+// kernel's end, worker_row) instead of a per-tile LDS reduction + row.
+template <int PT, int CT, bool RAWB, bool EXACT, bool SACC, int NT, bool SIDE = true, bool PRE = false>
 __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem, int p0, int c0, int by,
-                                                 float* ssum, float* ssq) {
+                                                 float* ssum, float* ssq, const char* pre = nullptr,
+                                                 const float* pre_ss = nullptr, float* aacc = nullptr) {
   constexpr int OROW = CT * 2 + 16;
   const int tid = threadIdx.x;
   epi_barrier<RAWB>();
@@ -161,7 +168,10 @@ __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem
   for (int e = 0; e < 8; ++e) sgr[e] = 0.f;
   if (act && !amask && kc < a.K) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { sc[e] = a.act_ss[kc + e]; sh[e] = a.act_ss[a.K + kc + e]; }
+    for (int e = 0; e < 8; ++e) {
+      sc[e] = PRE ? pre_ss[chn * 8 + e] : a.act_ss[kc + e];
+      sh[e] = PRE ? pre_ss[CT + chn * 8 + e] : a.act_ss[a.K + kc + e];
+    }
   }
   // side inputs of the dgrad post-ops (add_src, act_x, act_r, mask bytes) are loaded for a group of
   // GRP rows before any of them is used, so their latencies overlap instead of serialising per row
@@ -179,7 +189,16 @@ __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem
       pm[j] = 0u;
       ph[j] = false;
     }
-    if (side) {
+    if (PRE && side) {
+#pragma unroll
+      for (int j = 0; j < GRP; ++j) {
+        if (a.add_src) {
+          pa[j] = *(const uint4*)(pre + (size_t)(g0 + j) * NT * 16 + tid * 16);
+          ph[j] = true;
+        }
+        if (act) px[j] = *(const uint4*)(pre + (size_t)(NIT + g0 + j) * NT * 16 + tid * 16);
+      }
+    } else if (side) {
 #pragma unroll
       for (int j = 0; j < GRP; ++j) {
         const int row = ((g0 + j) * NT + tid) / CPR;
@@ -280,7 +299,10 @@ __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem
       }
     }
   }
-  if (act || bstats) {
+  if (act && aacc) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { aacc[e] += sgx[e]; aacc[8 + e] += sg[e]; aacc[16 + e] += sgr[e]; }
+  } else if (act || bstats) {
     // reduce the per-thread partial sums over the threads sharing this chunk column, one partial
     // row per pixel tile (reduced over tiles by dtm_reduce_rows / stats_reduce_finalize)
     epi_barrier<RAWB>();
@@ -318,10 +340,11 @@ __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem
 }
 
 template <int PT, int CT, int WP, int WC, int STG, bool RAWB = false, bool EXACT = false, bool NOBIAS = false,
-          bool SACC = false, int NT = 256, bool SIDE = true>
+          bool SACC = false, int NT = 256, bool SIDE = true, bool PRE = false>
 __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&acc)[WC / 16][WP / 16], char* smem,
                                                  int p0, int c0, int by, float* ssum = nullptr,
-                                                 float* ssq = nullptr) {
+                                                 float* ssq = nullptr, const char* pre = nullptr,
+                                                 const float* pre_ss = nullptr, float* aacc = nullptr) {
   constexpr int NWP = PT / WP;
   constexpr int TP = WP / 16, TC = WC / 16;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -385,7 +408,8 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
       }
     }
   }
-  if constexpr (staged) conv_nt_epi_tail<PT, CT, RAWB, EXACT, SACC, NT, SIDE>(a, smem, p0, c0, by, ssum, ssq);
+  if constexpr (staged)
+    conv_nt_epi_tail<PT, CT, RAWB, EXACT, SACC, NT, SIDE, PRE>(a, smem, p0, c0, by, ssum, ssq, pre, pre_ss, aacc);
 }
 
 // Epilogue of the 32x32x16-MFMA kernels (staged stores only: K % 8 == 0).  Register layout of a 32x32
@@ -1038,6 +1062,31 @@ __global__ __launch_bounds__(512) void conv_nt_w8_kernel(ConvNTArgs a) {
 // 16-B LDS-DMA issued through inline asm: hipcc does not see it as an LDS write, so it inserts none of
 // its conservative vmcnt(0) waits before later LDS reads/writes (every use is ordered by this file's own
 // counted vmcnt + barrier).  Its own waits for its own loads stay correct: the count is in issue order.
+// One partial row per persistent worker: the 256 threads' per-chunk-column sums lo[8] / hi[8] (thread tid owns
+// column tid % (CT/8)) are tree-reduced through red ([256][16] fp32 of free LDS) and written as
+// row[c0 + c] = sum lo, row[K + c0 + c] = sum hi for this block's CT channels.
+template <int CT>
+__device__ __forceinline__ void worker_row(float* red, const float* lo, const float* hi, float* row, int c0, int K) {
+  constexpr int CPR = CT / 8, RPT = 256 / CPR;
+  const int tid = threadIdx.x;
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[tid * 16 + e] = lo[e]; red[tid * 16 + 8 + e] = hi[e]; }
+  __syncthreads();
+  for (int h = RPT / 2; h >= 1; h >>= 1) {
+    if (tid < h * CPR) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) red[tid * 16 + e] += red[(tid + h * CPR) * 16 + e];
+    }
+    __syncthreads();
+  }
+  const int kc = c0 + tid * 8;
+  if (tid < CPR && kc < K) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { row[kc + e] = red[tid * 16 + e]; row[K + kc + e] = red[tid * 16 + 8 + e]; }
+  }
+}
+
 __device__ __forceinline__ void glds16(const void* gptr, const void* lds) {
   const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds);
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr), "s"(l) : "memory", "m0");
@@ -1159,9 +1208,11 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int n
 
   const int wp = wave % 2, wc = wave / 2;
   const int fr = lane & 15, fk = lane >> 4;
-  float ssum[8], ssq[8];
+  float ssum[8], ssq[8], aacc[24];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { ssum[e] = 0.f; ssq[e] = 0.f; }
+#pragma unroll
+  for (int e = 0; e < 24; ++e) aacc[e] = 0.f;
   int t = by0;
   const int gy = gridDim.y;
   if (t < ntiles) issue(t, 0);
@@ -1216,34 +1267,20 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int n
       }
     }
     conv_nt_epilogue<PT, CT, WP, WC, 1, true, true, true, true, 256, SIDE>(a, acc, smem + OFF_S, t * PT, c0, t, ssum,
-                                                                           ssq);
+                                                                           ssq, nullptr, nullptr, aacc);
 #pragma unroll
     for (int i = 0; i < NKT * AI; ++i) asm volatile("" ::"v"(srcs[i]));
     buf = buf + 1 == NBUF ? 0 : buf + 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (a.stats) {
-    // one partial row per worker (pixel-tile walker): [sum(K) | sumsq(K)], this block's CT channels
-    constexpr int CPR = CT / 8, RPT = 256 / CPR;
-    __syncthreads();
-    float* red = (float*)(smem + OFF_S);  // [256][16]
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { red[tid * 16 + e] = ssum[e]; red[tid * 16 + 8 + e] = ssq[e]; }
-    __syncthreads();
-    // tree over the RPT threads of each chunk column (thread tid owns column tid % CPR)
-    for (int h = RPT / 2; h >= 1; h >>= 1) {
-      if (tid < h * CPR) {
-#pragma unroll
-        for (int e = 0; e < 16; ++e) red[tid * 16 + e] += red[(tid + h * CPR) * 16 + e];
-      }
-      __syncthreads();
-    }
-    const int kc = c0 + tid * 8;
-    if (tid < CPR && kc < a.K) {
-      float* row = a.stats + (size_t)by0 * (2 * a.K);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { row[kc + e] = red[tid * 16 + e]; row[a.K + kc + e] = red[tid * 16 + 8 + e]; }
-    }
+  // one partial row per worker (pixel-tile walker): [sum(K) | sumsq(K)] statistics, or the dgrad's
+  // activation-backward sums [sum g*x | sum g (| sum g*r | sum g)] (SIDE)
+  if (a.stats) worker_row<CT>((float*)(smem + OFF_S), ssum, ssq, a.stats + (size_t)by0 * (2 * a.K), c0, a.K);
+  if (SIDE && a.act_x && a.act_sums) {
+    const int rw = a.act_r ? 4 : 2;
+    float* row = a.act_sums + (size_t)by0 * (rw * a.K);
+    worker_row<CT>((float*)(smem + OFF_S), aacc, aacc + 8, row, c0, a.K);
+    if (a.act_r) worker_row<CT>((float*)(smem + OFF_S), aacc + 16, aacc + 8, row + 2 * a.K, c0, a.K);
   }
 }
 
@@ -1270,14 +1307,20 @@ __global__ __launch_bounds__(256) void conv3x3_direct_kernel(ConvNTArgs a, int n
   constexpr int NDMA = (HCH + 255) / 256;         // halo DMA instructions per thread per tile
   constexpr int OROW = CT * 2 + 16;
   constexpr int HDMA = NDMA * 256 * 16;
-  // a slot also holds the staged output tile and the epilogue's [256][16] fp32 post-op reduction table
-  constexpr int HBUF = HDMA > PT * OROW ? (HDMA > 16384 ? HDMA : 16384) : (PT * OROW > 16384 ? PT * OROW : 16384);
+  // a slot also holds the staged output tile (the post-op sums accumulate per worker: no per-tile table)
+  constexpr int HBUF = HDMA > PT * OROW ? HDMA : PT * OROW;
+  static_assert(3 * HBUF >= 256 * 16 * 4, "worker_row's reduction table fits in the ring");
   constexpr int WBUF = 9 * CT * CIN * 2;
   constexpr int NIT = PT * (CT / 8) / 256;        // exact staged stores per thread per tile
   constexpr int TC = CT / 16, TP = 2;
-
-  static_assert(2 * NIT + NDMA <= 63, "vmcnt range");
-  __shared__ __attribute__((aligned(16))) char smem[WBUF + 3 * HBUF];
+  // SIDE: the dgrad post-op inputs (add_src / act_x chunks of each staged store) arrive by LDS-DMA issued at the
+  // top of the tile's iteration, and the act scale / shift sit in LDS: the epilogue makes no global loads
+  constexpr int SD = SIDE ? 2 * NIT : 0;          // side DMA instructions per thread per tile
+  constexpr int SBUF = SIDE ? 2 * NIT * 4096 + 2 * CT * 4 : 0;
+  static_assert(2 * NIT + SD + NDMA <= 63, "vmcnt range");
+  __shared__ __attribute__((aligned(16))) char smem[WBUF + 3 * HBUF + SBUF];
+  char* sside = smem + WBUF + 3 * HBUF;
+  float* s_ss = (float*)(sside + 2 * NIT * 4096);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nb = gridDim.x * gridDim.y;
@@ -1288,6 +1331,12 @@ __global__ __launch_bounds__(256) void conv3x3_direct_kernel(ConvNTArgs a, int n
   const char* zg = (const char*)a.zero;
   const int tiles_w = a.sp_tw, tiles_img = a.sp_th * a.sp_tw;
 
+  if constexpr (SIDE) {
+    for (int j = tid; j < 2 * CT; j += 256) {
+      const int ch = j % CT, k = c0 + ch;
+      s_ss[j] = (a.act_x && k < a.K) ? a.act_ss[(j / CT) * a.K + k] : (j < CT ? 1.f : 0.f);
+    }
+  }
   // resident weights: row (tap, channel) = tap * CT + ch, CIN-deep, swizzled 16-B chunks (plain loads)
   for (int q = tid; q < 9 * CT * CPP; q += 256) {
     const int row = q / CPP, c = q % CPP;
@@ -1324,10 +1373,31 @@ __global__ __launch_bounds__(256) void conv3x3_direct_kernel(ConvNTArgs a, int n
     }
   };
 
+  // side inputs of tile t: thread tid's staged store j is pixel row (j*256 + tid) / (CT/8), chunk tid % (CT/8)
+  const char* ssrc[SIDE ? 2 * NIT : 1];
+  auto side_issue = [&](int t) {
+    if constexpr (SIDE) {
+      constexpr int CPR = CT / 8;
+      const int kc = c0 + (tid % CPR) * 8;
+#pragma unroll
+      for (int j = 0; j < NIT; ++j) {
+        const int m = t * PT + (j * 256 + tid) / CPR;
+        const bool v = (kc < a.K) && out_valid(a, m);
+        const size_t o = v ? (size_t)out_row(a, m) * a.K + kc : 0;
+        ssrc[j] = (v && a.add_src) ? (const char*)(a.add_src + o) : zg;
+        ssrc[NIT + j] = (v && a.act_x) ? (const char*)(a.act_x + o) : zg;
+        glds16(ssrc[j], sside + (j * 4 + wave) * 1024);
+        glds16(ssrc[NIT + j], sside + ((NIT + j) * 4 + wave) * 1024);
+      }
+    }
+  };
+
   const int fr = lane & 15, fk = lane >> 4;
-  float ssum[8], ssq[8];
+  float ssum[8], ssq[8], aacc[24];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { ssum[e] = 0.f; ssq[e] = 0.f; }
+#pragma unroll
+  for (int e = 0; e < 24; ++e) aacc[e] = 0.f;
   const int gy = gridDim.y;
   int t = by0;
   if (t < ntiles) issue(t, 0);
@@ -1337,13 +1407,16 @@ __global__ __launch_bounds__(256) void conv3x3_direct_kernel(ConvNTArgs a, int n
   int buf = 0;
   for (int it = 0; t < ntiles; ++it, t += gy) {
     if (it >= 2) {
-      // issued after this wave's DMA of tile t: stores(it-2), the DMA of tile t+gy (if any), stores(it-1)
-      if (t + gy < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NIT + NDMA) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NIT) : "memory");
+      // issued after this wave's DMA of tile t: stores(it-2), side(it-1), the DMA of tile t+gy (if any),
+      // stores(it-1)
+      if (t + gy < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NIT + SD + NDMA) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NIT + SD) : "memory");
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // tile t visible; the slot of tile t-1 (its staging area) is free
-    if (t + 2 * gy < ntiles) issue(t + 2 * gy, buf == 0 ? 2 : buf - 1);
+    side_issue(t);
+    const bool pf = t + 2 * gy < ntiles;
+    if (pf) issue(t + 2 * gy, buf == 0 ? 2 : buf - 1);
     f32x4 acc[TC][TP];
 #pragma unroll
     for (int i = 0; i < TC; ++i)
@@ -1373,36 +1446,27 @@ __global__ __launch_bounds__(256) void conv3x3_direct_kernel(ConvNTArgs a, int n
           for (int j = 0; j < TP; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
       }
     }
+    if constexpr (SIDE) {  // this thread's side chunks of tile t have landed (only the halo prefetch may pend)
+      if (pf) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave is done reading the halo slot: it becomes the staging area
-    conv_nt_epilogue<PT, CT, 32, CT, 1, true, true, true, true, 256, SIDE>(a, acc, (char*)hb, t * PT, c0, t, ssum, ssq);
+    conv_nt_epilogue<PT, CT, 32, CT, 1, true, true, true, true, 256, SIDE, SIDE>(a, acc, (char*)hb, t * PT, c0, t, ssum,
+                                                                                  ssq, sside, s_ss, aacc);
 #pragma unroll
     for (int i = 0; i < NDMA; ++i) asm volatile("" ::"v"(srcs[i]));
+    if constexpr (SIDE) {
+#pragma unroll
+      for (int i = 0; i < 2 * NIT; ++i) asm volatile("" ::"v"(ssrc[i]));
+    }
     buf = buf == 2 ? 0 : buf + 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (a.stats) {
-    // one partial row per worker: [sum(K) | sumsq(K)] of this block's CT channels
-    constexpr int CPR = CT / 8, RPT = 256 / CPR;
-    __syncthreads();
-    float* red = (float*)(smem + WBUF);  // [256][16]
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { red[tid * 16 + e] = ssum[e]; red[tid * 16 + 8 + e] = ssq[e]; }
-    __syncthreads();
-    for (int h = RPT / 2; h >= 1; h >>= 1) {
-      if (tid < h * CPR) {
-#pragma unroll
-        for (int e = 0; e < 16; ++e) red[tid * 16 + e] += red[(tid + h * CPR) * 16 + e];
-      }
-      __syncthreads();
-    }
-    const int kc = c0 + tid * 8;
-    if (tid < CPR && kc < a.K) {
-      float* row = a.stats + (size_t)by0 * (2 * a.K);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { row[kc + e] = red[tid * 16 + e]; row[a.K + kc + e] = red[tid * 16 + 8 + e]; }
-    }
-  }
+  // one partial row per worker: [sum(K) | sumsq(K)] statistics, or the dgrad's [sum g*x | sum g] (SIDE)
+  float* red = (float*)(smem + WBUF);  // [256][16] (the halo ring is free)
+  if (a.stats) worker_row<CT>(red, ssum, ssq, a.stats + (size_t)by0 * (2 * a.K), c0, a.K);
+  if (SIDE && a.act_x && a.act_sums) worker_row<CT>(red, aacc, aacc + 8, a.act_sums + (size_t)by0 * (2 * a.K), c0, a.K);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2085,7 +2149,7 @@ DTM_API void dtm_conv_set_direct3(int on) { g_direct3 = on; }
 static bool direct_ok(const ConvNTArgs& a) {
   return a.R == 3 && a.S == 3 && a.stride == 1 && a.Hv == a.Hin && a.Wv == a.Win && (a.C == 32 || a.C == 64) &&
          a.K % 32 == 0 && !a.in_scale && !a.bias && !a.relu && a.pix_bytes == a.C * 2 && a.ostr == 1 &&
-         a.pad_h <= 2 && a.pad_w <= 2;
+         a.pad_h <= 2 && a.pad_w <= 2 && !a.act_mask && !a.act_r && (!a.add_src || a.add_stride == 1);
 }
 // spatial 8 x 16 output tiles, M = tiles * 128 (ConvNTArgs::sp_tw)
 static void direct_setup(ConvNTArgs& a) {
@@ -2115,8 +2179,7 @@ static void launch_direct_k(const ConvNTArgs& a, hipStream_t st) {
 }
 #define DTM_DIRECT_SEL(FN, ...)                                                                     \
   ((a.add_src || a.act_x)                                                                          \
-       ? (a.C == 64 ? (a.K % 64 == 0 ? FN<64, 64, true>(__VA_ARGS__) : FN<64, 32, true>(__VA_ARGS__)) \
-                    : (a.K % 64 == 0 ? FN<32, 64, true>(__VA_ARGS__) : FN<32, 32, true>(__VA_ARGS__))) \
+       ? (a.C == 64 ? FN<64, 32, true>(__VA_ARGS__) : FN<32, 32, true>(__VA_ARGS__))                 \
        : (a.C == 64 ? (a.K % 64 == 0 ? FN<64, 64, false>(__VA_ARGS__) : FN<64, 32, false>(__VA_ARGS__)) \
                     : (a.K % 64 == 0 ? FN<32, 64, false>(__VA_ARGS__) : FN<32, 32, false>(__VA_ARGS__))))
 static int direct_workers(const ConvNTArgs& a) { return DTM_DIRECT_SEL(direct_workers_k, a); }
@@ -2130,7 +2193,9 @@ static int device_cus();
 static int g_policy2 = 1;  // A/B knob: the v2 shape-policy rules (dtm_conv_set_policy2)
 DTM_API void dtm_conv_set_policy2(int on) { g_policy2 = on; }
 static int g_tile_w8 = 1;  // A/B knob: the 8-wave tile in the shape policy (dtm_conv_set_w8)
-static int g_stream_act = 1;  // A/B knob: the persistent streaming kernel also for act / block-output dgrads
+// A/B knob: the persistent streaming kernel also for act / block-output dgrads (off: -0.4 % ResNet-50 step once
+// the act sums accumulate per worker, profiles/ab/r3_ab_stream_act.log)
+static int g_stream_act = 0;
 DTM_API void dtm_conv_set_stream_act(int on) { g_stream_act = on; }
 static int g_kwide = 1;    // A/B knob: 64-channel tiles for K % 128 in (0, 64] (dtm_conv_set_kwide)
 DTM_API void dtm_conv_set_kwide(int on) { g_kwide = on; }
@@ -2170,6 +2235,8 @@ static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
   }
   // narrow 3x3 stride-1 layers: the direct kernel (resident weights, halo tiles; the caller sets the
   // spatial tiling with direct_setup)
+  // (dgrad post-op inputs come by LDS-DMA: with per-tile global side loads in the epilogue the compiler's waits
+  // drained the halo prefetch - Inception stem dgrads 551 / 252 us vs 355 / 195 on the GEMM tiles)
   if (((id == -1 && a.K == 32) || id == 60) && g_direct3 && direct_ok(a)) return {60, 128, 4};
   // the pipelined LDS-DMA 128x128 tile (2 slots, 2 blocks/CU) wins every deep-reduction layer without the
   // prologue (tools/conv_tile_sweep.py: 3x3 at 14x14 / 7x7 -13..-18 %, deep 1x1 -5..-16 %)
@@ -2446,7 +2513,10 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvD
       b.fd_PQ = make_fastdiv(b.P * b.Q); b.fd_Q = make_fastdiv(b.Q);
       lt[nl] = pick_tile(b);
       if (lt[nl].id == 60) direct_setup(b);
-      lrows[nl] = (b.M + lt[nl].PT - 1) / lt[nl].PT;  // pixel tiles
+      // act partial rows: one per pixel tile, or one per worker for the persistent kernels
+      lrows[nl] = lt[nl].id == 60 ? direct_workers(b)
+                  : (lt[nl].id == 30 || lt[nl].id == 31) ? stream_rows(b, lt[nl].id)
+                                                         : (b.M + lt[nl].PT - 1) / lt[nl].PT;
       rows += lrows[nl];
       la[nl++] = b;
     }

@@ -137,6 +137,41 @@ def test_direct3x3_conv_bn(H, W, C, K, pad, direct):
     assert all(v < 2e-2 for v in errs.values()), errs
 
 
+@pytest.mark.parametrize("C", [32, 64])
+def test_direct3x3_dgrad_post_ops(C):
+    """The direct kernel's dgrad with its post-op inputs arriving by LDS-DMA: the input is a BN+ReLU'd conv
+    output (activation backward: mask, scale, BN-gradient sums) read by two 3x3 convs with 32 outputs (the
+    second dgrad folds the first one's stashed gradient, add_src).  Every gradient matches torch fp32."""
+    torch.manual_seed(7)
+    x = torch.randn(2, 19, 23, 16, device=DEV).to(torch.bfloat16).float()
+    w0 = (torch.randn(C, 1, 1, 16, device=DEV) / 4.0).to(torch.bfloat16).float()
+    w1 = (torch.randn(32, 3, 3, C, device=DEV) / (9 * C) ** 0.5).to(torch.bfloat16).float()
+    w2 = (torch.randn(32, 3, 3, C, device=DEV) / (9 * C) ** 0.5).to(torch.bfloat16).float()
+    bn0, bn1, bn2 = _bn(C), _bn(32), _bn(32)
+    xk = x.to(torch.bfloat16).requires_grad_()
+    wk = [w.clone().requires_grad_() for w in (w0, w1, w2)]
+    l0 = fused.conv_bn(xk, wk[0], bn0, 1, "SAME", True, True)
+    m0 = ((l0.raw.detach().float() * l0.ss[0] + l0.ss[1]) > 0).float()
+    y1 = fused.conv_bn(l0, wk[1], bn1, 1, "SAME", True, False).materialize()
+    y2 = fused.conv_bn(l0, wk[2], bn2, 1, "VALID", True, False).materialize()
+    xr = x.clone().requires_grad_()
+    wr = [w.clone().requires_grad_() for w in (w0, w1, w2)]
+    g0, b0 = bn0.gamma.detach().clone().requires_grad_(), bn0.beta.detach().clone().requires_grad_()
+    a0 = ref.batch_norm(ref.conv2d(xr, wr[0]), g0, b0, None, None, True, 0.9, 1e-3, False) * m0
+    r1 = ref.batch_norm(ref.conv2d(a0, wr[1], None, 1, "SAME"), bn1.gamma.detach(), bn1.beta.detach(), None, None,
+                        True, 0.9, 1e-3, False)
+    r2 = ref.batch_norm(ref.conv2d(a0, wr[2], None, 1, "VALID"), bn2.gamma.detach(), bn2.beta.detach(), None, None,
+                        True, 0.9, 1e-3, False)
+    gy1, gy2 = (torch.randn_like(r).to(torch.bfloat16).float() for r in (r1, r2))
+    (r1 * gy1).sum().add((r2 * gy2).sum()).backward()
+    (y1.float() * gy1).sum().add((y2.float() * gy2).sum()).backward()
+    torch.cuda.synchronize()
+    errs = dict(y1=_rel(y1, r1), y2=_rel(y2, r2), dx=_rel(xk.grad, xr.grad), dw0=_rel(wk[0].grad, wr[0].grad),
+                dw1=_rel(wk[1].grad, wr[1].grad), dw2=_rel(wk[2].grad, wr[2].grad),
+                dg0=_rel(bn0.gamma.grad, g0.grad), db0=_rel(bn0.beta.grad, b0.grad))
+    assert all(v < 3e-2 for v in errs.values()), errs
+
+
 def test_full_window_conv_dgrad_gemm():
     """Inception's aux head: 1x1 conv+BN+ReLU folded into a 5x5 VALID conv over its 5x5 map (1x1 output). The
     second conv's dgrad runs as a plain GEMM with the act backward in torch (fused._full_window_dgrad_act);

@@ -37,7 +37,7 @@ def apply(cfg):
     L.dtm_conv_set_w8(int(cfg.get("w8", "1")))
     L.dtm_conv_set_kwide(int(cfg.get("kwide", "1")))
     L.dtm_set_reduce_few(int(cfg.get("few", "1")))
-    L.dtm_conv_set_stream_act(int(cfg.get("sact", "1")))
+    L.dtm_conv_set_stream_act(int(cfg.get("sact", "0")))
     L.dtm_conv_set_act_tile(int(cfg.get("atile", "-1")))
     L.dtm_conv_set_policy2(int(cfg.get("pol2", "1")))
     L.dtm_set_grid_cpt(int(cfg.get("cpt", "8")))
