@@ -1,0 +1,10 @@
+#!/bin/bash
+# Stem wgrad kernel time: 64x128 (2 column tiles) vs 64x256 (one) tiles.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+for v in 0 2 3; do
+VARIANTS="s=wwide:$v" ROUNDS=1 STEPS=3 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_ww$v -o run -- python3 -u tools/ab_step.py > gpurun_out/ww_prof$v.log 2>&1 || { tail -30 gpurun_out/ww_prof$v.log; exit 1; }
+f=$(ls gpurun_out/prof_ww$v/run_kernel_stats.csv gpurun_out/prof_ww$v/*/run_kernel_stats.csv 2>/dev/null | head -1)
+echo "== wwide=$v"; python3 tools/prof_summary.py "$f" 5 80 | grep -i "total\|conv_wgrad_kernel"
+done
