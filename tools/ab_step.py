@@ -80,18 +80,33 @@ def main():
     kw = {"fc_conv_padding": "SAME"} if model == "vgg_16" else {}  # (bench.py's CIFAR geometry)
     net = nets_factory.build(model, num_classes=ncls, **kw).to(dev)
     B = B or B0
-    step = TrainStep(net, optimizer=opt, lr=0.01, momentum=0.9, **extra)
+    # GRAPH=1: every variant replays its own captured hipGraph step (captured on the variant's first step;
+    # the knobs are baked in at capture), DTM_WGRAD_STREAM_GRAPH=1 lets the capture fork the side stream
+    graph = os.environ.get("GRAPH", "0") == "1"
+    step = TrainStep(net, optimizer=opt, lr=0.01, momentum=0.9, use_graph=graph, **extra)
+    graphs = {}
+
+    def select(n):
+        if graph:
+            step._graph, step._static_loss = graphs.get(n, (None, None))
+
+    def keep(n):
+        if graph and n not in graphs and step._graph is not None:
+            graphs[n] = (step._graph, step._static_loss)
     x = torch.randn(B, S, S, 1 if model == "lenet" else 3, device=dev).to(torch.bfloat16)
     y = torch.randint(0, ncls, (B,), device=dev)
     res = {n: [] for n, _ in variants}
     for n, cfg in variants:  # warm every variant (workspace growth, first-touch)
         apply(cfg)
-        for _ in range(2):
+        select(n)
+        for _ in range(2 + (2 if graph else 0)):
             step(x, y)
+            keep(n)
     torch.cuda.synchronize()
     for r in range(rounds):
         for n, cfg in variants:
             apply(cfg)
+            select(n)
             step(x, y)
             torch.cuda.synchronize()
             t = time.perf_counter()
