@@ -74,7 +74,36 @@ struct ConvNTArgs {
   // out of range (M = tiles * 128)
   int sp_tw, sp_th;
   FastDiv fd_sp_img, fd_sp_tw;
+  // grouped launch of a stride-decomposed dgrad (ngrp > 1, gridDim.z = ngrp): every output parity class is one
+  // z-slice of ONE launch instead of a launch of its own; the classes share M / P / Q / K and differ in the
+  // fields below (their taps of the decomposed weight, output parity, partial-sum rows)
+  int ngrp;
+  struct Grp {
+    const bf16_t* w;
+    float* act_sums;
+    int R, S, pad_h, pad_w, oa, ob, Kg;
+  } grp[4];
 };
+
+// block -> (class, tile) of a grouped launch (XCD remap over the whole grid; class = z-slice of the logical
+// order) and the class's fields copied into a; a plain launch (gridDim.z == 1) keeps the 2-D remap
+__device__ __forceinline__ int grp_tile(ConvNTArgs& a) {
+  const int gxy = gridDim.x * gridDim.y;
+  const int t = xcd_remap((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x, gxy * gridDim.z);
+  if (gridDim.z > 1) {
+    // constant indices only: a dynamically indexed member array would put the whole argument block in scratch
+    const int g = t / gxy;
+#define DTM_GRP_LOAD(k)                                                                   \
+  a.w = a.grp[k].w; a.act_sums = a.grp[k].act_sums; a.R = a.grp[k].R; a.S = a.grp[k].S; \
+  a.pad_h = a.grp[k].pad_h; a.pad_w = a.grp[k].pad_w; a.oa = a.grp[k].oa; a.ob = a.grp[k].ob; a.Kg = a.grp[k].Kg
+    if (g == 0) { DTM_GRP_LOAD(0); }
+    else if (g == 1) { DTM_GRP_LOAD(1); }
+    else if (g == 2) { DTM_GRP_LOAD(2); }
+    else { DTM_GRP_LOAD(3); }
+#undef DTM_GRP_LOAD
+  }
+  return t % gxy;
+}
 
 // full-resolution coordinates / row of output pixel m (see ConvNTArgs::ostr)
 __device__ __forceinline__ void out_nhw(const ConvNTArgs& a, int m, int& n, int& h, int& w) {
@@ -467,7 +496,7 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wp = wave % NWP, wc = wave / NWP;
-  const int tile = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const int tile = grp_tile(a);
   const int bx = tile % gridDim.x, by = tile / gridDim.x;
   const int p0 = by * PT, c0 = bx * CT;
   const int ch = tid & 7, rb = tid >> 3;
@@ -671,7 +700,7 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
   static_assert(G <= 31 && NS >= 2 && NS <= 4, "vmcnt range");
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tile = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const int tile = grp_tile(a);
   const int bx = tile % gridDim.x, by = tile / gridDim.x;
   const int p0 = by * PT, c0 = bx * CT;
   const int lr = lane >> 3;
@@ -903,7 +932,7 @@ __global__ __launch_bounds__(512) void conv_nt_w8_kernel(ConvNTArgs a) {
   typedef __attribute__((address_space(3))) void lvoid;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tile = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const int tile = grp_tile(a);
   const int bx = tile % gridDim.x, by = tile / gridDim.x;
   const int p0 = by * PT, c0 = bx * CT;
   const int lr = lane >> 3;
@@ -2029,13 +2058,13 @@ static const bf16_t* zero_chunk() {
 
 template <int PT, int CT, int NWP, int NS, int UD, bool M32 = false>
 static void launch_w8(const ConvNTArgs& a, hipStream_t st) {
-  dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT);
+  dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT, a.ngrp > 1 ? a.ngrp : 1);
   hipLaunchKernelGGL((conv_nt_w8_kernel<PT, CT, NWP, NS, UD, M32>), grid, dim3(512), 0, st, a);
 }
 
 template <int PT, int CT, int NS, int UD, int NWP = 2, bool M32 = false>
 static void launch_pipe(const ConvNTArgs& a, hipStream_t st) {
-  dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT);
+  dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT, a.ngrp > 1 ? a.ngrp : 1);
   if (a.in_scale) hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, true, NWP, M32>), grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, false, NWP, M32>), grid, dim3(256), 0, st, a);
 }
@@ -2130,7 +2159,7 @@ static bool stream_ok(const ConvNTArgs& a) {
 
 template <int PT, int CT, int WP, int WC, int UD, int NBUF = 2>
 static void launch_nt(const ConvNTArgs& a, hipStream_t st) {
-  dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT);
+  dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT, a.ngrp > 1 ? a.ngrp : 1);
   hipLaunchKernelGGL((conv_nt_kernel<PT, CT, WP, WC, UD, NBUF>), grid, dim3(256), 0, st, a);
 }
 
@@ -2358,6 +2387,7 @@ static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, cons
   if (d->C % 8 || d->K % 4) return -1;
   ConvNTArgs a;
   a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.y = (bf16_t*)y;
+  a.ngrp = 0;
   a.stats = nullptr; a.bias = bias; a.in_scale = in_scale; a.in_shift = in_shift;
   a.add_src = nullptr; a.act_x = nullptr; a.act_ss = nullptr; a.act_sums = nullptr;
   a.act_mask = nullptr; a.act_r = nullptr;
@@ -2452,6 +2482,10 @@ DTM_API int dtm_conv_dgrad_ex(const void* dy, const void* wt, void* dx, const Co
                          stream);
 }
 
+// A/B knob (dtm_conv_set_dec_group): the parity classes of a stride-decomposed dgrad as one grouped launch
+static int g_dec_group = 1;
+DTM_API void dtm_conv_set_dec_group(int on) { g_dec_group = on; }
+
 static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvDesc* d, const void* add_src,
                            int add_stride, const void* act_x, const float* act_ss, float* act_sums, int act_unscaled,
                            const void* act_mask, const void* act_r, void* stream) {
@@ -2461,6 +2495,7 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvD
   if ((add_src || act_x) && d->C % 8) return -5;
   ConvNTArgs a;
   a.x = (const bf16_t*)dy; a.w = (const bf16_t*)wt; a.y = (bf16_t*)dx;
+  a.ngrp = 0;
   a.stats = nullptr; a.bias = nullptr; a.in_scale = nullptr; a.in_shift = nullptr;
   a.add_src = (const bf16_t*)add_src; a.act_x = (const bf16_t*)act_x; a.act_ss = act_ss; a.act_sums = nullptr;
   a.act_mask = (const uint8_t*)act_mask; a.act_r = (const bf16_t*)act_r;
@@ -2520,15 +2555,43 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvD
       rows += lrows[nl];
       la[nl++] = b;
     }
+  // the parity classes of a stride-decomposed dgrad as ONE grouped launch (z = class) on the tile of the class
+  // with the most taps, when they share the output grid (even H, W) and that tile is a grouped-capable kernel
+  int gi = -1;
+  if (dec && nl > 1 && nl <= 4 && g_dec_group) {
+    gi = 0;
+    for (int i = 1; i < nl; ++i) {
+      if (la[i].M != la[0].M || la[i].P != la[0].P || la[i].Q != la[0].Q) gi = -2;
+      if (gi >= 0 && la[i].Kg > la[gi].Kg) gi = i;
+    }
+    const int id = gi >= 0 ? lt[gi].id : -1;
+    if (!(id == 0 || id == 3 || id == 4 || id == 21 || id == 24 || id == 26 || id == 32 || id == 40)) gi = -1;
+    if (gi >= 0) {  // every class on that tile: one partial-sum row per pixel tile of it
+      rows = 0;
+      for (int i = 0; i < nl; ++i) {
+        lt[i] = lt[gi];
+        lrows[i] = (la[i].M + lt[gi].PT - 1) / lt[gi].PT;
+        rows += lrows[i];
+      }
+    }
+  }
   float* ws = nullptr;
   if (act_x) {
     ws = dtm_ws_get_stream((size_t)rows * rw * d->C, (hipStream_t)stream);
     if (!ws) return -4;
   }
-  for (int i = 0, r = 0; i < nl; r += lrows[i], ++i) {
+  for (int i = 0, r = 0; i < nl; r += lrows[i], ++i)
     // every launch's partial-sum rows go to its own slice of one table, reduced together below
     if (act_x) la[i].act_sums = ws + (size_t)r * rw * d->C;
-    dispatch_nt(la[i], dec ? 1 : st, lt[i], (hipStream_t)stream);
+  if (gi >= 0) {
+    ConvNTArgs g = la[gi];
+    g.ngrp = nl;
+    for (int i = 0; i < nl; ++i) {
+      g.grp[i] = {la[i].w, la[i].act_sums, la[i].R, la[i].S, la[i].pad_h, la[i].pad_w, la[i].oa, la[i].ob, la[i].Kg};
+    }
+    dispatch_nt(g, 1, lt[gi], (hipStream_t)stream);
+  } else {
+    for (int i = 0; i < nl; ++i) dispatch_nt(la[i], dec ? 1 : st, lt[i], (hipStream_t)stream);
   }
   if (act_x && act_r) {
     // [sum g*x | sum g] -> act_sums rows 0-1, [sum g*r | sum g] -> rows 4-5 of an [8][C] buffer: rows 0-3

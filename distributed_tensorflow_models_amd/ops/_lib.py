@@ -59,6 +59,7 @@ _SIGS = {
     "dtm_conv_set_wgrad_atomic": (None, [_I]),
     "dtm_conv_set_wgrad_wide": (None, [_I]),
     "dtm_conv_set_direct3": (None, [_I]),
+    "dtm_conv_set_dec_group": (None, [_I]),
     "dtm_cat_desc_bytes": (_I, []),
     "dtm_cat_bn_apply": (_I, [_P, _I, _P, _L, _I, _P]),
     "dtm_cat_bn_apply_bwd": (_I, [_P, _I, _P, _P, _L, _I, _P]),
@@ -185,8 +186,10 @@ def side_stream():
         _side["on"] = os.environ.get("DTM_WGRAD_STREAM", "1") == "1"
     if not _side["on"] or not torch.cuda.is_available():
         return None
-    if torch.cuda.is_current_stream_capturing() and os.environ.get("DTM_WGRAD_STREAM_GRAPH", "0") != "1":
-        return None  # (hipGraph capture: single stream unless DTM_WGRAD_STREAM_GRAPH=1)
+    if torch.cuda.is_current_stream_capturing():
+        # hipGraph capture stays single-stream: a captured fork onto this stream faulted on replay (illegal
+        # address, Inception-v3; profiles/ab/README.md round 3), so captured steps never use it
+        return None
     dev = torch.cuda.current_device()
     st = _side["stream"]
     if st is None or st.device.index != dev:
@@ -217,6 +220,23 @@ def priority_stream():
         st = torch.cuda.Stream(device=dev, priority=min(lo, hi))
         _prio["stream"] = st
     return st
+
+
+_side_cu = {"frac": None}
+
+
+def set_side_cu_fraction(frac):
+    _side_cu["frac"] = float(frac)
+
+
+def side_cus():
+    """CU count the split-K policy of a side-stream weight gradient sizes its grid for (DTM_SIDE_CU_FRAC x the
+    device's CUs): the side stream shares the chip with the dgrad chain, so fewer splits mean fewer fp32
+    partial slabs to write and reduce and fewer workgroups taken from the main stream.  Measured on ResNet-50
+    (profiles/ab/r3_ab_side_cus.log, r3_ab_dgrp_bnst.log): 0.75 -1.0..-1.5 % step vs 1.0; 0.5 neutral; 0.35 +4 %."""
+    if _side_cu["frac"] is None:
+        _side_cu["frac"] = float(os.environ.get("DTM_SIDE_CU_FRAC", "0.75"))
+    return max(8, int(num_cus() * _side_cu["frac"]))
 
 
 def side_fork(*tensors):

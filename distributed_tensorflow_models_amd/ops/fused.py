@@ -98,6 +98,13 @@ def _bnout_enabled():
     return os.environ.get("DTM_BNOUT_FUSE", "1") != "0"
 
 
+def _bnout_strided():
+    """A/B knob DTM_BNOUT_STRIDED (default on): the dgrad-epilogue BN-apply backward also for the outputs of
+    stride-2 units (strided identity residual)."""
+    import os
+    return os.environ.get("DTM_BNOUT_STRIDED", "1") != "0"
+
+
 def _slot_register(x):
     if not (torch.is_grad_enabled() and x.requires_grad and x.is_cuda):
         return None
@@ -259,7 +266,7 @@ class _ConvBNFn(torch.autograd.Function):
             if st is not None:
                 with torch.cuda.stream(st):
                     _check(L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(w.main_grad), _lib.ptr(sc),
-                                            _lib.ptr(sh), ctypes.byref(d), _lib.num_cus(), _lib.stream_ptr()),
+                                            _lib.ptr(sh), ctypes.byref(d), _lib.side_cus(), _lib.stream_ptr()),
                            "conv_wgrad(side)")
                     _notify(w)
                 wg_side = True
@@ -445,10 +452,13 @@ class _BNApplyFn(torch.autograd.Function):
                                 res_mode, int(relu), _lib.stream_ptr())
         ctx.relu, ctx.res_mode, ctx.res_slot, ctx.res_stride = relu, res_mode, res_slot, res_stride
         ctx.unscaled = int(unscaled) if res_mode == 2 else int(unscaled) & 1
-        # eligible for the dgrad-epilogue backward: bitmask ReLU, unstrided residual, and every gradient
-        # this backward hands out equal to g itself (unscaled producers)
+        # eligible for the dgrad-epilogue backward: bitmask ReLU and every gradient this backward hands out
+        # equal to g itself (unscaled producers).  A strided identity residual (the subsampled block input of
+        # a stride-2 unit) qualifies too: its gradient is g at the subsampled pixels, handed to the block
+        # input's other consumer with the stride exactly as the separate pass does
         ctx.bnout = None
-        if (mask is not None and relu and res_stride == 1 and (ctx.unscaled & 1) and
+        if (mask is not None and relu and (res_stride == 1 or (res_mode == 1 and _bnout_strided())) and
+                (ctx.unscaled & 1) and
                 (res_mode != 2 or (ctx.unscaled & 2)) and C % 8 == 0 and _bnout_enabled()):
             ctx.bnout = _BNOutInfo(mask, x, res if res_mode == 2 else None)
             try:

@@ -47,6 +47,8 @@ def main():
     for (H, C, K, R, st, pad, cnt) in SHAPES:
         if only and only not in "%d_%d_%d_%d" % (H, C, K, R):
             continue
+        if os.environ.get("STRIDED") and st == 1:
+            continue
         x = torch.randn(B, H, H, C, device="cuda").to(torch.bfloat16)
         w = (torch.randn(K, R, R, C, device="cuda") * 0.05).to(torch.bfloat16)
         g = conv_geom(tuple(x.shape), tuple(w.shape), st, (pad, pad))

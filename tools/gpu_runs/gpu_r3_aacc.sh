@@ -9,5 +9,5 @@ MODEL=inception_v3_slim_old VARIANTS="direct=dir3:1;gemm=dir3:0" ROUNDS=6 timeou
 tail -3 gpurun_out/dir3_inc4.log
 VARIANTS="base=;sact0=sact:0" ROUNDS=5 timeout -k 10 400 python -u tools/ab_step.py > gpurun_out/sact_rn.log 2>&1 || { tail -30 gpurun_out/sact_rn.log; exit 1; }
 tail -3 gpurun_out/sact_rn.log
-bash tools/gpu_r3_inc.sh
+bash tools/gpu_runs/gpu_r3_inc.sh
 grep "conv3x3_direct" gpurun_out/r3_timeline_inc.txt | cut -c1-110

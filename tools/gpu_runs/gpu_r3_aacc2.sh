@@ -8,5 +8,5 @@ MODEL=inception_v3_slim_old VARIANTS="direct=dir3:1;gemm=dir3:0" ROUNDS=6 timeou
 tail -3 gpurun_out/dir3_inc5.log
 VARIANTS="sact0=sact:0;sact1=sact:1" ROUNDS=5 timeout -k 10 400 python -u tools/ab_step.py > gpurun_out/sact_rn2.log 2>&1 || { tail -30 gpurun_out/sact_rn2.log; exit 1; }
 tail -3 gpurun_out/sact_rn2.log
-bash tools/gpu_r3_inc.sh
+bash tools/gpu_runs/gpu_r3_inc.sh
 grep "conv3x3_direct" gpurun_out/r3_timeline_inc.txt | cut -c1-110

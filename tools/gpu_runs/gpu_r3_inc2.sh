@@ -7,4 +7,4 @@ MODEL=inception_v3_slim_old VARIANTS="direct=dir3:1;gemm=dir3:0" ROUNDS=6 timeou
 tail -3 gpurun_out/dir3_inc2.log
 timeout -k 10 300 python bench.py --model inception_v3_slim_old > gpurun_out/bench_inc.log 2>&1 || { tail -20 gpurun_out/bench_inc.log; exit 1; }
 grep '"value"' gpurun_out/bench_inc.log | cut -c1-200
-bash tools/gpu_r3_inc.sh
+bash tools/gpu_runs/gpu_r3_inc.sh

@@ -9,4 +9,4 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -1 gpurun_out/side3_suites.log
 MODEL=inception_v3_slim_old VARIANTS="direct=dir3:1;gemm=dir3:0" ROUNDS=6 timeout -k 10 400 python -u tools/ab_step.py > gpurun_out/dir3_inc3.log 2>&1 || { tail -30 gpurun_out/dir3_inc3.log; exit 1; }
 tail -3 gpurun_out/dir3_inc3.log
-bash tools/gpu_r3_inc.sh
+bash tools/gpu_runs/gpu_r3_inc.sh

@@ -6,5 +6,5 @@ for m in lenet vgg_16 inception_v3_slim_old; do
   timeout -k 10 300 python bench.py --model $m --steps 20 --warmup 5 > gpurun_out/all_$m.log 2>&1 || { echo "bench $m failed"; tail -20 gpurun_out/all_$m.log; exit 1; }
   grep -o '"value": [0-9.]*.\{0,120\}' gpurun_out/all_$m.log
 done
-TSTEPS=4 bash tools/gpu_session.sh trainers > gpurun_out/trainers.log 2>&1 || { tail -30 gpurun_out/trainers.log; exit 1; }
+TSTEPS=4 bash tools/gpu_runs/gpu_session.sh trainers > gpurun_out/trainers.log 2>&1 || { tail -30 gpurun_out/trainers.log; exit 1; }
 grep -c "==" gpurun_out/trainers.log
