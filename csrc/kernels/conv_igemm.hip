@@ -2627,6 +2627,8 @@ static int g_wgrad_atomic = -1;
 static int g_wgrad_wide = 0;
 DTM_API void dtm_conv_set_wgrad_wide(int on) { g_wgrad_wide = on; }
 DTM_API void dtm_conv_set_wgrad_atomic(int max_splits) { g_wgrad_atomic = max_splits; }
+static int g_wgrad_p64 = 0;
+DTM_API void dtm_conv_set_wgrad_p64(int v) { g_wgrad_p64 = v; }
 DTM_API void dtm_conv_set_wgrad_tile(int id, int occ) {
   g_wgrad_env = id;
   if (occ > 0) g_wgrad_occ = occ;
@@ -2699,10 +2701,17 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
     // 14x14 / 7x7 3x3 -8..-13 %, 7x7 1024->2048 -7 %; it loses on every K < 256 or short-RSC layer)
     if (g_tile_w8 && d->K >= 256 && a.Kg >= 1024 && (d->R * d->S > 1 || d->K >= 1024)) wt = 12;
   }
+  // the pipelined 64 x 128 tile (id 11, waves 1x4 of 64x32; A/B knob dtm_conv_set_wgrad_p64): 1 = for output widths
+  // whose last 128-row tile is at most half full (Inception's 192 / 320 / 160 ...), 2 = also for 33..64 outputs
+  if (wenv == -1 && !in_scale && !bn && g_wgrad_p64) {
+    if (wt == 10 && d->K % 128 != 0 && d->K % 128 <= 64) wt = 11;
+    else if (g_wgrad_p64 >= 2 && d->K > 32 && d->K <= 64 && (wt == 1 || wt == 7)) { wt = 11; occ = 2; }
+  }
   if (wt >= 10 && (in_scale || bn)) wt = d->K <= 64 ? 1 : 0;  // the pipelined kernels have no operand prologues
-  if (wt != 0 && wt != 1 && wt != 6 && wt != 7 && wt != 10 && wt != 12) wt = 0;
+  if (wt != 0 && wt != 1 && wt != 6 && wt != 7 && wt != 10 && wt != 11 && wt != 12) wt = 0;
   const bool big = wt == 12;  // 8-wave 256x256 (one block per CU)
-  const int MT = wt == 6 ? 32 : ((wt == 1 || wt == 7) ? 64 : (big ? 256 : 128)), NT = (big || wt == 7) ? 256 : 128;
+  const int MT = wt == 6 ? 32 : ((wt == 1 || wt == 7 || wt == 11) ? 64 : (big ? 256 : 128)),
+            NT = (big || wt == 7) ? 256 : 128;
   if (big) occ = (wenv == 12 && g_wgrad_occ != 4) ? g_wgrad_occ : 1;  // (sweeps: WTILES=12:<occ>)
   long tiles = (long)((a.Kg + NT - 1) / NT) * ((a.K + MT - 1) / MT);
   long target = (long)num_cus * (wt >= 10 ? occ : 3);
@@ -2731,6 +2740,8 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
     dim3 grid((a.Kg + NT - 1) / NT, (a.K + MT - 1) / MT, splits);
     if (wt == 12)
       hipLaunchKernelGGL((conv_wgrad_pipe_kernel<256, 256, 2, 2, 512>), grid, dim3(512), 0, (hipStream_t)stream, a);
+    else if (wt == 11)
+      hipLaunchKernelGGL((conv_wgrad_pipe_kernel<64, 128, 2, 1, 256>), grid, dim3(256), 0, (hipStream_t)stream, a);
     else
       hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 128, 2>), grid, dim3(256), 0, (hipStream_t)stream, a);
   } else if (wt == 1) launch_wgrad<64, 128, 32, 64>(a, (int)splits, (hipStream_t)stream);

@@ -60,6 +60,7 @@ _SIGS = {
     "dtm_conv_set_wgrad_wide": (None, [_I]),
     "dtm_conv_set_direct3": (None, [_I]),
     "dtm_conv_set_dec_group": (None, [_I]),
+    "dtm_conv_set_wgrad_p64": (None, [_I]),
     "dtm_cat_desc_bytes": (_I, []),
     "dtm_cat_bn_apply": (_I, [_P, _I, _P, _L, _I, _P]),
     "dtm_cat_bn_apply_bwd": (_I, [_P, _I, _P, _P, _L, _I, _P]),
@@ -237,6 +238,23 @@ def side_cus():
     if _side_cu["frac"] is None:
         _side_cu["frac"] = float(os.environ.get("DTM_SIDE_CU_FRAC", "0.75"))
     return max(8, int(num_cus() * _side_cu["frac"]))
+
+
+_wgrad_cu = {"main": None, "stem": None}
+
+
+def set_wgrad_cu_percent(kind, pct):
+    _wgrad_cu[kind] = float(pct)
+
+
+def wgrad_cus(kind="main"):
+    """CU count the split-K policy of a main-stream weight gradient sizes its grid for: ``kind`` 'main' (every
+    conv wgrad not on the side stream; DTM_WGRAD_CU percent) or 'stem' (the packed-row stem's BN-fused wgrad,
+    the last kernel of the backward; DTM_STEM_WGRAD_CU percent)."""
+    if _wgrad_cu[kind] is None:
+        env = "DTM_STEM_WGRAD_CU" if kind == "stem" else "DTM_WGRAD_CU"
+        _wgrad_cu[kind] = float(os.environ.get(env, "100"))
+    return max(8, int(num_cus() * _wgrad_cu[kind] / 100.0))
 
 
 def side_fork(*tensors):

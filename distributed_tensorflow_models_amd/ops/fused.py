@@ -319,7 +319,7 @@ class _ConvBNFn(torch.autograd.Function):
             mg = getattr(w, "main_grad", None)
             target = mg if mg is not None else torch.zeros(w.shape, device=dy.device, dtype=torch.float32)
             _check(L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(target), _lib.ptr(sc),
-                                                         _lib.ptr(sh), ctypes.byref(d), _lib.num_cus(), s),
+                                                         _lib.ptr(sh), ctypes.byref(d), _lib.wgrad_cus(), s),
                    "conv_wgrad")
             if mg is not None:
                 _notify(w)
@@ -600,7 +600,7 @@ class _StemConvBNFn(torch.autograd.Function):
                                           _lib.ptr(ss), _lib.ptr(gamma), ctx.count,
                                           _lib.ptr(gmg if gmg is not None else dgamma),
                                           _lib.ptr(bmg if bmg is not None else dbeta), _lib.ptr(tv), ctypes.byref(d),
-                                          _lib.num_cus(), s), "stem_conv_wgrad_bnbwd")
+                                          _lib.wgrad_cus("stem"), s), "stem_conv_wgrad_bnbwd")
             for p, m in ((gamma, gmg), (beta, bmg)):
                 if m is not None:
                     _notify(p)
@@ -631,7 +631,7 @@ class _StemConvBNFn(torch.autograd.Function):
             d = _lib.ConvDesc(N, Hp, Wp, 32, K, R, 1, P, Q, st, 0, 0, 8)
             tv = torch.zeros((K, R, 8, 4), device=dy.device, dtype=torch.float32)
             _check(L.dtm_conv_wgrad(_lib.ptr(xp), _lib.ptr(dy), _lib.ptr(tv), None, None, ctypes.byref(d),
-                                    _lib.num_cus(), s), "stem_conv_wgrad")
+                                    _lib.wgrad_cus("stem"), s), "stem_conv_wgrad")
             dw = _accum_param_grad(w, tv[:, :, :S, :C])
         return None, dw, dgamma, dbeta, None, None, None
 
@@ -736,9 +736,14 @@ def conv_bn(x, w, bn, stride, padding, training, relu):
         if mode == "apply" or x.ss.shape[1] % 8 != 0:
             x = x.materialize()
         else:
+            lz = x
             in_ss, in_unscaled, x = x.ss, x.unscaled, x.raw
             if mode == "mat":
-                x_mat = bn_apply_nograd(x, in_ss)
+                # one materialisation per LazyBN, whatever the number of conv consumers (Inception's split
+                # 1x3 / 3x1 pairs read the same activation)
+                if lz.mat is None:
+                    lz.mat = bn_apply_nograd(x, in_ss)
+                x_mat = lz.mat
     g = conv_geom(tuple(x.shape), tuple(w.shape), stride, padding)
     if in_ss is None and _stem_eligible(x, w, stride, g):
         if training:
@@ -775,7 +780,7 @@ class _BNStatsFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y):
         C = y.shape[-1]
-        stats = torch.zeros((2, C), device=y.device, dtype=torch.float32)
+        stats = arena.zeros((2, C), y.device)  # (per-step zeroed scratch: no fill launch)
         _lib.lib().dtm_bn_stats(_lib.ptr(y), _lib.ptr(stats), y.numel() // C, C, _lib.stream_ptr())
         ctx.save_for_backward(y)
         return stats, y.view_as(y)

@@ -463,7 +463,8 @@ class _BatchNormFn(torch.autograd.Function):
         x = x.contiguous()
         ss = torch.empty((4, C), device=x.device, dtype=torch.float32)
         if training:
-            stats = torch.zeros((2, C), device=x.device, dtype=torch.float32)
+            from .fused import arena  # (per-step zeroed scratch: no fill launch)
+            stats = arena.zeros((2, C), x.device)
             L.dtm_bn_stats(_lib.ptr(x), _lib.ptr(stats), M, C, s)
             L.dtm_bn_finalize(_lib.ptr(stats), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(moving_mean),
                               _lib.ptr(moving_var), _lib.ptr(ss), C, float(M), float(eps), float(decay),
@@ -490,7 +491,8 @@ class _BatchNormFn(torch.autograd.Function):
         M = x.numel() // C
         dy = dy.contiguous()
         mask_mode = 1 if ctx.relu else 0
-        sums = torch.zeros((2, C), device=x.device, dtype=torch.float32)
+        from .fused import arena
+        sums = arena.zeros((2, C), x.device)
         L.dtm_bn_bwd_reduce(_lib.ptr(dy), _lib.ptr(x), _lib.ptr(y), _lib.ptr(ss), _lib.ptr(sums), M, C, mask_mode, s)
         dx = torch.empty_like(x)
         gout = torch.empty_like(x) if ctx.has_res else None

@@ -3,7 +3,7 @@
 median ms/step per variant; one device, one process: MI355X_MICROARCH 'DVFS give-back' / rule 24).
 
 VARIANTS="base=;noW=wtile:-3;noT=tile:-3;fused=prologue:fused" python tools/ab_step.py
-keys: tile (conv_nt tile id), w8 (0/1: the 8-wave 256x256 conv tile in the shape policy), kwide (0/1: 64-channel tiles for K % 128 <= 64), few (0/1: streaming few-row slab reduction), bnout (0/1: block-output BN backward in the consuming dgrad's epilogue), bnst (0/1: also for stride-2 unit outputs), b1x1 (0/1: one-pass 1x1 conv+BN backward), stemw (0/1: stem BN backward in the wgrad operand staging), sact (0/1: streaming 1x1 kernel for act dgrads), pcom (0/1: Inception pool branches as conv -> pool -> BN), sbwd (0/1: HIP backward of the pooled-BN statistics), catm (0/1: one-launch multi-part concat BN-apply), dec (0/1: stride-decomposed strided dgrads), dgrp (0/1: their parity classes as one grouped launch), k32 (0/1: 256x32 tile for <=32-channel spatial convs), cpt (16-B chunks per thread of the BN-stream grids), pol2 (0/1: v2 conv tile-policy rules), m32 (0/1: 32x32x16-MFMA forms of the LDS-DMA conv tiles), sstr (0/1/2: the stem forward as a persistent stream, 3- / 2-slot ring), wgs (0/1: conv+BN weight gradients on a side stream), scu (percent of the CUs the side-stream wgrads size their split-K grid for), prio (0/1: eager step on a high-priority stream), dir3 (0/1: direct 3x3 kernel for C in {32, 64}), wwide (0/1/2: 64x256 register-staged wgrad tile for K <= 64, Kg > 128: never / always / BN-fused (stem) only), watom (max split count of the fp32-atomic split-K weight gradients; 0 = slabs + reduce), atile (tile id of the dgrads with a fused
+keys: tile (conv_nt tile id), w8 (0/1: the 8-wave 256x256 conv tile in the shape policy), kwide (0/1: 64-channel tiles for K % 128 <= 64), few (0/1: streaming few-row slab reduction), bnout (0/1: block-output BN backward in the consuming dgrad's epilogue), bnst (0/1: also for stride-2 unit outputs), b1x1 (0/1: one-pass 1x1 conv+BN backward), stemw (0/1: stem BN backward in the wgrad operand staging), sact (0/1: streaming 1x1 kernel for act dgrads), pcom (0/1: Inception pool branches as conv -> pool -> BN), sbwd (0/1: HIP backward of the pooled-BN statistics), catm (0/1: one-launch multi-part concat BN-apply), dec (0/1: stride-decomposed strided dgrads), dgrp (0/1: their parity classes as one grouped launch), wp64 (0/1/2: pipelined 64x128 wgrad tile for half-empty last 128-row tiles / also 33..64 outputs), k32 (0/1: 256x32 tile for <=32-channel spatial convs), cpt (16-B chunks per thread of the BN-stream grids), pol2 (0/1: v2 conv tile-policy rules), m32 (0/1: 32x32x16-MFMA forms of the LDS-DMA conv tiles), sstr (0/1/2: the stem forward as a persistent stream, 3- / 2-slot ring), wgs (0/1: conv+BN weight gradients on a side stream), scu (percent of the CUs the side-stream wgrads size their split-K grid for), wcu / swc (the same for the main-stream / stem wgrads), prio (0/1: eager step on a high-priority stream), dir3 (0/1: direct 3x3 kernel for C in {32, 64}), wwide (0/1/2: 64x256 register-staged wgrad tile for K <= 64, Kg > 128: never / always / BN-fused (stem) only), watom (max split count of the fp32-atomic split-K weight gradients; 0 = slabs + reduce), atile (tile id of the dgrads with a fused
 activation-backward epilogue, -1 = policy), wtile[:occ] (wgrad tile id / blocks-per-CU target), prologue (DTM_PROLOGUE),
 stem (DTM_STEM: 1 = packed-row stem path), red (target_blocks:max_chunks[:direct_max] of the
 partial-sum reductions; 0 = legacy 256 rows per block; direct_max = largest BN-backward grid that
@@ -46,10 +46,13 @@ def apply(cfg):
     L.dtm_conv_set_stem_stream(int(cfg.get("sstr", "1")))
     _lib.set_side_enabled(cfg.get("wgs", WGS_DEFAULT[0]) == "1")
     _lib.set_side_cu_fraction(float(cfg.get("scu", "75")) / 100.0)
+    _lib.set_wgrad_cu_percent("main", cfg.get("wcu", "100"))
+    _lib.set_wgrad_cu_percent("stem", cfg.get("swc", "100"))
     L.dtm_conv_set_wgrad_atomic(int(cfg.get("watom", os.environ.get("DTM_WGRAD_ATOMIC", "0"))))
     L.dtm_conv_set_wgrad_wide(int(cfg.get("wwide", "0")))
     L.dtm_conv_set_direct3(int(cfg.get("dir3", "1")))
     L.dtm_conv_set_dec_group(int(cfg.get("dgrp", "1")))
+    L.dtm_conv_set_wgrad_p64(int(cfg.get("wp64", "0")))
     _lib.set_priority_enabled(cfg.get("prio", os.environ.get("DTM_PRIORITY_STREAM", "0")) == "1")
     sc = cfg.get("sc", "5:4096").split(":")
     L.dtm_set_sc_policy(int(sc[0]), int(sc[1]))
@@ -83,35 +86,20 @@ def main():
     kw = {"fc_conv_padding": "SAME"} if model == "vgg_16" else {}  # (bench.py's CIFAR geometry)
     net = nets_factory.build(model, num_classes=ncls, **kw).to(dev)
     B = B or B0
-    # GRAPH=1: every variant replays its own captured hipGraph step (captured on the variant's first step;
-    # the knobs are baked in at capture; captures are single-stream, ops/_lib.py side_stream)
-    graph = os.environ.get("GRAPH", "0") == "1"
-    step = TrainStep(net, optimizer=opt, lr=0.01, momentum=0.9, use_graph=graph, **extra)
-    graphs = {}
-
-    def select(n):
-        if graph:
-            step._graph, step._static_loss = graphs.get(n, (None, None))
-            if step._graph is None:
-                step._eager_steps = 0  # eager warm-up under this variant first (its scratch grows outside capture)
-
-    def keep(n):
-        if graph and n not in graphs and step._graph is not None:
-            graphs[n] = (step._graph, step._static_loss)
+    # (eager steps only: captured hipGraphs of several variants in one process hold raw pointers into scratch
+    # that a later variant's eager warm-up may reallocate - two such runs faulted, profiles/ab/README.md)
+    step = TrainStep(net, optimizer=opt, lr=0.01, momentum=0.9, **extra)
     x = torch.randn(B, S, S, 1 if model == "lenet" else 3, device=dev).to(torch.bfloat16)
     y = torch.randint(0, ncls, (B,), device=dev)
     res = {n: [] for n, _ in variants}
     for n, cfg in variants:  # warm every variant (workspace growth, first-touch)
         apply(cfg)
-        select(n)
-        for _ in range(2 + (2 if graph else 0)):
+        for _ in range(2):
             step(x, y)
-            keep(n)
     torch.cuda.synchronize()
     for r in range(rounds):
         for n, cfg in variants:
             apply(cfg)
-            select(n)
             step(x, y)
             torch.cuda.synchronize()
             t = time.perf_counter()
