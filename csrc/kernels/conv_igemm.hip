@@ -2641,8 +2641,14 @@ struct WgradBN {
   float *dgamma, *dbeta;
 };
 
+struct WgradDst {  // row-split destinations of one wgrad: rows [r0, r0 + rows) of dW go to dw (ops/fused.py siblings)
+  float* const* dw;
+  const int* rows;
+  int n;
+};
 static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float* in_scale, const float* in_shift,
-                           const ConvDesc* d, int num_cus, const WgradBN* bn, void* stream);
+                           const ConvDesc* d, int num_cus, const WgradBN* bn, void* stream,
+                           const WgradDst* dst = nullptr);
 
 DTM_API int dtm_conv_wgrad(const void* x, const void* dy, float* dw, const float* in_scale,
                            const float* in_shift, const ConvDesc* d, int num_cus, void* stream) {
@@ -2659,8 +2665,20 @@ DTM_API int dtm_conv_wgrad_bnbwd(const void* x, const void* g, const void* y, co
   return conv_wgrad_impl(x, g, dw, nullptr, nullptr, d, num_cus, &bn, stream);
 }
 
+// dW of several convs that read the same input, from one wgrad over their output gradients laid side by side
+// (dy [M][sum K_i]): the split-K slabs' row ranges are reduced into each conv's own dW (n <= 8)
+DTM_API int dtm_conv_wgrad_multi(const void* x, const void* dy, float* const* dws, const int* rows, int n,
+                                 const ConvDesc* d, int num_cus, void* stream) {
+  if (n < 1 || n > 8) return -1;
+  int tot = 0;
+  for (int i = 0; i < n; ++i) tot += rows[i];
+  if (tot != d->K) return -1;
+  WgradDst dst{dws, rows, n};
+  return conv_wgrad_impl(x, dy, dws[0], nullptr, nullptr, d, num_cus, nullptr, stream, &dst);
+}
+
 static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float* in_scale, const float* in_shift,
-                           const ConvDesc* d, int num_cus, const WgradBN* bn, void* stream) {
+                           const ConvDesc* d, int num_cus, const WgradBN* bn, void* stream, const WgradDst* dst) {
   if (!dtm_device_ok()) return -9;
   if (d->C % 8 || d->K % 8) return -1;
   ConvWgradArgs a;
@@ -2728,7 +2746,7 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
     const char* e = getenv("DTM_WGRAD_ATOMIC");
     g_wgrad_atomic = e ? atoi(e) : 0;
   }
-  a.atomic = !dtm_get_deterministic() && splits <= g_wgrad_atomic;
+  a.atomic = !dtm_get_deterministic() && splits <= g_wgrad_atomic && !dst;
   float* ws = dw;
   if (!a.atomic) {
     ws = dtm_ws_get_stream((size_t)splits * a.K * a.Kg, (hipStream_t)stream);
@@ -2750,7 +2768,13 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   else if (wt == 6) launch_wgrad<32, 128, 16, 64>(a, (int)splits, (hipStream_t)stream);
   else launch_wgrad<128, 128, 64, 64>(a, (int)splits, (hipStream_t)stream);
   // dW += sum over the split slabs (every slab element is written: tiles cover [K][Kg] exactly)
-  if (!a.atomic) dtm_reduce_rows(ws, (int)splits, a.K * a.Kg, a.K * a.Kg, dw, (hipStream_t)stream);
+  if (dst) {
+    for (int i = 0, r0 = 0; i < dst->n; r0 += dst->rows[i], ++i)
+      dtm_reduce_rows(ws + (size_t)r0 * a.Kg, (int)splits, dst->rows[i] * a.Kg, a.K * a.Kg, dst->dw[i],
+                      (hipStream_t)stream);
+  } else if (!a.atomic) {
+    dtm_reduce_rows(ws, (int)splits, a.K * a.Kg, a.K * a.Kg, dw, (hipStream_t)stream);
+  }
   return 0;
 }
 

@@ -190,7 +190,7 @@ __global__ __launch_bounds__(256) void stats_combine_fin_kernel(const bf16_t* __
                                                                 const float* __restrict__ gamma, float count,
                                                                 float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                                 bf16_t* __restrict__ out, int M, int C, int prescale,
-                                                                int rpb) {
+                                                                int rpb, int ldo) {
   __shared__ float s_ab[2][2048];
   const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t % cols) * 8, lr0 = t / cols;
   for (int c = t; c < C; c += 256) {  // one channel per thread, shared through LDS
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(256) void stats_combine_fin_kernel(const bf16_t* __
       up8(vd[u], d); up8(vx[u], xv);
 #pragma unroll
       for (int e = 0; e < 8; ++e) d[e] = fmaf(d[e], sc[e], a[e] + b[e] * xv[e]);
-      st16<NTS>(out + (size_t)rr * C + c0, pk8(d));
+      st16<NTS>(out + (size_t)rr * ldo + c0, pk8(d));  // (ldo > C: a column slice of a wider buffer)
     }
   }
 }
@@ -512,16 +512,27 @@ DTM_API void dtm_bn_finalize_bwd(const float* dss, const float* ss, const float*
                      dstats, dgamma, dbeta, C, count);
 }
 
+DTM_API int dtm_stats_combine_fin_ld(const void* dy, const void* x, const float* dss, const float* ss,
+                                     const float* gamma, float count, float* dgamma, float* dbeta, void* out, long M, int C,
+                                     int prescale, int ldo, void* stream);
 DTM_API int dtm_stats_combine_fin(const void* dy, const void* x, const float* dss, const float* ss, const float* gamma,
                                   float count, float* dgamma, float* dbeta, void* out, long M, int C, int prescale,
                                   void* stream) {
-  if (!shape_ok(M, C) || C > 2048) return -1;
+  return dtm_stats_combine_fin_ld(dy, x, dss, ss, gamma, count, dgamma, dbeta, out, M, C, prescale, C, stream);
+}
+
+// out rows of ldo elements (ldo >= C, ldo % 8 == 0): the combined gradient of one conv written into its column
+// slice of a buffer shared with sibling convs (one merged dgrad / wgrad over all of them, ops/fused.py)
+DTM_API int dtm_stats_combine_fin_ld(const void* dy, const void* x, const float* dss, const float* ss,
+                                     const float* gamma, float count, float* dgamma, float* dbeta, void* out, long M, int C,
+                                     int prescale, int ldo, void* stream) {
+  if (!shape_ok(M, C) || C > 2048 || ldo < C || ldo % 8) return -1;
   int blocks, rpb;
   grid2(M, C, &blocks, &rpb, g_sc_cap);
 #define SCF_LAUNCH(U, NT, NTS)                                                                                    \
   hipLaunchKernelGGL((stats_combine_fin_kernel<U, NT, NTS>), dim3(blocks), dim3(256), 0, (hipStream_t)stream,          \
                      (const bf16_t*)dy, (const bf16_t*)x, dss, ss, gamma, count, dgamma, dbeta, (bf16_t*)out, (int)M, \
-                     C, prescale, rpb)
+                     C, prescale, rpb, ldo)
   switch (g_sc_var) {
     case 1: SCF_LAUNCH(8, false, false); break;
     case 2: SCF_LAUNCH(4, true, true); break;

@@ -181,8 +181,11 @@ class InceptionV3Slim(Layer):
                 if end_points is not None:
                     end_points["aux_logits"] = aux
                 continue
-            # branch outputs written straight into their channel slices (zero-copy concat)
-            net = concat_channels([p for b in branches for p in self._run(b, net, training)])
+            # branch outputs written straight into their channel slices (zero-copy concat); the branches' first
+            # 1x1 conv+BNs on the block input share one backward (ops.fused.sibling_group)
+            with _fused.sibling_group(net, training):
+                parts = [p for b in branches for p in self._run(b, net, training)]
+            net = concat_channels(parts)
             if end_points is not None:
                 end_points[name] = net
         k = net.shape[1]

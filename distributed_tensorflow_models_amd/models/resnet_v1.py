@@ -14,6 +14,7 @@ resnet_v1_50/block1/unit_1/bottleneck_v1/{shortcut,conv1,conv2,conv3}/..., resne
 import torch
 
 from ..ops import nn as F
+from ..ops import fused
 from ..ops.lazy import Subsampled, as_tensor
 from .layers import Conv2d, Layer, _join, apply_activation, fused_enabled
 
@@ -64,9 +65,14 @@ class BottleneckV1(Layer):
         self.conv3 = Conv2d(_join(scope, "conv3"), depth_bottleneck, depth, 1, 1, "SAME", None, bn, None, wd, init)
 
     def forward(self, x, training=True, end_points=None):
-        sc = self.shortcut(x, training) if self.shortcut is not None else \
-            subsample(x, self.stride, lazy=self.conv3.bn is not None and end_points is None)
-        r1 = self.conv1(x, training)
+        if self.shortcut is not None:
+            # projection shortcut and conv1: sibling 1x1 conv+BNs of x with one merged backward (ops.fused)
+            with fused.sibling_group(x, training and end_points is None):
+                sc = self.shortcut(x, training)
+                r1 = self.conv1(x, training)
+        else:
+            sc = subsample(x, self.stride, lazy=self.conv3.bn is not None and end_points is None)
+            r1 = self.conv1(x, training)
         r2 = self.conv2(r1, training)
         if end_points is not None:
             # slim collects every conv output (outputs_collections) plus the unit output

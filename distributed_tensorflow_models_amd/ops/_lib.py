@@ -49,6 +49,7 @@ _SIGS = {
     "dtm_conv1x1_bnbwd": (_I, [_P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _L, _I, _I, _P]),
     "dtm_conv_wgrad_bnbwd": (_I, [_P, _P, _P, _P, _P, _P, _F, _P, _P, _P, ctypes.POINTER(ConvDesc), _I, _P]),
     "dtm_conv_wgrad": (_I, [_P, _P, _P, _P, _P, ctypes.POINTER(ConvDesc), _I, _P]),
+    "dtm_conv_wgrad_multi": (_I, [_P, _P, _P, _P, _I, ctypes.POINTER(ConvDesc), _I, _P]),
     "dtm_conv_set_policy2": (None, [_I]),
     "dtm_set_grid_cpt": (None, [_I]),
     "dtm_conv_set_k32": (None, [_I]),
@@ -80,6 +81,7 @@ _SIGS = {
     "dtm_conv_set_wgrad_tile": (None, [_I, _I]),
     "dtm_conv_fwd_bn": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _I, _I, ctypes.POINTER(ConvDesc), _P]),
     "dtm_stats_combine_fin": (_I, [_P, _P, _P, _P, _P, _F, _P, _P, _P, _L, _I, _I, _P]),
+    "dtm_stats_combine_fin_ld": (_I, [_P, _P, _P, _P, _P, _F, _P, _P, _P, _L, _I, _I, _I, _P]),
     "dtm_bn_apply_res_strided": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "dtm_bn_bwd_reduce": (None, [_P, _P, _P, _P, _P, _L, _I, _I, _P]),
     "dtm_bn_bwd_apply": (None, [_P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _P]),

@@ -11,6 +11,7 @@ Each piece is an autograd Function with a hand-written backward kernel, so gradi
 exactly to TF's fused BatchNorm gradient (tests/test_fused_gpu.py checks it against torch).
 """
 import ctypes
+import os
 
 import torch
 
@@ -156,11 +157,13 @@ def _full_window(g):
     return g.P == 1 and g.Q == 1 and g.pad_h == 0 and g.pad_w == 0 and g.R == g.H and g.S == g.W
 
 
-def _full_window_dgrad_act(g, dy, w, x_raw, in_ss, d_in, dx, unscaled):
+def _full_window_dgrad_act(g, dy, w, x_raw, in_ss, d_in, dx, unscaled, add_src=None):
     """dgrad of a full-window conv (plain GEMM, hipBLASLt) with the input's BN+ReLU backward folded as the
     act epilogue does it: g = dgrad * [x_raw*scale + shift > 0]; d_in[0:2] = (sum g*x_raw, sum g) per channel;
     dx = g (unscaled producer) or g*scale."""
     gm = torch.mm(dy.reshape(g.N, g.K), weight_bf16(w).reshape(g.K, -1)).reshape(g.N, -1, g.C).float()
+    if add_src is not None:  # (another conv consumer's masked gradient of the same activation)
+        gm = gm + add_src.reshape(g.N, -1, g.C).float()
     xr = x_raw.reshape(g.N, -1, g.C).float()
     sc, sh = in_ss[0], in_ss[1]
     gm = gm * ((xr * sc + sh) > 0)
@@ -177,7 +180,7 @@ class _ConvBNFn(torch.autograd.Function):
     Backward: the finalize backward is folded into the stats-combine pass (dgamma / dbeta included)."""
 
     @staticmethod
-    def forward(ctx, x, in_ss, w, gamma, beta, geom, bn, slot=None, in_unscaled=False, x_mat=None):
+    def forward(ctx, x, in_ss, w, gamma, beta, geom, bn, slot=None, in_unscaled=False, x_mat=None, grp=None):
         L = _lib.lib()
         s = _lib.stream_ptr()
         w16 = weight_bf16(w)
@@ -207,6 +210,7 @@ class _ConvBNFn(torch.autograd.Function):
                                   ctypes.byref(d), s), "conv_fwd")
         ctx.geom = geom
         ctx.slot = slot
+        ctx.grp = grp  # (_SiblingGroup, member index): backward merged with the sibling 1x1 convs of x
         ctx.in_unscaled = bool(in_unscaled)
         # the input is a block output whose BN-apply backward this conv's dgrad can absorb (if it turns
         # out to be the input's last consumer)
@@ -228,6 +232,10 @@ class _ConvBNFn(torch.autograd.Function):
         M_out = g.N * g.P * g.Q
         dy = dy.contiguous()
         dgamma = dbeta = None
+        if ctx.grp is not None and ss is not None:
+            if dss is None:  # (no statistics gradient reached this member: a zero one keeps the group complete)
+                dss = torch.zeros((4, g.K), device=dy.device, dtype=torch.float32)
+            return _SiblingGroup.backward_member(ctx, dy, dss, x, w, y, ss, gamma, beta)
         if ss is not None and dss is not None and _bwd1x1_ok(ctx, g):
             out = _ConvBNFn._backward_1x1_fused(ctx, dy, dss, x_raw, in_ss, w, y, ss, gamma, beta)
             if out is not None:
@@ -279,12 +287,14 @@ class _ConvBNFn(torch.autograd.Function):
             dx = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
             if in_ss is not None and _full_window(g):
                 d_in = arena.zeros((4, g.C), dy.device)
-                _full_window_dgrad_act(g, dy, w, x_raw, in_ss, d_in, dx, ctx.in_unscaled)
+                _full_window_dgrad_act(g, dy, w, x_raw, in_ss, d_in, dx, ctx.in_unscaled, add_src)
             elif in_ss is not None:
                 # BN+ReLU of the input was fused into the forward prologue: mask, scale and the BN
-                # parameter-gradient sums are done in the dgrad epilogue
+                # parameter-gradient sums are done in the dgrad epilogue (+ the other conv consumers' masked
+                # gradient of the same activation, added before the mask: act hand-off, see conv_bn)
                 d_in = arena.zeros((4, g.C), dy.device)
-                _check(L.dtm_conv_dgrad_ex(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), None, 1,
+                _check(L.dtm_conv_dgrad_ex(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d),
+                                           _lib.ptr(add_src) if add_src is not None else None, 1,
                                            _lib.ptr(x_raw), _lib.ptr(in_ss), _lib.ptr(d_in), int(ctx.in_unscaled), s),
                        "conv_dgrad_act")
             else:
@@ -312,6 +322,11 @@ class _ConvBNFn(torch.autograd.Function):
                 if not last:
                     ctx.slot.buf, ctx.slot.stride = dx, 1
                     dx = None
+            if in_ss is not None and not last:
+                # act hand-off (conv_bn): the cumulative masked gradient waits for the next conv consumer, whose
+                # BN-gradient sums cover every consumer
+                ctx.slot.buf, ctx.slot.stride = dx, 1
+                dx = d_in = None
             d.dec = 0
         if wg_side:
             dw = None
@@ -328,7 +343,7 @@ class _ConvBNFn(torch.autograd.Function):
                 dw = target
         else:
             dw = None
-        return dx, d_in, dw, dgamma, dbeta, None, None, None, None, None
+        return dx, d_in, dw, dgamma, dbeta, None, None, None, None, None, None
 
 
     @staticmethod
@@ -340,6 +355,8 @@ class _ConvBNFn(torch.autograd.Function):
         g = ctx.geom
         act = in_ss is not None
         add_src = None
+        if act and ctx.slot is not None and (ctx.slot.pending > 1 or ctx.slot.buf is not None):
+            return None  # (an activation shared by several conv consumers: the dgrad-epilogue hand-off path)
         if not act:
             sl = ctx.slot
             if ctx.bnout is not None or (sl is not None and sl.buf is not None and sl.stride != 1):
@@ -376,7 +393,7 @@ class _ConvBNFn(torch.autograd.Function):
         for p, m in ((gamma, gmg), (beta, bmg), (w, mg)):
             if m is not None:
                 _notify(p)
-        return dx, d_in, (None if mg is not None else target), dgamma, dbeta, None, None, None, None, None
+        return dx, d_in, (None if mg is not None else target), dgamma, dbeta, None, None, None, None, None, None
 
 
 BWD1X1_FUSED = [0]  # count of 1x1 conv+BN backwards done by the one-pass kernel (tests / diagnostics)
@@ -693,6 +710,141 @@ def bn_inference_ss(bn):
     return torch.stack([scale, shift, bn.moving_mean.expand_as(scale), rstd.expand_as(scale)]).contiguous()
 
 
+class _SiblingGroup:
+    """1x1 stride-1 conv+BN siblings on one plain input - the first convs of an Inception mixed block's branches
+    (reference inception/slim/inception_model.py:67-320: branch1x1 / branch5x5 / branch3x3dbl / ... all start
+    with a 1x1 conv of the block input).  Forward is unchanged (one conv each).  In backward every member writes
+    its BN-combined output gradient into its column slice of ONE [M][sum K] buffer (stats_combine_fin with a row
+    pitch); the member whose backward runs last issues ONE dgrad with the members' transposed weights laid side
+    by side ([C][sum K]) and ONE weight gradient whose split-K slabs are reduced row range by row range into
+    each member's dW (dtm_conv_wgrad_multi).  Instead of one dgrad per member - each re-reading and
+    re-writing the whole block-input gradient through the _GradSlot hand-off - and one wgrad per member.
+    The group is one consumer of the input's _GradSlot."""
+    __slots__ = ("x", "members", "ktot", "slot", "buf", "done", "bnout")
+
+    def __init__(self, x):
+        self.x, self.members, self.ktot, self.slot, self.buf, self.done = x, [], 0, None, None, 0
+        # x is a block output whose BN-apply backward the merged dgrad's epilogue can absorb (ResNet unit 1)
+        self.bnout = getattr(x, "_dtm_bnout", None)
+
+    def join(self, w, geom):
+        if self.slot is None:
+            self.slot = _slot_register(self.x)
+        self.members.append((w, geom.K, self.ktot))
+        self.ktot += geom.K
+        return (self, len(self.members) - 1)
+
+    @staticmethod
+    def backward_member(ctx, dy, dss, x, w, y, ss, gamma, beta):
+        grp, idx = ctx.grp
+        g = ctx.geom
+        L = _lib.lib()
+        s = _lib.stream_ptr()
+        M = g.N * g.P * g.Q
+        if grp.buf is None:
+            grp.buf = torch.empty((M, grp.ktot), device=dy.device, dtype=torch.bfloat16)
+        off = grp.members[idx][2]
+        gmg = getattr(gamma, "main_grad", None) if gamma is not None else None
+        bmg = getattr(beta, "main_grad", None) if beta is not None else None
+        dgamma = torch.zeros(g.K, device=dy.device) if (gamma is not None and gmg is None) else None
+        dbeta = torch.zeros(g.K, device=dy.device) if (beta is not None and bmg is None) else None
+        _check(L.dtm_stats_combine_fin_ld(_lib.ptr(dy.contiguous()), _lib.ptr(y), _lib.ptr(dss.contiguous()),
+                                          _lib.ptr(ss), _lib.ptr(gamma), ctx.count,
+                                          _lib.ptr(gmg if gmg is not None else dgamma),
+                                          _lib.ptr(bmg if bmg is not None else dbeta),
+                                          ctypes.c_void_p(grp.buf.data_ptr() + 2 * off), M, g.K, 1, grp.ktot, s),
+               "stats_combine_fin(sibling)")
+        for p, m in ((gamma, gmg), (beta, bmg)):
+            if m is not None:
+                _notify(p)
+        grp.done += 1
+        if grp.done < len(grp.members):
+            return None, None, None, dgamma, dbeta, None, None, None, None, None, None
+        # the last member: one dgrad and one wgrad over every member's output gradient
+        buf, n = grp.buf, len(grp.members)
+        d = _lib.ConvDesc(g.N, g.H, g.W, g.C, grp.ktot, 1, 1, g.P, g.Q, 1, 0, 0, 0)
+        mgs = [getattr(m[0], "main_grad", None) for m in grp.members]
+        dws = [mg if mg is not None else torch.zeros(m[0].shape, device=dy.device, dtype=torch.float32)
+               for mg, m in zip(mgs, grp.members)]
+        ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in dws])
+        rows = (ctypes.c_int * n)(*[m[1] for m in grp.members])
+        st = _lib.side_fork(x, buf)
+
+        def wgrad(stream, cus):
+            _check(L.dtm_conv_wgrad_multi(_lib.ptr(x), _lib.ptr(buf), ptrs, rows, n, ctypes.byref(d), cus, stream),
+                   "conv_wgrad_multi")
+            # (the bucket all-reduces these notifications may launch are issued from the stream that wrote dW)
+            for m, mg in zip(grp.members, mgs):
+                if mg is not None:
+                    _notify(m[0])
+        if st is not None:
+            with torch.cuda.stream(st):
+                wgrad(_lib.stream_ptr(), _lib.side_cus())
+        else:
+            wgrad(s, _lib.wgrad_cus())
+        wts = [weight_flipped(m[0], m[1], 1, 1, g.C) for m in grp.members]
+        wt = wts[0] if n == 1 else torch.cat([t.view(g.C, m[1]) for t, m in zip(wts, grp.members)], dim=1)
+        last, add_src, add_stride = _slot_take(grp.slot)
+        use_add = add_src is not None
+        dx = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
+        info = grp.bnout
+        if last and info is not None and info.sums is None and tuple(info.x.shape) == tuple(dx.shape):
+            # last consumer of a block output: its BN-apply backward in this dgrad's epilogue (as _ConvBNFn)
+            sums = arena.zeros((8 if info.r is not None else 4, g.C), dy.device)
+            _check(L.dtm_conv_dgrad_bnout(_lib.ptr(buf), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d),
+                                          _lib.ptr(add_src) if use_add else None, add_stride if use_add else 1,
+                                          _lib.ptr(info.mask), _lib.ptr(info.x), _lib.ptr(info.r), _lib.ptr(sums), s),
+                   "conv_dgrad_bnout(sibling)")
+            info.sums, info.g = sums, dx
+            BNOUT_FUSED[0] += 1
+        else:
+            _check(L.dtm_conv_dgrad_ex(_lib.ptr(buf), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d),
+                                       _lib.ptr(add_src) if use_add else None, add_stride if use_add else 1,
+                                       None, None, None, 0, s), "conv_dgrad(sibling)")
+        if not last:
+            grp.slot.buf, grp.slot.stride = dx, 1
+            dx = None
+        grp.buf = None
+        SIBLING_MERGED[0] += 1
+        # member weights whose gradient has no main_grad: hand the fresh tensors back through this member only
+        dw = None if mgs[idx] is not None else dws[idx]
+        return dx, None, dw, dgamma, dbeta, None, None, None, None, None, None
+
+
+SIBLING_MERGED = [0]  # merged sibling backwards (tests / diagnostics)
+_SIBLINGS = [None]
+
+
+class sibling_group:
+    """Context: the eligible 1x1 conv+BN calls on ``x`` inside it share one backward (see _SiblingGroup).
+    Knob DTM_SIBLING_GROUP (default off until its whole-step A/B)."""
+
+    def __init__(self, x, training=True):
+        import os
+        on = (training and torch.is_grad_enabled() and isinstance(x, torch.Tensor) and x.is_cuda and
+              x.requires_grad and os.environ.get("DTM_SIBLING_GROUP", "0") != "0")
+        self.grp = _SiblingGroup(x) if on else None
+
+    def __enter__(self):
+        self.prev, _SIBLINGS[0] = _SIBLINGS[0], self.grp
+        return self.grp
+
+    def __exit__(self, *exc):
+        _SIBLINGS[0] = self.prev
+        return False
+
+
+def _sibling_join(xb, w, g, training, bn):
+    grp = _SIBLINGS[0]
+    if (grp is None or not training or bn is None or xb is not grp.x or g.R != 1 or g.S != 1 or g.stride != 1 or
+            g.pad_h or g.pad_w or g.P != g.H or g.Q != g.W or g.K % 8 or g.C % 8 or
+            getattr(w, "main_grad", None) is None):
+        return None
+    if g.K == 256 and g.C == 64 and os.environ.get("DTM_BWD1X1_FUSE", "1") != "0":
+        return None  # (the ResNet stage-1 64 -> 256 projection keeps its one-pass backward, dtm_conv1x1_bnbwd)
+    return grp.join(w, g)
+
+
 def _prologue_mode(x_shape, w_shape, stride):
     """How a conv consumes its input's BatchNorm-apply + ReLU (a LazyBN):
 
@@ -728,6 +880,7 @@ def _prologue_mode(x_shape, w_shape, stride):
 
 def conv_bn(x, w, bn, stride, padding, training, relu):
     """Fused conv -> BatchNorm; returns a LazyBN.  x: tensor or LazyBN(relu=True) (prologue-fused)."""
+    act_slot = None
     in_ss = None
     in_unscaled = False
     x_mat = None
@@ -738,6 +891,15 @@ def conv_bn(x, w, bn, stride, padding, training, relu):
         else:
             lz = x
             in_ss, in_unscaled, x = x.ss, x.unscaled, x.raw
+            if (training and lz.unscaled and torch.is_grad_enabled() and x.requires_grad and x.is_cuda and
+                    os.environ.get("DTM_ACT_HANDOFF", "0") != "0"):
+                # conv consumers of one activation hand the (unscaled, masked) input gradient on: the last one's
+                # act epilogue adds the others' before its mask and sums (Inception's split 1x3 / 3x1 pairs), so
+                # autograd adds neither the gradients nor the BN-gradient sums
+                if lz.aslot is None:
+                    lz.aslot = _GradSlot(x.shape)
+                lz.aslot.pending += 1
+                act_slot = lz.aslot
             if mode == "mat":
                 # one materialisation per LazyBN, whatever the number of conv consumers (Inception's split
                 # 1x3 / 3x1 pairs read the same activation)
@@ -761,11 +923,13 @@ def conv_bn(x, w, bn, stride, padding, training, relu):
         w = _PadChannels.apply(w, cp)
         g = conv_geom(tuple(x.shape), tuple(w.shape), stride, padding)
     xb = x.to(torch.bfloat16).contiguous()
-    # a shared (materialised) input: hand the gradient between its consumers (see _GradSlot)
-    slot = _slot_register(xb) if (xb is x and in_ss is None) else None
+    grp = _sibling_join(xb, w, g, training, bn) if (xb is x and in_ss is None) else None
+    # a shared (materialised) input: hand the gradient between its consumers (see _GradSlot); sibling-group
+    # members share the group's registration
+    slot = _slot_register(xb) if (xb is x and in_ss is None and grp is None) else act_slot
     x = xb
     if training:
-        y, ss = _ConvBNFn.apply(x, in_ss, w, bn.gamma, bn.beta, g, bn, slot, in_unscaled, x_mat)
+        y, ss = _ConvBNFn.apply(x, in_ss, w, bn.gamma, bn.beta, g, bn, slot, in_unscaled, x_mat, grp)
     else:
         y = _ConvBNFn.apply(x, in_ss, w, None, None, g, None, slot, in_unscaled)
         ss = bn_inference_ss(bn)

@@ -9,11 +9,12 @@ class LazyBN:
     gradient of the normalised pre-activation g rather than g*scale -- one elementwise multiply and, at
     a ResNet unit output, one whole gradient tensor fewer."""
 
-    __slots__ = ("raw", "ss", "relu", "unscaled", "mat")
+    __slots__ = ("raw", "ss", "relu", "unscaled", "mat", "aslot")
 
     def __init__(self, raw, ss, relu, unscaled=False):
         self.raw, self.ss, self.relu, self.unscaled = raw, ss, relu, unscaled
         self.mat = None  # relu(raw*scale+shift) materialised for conv consumers (ops.fused 'mat'), shared by all
+        self.aslot = None  # gradient hand-off between the conv consumers of this activation (ops.fused)
 
     @property
     def shape(self):

@@ -434,6 +434,88 @@ def test_wgrad_side_stream_matches_main_stream():
     assert _rel(side, ref0) <= max(10 * noise, 1e-5), (_rel(side, ref0), noise)
 
 
+@pytest.mark.parametrize("side", [False, True])
+@pytest.mark.parametrize("model,S,B,merged,last_unit,untouched",
+                         [("inception_v3_slim_old", 299, 2, 11, "mixed_8x8x2048b", "logits"),
+                          ("resnet_v1_50", 64, 8, 4, "units.13.", "units.15.")])
+def test_sibling_1x1_merged_backward(monkeypatch, side, model, S, B, merged, last_unit, untouched):
+    """Sibling 1x1 conv+BNs on one input - the first convs of an Inception-v3 mixed block's branches, a ResNet
+    unit's projection shortcut and conv1 - share one backward (column slices of one combined-gradient buffer,
+    one dgrad over the concatenated weights with the block-output BN-apply backward in its epilogue for ResNet,
+    one wgrad whose split-K slabs are reduced into each member's dW), main stream and side-stream wgrads.
+    Per parameter against the per-conv backward: the parameters before any group in backward order match to
+    run-to-run noise, the last group's own gradients (its members' dW: the same combined gradient, another
+    split-K order) tightly; further towards the stem the merged dgrad's single bf16 rounding of the summed input
+    gradient (the per-conv path rounds the stash) drifts the usual ~0.15 % per unit."""
+    from distributed_tensorflow_models_amd.engine import TrainStep
+    from distributed_tensorflow_models_amd.models import nets_factory
+    from distributed_tensorflow_models_amd.ops import _lib
+    from distributed_tensorflow_models_amd.ops import elementwise as ew
+    monkeypatch.setattr(ew, "advance_seed_offset", lambda device: None)  # the same dropout mask in both runs
+    torch.manual_seed(0)
+    net = nets_factory.build(model, num_classes=11).to(DEV)
+    if model == "resnet_v1_50":
+        step = TrainStep(net, optimizer="momentum", lr=0.0, momentum=0.9, wgrad_stream=side)
+    else:
+        step = TrainStep(net, optimizer="rmsprop", lr=0.0, rho=0.9, epsilon=1.0, label_smoothing=0.1, aux_weight=0.4,
+                         wgrad_stream=side)
+    x = torch.randn(B, S, S, 3, device=DEV).to(torch.bfloat16)
+    y = torch.randint(0, 11, (B,), device=DEV)
+    grads = {}
+    try:
+        for grp in ("0", "1"):
+            monkeypatch.setenv("DTM_SIBLING_GROUP", grp)
+            n0 = fused.SIBLING_MERGED[0]
+            step._forward_backward(x, y)
+            torch.cuda.synchronize()
+            grads[grp] = {k: p.main_grad.detach().float().clone() for k, p in net.named_parameters()
+                          if getattr(p, "main_grad", None) is not None}
+            assert fused.SIBLING_MERGED[0] - n0 == (merged if grp == "1" else 0)
+    finally:
+        _lib.set_side_enabled(False)
+    errs = {k: _rel(grads["1"][k], grads["0"][k]) for k in grads["0"]}
+    assert all(torch.isfinite(v).all() for v in grads["1"].values())
+    pre = [v for k, v in errs.items() if untouched in k]
+    own = [v for k, v in errs.items() if last_unit in k]
+    assert pre and own
+    assert max(pre) < 1e-3, (untouched, max(pre))
+    assert max(own) < 1e-2, (last_unit, sorted(((v, k) for k, v in errs.items() if last_unit in k))[-3:])
+    vals = sorted(errs.values())
+    assert vals[len(vals) // 2] < 1.5e-2 and vals[-1] < 8e-2, sorted(((v, k) for k, v in errs.items()))[-5:]
+
+
+def test_act_input_handoff_between_conv_consumers(monkeypatch):
+    """An activation (LazyBN) read by two convs (Inception's split 1x3 / 3x1 pair): the first conv's backward
+    hands its masked input gradient to the second, whose act epilogue adds it before the mask and the
+    BN-gradient sums - same gradients as autograd adding the two consumers' results."""
+    torch.manual_seed(4)
+    C = 64
+    x = torch.randn(4, 8, 8, C, device=DEV).to(torch.bfloat16).float()
+    w1 = (torch.randn(C, 1, 1, C, device=DEV) / C ** 0.5).to(torch.bfloat16).float()
+    wa = (torch.randn(C, 1, 3, C, device=DEV) / (3 * C) ** 0.5).to(torch.bfloat16).float()
+    wb = (torch.randn(C, 3, 1, C, device=DEV) / (3 * C) ** 0.5).to(torch.bfloat16).float()
+    bn1, bna, bnb = _bn(C), _bn(C), _bn(C)
+    ga = gb = None
+    out = {}
+    for on in ("0", "1"):
+        monkeypatch.setenv("DTM_ACT_HANDOFF", on)  # (knob default: off)
+        for p in (bn1.gamma, bn1.beta):
+            p.grad = None
+        xk = x.to(torch.bfloat16).requires_grad_()
+        w1k, wak, wbk = (t.clone().requires_grad_() for t in (w1, wa, wb))
+        l1 = fused.conv_bn(xk, w1k, bn1, 1, "SAME", True, True)
+        ya = fused.conv_bn(l1, wak, bna, 1, "SAME", True, False).materialize()
+        yb = fused.conv_bn(l1, wbk, bnb, 1, "SAME", True, False).materialize()
+        if ga is None:
+            ga, gb = torch.randn_like(ya.float()).to(torch.bfloat16), torch.randn_like(yb.float()).to(torch.bfloat16)
+        torch.autograd.backward([ya, yb], [ga, gb])
+        torch.cuda.synchronize()
+        out[on] = dict(dx=xk.grad.float().clone(), dw1=w1k.grad.float().clone(), dwa=wak.grad.float().clone(),
+                       dg1=bn1.gamma.grad.float().clone(), db1=bn1.beta.grad.float().clone())
+    errs = {k: _rel(out["1"][k], out["0"][k]) for k in out["0"]}
+    assert all(v < 1e-2 for v in errs.values()), errs
+
+
 def test_block_output_bn_backward_in_dgrad_epilogue(monkeypatch):
     """ResNet-50 v1: the block-output BN-apply backward (mask, d(scale)/d(shift) sums, the residual's
     share) runs inside the dgrad epilogue of the conv that consumes the block output last; every
