@@ -232,8 +232,8 @@ class _ConvBNFn(torch.autograd.Function):
         M_out = g.N * g.P * g.Q
         dy = dy.contiguous()
         dgamma = dbeta = None
-        if ctx.grp is not None and ss is not None:
-            if dss is None:  # (no statistics gradient reached this member: a zero one keeps the group complete)
+        if ctx.grp is not None:
+            if ss is not None and dss is None:  # (no statistics gradient reached this member: zero keeps it complete)
                 dss = torch.zeros((4, g.K), device=dy.device, dtype=torch.float32)
             return _SiblingGroup.backward_member(ctx, dy, dss, x, w, y, ss, gamma, beta)
         if ss is not None and dss is not None and _bwd1x1_ok(ctx, g):
@@ -744,19 +744,25 @@ class _SiblingGroup:
         if grp.buf is None:
             grp.buf = torch.empty((M, grp.ktot), device=dy.device, dtype=torch.bfloat16)
         off = grp.members[idx][2]
-        gmg = getattr(gamma, "main_grad", None) if gamma is not None else None
-        bmg = getattr(beta, "main_grad", None) if beta is not None else None
-        dgamma = torch.zeros(g.K, device=dy.device) if (gamma is not None and gmg is None) else None
-        dbeta = torch.zeros(g.K, device=dy.device) if (beta is not None and bmg is None) else None
-        _check(L.dtm_stats_combine_fin_ld(_lib.ptr(dy.contiguous()), _lib.ptr(y), _lib.ptr(dss.contiguous()),
-                                          _lib.ptr(ss), _lib.ptr(gamma), ctx.count,
-                                          _lib.ptr(gmg if gmg is not None else dgamma),
-                                          _lib.ptr(bmg if bmg is not None else dbeta),
-                                          ctypes.c_void_p(grp.buf.data_ptr() + 2 * off), M, g.K, 1, grp.ktot, s),
-               "stats_combine_fin(sibling)")
-        for p, m in ((gamma, gmg), (beta, bmg)):
-            if m is not None:
-                _notify(p)
+        dgamma = dbeta = None
+        if ss is None:
+            # a member without BatchNorm (Inception's commuted pool-branch conv: its gradient comes from the pool's
+            # backward): a strided copy into its column slice
+            grp.buf[:, off:off + g.K].copy_(dy.reshape(M, g.K))
+        else:
+            gmg = getattr(gamma, "main_grad", None) if gamma is not None else None
+            bmg = getattr(beta, "main_grad", None) if beta is not None else None
+            dgamma = torch.zeros(g.K, device=dy.device) if (gamma is not None and gmg is None) else None
+            dbeta = torch.zeros(g.K, device=dy.device) if (beta is not None and bmg is None) else None
+            _check(L.dtm_stats_combine_fin_ld(_lib.ptr(dy.contiguous()), _lib.ptr(y), _lib.ptr(dss.contiguous()),
+                                              _lib.ptr(ss), _lib.ptr(gamma), ctx.count,
+                                              _lib.ptr(gmg if gmg is not None else dgamma),
+                                              _lib.ptr(bmg if bmg is not None else dbeta),
+                                              ctypes.c_void_p(grp.buf.data_ptr() + 2 * off), M, g.K, 1, grp.ktot, s),
+                   "stats_combine_fin(sibling)")
+            for p, m in ((gamma, gmg), (beta, bmg)):
+                if m is not None:
+                    _notify(p)
         grp.done += 1
         if grp.done < len(grp.members):
             return None, None, None, dgamma, dbeta, None, None, None, None, None, None
@@ -817,12 +823,14 @@ _SIBLINGS = [None]
 
 class sibling_group:
     """Context: the eligible 1x1 conv+BN calls on ``x`` inside it share one backward (see _SiblingGroup).
-    Knob DTM_SIBLING_GROUP (default on: Inception-v3 -4.8 %, ResNet-50 -0.24 % step, profiles/ab/r3_ab_sibling_*)."""
+    Knob DTM_SIBLING_GROUP (default off: Inception-v3 -4.8 %, ResNet-50 -0.24 % step on one GPU,
+    profiles/ab/r3_ab_sibling_*, but the 2-rank data-parallel GPU test disagreed with the single-rank result
+    with it on - unresolved; see README Known gaps)."""
 
     def __init__(self, x, training=True):
         import os
         on = (training and torch.is_grad_enabled() and isinstance(x, torch.Tensor) and x.is_cuda and
-              x.requires_grad and os.environ.get("DTM_SIBLING_GROUP", "1") != "0")
+              x.requires_grad and os.environ.get("DTM_SIBLING_GROUP", "0") != "0")
         self.grp = _SiblingGroup(x) if on else None
 
     def __enter__(self):
@@ -834,9 +842,12 @@ class sibling_group:
         return False
 
 
-def _sibling_join(xb, w, g, training, bn):
+def _sibling_join(xb, w, g, training, bn, plain=False):
+    """The sibling group member handle of a conv(+BN) on x, or None.  plain: a conv without BatchNorm (its output
+    gradient is copied into the group buffer instead of stats-combined)."""
     grp = _SIBLINGS[0]
-    if (grp is None or not training or bn is None or xb is not grp.x or g.R != 1 or g.S != 1 or g.stride != 1 or
+    if (grp is None or not training or (bn is None and not plain) or xb is not grp.x or g.R != 1 or g.S != 1 or
+            g.stride != 1 or
             g.pad_h or g.pad_w or g.P != g.H or g.Q != g.W or g.K % 8 or g.C % 8 or
             getattr(w, "main_grad", None) is None):
         return None
@@ -892,7 +903,7 @@ def conv_bn(x, w, bn, stride, padding, training, relu):
             lz = x
             in_ss, in_unscaled, x = x.ss, x.unscaled, x.raw
             if (training and lz.unscaled and torch.is_grad_enabled() and x.requires_grad and x.is_cuda and
-                    os.environ.get("DTM_ACT_HANDOFF", "1") != "0"):
+                    os.environ.get("DTM_ACT_HANDOFF", "0") != "0"):
                 # conv consumers of one activation hand the (unscaled, masked) input gradient on: the last one's
                 # act epilogue adds the others' before its mask and sums (Inception's split 1x3 / 3x1 pairs), so
                 # autograd adds neither the gradients nor the BN-gradient sums
@@ -991,8 +1002,10 @@ def conv_avgpool_bn(x, w, bn, training, relu=True):
     from .nn import avg_pool
     xb = as_tensor(x).to(torch.bfloat16).contiguous()
     g = conv_geom(tuple(xb.shape), tuple(w.shape), 1, "SAME")
-    slot = _slot_register(xb) if xb is x else None
-    z = _ConvBNFn.apply(xb, None, w, None, None, g, None, slot)
+    grp = (_sibling_join(xb, w, g, training, None, plain=True)
+           if (xb is x and os.environ.get("DTM_SIBLING_POOL", "1") != "0") else None)
+    slot = _slot_register(xb) if (xb is x and grp is None) else None
+    z = _ConvBNFn.apply(xb, None, w, None, None, g, None, slot, False, None, grp)
     y = avg_pool(z, 3, 1, "SAME")
     if training:
         stats, y = _BNStatsFn.apply(y)  # (y: the alias whose gradient the statistics backward folds in)
