@@ -441,44 +441,6 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
     conv_nt_epi_tail<PT, CT, RAWB, EXACT, SACC, NT, SIDE, PRE>(a, smem, p0, c0, by, ssum, ssq, pre, pre_ss, aacc);
 }
 
-// Epilogue of the 32x32x16-MFMA kernels (staged stores only: K % 8 == 0).  Register layout of a 32x32
-// accumulator: lane holds pixel (lane & 31) and, in register quad q, the 4 consecutive channels
-// 8q + 4 (lane >> 5) .. +3 - so each quad is staged like one 16x16 subtile's 8-B lane write.
-template <int PT, int CT, int WP, int WC, int NT = 256>
-__device__ __forceinline__ void conv_nt_epilogue32(const ConvNTArgs& a, f32x16 (&acc)[WC / 32][WP / 32], char* smem,
-                                                   int p0, int c0, int by) {
-  constexpr int NWP = PT / WP;
-  constexpr int TP = WP / 32, TC = WC / 32;
-  constexpr int OROW = CT * 2 + 16;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wp = wave % NWP, wc = wave / NWP;
-  const int fr = lane & 31, fh = lane >> 5;
-#pragma unroll
-  for (int i = 0; i < TC; ++i)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int kloc = wc * WC + i * 32 + 8 * q + 4 * fh;
-      const int kch = c0 + kloc;
-      float bia[4] = {0.f, 0.f, 0.f, 0.f};
-      if (a.bias && kch < a.K) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bia[r] = a.bias[kch + r];
-      }
-#pragma unroll
-      for (int j = 0; j < TP; ++j) {
-        const int mloc = wp * WP + j * 32 + fr;
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[r] = acc[i][j][4 * q + r] + bia[r];
-          if (a.relu) v[r] = fmaxf(v[r], 0.f);
-        }
-        *(uint2*)(smem + mloc * OROW + kloc * 2) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
-      }
-    }
-  conv_nt_epi_tail<PT, CT, false, false, false, NT>(a, smem, p0, c0, by, nullptr, nullptr);
-}
-
 template <int PT, int CT, int WP, int WC, int UD, int NBUF>
 __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
   constexpr int BK = 64;
@@ -683,7 +645,7 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
 // array (a second object makes hipcc drain vmcnt before the fragment reads).
 // NWP: waves along the pixel dimension (4 / NWP along channels); NWP = 4 with PT = 512, CT = 64 gives every
 // wave a 128 x 64 tile (the 64-channel 3x3 layers: 2x the MFMAs per LDS byte of the 2x2 layout's 64x32)
-template <int PT, int CT, int NS, int UD, bool PRO, int NWP = 2, bool M32 = false>
+template <int PT, int CT, int NS, int UD, bool PRO, int NWP = 2>
 __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
   constexpr int BK = 64;
   constexpr int WP = PT / NWP, WC = CT / (4 / NWP);
@@ -807,51 +769,16 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
     }
   };
 
-  constexpr int TP32 = M32 ? WP / 32 : 1, TC32 = M32 ? WC / 32 : 1;
-  f32x4 acc[M32 ? 1 : TC][M32 ? 1 : TP];
-  f32x16 acc32[TC32][TP32];
-  if constexpr (M32) {
+  f32x4 acc[TC][TP];
 #pragma unroll
-    for (int i = 0; i < TC32; ++i)
+  for (int i = 0; i < TC; ++i)
 #pragma unroll
-      for (int j = 0; j < TP32; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc32[i][j][r] = 0.f;
-  } else {
-#pragma unroll
-    for (int i = 0; i < TC; ++i)
-#pragma unroll
-      for (int j = 0; j < TP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  }
+    for (int j = 0; j < TP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int wp = wave % NWP, wc = wave / NWP;
   const int fr = lane & 15, fk = lane >> 4;
   auto compute = [&](int slot) {
     const char* base = smem + slot * BUF;
-    if constexpr (M32) {  // 32x32x16 (see conv_nt_w8_kernel)
-      const int f32r = lane & 31, fh = lane >> 5;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int chn = ks * 2 + fh;
-        short8 bf[TP32], af[TC32];
-#pragma unroll
-        for (int j = 0; j < TP32; ++j) {
-          const int row = wp * WP + j * 32 + f32r;
-          bf[j] = *(const short8*)(base + row * 128 + ((chn ^ (row & 7)) << 4));
-        }
-#pragma unroll
-        for (int i = 0; i < TC32; ++i) {
-          const int row = wc * WC + i * 32 + f32r;
-          af[i] = *(const short8*)(base + PT * 128 + row * 128 + ((chn ^ (row & 7)) << 4));
-        }
-#pragma unroll
-        for (int i = 0; i < TC32; ++i)
-#pragma unroll
-          for (int j = 0; j < TP32; ++j)
-            acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc32[i][j], 0, 0, 0);
-      }
-      return;
-    }
     // all 2 x (TP + TC) fragment reads of the k-tile first: the ks = 1 reads are in flight under the
     // ks = 0 MFMAs (counted lgkmcnt) instead of a full LDS round trip between the two halves
     short8 bf[2][TP], af[2][TC];
@@ -898,8 +825,7 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // the epilogue reuses the ring
-  if constexpr (M32) conv_nt_epilogue32<PT, CT, WP, WC>(a, acc32, smem, p0, c0, by);
-  else if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1>(a, acc, smem, p0, c0, by);
+  if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1>(a, acc, smem, p0, c0, by);
   else conv_nt_epilogue<PT, CT, WP, WC, 2>(a, acc, smem, p0, c0, by);
 }
 
@@ -910,10 +836,9 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
 // (MI355X_MICROARCH: ~34.5 TB/s chip-wide); a 256x256 block halves the L2 bytes per MFMA (256x128: 0.75x).
 // Same LDS image / source-side swizzle / counted-vmcnt ring as conv_nt_pipe_kernel (no input prologue);
 // one 8-row x 128-B LDS-DMA group per wave-instruction, AI + WI of them per wave per k-tile.
-// M32: v_mfma_f32_32x32x16_bf16 instead of 16x16x32 (same LDS image, same FLOPs per k-tile, half the MFMA
-// instructions and half the operand-register reads per FLOP; tools/mfma_ab.hip measures it 16-60 % faster
-// on this inner-loop pattern); needs K % 8 == 0 (staged epilogue).
-template <int PT, int CT, int NWP, int NS, int UD, bool M32 = false>
+// (32x32x16-MFMA forms of these tiles measured +0.6 % ResNet-50 step - LDS / DMA bound, not MFMA-issue bound -
+// and were removed: profiles/ab/r3_ab_mfma32_step.log)
+template <int PT, int CT, int NWP, int NS, int UD>
 __global__ __launch_bounds__(512) void conv_nt_w8_kernel(ConvNTArgs a) {
   constexpr int NT = 512, NW = 8;
   constexpr int BK = 64;
@@ -990,52 +915,16 @@ __global__ __launch_bounds__(512) void conv_nt_w8_kernel(ConvNTArgs a) {
     }
   };
 
-  constexpr int TP32 = M32 ? WP / 32 : 1, TC32 = M32 ? WC / 32 : 1;
-  f32x4 acc[M32 ? 1 : TC][M32 ? 1 : TP];
-  f32x16 acc32[TC32][TP32];
-  if constexpr (M32) {
+  f32x4 acc[TC][TP];
 #pragma unroll
-    for (int i = 0; i < TC32; ++i)
+  for (int i = 0; i < TC; ++i)
 #pragma unroll
-      for (int j = 0; j < TP32; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc32[i][j][r] = 0.f;
-  } else {
-#pragma unroll
-    for (int i = 0; i < TC; ++i)
-#pragma unroll
-      for (int j = 0; j < TP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  }
+    for (int j = 0; j < TP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int wp = wave % NWP, wc = wave / NWP;
   const int fr = lane & 15, fk = lane >> 4;
   auto compute = [&](int slot) {
     const char* base = smem + slot * BUF;
-    if constexpr (M32) {
-      // k16 steps; lane: row lane & 31, 16-B chunk 2 ks + (lane >> 5) of the swizzled 128-B row
-      const int f32r = lane & 31, fh = lane >> 5;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int chn = ks * 2 + fh;
-        short8 bf[TP32], af[TC32];
-#pragma unroll
-        for (int j = 0; j < TP32; ++j) {
-          const int row = wp * WP + j * 32 + f32r;
-          bf[j] = *(const short8*)(base + row * 128 + ((chn ^ (row & 7)) << 4));
-        }
-#pragma unroll
-        for (int i = 0; i < TC32; ++i) {
-          const int row = wc * WC + i * 32 + f32r;
-          af[i] = *(const short8*)(base + PT * 128 + row * 128 + ((chn ^ (row & 7)) << 4));
-        }
-#pragma unroll
-        for (int i = 0; i < TC32; ++i)
-#pragma unroll
-          for (int j = 0; j < TP32; ++j)
-            acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc32[i][j], 0, 0, 0);
-      }
-      return;
-    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int chn = ks * 4 + fk;
@@ -1077,8 +966,7 @@ __global__ __launch_bounds__(512) void conv_nt_w8_kernel(ConvNTArgs a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // the epilogue reuses the ring
-  if constexpr (M32) conv_nt_epilogue32<PT, CT, WP, WC, NT>(a, acc32, smem, p0, c0, by);
-  else if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1, false, false, false, false, NT>(a, acc, smem, p0, c0, by);
+  if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1, false, false, false, false, NT>(a, acc, smem, p0, c0, by);
   else conv_nt_epilogue<PT, CT, WP, WC, 2, false, false, false, false, NT>(a, acc, smem, p0, c0, by);
 }
 
@@ -1511,7 +1399,6 @@ struct ConvWgradArgs {
   int Mpix;  // N*P*Q
   int Kg;    // R*S*C
   int pix_per_split;
-  int atomic;        // 1: the splits add their partial tiles straight into dw with fp32 atomics (no slabs)
   FastDiv fd_PQ, fd_Q;
   int pix_bytes;  // byte pitch of one x pixel (C*2, or less for the packed-row stem view)
   // optional BatchNorm backward of dy (register-staged kernels only): dy is the unscaled gradient g of
@@ -1764,8 +1651,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (ko + r < a.K) {
-            if (a.atomic) unsafeAtomicAdd(a.dw + (size_t)(ko + r) * a.Kg + col, acc[i][j][r]);
-            else slab[(size_t)(ko + r) * a.Kg + col] = acc[i][j][r];
+            slab[(size_t)(ko + r) * a.Kg + col] = acc[i][j][r];
           }
       }
     }
@@ -1932,8 +1818,7 @@ __global__ __launch_bounds__(NTH) void conv_wgrad_pipe_kernel(ConvWgradArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (ko + r < a.K) {
-            if (a.atomic) unsafeAtomicAdd(a.dw + (size_t)(ko + r) * a.Kg + col, acc[i][j][r]);
-            else slab[(size_t)(ko + r) * a.Kg + col] = acc[i][j][r];
+            slab[(size_t)(ko + r) * a.Kg + col] = acc[i][j][r];
           }
       }
     }
@@ -2056,17 +1941,17 @@ static const bf16_t* zero_chunk() {
   return (const bf16_t*)z;
 }
 
-template <int PT, int CT, int NWP, int NS, int UD, bool M32 = false>
+template <int PT, int CT, int NWP, int NS, int UD>
 static void launch_w8(const ConvNTArgs& a, hipStream_t st) {
   dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT, a.ngrp > 1 ? a.ngrp : 1);
-  hipLaunchKernelGGL((conv_nt_w8_kernel<PT, CT, NWP, NS, UD, M32>), grid, dim3(512), 0, st, a);
+  hipLaunchKernelGGL((conv_nt_w8_kernel<PT, CT, NWP, NS, UD>), grid, dim3(512), 0, st, a);
 }
 
-template <int PT, int CT, int NS, int UD, int NWP = 2, bool M32 = false>
+template <int PT, int CT, int NS, int UD, int NWP = 2>
 static void launch_pipe(const ConvNTArgs& a, hipStream_t st) {
   dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT, a.ngrp > 1 ? a.ngrp : 1);
-  if (a.in_scale) hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, true, NWP, M32>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, false, NWP, M32>), grid, dim3(256), 0, st, a);
+  if (a.in_scale) hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, true, NWP>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, false, NWP>), grid, dim3(256), 0, st, a);
 }
 
 static int device_cus() {
@@ -2235,13 +2120,7 @@ static int g_k32_tile = 1;  // A/B knob: the 256x32 tile for <= 32-channel spati
 DTM_API void dtm_conv_set_k32(int on) { g_k32_tile = on; }
 static int g_act_tile = -1;  // A/B knob: tile of the dgrads with a fused activation-backward epilogue (-1 = policy)
 DTM_API void dtm_conv_set_act_tile(int id) { g_act_tile = id; }
-static int g_mfma32 = -1;  // -1: DTM_MFMA32 env (default on once measured), 0 / 1: A/B knob
-DTM_API void dtm_conv_set_mfma32(int on) { g_mfma32 = on; }
 static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
-  if (g_mfma32 < 0) {
-    const char* e = getenv("DTM_MFMA32");
-    g_mfma32 = e ? atoi(e) : 0;
-  }
   if (g_tile_env == -2) {
     const char* e = getenv("DTM_CONV_TILE");
     g_tile_env = e ? atoi(e) : -1;
@@ -2311,28 +2190,14 @@ static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
   // (profiles/r2_conv_tiles_k64.txt: -4 % vs the register-staged single-buffer tile)
   if (id == -1 && !a.in_scale && a.K <= 64 && a.R * a.S > 1 && a.K % 64 == 0) id = 26;
   if (id < 0) id = a.K <= 64 ? g_k64_tile : ((a.M <= 16384 && a.Kg >= 2048) ? 0 : 4);
-  // the 32x32x16-MFMA forms of the LDS-DMA tiles (A/B knob dtm_conv_set_mfma32 / DTM_MFMA32; staged
-  // epilogue only: K % 8 == 0)
-  if (g_mfma32 && (a.K & 7) == 0) {
-    if (id == 40) id = 50;
-    else if (id == 21) id = 51;
-    else if (id == 26) id = 52;
-    else if (id == 24) id = 53;
-    else if (id == 32) id = 54;
-  }
-  if (id >= 50 && id <= 54 && (a.K & 7) != 0) id = 0;
-  if (id >= 51 && id <= 54 && a.in_scale && a.C > 512) id = 0;
   // pipelined LDS-DMA tiles stage the prologue affine in LDS: C <= 512
   if ((id == 21 || id == 24 || id == 26 || id == 32) && a.in_scale && a.C > 512) id = 0;
   if (id == 21 || id == 26) return {id, 128, 2};  // 128 x 128 / 128 x 64 pipelined, 2 slots
   if (id == 24) return {id, 256, 2};              // 256 x 64 pipelined (waves 2x2 of 128x32)
   if (id == 32) return {id, 256, 4};              // 256 x 32 pipelined, waves 4x1 of 64x32
   // 8-wave 256x256 tile (waves 2x4), no prologue
-  if ((id == 40 || id == 50) && a.in_scale) id = 0;
-  if (id == 40 || id == 50) return {id, 256, 2};
-  if (id == 51 || id == 52) return {id, 128, 2};
-  if (id == 53) return {id, 256, 2};
-  if (id == 54) return {id, 256, 4};
+  if (id == 40 && a.in_scale) id = 0;
+  if (id == 40) return {id, 256, 2};
   if (id == 30 || id == 31) {
     if (stream_ok(a)) return {id, 64, 2};
     id = a.K <= 64 ? 3 : 4;
@@ -2362,11 +2227,6 @@ static void dispatch_ud(const ConvNTArgs& a, const TileCfg& t, hipStream_t st) {
   else if (t.id == 26) launch_pipe<128, 64, 2, UD>(a, st);
   else if (t.id == 32) launch_pipe<256, 32, 2, UD, 4>(a, st);   // waves 4x1 of 64x32 (32-channel outputs)
   else if (t.id == 40) launch_w8<256, 256, 2, 2, UD>(a, st);
-  else if (t.id == 50) launch_w8<256, 256, 2, 2, UD, true>(a, st);
-  else if (t.id == 51) launch_pipe<128, 128, 2, UD, 2, true>(a, st);
-  else if (t.id == 52) launch_pipe<128, 64, 2, UD, 2, true>(a, st);
-  else if (t.id == 53) launch_pipe<256, 64, 2, UD, 2, true>(a, st);
-  else if (t.id == 54) launch_pipe<256, 32, 2, UD, 4, true>(a, st);
   else launch_nt<128, 128, 64, 64, UD>(a, st);
 }
 
@@ -2618,17 +2478,6 @@ static void launch_wgrad(const ConvWgradArgs& a, int splits, hipStream_t st) {
 // kernels (A/B sweeps: tools/conv_tile_sweep.py)
 static int g_wgrad_env = -2;
 static int g_wgrad_occ = 4;
-// split-K weight gradients with at most this many splits accumulate with fp32 atomics straight into dW
-// (no slab workspace, no reduce launch); -1: DTM_WGRAD_ATOMIC env (default 0 = always slabs)
-static int g_wgrad_atomic = -1;
-// A/B knob: the 64 x 256 register-staged wgrad tile (id 7) for K <= 64, Kg > 128: 0 never, 1 always (+3.5 %
-// ResNet-50 step), 2 only with the BN backward in the operand staging (the stem: +1.4 %); its 1 block per CU
-// loses to the 64 x 128 tile's occupancy (profiles/ab/r3_ab_wgrad_wide.log); 3 = 2 with a single LDS buffer
-static int g_wgrad_wide = 0;
-DTM_API void dtm_conv_set_wgrad_wide(int on) { g_wgrad_wide = on; }
-DTM_API void dtm_conv_set_wgrad_atomic(int max_splits) { g_wgrad_atomic = max_splits; }
-static int g_wgrad_p64 = 0;
-DTM_API void dtm_conv_set_wgrad_p64(int v) { g_wgrad_p64 = v; }
 DTM_API void dtm_conv_set_wgrad_tile(int id, int occ) {
   g_wgrad_env = id;
   if (occ > 0) g_wgrad_occ = occ;
@@ -2706,9 +2555,6 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   int wt = wenv >= 0 ? wenv : (d->K <= 64 ? 1 : 0);
   // <= 32 output channels: 32-row tiles (no half-empty 64-row tile; A/B knob dtm_conv_set_k32)
   if (wenv == -1 && wt == 1 && d->K <= 32 && g_k32_tile) wt = 6;
-  // <= 64 output channels over a wide reduction (Kg > 128): the 64 x 256 tile reads the dy / comb operand
-  // once per 256 columns instead of once per 128 (the stem: 224 columns in one tile, half the g / y reads)
-  if (wenv == -1 && wt == 1 && a.Kg > 128 && (g_wgrad_wide == 1 || (g_wgrad_wide >= 2 && bn))) wt = 7;
   int occ = g_wgrad_occ;
   // policy (tools/conv_tile_sweep.py WTILES sweep, ResNet-50 shapes): the pipelined kernel at 2 blocks
   // per CU wins every layer with K > 64 (-10..-25 %); 4 blocks' worth of splits for the deep 3x3 7x7s
@@ -2719,17 +2565,10 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
     // 14x14 / 7x7 3x3 -8..-13 %, 7x7 1024->2048 -7 %; it loses on every K < 256 or short-RSC layer)
     if (g_tile_w8 && d->K >= 256 && a.Kg >= 1024 && (d->R * d->S > 1 || d->K >= 1024)) wt = 12;
   }
-  // the pipelined 64 x 128 tile (id 11, waves 1x4 of 64x32; A/B knob dtm_conv_set_wgrad_p64): 1 = for output widths
-  // whose last 128-row tile is at most half full (Inception's 192 / 320 / 160 ...), 2 = also for 33..64 outputs
-  if (wenv == -1 && !in_scale && !bn && g_wgrad_p64) {
-    if (wt == 10 && d->K % 128 != 0 && d->K % 128 <= 64) wt = 11;
-    else if (g_wgrad_p64 >= 2 && d->K > 32 && d->K <= 64 && (wt == 1 || wt == 7)) { wt = 11; occ = 2; }
-  }
   if (wt >= 10 && (in_scale || bn)) wt = d->K <= 64 ? 1 : 0;  // the pipelined kernels have no operand prologues
-  if (wt != 0 && wt != 1 && wt != 6 && wt != 7 && wt != 10 && wt != 11 && wt != 12) wt = 0;
+  if (wt != 0 && wt != 1 && wt != 6 && wt != 10 && wt != 12) wt = 0;
   const bool big = wt == 12;  // 8-wave 256x256 (one block per CU)
-  const int MT = wt == 6 ? 32 : ((wt == 1 || wt == 7 || wt == 11) ? 64 : (big ? 256 : 128)),
-            NT = (big || wt == 7) ? 256 : 128;
+  const int MT = wt == 6 ? 32 : (wt == 1 ? 64 : (big ? 256 : 128)), NT = big ? 256 : 128;
   if (big) occ = (wenv == 12 && g_wgrad_occ != 4) ? g_wgrad_occ : 1;  // (sweeps: WTILES=12:<occ>)
   long tiles = (long)((a.Kg + NT - 1) / NT) * ((a.K + MT - 1) / MT);
   long target = (long)num_cus * (wt >= 10 ? occ : 3);
@@ -2742,29 +2581,19 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   long steps_per = (ksteps + splits - 1) / splits;
   a.pix_per_split = (int)(steps_per * 64);
   splits = (a.Mpix + a.pix_per_split - 1) / a.pix_per_split;
-  if (g_wgrad_atomic < 0) {
-    const char* e = getenv("DTM_WGRAD_ATOMIC");
-    g_wgrad_atomic = e ? atoi(e) : 0;
-  }
-  a.atomic = !dtm_get_deterministic() && splits <= g_wgrad_atomic && !dst;
-  float* ws = dw;
-  if (!a.atomic) {
-    ws = dtm_ws_get_stream((size_t)splits * a.K * a.Kg, (hipStream_t)stream);
-    if (!ws) return -4;
-  }
+  // split-K partial slabs, summed into dW below (fp32 atomics straight into dW measured +2.4..+12 % step:
+  // profiles/ab/r3_ab_wgrad_atomic_*.log)
+  float* ws = dtm_ws_get_stream((size_t)splits * a.K * a.Kg, (hipStream_t)stream);
+  if (!ws) return -4;
   a.dw = ws;
   if (wt >= 10) {
     a.in_shift = (const float*)zero_chunk();  // the zero DMA source
     dim3 grid((a.Kg + NT - 1) / NT, (a.K + MT - 1) / MT, splits);
     if (wt == 12)
       hipLaunchKernelGGL((conv_wgrad_pipe_kernel<256, 256, 2, 2, 512>), grid, dim3(512), 0, (hipStream_t)stream, a);
-    else if (wt == 11)
-      hipLaunchKernelGGL((conv_wgrad_pipe_kernel<64, 128, 2, 1, 256>), grid, dim3(256), 0, (hipStream_t)stream, a);
     else
       hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 128, 2>), grid, dim3(256), 0, (hipStream_t)stream, a);
   } else if (wt == 1) launch_wgrad<64, 128, 32, 64>(a, (int)splits, (hipStream_t)stream);
-  else if (wt == 7 && g_wgrad_wide == 3) launch_wgrad<64, 256, 32, 128, 1>(a, (int)splits, (hipStream_t)stream);
-  else if (wt == 7) launch_wgrad<64, 256, 32, 128>(a, (int)splits, (hipStream_t)stream);
   else if (wt == 6) launch_wgrad<32, 128, 16, 64>(a, (int)splits, (hipStream_t)stream);
   else launch_wgrad<128, 128, 64, 64>(a, (int)splits, (hipStream_t)stream);
   // dW += sum over the split slabs (every slab element is written: tiles cover [K][Kg] exactly)
@@ -2772,7 +2601,7 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
     for (int i = 0, r0 = 0; i < dst->n; r0 += dst->rows[i], ++i)
       dtm_reduce_rows(ws + (size_t)r0 * a.Kg, (int)splits, dst->rows[i] * a.Kg, a.K * a.Kg, dst->dw[i],
                       (hipStream_t)stream);
-  } else if (!a.atomic) {
+  } else {
     dtm_reduce_rows(ws, (int)splits, a.K * a.Kg, a.K * a.Kg, dw, (hipStream_t)stream);
   }
   return 0;

@@ -33,7 +33,8 @@ class TrainStep:
     def __init__(self, model, optimizer="momentum", lr=0.1, momentum=0.9, rho=0.9, epsilon=1e-10, bucket_mb=32.0,
                  label_smoothing=0.0, aux_weight=0.4, ema_decay=None, lr_schedule=None, use_graph=False,
                  process_group=None, weight_decay=None, batch_weight=1.0, nan_guard=True, timer=None,
-                 grad_comm_dtype=None, ema_buffers=True, bn_sync_every=1, wgrad_stream=None):
+                 grad_comm_dtype=None, ema_buffers=True, bn_sync_every=1, wgrad_stream=None, bsp_check=None,
+                 overlap=True):
         self.model = model
         if wgrad_stream is not None:
             # conv+BN weight gradients on the side stream (ops/_lib.py side_stream; process-wide): ResNet-50
@@ -41,7 +42,9 @@ class TrainStep:
             _lib.set_side_enabled(wgrad_stream)
         prepare_compute_copies(model)
         params = [p for p in model.parameters() if p.requires_grad]
-        self.dp = BSPDataParallel(params, bucket_mb, process_group, comm_dtype=grad_comm_dtype)
+        # bsp_check (or DTM_BSP_CHECK=1): assert every gradient write precedes its bucket's all-reduce (debug)
+        self.dp = BSPDataParallel(params, bucket_mb, process_group, comm_dtype=grad_comm_dtype, overlap=overlap,
+                                  check=bsp_check, names=list(model.named_parameters()))
         if use_graph and self.dp.world > 1:
             # a captured step would hold the bucket collectives (and their waits) inside the graph;
             # RCCL-in-hipGraph has never been validated here, so multi-rank runs stay eager
@@ -135,17 +138,6 @@ class TrainStep:
     def __call__(self, images, labels):
         if self.use_graph and images.is_cuda:
             return self._graph_step(images, labels)
-        ps = _lib.priority_stream() if images.is_cuda else None
-        if ps is not None:
-            # the step's critical path on a high-priority stream: the side-stream weight gradients only
-            # take the CUs it leaves idle (ops/_lib.py priority_stream)
-            caller = torch.cuda.current_stream()
-            ps.wait_stream(caller)
-            with torch.cuda.stream(ps):
-                loss = self._eager_step(images, labels)
-            caller.wait_stream(ps)
-            loss.record_stream(caller)
-            return loss
         return self._eager_step(images, labels)
 
     def _eager_step(self, images, labels):

@@ -53,15 +53,11 @@ _SIGS = {
     "dtm_conv_set_policy2": (None, [_I]),
     "dtm_set_grid_cpt": (None, [_I]),
     "dtm_conv_set_k32": (None, [_I]),
-    "dtm_conv_set_mfma32": (None, [_I]),
     "dtm_conv_set_stem_stream": (None, [_I]),
     "dtm_ws_set_side_stream": (None, [_I, _P]),
     "dtm_device_check": (_I, []),
-    "dtm_conv_set_wgrad_atomic": (None, [_I]),
-    "dtm_conv_set_wgrad_wide": (None, [_I]),
     "dtm_conv_set_direct3": (None, [_I]),
     "dtm_conv_set_dec_group": (None, [_I]),
-    "dtm_conv_set_wgrad_p64": (None, [_I]),
     "dtm_cat_desc_bytes": (_I, []),
     "dtm_cat_bn_apply": (_I, [_P, _I, _P, _L, _I, _P]),
     "dtm_cat_bn_apply_bwd": (_I, [_P, _I, _P, _P, _L, _I, _P]),
@@ -199,29 +195,6 @@ def side_stream():
         st = torch.cuda.Stream(device=dev)
         _side["stream"] = st
         lib().dtm_ws_set_side_stream(1, ctypes.c_void_p(st.cuda_stream))  # scratch slot 1
-    return st
-
-
-_prio = {"stream": None, "on": None}
-
-
-def set_priority_enabled(on):
-    _prio["on"] = bool(on)
-
-
-def priority_stream():
-    """High-priority stream an eager training step runs on when the weight-gradient side stream is in use
-    (DTM_PRIORITY_STREAM=0/1), so the command processor favours the dgrad chain's workgroups; None when off."""
-    if _prio["on"] is None:
-        _prio["on"] = os.environ.get("DTM_PRIORITY_STREAM", "0") == "1"
-    if not _prio["on"] or side_stream() is None:
-        return None
-    dev = torch.cuda.current_device()
-    st = _prio["stream"]
-    if st is None or st.device.index != dev:
-        lo, hi = torch.cuda.Stream.priority_range()
-        st = torch.cuda.Stream(device=dev, priority=min(lo, hi))
-        _prio["stream"] = st
     return st
 
 

@@ -18,7 +18,7 @@ import torch
 from . import _lib
 from .geometry import conv_geom
 from .lazy import LazyBN, Subsampled, as_tensor  # noqa: F401
-from .nn import _accum_param_grad, _check, _notify, dgrad_decomposable, weight_bf16, weight_flipped
+from .nn import _accum_param_grad, _check, _notify, dgrad_decomposable, grad_target, weight_bf16, weight_flipped
 
 
 class ZeroArena:
@@ -241,8 +241,8 @@ class _ConvBNFn(torch.autograd.Function):
             if out is not None:
                 return out
         if ss is not None and dss is not None:
-            gmg = getattr(gamma, "main_grad", None) if gamma is not None else None
-            bmg = getattr(beta, "main_grad", None) if beta is not None else None
+            gmg = grad_target(gamma) if gamma is not None else None
+            bmg = grad_target(beta) if beta is not None else None
             if gamma is not None and gmg is None:
                 dgamma = torch.zeros(g.K, device=dy.device)
             if beta is not None and bmg is None:
@@ -273,7 +273,7 @@ class _ConvBNFn(torch.autograd.Function):
             st = _lib.side_fork(x, dy, in_ss)
             if st is not None:
                 with torch.cuda.stream(st):
-                    _check(L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(w.main_grad), _lib.ptr(sc),
+                    _check(L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(grad_target(w)), _lib.ptr(sc),
                                             _lib.ptr(sh), ctypes.byref(d), _lib.side_cus(), _lib.stream_ptr()),
                            "conv_wgrad(side)")
                     _notify(w)
@@ -331,7 +331,7 @@ class _ConvBNFn(torch.autograd.Function):
         if wg_side:
             dw = None
         elif ctx.needs_input_grad[2]:
-            mg = getattr(w, "main_grad", None)
+            mg = grad_target(w)
             target = mg if mg is not None else torch.zeros(w.shape, device=dy.device, dtype=torch.float32)
             _check(L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(target), _lib.ptr(sc),
                                                          _lib.ptr(sh), ctypes.byref(d), _lib.wgrad_cus(), s),
@@ -363,14 +363,14 @@ class _ConvBNFn(torch.autograd.Function):
                 return None  # (block-output input: the dgrad-epilogue BN-apply backward wins)
         L = _lib.lib()
         s = _lib.stream_ptr()
-        gmg = getattr(gamma, "main_grad", None) if gamma is not None else None
-        bmg = getattr(beta, "main_grad", None) if beta is not None else None
+        gmg = grad_target(gamma) if gamma is not None else None
+        bmg = grad_target(beta) if beta is not None else None
         dgamma = torch.zeros(g.K, device=dy.device) if (gamma is not None and gmg is None) else None
         dbeta = torch.zeros(g.K, device=dy.device) if (beta is not None and bmg is None) else None
         wt = weight_flipped(w, g.K, g.R, g.S, g.C)  # 1x1: [C][K] = W transposed
         dx = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
         d_in = arena.zeros((4, g.C), dy.device) if act else None
-        mg = getattr(w, "main_grad", None)
+        mg = grad_target(w)
         target = mg if mg is not None else torch.zeros(w.shape, device=dy.device, dtype=torch.float32)
         last = True
         if not act:
@@ -427,8 +427,8 @@ class _BNFinalizeFn(torch.autograd.Function):
         (ss,) = ctx.saved_tensors
         C = ss.shape[1]
         dstats = torch.empty((2, C), device=ss.device, dtype=torch.float32)
-        gmg = getattr(ctx.gamma, "main_grad", None) if ctx.gamma is not None else None
-        bmg = getattr(ctx.beta, "main_grad", None) if ctx.beta is not None else None
+        gmg = grad_target(ctx.gamma) if ctx.gamma is not None else None
+        bmg = grad_target(ctx.beta) if ctx.beta is not None else None
         dg = None if (ctx.gamma is None or gmg is not None) else torch.zeros(C, device=ss.device)
         db = None if (ctx.beta is None or bmg is not None) else torch.zeros(C, device=ss.device)
         L.dtm_bn_finalize_bwd(_lib.ptr(dss.contiguous()), _lib.ptr(ss), _lib.ptr(ctx.gamma), _lib.ptr(dstats),
@@ -607,8 +607,8 @@ class _StemConvBNFn(torch.autograd.Function):
                 os.environ.get("DTM_STEM_WGRAD_FUSE", "1") != "0"):
             # no input gradient: comb (the BN backward of dy) has the wgrad as its only reader, so it is
             # formed in the wgrad's operand staging instead of being written and read back
-            gmg = getattr(gamma, "main_grad", None) if gamma is not None else None
-            bmg = getattr(beta, "main_grad", None) if beta is not None else None
+            gmg = grad_target(gamma) if gamma is not None else None
+            bmg = grad_target(beta) if beta is not None else None
             dgamma = torch.zeros(K, device=dy.device) if (gamma is not None and gmg is None) else None
             dbeta = torch.zeros(K, device=dy.device) if (beta is not None and bmg is None) else None
             d = _lib.ConvDesc(N, Hp, Wp, 32, K, R, 1, P, Q, st, 0, 0, 8)
@@ -624,8 +624,8 @@ class _StemConvBNFn(torch.autograd.Function):
             dw = _accum_param_grad(w, tv[:, :, :S, :C])
             return None, dw, dgamma, dbeta, None, None, None
         if ss is not None and dss is not None:
-            gmg = getattr(gamma, "main_grad", None) if gamma is not None else None
-            bmg = getattr(beta, "main_grad", None) if beta is not None else None
+            gmg = grad_target(gamma) if gamma is not None else None
+            bmg = grad_target(beta) if beta is not None else None
             if gamma is not None and gmg is None:
                 dgamma = torch.zeros(K, device=dy.device)
             if beta is not None and bmg is None:
@@ -750,8 +750,8 @@ class _SiblingGroup:
             # backward): a strided copy into its column slice
             grp.buf[:, off:off + g.K].copy_(dy.reshape(M, g.K))
         else:
-            gmg = getattr(gamma, "main_grad", None) if gamma is not None else None
-            bmg = getattr(beta, "main_grad", None) if beta is not None else None
+            gmg = grad_target(gamma) if gamma is not None else None
+            bmg = grad_target(beta) if beta is not None else None
             dgamma = torch.zeros(g.K, device=dy.device) if (gamma is not None and gmg is None) else None
             dbeta = torch.zeros(g.K, device=dy.device) if (beta is not None and bmg is None) else None
             _check(L.dtm_stats_combine_fin_ld(_lib.ptr(dy.contiguous()), _lib.ptr(y), _lib.ptr(dss.contiguous()),
@@ -769,7 +769,7 @@ class _SiblingGroup:
         # the last member: one dgrad and one wgrad over every member's output gradient
         buf, n = grp.buf, len(grp.members)
         d = _lib.ConvDesc(g.N, g.H, g.W, g.C, grp.ktot, 1, 1, g.P, g.Q, 1, 0, 0, 0)
-        mgs = [getattr(m[0], "main_grad", None) for m in grp.members]
+        mgs = [grad_target(m[0]) for m in grp.members]
         dws = [mg if mg is not None else torch.zeros(m[0].shape, device=dy.device, dtype=torch.float32)
                for mg, m in zip(mgs, grp.members)]
         ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in dws])

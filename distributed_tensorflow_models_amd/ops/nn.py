@@ -38,6 +38,32 @@ def _notify(p):
         h(p)
 
 
+# gradient-write hooks: every kernel launch (or torch op) that writes into a parameter's main_grad asks for
+# the target through grad_target() right before it is enqueued, so a checker (BSPDataParallel with
+# check=True / DTM_BSP_CHECK=1) can assert that the write precedes the parameter's ready notification and
+# the launch of its bucket's all-reduce - a later write would be clobbered by (or missing from) the collective
+_grad_write_hooks = []
+
+
+def add_grad_write_hook(fn):
+    _grad_write_hooks.append(fn)
+    return fn
+
+
+def remove_grad_write_hook(fn):
+    if fn in _grad_write_hooks:
+        _grad_write_hooks.remove(fn)
+
+
+def grad_target(p):
+    """``p.main_grad`` (or None) for a write about to be enqueued; write hooks see the parameter."""
+    mg = getattr(p, "main_grad", None)
+    if mg is not None:
+        for h in _grad_write_hooks:
+            h(p)
+    return mg
+
+
 # live-tap windows: a conv whose outer taps only ever read zero padding has a provably-zero weight
 # gradient outside its live window (VGG-16 fc6 on a 1x1 map: 48 of 49 taps).  The window is announced
 # during the forward (geometry only, identical on every rank) so the data-parallel layer can leave the
@@ -68,7 +94,7 @@ def _note_live_window(w, win):
 
 def _accum_param_grad(p, g):
     """Route a computed fp32 grad for parameter p; returns what autograd should receive."""
-    mg = getattr(p, "main_grad", None)
+    mg = grad_target(p)
     if mg is not None:
         mg.add_(g)
         _notify(p)
@@ -215,7 +241,7 @@ class _Conv2dFn(torch.autograd.Function):
             d.dec = 0
         dw = None
         if ctx.needs_input_grad[1]:
-            mg = getattr(w, "main_grad", None)
+            mg = grad_target(w)
             target = mg if mg is not None else torch.zeros(w.shape, device=dy.device, dtype=torch.float32)
             _check(L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(target), None, None,
                                                          ctypes.byref(d), _lib.num_cus(), s), "conv_wgrad")
@@ -351,7 +377,7 @@ class _Conv2dTransposeFn(torch.autograd.Function):
                                   ctypes.byref(d), s), "conv_transpose_bwd_data")
         dw = None
         if ctx.needs_input_grad[1]:
-            mg = getattr(w, "main_grad", None)
+            mg = grad_target(w)
             target = mg if mg is not None else torch.zeros(w.shape, device=dy.device, dtype=torch.float32)
             _check(L.dtm_conv_wgrad(_lib.ptr(dy), _lib.ptr(x), _lib.ptr(target), None, None,
                                                          ctypes.byref(d), _lib.num_cus(), s),
@@ -410,7 +436,7 @@ class _CropTaps(torch.autograd.Function):
     def backward(ctx, g):
         r0, r1, s0, s1 = ctx.win
         p = ctx.src
-        mg = getattr(p, "main_grad", None)
+        mg = grad_target(p)
         if mg is not None:
             mg[:, r0:r1, s0:s1, :].add_(g)
             _notify(p)
@@ -790,7 +816,7 @@ class _LinearHipFn(torch.autograd.Function):
                                   ctypes.byref(d), s), "fc_dgrad")
         dw = None
         if ctx.needs_input_grad[1]:
-            mg = getattr(w, "main_grad", None)
+            mg = grad_target(w)
             direct = mg is not None and Np == N
             target = mg if direct else torch.zeros((Kin, Np), device=dy.device, dtype=torch.float32)
             d = _fc_desc(B, Np, Kin)  # "input" dy (C = Np), "output gradient" x (K = Kin): dW[Kin][Np]

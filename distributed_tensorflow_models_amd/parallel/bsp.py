@@ -29,6 +29,8 @@ Design (MI355X-first):
     cost of bf16 rounding of the per-rank and summed gradients.
 With world_size == 1 no collective is issued.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -39,7 +41,7 @@ from ..utils.profiler import roctx
 
 class BSPDataParallel:
     def __init__(self, params, bucket_mb=32.0, process_group=None, device=None, overlap=True, grad_dtype=torch.float32,
-                 comm_dtype=None, tail_mb=1.0):
+                 comm_dtype=None, tail_mb=1.0, check=None, names=None):
         self.params = [p for p in params if p.requires_grad]
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
@@ -63,7 +65,6 @@ class BSPDataParallel:
         self.tail = max(0, int(tail_mb * (1 << 20) / self.flat.element_size()))
         # param -> live-tap window (r0, r1, s0, s1): compact bucket (windows announced to an earlier
         # instance are remembered on the parameter).  DTM_BSP_COMPACT=0 turns compaction off (A/B).
-        import os
         self._compact_on = os.environ.get("DTM_BSP_COMPACT", "1") != "0"
         self.windows = {p: p._live_win for p in self.params
                         if self._compact_on and getattr(p, "_live_win", None) is not None and p.dim() == 4}
@@ -81,6 +82,16 @@ class BSPDataParallel:
         for p in self.params:
             if hasattr(p, "register_post_accumulate_grad_hook"):
                 self._acc_hooks.append(p.register_post_accumulate_grad_hook(self._on_accumulated))
+        # debug mode (DTM_BSP_CHECK=1): every gradient write must precede its parameter's ready notification,
+        # which must come once per step; a write into a bucket whose all-reduce was already issued would be
+        # clobbered by the collective's copy-back or left out of the sum
+        self.check = (os.environ.get("DTM_BSP_CHECK", "0") not in ("", "0")) if check is None else bool(check)
+        self._names = {}
+        if names is not None:
+            self._names = {p: n for n, p in names}
+        self._write_hook = opsnn.add_grad_write_hook(self._on_write) if self.check else None
+        self.writes_checked = 0
+        self.unreported = []
 
     def _build_buckets(self):
         """Contiguous cap-sized buckets over the flat buffer, skipping the segments of windowed
@@ -157,6 +168,8 @@ class BSPDataParallel:
     def close(self):
         opsnn.remove_live_window_hook(self._win_hook)
         opsnn.remove_grad_ready_hook(self._hook)
+        if self._write_hook is not None:
+            opsnn.remove_grad_write_hook(self._write_hook)
         for h in self._acc_hooks:
             h.remove()
 
@@ -167,17 +180,40 @@ class BSPDataParallel:
         self._launched = [False] * len(self.buckets)
         self._works = []
         self._seen = set()
+        self.unreported = []
 
     def _on_accumulated(self, p):
         # plain autograd path (CPU ops / torch fallbacks): move .grad into the flat buffer
         if p.grad is not None:
+            if self.check:
+                self._on_write(p)
             p.main_grad.add_(p.grad.to(p.main_grad.dtype))
             p.grad = None
         self._on_ready(p)
 
+    def _pname(self, p):
+        return self._names.get(p, "<param %s>" % (tuple(p.shape),))
+
+    def _on_write(self, p):
+        """(check mode) a kernel / op is about to write p's gradient."""
+        lst = self.contrib.get(p)
+        if lst is None:
+            return
+        self.writes_checked += 1
+        if p in self._seen:
+            raise RuntimeError("BSP check: gradient of %s written after it was reported ready" % self._pname(p))
+        for bi, _n in lst:
+            if self._launched[bi]:
+                raise RuntimeError("BSP check: gradient of %s written after the all-reduce of its bucket %d was issued"
+                                   % (self._pname(p), bi))
+
     def _on_ready(self, p):
         lst = self.contrib.get(p)
-        if lst is None or p in self._seen:
+        if lst is None:
+            return
+        if p in self._seen:
+            if self.check:
+                raise RuntimeError("BSP check: %s reported ready twice in one step" % self._pname(p))
             return
         self._seen.add(p)
         for bi, n in lst:
@@ -220,6 +256,9 @@ class BSPDataParallel:
     def finish(self):
         """Launch any bucket not yet reduced (unused params / no overlap) and make the current
         stream wait for every reduction."""
+        if self.check:
+            # parameters that never reported a gradient this step (legal - an unused head - but listed)
+            self.unreported = [self._pname(p) for p in self.order if p not in self._seen]
         for bi in range(len(self.buckets)):
             if not self._launched[bi]:
                 self._launch(bi)
@@ -233,6 +272,9 @@ class BSPDataParallel:
             elif self.comm is not None:
                 s, e = self.buckets[bi]
                 self.flat[s:e].copy_(self.comm[s:e])
+        if self.check:
+            # nothing may write a gradient between the waits above and the next zero_grad
+            self._seen = set(self.contrib)
         self._done_works = self._works
         self._works = []
 

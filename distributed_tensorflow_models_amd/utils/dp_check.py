@@ -1,0 +1,76 @@
+"""Gradient-exactness check of BSP data parallelism on the real kernels.
+
+The reference's BSP step applies exactly the mean of the W workers' gradients
+(/root/reference/inception/imagenet_inception_bsp.py:123-157, /root/reference/vgg/cifar10_vgg_bsp.py:85-95).
+Here every rank reduces its flat fp32 gradient buffer with bucketed all-reduces issued from inside backward,
+so a kernel that writes a gradient after its bucket's collective was issued - or a ready notification that
+comes before the write - silently drops or clobbers part of the sum.  ``grad_worker`` runs ONE training step
+of a model with every rank on the SAME batch (so the mean of the replicas' gradients equals the single-rank
+gradient), with deterministic reductions (bit-reproducible kernels) and the BSP write checker on, and returns
+every parameter's step-1 gradient (flat buffer / W) in backward order; ``compare`` reports the per-tensor
+relative error between a W-rank run and a 1-rank run.
+
+Used by tests/test_distributed.py (GPU matrix over models and gradient-routing knobs) and
+tools/dp_grad_diag.py (the per-parameter table).
+"""
+import os
+
+import torch
+
+# model name -> (builder kwargs, image size, batch, optimizer kwargs)
+CONFIGS = {
+    "resnet_v1_50": (dict(num_classes=16), 64, 4, dict(optimizer="momentum", lr=0.05, momentum=0.9)),
+    # 299: the aux head's 5x5 VALID conv needs the 17x17 map (reference inception/slim/inception_model.py:227-236)
+    "inception_v3_slim_old": (dict(num_classes=11), 299, 2,
+                              dict(optimizer="rmsprop", lr=0.045, rho=0.9, epsilon=1.0, label_smoothing=0.1,
+                                   aux_weight=0.4)),
+    # the reference's CIFAR geometry: fc6 a 7x7 'SAME' conv over a 1x1 map -> compact dead-tap bucket
+    "vgg_16": (dict(num_classes=10, fc_conv_padding="SAME"), 32, 4, dict(optimizer="momentum", lr=0.01,
+                                                                          momentum=0.9)),
+}
+
+
+def grad_worker(rank, world, model_name, knobs=None, bucket_mb=2.0, overlap=True, steps=1):
+    """One rank (world 1 = the reference run).  knobs: environment overrides (DTM_* gradient-routing knobs),
+    set before any kernel call of this fresh process."""
+    os.environ.update({k: str(v) for k, v in (knobs or {}).items()})
+    os.environ["DTM_DETERMINISTIC"] = "1"
+    os.environ.setdefault("DTM_BSP_CHECK", "1")
+    from ..engine import TrainStep
+    from ..models import nets_factory
+    from ..ops import elementwise as ew
+    from ..ops import fused
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    torch.manual_seed(0)
+    ew.set_base_seed(0, 0)  # the same dropout masks on every rank (the batch is the same too)
+    kw, S, B, okw = CONFIGS[model_name]
+    model = nets_factory.build(model_name, **kw).to(dev)
+    step = TrainStep(model, bucket_mb=bucket_mb, overlap=overlap, **okw)
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(B, S, S, 3, generator=g).to(dev, torch.bfloat16)
+    y = torch.randint(0, kw["num_classes"], (B,), generator=g).to(dev)
+    n_sib = fused.SIBLING_MERGED[0]
+    grads = []
+    for _ in range(steps):
+        step(x, y)
+        torch.cuda.synchronize()
+        names = {p: n for n, p in model.named_parameters()}
+        grads.append([(names[p], (p.main_grad.detach().float() / world).cpu()) for p in step.dp.order])
+    out = {"grads": grads, "buckets": len(step.dp.buckets), "launched": sum(step.dp._launched),
+           "compact": len(step.dp.compact), "sibling_merged": fused.SIBLING_MERGED[0] - n_sib,
+           "writes_checked": step.dp.writes_checked, "unreported": list(step.dp.unreported),
+           "params": torch.cat([p.detach().float().reshape(-1) for p in model.parameters()]).cpu()}
+    step.dp.close()
+    return out
+
+
+def compare(multi, single, step=0):
+    """[(name, relative error, max abs error)] in backward order (relative: ||a - b|| / max(||b||, tiny))."""
+    rows = []
+    for (na, a), (nb, b) in zip(multi["grads"][step], single["grads"][step]):
+        assert na == nb, (na, nb)
+        d = (a - b).double()
+        rel = float(d.norm() / max(float(b.double().norm()), 1e-30))
+        rows.append((na, rel, float(d.abs().max()) if d.numel() else 0.0))
+    return rows

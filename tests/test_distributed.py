@@ -167,6 +167,60 @@ def test_bsp_gpu_two_ranks_hip_kernels_match_single_rank():
     assert two[0]["losses"] == pytest.approx(single["losses"], rel=1e-4)
 
 
+# Step-1 gradients of every BASELINE data-parallel model, per parameter, W = 2 ranks (same batch) vs 1 rank,
+# over the gradient-routing knobs: deterministic reductions make a correct run bit-exact, the BSP write
+# checker (DTM_BSP_CHECK) raises on a gradient written after its bucket's all-reduce was issued.
+_DP_MATRIX = [
+    ("resnet_v1_50", {}),
+    ("resnet_v1_50", {"DTM_WGRAD_STREAM": "0"}),
+    ("resnet_v1_50", {"DTM_SIBLING_GROUP": "1"}),
+    ("resnet_v1_50", {"DTM_SIBLING_GROUP": "0"}),
+    ("inception_v3_slim_old", {}),
+    ("inception_v3_slim_old", {"DTM_SIBLING_GROUP": "1", "DTM_ACT_HANDOFF": "1"}),
+    ("inception_v3_slim_old", {"DTM_SIBLING_GROUP": "0", "DTM_ACT_HANDOFF": "0"}),
+    ("inception_v3_slim_old", {"DTM_WGRAD_STREAM": "0"}),
+    ("vgg_16", {}),
+    ("vgg_16", {"DTM_WGRAD_STREAM": "0"}),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model,knobs", _DP_MATRIX, ids=lambda v: v if isinstance(v, str) else
+                         ("-".join("%s%s" % (k[4:].lower(), x) for k, x in v.items()) or "defaults"))
+def test_bsp_gpu_step1_gradients_match_single_rank(model, knobs):
+    from distributed_tensorflow_models_amd.utils import dp_check
+    single = run_workers(dp_check.grad_worker, 1, model, knobs)[0]
+    two = run_workers(dp_check.grad_worker, 2, model, knobs)
+    assert two[0]["launched"] == two[0]["buckets"] > 1 and two[0]["writes_checked"] > 0
+    if model == "vgg_16":
+        assert two[0]["compact"] == 1  # fc6's live window travels alone
+    rows = dp_check.compare(two[0], single)
+    bad = [r for r in rows if r[1] > 1e-5]
+    assert not bad, (len(bad), len(rows), bad[:6])
+    assert torch.equal(two[0]["params"], two[1]["params"])
+
+
+def test_bsp_check_catches_late_gradient_write():
+    """The BSP write checker: a ready notification before the gradient write (the defect class that drops a
+    write from the all-reduce) raises, naming the parameter."""
+    from distributed_tensorflow_models_amd.ops import nn as opsnn
+    from distributed_tensorflow_models_amd.parallel.bsp import BSPDataParallel
+    a, b = torch.nn.Parameter(torch.zeros(4)), torch.nn.Parameter(torch.zeros(3))
+    dp = BSPDataParallel([a, b], bucket_mb=1e-5, check=True, names=[("a", a), ("b", b)])
+    try:
+        dp.zero_grad()
+        opsnn.grad_target(b).add_(1.0)
+        opsnn._notify(b)  # b's bucket is complete -> issued
+        with pytest.raises(RuntimeError, match="gradient of b written after"):
+            opsnn.grad_target(b)
+        with pytest.raises(RuntimeError, match="b reported ready twice"):
+            opsnn._notify(b)
+        dp.finish()
+        assert dp.unreported == ["a"] and dp.writes_checked == 2
+    finally:
+        dp.close()
+
+
 def test_launcher_detects_hung_rank_and_resumes(tmp_path):
     """A rank that stops making progress (alive, silent) is caught by the heartbeat monitor; the job
     is stopped and restarted from the latest checkpoint."""

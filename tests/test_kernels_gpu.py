@@ -218,12 +218,12 @@ def test_conv_pipelined_tiles_match_reference(tile, prologue, case):
     assert _rel(stats[0], yf.sum(0)) < 1e-3 and _rel(stats[1], yf.square().sum(0)) < 1e-3
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 10, 11, 12, 13, 14, 15])
+@pytest.mark.parametrize("tile", [0, 1, 6, 10, 12])
 @pytest.mark.parametrize("case", [(4, 15, 15, 64, 96, 3, 2), (2, 14, 14, 128, 256, 3, 1), (3, 7, 7, 512, 200, 1, 1),
                                   (2, 9, 9, 24, 40, 3, 1), (5, 8, 8, 64, 64, 1, 1), (4, 9, 9, 256, 512, 3, 1),
                                   (3, 13, 13, 32, 32, 3, 1), (2, 11, 11, 32, 24, 3, 2)])
 def test_conv_wgrad_pipelined_tiles_match_reference(tile, case):
-    """The wgrad kernels - register-staged tiles 0-5 (64 / 128 rows x 128 / 256 columns) and the pipelined
+    """The wgrad kernels - register-staged tiles 0 / 1 / 6 (128 / 64 / 32 rows x 128 columns) and the pipelined
     LDS-DMA ones (inverse transposed-read image mapping for the DMA slots) - with split-K slabs against the
     fp32 reference, including K / R*S*C tails and empty splits."""
     import ctypes

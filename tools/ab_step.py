@@ -3,7 +3,7 @@
 median ms/step per variant; one device, one process: MI355X_MICROARCH 'DVFS give-back' / rule 24).
 
 VARIANTS="base=;noW=wtile:-3;noT=tile:-3;fused=prologue:fused" python tools/ab_step.py
-keys: tile (conv_nt tile id), w8 (0/1: the 8-wave 256x256 conv tile in the shape policy), kwide (0/1: 64-channel tiles for K % 128 <= 64), few (0/1: streaming few-row slab reduction), bnout (0/1: block-output BN backward in the consuming dgrad's epilogue), bnst (0/1: also for stride-2 unit outputs), b1x1 (0/1: one-pass 1x1 conv+BN backward), stemw (0/1: stem BN backward in the wgrad operand staging), sact (0/1: streaming 1x1 kernel for act dgrads), pcom (0/1: Inception pool branches as conv -> pool -> BN), sib (0/1: merged backward of sibling 1x1 convs), ahand (0/1: input-gradient hand-off between conv consumers of one activation), sibp (0/1: the commuted pool-branch conv joins the sibling group), sbwd (0/1: HIP backward of the pooled-BN statistics), catm (0/1: one-launch multi-part concat BN-apply), dec (0/1: stride-decomposed strided dgrads), dgrp (0/1: their parity classes as one grouped launch), wp64 (0/1/2: pipelined 64x128 wgrad tile for half-empty last 128-row tiles / also 33..64 outputs), k32 (0/1: 256x32 tile for <=32-channel spatial convs), cpt (16-B chunks per thread of the BN-stream grids), pol2 (0/1: v2 conv tile-policy rules), m32 (0/1: 32x32x16-MFMA forms of the LDS-DMA conv tiles), sstr (0/1/2: the stem forward as a persistent stream, 3- / 2-slot ring), wgs (0/1: conv+BN weight gradients on a side stream), scu (percent of the CUs the side-stream wgrads size their split-K grid for), wcu / swc (the same for the main-stream / stem wgrads), prio (0/1: eager step on a high-priority stream), dir3 (0/1: direct 3x3 kernel for C in {32, 64}), wwide (0/1/2: 64x256 register-staged wgrad tile for K <= 64, Kg > 128: never / always / BN-fused (stem) only), watom (max split count of the fp32-atomic split-K weight gradients; 0 = slabs + reduce), atile (tile id of the dgrads with a fused
+keys: tile (conv_nt tile id), w8 (0/1: the 8-wave 256x256 conv tile in the shape policy), kwide (0/1: 64-channel tiles for K % 128 <= 64), few (0/1: streaming few-row slab reduction), bnout (0/1: block-output BN backward in the consuming dgrad's epilogue), bnst (0/1: also for stride-2 unit outputs), b1x1 (0/1: one-pass 1x1 conv+BN backward), stemw (0/1: stem BN backward in the wgrad operand staging), sact (0/1: streaming 1x1 kernel for act dgrads), pcom (0/1: Inception pool branches as conv -> pool -> BN), sib (0/1: merged backward of sibling 1x1 convs), ahand (0/1: input-gradient hand-off between conv consumers of one activation), sibp (0/1: the commuted pool-branch conv joins the sibling group), sbwd (0/1: HIP backward of the pooled-BN statistics), catm (0/1: one-launch multi-part concat BN-apply), dec (0/1: stride-decomposed strided dgrads), dgrp (0/1: their parity classes as one grouped launch), k32 (0/1: 256x32 tile for <=32-channel spatial convs), cpt (16-B chunks per thread of the BN-stream grids), pol2 (0/1: v2 conv tile-policy rules), sstr (0/1/2: the stem forward as a persistent stream, 3- / 2-slot ring), wgs (0/1: conv+BN weight gradients on a side stream), scu (percent of the CUs the side-stream wgrads size their split-K grid for), wcu / swc (the same for the main-stream / stem wgrads), dir3 (0/1: direct 3x3 kernel for C in {32, 64}), atile (tile id of the dgrads with a fused
 activation-backward epilogue, -1 = policy), wtile[:occ] (wgrad tile id / blocks-per-CU target), prologue (DTM_PROLOGUE),
 stem (DTM_STEM: 1 = packed-row stem path), red (target_blocks:max_chunks[:direct_max] of the
 partial-sum reductions; 0 = legacy 256 rows per block; direct_max = largest BN-backward grid that
@@ -42,18 +42,13 @@ def apply(cfg):
     L.dtm_conv_set_policy2(int(cfg.get("pol2", "1")))
     L.dtm_set_grid_cpt(int(cfg.get("cpt", "8")))
     L.dtm_conv_set_k32(int(cfg.get("k32", "1")))
-    L.dtm_conv_set_mfma32(int(cfg.get("m32", os.environ.get("DTM_MFMA32", "0"))))
     L.dtm_conv_set_stem_stream(int(cfg.get("sstr", "1")))
     _lib.set_side_enabled(cfg.get("wgs", WGS_DEFAULT[0]) == "1")
     _lib.set_side_cu_fraction(float(cfg.get("scu", "75")) / 100.0)
     _lib.set_wgrad_cu_percent("main", cfg.get("wcu", "100"))
     _lib.set_wgrad_cu_percent("stem", cfg.get("swc", "100"))
-    L.dtm_conv_set_wgrad_atomic(int(cfg.get("watom", os.environ.get("DTM_WGRAD_ATOMIC", "0"))))
-    L.dtm_conv_set_wgrad_wide(int(cfg.get("wwide", "0")))
     L.dtm_conv_set_direct3(int(cfg.get("dir3", "1")))
     L.dtm_conv_set_dec_group(int(cfg.get("dgrp", "1")))
-    L.dtm_conv_set_wgrad_p64(int(cfg.get("wp64", "0")))
-    _lib.set_priority_enabled(cfg.get("prio", os.environ.get("DTM_PRIORITY_STREAM", "0")) == "1")
     sc = cfg.get("sc", "5:4096").split(":")
     L.dtm_set_sc_policy(int(sc[0]), int(sc[1]))
     os.environ["DTM_PROLOGUE"] = cfg.get("prologue", "auto")
