@@ -783,17 +783,21 @@ int dtm_bn_stats_finalize(const float* ws, int rows, int K, const float* gamma, 
   if (!dtm_device_ok()) return -9;
   const int k = dtm_ws_slot(st);
   if (K > g_fin_k[k]) {
-    hipDeviceSynchronize();
-    if (g_fin_acc[k]) hipFree(g_fin_acc[k]);
-    if (!g_fin_counter[k] && hipMalloc(&g_fin_counter[k], 64) != hipSuccess) return -4;
-    if (hipMalloc(&g_fin_acc[k], (size_t)2 * K * sizeof(float)) != hipSuccess) {
-      g_fin_acc[k] = nullptr;
-      g_fin_k[k] = 0;
+    // graph-safe growth (workspace.hip dtm_ws_get_stream): never inside a capture, the old accumulator kept
+    if (dtm_stream_capturing(st)) {
+      dtm_ws_set_error(-10);
       return -4;
     }
-    hipMemset(g_fin_acc[k], 0, (size_t)2 * K * sizeof(float));
-    hipMemset(g_fin_counter[k], 0, 64);
-    hipDeviceSynchronize();
+    unsigned* cnt = nullptr;
+    float* acc = nullptr;
+    if (hipMalloc(&cnt, 64) != hipSuccess) return -4;
+    if (hipMalloc(&acc, (size_t)2 * K * sizeof(float)) != hipSuccess) return -4;
+    // zeroed in stream order (kernels still queued on st keep using the old pair)
+    hipMemsetAsync(acc, 0, (size_t)2 * K * sizeof(float), st);
+    hipMemsetAsync(cnt, 0, 64, st);
+    if (g_fin_acc[k]) dtm_ws_note_retired();
+    g_fin_acc[k] = acc;
+    g_fin_counter[k] = cnt;
     g_fin_k[k] = K;
   }
   if (K % 2) return -1;  // float4 columns over [2K]

@@ -59,6 +59,9 @@ __host__ static inline FastDiv make_fastdiv(uint32_t d) {
 void dtm_reduce_rows(const float* ws, int rows, int width, int ld, float* out, hipStream_t st);
 constexpr int DTM_WS_SLOTS = 5;
 float* dtm_ws_get_stream(size_t floats, hipStream_t st);  // scratch arena of the stream's slot
+bool dtm_stream_capturing(hipStream_t st);  // st is being captured into a hipGraph
+void dtm_ws_set_error(int e);               // -10: growth refused during capture, -4: out of memory
+void dtm_ws_note_retired();
 int dtm_ws_slot(hipStream_t st);  // 0 = main, 1.. = registered side streams
 bool dtm_device_ok();  // false when called from another device than the first one used
 void dtm_reduce_split(int rows, int xblocks, int* rpb, int* ychunks);

@@ -4,7 +4,8 @@
 // `reduce_rows` then sums the rows with a handful of atomics per output.  (fp32 atomics from
 // thousands of workgroups onto the same few hundred addresses serialise at the memory-side
 // atomic units -- measured 10-100x slower on MI355X than this two-stage form.)
-// The arena grows on first use (warm-up step, before any hipGraph capture) and is reused.
+// The arena grows on first use (warm-up step, before any hipGraph capture) and is reused; retired arenas are
+// never freed (see dtm_ws_get_stream).
 #include "common.h"
 
 // One arena per stream class: slot 0 serves every stream not registered as a side stream, slots
@@ -36,20 +37,40 @@ bool dtm_device_ok() {
 }
 DTM_API int dtm_device_check() { return dtm_device_ok() ? 0 : -9; }
 
+// Growth is hipGraph-safe: a captured graph holds raw pointers into whatever arena was current at capture
+// time, so a retired arena is never freed (it stays allocated until process exit; growth is rare and happens
+// in the warm-up steps), and growth while the stream is being captured is refused (hipMalloc is not a legal
+// call inside a global-mode capture; the caller's -4 surfaces as dtm_ws_last_error() == -10: run the eager
+// warm-up steps at the captured shapes first).  Freeing the old arena after a device sync used to leave an
+// earlier captured graph pointing into freed memory (illegal address on replay, profiles/ab/README.md round 3).
+static int g_ws_err = 0;
+static long g_ws_retired = 0;
+DTM_API int dtm_ws_last_error() { return g_ws_err; }
+DTM_API long dtm_ws_retired() { return g_ws_retired; }
+bool dtm_stream_capturing(hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) return false;
+  return cs != hipStreamCaptureStatusNone;
+}
+void dtm_ws_set_error(int e) { g_ws_err = e; }
+void dtm_ws_note_retired() { ++g_ws_retired; }
+
 float* dtm_ws_get_stream(size_t floats, hipStream_t st) {
   if (!dtm_device_ok()) return nullptr;
   const int k = dtm_ws_slot(st);
   if (floats > g_ws_floats[k]) {
-    size_t n = floats < (16u << 20) ? (16u << 20) : floats;  // >= 64 MB
-    if (g_ws[k]) {
-      hipDeviceSynchronize();
-      hipFree(g_ws[k]);
-    }
-    if (hipMalloc(&g_ws[k], n * sizeof(float)) != hipSuccess) {
-      g_ws[k] = nullptr;
-      g_ws_floats[k] = 0;
+    if (dtm_stream_capturing(st)) {
+      g_ws_err = -10;
       return nullptr;
     }
+    size_t n = floats < (16u << 20) ? (16u << 20) : floats;  // >= 64 MB
+    float* p = nullptr;
+    if (hipMalloc(&p, n * sizeof(float)) != hipSuccess) {
+      g_ws_err = -4;
+      return nullptr;
+    }
+    if (g_ws[k]) ++g_ws_retired;  // (kept: in-flight kernels and captured graphs may still use it)
+    g_ws[k] = p;
     g_ws_floats[k] = n;
   }
   return g_ws[k];
@@ -190,3 +211,9 @@ void dtm_reduce_rows(const float* ws, int rows, int width, int ld, float* out, h
 }
 
 DTM_API int dtm_ws_reserve(long floats) { return dtm_ws_get_stream((size_t)floats, nullptr) ? 0 : -1; }
+// the arena of the stream's slot: grow to >= floats (0, or -4 with dtm_ws_last_error() -10 / -4) / its capacity
+DTM_API int dtm_ws_reserve_stream(long floats, void* stream) {
+  g_ws_err = 0;
+  return dtm_ws_get_stream((size_t)floats, (hipStream_t)stream) ? 0 : -4;
+}
+DTM_API long dtm_ws_capacity(void* stream) { return (long)g_ws_floats[dtm_ws_slot((hipStream_t)stream)]; }

@@ -101,6 +101,10 @@ _SIGS = {
     "dtm_bn_finalize_bwd": (None, [_P, _P, _P, _P, _P, _P, _I, _F, _P]),
     "dtm_lrn": (_I, [_P, _P, _P, _L, _I, _I, _F, _F, _F, _I, _P]),
     "dtm_ws_reserve": (_I, [_L]),
+    "dtm_ws_last_error": (_I, []),
+    "dtm_ws_retired": (_L, []),
+    "dtm_ws_reserve_stream": (_I, [_L, _P]),
+    "dtm_ws_capacity": (_L, [_P]),
     "dtm_depthwise_fwd": (_I, [_P, _P, _P, _P, _P]),
     "dtm_depthwise_dgrad": (_I, [_P, _P, _P, _P, _P]),
     "dtm_depthwise_wgrad": (_I, [_P, _P, _P, _P, _P]),

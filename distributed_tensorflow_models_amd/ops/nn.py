@@ -106,6 +106,10 @@ def _check(rc, what):
     if rc == -9:
         raise RuntimeError("%s: the kernel library's device state belongs to another device (one process per "
                            "GPU; csrc/kernels/workspace.hip dtm_device_ok)" % what)
+    if rc == -4 and _lib.lib().dtm_ws_last_error() == -10:
+        raise RuntimeError("%s: its scratch arena would have to grow while the stream is being captured into a "
+                           "hipGraph (run eager warm-up steps at the captured shapes first; "
+                           "csrc/kernels/workspace.hip dtm_ws_get_stream)" % what)
     if rc != 0:
         raise RuntimeError("%s failed with code %d" % (what, rc))
 
@@ -161,6 +165,9 @@ def weight_flipped(w, K, R, S, C, dec=None):
     return wt
 
 
+_RETIRED = []  # device tables a captured graph may still point into (kept for the process lifetime)
+
+
 def refresh_flipped(stream=None):
     """After a weight update: one batched launch re-deriving every registered dgrad copy."""
     WEIGHT_VERSION[0] += 1
@@ -182,6 +189,9 @@ def refresh_flipped(stream=None):
             st, ph, pw = d if d is not None else (1, 0, 0)
             tab[i, 4:6] = np.array([st, ph, pw, 0], dtype=np.int32).view(np.int64)
         dev_tab = torch.from_numpy(tab.view(np.uint8).reshape(-1).copy()).to(entries[0][0].device)
+        if cache is not None:
+            # a captured hipGraph may hold the old table's pointer (its refresh launch): never free it
+            _RETIRED.append(cache[1])
         refresh_flipped.table = cache = (key, dev_tab, len(entries))
     L.dtm_weight_flip_transpose_batched(_lib.ptr(cache[1]), cache[2], stream or _lib.stream_ptr())
     for w, wt, d in entries:

@@ -183,12 +183,15 @@ class BSPDataParallel:
         self.unreported = []
 
     def _on_accumulated(self, p):
-        # plain autograd path (CPU ops / torch fallbacks): move .grad into the flat buffer
-        if p.grad is not None:
-            if self.check:
-                self._on_write(p)
-            p.main_grad.add_(p.grad.to(p.main_grad.dtype))
-            p.grad = None
+        # plain autograd path (CPU ops / torch fallbacks): move .grad into the flat buffer.  (autograd also
+        # runs this hook with no .grad when a HIP op already wrote main_grad and returned None for p: that
+        # op notified p itself)
+        if p.grad is None:
+            return
+        if self.check:
+            self._on_write(p)
+        p.main_grad.add_(p.grad.to(p.main_grad.dtype))
+        p.grad = None
         self._on_ready(p)
 
     def _pname(self, p):
@@ -325,20 +328,25 @@ def flatten_tensors(tensors):
 
 
 class BufferSync:
-    """Replica-consistent BN moving statistics under BSP.
+    """Replica-consistent BN moving statistics under BSP, with the reference's update semantics.
 
-    In the reference every worker's BN update op writes the ONE PS-resident ``moving_mean`` /
-    ``moving_variance`` (inception/imagenet_inception_bsp.py:145-149; slim BN puts them in
-    UPDATE_OPS, inception/slim/ops.py:117-131), so there is a single set of moving statistics for
-    the whole job, and it is what the checkpoint and eval see.  Here each replica updates its own
-    copy from its local batch in forward; this class keeps the replicas identical: the statistics
-    live in one flat fp32 buffer (``flatten_tensors``), whose SUM all-reduce is issued right after
-    forward (they are final then; backward never reads them), so the collective runs on the comm
-    stream underneath the whole backward, and ``finish`` waits and scales by 1/W.  The result is
-    ``m <- d*m + (1-d)*mean_r(batch_stat_r)`` on every rank - the reference's update with the
-    average of the workers' batch statistics.  EMA shadows of the statistics are updated by the
-    optimizer from the averaged values, so they stay replica-identical without a collective of
-    their own.  ``every`` > 1 syncs only every k-th step (cheaper; replicas drift in between)."""
+    In the reference every worker's BN update op (``AssignMovingAvg`` in UPDATE_OPS, run as control
+    dependencies of each worker's train op: inception/imagenet_inception_bsp.py:145-149,
+    inception/slim/ops.py:117-131) writes the ONE PS-resident ``moving_mean`` / ``moving_variance``, so one
+    global step applies W updates m <- d*m + (1-d)*b_r, one per worker batch, to a single copy - the same as
+    the ASP store here (parallel/asp.py push_buffers: each worker adds its forward's delta).  Here each replica
+    updates its own copy in its forward; this class makes every replica end the step with
+        m = m_prev + sum_r (m_r - m_prev) = m_prev + (1 - d) * sum_r (b_r - m_prev),
+    the W sequential updates to first order in (1 - d) (exact for W = 1; the second-order terms are
+    O((1-d)^2), ~1e-5 relative at d = 0.997), instead of one update with the averaged batch statistics (which
+    would adapt W times slower per step than the reference).
+    Mechanics: the statistics live in one flat fp32 buffer (``flatten_tensors``); ``begin`` snapshots it
+    before the forward, ``issue`` (right after the forward: the statistics are final then, backward never
+    reads them) turns the buffer into this replica's delta and issues its SUM all-reduce, which runs on the
+    comm stream underneath the whole backward; ``finish`` waits and adds the snapshot back.  EMA shadows of
+    the statistics are updated by the optimizer from the synced values, so they stay replica-identical
+    without a collective of their own.  ``every`` > 1 syncs only every k-th step (replicas drift in between;
+    the skipped steps' local deltas are folded into the next synced step's delta)."""
 
     def __init__(self, buffers, process_group=None, every=1):
         self.pg = process_group
@@ -346,8 +354,13 @@ class BufferSync:
         self.buffers = [b for b in buffers]
         self.every = max(1, int(every))
         self.flat = flatten_tensors(self.buffers) if (self.world > 1 and self.buffers) else None
+        # the statistics as of the last sync (every replica holds the same values there)
+        self.prev = self.flat.detach().clone() if self.flat is not None else None
         self._work = None
         self._n = 0
+
+    def begin(self):
+        """(kept for API symmetry: the snapshot is the state after the last sync, see finish)"""
 
     def issue(self):
         if self.flat is None:
@@ -356,6 +369,7 @@ class BufferSync:
         if (self._n - 1) % self.every:
             return
         with roctx("bn_stats_allreduce"):
+            self.flat.sub_(self.prev)  # this replica's delta since the last sync
             self._work = dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
     def finish(self):
@@ -363,7 +377,13 @@ class BufferSync:
             return
         self._work.wait()
         self._work = None
-        self.flat.mul_(1.0 / self.world)
+        self.flat.add_(self.prev)
+        self.prev.copy_(self.flat)
+
+    def resync(self):
+        """The statistics were overwritten outside a step (checkpoint restore, broadcast): re-snapshot."""
+        if self.flat is not None:
+            self.prev.copy_(self.flat)
 
     def numel(self):
         return 0 if self.flat is None else self.flat.numel()

@@ -15,6 +15,7 @@ import os
 import shutil
 import time
 
+import numpy as np
 import torch
 
 from .ckpt.saver import Saver, TFVar, model_variables
@@ -146,6 +147,10 @@ def define_common_flags(flags, preset):
             ("seed", I, 0, "random seed"),
             ("depth_multiplier", Fl, 1.0, "MobileNet depth multiplier"),
             ("fine_tune_checkpoint", S, "", "initialise model variables from this checkpoint (fresh runs only)"),
+            ("train_accuracy_every", I, p.get("train_accuracy_every", 0),
+             "chief: every N steps, accuracy of the training-mode network on a fed batch of distorted training "
+             "images (reference resnet/cifar10_resnet_bsp.py:146-148; 0 = off)"),
+            ("train_accuracy_batch", I, 10000, "images in that fed batch (the reference feeds 10000)"),
     ):
         fn(name, default, h)
         flags.FLAGS.reset(name)  # the entry script's preset defaults win
@@ -297,6 +302,7 @@ def train(preset, flags, default_mode="bsp"):
                                  [b for b in model.buffers()])
         from .ops.nn import invalidate_weight_copies
         invalidate_weight_copies(model.parameters())  # bf16 compute copies follow the restored weights
+        step_fn.bufsync.resync()  # the BN statistics' sync snapshot follows the restored / broadcast values
         step_fn.global_step = int(gstep)
         step_fn.opt.num_updates = int(gstep)
     elif mode in ("asp", "ssp"):
@@ -358,6 +364,7 @@ def train(preset, flags, default_mode="bsp"):
 
     # ---- loop (reference hot loop) ------------------------------------------------
     step = start if mode == "bsp" else 0
+    probe = None  # the --train_accuracy_every input pipeline (created on first use)
     loss_v = float("nan")
     t_log, n_since = time.time(), 0
     while step < FLAGS.max_steps:
@@ -395,6 +402,11 @@ def train(preset, flags, default_mode="bsp"):
         if cfg.get("nan_guard") and math.isnan(loss_v):  # imagenet_inception_bsp.py:191
             raise FloatingPointError("Model diverged with loss = NaN")
         if mode == "bsp" and need_log and step_fn.poll_skipped():
+            if cfg.get("nan_guard"):
+                # the reference asserts on a NaN loss every step; here the device-side guard skipped the update
+                # of a non-finite step and the check fires at the next log line (at most --log_every steps late)
+                raise FloatingPointError("Model diverged with loss = NaN (non-finite gradients at a step since "
+                                         "the last log line; %d update(s) skipped)" % step_fn.skipped)
             logging.warning("step %d: non-finite gradients since the last log line, update(s) skipped (%d so far)",
                             step, step_fn.skipped)
         gstep.fill_(gs)
@@ -418,11 +430,12 @@ def train(preset, flags, default_mode="bsp"):
             metrics.write(step=step, global_step=gs, loss=loss_v, lr=sched(gs), images_per_sec=B / max(dt, 1e-9),
                           node_images_per_sec=world * B / max(dt, 1e-9), step_ms=dt * 1e3, world=world, mode=mode,
                           **extra)
-        if cfg.get("train_accuracy_every") and step % cfg["train_accuracy_every"] == 0 and is_chief:
-            with torch.no_grad():
-                out = model(images, training=False)
-                acc = (out.float().argmax(-1) == labels).float().mean().item()
-            logging.info("train-batch precision @ 1 = %.3f", acc)
+        if FLAGS.train_accuracy_every and step % FLAGS.train_accuracy_every == 0 and is_chief:
+            if probe is None:
+                probe = make_input(cfg, FLAGS.train_accuracy_batch, device, FLAGS, rank + 7919)
+            acc = train_accuracy_probe(model, probe)
+            # tf.logging.info('evaluation: step - '+str(step)+'; accuracy: '+ str(accuracy))
+            logging.info("evaluation: step - %d; accuracy: %s", step, str(np.float32(acc)))
         if mode == "bsp" or is_chief:
             sv.maybe_save(gs, force=bool(FLAGS.save_every_steps) and gs % FLAGS.save_every_steps == 0)
         heartbeat.beat(step)
@@ -441,6 +454,27 @@ def train(preset, flags, default_mode="bsp"):
         store.close()
     pg.barrier()
     return 0
+
+
+def train_accuracy_probe(model, data):
+    """The reference's training-set accuracy probe (resnet/cifar10_resnet_bsp.py:66-70,146-148): accuracy_op =
+    mean(argmax(network(inputs, True)) == labels) run on one fed batch of distorted training images - the
+    network in TRAINING mode (batch statistics), whose BN moving averages that sess.run leaves alone (the
+    reference never runs UPDATE_OPS there).  Here the moving statistics are saved and restored around the
+    forward (the fused training-mode kernels update them in place)."""
+    from .engine import moving_average_buffers
+    bufs = moving_average_buffers(model)
+    saved = [b.detach().clone() for b in bufs]
+    images, labels = data.next_batch()
+    with torch.no_grad():
+        out = model(images, training=True)
+        if isinstance(out, tuple):
+            out = out[0]
+        from .ops.lazy import as_tensor
+        acc = (as_tensor(out).float().argmax(-1) == labels).float().mean().item()
+        for b, v in zip(bufs, saved):
+            b.copy_(v)
+    return acc
 
 
 def build_model_for_eval(preset, flags_values=None, **kw):

@@ -378,7 +378,7 @@ def test_asp_gpu_ipc_fused_push(kind):
 # ---------------------------------------------------------------------------------------------
 # BN moving statistics under BSP: the reference keeps ONE PS-resident copy that every worker's
 # update op writes (inception/imagenet_inception_bsp.py:145-149); here every replica must end each
-# step with the same statistics = the average of what the replicas computed from their own batches.
+# step with the same statistics = the pre-step value plus every replica's update of it.
 
 def _bn_sync_worker(rank, world, steps=3):
     import copy
@@ -390,6 +390,7 @@ def _bn_sync_worker(rank, world, steps=3):
     step = TrainStep(model, optimizer="momentum", lr=0.05, momentum=0.9, ema_decay=0.99, bucket_mb=0.05)
     g = torch.Generator().manual_seed(100 + rank)  # a DIFFERENT batch on every rank
     local, synced = [], []
+    init = torch.cat([b.reshape(-1) for b in moving_average_buffers(model)]).clone()
     for _ in range(steps):
         x, y = torch.randn(4, 32, 32, 3, generator=g) * (1 + rank), torch.randint(0, 10, (4,), generator=g)
         shadow = copy.deepcopy(model)  # what this replica's forward alone makes of the statistics
@@ -399,7 +400,7 @@ def _bn_sync_worker(rank, world, steps=3):
         step(x, y)
         synced.append(torch.cat([b.reshape(-1) for b in moving_average_buffers(model)]).clone())
     shadows = torch.cat([s.reshape(-1) for _b, s in step.opt.buffer_shadows()])
-    return {"local": torch.stack(local), "synced": torch.stack(synced), "shadows": shadows,
+    return {"local": torch.stack(local), "synced": torch.stack(synced), "shadows": shadows, "init": init,
             "flat": step.bufsync.numel(), "nbuf": len(moving_average_buffers(model))}
 
 
@@ -411,9 +412,12 @@ def test_bsp_bn_moving_statistics_replica_consistent():
     assert torch.equal(res[0]["shadows"], res[1]["shadows"])
     # the ranks saw different data, so their own statistics differ ...
     assert not torch.allclose(res[0]["local"][0], res[1]["local"][0])
-    # ... and the synced value is their average (from the same pre-step state on both ranks)
-    mean = (res[0]["local"] + res[1]["local"]) / 2
-    torch.testing.assert_close(res[0]["synced"], mean, rtol=1e-5, atol=1e-6)
+    # ... and the synced value applies BOTH replicas' updates to the one shared copy, as the reference's W
+    # per-worker AssignMovingAvg ops on the PS variable do (first order in 1 - decay): prev + sum_r delta_r,
+    # from the same pre-step state on both ranks
+    prev = torch.cat([res[0]["init"][None], res[0]["synced"][:-1]])
+    want = prev + (res[0]["local"] - prev) + (res[1]["local"] - prev)
+    torch.testing.assert_close(res[0]["synced"], want, rtol=1e-5, atol=1e-6)
 
 
 def test_bsp_single_rank_keeps_buffers_unflattened():

@@ -212,3 +212,59 @@ def test_bsp_bucket_layout_small_tail():
         assert sum(n for p in dp.params for _, n in dp.contrib[p]) == dp.flat.numel()
     finally:
         dp.close()
+
+
+@pytest.mark.gpu
+def test_scratch_growth_refused_inside_capture_and_graph_safe_after():
+    """Scratch arenas never grow inside a hipGraph capture (a clear error instead of a hipMalloc in the
+    captured region) and never free a retired arena (a graph captured earlier may point into it)."""
+    from distributed_tensorflow_models_amd.ops import _lib
+    from distributed_tensorflow_models_amd.ops.nn import _check
+    L = _lib.lib()
+    torch.cuda.synchronize()
+    cap = int(L.dtm_ws_capacity(_lib.stream_ptr()))
+    g = torch.cuda.CUDAGraph()
+    t = torch.zeros(16, device="cuda")
+    with torch.cuda.graph(g):
+        t.add_(1.0)  # (a non-empty capture)
+        rc = L.dtm_ws_reserve_stream(cap + 1, _lib.stream_ptr())
+        err = L.dtm_ws_last_error()
+        with pytest.raises(RuntimeError, match="captured into a hipGraph"):
+            _check(rc, "probe")
+    assert rc == -4 and err == -10
+    r0 = int(L.dtm_ws_retired())
+    assert L.dtm_ws_reserve_stream(cap + 1, _lib.stream_ptr()) == 0  # eager: grows
+    assert int(L.dtm_ws_capacity(_lib.stream_ptr())) > cap and int(L.dtm_ws_retired()) == r0 + (1 if cap else 0)
+
+
+@pytest.mark.gpu
+def test_hipgraph_replay_after_larger_eager_step_matches_eager():
+    """Capture a ResNet step, then run a much larger eager step in the same process (the scratch arenas and the
+    flip-refresh table grow), then keep replaying: the replayed trajectory still follows the eager one (the
+    round-3 illegal-address-after-capture mode: a captured graph pointing into a freed arena)."""
+    from distributed_tensorflow_models_amd.ops import _lib
+    le, pe, _, _ = _run_steps("resnet_v1_50", False, 6, 64, 16)
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = nets_factory.build("resnet_v1_50", num_classes=16).to(dev)
+    step = TrainStep(model, optimizer="momentum", lr=0.05, momentum=0.9, use_graph=True)
+    g = torch.Generator().manual_seed(3)
+    xs = [torch.randn(4, 64, 64, 3, generator=g).to(dev, torch.bfloat16) for _ in range(2)]
+    ys = [torch.randint(0, 16, (4,), generator=g).to(dev) for _ in range(2)]
+    losses = [float(step(xs[i % 2], ys[i % 2])) for i in range(3)]
+    assert step._graph is not None
+    # a second model, eager, at 16x the pixels and 8x the batch: every growable arena grows
+    r0 = int(_lib.lib().dtm_ws_retired())
+    other = nets_factory.build("resnet_v1_50", num_classes=1000).to(dev)
+    big = TrainStep(other, optimizer="momentum", lr=0.01, momentum=0.9)
+    big(torch.randn(32, 256, 256, 3, device=dev).to(torch.bfloat16), torch.randint(0, 1000, (32,), device=dev))
+    torch.cuda.synchronize()
+    assert int(_lib.lib().dtm_ws_retired()) > r0
+    big.dp.close()
+    del big, other
+    losses += [float(step(xs[i % 2], ys[i % 2])) for i in range(3, 6)]
+    torch.cuda.synchronize()
+    params = torch.cat([p.detach().float().reshape(-1) for p in model.parameters()])
+    step.dp.close()
+    assert losses == pytest.approx(le, rel=2e-2, abs=2e-3)
+    assert ((params - pe).norm() / pe.norm()).item() < 1e-3

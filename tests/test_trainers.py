@@ -141,3 +141,29 @@ def test_training_tb_scalars(tmp_path):
     blob = open(os.path.join(d, ev[0]), "rb").read()
     for tag in (b"learning_rate", b"total_loss (raw)", b"total_loss", b"images_per_sec"):
         assert tag in blob
+
+
+def test_resnet_training_accuracy_probe(tmp_path):
+    """ResNet-CIFAR: every --train_accuracy_every steps the chief logs the reference's line
+    'evaluation: step - N; accuracy: X' for the training-mode network on a fed batch of distorted training
+    images (resnet/cifar10_resnet_bsp.py:146-148; 10,000 images by default, 32 here)."""
+    d = str(tmp_path / "train")
+    out = _run("cifar10_resnet_bsp", "--max_steps=3", "--batch_size=4", "--train_dir=" + d, "--data_dir=/nonexistent",
+               "--train_accuracy_every=2", "--train_accuracy_batch=32", "--resnet_size=8")
+    lines = [l for l in out.splitlines() if "evaluation: step - " in l]
+    assert len(lines) == 2 and "evaluation: step - 0; accuracy: " in lines[0] and "step - 2;" in lines[1], out[-2000:]
+    acc = float(lines[0].rsplit("accuracy: ", 1)[1])
+    assert 0.0 <= acc <= 1.0
+
+
+def test_training_accuracy_probe_leaves_moving_statistics():
+    from distributed_tensorflow_models_amd.data.synthetic import SyntheticImages
+    from distributed_tensorflow_models_amd.engine import moving_average_buffers
+    from distributed_tensorflow_models_amd.models import nets_factory
+    from distributed_tensorflow_models_amd.trainer import train_accuracy_probe
+    torch.manual_seed(0)
+    model = nets_factory.build("cifar10_resnet_v2", num_classes=10, resnet_size=8)
+    before = [b.clone() for b in moving_average_buffers(model)]
+    acc = train_accuracy_probe(model, SyntheticImages(16, 32, 32, 3, 10, "cpu", dtype=torch.float32))
+    assert 0.0 <= acc <= 1.0
+    assert all(torch.equal(a, b) for a, b in zip(before, moving_average_buffers(model)))
