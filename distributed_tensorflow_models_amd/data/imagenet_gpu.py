@@ -171,10 +171,15 @@ def _shm_worker(wid, nworkers, files, seed, split, train, nthreads, shm_name, ns
 class _ShmDecoders:
     """N decoder processes, each with a ring of shared-memory slots (see _shm_worker)."""
 
-    def __init__(self, files, n, seed, split, train, nthreads, nslots=6, slot_mb=24, per_slot=16):
+    def __init__(self, files, n, seed, split, train, nthreads, nslots=None, slot_mb=24, per_slot=16, batch=0):
         import multiprocessing as mp
         from multiprocessing import shared_memory
         ctx = mp.get_context("spawn")  # never fork a process that may hold a HIP context
+        # enough slots that a batch normally fits in what the workers own with one slot each left to fill
+        # (the assembler's copy-out under pressure, detach_worker, covers the rest: large images fill a slot
+        # with fewer than per_slot items)
+        if nslots is None:
+            nslots = max(6, -(-int(batch) // max(1, n * per_slot)) + 2)
         self.n, self.nslots, self.slot_bytes = n, nslots, int(slot_mb * (1 << 20))
         self.stop = ctx.Event()
         self.done_q = ctx.Queue()
@@ -194,6 +199,7 @@ class _ShmDecoders:
             p.start()
             self.procs.append(p)
         self.refs = {}
+        self.detached = 0  # items copied out of shared memory under slot pressure (detach_worker)
 
     def items(self, msg):
         """(wid, slot, meta) -> decoded items in the pool format, views into the slot (release after use)."""
@@ -230,6 +236,25 @@ class _ShmDecoders:
         if self.refs[key] == 0:
             del self.refs[key]
             self.free_q[key[0]].put(key[1])
+
+    def held(self, wid):
+        """Slots of worker ``wid`` the assembler still holds items in."""
+        return sum(1 for k in self.refs if k[0] == wid)
+
+    def detach_worker(self, items, wid):
+        """Copy the payloads of ``items`` (a mutable sequence of pool-format items) that live in worker wid's
+        slots out of shared memory and release those slots.  Called when the assembler holds all but one of
+        a worker's slots: a worker with no free slot blocks, and if the batch still needs its items the
+        pipeline would stall for good (large images, or a batch larger than the slots can hold)."""
+        for i, d in enumerate(items):
+            key = d[4]
+            if key is None or key[0] != wid:
+                continue
+            px = d[0].copy() if d[0] is not None else None
+            coef = (d[3][0], d[3][1].copy()) if d[3] is not None else None
+            items[i] = (px, d[1], d[2], coef, None)
+            self.release(key)
+            self.detached += 1
 
     def close(self):
         self.stop.set()
@@ -306,7 +331,7 @@ class GPUBatchInputs:
 
     def __init__(self, dataset, batch_size, train=True, image_size=299, num_preprocess_threads=4, num_readers=4,
                  num_decoders=8, seed=0, device="cuda", shuffle_buffer=1024, prefetch=2, decode_processes=None,
-                 split_decode=None):
+                 split_decode=None, shm_kw=None):
         self.files = dataset.data_files()
         # split JPEG decode (host Huffman + device IDCT / colour, data/jpeg.py; bit-exact with PIL): opt-in
         # (DTM_SPLIT_DECODE=1).  Measured on one MI355X box with 16 decoder processes
@@ -340,7 +365,8 @@ class GPUBatchInputs:
         if decode_processes:
             # decoder processes read their own shards and return results through shared memory (the
             # record / pixel pickling of a process pool capped the pipeline at ~4k img/s per box)
-            self.workers = _ShmDecoders(self.files, self.ndec, seed, self.split, train, self.nthreads)
+            self.workers = _ShmDecoders(self.files, self.ndec, seed, self.split, train, self.nthreads,
+                                        batch=batch_size, **(shm_kw or {}))
             t = threading.Thread(target=self._assemble_shm, daemon=True)
             t.start()
             self.threads.append(t)
@@ -486,6 +512,10 @@ class GPUBatchInputs:
                         W.release(d[4])
                     else:
                         done.append(d)
+                if len(done) < self.B and W.held(msg[0]) >= W.nslots - 1:
+                    # the worker is down to its last slot while the batch still needs more items: copy this
+                    # worker's pending items out of shared memory so it can keep decoding (no deadlock)
+                    W.detach_worker(done, msg[0])
             if len(done) < self.B:
                 continue
             dec = [done.popleft() for _ in range(self.B)]

@@ -259,6 +259,35 @@ def test_gpu_pipeline_assembler_host_side(tmp_path):
     assert seen == set(range(1, 13))  # both decoder processes' shards arrive
 
 
+@pytest.mark.timeout(180)
+def test_gpu_pipeline_shm_slots_never_starve(tmp_path):
+    """Decoder processes with fewer shared-memory slots than a batch needs (2 slots of 1 item per worker, batch
+    of 12 from 2 workers): the assembler copies a worker's pending items out once it holds all but one of its
+    slots, so batches keep coming instead of every worker blocking on a free slot (advisor finding, round 3)."""
+    from PIL import Image
+
+    from distributed_tensorflow_models_amd.data import imagenet_gpu
+    out = tmp_path / "d"
+    out.mkdir()
+    rng = np.random.RandomState(0)
+    for shard in range(2):
+        with TFRecordWriter(str(out / ("train-%05d-of-00002" % shard))) as w:
+            for i in range(8):
+                b = io.BytesIO()
+                Image.fromarray((rng.rand(24, 24, 3) * 255).astype(np.uint8)).save(b, format="JPEG")
+                w.write(encode_example({"image/encoded": b.getvalue(), "image/class/label": shard * 8 + i + 1}))
+    ds = imagenet.ImagenetData("train", str(out))
+    bi = imagenet_gpu.GPUBatchInputs(ds, 12, train=True, image_size=16, num_readers=1, num_decoders=2, seed=3,
+                                     device="cpu", decode_processes=True, split_decode=False,
+                                     shm_kw=dict(nslots=2, per_slot=1))
+    try:
+        got = [bi.ready.get(timeout=60) for _ in range(3)]
+    finally:
+        bi.close()
+    assert all(len(g[2]) == 12 for g in got)
+    assert bi.workers.detached > 0
+
+
 @pytest.mark.timeout(120)
 def test_imagenet_eval_pipeline_loops_and_skips_corrupt_records(tmp_path):
     """Eval readers loop over the files like string_input_producer (no num_epochs): more batches than
