@@ -18,6 +18,7 @@ weights -> push (apply this worker's gradient to the owner shard with the TF upd
 averaging, no barrier).  ``global_step`` is an atomic counter in the TCPStore, incremented once
 per worker step (TF ASP semantics).  Concurrent pushes to one shard race exactly as Hogwild does.
 """
+import datetime
 import os
 import pickle
 import time
@@ -34,6 +35,22 @@ STORE_PREFIX = "dtm_asp"
 def owner_map(params, world):
     """Round-robin tensor -> owner rank (replica_device_setter semantics, C14)."""
     return {i: i % world for i in range(len(params))}
+
+
+def _enable_peer_access(me, peers):
+    """hipDeviceEnablePeerAccess(peer) from device ``me``'s context for every peer (already-enabled is fine)."""
+    import ctypes
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+    except OSError:
+        return False
+    if hip.hipSetDevice(ctypes.c_int(me)) != 0:
+        return False
+    for d in peers:
+        rc = hip.hipDeviceEnablePeerAccess(ctypes.c_int(d), ctypes.c_uint(0))
+        if rc not in (0, 704):  # hipSuccess, hipErrorPeerAccessAlreadyEnabled
+            return False
+    return True
 
 
 class ParamStore:
@@ -129,20 +146,20 @@ class ParamStore:
             self._local16[k] = flatten_tensors(w16) if w16 else None
 
     def _negotiate_ipc(self):
-        """Owner shards are written from other GPUs over xGMI: every rank checks that its device can
-        access every other rank's device; if any pair cannot, ALL ranks fall back to the host
-        (/dev/shm) store - the decision is collective, since the owners' allocations depend on it."""
+        """Owner shards are written from other GPUs over xGMI: the ranks exchange their device indices
+        through the store, every rank checks (and enables, from its own device) peer access to the OTHER
+        ranks' devices only; if any pair cannot, ALL ranks fall back to the host (/dev/shm) store - the
+        decision is collective, since the owners' allocations depend on it.  Nothing is allocated on a peer
+        device (no extra HIP context / HBM there)."""
         me = self.params[0].device.index
-        ndev = torch.cuda.device_count()
-        ok = True
-        for d in range(ndev):
-            if d != me and not torch.cuda.can_device_access_peer(me, d):
-                ok = False
-        if ok:
-            for d in range(ndev):  # enable peer access now (torch turns it on with a first P2P copy)
-                if d != me:
-                    torch.empty(1, device=d).copy_(torch.zeros(1, device=me))
         key = "%s/%s/p2p" % (STORE_PREFIX, self.run_id)
+        self.store.set("%s_dev%d" % (key, self.rank), str(me))
+        self.store.wait(["%s_dev%d" % (key, r) for r in range(self.world)], datetime.timedelta(seconds=300))
+        peers = sorted({int(self.store.get("%s_dev%d" % (key, r))) for r in range(self.world)} - {me})
+        ok = all(torch.cuda.can_device_access_peer(me, d) for d in peers)
+        if ok and peers:
+            ok = _enable_peer_access(me, peers)
+        self.peers = peers
         self.store.add(key + "_n", 1)
         if not ok:
             self.store.add(key + "_bad", 1)
@@ -157,6 +174,7 @@ class ParamStore:
                 "ASP: peer access between the ranks' GPUs is unavailable; using the host (/dev/shm) store")
             return "shm"
         return "ipc"
+
     def _open_flat(self, k, total, init_from):
         if self.mode == "shm":
             path = "/dev/shm/%s_%s_owner%d" % (STORE_PREFIX, self.run_id, k)
