@@ -64,6 +64,7 @@ void dtm_ws_set_error(int e);               // -10: growth refused during captur
 void dtm_ws_note_retired();
 int dtm_ws_slot(hipStream_t st);  // 0 = main, 1.. = registered side streams
 bool dtm_device_ok();  // false when called from another device than the first one used
+int dtm_compute_cus();  // CUs the persistent / split-K grids size for: the device's CUs minus the reserved ones
 void dtm_reduce_split(int rows, int xblocks, int* rpb, int* ychunks);
 int dtm_reduce_direct_max();
 int dtm_ntld_bits();  // non-temporal input-load policy of the BN-apply kernels (fused_bn.hip)  // grids up to this many blocks reduce with atomics in the producer

@@ -300,16 +300,13 @@ __global__ __launch_bounds__(512) void conv1x1_bnbwd_kernel(Bwd1x1Args a) {
 using namespace dtm;
 
 static int bwd1x1_blocks(int ntiles) {
-  static int cap = 0;
-  if (!cap) {
-    int occ = 0, dev = 0, cus = 0;
+  static int occ = 0;
+  if (!occ) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv1x1_bnbwd_kernel<256, 64, true>, 512, 0) != hipSuccess ||
         occ <= 0)
       occ = 1;
-    hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    cap = occ * cus;
   }
+  const int cap = occ * dtm_compute_cus();  // (minus the CUs reserved for RCCL)
   return ntiles < cap ? ntiles : cap;
 }
 

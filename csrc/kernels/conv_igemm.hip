@@ -23,6 +23,7 @@
 //    ds_read_b64_tr_b16 (the CDNA4 hardware transpose) straight into MFMA fragments.
 //    Split-K over pixels; partial tiles are added into the fp32 gradient with float atomics.
 #include "common.h"
+#include <cstdio>
 
 namespace dtm {
 
@@ -166,15 +167,17 @@ __device__ __forceinline__ void epi_barrier() {
 // and a persistent kernel's loop-carried wait for them (vmcnt(n) with the LDS-DMA prefetch issued after
 // them, which the compiler does not count) would drain the prefetch every tile.
 // PRE: the side inputs were DMA'd to LDS by the kernel (pre: [NIT][NT] 16-B add_src chunks, then [NIT][NT]
-// act_x chunks, slot = thread; pre_ss: the block's act scale / shift [2][CT]) - no global loads here, so no
-// compiler-generated vmcnt waits (add_stride 1, no mask / act_r).
+// act_x chunks, slot = thread; pre_ss: the block's act scale / shift [2][CT], or nullptr: from a.act_ss) - no
+// global loads here, so no compiler-generated vmcnt waits (add_stride 1, no mask / act_r).  pre_act: the act_x
+// chunks at their own address instead ([PT][CT] bf16 row-major = [NIT][NT] 16-B chunks, slot = thread).
 // aacc (persistent kernels, with SACC): the activation-backward sums [sum g*x | sum g | sum g*r] of this
 // thread's chunk column are added into aacc[24] across all the block's tiles (one partial row per worker at the
 // kernel's end, worker_row) instead of a per-tile LDS reduction + row.
 template <int PT, int CT, bool RAWB, bool EXACT, bool SACC, int NT, bool SIDE = true, bool PRE = false>
 __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem, int p0, int c0, int by,
                                                  float* ssum, float* ssq, const char* pre = nullptr,
-                                                 const float* pre_ss = nullptr, float* aacc = nullptr) {
+                                                 const float* pre_ss = nullptr, float* aacc = nullptr,
+                                                 const char* pre_act = nullptr) {
   constexpr int OROW = CT * 2 + 16;
   const int tid = threadIdx.x;
   epi_barrier<RAWB>();
@@ -198,8 +201,8 @@ __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem
   if (act && !amask && kc < a.K) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      sc[e] = PRE ? pre_ss[chn * 8 + e] : a.act_ss[kc + e];
-      sh[e] = PRE ? pre_ss[CT + chn * 8 + e] : a.act_ss[a.K + kc + e];
+      sc[e] = (PRE && pre_ss) ? pre_ss[chn * 8 + e] : a.act_ss[kc + e];
+      sh[e] = (PRE && pre_ss) ? pre_ss[CT + chn * 8 + e] : a.act_ss[a.K + kc + e];
     }
   }
   // side inputs of the dgrad post-ops (add_src, act_x, act_r, mask bytes) are loaded for a group of
@@ -225,7 +228,9 @@ __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem
           pa[j] = *(const uint4*)(pre + (size_t)(g0 + j) * NT * 16 + tid * 16);
           ph[j] = true;
         }
-        if (act) px[j] = *(const uint4*)(pre + (size_t)(NIT + g0 + j) * NT * 16 + tid * 16);
+        if (act)
+          px[j] = *(const uint4*)((pre_act ? pre_act : pre + (size_t)NIT * NT * 16) + (size_t)(g0 + j) * NT * 16 +
+                                  tid * 16);
       }
     } else if (side) {
 #pragma unroll
@@ -373,7 +378,8 @@ template <int PT, int CT, int WP, int WC, int STG, bool RAWB = false, bool EXACT
 __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&acc)[WC / 16][WP / 16], char* smem,
                                                  int p0, int c0, int by, float* ssum = nullptr,
                                                  float* ssq = nullptr, const char* pre = nullptr,
-                                                 const float* pre_ss = nullptr, float* aacc = nullptr) {
+                                                 const float* pre_ss = nullptr, float* aacc = nullptr,
+                                                 const char* pre_act = nullptr) {
   constexpr int NWP = PT / WP;
   constexpr int TP = WP / 16, TC = WC / 16;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -438,7 +444,8 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
     }
   }
   if constexpr (staged)
-    conv_nt_epi_tail<PT, CT, RAWB, EXACT, SACC, NT, SIDE, PRE>(a, smem, p0, c0, by, ssum, ssq, pre, pre_ss, aacc);
+    conv_nt_epi_tail<PT, CT, RAWB, EXACT, SACC, NT, SIDE, PRE>(a, smem, p0, c0, by, ssum, ssq, pre, pre_ss, aacc,
+                                                               pre_act);
 }
 
 template <int PT, int CT, int WP, int WC, int UD, int NBUF>
@@ -645,7 +652,13 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
 // array (a second object makes hipcc drain vmcnt before the fragment reads).
 // NWP: waves along the pixel dimension (4 / NWP along channels); NWP = 4 with PT = 512, CT = 64 gives every
 // wave a 128 x 64 tile (the 64-channel 3x3 layers: 2x the MFMAs per LDS byte of the 2x2 layout's 64x32)
-template <int PT, int CT, int NS, int UD, bool PRO, int NWP = 2>
+//
+// ACTL (act dgrads: the input's BatchNorm+ReLU backward in the epilogue, act_x only - no add_src / mask / act_r;
+// NS = 2): the epilogue's act_x tile [PT][CT] is LDS-DMA'd into the ring slot the last k-tile does not read, issued
+// right after the last k-tile's barrier so it lands under that tile's MFMAs; the epilogue then reads it from LDS
+// (conv_nt_epi_tail pre_act) instead of issuing global loads after the main loop.  The slot left free holds the act
+// tile at one end of the (slightly enlarged) ring and the output staging at the other.
+template <int PT, int CT, int NS, int UD, bool PRO, int NWP = 2, bool ACTL = false>
 __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
   constexpr int BK = 64;
   constexpr int WP = PT / NWP, WC = CT / (4 / NWP);
@@ -655,7 +668,12 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
   constexpr int BUF = (PT + CT) * 128;
   constexpr int OROW = CT * 2 + 16;
   constexpr int MAXC = 512;
-  constexpr int RING = NS * BUF > PT * OROW ? NS * BUF : PT * OROW;
+  constexpr int STGB = PT * OROW;                  // epilogue output staging
+  constexpr int ACTB = ACTL ? PT * CT * 2 : 0;     // act_x tile
+  constexpr int RING0 = NS * BUF > STGB ? NS * BUF : STGB;
+  constexpr int RING1 = ACTB + STGB > BUF + ACTB ? ACTB + STGB : BUF + ACTB;
+  constexpr int RING = ACTL ? (RING1 > NS * BUF ? RING1 : NS * BUF) : RING0;
+  static_assert(!ACTL || (NS == 2 && !PRO && ACTB % 4096 == 0), "act-tile staging: 2 slots, whole wave groups");
   __shared__ __attribute__((aligned(16))) char smem[RING + (PRO ? MAXC * 8 : 0)];
   typedef __attribute__((address_space(1))) const void gvoid;
   typedef __attribute__((address_space(3))) void lvoid;
@@ -805,11 +823,25 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bf[ks][j], acc[i][j], 0, 0, 0);
   };
 
+  // (ACTL) the act_x tile: chunk q = (wave + 4 i) * 64 + lane -> pixel row q / (CT / 8), channel chunk q % (CT / 8),
+  // LDS bytes q * 16 of the act region (row-major [PT][CT] bf16)
+  auto issue_act = [&](char* dst) {
+    const char* ag = (const char*)a.act_x;
+#pragma unroll
+    for (int i = 0; i < ACTB / 4096; ++i) {
+      const int q = (wave + 4 * i) * 64 + lane;
+      const int m = p0 + q / (CT / 8), kc = c0 + (q % (CT / 8)) * 8;
+      const bool v = (m < a.M) & (kc < a.K);
+      const char* src = ag + ((size_t)out_row(a, v ? m : 0) * a.K + kc) * 2;
+      __builtin_amdgcn_global_load_lds((gvoid*)(v ? src : zg), (lvoid*)(dst + (wave + 4 * i) * 1024), 16, 0, 0);
+    }
+  };
+
   const int nk = (a.Kg + BK - 1) / BK;
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (s < nk) issue(s, s);
-  int slot = 0;
+  int slot = 0, last = 0;
   for (int kt = 0; kt < nk; ++kt) {
     // this wave's DMA of k-tile kt has landed once at most the later stages are still counted
     const int ahead = min(nk - 1, kt + NS - 2) - kt;
@@ -820,13 +852,27 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // stage kt visible to all waves; stage kt-1 no longer read
     if (kt + NS - 1 < nk) issue(kt + NS - 1, slot == 0 ? NS - 1 : slot - 1);
+    if constexpr (ACTL) {
+      // last k-tile: the other slot is free (every wave passed the barrier after reading it)
+      if (kt == nk - 1) issue_act(smem + (slot == 1 ? 0 : RING - ACTB));
+    }
     compute(slot);
+    last = slot;
     slot = slot == NS - 1 ? 0 : slot + 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // the epilogue reuses the ring
-  if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1>(a, acc, smem, p0, c0, by);
-  else conv_nt_epilogue<PT, CT, WP, WC, 2>(a, acc, smem, p0, c0, by);
+  if constexpr (ACTL) {
+    // act tile in the slot the last k-tile did not read, output staging at the ring's other end
+    const char* act = smem + (last == 1 ? 0 : RING - ACTB);
+    char* stg = smem + (last == 1 ? RING - STGB : 0);
+    conv_nt_epilogue<PT, CT, WP, WC, 1, false, false, false, false, 256, true, true>(a, acc, stg, p0, c0, by, nullptr,
+                                                                                     nullptr, nullptr, nullptr, nullptr,
+                                                                                     act);
+  } else {
+    if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1>(a, acc, smem, p0, c0, by);
+    else conv_nt_epilogue<PT, CT, WP, WC, 2>(a, acc, smem, p0, c0, by);
+  }
 }
 
 // 8-wave big-tile variant of the pipelined kernel: PT = 256 pixels x CT (128 | 256) channels per
@@ -1947,22 +1993,23 @@ static void launch_w8(const ConvNTArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((conv_nt_w8_kernel<PT, CT, NWP, NS, UD>), grid, dim3(512), 0, st, a);
 }
 
+// act dgrads whose epilogue side input is act_x alone (the pipelined kernel's ACTL form: the tile LDS-DMA'd under the
+// last k-tile); A/B knob dtm_conv_set_act_lds
+static int g_act_lds = 1;
+DTM_API void dtm_conv_set_act_lds(int on) { g_act_lds = on; }
+static bool act_lds_ok(const ConvNTArgs& a) {
+  return g_act_lds && a.act_x && !a.act_mask && !a.act_r && !a.add_src && !a.in_scale && (a.K & 7) == 0 && !a.sp_tw;
+}
 template <int PT, int CT, int NS, int UD, int NWP = 2>
 static void launch_pipe(const ConvNTArgs& a, hipStream_t st) {
   dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT, a.ngrp > 1 ? a.ngrp : 1);
   if (a.in_scale) hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, true, NWP>), grid, dim3(256), 0, st, a);
+  else if (NS == 2 && (PT * CT) % 2048 == 0 && act_lds_ok(a))
+    hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, 2, UD, false, NWP, true>), grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, false, NWP>), grid, dim3(256), 0, st, a);
 }
 
-static int device_cus() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  }
-  return cus;
-}
+static int device_cus() { return dtm_compute_cus(); }  // (minus the CUs reserved for RCCL: workspace.hip)
 
 static bf16_t* dump_chunk() {
   static void* z = nullptr;
@@ -2120,7 +2167,22 @@ static int g_k32_tile = 1;  // A/B knob: the 256x32 tile for <= 32-channel spati
 DTM_API void dtm_conv_set_k32(int on) { g_k32_tile = on; }
 static int g_act_tile = -1;  // A/B knob: tile of the dgrads with a fused activation-backward epilogue (-1 = policy)
 DTM_API void dtm_conv_set_act_tile(int id) { g_act_tile = id; }
+static TileCfg pick_tile_impl(const ConvNTArgs& a, bool stats);
+// DTM_TILE_LOG=1: one stderr line per conv_nt launch decision (shape, side inputs, tile) for profiling runs
 static TileCfg pick_tile(const ConvNTArgs& a, bool stats = false) {
+  static int log = -1;
+  if (log < 0) {
+    const char* e = getenv("DTM_TILE_LOG");
+    log = e ? atoi(e) : 0;
+  }
+  const TileCfg t = pick_tile_impl(a, stats);
+  if (log)
+    fprintf(stderr, "dtm_tile M=%d K=%d C=%d RxS=%dx%d Kg=%d st=%d ostr=%d pro=%d stats=%d add=%d act=%d mask=%d r=%d -> %d\n",
+            a.M, a.K, a.C, a.R, a.S, a.Kg, a.stride, a.ostr, a.in_scale != nullptr, (int)stats, a.add_src != nullptr,
+            a.act_x != nullptr, a.act_mask != nullptr, a.act_r != nullptr, t.id);
+  return t;
+}
+static TileCfg pick_tile_impl(const ConvNTArgs& a, bool stats) {
   if (g_tile_env == -2) {
     const char* e = getenv("DTM_CONV_TILE");
     g_tile_env = e ? atoi(e) : -1;

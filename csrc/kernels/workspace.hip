@@ -37,6 +37,25 @@ bool dtm_device_ok() {
 }
 DTM_API int dtm_device_check() { return dtm_device_ok() ? 0 : -9; }
 
+// CUs left to the compute kernels.  Under data parallelism the RCCL collectives overlapped with backward run one
+// workgroup per channel on the same chip; a persistent kernel whose grid is sized for every CU would then run a
+// second, mostly empty round of blocks behind them.  dtm_set_reserved_cus(n) takes n CUs out of the count the
+// persistent kernels (resident capacity x CUs) and the split-K weight-gradient policies size for.
+static int g_reserved_cus = 0;
+DTM_API void dtm_set_reserved_cus(int n) { g_reserved_cus = n > 0 ? n : 0; }
+DTM_API int dtm_get_reserved_cus() { return g_reserved_cus; }
+int dtm_compute_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  const int left = cus - g_reserved_cus;
+  return left < 8 ? 8 : left;
+}
+DTM_API int dtm_compute_cus_api() { return dtm_compute_cus(); }
+
 // Growth is hipGraph-safe: a captured graph holds raw pointers into whatever arena was current at capture
 // time, so a retired arena is never freed (it stays allocated until process exit; growth is rare and happens
 // in the warm-up steps), and growth while the stream is being captured is refused (hipMalloc is not a legal
@@ -217,3 +236,44 @@ DTM_API int dtm_ws_reserve_stream(long floats, void* stream) {
   return dtm_ws_get_stream((size_t)floats, (hipStream_t)stream) ? 0 : -4;
 }
 DTM_API long dtm_ws_capacity(void* stream) { return (long)g_ws_floats[dtm_ws_slot((hipStream_t)stream)]; }
+
+// ---- CU-contention stand-in for the RCCL channels (tools/ab_step.py 'hog', DP=8 readiness on one GPU) ----
+// nblocks workgroups, each holding 96 KiB of LDS (one per CU) and streaming its own 1 MiB slice src -> dst for
+// `ms` milliseconds of the 100 MHz constant clock, like a collective's per-channel copy loop occupying a CU while
+// the overlapped backward runs.  Every wave leaves after at most `ms` (or 1 << 16 sweeps), so the grid drains.
+__global__ __launch_bounds__(256) void cu_hog_kernel(const float4* __restrict__ src, float4* __restrict__ dst,
+                                                     unsigned long long ticks) {
+  __shared__ float4 hold[6144];  // 96 KiB: one hog block per CU
+  constexpr int SLICE = (1 << 20) / 16;
+  const float4* s = src + (size_t)blockIdx.x * SLICE;
+  float4* d = dst + (size_t)blockIdx.x * SLICE;
+  const unsigned long long t0 = wall_clock64();
+  hold[threadIdx.x] = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 keep = hold[(threadIdx.x * 24) % 6144];
+  for (int it = 0; it < (1 << 16); ++it) {
+    for (int i = threadIdx.x; i < SLICE; i += 256) d[i] = s[i];
+    if (wall_clock64() - t0 > ticks) break;
+  }
+  if (keep.x != 0.f) d[threadIdx.x] = keep;  // (never true: keeps the LDS allocation)
+}
+
+DTM_API int dtm_cu_hog(int nblocks, float ms, void* stream) {
+  static void* buf = nullptr;
+  static int cap = 0;
+  if (nblocks <= 0) return 0;
+  if (nblocks > 256) return -1;
+  if (nblocks > cap) {
+    if (buf) {
+      hipDeviceSynchronize();
+      hipFree(buf);
+      buf = nullptr;
+    }
+    if (hipMalloc(&buf, (size_t)nblocks * 2 << 20) != hipSuccess) return -4;
+    hipMemset(buf, 0, (size_t)nblocks * 2 << 20);
+    cap = nblocks;
+  }
+  const unsigned long long ticks = (unsigned long long)(ms * 1e5f);  // wall_clock64: 100 MHz
+  hipLaunchKernelGGL(cu_hog_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, (const float4*)buf,
+                     (float4*)((char*)buf + ((size_t)cap << 20)), ticks);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}

@@ -29,6 +29,23 @@ def moving_average_buffers(model):
             if not trainable and t.dtype == torch.float32 and t.is_floating_point()]
 
 
+def reserved_cus_default():
+    """CUs kept out of the compute grids' sizing under data parallelism (ops/_lib.set_reserved_cus):
+    DTM_RESERVED_CUS if set, else the pinned RCCL channel count (NCCL_MAX_NCHANNELS: one workgroup per
+    channel), else RESERVED_CUS_DP."""
+    import os
+    v = os.environ.get("DTM_RESERVED_CUS")
+    if v is not None:
+        return int(v)
+    ch = os.environ.get("NCCL_MAX_NCHANNELS")
+    if ch:
+        return int(ch)
+    return RESERVED_CUS_DP
+
+
+RESERVED_CUS_DP = 0
+
+
 class TrainStep:
     def __init__(self, model, optimizer="momentum", lr=0.1, momentum=0.9, rho=0.9, epsilon=1e-10, bucket_mb=32.0,
                  label_smoothing=0.0, aux_weight=0.4, ema_decay=None, lr_schedule=None, use_graph=False,
@@ -73,6 +90,9 @@ class TrainStep:
         self._eager_steps = 0
         self._skip_total = None  # device int32: number of skipped (non-finite) steps so far
         self._skip_seen = 0
+        self.on_backward = None  # optional callable run right before loss.backward() (tools/ab_step.py 'hog')
+        if self.dp.world > 1 and params and params[0].is_cuda:
+            _lib.set_reserved_cus(reserved_cus_default())
 
     def loss_fn(self, out, labels):
         aux = None
@@ -107,6 +127,8 @@ class TrainStep:
                 loss = self.loss_fn(out, labels)
             self._mark("fwd")
             self.bufsync.issue()  # forward has finished every moving-statistics update
+            if self.on_backward is not None:
+                self.on_backward()
             with roctx("backward"):  # bucket all-reduces are issued (own ranges) from the grad hooks
                 loss.backward()
             if images.is_cuda:

@@ -119,6 +119,11 @@ _SIGS = {
     "dtm_conv_set_w8": (None, [_I]),
     "dtm_conv_set_kwide": (None, [_I]),
     "dtm_set_reduce_few": (None, [_I]),
+    "dtm_set_reserved_cus": (None, [_I]),
+    "dtm_conv_set_act_lds": (None, [_I]),
+    "dtm_get_reserved_cus": (_I, []),
+    "dtm_compute_cus_api": (_I, []),
+    "dtm_cu_hog": (_I, [_I, _F, _P]),
     "dtm_conv_set_stream_act": (None, [_I]),
     "dtm_conv_set_act_tile": (None, [_I]),
     "dtm_stem_pack": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
@@ -270,10 +275,24 @@ def ptr(t):
 
 
 _num_cus = None
+_reserved = [0]
+
+
+def set_reserved_cus(n):
+    """Take ``n`` CUs out of the count that the persistent conv kernels and the split-K weight-gradient policies
+    size their grids for (the RCCL channels' workgroups share the chip with the overlapped backward under data
+    parallelism: a grid sized for every CU would run a short second round behind them).  0 = all CUs."""
+    _reserved[0] = max(0, int(n))
+    lib().dtm_set_reserved_cus(_reserved[0])
+
+
+def reserved_cus():
+    return _reserved[0]
 
 
 def num_cus():
+    """CUs available to compute grids: the device's CUs minus the reserved ones (set_reserved_cus)."""
     global _num_cus
     if _num_cus is None:
         _num_cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
-    return _num_cus
+    return max(8, _num_cus - _reserved[0])

@@ -218,6 +218,58 @@ def test_conv_pipelined_tiles_match_reference(tile, prologue, case):
     assert _rel(stats[0], yf.sum(0)) < 1e-3 and _rel(stats[1], yf.square().sum(0)) < 1e-3
 
 
+@pytest.mark.parametrize("tile", [-1, 4, 21, 24, 26, 32])
+@pytest.mark.parametrize("act_lds", [1, 0])
+@pytest.mark.parametrize("case", [(2, 14, 14, 128, 256, 3, 1), (3, 7, 7, 512, 200, 1, 1), (4, 15, 15, 96, 64, 3, 2),
+                                  (2, 28, 28, 128, 128, 3, 2), (2, 9, 9, 64, 40, 3, 1), (2, 30, 30, 64, 128, 1, 1)])
+def test_conv_act_dgrad_tiles_match_reference(tile, act_lds, case):
+    """dgrad with the input's BatchNorm+ReLU backward in the epilogue (the bottleneck conv2 / conv3 dgrads) on every
+    tile the policy can pick, with the act_x tile LDS-DMA'd under the last k-tile (act_lds 1: the pipelined kernels'
+    ACTL form) or loaded in the epilogue: g = dgrad * [x*scale + shift > 0] (unscaled output), sums = (sum g*x,
+    sum g) per channel; strided cases through the grouped parity-class dgrad."""
+    import ctypes
+
+    from distributed_tensorflow_models_amd.ops import _lib
+    from distributed_tensorflow_models_amd.ops.geometry import conv_geom
+    N, H, W, C, K, R, st = case
+    torch.manual_seed(0)
+    L = _lib.lib()
+    x = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(K, R, R, C, device=DEV) / (R * R * C) ** 0.5).to(torch.bfloat16)
+    sc = torch.rand(C, device=DEV) + 0.5
+    sh = torch.randn(C, device=DEV) * 0.5
+    g = conv_geom(tuple(x.shape), tuple(w.shape), st, "SAME")
+    yr = ref.conv2d(x.float(), w.float(), None, st, "SAME")
+    dy = torch.randn_like(yr).to(torch.bfloat16)
+    xr = x.float().clone().requires_grad_()
+    ref.conv2d(xr, w.float(), None, st, "SAME").backward(dy.float())
+    mask = (x.float() * sc + sh) > 0
+    gref = xr.grad * mask
+    wt = torch.empty(C, R, R, K, device=DEV, dtype=torch.bfloat16)
+    d = g.as_desc(_lib.ConvDesc)
+    if st > 1:
+        L.dtm_weight_flip_transpose_dec(_lib.ptr(w), _lib.ptr(wt), K, R, R, C, st, g.pad_h, g.pad_w, _lib.stream_ptr())
+        d.dec = 1
+    else:
+        L.dtm_weight_flip_transpose(_lib.ptr(w), _lib.ptr(wt), K, R, R, C, _lib.stream_ptr())
+    ss4 = torch.stack([sc, sh, sh, sc]).contiguous()
+    sums = torch.zeros(2, C, device=DEV)
+    dx = torch.empty_like(x)
+    L.dtm_conv_set_tile(tile)
+    L.dtm_conv_set_act_lds(act_lds)
+    try:
+        rc = L.dtm_conv_dgrad_ex(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), None, 1, _lib.ptr(x),
+                                 _lib.ptr(ss4), _lib.ptr(sums), 1, _lib.stream_ptr())
+        assert rc == 0
+        torch.cuda.synchronize()
+    finally:
+        L.dtm_conv_set_tile(-1)
+        L.dtm_conv_set_act_lds(1)
+    assert _rel(dx, gref) < 1e-2
+    assert _rel(sums[0], (gref * x.float()).sum((0, 1, 2))) < 1e-2
+    assert _rel(sums[1], gref.sum((0, 1, 2))) < 1e-2
+
+
 @pytest.mark.parametrize("tile", [0, 1, 6, 10, 12])
 @pytest.mark.parametrize("case", [(4, 15, 15, 64, 96, 3, 2), (2, 14, 14, 128, 256, 3, 1), (3, 7, 7, 512, 200, 1, 1),
                                   (2, 9, 9, 24, 40, 3, 1), (5, 8, 8, 64, 64, 1, 1), (4, 9, 9, 256, 512, 3, 1),

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B sweep of the conv_nt tile variants (DTM_CONV_TILE ids) on the ResNet-50 shapes, in ONE process
 with interleaved rounds (per-shape median over rounds): forward, forward with the BatchNorm-apply
-prologue, and dgrad.  Usage: TILES=-1,21,26 python tools/conv_tile_sweep.py"""
+prologue, and dgrad (ACT=1: also the dgrad with the input's BN+ReLU backward epilogue).  Usage: TILES=-1,21,26 python tools/conv_tile_sweep.py"""
 import ctypes
 import os
 import statistics
@@ -88,6 +88,12 @@ def main():
                                             _lib.ptr(sh), 0, ctypes.byref(d), st),
             "dgrad": lambda: L.dtm_conv_dgrad(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), st),
         }
+        if os.environ.get("ACT"):
+            # dgrad with the input's BatchNorm+ReLU backward in the epilogue (the bottleneck conv2 / conv3 dgrads)
+            ss4 = torch.stack([sc, sh, sh, sc]).contiguous()
+            asums = torch.zeros(2, C, device="cuda")
+            passes["dgact"] = lambda: L.dtm_conv_dgrad_ex(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d),
+                                                          None, 1, _lib.ptr(x), _lib.ptr(ss4), _lib.ptr(asums), 1, st)
         if stride > 1 and R >= stride and S >= stride:
             # the stride-decomposed dgrad (ConvDesc.dec: one stride-1 conv per output parity class) as training runs it
             wtd = torch.empty(C, R, S, K, device="cuda", dtype=torch.bfloat16)
