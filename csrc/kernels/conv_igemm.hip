@@ -169,7 +169,9 @@ __device__ __forceinline__ void epi_barrier() {
 // PRE: the side inputs were DMA'd to LDS by the kernel (pre: [NIT][NT] 16-B add_src chunks, then [NIT][NT]
 // act_x chunks, slot = thread; pre_ss: the block's act scale / shift [2][CT], or nullptr: from a.act_ss) - no
 // global loads here, so no compiler-generated vmcnt waits (add_stride 1, no mask / act_r).  pre_act: the act_x
-// chunks at their own address instead ([PT][CT] bf16 row-major = [NIT][NT] 16-B chunks, slot = thread).
+// chunks at their own address instead ([PT][CT] bf16 row-major = [NIT][NT] 16-B chunks, slot = thread); pre_r /
+// pre_mask (block-output form, CT = 128): the act_r chunks in the same layout and the ReLU-mask bytes of pixel row p
+// at (p / 16) * 1024 + (p % 16) * 16.
 // aacc (persistent kernels, with SACC): the activation-backward sums [sum g*x | sum g | sum g*r] of this
 // thread's chunk column are added into aacc[24] across all the block's tiles (one partial row per worker at the
 // kernel's end, worker_row) instead of a per-tile LDS reduction + row.
@@ -177,7 +179,8 @@ template <int PT, int CT, bool RAWB, bool EXACT, bool SACC, int NT, bool SIDE = 
 __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem, int p0, int c0, int by,
                                                  float* ssum, float* ssq, const char* pre = nullptr,
                                                  const float* pre_ss = nullptr, float* aacc = nullptr,
-                                                 const char* pre_act = nullptr) {
+                                                 const char* pre_act = nullptr, const char* pre_r = nullptr,
+                                                 const char* pre_mask = nullptr) {
   constexpr int OROW = CT * 2 + 16;
   const int tid = threadIdx.x;
   epi_barrier<RAWB>();
@@ -231,6 +234,12 @@ __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem
         if (act)
           px[j] = *(const uint4*)((pre_act ? pre_act : pre + (size_t)NIT * NT * 16) + (size_t)(g0 + j) * NT * 16 +
                                   tid * 16);
+        if (amask && pre_mask) {
+          // mask bytes of pixel row p at (p / 16) * 1024 + (p % 16) * 16 (one 16-B DMA per pixel: CT = 128)
+          const int row = ((g0 + j) * NT + tid) / CPR;
+          pm[j] = (uint8_t)pre_mask[((row >> 4) << 10) + ((row & 15) << 4) + chn];
+          if (a.act_r && pre_r) pr[j] = *(const uint4*)(pre_r + (size_t)(g0 + j) * NT * 16 + tid * 16);
+        }
       }
     } else if (side) {
 #pragma unroll
@@ -379,7 +388,8 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
                                                  int p0, int c0, int by, float* ssum = nullptr,
                                                  float* ssq = nullptr, const char* pre = nullptr,
                                                  const float* pre_ss = nullptr, float* aacc = nullptr,
-                                                 const char* pre_act = nullptr) {
+                                                 const char* pre_act = nullptr, const char* pre_r = nullptr,
+                                                 const char* pre_mask = nullptr) {
   constexpr int NWP = PT / WP;
   constexpr int TP = WP / 16, TC = WC / 16;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -445,7 +455,7 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
   }
   if constexpr (staged)
     conv_nt_epi_tail<PT, CT, RAWB, EXACT, SACC, NT, SIDE, PRE>(a, smem, p0, c0, by, ssum, ssq, pre, pre_ss, aacc,
-                                                               pre_act);
+                                                               pre_act, pre_r, pre_mask);
 }
 
 template <int PT, int CT, int WP, int WC, int UD, int NBUF>
@@ -1060,7 +1070,13 @@ __device__ __forceinline__ void glds16(const void* gptr, const void* lds) {
 // p*stride + k/32, column q*stride, byte (k % 32) * 2 of the zero-bordered [N][Hp][Wp][4] image -
 // the 7x7/2 ResNet stem as a persistent stream with its 64 x 224 weights resident in LDS.  Its A tiles
 // (28 KiB of L2-resident rows per 64 pixels) ride a 3-slot ring (NBUF = 3): two tiles in flight.
-template <int PT, int CT, int NKT, bool PRO, bool STEM = false, int NBUF = 2, bool SIDE = true>
+//
+// SIDEP (block-output dgrads: add_src + act_x + ReLU bitmask (+ act_r with SIDEP = 2), CT = 128, 2-slot ring): the
+// epilogue's side inputs of tile t+gy are LDS-DMA'd into the other of two side slots right after tile t+gy's A
+// tile, so they land during tile t's MFMAs and epilogue; the epilogue reads them from LDS (no global loads whose
+// compiler waits would drain the prefetch - the reason the global-load form of this kernel did not beat the
+// register-staged tile on these memory-bound dgrads).
+template <int PT, int CT, int NKT, bool PRO, bool STEM = false, int NBUF = 2, bool SIDE = true, int SIDEP = 0>
 __global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int ntiles) {
   constexpr int WP = PT / 2, WC = CT / 2;
   constexpr int TP = WP / 16, TC = WC / 16;
@@ -1073,9 +1089,15 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int n
   constexpr int MAXC = 512;
   constexpr int OFF_A = WBUF, OFF_S = WBUF + NBUF * ABUF, OFF_P = OFF_S + STG;
   constexpr int NDMA = NKT * AI;                // DMA instructions per thread per tile
+  // side slots (SIDEP): [add | act_x | (act_r) chunks: NIT * 4 KiB each][mask: 4 KiB]
+  constexpr int NSR = SIDEP == 2 ? 3 : 2;       // chunk regions per side slot
+  constexpr int SSZ = SIDEP ? NSR * NIT * 4096 + 4096 : 0;
+  constexpr int NSD = SIDEP ? NSR * NIT + 1 : 0;  // side DMA instructions per thread per tile
+  constexpr int OFF_SD = OFF_P + (PRO ? MAXC * 8 : 0);
   static_assert(NBUF == 2 || NBUF == 3, "ring depth");
-  static_assert(2 * NIT + NDMA <= 63, "vmcnt range");
-  __shared__ __attribute__((aligned(16))) char smem[OFF_P + (PRO ? MAXC * 8 : 0)];
+  static_assert(2 * NIT + NDMA + NSD <= 63, "vmcnt range");
+  static_assert(!SIDEP || (SIDE && NBUF == 2 && PT == 64 && CT == 128 && !STEM), "side prefetch form");
+  __shared__ __attribute__((aligned(16))) char smem[OFF_SD + 2 * SSZ];
   typedef __attribute__((address_space(1))) const void gvoid;
   typedef __attribute__((address_space(3))) void lvoid;
   static_assert(NIT >= 1 && NIT <= 15, "vmcnt lower bound");
@@ -1139,6 +1161,34 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int n
       }
     }
   };
+  // (SIDEP) side inputs of tile t into side slot sb: thread tid's staged store j is pixel row (j*256 + tid) / 16,
+  // chunk tid % 16 (conv_nt_epi_tail's slot = thread layout); mask: lane l < 16 of wave w moves the 16 mask
+  // bytes (128 channels) of pixel row 16 w + l
+  const char* ssrc[SIDEP ? NSD : 1];
+  auto side_issue = [&](int t, int sb) {
+    if constexpr (SIDEP) {
+      char* base = smem + OFF_SD + sb * SSZ;
+      const int kc = c0 + (tid & 15) * 8;
+#pragma unroll
+      for (int j = 0; j < NIT; ++j) {
+        const int m = t * PT + (j * 256 + tid) / 16;
+        const bool v = (m < a.M) & (kc < a.K);
+        const size_t o = v ? (size_t)m * a.K + kc : 0;
+        ssrc[j] = (v && a.add_src) ? (const char*)(a.add_src + o) : zg;
+        ssrc[NIT + j] = v ? (const char*)(a.act_x + o) : zg;
+        glds16(ssrc[j], base + (j * 4 + wave) * 1024);
+        glds16(ssrc[NIT + j], base + NIT * 4096 + (j * 4 + wave) * 1024);
+        if constexpr (SIDEP == 2) {
+          ssrc[2 * NIT + j] = (v && a.act_r) ? (const char*)(a.act_r + o) : zg;
+          glds16(ssrc[2 * NIT + j], base + 2 * NIT * 4096 + (j * 4 + wave) * 1024);
+        }
+      }
+      const int mp = t * PT + wave * 16 + (lane & 15);
+      const bool mv = (lane < 16) & (mp < a.M) & (c0 < a.K);
+      ssrc[NSR * NIT] = mv ? (const char*)(a.act_mask + ((size_t)mp * a.K + c0) / 8) : zg;
+      glds16(ssrc[NSR * NIT], base + NSR * NIT * 4096 + wave * 1024);
+    }
+  };
   auto transform = [&](int t, int buf) {
     char* base = smem + OFF_A + buf * ABUF;
 #pragma unroll
@@ -1179,6 +1229,7 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int n
   int t = by0;
   const int gy = gridDim.y;
   if (t < ntiles) issue(t, 0);
+  if (SIDEP && t < ntiles) side_issue(t, 0);
   if (NBUF == 3 && t + gy < ntiles) issue(t + gy, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // weights (+ prologue affine) resident, tile 0 (and 1) landed
@@ -1196,7 +1247,11 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int n
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // tile t visible; the slot read last iteration and the stage area are free
     if constexpr (NBUF == 2) {
-      if (t + gy < ntiles) issue(t + gy, buf ^ 1);
+      if (t + gy < ntiles) {
+        issue(t + gy, buf ^ 1);
+        // (SIDEP) the other side slot was read by the previous epilogue, finished before the barrier above
+        if constexpr (SIDEP) side_issue(t + gy, buf ^ 1);
+      }
     } else {
       if (t + 2 * gy < ntiles) issue(t + 2 * gy, buf == 0 ? 2 : buf - 1);
     }
@@ -1229,8 +1284,17 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int n
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
       }
     }
-    conv_nt_epilogue<PT, CT, WP, WC, 1, true, true, true, true, 256, SIDE>(a, acc, smem + OFF_S, t * PT, c0, t, ssum,
-                                                                           ssq, nullptr, nullptr, aacc);
+    if constexpr (SIDEP) {
+      const char* sbase = smem + OFF_SD + buf * SSZ;
+      conv_nt_epilogue<PT, CT, WP, WC, 1, true, true, true, true, 256, SIDE, true>(
+          a, acc, smem + OFF_S, t * PT, c0, t, ssum, ssq, sbase, nullptr, aacc, sbase + NIT * 4096,
+          SIDEP == 2 ? sbase + 2 * NIT * 4096 : nullptr, sbase + NSR * NIT * 4096);
+#pragma unroll
+      for (int i = 0; i < NSD; ++i) asm volatile("" ::"v"(ssrc[i]));
+    } else {
+      conv_nt_epilogue<PT, CT, WP, WC, 1, true, true, true, true, 256, SIDE>(a, acc, smem + OFF_S, t * PT, c0, t, ssum,
+                                                                             ssq, nullptr, nullptr, aacc);
+    }
 #pragma unroll
     for (int i = 0; i < NKT * AI; ++i) asm volatile("" ::"v"(srcs[i]));
     buf = buf + 1 == NBUF ? 0 : buf + 1;
@@ -2019,11 +2083,12 @@ static bf16_t* dump_chunk() {
 
 // persistent streaming 1x1 kernel: blocks = resident capacity (occupancy x CUs), channel tiles x
 // pixel-tile workers
-template <int PT, int CT, int NKT, bool PRO, bool STEM = false, int NBUF = 2, bool SIDE = true>
+template <int PT, int CT, int NKT, bool PRO, bool STEM = false, int NBUF = 2, bool SIDE = true, int SIDEP = 0>
 static int stream_workers_k(const ConvNTArgs& a) {
   static int occ = 0;
   if (!occ) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv1x1_stream_kernel<PT, CT, NKT, PRO, STEM, NBUF, SIDE>,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ,
+                                                     conv1x1_stream_kernel<PT, CT, NKT, PRO, STEM, NBUF, SIDE, SIDEP>,
                                                      256, 0) !=
             hipSuccess || occ <= 0)
       occ = 1;
@@ -2036,13 +2101,27 @@ static int stream_workers_k(const ConvNTArgs& a) {
   return workers;
 }
 
-template <int PT, int CT, int NKT, bool PRO, bool STEM = false, int NBUF = 2, bool SIDE = true>
+template <int PT, int CT, int NKT, bool PRO, bool STEM = false, int NBUF = 2, bool SIDE = true, int SIDEP = 0>
 static void launch_stream_k(const ConvNTArgs& a, hipStream_t st) {
   const int ctiles = (a.K + CT - 1) / CT;
   const int ntiles = (a.M + PT - 1) / PT;
-  hipLaunchKernelGGL((conv1x1_stream_kernel<PT, CT, NKT, PRO, STEM, NBUF, SIDE>),
-                     dim3(ctiles, stream_workers_k<PT, CT, NKT, PRO, STEM, NBUF, SIDE>(a)), dim3(256), 0, st, a, ntiles);
+  hipLaunchKernelGGL((conv1x1_stream_kernel<PT, CT, NKT, PRO, STEM, NBUF, SIDE, SIDEP>),
+                     dim3(ctiles, stream_workers_k<PT, CT, NKT, PRO, STEM, NBUF, SIDE, SIDEP>(a)), dim3(256), 0, st, a,
+                     ntiles);
 }
+
+// block-output dgrads (ReLU bitmask + add_src (+ act_r)) on the persistent stream with side-input prefetch (tile id
+// 34; A/B knob dtm_conv_set_stream_side): 1x1, whole 128-channel tiles, Kg <= 128 (act_r: Kg <= 64 - LDS)
+static int g_stream_side = 1;
+DTM_API void dtm_conv_set_stream_side(int on) { g_stream_side = on; }
+static bool stream_side_ok(const ConvNTArgs& a) {
+  return g_stream_side && a.act_mask && a.act_x && !a.in_scale && a.K % 128 == 0 && a.Kg <= 128 &&
+         (a.Kg <= 64 || !a.act_r) && (!a.add_src || a.add_stride == 1);
+}
+#define DTM_SSIDE_SEL(FN, ...)                                                                    \
+  (a.Kg <= 64 ? (a.act_r ? FN<64, 128, 1, false, false, 2, true, 2>(__VA_ARGS__)                  \
+                         : FN<64, 128, 1, false, false, 2, true, 1>(__VA_ARGS__))                 \
+              : FN<64, 128, 2, false, false, 2, true, 1>(__VA_ARGS__))
 
 static bool stem_stream_ok(const ConvNTArgs& a) {
   // the packed-row stem view, no prologue / bias / relu, whole 64-channel tiles, R <= 8 kernel rows
@@ -2073,7 +2152,9 @@ static int stream_workers(const ConvNTArgs& a) {
 static int g_stem_stream = -1;
 DTM_API void dtm_conv_set_stem_stream(int on) { g_stem_stream = on; }
 // statistics partial rows of the streaming kernel (tile id 30 / 31 / 33): one per worker
+static bool stream_ok(const ConvNTArgs& a);
 static int stream_rows(const ConvNTArgs& a, int id) {
+  if (id == 34) return DTM_SSIDE_SEL(stream_workers_k, a);
   if (id == 33) return g_stem_stream == 2 ? stream_workers_k<64, 64, 4, false, true, 2, false>(a)
                                           : stream_workers_k<64, 64, 4, false, true, 3, false>(a);
   const bool k1 = a.Kg <= 64;
@@ -2210,6 +2291,8 @@ static TileCfg pick_tile_impl(const ConvNTArgs& a, bool stats) {
   if (((id == -1 && a.K == 32) || id == 60) && g_direct3 && direct_ok(a)) return {60, 128, 4};
   // the pipelined LDS-DMA 128x128 tile (2 slots, 2 blocks/CU) wins every deep-reduction layer without the
   // prologue (tools/conv_tile_sweep.py: 3x3 at 14x14 / 7x7 -13..-18 %, deep 1x1 -5..-16 %)
+  // block-output dgrads: the persistent stream with side-input prefetch
+  if ((id == -1 || id == 34) && stream_ok(a) && stream_side_ok(a)) return {34, 64, 2};
   if (id == -4) id = -1;  // (-4: the policy without the streaming kernel, for A/B runs)
   else if (id == -1 && a.Kg == 64 && stream_ok(a) && (g_stream_act || !a.act_x) &&
            (!g_policy2 || a.K % 128 == 0 || a.K <= 64))  // (v2: no partial channel tiles: 35x35 ->288 -33 %)
@@ -2281,6 +2364,8 @@ static void dispatch_ud(const ConvNTArgs& a, const TileCfg& t, hipStream_t st) {
   } else if (t.id == 33 && UD == 1) {
     if (g_stem_stream == 2) launch_stream_k<64, 64, 4, false, true, 2, false>(a, st);  // (A/B: 2-slot ring)
     else launch_stream_k<64, 64, 4, false, true, 3, false>(a, st);
+  } else if (t.id == 34 && UD == 1) {
+    DTM_SSIDE_SEL(launch_stream_k, a, st);
   } else if (t.id == 31 && UD == 1) {
     if (a.Kg <= 64) launch_stream<64, 1>(a, st);
     else launch_stream<64, 2>(a, st);
@@ -2472,7 +2557,7 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvD
       if (lt[nl].id == 60) direct_setup(b);
       // act partial rows: one per pixel tile, or one per worker for the persistent kernels
       lrows[nl] = lt[nl].id == 60 ? direct_workers(b)
-                  : (lt[nl].id == 30 || lt[nl].id == 31) ? stream_rows(b, lt[nl].id)
+                  : (lt[nl].id == 30 || lt[nl].id == 31 || lt[nl].id == 34) ? stream_rows(b, lt[nl].id)
                                                          : (b.M + lt[nl].PT - 1) / lt[nl].PT;
       rows += lrows[nl];
       la[nl++] = b;

@@ -153,23 +153,28 @@ def _slot_stash(slot, g, stride=1):
 def _full_window(g):
     """A VALID conv whose kernel covers the whole input (1x1 output, e.g. Inception's 5x5 aux conv on its 5x5
     map): its dgrad is the plain GEMM dx[n, (r, s, c)] = dy[n, :] . W[:, (r, s, c)]; as an implicit-GEMM conv
-    over the zero-padded dy it ran 25x the work in 25 blocks (282 us -> a library GEMM + small passes)."""
+    over the zero-padded dy it ran 25x the work in 25 blocks (282 us) - see _full_window_dgrad_act."""
     return g.P == 1 and g.Q == 1 and g.pad_h == 0 and g.pad_w == 0 and g.R == g.H and g.S == g.W
 
 
 def _full_window_dgrad_act(g, dy, w, x_raw, in_ss, d_in, dx, unscaled, add_src=None):
-    """dgrad of a full-window conv (plain GEMM, hipBLASLt) with the input's BN+ReLU backward folded as the
-    act epilogue does it: g = dgrad * [x_raw*scale + shift > 0]; d_in[0:2] = (sum g*x_raw, sum g) per channel;
-    dx = g (unscaled producer) or g*scale."""
-    gm = torch.mm(dy.reshape(g.N, g.K), weight_bf16(w).reshape(g.K, -1)).reshape(g.N, -1, g.C).float()
-    if add_src is not None:  # (another conv consumer's masked gradient of the same activation)
-        gm = gm + add_src.reshape(g.N, -1, g.C).float()
-    xr = x_raw.reshape(g.N, -1, g.C).float()
-    sc, sh = in_ss[0], in_ss[1]
-    gm = gm * ((xr * sc + sh) > 0)
-    d_in[0].copy_((gm * xr).sum((0, 1)))
-    d_in[1].copy_(gm.sum((0, 1)))
-    dx.copy_((gm if unscaled else gm * sc).reshape(dx.shape))
+    """dgrad of a full-window conv with the input's BN+ReLU backward, on the MFMA conv kernels: the GEMM
+    dx[n, (r, s, c)] = dy[n, :] . W[:, (r, s, c)] is the dgrad of a 1x1 conv from R*S*C input channels to K outputs
+    on a 1x1 map, whose transposed weight [R*S*C][K] is the flipped-weight copy of W viewed as [K][1][1][R*S*C]
+    (cached and refreshed by the optimizer like every dgrad copy).  The act epilogue sees pixel n's R*S*C
+    channels, i.e. x_raw[n] flattened, so it takes the BN scale / shift tiled R*S times and its partial sums
+    [sum g*x_raw | sum g] per (r, s, c) are folded over the R*S taps into d_in[0:2]."""
+    L = _lib.lib()
+    s = _lib.stream_ptr()
+    rsc, rs = g.R * g.S * g.C, g.R * g.S
+    wt = weight_flipped(w, g.K, 1, 1, rsc)
+    d = _lib.ConvDesc(g.N, 1, 1, rsc, g.K, 1, 1, 1, 1, 1, 0, 0, 0, 0)
+    ss_t = in_ss[:2].repeat(1, rs)  # [2][R*S*C]: channel (r, s, c) -> the BN's channel c
+    sums = arena.zeros((2, rsc), dy.device)
+    _check(L.dtm_conv_dgrad_ex(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d),
+                               _lib.ptr(add_src) if add_src is not None else None, 1, _lib.ptr(x_raw), _lib.ptr(ss_t),
+                               _lib.ptr(sums), int(unscaled), s), "conv_dgrad_act(full window)")
+    torch.sum(sums.view(2, rs, g.C), 1, out=d_in[0:2])
 
 
 # ---------------------------------------------------------------------------------------------
@@ -282,10 +287,11 @@ class _ConvBNFn(torch.autograd.Function):
             last, add_src, add_stride = _slot_take(ctx.slot)
             # stride > 1: one stride-1 conv per output parity class instead of the zero-dilated dgrad
             dec = (g.stride, g.pad_h, g.pad_w) if dgrad_decomposable(g) else None
-            wt = weight_flipped(w, g.K, g.R, g.S, g.C, dec)
+            fullw = in_ss is not None and _full_window(g)
+            wt = weight_flipped(w, g.K, g.R, g.S, g.C, dec) if not fullw else None
             d.dec = int(dec is not None)
             dx = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
-            if in_ss is not None and _full_window(g):
+            if fullw:
                 d_in = arena.zeros((4, g.C), dy.device)
                 _full_window_dgrad_act(g, dy, w, x_raw, in_ss, d_in, dx, ctx.in_unscaled, add_src)
             elif in_ss is not None:

@@ -380,32 +380,47 @@ def test_asp_gpu_ipc_fused_push(kind):
 # update op writes (inception/imagenet_inception_bsp.py:145-149); here every replica must end each
 # step with the same statistics = the pre-step value plus every replica's update of it.
 
-def _bn_sync_worker(rank, world, steps=3):
+def _bn_sync_worker(rank, world, steps=3, gpu=False):
     import copy
 
     from distributed_tensorflow_models_amd.engine import TrainStep, moving_average_buffers
     from distributed_tensorflow_models_amd.models import nets_factory
+    if gpu:  # the HIP kernels (conv epilogue statistics, stats_reduce_finalize moving-average update)
+        os.environ["DTM_DETERMINISTIC"] = "1"
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
     torch.manual_seed(0)
-    model = nets_factory.build("cifar10_resnet_v2", num_classes=10, resnet_size=8)
+    if gpu:
+        model = nets_factory.build("resnet_v1_50", num_classes=16).to(dev)
+        S, ncls, bdt = 64, 16, torch.bfloat16
+    else:
+        dev = torch.device("cpu")
+        model = nets_factory.build("cifar10_resnet_v2", num_classes=10, resnet_size=8)
+        S, ncls, bdt = 32, 10, torch.float32
     step = TrainStep(model, optimizer="momentum", lr=0.05, momentum=0.9, ema_decay=0.99, bucket_mb=0.05)
     g = torch.Generator().manual_seed(100 + rank)  # a DIFFERENT batch on every rank
     local, synced = [], []
     init = torch.cat([b.reshape(-1) for b in moving_average_buffers(model)]).clone()
     for _ in range(steps):
-        x, y = torch.randn(4, 32, 32, 3, generator=g) * (1 + rank), torch.randint(0, 10, (4,), generator=g)
+        x = (torch.randn(4, S, S, 3, generator=g) * (1 + rank)).to(dev, bdt)
+        y = torch.randint(0, ncls, (4,), generator=g).to(dev)
         shadow = copy.deepcopy(model)  # what this replica's forward alone makes of the statistics
         with torch.no_grad():
             shadow(x, training=True)
-        local.append(torch.cat([b.reshape(-1) for b in moving_average_buffers(shadow)]))
+        local.append(torch.cat([b.reshape(-1) for b in moving_average_buffers(shadow)]).cpu())
         step(x, y)
-        synced.append(torch.cat([b.reshape(-1) for b in moving_average_buffers(model)]).clone())
-    shadows = torch.cat([s.reshape(-1) for _b, s in step.opt.buffer_shadows()])
-    return {"local": torch.stack(local), "synced": torch.stack(synced), "shadows": shadows, "init": init,
-            "flat": step.bufsync.numel(), "nbuf": len(moving_average_buffers(model))}
+        synced.append(torch.cat([b.reshape(-1) for b in moving_average_buffers(model)]).cpu().clone())
+    shadows = torch.cat([s.reshape(-1) for _b, s in step.opt.buffer_shadows()]).cpu()
+    out = {"local": torch.stack(local), "synced": torch.stack(synced), "shadows": shadows, "init": init.cpu(),
+           "flat": step.bufsync.numel(), "nbuf": len(moving_average_buffers(model))}
+    step.dp.close()
+    return out
 
 
-def test_bsp_bn_moving_statistics_replica_consistent():
-    res = run_workers(_bn_sync_worker, 2)
+@pytest.mark.parametrize("gpu", [False, pytest.param(True, marks=pytest.mark.gpu)], ids=["cpu", "gpu"])
+def test_bsp_bn_moving_statistics_replica_consistent(gpu):
+    """CPU: reference ops; GPU: two gloo ranks sharing cuda:0 with the HIP kernels computing the statistics."""
+    res = run_workers(_bn_sync_worker, 2, 3, gpu)
     assert res[0]["nbuf"] > 0 and res[0]["flat"] > 0
     # bit-identical replicas after every step (and so are the EMA shadows of the statistics)
     assert torch.equal(res[0]["synced"], res[1]["synced"])

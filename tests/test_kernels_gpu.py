@@ -270,6 +270,58 @@ def test_conv_act_dgrad_tiles_match_reference(tile, act_lds, case):
     assert _rel(sums[1], gref.sum((0, 1, 2))) < 1e-2
 
 
+@pytest.mark.parametrize("stream_side", [1, 0])
+@pytest.mark.parametrize("case", [(4, 28, 28, 64, 256, True, True), (4, 28, 28, 64, 256, False, True),
+                                  (3, 13, 13, 128, 512, True, False), (2, 9, 11, 128, 384, False, True),
+                                  (5, 14, 14, 64, 128, True, True)])
+def test_conv_bnout_dgrad_stream_side(stream_side, case):
+    """Block-output dgrad (the next unit's 1x1 conv1 consuming relu(bn(conv3) + residual)): total = dgrad +
+    add_src, g = total * ReLU bit, sums rows 0-1 = (sum g*x_raw, sum g), rows 4-5 = (sum g*r_raw, sum g) with a BN'd
+    residual.  stream_side 1: the persistent streaming kernel with the side inputs (add_src, x_raw, mask bytes, r_raw)
+    LDS-DMA'd one tile ahead (tile id 34; ragged pixel tail, 1 or 2 k sub-tiles); 0: the shape policy without it."""
+    import ctypes
+
+    import numpy as np
+
+    from distributed_tensorflow_models_amd.ops import _lib
+    from distributed_tensorflow_models_amd.ops.geometry import conv_geom
+    N, H, W, Kc, C, has_r, has_add = case  # Kc: conv1's output channels (the dgrad's reduction), C: its input
+    torch.manual_seed(0)
+    L = _lib.lib()
+    w = (torch.randn(Kc, 1, 1, C, device=DEV) / C ** 0.5).to(torch.bfloat16)
+    g = conv_geom((N, H, W, C), tuple(w.shape), 1, "SAME")
+    dy = torch.randn(N, H, W, Kc, device=DEV).to(torch.bfloat16)
+    wt = torch.empty(C, 1, 1, Kc, device=DEV, dtype=torch.bfloat16)
+    L.dtm_weight_flip_transpose(_lib.ptr(w), _lib.ptr(wt), Kc, 1, 1, C, _lib.stream_ptr())
+    add = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16) if has_add else None
+    xr = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16)
+    rr = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16) if has_r else None
+    bits = np.random.RandomState(1).rand(N * H * W * C) > 0.4
+    mask = torch.from_numpy(np.packbits(bits, bitorder="little")).to(DEV)
+    bm = torch.from_numpy(bits.reshape(N, H, W, C)).to(DEV).float()
+    tot = torch.einsum("nhwk,kc->nhwc", dy.float(), w.float().reshape(Kc, C))
+    if has_add:
+        tot = tot + add.float()
+    gref = tot * bm
+    dx = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
+    sums = torch.zeros(8, C, device=DEV)
+    d = g.as_desc(_lib.ConvDesc)
+    L.dtm_conv_set_stream_side(stream_side)
+    try:
+        rc = L.dtm_conv_dgrad_bnout(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), _lib.ptr(add), 1,
+                                    _lib.ptr(mask), _lib.ptr(xr), _lib.ptr(rr), _lib.ptr(sums), _lib.stream_ptr())
+        assert rc == 0
+        torch.cuda.synchronize()
+    finally:
+        L.dtm_conv_set_stream_side(1)
+    assert _rel(dx, gref) < 1e-2
+    assert _rel(sums[0], (gref * xr.float()).sum((0, 1, 2))) < 1e-2
+    assert _rel(sums[1], gref.sum((0, 1, 2))) < 1e-2
+    if has_r:
+        assert _rel(sums[4], (gref * rr.float()).sum((0, 1, 2))) < 1e-2
+        assert _rel(sums[5], gref.sum((0, 1, 2))) < 1e-2
+
+
 @pytest.mark.parametrize("tile", [0, 1, 6, 10, 12])
 @pytest.mark.parametrize("case", [(4, 15, 15, 64, 96, 3, 2), (2, 14, 14, 128, 256, 3, 1), (3, 7, 7, 512, 200, 1, 1),
                                   (2, 9, 9, 24, 40, 3, 1), (5, 8, 8, 64, 64, 1, 1), (4, 9, 9, 256, 512, 3, 1),
