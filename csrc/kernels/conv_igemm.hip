@@ -167,20 +167,15 @@ __device__ __forceinline__ void epi_barrier() {
 // and a persistent kernel's loop-carried wait for them (vmcnt(n) with the LDS-DMA prefetch issued after
 // them, which the compiler does not count) would drain the prefetch every tile.
 // PRE: the side inputs were DMA'd to LDS by the kernel (pre: [NIT][NT] 16-B add_src chunks, then [NIT][NT]
-// act_x chunks, slot = thread; pre_ss: the block's act scale / shift [2][CT], or nullptr: from a.act_ss) - no
-// global loads here, so no compiler-generated vmcnt waits (add_stride 1, no mask / act_r).  pre_act: the act_x
-// chunks at their own address instead ([PT][CT] bf16 row-major = [NIT][NT] 16-B chunks, slot = thread); pre_r /
-// pre_mask (block-output form, CT = 128): the act_r chunks in the same layout and the ReLU-mask bytes of pixel row p
-// at (p / 16) * 1024 + (p % 16) * 16.
+// act_x chunks, slot = thread; pre_ss: the block's act scale / shift [2][CT]) - no global loads here, so no
+// compiler-generated vmcnt waits (add_stride 1, no mask / act_r).
 // aacc (persistent kernels, with SACC): the activation-backward sums [sum g*x | sum g | sum g*r] of this
 // thread's chunk column are added into aacc[24] across all the block's tiles (one partial row per worker at the
 // kernel's end, worker_row) instead of a per-tile LDS reduction + row.
 template <int PT, int CT, bool RAWB, bool EXACT, bool SACC, int NT, bool SIDE = true, bool PRE = false>
 __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem, int p0, int c0, int by,
                                                  float* ssum, float* ssq, const char* pre = nullptr,
-                                                 const float* pre_ss = nullptr, float* aacc = nullptr,
-                                                 const char* pre_act = nullptr, const char* pre_r = nullptr,
-                                                 const char* pre_mask = nullptr) {
+                                                 const float* pre_ss = nullptr, float* aacc = nullptr) {
   constexpr int OROW = CT * 2 + 16;
   const int tid = threadIdx.x;
   epi_barrier<RAWB>();
@@ -204,8 +199,8 @@ __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem
   if (act && !amask && kc < a.K) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      sc[e] = (PRE && pre_ss) ? pre_ss[chn * 8 + e] : a.act_ss[kc + e];
-      sh[e] = (PRE && pre_ss) ? pre_ss[CT + chn * 8 + e] : a.act_ss[a.K + kc + e];
+      sc[e] = PRE ? pre_ss[chn * 8 + e] : a.act_ss[kc + e];
+      sh[e] = PRE ? pre_ss[CT + chn * 8 + e] : a.act_ss[a.K + kc + e];
     }
   }
   // side inputs of the dgrad post-ops (add_src, act_x, act_r, mask bytes) are loaded for a group of
@@ -231,15 +226,7 @@ __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem
           pa[j] = *(const uint4*)(pre + (size_t)(g0 + j) * NT * 16 + tid * 16);
           ph[j] = true;
         }
-        if (act)
-          px[j] = *(const uint4*)((pre_act ? pre_act : pre + (size_t)NIT * NT * 16) + (size_t)(g0 + j) * NT * 16 +
-                                  tid * 16);
-        if (amask && pre_mask) {
-          // mask bytes of pixel row p at (p / 16) * 1024 + (p % 16) * 16 (one 16-B DMA per pixel: CT = 128)
-          const int row = ((g0 + j) * NT + tid) / CPR;
-          pm[j] = (uint8_t)pre_mask[((row >> 4) << 10) + ((row & 15) << 4) + chn];
-          if (a.act_r && pre_r) pr[j] = *(const uint4*)(pre_r + (size_t)(g0 + j) * NT * 16 + tid * 16);
-        }
+        if (act) px[j] = *(const uint4*)(pre + (size_t)(NIT + g0 + j) * NT * 16 + tid * 16);
       }
     } else if (side) {
 #pragma unroll
@@ -387,9 +374,7 @@ template <int PT, int CT, int WP, int WC, int STG, bool RAWB = false, bool EXACT
 __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&acc)[WC / 16][WP / 16], char* smem,
                                                  int p0, int c0, int by, float* ssum = nullptr,
                                                  float* ssq = nullptr, const char* pre = nullptr,
-                                                 const float* pre_ss = nullptr, float* aacc = nullptr,
-                                                 const char* pre_act = nullptr, const char* pre_r = nullptr,
-                                                 const char* pre_mask = nullptr) {
+                                                 const float* pre_ss = nullptr, float* aacc = nullptr) {
   constexpr int NWP = PT / WP;
   constexpr int TP = WP / 16, TC = WC / 16;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -454,8 +439,7 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
     }
   }
   if constexpr (staged)
-    conv_nt_epi_tail<PT, CT, RAWB, EXACT, SACC, NT, SIDE, PRE>(a, smem, p0, c0, by, ssum, ssq, pre, pre_ss, aacc,
-                                                               pre_act, pre_r, pre_mask);
+    conv_nt_epi_tail<PT, CT, RAWB, EXACT, SACC, NT, SIDE, PRE>(a, smem, p0, c0, by, ssum, ssq, pre, pre_ss, aacc);
 }
 
 template <int PT, int CT, int WP, int WC, int UD, int NBUF>
@@ -663,12 +647,9 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
 // NWP: waves along the pixel dimension (4 / NWP along channels); NWP = 4 with PT = 512, CT = 64 gives every
 // wave a 128 x 64 tile (the 64-channel 3x3 layers: 2x the MFMAs per LDS byte of the 2x2 layout's 64x32)
 //
-// ACTL (act dgrads: the input's BatchNorm+ReLU backward in the epilogue, act_x only - no add_src / mask / act_r;
-// NS = 2): the epilogue's act_x tile [PT][CT] is LDS-DMA'd into the ring slot the last k-tile does not read, issued
-// right after the last k-tile's barrier so it lands under that tile's MFMAs; the epilogue then reads it from LDS
-// (conv_nt_epi_tail pre_act) instead of issuing global loads after the main loop.  The slot left free holds the act
-// tile at one end of the (slightly enlarged) ring and the output staging at the other.
-template <int PT, int CT, int NS, int UD, bool PRO, int NWP = 2, bool ACTL = false>
+// (An ACTL form - the act dgrads' act_x tile LDS-DMA'd under the last k-tile, read by the epilogue from LDS - was
+// neutral at step level, profiles/ab/r4_ab_sside_alds.log, and was removed.)
+template <int PT, int CT, int NS, int UD, bool PRO, int NWP = 2>
 __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
   constexpr int BK = 64;
   constexpr int WP = PT / NWP, WC = CT / (4 / NWP);
@@ -678,12 +659,7 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
   constexpr int BUF = (PT + CT) * 128;
   constexpr int OROW = CT * 2 + 16;
   constexpr int MAXC = 512;
-  constexpr int STGB = PT * OROW;                  // epilogue output staging
-  constexpr int ACTB = ACTL ? PT * CT * 2 : 0;     // act_x tile
-  constexpr int RING0 = NS * BUF > STGB ? NS * BUF : STGB;
-  constexpr int RING1 = ACTB + STGB > BUF + ACTB ? ACTB + STGB : BUF + ACTB;
-  constexpr int RING = ACTL ? (RING1 > NS * BUF ? RING1 : NS * BUF) : RING0;
-  static_assert(!ACTL || (NS == 2 && !PRO && ACTB % 4096 == 0), "act-tile staging: 2 slots, whole wave groups");
+  constexpr int RING = NS * BUF > PT * OROW ? NS * BUF : PT * OROW;
   __shared__ __attribute__((aligned(16))) char smem[RING + (PRO ? MAXC * 8 : 0)];
   typedef __attribute__((address_space(1))) const void gvoid;
   typedef __attribute__((address_space(3))) void lvoid;
@@ -833,25 +809,11 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bf[ks][j], acc[i][j], 0, 0, 0);
   };
 
-  // (ACTL) the act_x tile: chunk q = (wave + 4 i) * 64 + lane -> pixel row q / (CT / 8), channel chunk q % (CT / 8),
-  // LDS bytes q * 16 of the act region (row-major [PT][CT] bf16)
-  auto issue_act = [&](char* dst) {
-    const char* ag = (const char*)a.act_x;
-#pragma unroll
-    for (int i = 0; i < ACTB / 4096; ++i) {
-      const int q = (wave + 4 * i) * 64 + lane;
-      const int m = p0 + q / (CT / 8), kc = c0 + (q % (CT / 8)) * 8;
-      const bool v = (m < a.M) & (kc < a.K);
-      const char* src = ag + ((size_t)out_row(a, v ? m : 0) * a.K + kc) * 2;
-      __builtin_amdgcn_global_load_lds((gvoid*)(v ? src : zg), (lvoid*)(dst + (wave + 4 * i) * 1024), 16, 0, 0);
-    }
-  };
-
   const int nk = (a.Kg + BK - 1) / BK;
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (s < nk) issue(s, s);
-  int slot = 0, last = 0;
+  int slot = 0;
   for (int kt = 0; kt < nk; ++kt) {
     // this wave's DMA of k-tile kt has landed once at most the later stages are still counted
     const int ahead = min(nk - 1, kt + NS - 2) - kt;
@@ -862,27 +824,13 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // stage kt visible to all waves; stage kt-1 no longer read
     if (kt + NS - 1 < nk) issue(kt + NS - 1, slot == 0 ? NS - 1 : slot - 1);
-    if constexpr (ACTL) {
-      // last k-tile: the other slot is free (every wave passed the barrier after reading it)
-      if (kt == nk - 1) issue_act(smem + (slot == 1 ? 0 : RING - ACTB));
-    }
     compute(slot);
-    last = slot;
     slot = slot == NS - 1 ? 0 : slot + 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // the epilogue reuses the ring
-  if constexpr (ACTL) {
-    // act tile in the slot the last k-tile did not read, output staging at the ring's other end
-    const char* act = smem + (last == 1 ? 0 : RING - ACTB);
-    char* stg = smem + (last == 1 ? RING - STGB : 0);
-    conv_nt_epilogue<PT, CT, WP, WC, 1, false, false, false, false, 256, true, true>(a, acc, stg, p0, c0, by, nullptr,
-                                                                                     nullptr, nullptr, nullptr, nullptr,
-                                                                                     act);
-  } else {
-    if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1>(a, acc, smem, p0, c0, by);
-    else conv_nt_epilogue<PT, CT, WP, WC, 2>(a, acc, smem, p0, c0, by);
-  }
+  if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1>(a, acc, smem, p0, c0, by);
+  else conv_nt_epilogue<PT, CT, WP, WC, 2>(a, acc, smem, p0, c0, by);
 }
 
 // 8-wave big-tile variant of the pipelined kernel: PT = 256 pixels x CT (128 | 256) channels per
@@ -1071,12 +1019,10 @@ __device__ __forceinline__ void glds16(const void* gptr, const void* lds) {
 // the 7x7/2 ResNet stem as a persistent stream with its 64 x 224 weights resident in LDS.  Its A tiles
 // (28 KiB of L2-resident rows per 64 pixels) ride a 3-slot ring (NBUF = 3): two tiles in flight.
 //
-// SIDEP (block-output dgrads: add_src + act_x + ReLU bitmask (+ act_r with SIDEP = 2), CT = 128, 2-slot ring): the
-// epilogue's side inputs of tile t+gy are LDS-DMA'd into the other of two side slots right after tile t+gy's A
-// tile, so they land during tile t's MFMAs and epilogue; the epilogue reads them from LDS (no global loads whose
-// compiler waits would drain the prefetch - the reason the global-load form of this kernel did not beat the
-// register-staged tile on these memory-bound dgrads).
-template <int PT, int CT, int NKT, bool PRO, bool STEM = false, int NBUF = 2, bool SIDE = true, int SIDEP = 0>
+// (A form with the block-output dgrads' side inputs - add_src, x_raw, ReLU mask bytes, act_r - LDS-DMA'd one tile
+// ahead was faster per kernel on the 28x28 stage but slower at step level: its 1-block/CU LDS footprint locks the
+// side-stream weight gradients out of the CUs it holds; profiles/ab/r4_ab_sside_alds.log.  Removed.)
+template <int PT, int CT, int NKT, bool PRO, bool STEM = false, int NBUF = 2, bool SIDE = true>
 __global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int ntiles) {
   constexpr int WP = PT / 2, WC = CT / 2;
   constexpr int TP = WP / 16, TC = WC / 16;
@@ -1089,15 +1035,9 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int n
   constexpr int MAXC = 512;
   constexpr int OFF_A = WBUF, OFF_S = WBUF + NBUF * ABUF, OFF_P = OFF_S + STG;
   constexpr int NDMA = NKT * AI;                // DMA instructions per thread per tile
-  // side slots (SIDEP): [add | act_x | (act_r) chunks: NIT * 4 KiB each][mask: 4 KiB]
-  constexpr int NSR = SIDEP == 2 ? 3 : 2;       // chunk regions per side slot
-  constexpr int SSZ = SIDEP ? NSR * NIT * 4096 + 4096 : 0;
-  constexpr int NSD = SIDEP ? NSR * NIT + 1 : 0;  // side DMA instructions per thread per tile
-  constexpr int OFF_SD = OFF_P + (PRO ? MAXC * 8 : 0);
   static_assert(NBUF == 2 || NBUF == 3, "ring depth");
-  static_assert(2 * NIT + NDMA + NSD <= 63, "vmcnt range");
-  static_assert(!SIDEP || (SIDE && NBUF == 2 && PT == 64 && CT == 128 && !STEM), "side prefetch form");
-  __shared__ __attribute__((aligned(16))) char smem[OFF_SD + 2 * SSZ];
+  static_assert(2 * NIT + NDMA <= 63, "vmcnt range");
+  __shared__ __attribute__((aligned(16))) char smem[OFF_P + (PRO ? MAXC * 8 : 0)];
   typedef __attribute__((address_space(1))) const void gvoid;
   typedef __attribute__((address_space(3))) void lvoid;
   static_assert(NIT >= 1 && NIT <= 15, "vmcnt lower bound");
@@ -1161,34 +1101,6 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int n
       }
     }
   };
-  // (SIDEP) side inputs of tile t into side slot sb: thread tid's staged store j is pixel row (j*256 + tid) / 16,
-  // chunk tid % 16 (conv_nt_epi_tail's slot = thread layout); mask: lane l < 16 of wave w moves the 16 mask
-  // bytes (128 channels) of pixel row 16 w + l
-  const char* ssrc[SIDEP ? NSD : 1];
-  auto side_issue = [&](int t, int sb) {
-    if constexpr (SIDEP) {
-      char* base = smem + OFF_SD + sb * SSZ;
-      const int kc = c0 + (tid & 15) * 8;
-#pragma unroll
-      for (int j = 0; j < NIT; ++j) {
-        const int m = t * PT + (j * 256 + tid) / 16;
-        const bool v = (m < a.M) & (kc < a.K);
-        const size_t o = v ? (size_t)m * a.K + kc : 0;
-        ssrc[j] = (v && a.add_src) ? (const char*)(a.add_src + o) : zg;
-        ssrc[NIT + j] = v ? (const char*)(a.act_x + o) : zg;
-        glds16(ssrc[j], base + (j * 4 + wave) * 1024);
-        glds16(ssrc[NIT + j], base + NIT * 4096 + (j * 4 + wave) * 1024);
-        if constexpr (SIDEP == 2) {
-          ssrc[2 * NIT + j] = (v && a.act_r) ? (const char*)(a.act_r + o) : zg;
-          glds16(ssrc[2 * NIT + j], base + 2 * NIT * 4096 + (j * 4 + wave) * 1024);
-        }
-      }
-      const int mp = t * PT + wave * 16 + (lane & 15);
-      const bool mv = (lane < 16) & (mp < a.M) & (c0 < a.K);
-      ssrc[NSR * NIT] = mv ? (const char*)(a.act_mask + ((size_t)mp * a.K + c0) / 8) : zg;
-      glds16(ssrc[NSR * NIT], base + NSR * NIT * 4096 + wave * 1024);
-    }
-  };
   auto transform = [&](int t, int buf) {
     char* base = smem + OFF_A + buf * ABUF;
 #pragma unroll
@@ -1229,7 +1141,6 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int n
   int t = by0;
   const int gy = gridDim.y;
   if (t < ntiles) issue(t, 0);
-  if (SIDEP && t < ntiles) side_issue(t, 0);
   if (NBUF == 3 && t + gy < ntiles) issue(t + gy, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // weights (+ prologue affine) resident, tile 0 (and 1) landed
@@ -1247,11 +1158,7 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int n
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // tile t visible; the slot read last iteration and the stage area are free
     if constexpr (NBUF == 2) {
-      if (t + gy < ntiles) {
-        issue(t + gy, buf ^ 1);
-        // (SIDEP) the other side slot was read by the previous epilogue, finished before the barrier above
-        if constexpr (SIDEP) side_issue(t + gy, buf ^ 1);
-      }
+      if (t + gy < ntiles) issue(t + gy, buf ^ 1);
     } else {
       if (t + 2 * gy < ntiles) issue(t + 2 * gy, buf == 0 ? 2 : buf - 1);
     }
@@ -1284,17 +1191,8 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(ConvNTArgs a, int n
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
       }
     }
-    if constexpr (SIDEP) {
-      const char* sbase = smem + OFF_SD + buf * SSZ;
-      conv_nt_epilogue<PT, CT, WP, WC, 1, true, true, true, true, 256, SIDE, true>(
-          a, acc, smem + OFF_S, t * PT, c0, t, ssum, ssq, sbase, nullptr, aacc, sbase + NIT * 4096,
-          SIDEP == 2 ? sbase + 2 * NIT * 4096 : nullptr, sbase + NSR * NIT * 4096);
-#pragma unroll
-      for (int i = 0; i < NSD; ++i) asm volatile("" ::"v"(ssrc[i]));
-    } else {
-      conv_nt_epilogue<PT, CT, WP, WC, 1, true, true, true, true, 256, SIDE>(a, acc, smem + OFF_S, t * PT, c0, t, ssum,
-                                                                             ssq, nullptr, nullptr, aacc);
-    }
+    conv_nt_epilogue<PT, CT, WP, WC, 1, true, true, true, true, 256, SIDE>(a, acc, smem + OFF_S, t * PT, c0, t, ssum,
+                                                                           ssq, nullptr, nullptr, aacc);
 #pragma unroll
     for (int i = 0; i < NKT * AI; ++i) asm volatile("" ::"v"(srcs[i]));
     buf = buf + 1 == NBUF ? 0 : buf + 1;
@@ -2057,19 +1955,10 @@ static void launch_w8(const ConvNTArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((conv_nt_w8_kernel<PT, CT, NWP, NS, UD>), grid, dim3(512), 0, st, a);
 }
 
-// act dgrads whose epilogue side input is act_x alone (the pipelined kernel's ACTL form: the tile LDS-DMA'd under the
-// last k-tile); A/B knob dtm_conv_set_act_lds
-static int g_act_lds = 1;
-DTM_API void dtm_conv_set_act_lds(int on) { g_act_lds = on; }
-static bool act_lds_ok(const ConvNTArgs& a) {
-  return g_act_lds && a.act_x && !a.act_mask && !a.act_r && !a.add_src && !a.in_scale && (a.K & 7) == 0 && !a.sp_tw;
-}
 template <int PT, int CT, int NS, int UD, int NWP = 2>
 static void launch_pipe(const ConvNTArgs& a, hipStream_t st) {
   dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT, a.ngrp > 1 ? a.ngrp : 1);
   if (a.in_scale) hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, true, NWP>), grid, dim3(256), 0, st, a);
-  else if (NS == 2 && (PT * CT) % 2048 == 0 && act_lds_ok(a))
-    hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, 2, UD, false, NWP, true>), grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, false, NWP>), grid, dim3(256), 0, st, a);
 }
 
@@ -2083,12 +1972,11 @@ static bf16_t* dump_chunk() {
 
 // persistent streaming 1x1 kernel: blocks = resident capacity (occupancy x CUs), channel tiles x
 // pixel-tile workers
-template <int PT, int CT, int NKT, bool PRO, bool STEM = false, int NBUF = 2, bool SIDE = true, int SIDEP = 0>
+template <int PT, int CT, int NKT, bool PRO, bool STEM = false, int NBUF = 2, bool SIDE = true>
 static int stream_workers_k(const ConvNTArgs& a) {
   static int occ = 0;
   if (!occ) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ,
-                                                     conv1x1_stream_kernel<PT, CT, NKT, PRO, STEM, NBUF, SIDE, SIDEP>,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv1x1_stream_kernel<PT, CT, NKT, PRO, STEM, NBUF, SIDE>,
                                                      256, 0) !=
             hipSuccess || occ <= 0)
       occ = 1;
@@ -2101,27 +1989,13 @@ static int stream_workers_k(const ConvNTArgs& a) {
   return workers;
 }
 
-template <int PT, int CT, int NKT, bool PRO, bool STEM = false, int NBUF = 2, bool SIDE = true, int SIDEP = 0>
+template <int PT, int CT, int NKT, bool PRO, bool STEM = false, int NBUF = 2, bool SIDE = true>
 static void launch_stream_k(const ConvNTArgs& a, hipStream_t st) {
   const int ctiles = (a.K + CT - 1) / CT;
   const int ntiles = (a.M + PT - 1) / PT;
-  hipLaunchKernelGGL((conv1x1_stream_kernel<PT, CT, NKT, PRO, STEM, NBUF, SIDE, SIDEP>),
-                     dim3(ctiles, stream_workers_k<PT, CT, NKT, PRO, STEM, NBUF, SIDE, SIDEP>(a)), dim3(256), 0, st, a,
-                     ntiles);
+  hipLaunchKernelGGL((conv1x1_stream_kernel<PT, CT, NKT, PRO, STEM, NBUF, SIDE>),
+                     dim3(ctiles, stream_workers_k<PT, CT, NKT, PRO, STEM, NBUF, SIDE>(a)), dim3(256), 0, st, a, ntiles);
 }
-
-// block-output dgrads (ReLU bitmask + add_src (+ act_r)) on the persistent stream with side-input prefetch (tile id
-// 34; A/B knob dtm_conv_set_stream_side): 1x1, whole 128-channel tiles, Kg <= 128 (act_r: Kg <= 64 - LDS)
-static int g_stream_side = 1;
-DTM_API void dtm_conv_set_stream_side(int on) { g_stream_side = on; }
-static bool stream_side_ok(const ConvNTArgs& a) {
-  return g_stream_side && a.act_mask && a.act_x && !a.in_scale && a.K % 128 == 0 && a.Kg <= 128 &&
-         (a.Kg <= 64 || !a.act_r) && (!a.add_src || a.add_stride == 1);
-}
-#define DTM_SSIDE_SEL(FN, ...)                                                                    \
-  (a.Kg <= 64 ? (a.act_r ? FN<64, 128, 1, false, false, 2, true, 2>(__VA_ARGS__)                  \
-                         : FN<64, 128, 1, false, false, 2, true, 1>(__VA_ARGS__))                 \
-              : FN<64, 128, 2, false, false, 2, true, 1>(__VA_ARGS__))
 
 static bool stem_stream_ok(const ConvNTArgs& a) {
   // the packed-row stem view, no prologue / bias / relu, whole 64-channel tiles, R <= 8 kernel rows
@@ -2152,9 +2026,7 @@ static int stream_workers(const ConvNTArgs& a) {
 static int g_stem_stream = -1;
 DTM_API void dtm_conv_set_stem_stream(int on) { g_stem_stream = on; }
 // statistics partial rows of the streaming kernel (tile id 30 / 31 / 33): one per worker
-static bool stream_ok(const ConvNTArgs& a);
 static int stream_rows(const ConvNTArgs& a, int id) {
-  if (id == 34) return DTM_SSIDE_SEL(stream_workers_k, a);
   if (id == 33) return g_stem_stream == 2 ? stream_workers_k<64, 64, 4, false, true, 2, false>(a)
                                           : stream_workers_k<64, 64, 4, false, true, 3, false>(a);
   const bool k1 = a.Kg <= 64;
@@ -2291,8 +2163,6 @@ static TileCfg pick_tile_impl(const ConvNTArgs& a, bool stats) {
   if (((id == -1 && a.K == 32) || id == 60) && g_direct3 && direct_ok(a)) return {60, 128, 4};
   // the pipelined LDS-DMA 128x128 tile (2 slots, 2 blocks/CU) wins every deep-reduction layer without the
   // prologue (tools/conv_tile_sweep.py: 3x3 at 14x14 / 7x7 -13..-18 %, deep 1x1 -5..-16 %)
-  // block-output dgrads: the persistent stream with side-input prefetch
-  if ((id == -1 || id == 34) && stream_ok(a) && stream_side_ok(a)) return {34, 64, 2};
   if (id == -4) id = -1;  // (-4: the policy without the streaming kernel, for A/B runs)
   else if (id == -1 && a.Kg == 64 && stream_ok(a) && (g_stream_act || !a.act_x) &&
            (!g_policy2 || a.K % 128 == 0 || a.K <= 64))  // (v2: no partial channel tiles: 35x35 ->288 -33 %)
@@ -2364,8 +2234,6 @@ static void dispatch_ud(const ConvNTArgs& a, const TileCfg& t, hipStream_t st) {
   } else if (t.id == 33 && UD == 1) {
     if (g_stem_stream == 2) launch_stream_k<64, 64, 4, false, true, 2, false>(a, st);  // (A/B: 2-slot ring)
     else launch_stream_k<64, 64, 4, false, true, 3, false>(a, st);
-  } else if (t.id == 34 && UD == 1) {
-    DTM_SSIDE_SEL(launch_stream_k, a, st);
   } else if (t.id == 31 && UD == 1) {
     if (a.Kg <= 64) launch_stream<64, 1>(a, st);
     else launch_stream<64, 2>(a, st);
@@ -2557,7 +2425,7 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvD
       if (lt[nl].id == 60) direct_setup(b);
       // act partial rows: one per pixel tile, or one per worker for the persistent kernels
       lrows[nl] = lt[nl].id == 60 ? direct_workers(b)
-                  : (lt[nl].id == 30 || lt[nl].id == 31 || lt[nl].id == 34) ? stream_rows(b, lt[nl].id)
+                  : (lt[nl].id == 30 || lt[nl].id == 31) ? stream_rows(b, lt[nl].id)
                                                          : (b.M + lt[nl].PT - 1) / lt[nl].PT;
       rows += lrows[nl];
       la[nl++] = b;

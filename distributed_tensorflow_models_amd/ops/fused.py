@@ -829,14 +829,16 @@ _SIBLINGS = [None]
 
 class sibling_group:
     """Context: the eligible 1x1 conv+BN calls on ``x`` inside it share one backward (see _SiblingGroup).
-    Knob DTM_SIBLING_GROUP (default off: Inception-v3 -4.8 %, ResNet-50 -0.24 % step on one GPU,
-    profiles/ab/r3_ab_sibling_*, but the 2-rank data-parallel GPU test disagreed with the single-rank result
-    with it on - unresolved; see README Known gaps)."""
+    Knob DTM_SIBLING_GROUP (default on: Inception-v3 -4.8 %, ResNet-50 -0.24 % step on one GPU,
+    profiles/ab/r3_ab_sibling_*).  Data-parallel exactness: the step-1 and step-2 per-parameter gradients of 2 ranks
+    equal the single-rank ones bit for bit (profiles/r4/r4_diag_resnet_sib_2steps.log, tests/test_distributed.py
+    test_bsp_gpu_step1_gradients_match_single_rank); the round-3 2-rank mismatch no longer reproduces
+    (profiles/r4/README.md)."""
 
     def __init__(self, x, training=True):
         import os
         on = (training and torch.is_grad_enabled() and isinstance(x, torch.Tensor) and x.is_cuda and
-              x.requires_grad and os.environ.get("DTM_SIBLING_GROUP", "0") != "0")
+              x.requires_grad and os.environ.get("DTM_SIBLING_GROUP", "1") != "0")
         self.grp = _SiblingGroup(x) if on else None
 
     def __enter__(self):
@@ -909,7 +911,7 @@ def conv_bn(x, w, bn, stride, padding, training, relu):
             lz = x
             in_ss, in_unscaled, x = x.ss, x.unscaled, x.raw
             if (training and lz.unscaled and torch.is_grad_enabled() and x.requires_grad and x.is_cuda and
-                    os.environ.get("DTM_ACT_HANDOFF", "0") != "0"):
+                    os.environ.get("DTM_ACT_HANDOFF", "1") != "0"):
                 # conv consumers of one activation hand the (unscaled, masked) input gradient on: the last one's
                 # act epilogue adds the others' before its mask and sums (Inception's split 1x3 / 3x1 pairs), so
                 # autograd adds neither the gradients nor the BN-gradient sums

@@ -219,14 +219,12 @@ def test_conv_pipelined_tiles_match_reference(tile, prologue, case):
 
 
 @pytest.mark.parametrize("tile", [-1, 4, 21, 24, 26, 32])
-@pytest.mark.parametrize("act_lds", [1, 0])
 @pytest.mark.parametrize("case", [(2, 14, 14, 128, 256, 3, 1), (3, 7, 7, 512, 200, 1, 1), (4, 15, 15, 96, 64, 3, 2),
                                   (2, 28, 28, 128, 128, 3, 2), (2, 9, 9, 64, 40, 3, 1), (2, 30, 30, 64, 128, 1, 1)])
-def test_conv_act_dgrad_tiles_match_reference(tile, act_lds, case):
+def test_conv_act_dgrad_tiles_match_reference(tile, case):
     """dgrad with the input's BatchNorm+ReLU backward in the epilogue (the bottleneck conv2 / conv3 dgrads) on every
-    tile the policy can pick, with the act_x tile LDS-DMA'd under the last k-tile (act_lds 1: the pipelined kernels'
-    ACTL form) or loaded in the epilogue: g = dgrad * [x*scale + shift > 0] (unscaled output), sums = (sum g*x,
-    sum g) per channel; strided cases through the grouped parity-class dgrad."""
+    tile the policy can pick: g = dgrad * [x*scale + shift > 0] (unscaled output), sums = (sum g*x, sum g) per
+    channel; strided cases through the grouped parity-class dgrad."""
     import ctypes
 
     from distributed_tensorflow_models_amd.ops import _lib
@@ -256,7 +254,6 @@ def test_conv_act_dgrad_tiles_match_reference(tile, act_lds, case):
     sums = torch.zeros(2, C, device=DEV)
     dx = torch.empty_like(x)
     L.dtm_conv_set_tile(tile)
-    L.dtm_conv_set_act_lds(act_lds)
     try:
         rc = L.dtm_conv_dgrad_ex(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), None, 1, _lib.ptr(x),
                                  _lib.ptr(ss4), _lib.ptr(sums), 1, _lib.stream_ptr())
@@ -264,21 +261,19 @@ def test_conv_act_dgrad_tiles_match_reference(tile, act_lds, case):
         torch.cuda.synchronize()
     finally:
         L.dtm_conv_set_tile(-1)
-        L.dtm_conv_set_act_lds(1)
     assert _rel(dx, gref) < 1e-2
     assert _rel(sums[0], (gref * x.float()).sum((0, 1, 2))) < 1e-2
     assert _rel(sums[1], gref.sum((0, 1, 2))) < 1e-2
 
 
-@pytest.mark.parametrize("stream_side", [1, 0])
 @pytest.mark.parametrize("case", [(4, 28, 28, 64, 256, True, True), (4, 28, 28, 64, 256, False, True),
                                   (3, 13, 13, 128, 512, True, False), (2, 9, 11, 128, 384, False, True),
-                                  (5, 14, 14, 64, 128, True, True)])
-def test_conv_bnout_dgrad_stream_side(stream_side, case):
+                                  (5, 14, 14, 64, 128, True, True), (3, 14, 14, 256, 1024, False, True),
+                                  (2, 7, 9, 256, 256, True, True)])
+def test_conv_bnout_dgrad(case):
     """Block-output dgrad (the next unit's 1x1 conv1 consuming relu(bn(conv3) + residual)): total = dgrad +
     add_src, g = total * ReLU bit, sums rows 0-1 = (sum g*x_raw, sum g), rows 4-5 = (sum g*r_raw, sum g) with a BN'd
-    residual.  stream_side 1: the persistent streaming kernel with the side inputs (add_src, x_raw, mask bytes, r_raw)
-    LDS-DMA'd one tile ahead (tile id 34; ragged pixel tail, 1 or 2 k sub-tiles); 0: the shape policy without it."""
+    residual (ragged pixel tails; reductions of 64 / 128 / 256)."""
     import ctypes
 
     import numpy as np
@@ -306,14 +301,10 @@ def test_conv_bnout_dgrad_stream_side(stream_side, case):
     dx = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
     sums = torch.zeros(8, C, device=DEV)
     d = g.as_desc(_lib.ConvDesc)
-    L.dtm_conv_set_stream_side(stream_side)
-    try:
-        rc = L.dtm_conv_dgrad_bnout(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), _lib.ptr(add), 1,
-                                    _lib.ptr(mask), _lib.ptr(xr), _lib.ptr(rr), _lib.ptr(sums), _lib.stream_ptr())
-        assert rc == 0
-        torch.cuda.synchronize()
-    finally:
-        L.dtm_conv_set_stream_side(1)
+    rc = L.dtm_conv_dgrad_bnout(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), _lib.ptr(add), 1,
+                                _lib.ptr(mask), _lib.ptr(xr), _lib.ptr(rr), _lib.ptr(sums), _lib.stream_ptr())
+    assert rc == 0
+    torch.cuda.synchronize()
     assert _rel(dx, gref) < 1e-2
     assert _rel(sums[0], (gref * xr.float()).sum((0, 1, 2))) < 1e-2
     assert _rel(sums[1], gref.sum((0, 1, 2))) < 1e-2
