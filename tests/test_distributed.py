@@ -200,6 +200,101 @@ def test_bsp_gpu_step1_gradients_match_single_rank(model, knobs):
     assert torch.equal(two[0]["params"], two[1]["params"])
 
 
+# The round-3 sibling-merge data-parallel mismatch, reduced to its mechanism (profiles/r4/README.md): a fused op
+# that returns None for a parameter whose gradient a LATER op of the same backward writes into main_grad (the
+# non-last members of a merged sibling group).  PyTorch still runs the parameter's post-accumulate-grad hook when
+# the op returned None; the round-3 hook treated that as "ready", so the bucket's all-reduce was issued before the
+# real gradient was written and the write was lost from the sum (world 1 never launches a collective, hence
+# invisible single-rank).
+class _DeferredGradFn(torch.autograd.Function):
+    """y = x * w; the gradient of w is left to a later op (returned as None here, stashed in PENDING)."""
+    PENDING = []
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x)
+        return x * w
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        _DeferredGradFn.PENDING.append((g * x).sum(0))
+        return g * ctx.w_value, None
+
+
+class _MergedGradFn(torch.autograd.Function):
+    """y = x * v; writes v's gradient and the deferred one of w straight into main_grad, then notifies both."""
+
+    @staticmethod
+    def forward(ctx, x, v, w):
+        ctx.save_for_backward(x, v)
+        ctx.w = w
+        return x * v
+
+    @staticmethod
+    def backward(ctx, g):
+        from distributed_tensorflow_models_amd.ops import nn as opsnn
+        x, v = ctx.saved_tensors
+        w = ctx.w
+        opsnn.grad_target(v).add_((g * x).sum(0))
+        opsnn._notify(v)
+        opsnn.grad_target(w).add_(_DeferredGradFn.PENDING.pop())
+        opsnn._notify(w)
+        return g * v, None, None
+
+
+def _deferred_grad_worker(rank, world):
+    from distributed_tensorflow_models_amd.parallel.bsp import BSPDataParallel
+    torch.manual_seed(0)
+    v = torch.nn.Parameter(torch.randn(5))
+    w = torch.nn.Parameter(torch.randn(5))
+    dp = BSPDataParallel([v, w], bucket_mb=1e-5, check=True, names=[("v", v), ("w", w)])
+    try:
+        x = torch.randn(3, 5, generator=torch.Generator().manual_seed(1 + rank))
+        dp.zero_grad()
+        ctx_w = w.detach()
+        y = _MergedGradFn.apply(x, v, w)      # backward runs second: writes both gradients
+        z = _DeferredGradFn.apply(y, w)       # backward runs first: returns None for w
+        z.grad_fn.w_value = ctx_w
+        z.sum().backward()
+        dp.finish()
+        return {"v": v.main_grad.clone() / world, "w": w.main_grad.clone() / world, "x": x, "vv": v.detach(),
+                "wv": w.detach(), "launched": sum(dp._launched), "buckets": len(dp.buckets)}
+    finally:
+        dp.close()
+
+
+def test_bsp_deferred_gradient_not_reported_early():
+    res = run_workers(_deferred_grad_worker, 2)
+    xs = [r["x"] for r in res]
+    v, w = res[0]["vv"], res[0]["wv"]
+    # d/dw sum((x*v)*w) = sum_rows x*v ; d/dv = sum_rows x*w ; mean over the two ranks' batches
+    want_w = sum((x * v).sum(0) for x in xs) / 2
+    want_v = sum((x * w).sum(0) for x in xs) / 2
+    for r in res:
+        assert r["launched"] == r["buckets"] > 1
+        torch.testing.assert_close(r["w"], want_w)
+        torch.testing.assert_close(r["v"], want_v)
+
+
+def test_bsp_post_accumulate_hook_without_grad_is_not_ready():
+    """The unit form: the hook with p.grad None (an op returned None and will write main_grad itself) must not
+    mark p ready."""
+    from distributed_tensorflow_models_amd.parallel.bsp import BSPDataParallel
+    a, b = torch.nn.Parameter(torch.zeros(4)), torch.nn.Parameter(torch.zeros(3))
+    dp = BSPDataParallel([a, b], bucket_mb=1e-5)
+    try:
+        dp.zero_grad()
+        a.grad = None
+        dp._on_accumulated(a)
+        assert a not in dp._seen and not any(dp._launched)
+        a.grad = torch.ones(4)
+        dp._on_accumulated(a)
+        assert a in dp._seen and a.grad is None and torch.equal(a.main_grad, torch.ones(4))
+    finally:
+        dp.close()
+
+
 def test_bsp_check_catches_late_gradient_write():
     """The BSP write checker: a ready notification before the gradient write (the defect class that drops a
     write from the all-reduce) raises, naming the parameter."""
