@@ -2360,6 +2360,8 @@ DTM_API int dtm_conv_dgrad_ex(const void* dy, const void* wt, void* dx, const Co
 // A/B knob (dtm_conv_set_dec_group): the parity classes of a stride-decomposed dgrad as one grouped launch
 static int g_dec_group = 1;
 DTM_API void dtm_conv_set_dec_group(int on) { g_dec_group = on; }
+static int g_dec_lpt = 1;  // A/B knob: the grouped classes in descending tap count (dtm_conv_set_dec_lpt)
+DTM_API void dtm_conv_set_dec_lpt(int on) { g_dec_lpt = on; }
 
 static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvDesc* d, const void* add_src,
                            int add_stride, const void* act_x, const float* act_ss, float* act_sums, int act_unscaled,
@@ -2461,8 +2463,19 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvD
   if (gi >= 0) {
     ConvNTArgs g = la[gi];
     g.ngrp = nl;
-    for (int i = 0; i < nl; ++i) {
-      g.grp[i] = {la[i].w, la[i].act_sums, la[i].R, la[i].S, la[i].pad_h, la[i].pad_w, la[i].oa, la[i].ob, la[i].Kg};
+    // classes in descending tap count: blocks are dispatched roughly in grid order and z-slice g covers the g-th
+    // block range, so the heaviest class (4 of a 3x3's 9 taps at stride 2) starts first and the 1-tap class fills
+    // the tail (longest-processing-time order) instead of the reverse
+    int ord[4] = {0, 1, 2, 3};
+    for (int i = 1; i < nl; ++i)
+      for (int j = i; j > 0 && la[ord[j]].Kg > la[ord[j - 1]].Kg; --j) {
+        const int t = ord[j];
+        ord[j] = ord[j - 1];
+        ord[j - 1] = t;
+      }
+    for (int q = 0; q < nl; ++q) {
+      const int i = g_dec_lpt ? ord[q] : q;
+      g.grp[q] = {la[i].w, la[i].act_sums, la[i].R, la[i].S, la[i].pad_h, la[i].pad_w, la[i].oa, la[i].ob, la[i].Kg};
     }
     dispatch_nt(g, 1, lt[gi], (hipStream_t)stream);
   } else {

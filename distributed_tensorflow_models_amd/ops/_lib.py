@@ -120,6 +120,7 @@ _SIGS = {
     "dtm_conv_set_kwide": (None, [_I]),
     "dtm_set_reduce_few": (None, [_I]),
     "dtm_set_reserved_cus": (None, [_I]),
+    "dtm_conv_set_dec_lpt": (None, [_I]),
     "dtm_get_reserved_cus": (_I, []),
     "dtm_compute_cus_api": (_I, []),
     "dtm_cu_hog": (_I, [_I, _F, _P]),
