@@ -52,9 +52,14 @@ def grad_worker(rank, world, model_name, knobs=None, bucket_mb=2.0, overlap=True
     y = torch.randint(0, kw["num_classes"], (B,), generator=g).to(dev)
     n_sib = fused.SIBLING_MERGED[0]
     grads = []
-    for _ in range(steps):
+    import sys
+    import time
+    t0 = time.time()
+    for i in range(steps):
         step(x, y)
         torch.cuda.synchronize()
+        print("dp_check rank %d/%d %s %s: step %d done (%.1f s)" % (rank, world, model_name, knobs or {}, i + 1,
+                                                                   time.time() - t0), file=sys.stderr, flush=True)
         names = {p: n for n, p in model.named_parameters()}
         grads.append([(names[p], (p.main_grad.detach().float() / world).cpu()) for p in step.dp.order])
     out = {"grads": grads, "buckets": len(step.dp.buckets), "launched": sum(step.dp._launched),

@@ -22,11 +22,16 @@ def _entry(rank, fn, world, port, outdir, args):
     torch.set_num_threads(max(1, (os.cpu_count() or 2) // world))
     from ..parallel import process_group as pg
     pg.init(backend="gloo", timeout_s=120)
+    ok = False
     try:
         out = fn(rank, world, *args)
         torch.save(out, os.path.join(outdir, "r%d.pt" % rank))
+        ok = True
     finally:
-        pg.barrier()
+        # a failed rank leaves at once (no barrier): the others' pending collectives then fail instead of waiting
+        # for the gloo timeout, and start_processes reports the first error
+        if ok:
+            pg.barrier()
         pg.destroy()
 
 
