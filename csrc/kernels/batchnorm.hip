@@ -536,10 +536,12 @@ static void fast_grid(long M, int C, int* blocks, int* rpb) {
 // without a separate launch.  Correctness of the hand-off: each block's atomics complete (s_waitcnt in
 // the issuing wave) before its counter increment, and the totals are read with memory-side atomics
 // (never a stale L2 line of another XCD).
+template <bool MULTI>
 __global__ __launch_bounds__(256) void stats_reduce_finalize_kernel(
     const float* __restrict__ ws, int rows, int K, int rpb, float* acc, unsigned* counter,
     const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ mov_mean,
-    float* __restrict__ mov_var, float* __restrict__ out, float count, float eps, float decay, int update, int bessel) {
+    float* __restrict__ mov_var, float* __restrict__ out, float count, float eps, float decay, int update, int bessel,
+    FinGroup grp) {
   __shared__ float4 red[16][16];
   __shared__ int is_last;
   const int width = 2 * K;
@@ -592,9 +594,19 @@ __global__ __launch_bounds__(256) void stats_reduce_finalize_kernel(
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-    const int c = cb + i * 256 + threadIdx.x;
-    if (c >= K) break;
-    bn_fin_channel(sv[i], qv[i], c, K, gamma, beta, mov_mean, mov_var, out, count, eps, decay, update, bessel);
+      const int c = cb + i * 256 + threadIdx.x;
+      if (c >= K) break;
+      if constexpr (MULTI) {
+        FinMember mb = grp.m[0];
+#pragma unroll
+        for (int j = 1; j < 8; ++j)  // (constant indices: no scratch copy of the argument table)
+          if (j < grp.n && c >= grp.m[j].off) mb = grp.m[j];
+        if (mb.out)
+          bn_fin_channel(sv[i], qv[i], c - mb.off, mb.K, mb.gamma, mb.beta, mb.mov_mean, mb.mov_var, mb.out, count,
+                         eps, decay, update, bessel);
+      } else {
+        bn_fin_channel(sv[i], qv[i], c, K, gamma, beta, mov_mean, mov_var, out, count, eps, decay, update, bessel);
+      }
     }
   }
   if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -776,10 +788,17 @@ static float* g_fin_acc[DTM_WS_SLOTS] = {};
 static unsigned* g_fin_counter[DTM_WS_SLOTS] = {};
 static int g_fin_k[DTM_WS_SLOTS] = {};
 
-// ss[4][K] (+ moving averages) from the partial statistics rows ws[rows][2K], one launch.
+// ss[4][K] (+ moving averages) from the partial statistics rows ws[rows][2K], one launch.  fg (optional): the
+// K columns belong to several BatchNorms (FinGroup, common.h).
 int dtm_bn_stats_finalize(const float* ws, int rows, int K, const float* gamma, const float* beta, float* mov_mean,
                           float* mov_var, float* ss, float count, float eps, float decay, int update, int bessel,
                           hipStream_t st) {
+  return dtm_bn_stats_finalize_g(ws, rows, K, gamma, beta, mov_mean, mov_var, ss, count, eps, decay, update, bessel, st,
+                                 nullptr);
+}
+int dtm_bn_stats_finalize_g(const float* ws, int rows, int K, const float* gamma, const float* beta, float* mov_mean,
+                            float* mov_var, float* ss, float count, float eps, float decay, int update, int bessel,
+                            hipStream_t st, const FinGroup* fg) {
   if (!dtm_device_ok()) return -9;
   const int k = dtm_ws_slot(st);
   if (K > g_fin_k[k]) {
@@ -803,8 +822,16 @@ int dtm_bn_stats_finalize(const float* ws, int rows, int K, const float* gamma, 
   if (K % 2) return -1;  // float4 columns over [2K]
   int rpb, ychunks;
   dtm_reduce_split(rows, (2 * K + 63) / 64, &rpb, &ychunks);
-  hipLaunchKernelGGL(stats_reduce_finalize_kernel, dim3((2 * K + 63) / 64, ychunks), dim3(256), 0, st, ws, rows, K, rpb,
-                     g_fin_acc[k], g_fin_counter[k], gamma, beta, mov_mean, mov_var, ss, count, eps, decay, update,
-                     bessel);
+  if (fg) {
+    hipLaunchKernelGGL(stats_reduce_finalize_kernel<true>, dim3((2 * K + 63) / 64, ychunks), dim3(256), 0, st, ws, rows,
+                       K, rpb, g_fin_acc[k], g_fin_counter[k], gamma, beta, mov_mean, mov_var, ss, count, eps, decay,
+                       update, bessel, *fg);
+  } else {
+    FinGroup none;
+    none.n = 0;
+    hipLaunchKernelGGL(stats_reduce_finalize_kernel<false>, dim3((2 * K + 63) / 64, ychunks), dim3(256), 0, st, ws,
+                       rows, K, rpb, g_fin_acc[k], g_fin_counter[k], gamma, beta, mov_mean, mov_var, ss, count, eps,
+                       decay, update, bessel, none);
+  }
   return 0;
 }

@@ -68,6 +68,24 @@ int dtm_compute_cus();  // CUs the persistent / split-K grids size for: the devi
 void dtm_reduce_split(int rows, int xblocks, int* rpb, int* ychunks);
 int dtm_reduce_direct_max();
 int dtm_ntld_bits();  // non-temporal input-load policy of the BN-apply kernels (fused_bn.hip)  // grids up to this many blocks reduce with atomics in the producer
+// FinGroup (merged sibling convs, ops/fused.py): the K columns of one statistics table are several BatchNorms side by
+// side - member j owns columns [off_j, off_j + K_j) and its own parameters / moving statistics / ss output (out ==
+// nullptr: a member without BatchNorm, e.g. Inception's commuted pool-branch conv, whose statistics are unused)
+struct FinMember {
+  const float* gamma;
+  const float* beta;
+  float* mov_mean;
+  float* mov_var;
+  float* out;
+  int off, K;
+};
+struct FinGroup {
+  int n;
+  FinMember m[8];
+};
+int dtm_bn_stats_finalize_g(const float* ws, int rows, int K, const float* gamma, const float* beta, float* mov_mean,
+                            float* mov_var, float* ss, float count, float eps, float decay, int update, int bessel,
+                            hipStream_t st, const FinGroup* fg);
 int dtm_bn_stats_finalize(const float* ws, int rows, int K, const float* gamma, const float* beta, float* mov_mean,
                           float* mov_var, float* ss, float count, float eps, float decay, int update, int bessel,
                           hipStream_t st);

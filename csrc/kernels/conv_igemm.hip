@@ -84,6 +84,14 @@ struct ConvNTArgs {
     float* act_sums;
     int R, S, pad_h, pad_w, oa, ob, Kg;
   } grp[4];
+  // merged sibling convs (forward, nsplit > 0): output channel k belongs to member j (split[j].off <= k <
+  // split[j+1].off) and is stored at split[j].y[pixel][k - off_j] (row of split[j].K) - one conv over the members'
+  // concatenated weights writing each member's own contiguous output (ops/fused.py _SiblingGroup)
+  int nsplit;
+  struct Split {
+    bf16_t* y;
+    int off, K;
+  } split[8];
 };
 
 // block -> (class, tile) of a grouped launch (XCD remap over the whole grid; class = z-slice of the logical
@@ -325,7 +333,16 @@ __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem
           }
           v = make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
         }
-        *(uint4*)(inb ? a.y + o : a.dump) = v;
+        bf16_t* dst = a.y + o;
+        if (a.nsplit) {  // (merged siblings: each member's own output tensor; constant indices, no scratch)
+          int off = a.split[0].off, kk = a.split[0].K;
+          bf16_t* yb = a.split[0].y;
+#pragma unroll
+          for (int q = 1; q < 8; ++q)
+            if (q < a.nsplit && kc >= a.split[q].off) { yb = a.split[q].y; off = a.split[q].off; kk = a.split[q].K; }
+          dst = yb + (size_t)out_row(a, m) * kk + (kc - off);
+        }
+        *(uint4*)(inb ? dst : a.dump) = v;
       }
     }
   }
@@ -2257,12 +2274,13 @@ DTM_API int dtm_get_deterministic();
 
 static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, const float* bias, const float* in_scale,
                          const float* in_shift, int relu, const ConvDesc* d, hipStream_t stream, float** rows_ws,
-                         int* nrows) {
+                         int* nrows, const ConvNTArgs::Split* split = nullptr, int nsplit = 0) {
   if (!dtm_device_ok()) return -9;
   if (d->C % 8 || d->K % 4) return -1;
   ConvNTArgs a;
   a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.y = (bf16_t*)y;
   a.ngrp = 0;
+  a.nsplit = 0;
   a.stats = nullptr; a.bias = bias; a.in_scale = in_scale; a.in_shift = in_shift;
   a.add_src = nullptr; a.act_x = nullptr; a.act_ss = nullptr; a.act_sums = nullptr;
   a.act_mask = nullptr; a.act_r = nullptr;
@@ -2281,8 +2299,19 @@ static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, cons
   a.fd_PQ = make_fastdiv(d->P * d->Q); a.fd_Q = make_fastdiv(d->Q);
   a.ostr = 1; a.oa = a.ob = 0; a.OH = a.P; a.OW = a.Q;
   a.sp_tw = a.sp_th = 0;
+  if (nsplit > 0) {
+    if (nsplit > 8 || d->K % 8) return -1;
+    a.nsplit = nsplit;
+    for (int i = 0; i < nsplit; ++i) {
+      if (split[i].off % 8 || split[i].K % 8) return -1;
+      a.split[i] = split[i];
+    }
+  }
   int rows = 0;
   const TileCfg tc = pick_tile(a, stats);
+  // (merged-sibling stores happen in the LDS-staged epilogue only: K % 8 == 0 above; the persistent / direct
+  // kernels have their own store paths)
+  if (nsplit > 0 && (tc.id == 30 || tc.id == 31 || tc.id == 33 || tc.id == 60)) return -1;
   if (tc.id == 60) direct_setup(a);
   if (stats) {
     // one per streaming / direct worker; one per pixel tile (staged epilogue, K % 8 == 0); else per (pixel
@@ -2309,6 +2338,43 @@ DTM_API int dtm_conv_fwd(const void* x, const void* w, void* y, float* stats, co
   if (rc) return rc;
   if (stats) dtm_reduce_rows(ws, rows, 2 * d->K, 2 * d->K, stats, (hipStream_t)stream);
   return 0;
+}
+
+// Merged sibling 1x1 convs on one input (ops/fused.py _SiblingGroup, Inception mixed-block branch heads): ONE conv
+// over the members' concatenated weights w [sum K][1][1][C] (d->K = sum K) storing each member's output in its own
+// tensor (ys[j], K_j channels), the BatchNorm statistics of all columns from its epilogue, and ONE finalize writing
+// every BN member's ss / moving statistics (bn_ptrs[j] = {gamma, beta, mov_mean, mov_var, ss} or ss = 0 for a
+// member without BatchNorm).  Instead of one conv + one finalize launch per member.
+DTM_API int dtm_conv_fwd_bn_multi(const void* x, const void* w, void* const* ys, const int* ks, int n,
+                                  void* const* bn_ptrs, float count, float eps, float decay, int update, int bessel,
+                                  const ConvDesc* d, void* stream) {
+  if (n < 1 || n > 8) return -1;
+  ConvNTArgs::Split sp[8];
+  FinGroup fg;
+  fg.n = n;
+  int off = 0;
+  for (int i = 0; i < n; ++i) {
+    sp[i].y = (bf16_t*)ys[i];
+    sp[i].off = off;
+    sp[i].K = ks[i];
+    FinMember& m = fg.m[i];
+    m.gamma = (const float*)bn_ptrs[5 * i];
+    m.beta = (const float*)bn_ptrs[5 * i + 1];
+    m.mov_mean = (float*)bn_ptrs[5 * i + 2];
+    m.mov_var = (float*)bn_ptrs[5 * i + 3];
+    m.out = (float*)bn_ptrs[5 * i + 4];
+    m.off = off;
+    m.K = ks[i];
+    off += ks[i];
+  }
+  for (int i = n; i < 8; ++i) fg.m[i] = fg.m[0];
+  if (off != d->K || d->R != 1 || d->S != 1) return -1;
+  float* ws = nullptr;
+  int rows = 0;
+  int rc = conv_fwd_impl(x, w, nullptr, true, nullptr, nullptr, nullptr, 0, d, (hipStream_t)stream, &ws, &rows, sp, n);
+  if (rc) return rc;
+  return dtm_bn_stats_finalize_g(ws, rows, d->K, nullptr, nullptr, nullptr, nullptr, nullptr, count, eps, decay, update,
+                                 bessel, (hipStream_t)stream, &fg);
 }
 
 // Training conv -> BatchNorm statistics -> finalize in two launches: the conv (statistics partial
@@ -2373,6 +2439,7 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvD
   ConvNTArgs a;
   a.x = (const bf16_t*)dy; a.w = (const bf16_t*)wt; a.y = (bf16_t*)dx;
   a.ngrp = 0;
+  a.nsplit = 0;
   a.stats = nullptr; a.bias = nullptr; a.in_scale = nullptr; a.in_shift = nullptr;
   a.add_src = (const bf16_t*)add_src; a.act_x = (const bf16_t*)act_x; a.act_ss = act_ss; a.act_sums = nullptr;
   a.act_mask = (const uint8_t*)act_mask; a.act_r = (const bf16_t*)act_r;

@@ -546,6 +546,118 @@ DTM_API int dtm_stats_combine_fin_ld(const void* dy, const void* x, const float*
   return 0;
 }
 
+// ---- grouped stats-combine of a merged sibling group (ops/fused.py _SiblingGroup): every member's combined
+// gradient comb_i = g_i*scale_i + ds_i + 2*dq_i*y_i written into its column slice [off_i, off_i + C_i) of ONE
+// [M][ldo] buffer, members as gridDim.y, in one launch instead of one per member; a member without BatchNorm
+// (dss == nullptr: Inception's commuted pool-branch conv) is copied into its slice.
+struct CombMember {
+  const bf16_t* dy;
+  const bf16_t* x;
+  const float* dss;
+  const float* ss;
+  const float* gamma;
+  float* dgamma;
+  float* dbeta;
+  int C, off;
+};
+struct CombGroup {
+  CombMember m[8];
+};
+
+__global__ __launch_bounds__(256) void stats_combine_multi_kernel(CombGroup grp, float count, bf16_t* __restrict__ out,
+                                                                  int M, int rpb, int ldo) {
+  __shared__ float s_ab[2][2048];
+  CombMember mb;
+  // constant-index selection (a dynamically indexed argument array would go through scratch)
+  switch (blockIdx.y) {
+    case 0: mb = grp.m[0]; break;
+    case 1: mb = grp.m[1]; break;
+    case 2: mb = grp.m[2]; break;
+    case 3: mb = grp.m[3]; break;
+    case 4: mb = grp.m[4]; break;
+    case 5: mb = grp.m[5]; break;
+    case 6: mb = grp.m[6]; break;
+    default: mb = grp.m[7]; break;
+  }
+  const int C = mb.C;
+  const int cols = C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t % cols) * 8, lr0 = t / cols;
+  const bool bn = mb.dss != nullptr;
+  for (int c = t; c < C; c += 256) {
+    float ds = 0.f, dq = 0.f, dg, db;
+    if (bn) {
+      fin_bwd_channel(mb.dss, mb.ss, mb.gamma, C, c, count, &ds, &dq, &dg, &db);
+      if (blockIdx.x == 0) {
+        if (mb.dgamma) mb.dgamma[c] += dg;
+        if (mb.dbeta) mb.dbeta[c] += db;
+      }
+    }
+    s_ab[0][c] = ds;
+    s_ab[1][c] = 2.f * dq;
+  }
+  __syncthreads();
+  float a[8], b[8], sc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    a[e] = s_ab[0][c0 + e];
+    b[e] = s_ab[1][c0 + e];
+    sc[e] = bn ? mb.ss[c0 + e] : 1.f;  // (dy is the unscaled g)
+  }
+  const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
+  bf16_t* o = out + mb.off;
+  for (int row = lr0 < RP ? r0 + lr0 : r1; row < r1; row += RP * 4) {
+    uint4 vd[4], vx[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int rr = row + u * RP;
+      const bool ok = rr < r1;
+      const size_t q = (size_t)rr * C + c0;
+      vd[u] = ok ? *(const uint4*)(mb.dy + q) : make_uint4(0, 0, 0, 0);
+      vx[u] = (ok && bn) ? *(const uint4*)(mb.x + q) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int rr = row + u * RP;
+      if (rr >= r1) break;
+      float d[8], xv[8];
+      up8(vd[u], d); up8(vx[u], xv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = fmaf(d[e], sc[e], a[e] + b[e] * xv[e]);
+      *(uint4*)(o + (size_t)rr * ldo + c0) = pk8(d);
+    }
+  }
+}
+
+// descs: n x {dy, x, dss (or 0), ss, gamma, dgamma, dbeta} pointers as int64 + {C, off} ints, host memory
+DTM_API int dtm_stats_combine_multi(const void* const* ptrs, const int* dims, int n, float count, void* out, long M,
+                                    int ldo, void* stream) {
+  if (n < 1 || n > 8 || ldo % 8 || M >= (1l << 31)) return -1;
+  CombGroup g;
+  int cmax = 0;
+  for (int i = 0; i < 8; ++i) {
+    CombMember& m = g.m[i];
+    if (i >= n) {
+      m = g.m[0];
+      continue;
+    }
+    m.dy = (const bf16_t*)ptrs[7 * i];
+    m.x = (const bf16_t*)ptrs[7 * i + 1];
+    m.dss = (const float*)ptrs[7 * i + 2];
+    m.ss = (const float*)ptrs[7 * i + 3];
+    m.gamma = (const float*)ptrs[7 * i + 4];
+    m.dgamma = (float*)ptrs[7 * i + 5];
+    m.dbeta = (float*)ptrs[7 * i + 6];
+    m.C = dims[2 * i];
+    m.off = dims[2 * i + 1];
+    if (!shape_ok(M, m.C) || m.C > 2048 || m.off % 8 || m.off + m.C > ldo) return -1;
+    if (m.C > cmax) cmax = m.C;
+  }
+  int blocks, rpb;
+  grid2(M, cmax, &blocks, &rpb, g_sc_cap);
+  hipLaunchKernelGGL(stats_combine_multi_kernel, dim3(blocks, n), dim3(256), 0, (hipStream_t)stream, g, count,
+                     (bf16_t*)out, (int)M, rpb, ldo);
+  return 0;
+}
+
 // A/B policy of the stats-combine stream: variant (0 U4, 1 U8, 2 U4 nt, 3 U8 nt, 4 U2, 5 U4 nt loads,
 // 6 U4 nt stores) and block cap
 DTM_API void dtm_set_sc_policy(int variant, int cap) {

@@ -16,7 +16,25 @@ from .utils.profiler import range_pop, range_push, roctx
 
 
 def prepare_compute_copies(model):
-    """Create the bf16 compute copy of every matrix/conv weight (refreshed by the optimizer)."""
+    """Create the bf16 compute copy of every matrix/conv weight (refreshed by the optimizer).  Weight groups the
+    model declares (``sibling_weight_groups``: the 1x1 branch heads of an Inception mixed block, same input
+    channels) get their copies as consecutive views of ONE [sum K][1][1][C] buffer, recorded as ``p._sib_cat =
+    (buffer, row offset)``: the merged head conv reads them as one weight (ops.fused._SiblingGroup.forward_all)."""
+    groups = model.sibling_weight_groups() if hasattr(model, "sibling_weight_groups") else []
+    for grp in groups:
+        if not grp or not all(p.is_cuda and p.dim() == 4 and p.shape[1:] == grp[0].shape[1:] for p in grp):
+            continue
+        if any(getattr(p, "_sib_cat", None) is not None for p in grp):
+            continue
+        buf = torch.empty((sum(p.shape[0] for p in grp),) + tuple(grp[0].shape[1:]), device=grp[0].device,
+                          dtype=torch.bfloat16)
+        off = 0
+        for p in grp:
+            v = buf[off:off + p.shape[0]]
+            v.copy_(p.detach())
+            p.bf16 = v
+            p._sib_cat = (buf, off)
+            off += p.shape[0]
     for p in model.parameters():
         if p.is_cuda and p.dim() >= 2 and getattr(p, "bf16", None) is None:
             p.bf16 = p.detach().to(torch.bfloat16)

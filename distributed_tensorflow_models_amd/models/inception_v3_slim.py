@@ -9,6 +9,8 @@ Defaults (inception_v3_parameters): weight decay 4e-5 on conv+fc weights, conv s
 BN decay 0.9997 eps 1e-3 (biased moving variance - tf.nn.moments path), dropout keep 0.8.
 Returns (logits, aux_logits) in training mode; the trainer weights the aux loss by 0.4.
 """
+import os
+
 import torch
 
 from ..ops import nn as F
@@ -139,6 +141,29 @@ class InceptionV3Slim(Layer):
         self.plan.append((s, "cat", [b1, b3, b3d, bp]))
         return 320 + 768 + 768 + 192
 
+    # ---- merged branch heads ----------------------------------------------------------------------
+    @staticmethod
+    def _sibling_heads(branches):
+        """The branches' first convs that join the block's sibling group, in call order, as (weight, BatchNorm or
+        None): a 1x1 stride-1 conv+BN at the branch start, and the commuted pool branch's 1x1 conv (no BN on its
+        output: the BN follows the pool).  None when fewer than two."""
+        heads = []
+        for b in branches:
+            op = b[0]
+            if isinstance(op, Conv2d) and op.kh == 1 and op.kw == 1 and op.stride == 1 and op.bn is not None:
+                heads.append((op.weights, op.bn))
+            elif (op == "avg3" and len(b) > 1 and isinstance(b[1], Conv2d) and b[1].kh == 1 and b[1].kw == 1 and
+                  b[1].stride == 1 and b[1].bn is not None and _fused.pool_commute_enabled() and
+                  os.environ.get("DTM_SIBLING_POOL", "1") != "0"):
+                heads.append((b[1].weights, None))
+        return heads if len(heads) >= 2 else None
+
+    def sibling_weight_groups(self):
+        """Weight groups whose bf16 compute copies live side by side in one buffer (engine.prepare_compute_copies),
+        so a mixed block's merged head conv reads its concatenated weights without a copy."""
+        return [[w for w, _bn in h] for _n, kind, branches in self.plan if kind == "cat"
+                for h in [self._sibling_heads(branches)] if h]
+
     # ---- forward --------------------------------------------------------------------------------
     @staticmethod
     def _run(branch, x, training):
@@ -182,8 +207,9 @@ class InceptionV3Slim(Layer):
                     end_points["aux_logits"] = aux
                 continue
             # branch outputs written straight into their channel slices (zero-copy concat); the branches' first
-            # 1x1 conv+BNs on the block input share one backward (ops.fused.sibling_group)
-            with _fused.sibling_group(net, training):
+            # 1x1 conv+BNs on the block input share one forward (one conv + one finalize) and one backward
+            # (ops.fused.sibling_group)
+            with _fused.sibling_group(net, training, heads=self._sibling_heads(branches)):
                 parts = [p for b in branches for p in self._run(b, net, training)]
             net = concat_channels(parts)
             if end_points is not None:

@@ -188,6 +188,18 @@ class _ConvBNFn(torch.autograd.Function):
     def forward(ctx, x, in_ss, w, gamma, beta, geom, bn, slot=None, in_unscaled=False, x_mat=None, grp=None):
         L = _lib.lib()
         s = _lib.stream_ptr()
+        pre = grp[0].fwd.get(id(w)) if (grp is not None and grp[0].fwd is not None) else None
+        if pre is not None:
+            # computed by the group's merged forward (_SiblingGroup.forward_all): nothing to launch
+            ctx.geom, ctx.slot, ctx.grp, ctx.in_unscaled = geom, slot, grp, bool(in_unscaled)
+            ctx.mat = False
+            ctx.bnout = getattr(x, "_dtm_bnout", None)
+            ctx.has_gamma, ctx.has_beta = gamma is not None, beta is not None
+            y, ss = pre
+            if ss is not None:
+                ctx.count = float(geom.N * geom.P * geom.Q)
+            ctx.save_for_backward(x, in_ss, w, y, ss, gamma, beta, None)
+            return y if ss is None else (y, ss)
         w16 = weight_bf16(w)
         y = torch.empty((geom.N, geom.P, geom.Q, geom.K), device=x.device, dtype=torch.bfloat16)
         d = geom.as_desc(_lib.ConvDesc)
@@ -726,19 +738,74 @@ class _SiblingGroup:
     each member's dW (dtm_conv_wgrad_multi).  Instead of one dgrad per member - each re-reading and
     re-writing the whole block-input gradient through the _GradSlot hand-off - and one wgrad per member.
     The group is one consumer of the input's _GradSlot."""
-    __slots__ = ("x", "members", "ktot", "slot", "buf", "done", "bnout")
+    __slots__ = ("x", "members", "ktot", "slot", "buf", "done", "bnout", "pend", "heads", "fwd")
 
-    def __init__(self, x):
+    def __init__(self, x, heads=None):
         self.x, self.members, self.ktot, self.slot, self.buf, self.done = x, [], 0, None, None, 0
+        # heads: the members' (weight, BatchNorm or None) in call order, declared by the model: the first member's
+        # forward then runs ONE conv + ONE finalize for all of them (forward_all); fwd: weight -> (y, ss)
+        self.heads, self.fwd = heads, None
+        # deferred stats-combines (one grouped launch at the last member): (keep-alive tensors, 7 pointers, C, off,
+        # parameters to notify)
+        self.pend = []
         # x is a block output whose BN-apply backward the merged dgrad's epilogue can absorb (ResNet unit 1)
         self.bnout = getattr(x, "_dtm_bnout", None)
 
     def join(self, w, geom):
         if self.slot is None:
             self.slot = _slot_register(self.x)
+        if self.heads is not None and (len(self.members) >= len(self.heads) or
+                                       self.heads[len(self.members)][0] is not w):
+            raise RuntimeError("sibling group: member %d joined out of the declared head order" % len(self.members))
         self.members.append((w, geom.K, self.ktot))
         self.ktot += geom.K
         return (self, len(self.members) - 1)
+
+    def forward_all(self, geom, training):
+        """The declared heads' forward as ONE conv over their concatenated bf16 weights (the members' compute
+        copies are views of one buffer, engine.prepare_compute_copies) storing each member's own output, and ONE
+        BatchNorm finalize writing each BN member's ss and moving statistics (dtm_conv_fwd_bn_multi).  Returns
+        False (per-member launches instead) when the heads do not form such a group."""
+        heads = self.heads
+        if self.fwd is not None:
+            return True
+        cat = getattr(heads[0][0], "_sib_cat", None)
+        if cat is None or len(heads) > 8:
+            return False
+        buf, off = cat[0], 0
+        bns = [bn for _w, bn in heads if bn is not None]
+        for w, bn in heads:
+            c = getattr(w, "_sib_cat", None)
+            if c is None or c[0] is not buf or c[1] != off or w.shape[1:3] != (1, 1) or w.shape[0] % 8:
+                return False
+            if bn is not None and (bn.eps, bn.decay, bn.bessel) != (bns[0].eps, bns[0].decay, bns[0].bessel):
+                return False
+            off += w.shape[0]
+        if buf.shape[0] != off or geom.stride != 1 or geom.pad_h or geom.pad_w:
+            return False
+        L = _lib.lib()
+        x = self.x
+        N, H, W, C = x.shape
+        M = N * H * W
+        ys = [torch.empty((N, H, W, w.shape[0]), device=x.device, dtype=torch.bfloat16) for w, _bn in heads]
+        sss = [torch.empty((4, w.shape[0]), device=x.device, dtype=torch.float32) if bn is not None else None
+               for w, bn in heads]
+        ptrs = []
+        dp = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
+        for (w, bn), ss in zip(heads, sss):
+            ptrs += ([dp(bn.gamma), dp(bn.beta), dp(bn.moving_mean), dp(bn.moving_variance), dp(ss)]
+                     if bn is not None else [0, 0, 0, 0, 0])
+        d = _lib.ConvDesc(N, H, W, C, off, 1, 1, H, W, 1, 0, 0, 0, 0)
+        b0 = bns[0] if bns else None
+        _check(L.dtm_conv_fwd_bn_multi(_lib.ptr(x), _lib.ptr(buf), (ctypes.c_void_p * len(ys))(*[y.data_ptr() for y in ys]),
+                                       (ctypes.c_int * len(ys))(*[w.shape[0] for w, _bn in heads]), len(ys),
+                                       (ctypes.c_void_p * len(ptrs))(*ptrs), float(M),
+                                       float(b0.eps) if b0 else 1e-3, float(b0.decay) if b0 else 0.9, 1 if training else 0,
+                                       int(b0.bessel) if b0 else 0, ctypes.byref(d), _lib.stream_ptr()),
+               "conv_fwd_bn_multi(sibling heads)")
+        self.fwd = {id(w): (y, ss) for (w, _bn), y, ss in zip(heads, ys, sss)}
+        SIBLING_FWD_MERGED[0] += 1
+        return True
 
     @staticmethod
     def backward_member(ctx, dy, dss, x, w, y, ss, gamma, beta):
@@ -751,13 +818,28 @@ class _SiblingGroup:
             grp.buf = torch.empty((M, grp.ktot), device=dy.device, dtype=torch.bfloat16)
         off = grp.members[idx][2]
         dgamma = dbeta = None
-        if ss is None:
+        gmg = grad_target(gamma) if (ss is not None and gamma is not None) else None
+        bmg = grad_target(beta) if (ss is not None and beta is not None) else None
+        # every BN parameter gradient lands in main_grad: the members' combines are deferred to ONE grouped launch
+        # at the last member (dgamma / dbeta written there, then reported); otherwise per member, now
+        grouped = (os.environ.get("DTM_SIBLING_COMBINE", "1") != "0" and len(grp.members) <= 8 and g.K % 8 == 0 and
+                   (gamma is None or gmg is not None) and (beta is None or bmg is not None))
+        if grouped:
+            dyc = dy.contiguous()
+            dssc = dss.contiguous() if ss is not None else None
+            grp.pend.append(((dyc, dssc, y), [dyc.data_ptr(), y.data_ptr() if ss is not None else 0,
+                                              dssc.data_ptr() if ss is not None else 0,
+                                              ss.data_ptr() if ss is not None else 0,
+                                              gamma.data_ptr() if (ss is not None and gamma is not None) else 0,
+                                              gmg.data_ptr() if gmg is not None else 0,
+                                              bmg.data_ptr() if bmg is not None else 0],
+                             g.K, off, [p for p, m in ((gamma, gmg), (beta, bmg)) if m is not None],
+                             getattr(ctx, "count", None) if ss is not None else None))
+        elif ss is None:
             # a member without BatchNorm (Inception's commuted pool-branch conv: its gradient comes from the pool's
             # backward): a strided copy into its column slice
             grp.buf[:, off:off + g.K].copy_(dy.reshape(M, g.K))
         else:
-            gmg = grad_target(gamma) if gamma is not None else None
-            bmg = grad_target(beta) if beta is not None else None
             dgamma = torch.zeros(g.K, device=dy.device) if (gamma is not None and gmg is None) else None
             dbeta = torch.zeros(g.K, device=dy.device) if (beta is not None and bmg is None) else None
             _check(L.dtm_stats_combine_fin_ld(_lib.ptr(dy.contiguous()), _lib.ptr(y), _lib.ptr(dss.contiguous()),
@@ -772,6 +854,17 @@ class _SiblingGroup:
         grp.done += 1
         if grp.done < len(grp.members):
             return None, None, None, dgamma, dbeta, None, None, None, None, None, None
+        if grp.pend:
+            # (members' geometry is the shared input's: one pixel count; the count of a BN'd member is its N*P*Q)
+            cnt = next((c for *_r, c in grp.pend if c), float(M))
+            ptrs = (ctypes.c_void_p * (7 * len(grp.pend)))(*[q for _k, pp, *_r in grp.pend for q in pp])
+            dims = (ctypes.c_int * (2 * len(grp.pend)))(*[v for _k, _p, K_, off_, *_r in grp.pend for v in (K_, off_)])
+            _check(L.dtm_stats_combine_multi(ptrs, dims, len(grp.pend), float(cnt), _lib.ptr(grp.buf), M, grp.ktot, s),
+                   "stats_combine_multi(sibling)")
+            for _k, _p, _K, _off, params, _c in grp.pend:
+                for p in params:
+                    _notify(p)
+            grp.pend = []
         # the last member: one dgrad and one wgrad over every member's output gradient
         buf, n = grp.buf, len(grp.members)
         d = _lib.ConvDesc(g.N, g.H, g.W, g.C, grp.ktot, 1, 1, g.P, g.Q, 1, 0, 0, 0)
@@ -824,6 +917,7 @@ class _SiblingGroup:
 
 
 SIBLING_MERGED = [0]  # merged sibling backwards (tests / diagnostics)
+SIBLING_FWD_MERGED = [0]  # merged sibling forwards
 _SIBLINGS = [None]
 
 
@@ -835,11 +929,13 @@ class sibling_group:
     test_bsp_gpu_step1_gradients_match_single_rank); the round-3 2-rank mismatch no longer reproduces
     (profiles/r4/README.md)."""
 
-    def __init__(self, x, training=True):
+    def __init__(self, x, training=True, heads=None):
         import os
         on = (training and torch.is_grad_enabled() and isinstance(x, torch.Tensor) and x.is_cuda and
               x.requires_grad and os.environ.get("DTM_SIBLING_GROUP", "1") != "0")
-        self.grp = _SiblingGroup(x) if on else None
+        if heads is not None and (len(heads) < 2 or os.environ.get("DTM_SIBLING_FWD", "1") == "0"):
+            heads = None
+        self.grp = _SiblingGroup(x, heads) if on else None
 
     def __enter__(self):
         self.prev, _SIBLINGS[0] = _SIBLINGS[0], self.grp
@@ -861,7 +957,10 @@ def _sibling_join(xb, w, g, training, bn, plain=False):
         return None
     if g.K == 256 and g.C == 64 and os.environ.get("DTM_BWD1X1_FUSE", "1") != "0":
         return None  # (the ResNet stage-1 64 -> 256 projection keeps its one-pass backward, dtm_conv1x1_bnbwd)
-    return grp.join(w, g)
+    h = grp.join(w, g)
+    if grp.heads is not None and len(grp.members) == 1 and not grp.forward_all(g, training):
+        grp.heads = None  # (not a mergeable head set: per-member forwards)
+    return h
 
 
 def _prologue_mode(x_shape, w_shape, stride):

@@ -488,6 +488,78 @@ def test_sibling_1x1_merged_backward(monkeypatch, side, model, S, B, merged, las
     assert vals[len(vals) // 2] < 1.5e-2 and vals[-1] < 5e-2, sorted(((v, k) for k, v in errs.items()))[-5:]
 
 
+@pytest.mark.parametrize("model,S,B", [("inception_v3_slim_old", 299, 2), ("resnet_v1_50", 64, 4)])
+def test_sibling_grouped_stats_combine_bit_exact(monkeypatch, model, S, B):
+    """The merged sibling group's members' BN stats-combines as ONE grouped launch at the last member
+    (dtm_stats_combine_multi, the default) vs one launch per member: the same arithmetic per element, so every
+    parameter gradient is bit-identical under deterministic reductions (Inception: BN'd heads + the commuted
+    pool-branch conv copied into its slice)."""
+    from distributed_tensorflow_models_amd.engine import TrainStep
+    from distributed_tensorflow_models_amd.models import nets_factory
+    from distributed_tensorflow_models_amd.ops import _lib
+    from distributed_tensorflow_models_amd.ops import elementwise as ew
+    monkeypatch.setattr(ew, "advance_seed_offset", lambda device: None)
+    monkeypatch.setattr(ew, "next_seed", lambda: 1234)
+    monkeypatch.setenv("DTM_SIBLING_GROUP", "1")
+    _lib.lib().dtm_set_deterministic(1)
+    try:
+        torch.manual_seed(0)
+        net = nets_factory.build(model, num_classes=11).to(DEV)
+        step = TrainStep(net, optimizer="momentum", lr=0.0, momentum=0.9, wgrad_stream=False)
+        x = torch.randn(B, S, S, 3, device=DEV).to(torch.bfloat16)
+        y = torch.randint(0, 11, (B,), device=DEV)
+        grads = {}
+        for comb in ("1", "0"):
+            monkeypatch.setenv("DTM_SIBLING_COMBINE", comb)
+            step._forward_backward(x, y)
+            torch.cuda.synchronize()
+            grads[comb] = {k: p.main_grad.detach().clone() for k, p in net.named_parameters()
+                           if getattr(p, "main_grad", None) is not None}
+        bad = [k for k in grads["0"] if not torch.equal(grads["1"][k], grads["0"][k])]
+        assert not bad, bad[:5]
+    finally:
+        _lib.lib().dtm_set_deterministic(0)
+
+
+def test_sibling_merged_head_forward(monkeypatch):
+    """Inception-v3 mixed blocks: the branch-head 1x1 conv+BNs (and the commuted pool-branch conv) as ONE conv over
+    their concatenated bf16 weights (one buffer, engine.prepare_compute_copies) writing each member's own output,
+    plus ONE finalize (dtm_conv_fwd_bn_multi), vs one conv + finalize per head: same logits / loss, moving
+    statistics and per-parameter gradients up to the BatchNorm-statistics summation order."""
+    from distributed_tensorflow_models_amd.engine import TrainStep, moving_average_buffers
+    from distributed_tensorflow_models_amd.models import nets_factory
+    from distributed_tensorflow_models_amd.ops import elementwise as ew
+    monkeypatch.setattr(ew, "advance_seed_offset", lambda device: None)
+    monkeypatch.setattr(ew, "next_seed", lambda: 1234)
+    torch.manual_seed(0)
+    net = nets_factory.build("inception_v3_slim_old", num_classes=11).to(DEV)
+    step = TrainStep(net, optimizer="rmsprop", lr=0.0, rho=0.9, epsilon=1.0, label_smoothing=0.1, aux_weight=0.4,
+                     wgrad_stream=False)
+    assert any(getattr(p, "_sib_cat", None) is not None for p in net.parameters())
+    x = torch.randn(2, 299, 299, 3, device=DEV).to(torch.bfloat16)
+    y = torch.randint(0, 11, (2,), device=DEV)
+    init = [b.detach().clone() for b in moving_average_buffers(net)]
+    out = {}
+    for fwd in ("0", "1"):
+        monkeypatch.setenv("DTM_SIBLING_FWD", fwd)
+        with torch.no_grad():
+            for b, v in zip(moving_average_buffers(net), init):
+                b.copy_(v)
+        n0 = fused.SIBLING_FWD_MERGED[0]
+        loss, _skip = step._forward_backward(x, y)
+        torch.cuda.synchronize()
+        merged = fused.SIBLING_FWD_MERGED[0] - n0
+        assert merged == (10 if fwd == "1" else 0), merged  # 3 x 35x35 + 4 x 17x17 + 1280 + 2 x 8x8 blocks
+        out[fwd] = (float(loss), [b.detach().clone() for b in moving_average_buffers(net)],
+                    {k: p.main_grad.detach().float().clone() for k, p in net.named_parameters()
+                     if getattr(p, "main_grad", None) is not None})
+    assert abs(out["1"][0] - out["0"][0]) < 1e-3 * abs(out["0"][0])
+    for a, b in zip(out["1"][1], out["0"][1]):
+        assert _rel(a, b) < 1e-4
+    errs = sorted((_rel(out["1"][2][k], out["0"][2][k]), k) for k in out["0"][2])
+    assert errs[len(errs) // 2][0] < 1e-3 and errs[-1][0] < 2e-2, errs[-5:]
+
+
 def test_act_input_handoff_between_conv_consumers(monkeypatch):
     """An activation (LazyBN) read by two convs (Inception's split 1x3 / 3x1 pair): the first conv's backward
     hands its masked input gradient to the second, whose act epilogue adds it before the mask and the
