@@ -11,6 +11,8 @@ vgg/nets/resnet_utils.py:59-272:
 Variables: resnet_v1_50/conv1/weights, resnet_v1_50/conv1/BatchNorm/{gamma,beta,moving_*},
 resnet_v1_50/block1/unit_1/bottleneck_v1/{shortcut,conv1,conv2,conv3}/..., resnet_v1_50/logits/{weights,biases}.
 """
+import os
+
 import torch
 
 from ..ops import nn as F
@@ -64,10 +66,19 @@ class BottleneckV1(Layer):
                             conv2d_same_padding(3, stride, rate), "relu", bn, None, wd, init, rate=rate)
         self.conv3 = Conv2d(_join(scope, "conv3"), depth_bottleneck, depth, 1, 1, "SAME", None, bn, None, wd, init)
 
+    def sibling_heads(self):
+        """(weight, BatchNorm) of the projection shortcut and conv1 when they form a mergeable sibling pair (both 1x1
+        stride-1 conv+BNs of x; not the stage-1 64 -> 256 projection, which keeps its one-pass backward)."""
+        s = self.shortcut
+        if (s is None or s.stride != 1 or s.bn is None or self.conv1.bn is None or
+                (s.cout == 256 and s.cin == 64 and os.environ.get("DTM_BWD1X1_FUSE", "1") != "0")):
+            return None
+        return [(s.weights, s.bn), (self.conv1.weights, self.conv1.bn)]
+
     def forward(self, x, training=True, end_points=None):
         if self.shortcut is not None:
-            # projection shortcut and conv1: sibling 1x1 conv+BNs of x with one merged backward (ops.fused)
-            with fused.sibling_group(x, training and end_points is None):
+            # projection shortcut and conv1: sibling 1x1 conv+BNs of x with one merged forward and backward (ops.fused)
+            with fused.sibling_group(x, training and end_points is None, heads=self.sibling_heads()):
                 sc = self.shortcut(x, training)
                 r1 = self.conv1(x, training)
         else:
@@ -139,6 +150,11 @@ BLOCKS = {
 
 
 class ResNetV1(Layer):
+    def sibling_weight_groups(self):
+        """Projection units' shortcut + conv1 weights: bf16 compute copies side by side in one buffer
+        (engine.prepare_compute_copies) for the merged forward."""
+        return [[w for w, _bn in h] for u in self.units for h in [u.sibling_heads()] if h]
+
     default_image_size = 224
 
     def __init__(self, depth=50, num_classes=1000, global_pool=True, spatial_squeeze=True, scope=None,

@@ -521,9 +521,10 @@ def test_sibling_grouped_stats_combine_bit_exact(monkeypatch, model, S, B):
         _lib.lib().dtm_set_deterministic(0)
 
 
-def test_sibling_merged_head_forward(monkeypatch):
-    """Inception-v3 mixed blocks: the branch-head 1x1 conv+BNs (and the commuted pool-branch conv) as ONE conv over
-    their concatenated bf16 weights (one buffer, engine.prepare_compute_copies) writing each member's own output,
+@pytest.mark.parametrize("model,S,B,nmerged", [("inception_v3_slim_old", 299, 2, 10), ("resnet_v1_50", 64, 4, 3)])
+def test_sibling_merged_head_forward(monkeypatch, model, S, B, nmerged):
+    """Inception-v3 mixed blocks' branch-head 1x1 conv+BNs (and the commuted pool-branch conv), ResNet-50 projection
+    units' shortcut + conv1, as ONE conv over their concatenated bf16 weights (one buffer, engine.prepare_compute_copies) writing each member's own output,
     plus ONE finalize (dtm_conv_fwd_bn_multi), vs one conv + finalize per head: same logits / loss, moving
     statistics and per-parameter gradients up to the BatchNorm-statistics summation order."""
     from distributed_tensorflow_models_amd.engine import TrainStep, moving_average_buffers
@@ -532,12 +533,11 @@ def test_sibling_merged_head_forward(monkeypatch):
     monkeypatch.setattr(ew, "advance_seed_offset", lambda device: None)
     monkeypatch.setattr(ew, "next_seed", lambda: 1234)
     torch.manual_seed(0)
-    net = nets_factory.build("inception_v3_slim_old", num_classes=11).to(DEV)
-    step = TrainStep(net, optimizer="rmsprop", lr=0.0, rho=0.9, epsilon=1.0, label_smoothing=0.1, aux_weight=0.4,
-                     wgrad_stream=False)
+    net = nets_factory.build(model, num_classes=11).to(DEV)
+    step = TrainStep(net, optimizer="momentum", lr=0.0, momentum=0.9, wgrad_stream=False)
     assert any(getattr(p, "_sib_cat", None) is not None for p in net.parameters())
-    x = torch.randn(2, 299, 299, 3, device=DEV).to(torch.bfloat16)
-    y = torch.randint(0, 11, (2,), device=DEV)
+    x = torch.randn(B, S, S, 3, device=DEV).to(torch.bfloat16)
+    y = torch.randint(0, 11, (B,), device=DEV)
     init = [b.detach().clone() for b in moving_average_buffers(net)]
     out = {}
     for fwd in ("0", "1"):
@@ -549,7 +549,8 @@ def test_sibling_merged_head_forward(monkeypatch):
         loss, _skip = step._forward_backward(x, y)
         torch.cuda.synchronize()
         merged = fused.SIBLING_FWD_MERGED[0] - n0
-        assert merged == (10 if fwd == "1" else 0), merged  # 3 x 35x35 + 4 x 17x17 + 1280 + 2 x 8x8 blocks
+        # Inception: 3 x 35x35 + 4 x 17x17 + 1280 + 2 x 8x8 blocks; ResNet-50: the projection units of stages 2-4
+        assert merged == (nmerged if fwd == "1" else 0), merged
         out[fwd] = (float(loss), [b.detach().clone() for b in moving_average_buffers(net)],
                     {k: p.main_grad.detach().float().clone() for k, p in net.named_parameters()
                      if getattr(p, "main_grad", None) is not None})
