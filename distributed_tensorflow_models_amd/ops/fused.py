@@ -887,8 +887,10 @@ class _SiblingGroup:
                 wgrad(_lib.stream_ptr(), _lib.side_cus())
         else:
             wgrad(s, _lib.wgrad_cus())
-        wts = [weight_flipped(m[0], m[1], 1, 1, g.C) for m in grp.members]
-        wt = wts[0] if n == 1 else torch.cat([t.view(g.C, m[1]) for t, m in zip(wts, grp.members)], dim=1)
+        wt = _group_flipped(grp, g.C)
+        if wt is None:
+            wts = [weight_flipped(m[0], m[1], 1, 1, g.C) for m in grp.members]
+            wt = wts[0] if n == 1 else torch.cat([t.view(g.C, m[1]) for t, m in zip(wts, grp.members)], dim=1)
         last, add_src, add_stride = _slot_take(grp.slot)
         use_add = add_src is not None
         dx = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
@@ -914,6 +916,32 @@ class _SiblingGroup:
         # member weights whose gradient has no main_grad: hand the fresh tensors back through this member only
         dw = None if mgs[idx] is not None else dws[idx]
         return dx, None, dw, dgamma, dbeta, None, None, None, None, None, None
+
+
+_CAT_PARAMS = {}  # id(concatenated bf16 weight buffer) -> a bf16 pseudo-parameter over it (its flipped-copy owner)
+
+
+def _group_flipped(grp, C):
+    """The merged dgrad's [C][sum K] weight when the members' bf16 copies are consecutive rows of one buffer
+    (engine.prepare_compute_copies): the flipped (for a 1x1: transposed) copy of that buffer as ONE weight, cached
+    and refreshed by the optimizer like every dgrad copy (ops.nn.refresh_flipped) - no per-step concatenation."""
+    ms = grp.members
+    cat = getattr(ms[0][0], "_sib_cat", None)
+    if len(ms) < 2 or cat is None or cat[1] != 0:
+        return None
+    buf = cat[0]
+    for w, K, off in ms:
+        c = getattr(w, "_sib_cat", None)
+        if c is None or c[0] is not buf or c[1] != off:
+            return None
+    if buf.shape[0] != grp.ktot:
+        return None
+    cp = _CAT_PARAMS.get(id(buf))
+    if cp is None or cp.data_ptr() != buf.data_ptr():
+        cp = torch.nn.Parameter(buf, requires_grad=False)
+        cp.bf16 = buf
+        _CAT_PARAMS[id(buf)] = cp
+    return weight_flipped(cp, grp.ktot, 1, 1, C)
 
 
 SIBLING_MERGED = [0]  # merged sibling backwards (tests / diagnostics)
