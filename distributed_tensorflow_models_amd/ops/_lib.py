@@ -121,6 +121,7 @@ _SIGS = {
     "dtm_set_reduce_few": (None, [_I]),
     "dtm_set_reserved_cus": (None, [_I]),
     "dtm_stats_combine_multi": (_I, [_P, _P, _I, _F, _P, _L, _I, _P]),
+    "dtm_conv_fwd_bn_multi": (_I, [_P, _P, _P, _P, _I, _P, _F, _F, _F, _I, _I, ctypes.POINTER(ConvDesc), _P]),
     "dtm_conv_set_dec_lpt": (None, [_I]),
     "dtm_get_reserved_cus": (_I, []),
     "dtm_compute_cus_api": (_I, []),

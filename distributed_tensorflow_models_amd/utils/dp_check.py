@@ -79,3 +79,24 @@ def compare(multi, single, step=0):
         rel = float(d.norm() / max(float(b.double().norm()), 1e-30))
         rows.append((na, rel, float(d.abs().max()) if d.numel() else 0.0))
     return rows
+
+
+def grad_worker_multi(rank, world, configs, bucket_mb=2.0, overlap=True, steps=1):
+    """grad_worker over several (model, knobs) configs in ONE process (process start-up and the gloo rendezvous
+    dominate a config's cost): each config's knobs are set for its run and restored after; the side-stream switch,
+    cached process-wide, is set explicitly."""
+    from ..ops import _lib
+    outs = []
+    for model_name, knobs in configs:
+        saved = {k: os.environ.get(k) for k in knobs}
+        try:
+            _lib.set_side_enabled(knobs.get("DTM_WGRAD_STREAM", "1") == "1")
+            outs.append(grad_worker(rank, world, model_name, knobs, bucket_mb, overlap, steps))
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+            torch.cuda.empty_cache()
+    return outs
