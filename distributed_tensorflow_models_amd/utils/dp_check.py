@@ -30,9 +30,10 @@ CONFIGS = {
 }
 
 
-def grad_worker(rank, world, model_name, knobs=None, bucket_mb=2.0, overlap=True, steps=1):
+def grad_worker(rank, world, model_name, knobs=None, bucket_mb=2.0, overlap=True, steps=1, group=None):
     """One rank (world 1 = the reference run).  knobs: environment overrides (DTM_* gradient-routing knobs),
-    set before any kernel call of this fresh process."""
+    set before any kernel call of this fresh process.  group: the process group of the data-parallel run (a
+    singleton group gives the single-rank reference inside a multi-rank job); gradients are divided by its size."""
     os.environ.update({k: str(v) for k, v in (knobs or {}).items()})
     os.environ["DTM_DETERMINISTIC"] = "1"
     os.environ.setdefault("DTM_BSP_CHECK", "1")
@@ -46,7 +47,8 @@ def grad_worker(rank, world, model_name, knobs=None, bucket_mb=2.0, overlap=True
     ew.set_base_seed(0, 0)  # the same dropout masks on every rank (the batch is the same too)
     kw, S, B, okw = CONFIGS[model_name]
     model = nets_factory.build(model_name, **kw).to(dev)
-    step = TrainStep(model, bucket_mb=bucket_mb, overlap=overlap, **okw)
+    step = TrainStep(model, bucket_mb=bucket_mb, overlap=overlap, process_group=group, **okw)
+    world = step.dp.world
     g = torch.Generator().manual_seed(7)
     x = torch.randn(B, S, S, 3, generator=g).to(dev, torch.bfloat16)
     y = torch.randint(0, kw["num_classes"], (B,), generator=g).to(dev)
@@ -81,22 +83,14 @@ def compare(multi, single, step=0):
     return rows
 
 
-def grad_worker_multi(rank, world, configs, bucket_mb=2.0, overlap=True, steps=1):
-    """grad_worker over several (model, knobs) configs in ONE process (process start-up and the gloo rendezvous
-    dominate a config's cost): each config's knobs are set for its run and restored after; the side-stream switch,
-    cached process-wide, is set explicitly."""
-    from ..ops import _lib
-    outs = []
-    for model_name, knobs in configs:
-        saved = {k: os.environ.get(k) for k in knobs}
-        try:
-            _lib.set_side_enabled(knobs.get("DTM_WGRAD_STREAM", "1") == "1")
-            outs.append(grad_worker(rank, world, model_name, knobs, bucket_mb, overlap, steps))
-        finally:
-            for k, v in saved.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
-            torch.cuda.empty_cache()
-    return outs
+
+def grad_worker_pair(rank, world, model_name, knobs=None, bucket_mb=2.0, overlap=True, steps=1):
+    """The single-rank reference AND the world-rank run in ONE multi-rank job (process start-up and the rendezvous
+    dominate the cost of a config): each rank first runs the model alone in a singleton process group (no
+    collective: the reference), then in the full group.  Returns {"single": ..., "multi": ...}."""
+    import torch.distributed as dist
+    singles = [dist.new_group([r]) for r in range(world)]  # (every rank creates every group, in one order)
+    single = grad_worker(rank, world, model_name, knobs, bucket_mb, overlap, steps, group=singles[rank])
+    torch.cuda.empty_cache()
+    multi = grad_worker(rank, world, model_name, knobs, bucket_mb, overlap, steps)
+    return {"single": single, "multi": multi}

@@ -184,23 +184,26 @@ _DP_MATRIX = [
 ]
 
 
+# the driver's GPU suite runs the default configs; DTM_DP_MATRIX=1 runs every knob combination
+_DP_RUN = _DP_MATRIX if os.environ.get("DTM_DP_MATRIX") == "1" else [c for c in _DP_MATRIX if not c[1]]
+
+
 @pytest.mark.gpu
-def test_bsp_gpu_step1_gradients_match_single_rank():
-    """The whole matrix in one 1-rank and one 2-rank run (workers loop over the configs)."""
+@pytest.mark.parametrize("model,knobs", _DP_RUN, ids=lambda v: v if isinstance(v, str) else
+                         ("-".join("%s%s" % (k[4:].lower(), x) for k, x in v.items()) or "defaults"))
+def test_bsp_gpu_step1_gradients_match_single_rank(model, knobs):
+    """Per-parameter step-1 gradients of 2 ranks (the same batch) vs the single-rank run (computed inside the same
+    2-rank job in a singleton group), deterministic reductions, BSP write checker on."""
     from distributed_tensorflow_models_amd.utils import dp_check
-    single = run_workers(dp_check.grad_worker_multi, 1, _DP_MATRIX)[0]
-    two = run_workers(dp_check.grad_worker_multi, 2, _DP_MATRIX)
-    fails = []
-    for i, (model, knobs) in enumerate(_DP_MATRIX):
-        t0, t1, s = two[0][i], two[1][i], single[i]
-        assert t0["launched"] == t0["buckets"] > 1 and t0["writes_checked"] > 0, (model, knobs)
-        if model == "vgg_16":
-            assert t0["compact"] == 1  # fc6's live window travels alone
-        rows = dp_check.compare(t0, s)
-        bad = [r for r in rows if r[1] > 1e-5]
-        if bad or not torch.equal(t0["params"], t1["params"]):
-            fails.append((model, knobs, len(bad), len(rows), bad[:4]))
-    assert not fails, fails
+    res = run_workers(dp_check.grad_worker_pair, 2, model, knobs)
+    single, two = res[0]["single"], [r["multi"] for r in res]
+    assert two[0]["launched"] == two[0]["buckets"] > 1 and two[0]["writes_checked"] > 0
+    if model == "vgg_16":
+        assert two[0]["compact"] == 1  # fc6's live window travels alone
+    rows = dp_check.compare(two[0], single)
+    bad = [r for r in rows if r[1] > 1e-5]
+    assert not bad, (len(bad), len(rows), bad[:6])
+    assert torch.equal(two[0]["params"], two[1]["params"])
 
 
 # The round-3 sibling-merge data-parallel mismatch, reduced to its mechanism (profiles/r4/README.md): a fused op

@@ -464,6 +464,7 @@ def test_sibling_1x1_merged_backward(monkeypatch, side, model, S, B, merged, las
     y = torch.randint(0, 11, (B,), device=DEV)
     grads = {}
     try:
+        monkeypatch.setenv("DTM_SIBLING_FWD", "0")  # (the merged forward has its own test)
         for grp in ("0", "1"):
             monkeypatch.setenv("DTM_SIBLING_GROUP", grp)
             n0 = fused.SIBLING_MERGED[0]
@@ -554,10 +555,12 @@ def test_sibling_merged_head_forward(monkeypatch, model, S, B, nmerged):
         out[fwd] = (float(loss), [b.detach().clone() for b in moving_average_buffers(net)],
                     {k: p.main_grad.detach().float().clone() for k, p in net.named_parameters()
                      if getattr(p, "main_grad", None) is not None})
-    assert abs(out["1"][0] - out["0"][0]) < 1e-3 * abs(out["0"][0])
-    for a, b in zip(out["1"][1], out["0"][1]):
-        assert _rel(a, b) < 1e-4
     errs = sorted((_rel(out["1"][2][k], out["0"][2][k]), k) for k in out["0"][2])
+    mv = max(_rel(a, b) for a, b in zip(out["1"][1], out["0"][1]))
+    # the logits weights' gradient is the pooled features times dL/dlogits: any forward difference shows there
+    logit = max(v for v, k in errs if "logits" in k and "aux" not in k)
+    assert abs(out["1"][0] - out["0"][0]) < 1e-3 * abs(out["0"][0]), (out["1"][0], out["0"][0])
+    assert mv < 1e-3 and logit < 1e-3, (mv, logit, errs[-5:])
     assert errs[len(errs) // 2][0] < 1e-3 and errs[-1][0] < 2e-2, errs[-5:]
 
 

@@ -313,6 +313,64 @@ def test_conv_bnout_dgrad(case):
         assert _rel(sums[5], gref.sum((0, 1, 2))) < 1e-2
 
 
+@pytest.mark.parametrize("case", [(2, 8, 1280, [320, 384, 448, 192]), (128, 8, 2048, [320, 384, 448, 192]),
+                                  (3, 35, 288, [64, 48, 64, 32]), (8, 17, 768, [192, 128, 128, 192]),
+                                  (4, 14, 256, [512, 128]), (2, 17, 768, [192, 192])])
+def test_conv_fwd_bn_multi_matches_separate(case):
+    """Merged sibling forward (dtm_conv_fwd_bn_multi): one 1x1 conv over the members' concatenated weights writing
+    each member's own output + one grouped finalize, vs one dtm_conv_fwd_bn per member: outputs, ss and moving
+    statistics (the last member without BatchNorm: its ss untouched)."""
+    import ctypes
+
+    from distributed_tensorflow_models_amd.ops import _lib
+    N, H, C, ks = case
+    torch.manual_seed(0)
+    L = _lib.lib()
+    st = _lib.stream_ptr()
+    x = torch.randn(N, H, H, C, device=DEV).to(torch.bfloat16)
+    ws = [(torch.randn(k, 1, 1, C, device=DEV) / C ** 0.5).to(torch.bfloat16) for k in ks]
+    wcat = torch.cat(ws).contiguous()
+    nbn = len(ks) - 1  # the last member has no BatchNorm
+    beta = [torch.randn(k, device=DEV) for k in ks]
+    mm = [torch.randn(k, device=DEV) * 0.1 for k in ks]
+    mv = [torch.rand(k, device=DEV) + 0.5 for k in ks]
+    M = N * H * H
+    ref_y, ref_ss, ref_mm, ref_mv = [], [], [], []
+    for i, (w, k) in enumerate(zip(ws, ks)):
+        d = _lib.ConvDesc(N, H, H, C, k, 1, 1, H, H, 1, 0, 0, 0, 0)
+        y = torch.empty(N, H, H, k, device=DEV, dtype=torch.bfloat16)
+        m2, v2 = mm[i].clone(), mv[i].clone()
+        ss = torch.zeros(4, k, device=DEV)
+        if i < nbn:
+            assert L.dtm_conv_fwd_bn(_lib.ptr(x), _lib.ptr(w), _lib.ptr(y), None, None, None, _lib.ptr(beta[i]),
+                                     _lib.ptr(m2), _lib.ptr(v2), _lib.ptr(ss), float(M), 1e-3, 0.9997, 1, 0,
+                                     ctypes.byref(d), st) == 0
+        else:
+            assert L.dtm_conv_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(y), None, None, None, None, 0, ctypes.byref(d),
+                                  st) == 0
+        ref_y.append(y); ref_ss.append(ss); ref_mm.append(m2); ref_mv.append(v2)
+    ys = [torch.empty(N, H, H, k, device=DEV, dtype=torch.bfloat16) for k in ks]
+    sss = [torch.zeros(4, k, device=DEV) for k in ks]
+    m3, v3 = [t.clone() for t in mm], [t.clone() for t in mv]
+    ptrs = []
+    for i in range(len(ks)):
+        ptrs += ([0, beta[i].data_ptr(), m3[i].data_ptr(), v3[i].data_ptr(), sss[i].data_ptr()] if i < nbn
+                 else [0, 0, 0, 0, 0])
+    d = _lib.ConvDesc(N, H, H, C, sum(ks), 1, 1, H, H, 1, 0, 0, 0, 0)
+    rc = L.dtm_conv_fwd_bn_multi(_lib.ptr(x), _lib.ptr(wcat), (ctypes.c_void_p * len(ys))(*[y.data_ptr() for y in ys]),
+                                 (ctypes.c_int * len(ks))(*ks), len(ks), (ctypes.c_void_p * len(ptrs))(*ptrs),
+                                 float(M), 1e-3, 0.9997, 1, 0, ctypes.byref(d), st)
+    assert rc == 0
+    torch.cuda.synchronize()
+    for i in range(len(ks)):
+        assert torch.equal(ys[i], ref_y[i]), (i, _rel(ys[i], ref_y[i]))
+        if i < nbn:
+            assert _rel(sss[i], ref_ss[i]) < 1e-5, (i, _rel(sss[i], ref_ss[i]))
+            assert _rel(m3[i], ref_mm[i]) < 1e-5 and _rel(v3[i], ref_mv[i]) < 1e-5
+        else:
+            assert not sss[i].any()
+
+
 @pytest.mark.parametrize("tile", [0, 1, 6, 10, 12])
 @pytest.mark.parametrize("case", [(4, 15, 15, 64, 96, 3, 2), (2, 14, 14, 128, 256, 3, 1), (3, 7, 7, 512, 200, 1, 1),
                                   (2, 9, 9, 24, 40, 3, 1), (5, 8, 8, 64, 64, 1, 1), (4, 9, 9, 256, 512, 3, 1),
