@@ -44,7 +44,8 @@ def grad_worker(rank, world, model_name, knobs=None, bucket_mb=2.0, overlap=True
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     torch.manual_seed(0)
-    ew.set_base_seed(0, 0)  # the same dropout masks on every rank (the batch is the same too)
+    ew.set_base_seed(0, 0)  # the same dropout masks on every rank (the batch is the same too) ...
+    ew.seed_offset(dev).zero_()  # ... and in every run of this process (the per-step offset is process state)
     kw, S, B, okw = CONFIGS[model_name]
     model = nets_factory.build(model_name, **kw).to(dev)
     step = TrainStep(model, bucket_mb=bucket_mb, overlap=overlap, process_group=group, **okw)

@@ -558,7 +558,7 @@ def test_sibling_merged_head_forward(monkeypatch, model, S, B, nmerged):
     errs = sorted((_rel(out["1"][2][k], out["0"][2][k]), k) for k in out["0"][2])
     mv = max(_rel(a, b) for a, b in zip(out["1"][1], out["0"][1]))
     # the logits weights' gradient is the pooled features times dL/dlogits: any forward difference shows there
-    logit = max(v for v, k in errs if "logits" in k and "aux" not in k)
+    logit = max(v for v, k in errs if (k.startswith("fc.") or "logits" in k) and "aux" not in k)
     assert abs(out["1"][0] - out["0"][0]) < 1e-3 * abs(out["0"][0]), (out["1"][0], out["0"][0])
     assert mv < 1e-3 and logit < 1e-3, (mv, logit, errs[-5:])
     assert errs[len(errs) // 2][0] < 1e-3 and errs[-1][0] < 2e-2, errs[-5:]
