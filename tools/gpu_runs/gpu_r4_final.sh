@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round-4 final evidence: GPU suite, smoke, benches (every BASELINE config), 8-rank gloo rehearsal of the driver's
+# launch (ranks sharing the GPU), ResNet-50 kernel trace (per-kernel stats + two-stream step timeline).
+set -o pipefail
+mkdir -p gpurun_out/r4
+export TMPDIR=/tmp
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 450 --timeout-method thread > gpurun_out/r4/r4_final_pytest_gpu.log 2>&1
+rc=$?; echo "gpu suite rc=$rc"; grep -E "FAILED|ERROR" gpurun_out/r4/r4_final_pytest_gpu.log | head -10; tail -1 gpurun_out/r4/r4_final_pytest_gpu.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4/r4_final_smoke.log 2>&1 || { tail -20 gpurun_out/r4/r4_final_smoke.log; exit 1; }
+tail -1 gpurun_out/r4/r4_final_smoke.log
+for m in resnet_v1_50 inception_v3_slim_old vgg_16 lenet; do
+  timeout -k 10 300 python bench.py --model $m > gpurun_out/r4/r4_final_bench_$m.log 2>&1 || { tail -20 gpurun_out/r4/r4_final_bench_$m.log; exit 1; }
+  tail -1 gpurun_out/r4/r4_final_bench_$m.log | cut -c1-220
+done
