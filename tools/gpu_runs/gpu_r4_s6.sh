@@ -4,6 +4,8 @@
 set -o pipefail
 mkdir -p gpurun_out/r4
 export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -v --timeout 200 --timeout-method thread tests/test_fused_ops_gpu.py -k "merged_head_forward" > gpurun_out/r4/pytest_mergedfwd.log 2>&1
+echo "merged fwd tests rc=$?"; grep -E "PASS|FAIL|^E  " gpurun_out/r4/pytest_mergedfwd.log | cut -c1-400 | tail -6
 rm -rf gpurun_out/r4/prof_inc
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r4/prof_inc -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --model inception_v3_slim_old --graph 0 --steps 3 --warmup 2 > $GRAFT_REPO_ROOT/gpurun_out/r4/prof_inc.log 2>&1 || { echo "prof failed"; tail -30 $GRAFT_REPO_ROOT/gpurun_out/r4/prof_inc.log; exit 1; }
 cd $GRAFT_REPO_ROOT
