@@ -188,7 +188,9 @@ class _ConvBNFn(torch.autograd.Function):
     def forward(ctx, x, in_ss, w, gamma, beta, geom, bn, slot=None, in_unscaled=False, x_mat=None, grp=None):
         L = _lib.lib()
         s = _lib.stream_ptr()
-        pre = grp[0].fwd.get(id(w)) if (grp is not None and grp[0].fwd is not None) else None
+        # (popped: the group must not keep the members' outputs - ctx -> group -> output -> grad_fn -> ctx would be
+        # a reference cycle through C++ autograd nodes that the garbage collector cannot break: a per-step leak)
+        pre = grp[0].fwd.pop(id(w), None) if (grp is not None and grp[0].fwd is not None) else None
         if pre is not None:
             # computed by the group's merged forward (_SiblingGroup.forward_all): nothing to launch
             ctx.geom, ctx.slot, ctx.grp, ctx.in_unscaled = geom, slot, grp, bool(in_unscaled)

@@ -259,6 +259,11 @@ def test_hipgraph_replay_after_larger_eager_step_matches_eager():
     big = TrainStep(other, optimizer="momentum", lr=0.01, momentum=0.9)
     big(torch.randn(32, 256, 256, 3, device=dev).to(torch.bfloat16), torch.randint(0, 1000, (32,), device=dev))
     torch.cuda.synchronize()
+    if int(_lib.lib().dtm_ws_retired()) == r0:
+        # (earlier tests of this process already grew the arenas past the big step's needs: force a growth of the
+        # main-stream arena the captured graph points into)
+        cap = int(_lib.lib().dtm_ws_capacity(_lib.stream_ptr()))
+        assert _lib.lib().dtm_ws_reserve_stream(cap + 1, _lib.stream_ptr()) == 0
     assert int(_lib.lib().dtm_ws_retired()) > r0
     big.dp.close()
     del big, other
