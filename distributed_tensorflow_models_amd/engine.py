@@ -61,6 +61,10 @@ def reserved_cus_default():
     return RESERVED_CUS_DP
 
 
+# Measured on one MI355X with a CU-occupying copy kernel on a second stream for 8 ms of every backward standing in
+# for the RCCL channels (profiles/ab/r4_ab_hog_reserve.log, ResNet-50): 16 CUs taken +2.4 % step, 32 CUs +3.5 %;
+# reserving the same CUs from the compute grids' sizing made both worse (+3.3 %, +4.8 %; +0.8 % with no
+# contention): the non-persistent tiles rebalance by themselves, so nothing is reserved by default.
 RESERVED_CUS_DP = 0
 
 

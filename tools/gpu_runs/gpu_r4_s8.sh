@@ -12,3 +12,5 @@ python3 tools/pmc_summary.py $(find gpurun_out/r4/pmc1 -name "*counter_collectio
 python3 tools/pmc_summary.py $(find gpurun_out/r4/pmc2 -name "*counter_collection.csv" | head -1) > gpurun_out/r4/pmc2_summary.txt 2>&1
 head -60 gpurun_out/r4/pmc1_summary.txt
 rm -rf gpurun_out/r4/pmc1 gpurun_out/r4/pmc2
+timeout -k 10 300 python -u tools/aten_sites.py --model inception_v3_slim_old --dispatch > gpurun_out/r4/aten_sites_inception.txt 2>&1 || { tail -20 gpurun_out/r4/aten_sites_inception.txt; exit 1; }
+head -40 gpurun_out/r4/aten_sites_inception.txt | cut -c1-200
