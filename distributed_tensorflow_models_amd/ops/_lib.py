@@ -183,22 +183,34 @@ def stream_ptr():
 # stream after it has waited for the main one (parallel/bsp.py), and the engine joins the side stream
 # before the optimizer (side_join).  DTM_WGRAD_STREAM=0/1 (default 1) or set_side_enabled().  Measured
 # (profiles/ab/r3_ab_wgrad_side_stream.log): ResNet-50 b256 step 18.02 -> 17.26 ms (-4.3 %).
-_side = {"stream": None, "on": None, "used": False}
+_side = {"stream": None, "on": None, "used": False, "capture": False}
 
 
 def set_side_enabled(on):
     _side["on"] = bool(on)
 
 
-def side_stream():
-    """The weight-gradient side stream, or None when off / not on a GPU."""
+def side_enabled():
     if _side["on"] is None:
         _side["on"] = os.environ.get("DTM_WGRAD_STREAM", "1") == "1"
-    if not _side["on"] or not torch.cuda.is_available():
+    return _side["on"]
+
+
+def set_side_capture(on):
+    """Allow the side stream inside a hipGraph capture (engine.TrainStep graph_side_stream): the fork / join
+    become graph edges, so the captured weight gradients run beside the dgrad chain on replay.  The stream and
+    its scratch arena must already exist from eager steps (growth inside a capture is refused)."""
+    _side["capture"] = bool(on)
+
+
+def side_stream():
+    """The weight-gradient side stream, or None when off / not on a GPU."""
+    if not side_enabled() or not torch.cuda.is_available():
         return None
-    if torch.cuda.is_current_stream_capturing():
-        # hipGraph capture stays single-stream: a captured fork onto this stream faulted on replay (illegal
-        # address, Inception-v3; profiles/ab/README.md round 3), so captured steps never use it
+    if torch.cuda.is_current_stream_capturing() and not _side["capture"]:
+        # captures are single-stream unless the engine opted in (set_side_capture): round 3's captured fork
+        # faulted on replay when a later, larger request reallocated a scratch arena the graph pointed into
+        # (arenas are now never freed and refuse growth inside a capture: csrc/kernels/workspace.hip)
         return None
     dev = torch.cuda.current_device()
     st = _side["stream"]

@@ -71,12 +71,16 @@ def test_nan_guard_skips_update_gpu():
     assert all(torch.equal(a, p.detach()) for a, p in zip(before, m.parameters()))
 
 
-def _run_steps(name, use_graph, steps, size, ncls, opt="momentum", ema=None, sched=None, lr=0.05):
+def _run_steps(name, use_graph, steps, size, ncls, opt="momentum", ema=None, sched=None, lr=0.05, graph_side=False,
+               reset_seed=False):
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
+    if reset_seed:  # the same dropout masks in both runs of a comparison (the device offset is process state)
+        from distributed_tensorflow_models_amd.ops import elementwise as E
+        E.seed_offset(dev).zero_()
     model = nets_factory.build(name, num_classes=ncls).to(dev)
     step = TrainStep(model, optimizer=opt, lr=lr, momentum=0.9, use_graph=use_graph, ema_decay=ema,
-                     lr_schedule=sched)
+                     lr_schedule=sched, graph_side_stream=graph_side)
     g = torch.Generator().manual_seed(3)
     cin = 1 if name == "lenet" else 3
     xs = [torch.randn(4, size, size, cin, generator=g).to(dev, torch.bfloat16) for _ in range(2)]
@@ -90,13 +94,16 @@ def _run_steps(name, use_graph, steps, size, ncls, opt="momentum", ema=None, sch
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,size,ncls", [("resnet_v1_50", 64, 16), ("cifar10_cnn", 24, 10)])
-def test_hipgraph_step_matches_eager(name, size, ncls):
+@pytest.mark.parametrize("name,size,ncls,side", [("resnet_v1_50", 64, 16, False), ("cifar10_cnn", 24, 10, False),
+                                                 ("resnet_v1_50", 64, 16, True),
+                                                 ("inception_v3_slim_old", 299, 11, True)])
+def test_hipgraph_step_matches_eager(name, size, ncls, side):
     """Captured-and-replayed steps (alternating input buffers, lr schedule and EMA decay staged per
-    replay) follow the eager trajectory."""
+    replay) follow the eager trajectory; ``side``: the weight gradients captured on the side stream
+    (fork / join as graph edges)."""
     sched = lambda s: 0.05 * (0.5 ** (s // 3))  # noqa: E731
-    le, pe, ee, _ = _run_steps(name, False, 6, size, ncls, ema=0.99, sched=sched)
-    lg, pg_, eg, st = _run_steps(name, True, 6, size, ncls, ema=0.99, sched=sched)
+    le, pe, ee, _ = _run_steps(name, False, 6, size, ncls, ema=0.99, sched=sched, reset_seed=True)
+    lg, pg_, eg, st = _run_steps(name, True, 6, size, ncls, ema=0.99, sched=sched, graph_side=side, reset_seed=True)
     assert st._graph is not None and st.global_step == 6 and st.opt.num_updates == 6
     assert lg == pytest.approx(le, rel=2e-2, abs=2e-3)
     # BN statistics are summed with fp32 atomics, so two runs are not bit-identical, and the 2x2
