@@ -84,6 +84,7 @@ class TrainStep:
         # the side stream inside a captured step (use_graph): the forks and joins are graph edges there, so the
         # host cost that made it lose eagerly is gone (DTM_GRAPH_SIDE=0/1)
         if graph_side_stream is None:
+            # (measured slower on Inception-v3: +6.3 % step, profiles/ab/r4_ab_graph_side_inception.log)
             graph_side_stream = os.environ.get("DTM_GRAPH_SIDE", "0") == "1"
         self.graph_side = bool(graph_side_stream)
         prepare_compute_copies(model)

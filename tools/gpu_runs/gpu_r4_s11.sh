@@ -4,7 +4,11 @@
 set -o pipefail
 mkdir -p gpurun_out/r4
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread tests/test_engine.py -m gpu -k "hipgraph" > gpurun_out/r4/pytest_graphside.log 2>&1 || { tail -40 gpurun_out/r4/pytest_graphside.log; exit 1; }
+timeout -k 10 400 python -u -m pytest -v -s --timeout 300 --timeout-method thread tests/test_engine.py -m gpu -k "hipgraph or deterministic" > gpurun_out/r4/pytest_graphside.log 2>&1
+rc=$?
+# plain test failures (rc 1) still allow the benches; a crash, abort or time limit ends the call
+if [ $rc -ne 0 ]; then grep -E "FAILED|Error|assert" gpurun_out/r4/pytest_graphside.log | head -30; fi
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 tail -8 gpurun_out/r4/pytest_graphside.log
 for i in 1 2; do
   for gs in 0 1; do
