@@ -180,7 +180,10 @@ __device__ __forceinline__ void epi_barrier() {
 // aacc (persistent kernels, with SACC): the activation-backward sums [sum g*x | sum g | sum g*r] of this
 // thread's chunk column are added into aacc[24] across all the block's tiles (one partial row per worker at the
 // kernel's end, worker_row) instead of a per-tile LDS reduction + row.
-template <int PT, int CT, bool RAWB, bool EXACT, bool SACC, int NT, bool SIDE = true, bool PRE = false>
+// SPL: the merged-sibling split store (ConvNTArgs::split) - a separate instantiation, so the kernels without it
+// carry no per-chunk branch or split-table kernel arguments in their store loop (measured +3.6 % ResNet-50 step
+// when it was a runtime branch in every kernel: profiles/r4/README.md).
+template <int PT, int CT, bool RAWB, bool EXACT, bool SACC, int NT, bool SIDE = true, bool PRE = false, bool SPL = false>
 __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem, int p0, int c0, int by,
                                                  float* ssum, float* ssq, const char* pre = nullptr,
                                                  const float* pre_ss = nullptr, float* aacc = nullptr) {
@@ -333,16 +336,16 @@ __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem
           }
           v = make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
         }
-        bf16_t* dst = a.y + o;
-        if (a.nsplit) {  // (merged siblings: each member's own output tensor; constant indices, no scratch)
+        if constexpr (SPL) {  // (merged siblings: each member's own output tensor; constant indices, no scratch)
           int off = a.split[0].off, kk = a.split[0].K;
           bf16_t* yb = a.split[0].y;
 #pragma unroll
           for (int q = 1; q < 8; ++q)
             if (q < a.nsplit && kc >= a.split[q].off) { yb = a.split[q].y; off = a.split[q].off; kk = a.split[q].K; }
-          dst = yb + (size_t)out_row(a, m) * kk + (kc - off);
+          *(uint4*)(inb ? yb + (size_t)out_row(a, m) * kk + (kc - off) : a.dump) = v;
+        } else {
+          *(uint4*)(inb ? a.y + o : a.dump) = v;
         }
-        *(uint4*)(inb ? dst : a.dump) = v;
       }
     }
   }
@@ -387,7 +390,7 @@ __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem
 }
 
 template <int PT, int CT, int WP, int WC, int STG, bool RAWB = false, bool EXACT = false, bool NOBIAS = false,
-          bool SACC = false, int NT = 256, bool SIDE = true, bool PRE = false>
+          bool SACC = false, int NT = 256, bool SIDE = true, bool PRE = false, bool SPL = false>
 __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&acc)[WC / 16][WP / 16], char* smem,
                                                  int p0, int c0, int by, float* ssum = nullptr,
                                                  float* ssq = nullptr, const char* pre = nullptr,
@@ -456,10 +459,10 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
     }
   }
   if constexpr (staged)
-    conv_nt_epi_tail<PT, CT, RAWB, EXACT, SACC, NT, SIDE, PRE>(a, smem, p0, c0, by, ssum, ssq, pre, pre_ss, aacc);
+    conv_nt_epi_tail<PT, CT, RAWB, EXACT, SACC, NT, SIDE, PRE, SPL>(a, smem, p0, c0, by, ssum, ssq, pre, pre_ss, aacc);
 }
 
-template <int PT, int CT, int WP, int WC, int UD, int NBUF>
+template <int PT, int CT, int WP, int WC, int UD, int NBUF, bool SPL = false>
 __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
   constexpr int BK = 64;
   constexpr int NWP = PT / WP;
@@ -648,7 +651,8 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
   }
 
   static_assert(PT * (CT * 2 + 16) <= NBUF * BUF, "output staging fits in the operand buffers");
-  if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1>(a, acc, smem, p0, c0, by);
+  if ((a.K & 7) == 0)
+    conv_nt_epilogue<PT, CT, WP, WC, 1, false, false, false, false, 256, true, false, SPL>(a, acc, smem, p0, c0, by);
   else conv_nt_epilogue<PT, CT, WP, WC, 2>(a, acc, smem, p0, c0, by);
 }
 
@@ -666,7 +670,7 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
 //
 // (An ACTL form - the act dgrads' act_x tile LDS-DMA'd under the last k-tile, read by the epilogue from LDS - was
 // neutral at step level, profiles/ab/r4_ab_sside_alds.log, and was removed.)
-template <int PT, int CT, int NS, int UD, bool PRO, int NWP = 2>
+template <int PT, int CT, int NS, int UD, bool PRO, int NWP = 2, bool SPL = false>
 __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
   constexpr int BK = 64;
   constexpr int WP = PT / NWP, WC = CT / (4 / NWP);
@@ -846,7 +850,8 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // the epilogue reuses the ring
-  if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1>(a, acc, smem, p0, c0, by);
+  if ((a.K & 7) == 0)
+    conv_nt_epilogue<PT, CT, WP, WC, 1, false, false, false, false, 256, true, false, SPL>(a, acc, smem, p0, c0, by);
   else conv_nt_epilogue<PT, CT, WP, WC, 2>(a, acc, smem, p0, c0, by);
 }
 
@@ -859,7 +864,7 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
 // one 8-row x 128-B LDS-DMA group per wave-instruction, AI + WI of them per wave per k-tile.
 // (32x32x16-MFMA forms of these tiles measured +0.6 % ResNet-50 step - LDS / DMA bound, not MFMA-issue bound -
 // and were removed: profiles/ab/r3_ab_mfma32_step.log)
-template <int PT, int CT, int NWP, int NS, int UD>
+template <int PT, int CT, int NWP, int NS, int UD, bool SPL = false>
 __global__ __launch_bounds__(512) void conv_nt_w8_kernel(ConvNTArgs a) {
   constexpr int NT = 512, NW = 8;
   constexpr int BK = 64;
@@ -987,7 +992,8 @@ __global__ __launch_bounds__(512) void conv_nt_w8_kernel(ConvNTArgs a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // the epilogue reuses the ring
-  if ((a.K & 7) == 0) conv_nt_epilogue<PT, CT, WP, WC, 1, false, false, false, false, NT>(a, acc, smem, p0, c0, by);
+  if ((a.K & 7) == 0)
+    conv_nt_epilogue<PT, CT, WP, WC, 1, false, false, false, false, NT, true, false, SPL>(a, acc, smem, p0, c0, by);
   else conv_nt_epilogue<PT, CT, WP, WC, 2, false, false, false, false, NT>(a, acc, smem, p0, c0, by);
 }
 
@@ -1966,16 +1972,17 @@ static const bf16_t* zero_chunk() {
   return (const bf16_t*)z;
 }
 
-template <int PT, int CT, int NWP, int NS, int UD>
+template <int PT, int CT, int NWP, int NS, int UD, bool SPL = false>
 static void launch_w8(const ConvNTArgs& a, hipStream_t st) {
   dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT, a.ngrp > 1 ? a.ngrp : 1);
-  hipLaunchKernelGGL((conv_nt_w8_kernel<PT, CT, NWP, NS, UD>), grid, dim3(512), 0, st, a);
+  hipLaunchKernelGGL((conv_nt_w8_kernel<PT, CT, NWP, NS, UD, SPL>), grid, dim3(512), 0, st, a);
 }
 
-template <int PT, int CT, int NS, int UD, int NWP = 2>
+template <int PT, int CT, int NS, int UD, int NWP = 2, bool SPL = false>
 static void launch_pipe(const ConvNTArgs& a, hipStream_t st) {
   dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT, a.ngrp > 1 ? a.ngrp : 1);
-  if (a.in_scale) hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, true, NWP>), grid, dim3(256), 0, st, a);
+  if (SPL) hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, false, NWP, true>), grid, dim3(256), 0, st, a);
+  else if (a.in_scale) hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, true, NWP>), grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((conv_nt_pipe_kernel<PT, CT, NS, UD, false, NWP>), grid, dim3(256), 0, st, a);
 }
 
@@ -2059,10 +2066,10 @@ static bool stream_ok(const ConvNTArgs& a) {
          (!a.in_scale || a.C <= 512) && a.dump != nullptr && a.ostr == 1;
 }
 
-template <int PT, int CT, int WP, int WC, int UD, int NBUF = 2>
+template <int PT, int CT, int WP, int WC, int UD, int NBUF = 2, bool SPL = false>
 static void launch_nt(const ConvNTArgs& a, hipStream_t st) {
   dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT, a.ngrp > 1 ? a.ngrp : 1);
-  hipLaunchKernelGGL((conv_nt_kernel<PT, CT, WP, WC, UD, NBUF>), grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((conv_nt_kernel<PT, CT, WP, WC, UD, NBUF, SPL>), grid, dim3(256), 0, st, a);
 }
 
 // tile variants (the ones the shape policy uses; the rejected ones and their A/B logs are listed in
@@ -2239,9 +2246,22 @@ static TileCfg pick_tile_impl(const ConvNTArgs& a, bool stats) {
   return {0, 128, 2};
 }
 
+// merged-sibling forwards (split store; no prologue, stride-1 1x1): the tiles conv_fwd_impl lets through
+static void dispatch_split(const ConvNTArgs& a, const TileCfg& t, hipStream_t st) {
+  if (t.id == 3) launch_nt<128, 64, 32, 64, 1, 1, true>(a, st);
+  else if (t.id == 4) launch_nt<64, 128, 32, 64, 1, 1, true>(a, st);
+  else if (t.id == 21) launch_pipe<128, 128, 2, 1, 2, true>(a, st);
+  else if (t.id == 24) launch_pipe<256, 64, 2, 1, 2, true>(a, st);
+  else if (t.id == 26) launch_pipe<128, 64, 2, 1, 2, true>(a, st);
+  else if (t.id == 32) launch_pipe<256, 32, 2, 1, 4, true>(a, st);
+  else if (t.id == 40) launch_w8<256, 256, 2, 2, 1, true>(a, st);
+  else launch_nt<128, 128, 64, 64, 1, 2, true>(a, st);
+}
+
 template <int UD>
 static void dispatch_ud(const ConvNTArgs& a, const TileCfg& t, hipStream_t st) {
-  if (t.id == 3) launch_nt<128, 64, 32, 64, UD, 1>(a, st);
+  if (UD == 1 && a.nsplit > 0) dispatch_split(a, t, st);
+  else if (t.id == 3) launch_nt<128, 64, 32, 64, UD, 1>(a, st);
   else if (t.id == 4) launch_nt<64, 128, 32, 64, UD, 1>(a, st);
   else if (t.id == 30 && UD == 1) {
     if (a.Kg <= 64) launch_stream<128, 1>(a, st);
@@ -2428,6 +2448,14 @@ static int g_dec_group = 1;
 DTM_API void dtm_conv_set_dec_group(int on) { g_dec_group = on; }
 static int g_dec_lpt = 1;  // A/B knob: the grouped classes in descending tap count (dtm_conv_set_dec_lpt)
 DTM_API void dtm_conv_set_dec_lpt(int on) { g_dec_lpt = on; }
+// Tile of a grouped strided dgrad, chosen for the whole grouped grid rather than for its heaviest class alone (that
+// class's own rule sees a quarter of the tiles).  Measured per tile on the ResNet-50 stride-2 3x3 dgrads
+// (tools/conv_microbench.py STRIDED=1 DTM_CONV_TILE sweep, profiles/r4/r4_strided_dgrad_tiles.log): 256 output
+// channels (dx 14x14) the 8-wave 256x256 tile 41 us vs 49 on the per-class pick (MIOpen 42), 128 channels (dx
+// 28x28) the pipelined 128x64 tile 51 vs 57 (MIOpen 50-53), 64 channels (dx 56x56) already 128x64.
+// A/B knob dtm_conv_set_dec_tile.
+static int g_dec_tile = 1;
+DTM_API void dtm_conv_set_dec_tile(int on) { g_dec_tile = on; }
 
 static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvDesc* d, const void* add_src,
                            int add_stride, const void* act_x, const float* act_ss, float* act_sums, int act_unscaled,
@@ -2508,7 +2536,12 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvD
       if (la[i].M != la[0].M || la[i].P != la[0].P || la[i].Q != la[0].Q) gi = -2;
       if (gi >= 0 && la[i].Kg > la[gi].Kg) gi = i;
     }
-    const int id = gi >= 0 ? lt[gi].id : -1;
+    int id = gi >= 0 ? lt[gi].id : -1;
+    if (gi >= 0 && g_dec_tile && (id == 21 || id == 26) && g_tile_env < 0 && g_act_tile < 0) {
+      if (la[gi].K % 256 == 0 && g_tile_w8) lt[gi] = {40, 256, 2};
+      else if (la[gi].K <= 128) lt[gi] = {26, 128, 2};
+      id = lt[gi].id;
+    }
     if (!(id == 0 || id == 3 || id == 4 || id == 21 || id == 24 || id == 26 || id == 32 || id == 40)) gi = -1;
     if (gi >= 0) {  // every class on that tile: one partial-sum row per pixel tile of it
       rows = 0;

@@ -40,6 +40,8 @@ def main():
     L = _lib.lib()
     s = _lib.stream_ptr()
     only = os.environ.get("ONLY")
+    if os.environ.get("DEC_TILE") is not None:  # A/B: grouped strided-dgrad tile for the whole grouped grid
+        L.dtm_conv_set_dec_tile(int(os.environ["DEC_TILE"]))
     if os.environ.get("DEC_LPT") is not None:  # A/B: grouped strided-dgrad classes in descending tap count
         L.dtm_conv_set_dec_lpt(int(os.environ["DEC_LPT"]))
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0, "miopen_fwd": 0.0, "miopen_bwd": 0.0, "miopen_dgrad": 0.0,
