@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--batch", type=int, default=2)
     ap.add_argument("--size", type=int, default=299)
     ap.add_argument("--model", default="inception_v3_slim_old")
+    ap.add_argument("--block", default="", help="backprop a fixed gradient from this end point only (no loss): "
+                    "the merged path of the blocks up to it, without the whole random-init net's drift")
     args = ap.parse_args()
     from distributed_tensorflow_models_amd.engine import TrainStep, moving_average_buffers
     from distributed_tensorflow_models_amd.models import nets_factory
@@ -42,7 +44,19 @@ def main():
         with torch.no_grad():
             for b, v in zip(moving_average_buffers(net), init):
                 b.copy_(v)
-        loss, _ = step._forward_backward(x, y)
+        if args.block:
+            step.dp.zero_grad()
+            ep = {}
+            net(x, training=True, end_points=ep)
+            t = ep[args.block]
+            g = torch.Generator(device="cpu").manual_seed(7)
+            G = torch.randn(tuple(t.shape), generator=g).to(dev, t.dtype)
+            torch.autograd.backward(t, G)
+            from distributed_tensorflow_models_amd.ops import _lib as L2
+            L2.side_join()
+            loss = float(t.float().norm())
+        else:
+            loss, _ = step._forward_backward(x, y)
         torch.cuda.synchronize()
         out[run] = (float(loss), {k: p.main_grad.detach().float().clone() for k, p in net.named_parameters()
                                   if getattr(p, "main_grad", None) is not None},
@@ -52,6 +66,9 @@ def main():
     def rel(a, b):
         return float((a - b).norm() / b.norm().clamp_min(1e-30))
 
+    if args.block:
+        live = [n for n, t in out["0"][1].items() if float(t.abs().max()) > 0]  # the parameters the gradient reached
+        out = {k: (v[0], {n: v[1][n] for n in live}, v[2]) for k, v in out.items()}
     print("per-head repeat (0 vs 0b) identical:", all(torch.equal(out["0"][1][k], out["0b"][1][k]) for k in out["0"][1]))
     errs = {k: rel(out["1"][1][k], out["0"][1][k]) for k in out["0"][1]}
     blocks = {}
