@@ -45,16 +45,21 @@ def main():
             for b, v in zip(moving_average_buffers(net), init):
                 b.copy_(v)
         if args.block:
+            from distributed_tensorflow_models_amd.ops import fused as _fz
             step.dp.zero_grad()
-            ep = {}
-            net(x, training=True, end_points=ep)
-            t = ep[args.block]
-            g = torch.Generator(device="cpu").manual_seed(7)
-            G = torch.randn(tuple(t.shape), generator=g).to(dev, t.dtype)
-            torch.autograd.backward(t, G)
-            from distributed_tensorflow_models_amd.ops import _lib as L2
-            L2.side_join()
-            loss = float(t.float().norm())
+            _fz.arena.begin_step(dev)  # (the per-step zero arena, as TrainStep does around every step)
+            try:
+                ep = {}
+                net(x, training=True, end_points=ep)
+                t = ep[args.block]
+                g = torch.Generator(device="cpu").manual_seed(7)
+                G = torch.randn(tuple(t.shape), generator=g).to(dev, t.dtype)
+                torch.autograd.backward(t, G)
+                _lib.side_join()
+                loss = float(t.detach().float().norm())
+                del ep, t
+            finally:
+                _fz.arena.end_step()
         else:
             loss, _ = step._forward_backward(x, y)
         torch.cuda.synchronize()
