@@ -78,7 +78,11 @@ class BottleneckV1(Layer):
     def forward(self, x, training=True, end_points=None):
         if self.shortcut is not None:
             # projection shortcut and conv1: sibling 1x1 conv+BNs of x with one merged forward and backward (ops.fused)
-            with fused.sibling_group(x, training and end_points is None, heads=self.sibling_heads()):
+            # (the merged FORWARD is opt-in here, DTM_RESNET_SIBLING_FWD=1: the 512 + 128 -> 640-channel merged conv
+            # loses the 8-wave tile the 512-channel shortcut gets alone - ResNet-50 +0.41 % step with it,
+            # profiles/ab/r4_ab_fwd_dtile_resnet.log; the merged backward stays on)
+            heads = self.sibling_heads() if os.environ.get("DTM_RESNET_SIBLING_FWD", "0") == "1" else None
+            with fused.sibling_group(x, training and end_points is None, heads=heads):
                 sc = self.shortcut(x, training)
                 r1 = self.conv1(x, training)
         else:

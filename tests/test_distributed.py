@@ -173,7 +173,7 @@ def test_bsp_gpu_two_ranks_hip_kernels_match_single_rank():
 _DP_MATRIX = [
     ("resnet_v1_50", {}),
     ("resnet_v1_50", {"DTM_WGRAD_STREAM": "0"}),
-    ("resnet_v1_50", {"DTM_SIBLING_FWD": "0"}),
+    ("resnet_v1_50", {"DTM_RESNET_SIBLING_FWD": "1"}),
     ("resnet_v1_50", {"DTM_SIBLING_GROUP": "0"}),
     ("inception_v3_slim_old", {}),
     ("inception_v3_slim_old", {"DTM_SIBLING_FWD": "0", "DTM_SIBLING_COMBINE": "0"}),
