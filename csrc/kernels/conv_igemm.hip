@@ -2292,6 +2292,9 @@ static void dispatch_nt(const ConvNTArgs& a, int ud, const TileCfg& t, hipStream
 
 DTM_API int dtm_get_deterministic();
 
+static int g_split_tile = 1;  // A/B knob: the merged-head tile rule in conv_fwd_impl (dtm_conv_set_split_tile)
+DTM_API void dtm_conv_set_split_tile(int on) { g_split_tile = on; }
+
 static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, const float* bias, const float* in_scale,
                          const float* in_shift, int relu, const ConvDesc* d, hipStream_t stream, float** rows_ws,
                          int* nrows, const ConvNTArgs::Split* split = nullptr, int nsplit = 0) {
@@ -2328,10 +2331,14 @@ static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, cons
     }
   }
   int rows = 0;
-  const TileCfg tc = pick_tile(a, stats);
+  TileCfg tc = pick_tile(a, stats);
   // (merged-sibling stores happen in the LDS-staged epilogue only: K % 8 == 0 above; the persistent / direct
-  // kernels have their own store paths)
-  if (nsplit > 0 && (tc.id == 30 || tc.id == 31 || tc.id == 33 || tc.id == 60)) return -1;
+  // kernels have their own store paths, so a split launch the policy sends there takes the 64x128 tile instead)
+  if (nsplit > 0 && (tc.id == 30 || tc.id == 31 || tc.id == 33 || tc.id == 60)) tc = {4, 64, 2};
+  // merged heads: the pipelined 128x128 tile unless the policy took the 8-wave one - measured on every Inception-v3
+  // head shape (tools/split_tile_sweep.py, profiles/r4/r4_split_tile_sweep.log): 799 -> ~765 us per step, e.g.
+  // 17x17 768 -> 640 85 -> 77 us, 35x35 288 -> 240 84 -> 80 us (the policy's 64x128 / 128x64 picks)
+  if (nsplit > 0 && g_split_tile && g_tile_env < 0 && tc.id != 40 && tc.id != 21) tc = {21, 128, 2};
   if (tc.id == 60) direct_setup(a);
   if (stats) {
     // one per streaming / direct worker; one per pixel tile (staged epilogue, K % 8 == 0); else per (pixel

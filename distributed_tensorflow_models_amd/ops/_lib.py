@@ -124,6 +124,7 @@ _SIGS = {
     "dtm_conv_fwd_bn_multi": (_I, [_P, _P, _P, _P, _I, _P, _F, _F, _F, _I, _I, ctypes.POINTER(ConvDesc), _P]),
     "dtm_conv_set_dec_lpt": (None, [_I]),
     "dtm_conv_set_dec_tile": (None, [_I]),
+    "dtm_conv_set_split_tile": (None, [_I]),
     "dtm_get_reserved_cus": (_I, []),
     "dtm_compute_cus_api": (_I, []),
     "dtm_cu_hog": (_I, [_I, _F, _P]),

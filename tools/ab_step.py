@@ -6,7 +6,7 @@ VARIANTS="base=;noW=wtile:-3;noT=tile:-3;fused=prologue:fused" python tools/ab_s
 keys: tile (conv_nt tile id), w8 (0/1: the 8-wave 256x256 conv tile in the shape policy), kwide (0/1: 64-channel tiles for K % 128 <= 64), few (0/1: streaming few-row slab reduction), bnout (0/1: block-output BN backward in the consuming dgrad's epilogue), bnst (0/1: also for stride-2 unit outputs), b1x1 (0/1: one-pass 1x1 conv+BN backward), stemw (0/1: stem BN backward in the wgrad operand staging), sact (0/1: streaming 1x1 kernel for act dgrads), pcom (0/1: Inception pool branches as conv -> pool -> BN), sib (0/1: merged backward of sibling 1x1 convs), ahand (0/1: input-gradient hand-off between conv consumers of one activation), sibp (0/1: the commuted pool-branch conv joins the sibling group), sbwd (0/1: HIP backward of the pooled-BN statistics), catm (0/1: one-launch multi-part concat BN-apply), dec (0/1: stride-decomposed strided dgrads), dgrp (0/1: their parity classes as one grouped launch), k32 (0/1: 256x32 tile for <=32-channel spatial convs), cpt (16-B chunks per thread of the BN-stream grids), pol2 (0/1: v2 conv tile-policy rules), sstr (0/1/2: the stem forward as a persistent stream, 3- / 2-slot ring), wgs (0/1: conv+BN weight gradients on a side stream), scu (percent of the CUs the side-stream wgrads size their split-K grid for), wcu / swc (the same for the main-stream / stem wgrads), dir3 (0/1: direct 3x3 kernel for C in {32, 64}), atile (tile id of the dgrads with a fused
 activation-backward epilogue, -1 = policy), rsv (CUs reserved from the compute grids' sizing), sfwd (0/1: merged sibling-head forward), rfwd (0/1: also for ResNet projection units), scomb (0/1: grouped sibling
 stats-combine), lpt (0/1: grouped parity classes of strided dgrads in descending tap
-count), dtile (0/1: grouped strided-dgrad tile chosen for the whole grouped grid), hog (blocks:ms - a
+count), dtile (0/1: grouped strided-dgrad tile chosen for the whole grouped grid), stile (0/1: merged-head convs on the pipelined 128x128 tile), hog (blocks:ms - a
 CU-occupying copy kernel on another stream from every backward start, standing in for RCCL channels), wtile[:occ] (wgrad tile id / blocks-per-CU target), prologue (DTM_PROLOGUE),
 stem (DTM_STEM: 1 = packed-row stem path), red (target_blocks:max_chunks[:direct_max] of the
 partial-sum reductions; 0 = legacy 256 rows per block; direct_max = largest BN-backward grid that
@@ -71,6 +71,7 @@ def apply(cfg):
     _lib.set_reserved_cus(int(cfg.get("rsv", "0")))
     L.dtm_conv_set_dec_lpt(int(cfg.get("lpt", "1")))
     L.dtm_conv_set_dec_tile(int(cfg.get("dtile", "1")))
+    L.dtm_conv_set_split_tile(int(cfg.get("stile", "1")))
     HOG[0] = cfg.get("hog")
     sc = cfg.get("sc", "5:4096").split(":")
     L.dtm_set_sc_policy(int(sc[0]), int(sc[1]))
