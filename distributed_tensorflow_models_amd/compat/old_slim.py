@@ -66,6 +66,7 @@ def batch_norm(inputs, decay=0.999, center=True, scale=False, epsilon=0.001, mov
                 name = sc + "/" + suffix
                 if name not in store.collections.get(UPDATE_OPS_COLLECTION, []):
                     store.add_to_collection(UPDATE_OPS_COLLECTION, name)
+    mm._bn_decay = mv._bn_decay = float(decay)  # BSP BufferSync combines replicas with the layer's own decay
     relu = activation in (torch.relu, E.relu, "relu")
     y = F.batch_norm(x, gamma, beta, mm.data, mv.data, bool(is_training), decay, epsilon, relu, None, False)
     return y if relu else _activate(y, activation)

@@ -393,6 +393,7 @@ def batch_norm(inputs, decay=0.999, center=True, scale=False, epsilon=0.001, act
                       collections=[GraphKeys.MOVING_AVERAGE_VARIABLES])
         mv = variable("moving_variance", (C,), initializer=("constant", 1.0), trainable=False, buffer=True,
                       collections=[GraphKeys.MOVING_AVERAGE_VARIABLES])
+    mm._bn_decay = mv._bn_decay = float(decay)  # BSP BufferSync combines replicas with the layer's own decay
     if _fold is not None:  # outside the BatchNorm scope: the weight quantiser lives in the conv's scope
         return _folded_bn(_fold, gamma, beta, mm, mv, is_training, decay, epsilon, activation_fn,
                           True if bessel is None else bessel)

@@ -49,16 +49,25 @@ def moving_average_buffers(model):
             if not trainable and t.dtype == torch.float32 and t.is_floating_point()]
 
 
+def moving_average_decays(model, buffers):
+    """The moving-average decay of each BN statistic in ``buffers`` (None where unknown): a module BatchNorm
+    (models/layers.py) carries ``decay``; slim / old-slim batch_norm tag their variables with ``_bn_decay``."""
+    by_id = {}
+    for m in model.modules():
+        names = getattr(m, "tf_buffer_names", None)
+        if names and getattr(m, "decay", None) is not None:
+            for b in names:
+                by_id[id(getattr(m, b))] = float(m.decay)
+    return [getattr(b, "_bn_decay", by_id.get(id(b))) for b in buffers]
+
+
 def reserved_cus_default():
     """CUs kept out of the compute grids' sizing under data parallelism (ops/_lib.set_reserved_cus):
-    DTM_RESERVED_CUS if set, else the pinned RCCL channel count (NCCL_MAX_NCHANNELS: one workgroup per
-    channel), else RESERVED_CUS_DP."""
+    DTM_RESERVED_CUS if set, else RESERVED_CUS_DP.  (A pinned RCCL channel count - NCCL_MAX_NCHANNELS, trainer
+    --rccl_channels - does not reserve anything by itself: reserving measured slower, see below.)"""
     v = os.environ.get("DTM_RESERVED_CUS")
     if v is not None:
         return int(v)
-    ch = os.environ.get("NCCL_MAX_NCHANNELS")
-    if ch:
-        return int(ch)
     return RESERVED_CUS_DP
 
 
@@ -99,7 +108,9 @@ class TrainStep:
                              % self.dp.world)
         # BN moving statistics: one flat buffer, averaged over the replicas every step (reference
         # keeps ONE PS-resident copy that every worker updates); must precede the optimizer tables
-        self.bufsync = BufferSync(moving_average_buffers(model), process_group, every=bn_sync_every)
+        bufs = moving_average_buffers(model)
+        self.bufsync = BufferSync(bufs, process_group, every=bn_sync_every,
+                                  decays=moving_average_decays(model, bufs))
         # ema_buffers: whether the statistics also get EMA shadows (slim BN lists them in
         # moving_average_variables(); tf.layers BN - the CIFAR ResNet preset - does not)
         self.opt = FusedOptimizer(params, optimizer, lr, momentum, rho, epsilon, ema_decay, weight_decay,
@@ -164,6 +175,9 @@ class TrainStep:
             if images.is_cuda:
                 _lib.side_join()  # weight gradients enqueued on the side stream (ops/_lib.py)
             self._mark("bwd")
+        except BaseException:
+            self.bufsync.abort()  # the live BN statistics stay this replica's own (never a partial sum)
+            raise
         finally:
             _fused.arena.end_step()
         with roctx("allreduce_wait"):

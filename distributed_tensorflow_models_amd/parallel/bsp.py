@@ -335,29 +335,52 @@ class BufferSync:
     inception/slim/ops.py:117-131) writes the ONE PS-resident ``moving_mean`` / ``moving_variance``, so one
     global step applies W updates m <- d*m + (1-d)*b_r, one per worker batch, to a single copy - the same as
     the ASP store here (parallel/asp.py push_buffers: each worker adds its forward's delta).  Here each replica
-    updates its own copy in its forward; this class makes every replica end the step with
-        m = m_prev + sum_r (m_r - m_prev) = m_prev + (1 - d) * sum_r (b_r - m_prev),
-    the W sequential updates to first order in (1 - d) (exact for W = 1; the second-order terms are
-    O((1-d)^2), ~1e-5 relative at d = 0.997), instead of one update with the averaged batch statistics (which
-    would adapt W times slower per step than the reference).
-    Mechanics: the statistics live in one flat fp32 buffer (``flatten_tensors``); ``begin`` snapshots it
-    before the forward, ``issue`` (right after the forward: the statistics are final then, backward never
-    reads them) turns the buffer into this replica's delta and issues its SUM all-reduce, which runs on the
-    comm stream underneath the whole backward; ``finish`` waits and adds the snapshot back.  EMA shadows of
-    the statistics are updated by the optimizer from the synced values, so they stay replica-identical
-    without a collective of their own.  ``every`` > 1 syncs only every k-th step (replicas drift in between;
-    the skipped steps' local deltas are folded into the next synced step's delta)."""
+    updates its own copy in its forward (k local steps since the last sync, k = ``every``); this class makes
+    every replica end the synced step with
+        m = d^(W*k) * m_prev + (1 - d^(W*k)) * mean_r(B_r),    B_r = (m_r - d^k * m_prev) / (1 - d^k),
+    i.e. W*k sequential moving-average updates of the one shared copy, each replica contributing its own
+    implied (decay-weighted) batch statistic B_r.  This is exact for W = 1, equal to the reference's W
+    sequential updates up to the order in which the workers' batches land, and a convex combination of
+    m_prev and the replicas' statistics for ANY decay (NASNet-CIFAR's d = 0.9 at W = 8 included: a
+    first-order form m_prev + sum_r (m_r - m_prev) would weight m_prev by 1 - W(1-d) <= 0 there and could drive
+    a variance negative).  Statistics whose decay is unknown get d = 0: plain averaging over the replicas.
+    Mechanics: the statistics live in one flat fp32 buffer (``flatten_tensors``); ``issue`` (right after the
+    forward: the statistics are final then, backward never reads them) computes B_r into a separate send
+    buffer and issues its SUM all-reduce, which runs on the comm stream underneath the whole backward;
+    ``finish`` waits and writes the combined statistics.  The live statistics are never overwritten by a
+    partial result, so an exception between ``issue`` and ``finish`` (``abort``) leaves them at this replica's
+    own values.  EMA shadows of the statistics are updated by the optimizer from the synced values, so they
+    stay replica-identical without a collective of their own."""
 
-    def __init__(self, buffers, process_group=None, every=1):
+    def __init__(self, buffers, process_group=None, every=1, decays=None):
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
         self.buffers = [b for b in buffers]
         self.every = max(1, int(every))
         self.flat = flatten_tensors(self.buffers) if (self.world > 1 and self.buffers) else None
-        # the statistics as of the last sync (every replica holds the same values there)
-        self.prev = self.flat.detach().clone() if self.flat is not None else None
+        self.prev = self.send = self.decay = None
+        if self.flat is not None:
+            # the statistics as of the last sync (every replica holds the same values there)
+            self.prev = self.flat.detach().clone()
+            self.send = torch.empty_like(self.flat)
+            ds = list(decays) if decays is not None else [None] * len(self.buffers)
+            assert len(ds) == len(self.buffers), "BufferSync: one decay per buffer"
+            # per-element decay, fp64 so d^(W*k) keeps its digits; unknown decay -> 0 (averaging)
+            self.decay = torch.cat([torch.full((b.numel(),), float(d) if d is not None else 0.0,
+                                               dtype=torch.float64) for b, d in zip(self.buffers, ds)]
+                                   ).to(self.flat.device)
+            assert bool(((self.decay >= 0) & (self.decay < 1)).all()), "BN decay must lie in [0, 1)"
         self._work = None
-        self._n = 0
+        self._n = 0       # steps since construction
+        self._local = 0   # local (unsynced) moving-average updates since the last sync
+        self._k = 0       # local updates covered by the in-flight all-reduce
+        self._pow = {}    # k -> (d^k, 1 / (1 - d^k), d^(W*k)) (k is constant in steady state)
+
+    def _powers(self, k):
+        if k not in self._pow:
+            dk = self.decay.pow(k)
+            self._pow[k] = (dk, 1.0 / (1.0 - dk), self.decay.pow(self.world * k))
+        return self._pow[k]
 
     def begin(self):
         """(kept for API symmetry: the snapshot is the state after the last sync, see finish)"""
@@ -366,24 +389,42 @@ class BufferSync:
         if self.flat is None:
             return
         self._n += 1
+        self._local += 1
         if (self._n - 1) % self.every:
             return
+        k = self._local
         with roctx("bn_stats_allreduce"):
-            self.flat.sub_(self.prev)  # this replica's delta since the last sync
-            self._work = dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            dk, inv, _ = self._powers(k)
+            # B_r = (m_r - d^k m_prev) / (1 - d^k)   (this replica's implied batch statistic)
+            self.send.copy_((self.flat.double() - dk * self.prev.double()) * inv)
+            self._k = k
+            self._work = dist.all_reduce(self.send, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
     def finish(self):
         if self._work is None:
             return
         self._work.wait()
         self._work = None
-        self.flat.add_(self.prev)
+        dwk = self._powers(self._k)[2]
+        m = dwk * self.prev.double() + (1.0 - dwk) * (self.send.double() / self.world)
+        self.flat.copy_(m)
         self.prev.copy_(self.flat)
+        self._local = 0
+
+    def abort(self):
+        """An exception between issue() and finish(): drain the collective, keep this replica's own statistics
+        (the live buffer was never overwritten) - the next completed sync folds them in."""
+        if self._work is not None:
+            try:
+                self._work.wait()
+            finally:
+                self._work = None
 
     def resync(self):
         """The statistics were overwritten outside a step (checkpoint restore, broadcast): re-snapshot."""
         if self.flat is not None:
             self.prev.copy_(self.flat)
+            self._local = 0
 
     def numel(self):
         return 0 if self.flat is None else self.flat.numel()

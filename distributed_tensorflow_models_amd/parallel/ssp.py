@@ -15,7 +15,8 @@ from . import process_group as pg
 
 class StalenessClock:
     def __init__(self, max_staleness=5, store=None, rank=None, world=None, run_id="0", poll_s=0.002,
-                 timeout_s=3600.0, log_fn=None):
+                 timeout_s=3600.0, log_fn=None, read_only=False):
+        """``read_only``: an observer (the debug CLI) - publishes nothing, cannot tick."""
         if store is None:
             from .asp import _default_store
             store = _default_store()
@@ -28,7 +29,9 @@ class StalenessClock:
         self.log_fn = log_fn
         self.waited_s = 0.0
         self.max_observed_gap = 0
-        self.store.set(self.prefix + str(self.rank), "0")
+        self.read_only = bool(read_only)
+        if not self.read_only:
+            self.store.set(self.prefix + str(self.rank), "0")
 
     def _keys(self):
         return [self.prefix + str(r) for r in range(self.world)]
@@ -42,6 +45,8 @@ class StalenessClock:
 
     def tick(self, local_step):
         """check_staleness(task_index, local_step): publish, then wait until within the bound."""
+        if self.read_only:
+            raise RuntimeError("StalenessClock: a read-only observer cannot tick")
         self.store.set(self.prefix + str(self.rank), str(int(local_step)))
         t0 = time.time()
         warned = False
@@ -62,6 +67,8 @@ class StalenessClock:
 
     def finish(self, final_step=None):
         """Release waiters when this worker stops (publish a step that never blocks anyone)."""
+        if self.read_only:
+            return
         self.store.set(self.prefix + str(self.rank), str(1 << 40))
 
 
@@ -102,7 +109,7 @@ def main():  # debug CLI (replaces CheckStaleness-remote): print the clock of a 
     ap.add_argument("--run-id", default="0")
     a = ap.parse_args()
     st = dist.TCPStore(a.host, a.port, is_master=False, timeout=datetime.timedelta(seconds=10))
-    c = StalenessClock(store=st, rank=-1, world=a.world, run_id=a.run_id)
+    c = StalenessClock(store=st, rank=-1, world=a.world, run_id=a.run_id, read_only=True)
     print(c.steps())
 
 

@@ -148,7 +148,7 @@ def define_common_flags(flags, preset):
             ("depth_multiplier", Fl, 1.0, "MobileNet depth multiplier"),
             ("fine_tune_checkpoint", S, "", "initialise model variables from this checkpoint (fresh runs only)"),
             ("train_accuracy_every", I, p.get("train_accuracy_every", 0),
-             "chief: every N steps, accuracy of the training-mode network on a fed batch of distorted training "
+             "every worker: every N steps, accuracy of the training-mode network on a fed batch of distorted training "
              "images (reference resnet/cifar10_resnet_bsp.py:146-148; 0 = off)"),
             ("train_accuracy_batch", I, 10000, "images in that fed batch (the reference feeds 10000)"),
     ):
@@ -282,6 +282,14 @@ def train(preset, flags, default_mode="bsp"):
     gstep = torch.zeros((), dtype=torch.int64)
     loss_fn = make_loss_fn(cfg.get("label_smoothing", 0.0), cfg.get("aux_weight", 0.4), FLAGS.batch_weight)
     store = clock = None
+    ft_missing = None
+    if FLAGS.fine_tune_checkpoint and not path:
+        # model variables only (no slots, no global step: the schedule restarts), missing ones keep their
+        # initialisation (e.g. a new logits layer).  Restored BEFORE the engine / store exist, so the BSP
+        # broadcast, the BN-statistics sync snapshot, the bf16 compute copies and the ASP owner shards all start
+        # from the fine-tune values (a restore after them would be folded into the next BN sync as a W-fold delta)
+        ft = [v for v in model_variables(model, None, None, prefix=ckpt_kw["prefix"])]
+        ft_missing = Saver(ft).restore(FLAGS.fine_tune_checkpoint, strict=False)
     if mode == "bsp":
         if FLAGS.use_hipgraph and world > 1:
             logging.warning("--use_hipgraph ignored: step capture is single-rank only (world size %d)", world)
@@ -334,12 +342,8 @@ def train(preset, flags, default_mode="bsp"):
     if path:
         logging.info("rank %d restored %s (global_step %d)", rank, path, int(gstep))
     elif FLAGS.fine_tune_checkpoint:
-        # model variables only (no slots, no global step: the schedule restarts), missing ones keep
-        # their initialisation (e.g. a new logits layer)
-        ft = [v for v in model_variables(model, None, None, prefix=ckpt_kw["prefix"])]
-        missing = Saver(ft).restore(FLAGS.fine_tune_checkpoint, strict=False)
         logging.info("fine-tuning from %s (%d variables not in the checkpoint)", FLAGS.fine_tune_checkpoint,
-                     len(missing or []))
+                     len(ft_missing or []))
     saver = Saver(vars_, max_to_keep=cfg["max_to_keep"])
     if is_chief and os.path.isdir(FLAGS.train_dir):
         saver.recover_last_checkpoints(FLAGS.train_dir)
@@ -430,7 +434,8 @@ def train(preset, flags, default_mode="bsp"):
             metrics.write(step=step, global_step=gs, loss=loss_v, lr=sched(gs), images_per_sec=B / max(dt, 1e-9),
                           node_images_per_sec=world * B / max(dt, 1e-9), step_ms=dt * 1e3, world=world, mode=mode,
                           **extra)
-        if FLAGS.train_accuracy_every and step % FLAGS.train_accuracy_every == 0 and is_chief:
+        # every worker runs the probe, as every reference worker does (resnet/cifar10_resnet_bsp.py:146-148)
+        if FLAGS.train_accuracy_every and step % FLAGS.train_accuracy_every == 0:
             if probe is None:
                 probe = make_input(cfg, FLAGS.train_accuracy_batch, device, FLAGS, rank + 7919)
             acc = train_accuracy_probe(model, probe)
