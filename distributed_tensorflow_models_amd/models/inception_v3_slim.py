@@ -193,31 +193,49 @@ class InceptionV3Slim(Layer):
                 x = op(x, training)
         return [x]
 
-    def forward(self, x, training=True, end_points=None):
+    STEM_END_POINTS = ("conv0", "conv1", "conv2", "pool1", "conv3", "conv4", "pool2")
+
+    def run_stem(self, x, training=True, end_points=None):
         net = x
-        for op in self.stem:
+        for op, name in zip(self.stem, self.STEM_END_POINTS):
             net = F.max_pool(net, 3, 2, "VALID") if isinstance(op, str) else op(net, training)
-        aux = None
-        for name, kind, branches in self.plan:
-            if kind == "aux":
-                a = F.avg_pool(net, 5, 3, "VALID")
-                a = self.aux_conv(self.aux_proj(a, training), training)
-                aux = self.aux_fc(_t(a).reshape(a.shape[0], -1), training)
-                if end_points is not None:
-                    end_points["aux_logits"] = aux
-                continue
-            # branch outputs written straight into their channel slices (zero-copy concat); the branches' first
-            # 1x1 conv+BNs on the block input share one forward (one conv + one finalize) and one backward
-            # (ops.fused.sibling_group)
-            with _fused.sibling_group(net, training, heads=self._sibling_heads(branches)):
-                parts = [p for b in branches for p in self._run(b, net, training)]
-            net = concat_channels(parts)
             if end_points is not None:
                 end_points[name] = net
+        return net
+
+    def run_block(self, branches, net, training=True):
+        """One mixed block: branch outputs written straight into their channel slices (zero-copy concat); the
+        branches' first 1x1 conv+BNs on the block input share one forward (one conv + one finalize) and one
+        backward (ops.fused.sibling_group)."""
+        with _fused.sibling_group(net, training, heads=self._sibling_heads(branches)):
+            parts = [p for b in branches for p in self._run(b, net, training)]
+        return concat_channels(parts)
+
+    def run_aux(self, net, training=True):
+        a = F.avg_pool(net, 5, 3, "VALID")
+        a = self.aux_conv(self.aux_proj(a, training), training)
+        return self.aux_fc(_t(a).reshape(a.shape[0], -1), training)
+
+    def run_logits(self, net, training=True):
         k = net.shape[1]
         net = F.avg_pool(net, (k, net.shape[2]), 1, "VALID")
         net = self.dropout(_t(net).reshape(net.shape[0], -1), training)
-        logits = self.fc(net, training)
+        return self.fc(net, training)
+
+    def forward(self, x, training=True, end_points=None):
+        # end points as the reference names them (inception/slim/inception_model.py:88-331)
+        net = self.run_stem(x, training, end_points)
+        aux = None
+        for name, kind, branches in self.plan:
+            if kind == "aux":
+                aux = self.run_aux(net, training)
+                if end_points is not None:
+                    end_points["aux_logits"] = aux
+                continue
+            net = self.run_block(branches, net, training)
+            if end_points is not None:
+                end_points[name] = net
+        logits = self.run_logits(net, training)
         if end_points is not None:
             end_points["logits"] = logits
             end_points["predictions"] = torch.softmax(logits.float(), -1)

@@ -315,3 +315,22 @@ def test_sibling_weight_groups_declared():
     assert all(len({tuple(w.shape[1:]) for w in g}) == 1 for g in groups)
     rn = nets_factory.build("resnet_v1_50", num_classes=11)
     assert [[w.shape[0] for w in g] for g in rn.sibling_weight_groups()] == [[512, 128], [1024, 256], [2048, 512]]
+
+
+def test_inception_v3_slim_old_endpoints():
+    """End points of the old-slim Inception-v3 as /root/reference/inception/slim/inception_model.py:88-331 names
+    them (shapes from its inception_test.py geometry at 299x299)."""
+    B, nc = 2, 1001
+    ep = {}
+    m = nets_factory.build("inception_v3_slim_old", nc)
+    logits, aux = m(torch.zeros(B, 299, 299, 3), training=True, end_points=ep)
+    g = {'conv0': [B, 149, 149, 32], 'conv1': [B, 147, 147, 32], 'conv2': [B, 147, 147, 64],
+         'pool1': [B, 73, 73, 64], 'conv3': [B, 73, 73, 80], 'conv4': [B, 71, 71, 192], 'pool2': [B, 35, 35, 192],
+         'mixed_35x35x256a': [B, 35, 35, 256], 'mixed_35x35x288a': [B, 35, 35, 288],
+         'mixed_35x35x288b': [B, 35, 35, 288], 'mixed_17x17x768a': [B, 17, 17, 768],
+         'mixed_17x17x768b': [B, 17, 17, 768], 'mixed_17x17x768c': [B, 17, 17, 768],
+         'mixed_17x17x768d': [B, 17, 17, 768], 'mixed_17x17x768e': [B, 17, 17, 768],
+         'aux_logits': [B, nc], 'mixed_17x17x1280a': [B, 8, 8, 1280], 'mixed_8x8x2048a': [B, 8, 8, 2048],
+         'mixed_8x8x2048b': [B, 8, 8, 2048], 'logits': [B, nc], 'predictions': [B, nc]}
+    _check_eps(ep, g)
+    assert list(aux.shape) == [B, nc] and list(logits.shape) == [B, nc]
