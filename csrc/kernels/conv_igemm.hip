@@ -2047,7 +2047,7 @@ static int stream_workers(const ConvNTArgs& a) {
 
 // the stem forward as a persistent stream: -1: DTM_STEM_STREAM env (default 1), 0 off, 1 on (3-slot ring),
 // 2 on with the 2-slot ring (A/B knob)
-static int g_stem_stream = -1;
+static int g_stem_stream = 1;  // A/B API dtm_conv_set_stem_stream (2 = the 2-slot ring)
 DTM_API void dtm_conv_set_stem_stream(int on) { g_stem_stream = on; }
 // statistics partial rows of the streaming kernel (tile id 30 / 31 / 33): one per worker
 static int stream_rows(const ConvNTArgs& a, int id) {
@@ -2078,7 +2078,7 @@ static void launch_nt(const ConvNTArgs& a, hipStream_t st) {
 // pipelined 128x128 / 256x64 / 128x64 / 256x32, 30 / 31 = the persistent streaming 1x1 kernel (128 / 64
 // channels), 40 = the 8-wave 256x256 tile.  DTM_CONV_TILE forces one (sweeps: tools/conv_tile_sweep.py).
 // the direct 3x3 kernel (tile id 60): -1: DTM_DIRECT3X3 env (default 1), 0 / 1: A/B knob
-static int g_direct3 = -1;
+static int g_direct3 = 1;  // A/B API dtm_conv_set_direct3
 DTM_API void dtm_conv_set_direct3(int on) { g_direct3 = on; }
 // Measured (tools/conv_tile_sweep.py, profiles/r3/r3_sweep_direct3x3.log): 32 output channels win 1.8-2.2x
 // (Inception stem 3x3 32->32 fwd 108 vs 185 us, dgrads 64->32 / 32->32 185 / 100 vs 274 / 182 us); 64 output
@@ -2163,23 +2163,13 @@ static TileCfg pick_tile_impl(const ConvNTArgs& a, bool stats) {
   if (g_tile_env == -2) {
     const char* e = getenv("DTM_CONV_TILE");
     g_tile_env = e ? atoi(e) : -1;
-    const char* p2 = getenv("DTM_CONV_POLICY2");  // (0: the round-1 shape policy, for A/B runs)
-    if (p2) g_policy2 = atoi(p2);
   }
   // measured per ResNet-50 shape (tools/conv_microbench.py, DTM_CONV_TILE sweep): the single-buffer
   // variants win almost everywhere (more resident blocks hide the short-K latency); the 2-buffer
   // 128x128 tile keeps the small-M / deep-K layers (7x7 maps, K-reduction >= 2048)
   int id = g_tile_env;
-  if (g_stem_stream < 0) {
-    const char* e = getenv("DTM_STEM_STREAM");
-    g_stem_stream = e ? atoi(e) : 1;
-  }
   // the packed-row stem as a persistent stream (weights resident, pixel tiles prefetched)
   if (id == -1 && g_stem_stream && stem_stream_ok(a)) return {33, 64, 2};
-  if (g_direct3 < 0) {
-    const char* e = getenv("DTM_DIRECT3X3");
-    g_direct3 = e ? atoi(e) : 1;
-  }
   // narrow 3x3 stride-1 layers: the direct kernel (resident weights, halo tiles; the caller sets the
   // spatial tiling with direct_setup)
   // (dgrad post-op inputs come by LDS-DMA: with per-tile global side loads in the epilogue the compiler's waits
@@ -2681,11 +2671,8 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   a.fd_PQ = make_fastdiv(d->P * d->Q); a.fd_Q = make_fastdiv(d->Q);
   // wgrad tile variants: 0 = 128 (K) x 128 (RSC) register-staged, 1 = 64 x 128, 6 = 32 x 128, 10 = the
   // pipelined LDS-DMA 128 x 128, 12 = the 8-wave pipelined 256 x 256 (the rejected variants and their A/B
-  // logs: profiles/ab/README.md).  DTM_WGRAD_TILE forces one (A/B experiments).
-  if (g_wgrad_env == -2) {
-    const char* e = getenv("DTM_WGRAD_TILE");
-    g_wgrad_env = e ? atoi(e) : -1;
-  }
+  // logs: profiles/ab/README.md).  dtm_conv_set_wgrad_tile forces one (A/B experiments).
+  if (g_wgrad_env == -2) g_wgrad_env = -1;
   const int wenv = g_wgrad_env;
   int wt = wenv >= 0 ? wenv : (d->K <= 64 ? 1 : 0);
   // <= 32 output channels: 32-row tiles (no half-empty 64-row tile; A/B knob dtm_conv_set_k32)

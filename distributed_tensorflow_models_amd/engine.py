@@ -83,19 +83,13 @@ class TrainStep:
                  label_smoothing=0.0, aux_weight=0.4, ema_decay=None, lr_schedule=None, use_graph=False,
                  process_group=None, weight_decay=None, batch_weight=1.0, nan_guard=True, timer=None,
                  grad_comm_dtype=None, ema_buffers=True, bn_sync_every=1, wgrad_stream=None, bsp_check=None,
-                 overlap=True, graph_side_stream=None):
+                 overlap=True):
         self.model = model
         if wgrad_stream is not None:
             # conv+BN weight gradients on the side stream (ops/_lib.py side_stream; process-wide): ResNet-50
             # -4.3 % step time, Inception-v3 +3.4 % eager (its per-conv stream forks cost more host time than
             # they overlap)
             _lib.set_side_enabled(wgrad_stream)
-        # the side stream inside a captured step (use_graph): the forks and joins are graph edges there, so the
-        # host cost that made it lose eagerly is gone (DTM_GRAPH_SIDE=0/1)
-        if graph_side_stream is None:
-            # (measured slower on Inception-v3: +6.3 % step, profiles/ab/r4_ab_graph_side_inception.log)
-            graph_side_stream = os.environ.get("DTM_GRAPH_SIDE", "0") == "1"
-        self.graph_side = bool(graph_side_stream)
         prepare_compute_copies(model)
         params = [p for p in model.parameters() if p.requires_grad]
         # bsp_check (or DTM_BSP_CHECK=1): assert every gradient write precedes its bucket's all-reduce (debug)
@@ -228,26 +222,19 @@ class TrainStep:
     graph_warmup = 2
 
     def _graph_step(self, images, labels):
-        side_was = _lib.side_enabled()
         if self._graph is None and self._eager_steps < self.graph_warmup:
             self._eager_steps += 1
             self.use_graph = False
-            if self.graph_side:  # the warm-up steps create the side stream and grow its scratch arena
-                _lib.set_side_enabled(True)
             try:
                 return self(images, labels)
             finally:
                 self.use_graph = True
-                _lib.set_side_enabled(side_was)
         if self._graph is None:
             self._static_x = images.clone()
             self._static_y = labels.clone()
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             timer, self.timer = self.timer, None  # no event records inside the capture
-            if self.graph_side:
-                _lib.set_side_enabled(True)
-                _lib.set_side_capture(True)
             try:
                 with torch.cuda.graph(g):
                     loss, skip = self._forward_backward(self._static_x, self._static_y)
@@ -256,8 +243,6 @@ class TrainStep:
                     refresh_flipped()
             finally:
                 self.timer = timer
-                _lib.set_side_capture(False)
-                _lib.set_side_enabled(side_was)
             self._graph, self._static_loss = g, loss
         else:
             if images.data_ptr() != self._static_x.data_ptr():

@@ -9,8 +9,6 @@ Defaults (inception_v3_parameters): weight decay 4e-5 on conv+fc weights, conv s
 BN decay 0.9997 eps 1e-3 (biased moving variance - tf.nn.moments path), dropout keep 0.8.
 Returns (logits, aux_logits) in training mode; the trainer weights the aux loss by 0.4.
 """
-import os
-
 import torch
 
 from ..ops import nn as F
@@ -153,8 +151,7 @@ class InceptionV3Slim(Layer):
             if isinstance(op, Conv2d) and op.kh == 1 and op.kw == 1 and op.stride == 1 and op.bn is not None:
                 heads.append((op.weights, op.bn))
             elif (op == "avg3" and len(b) > 1 and isinstance(b[1], Conv2d) and b[1].kh == 1 and b[1].kw == 1 and
-                  b[1].stride == 1 and b[1].bn is not None and _fused.pool_commute_enabled() and
-                  os.environ.get("DTM_SIBLING_POOL", "1") != "0"):
+                  b[1].stride == 1 and b[1].bn is not None and _fused.pool_commute_enabled()):
                 heads.append((b[1].weights, None))
         return heads if len(heads) >= 2 else None
 

@@ -15,7 +15,6 @@ import math
 import torch
 import torch.nn as nn
 
-import os
 
 from ..ops import elementwise as E
 from ..ops import fused
@@ -24,7 +23,8 @@ from ..ops.lazy import as_tensor
 
 
 def fused_enabled():
-    return os.environ.get("DTM_FUSED_BN", "1") != "0"
+    from ..ops import features
+    return features.on("fused_bn")
 
 
 # ---------------------------------------------------------------------------------------------

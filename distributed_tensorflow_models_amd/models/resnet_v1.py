@@ -11,7 +11,6 @@ vgg/nets/resnet_utils.py:59-272:
 Variables: resnet_v1_50/conv1/weights, resnet_v1_50/conv1/BatchNorm/{gamma,beta,moving_*},
 resnet_v1_50/block1/unit_1/bottleneck_v1/{shortcut,conv1,conv2,conv3}/..., resnet_v1_50/logits/{weights,biases}.
 """
-import os
 
 import torch
 
@@ -66,23 +65,13 @@ class BottleneckV1(Layer):
                             conv2d_same_padding(3, stride, rate), "relu", bn, None, wd, init, rate=rate)
         self.conv3 = Conv2d(_join(scope, "conv3"), depth_bottleneck, depth, 1, 1, "SAME", None, bn, None, wd, init)
 
-    def sibling_heads(self):
-        """(weight, BatchNorm) of the projection shortcut and conv1 when they form a mergeable sibling pair (both 1x1
-        stride-1 conv+BNs of x; not the stage-1 64 -> 256 projection, which keeps its one-pass backward)."""
-        s = self.shortcut
-        if (s is None or s.stride != 1 or s.bn is None or self.conv1.bn is None or
-                (s.cout == 256 and s.cin == 64 and os.environ.get("DTM_BWD1X1_FUSE", "1") != "0")):
-            return None
-        return [(s.weights, s.bn), (self.conv1.weights, self.conv1.bn)]
-
     def forward(self, x, training=True, end_points=None):
         if self.shortcut is not None:
-            # projection shortcut and conv1: sibling 1x1 conv+BNs of x with one merged forward and backward (ops.fused)
-            # (the merged FORWARD is opt-in here, DTM_RESNET_SIBLING_FWD=1: the 512 + 128 -> 640-channel merged conv
-            # loses the 8-wave tile the 512-channel shortcut gets alone - ResNet-50 +0.41 % step with it,
-            # profiles/ab/r4_ab_fwd_dtile_resnet.log; the merged backward stays on)
-            heads = self.sibling_heads() if os.environ.get("DTM_RESNET_SIBLING_FWD", "0") == "1" else None
-            with fused.sibling_group(x, training and end_points is None, heads=heads):
+            # projection shortcut and conv1: sibling 1x1 conv+BNs of x with one merged backward (ops.fused).  (A merged
+            # FORWARD, as Inception's heads have, was measured +0.31..+0.41 % step here - the 512 + 128 -> 640-channel
+            # conv loses the 8-wave tile the 512-channel shortcut gets alone, profiles/ab/r4_ab_fwd_dtile_resnet.log,
+            # r4_ab_rfwd_resnet.log - and was removed.)
+            with fused.sibling_group(x, training and end_points is None):
                 sc = self.shortcut(x, training)
                 r1 = self.conv1(x, training)
         else:
@@ -154,11 +143,6 @@ BLOCKS = {
 
 
 class ResNetV1(Layer):
-    def sibling_weight_groups(self):
-        """Projection units' shortcut + conv1 weights: bf16 compute copies side by side in one buffer
-        (engine.prepare_compute_copies) for the merged forward."""
-        return [[w for w, _bn in h] for u in self.units for h in [u.sibling_heads()] if h]
-
     default_image_size = 224
 
     def __init__(self, depth=50, num_classes=1000, global_pool=True, spatial_squeeze=True, scope=None,

@@ -183,9 +183,9 @@ def stream_ptr():
 # the latter's tails and small launches leave idle.  The C++ side gives that stream its own scratch
 # arena (dtm_ws_set_side_stream).  The data-parallel layer launches bucket all-reduces from the side
 # stream after it has waited for the main one (parallel/bsp.py), and the engine joins the side stream
-# before the optimizer (side_join).  DTM_WGRAD_STREAM=0/1 (default 1) or set_side_enabled().  Measured
+# before the optimizer (side_join).  Feature wgrad_stream (ops/features.py; default on) or set_side_enabled().  Measured
 # (profiles/ab/r3_ab_wgrad_side_stream.log): ResNet-50 b256 step 18.02 -> 17.26 ms (-4.3 %).
-_side = {"stream": None, "on": None, "used": False, "capture": False}
+_side = {"stream": None, "on": None, "used": False}
 
 
 def set_side_enabled(on):
@@ -194,25 +194,18 @@ def set_side_enabled(on):
 
 def side_enabled():
     if _side["on"] is None:
-        _side["on"] = os.environ.get("DTM_WGRAD_STREAM", "1") == "1"
+        from . import features
+        _side["on"] = features.on("wgrad_stream")
     return _side["on"]
-
-
-def set_side_capture(on):
-    """Allow the side stream inside a hipGraph capture (engine.TrainStep graph_side_stream): the fork / join
-    become graph edges, so the captured weight gradients run beside the dgrad chain on replay.  The stream and
-    its scratch arena must already exist from eager steps (growth inside a capture is refused)."""
-    _side["capture"] = bool(on)
 
 
 def side_stream():
     """The weight-gradient side stream, or None when off / not on a GPU."""
     if not side_enabled() or not torch.cuda.is_available():
         return None
-    if torch.cuda.is_current_stream_capturing() and not _side["capture"]:
-        # captures are single-stream unless the engine opted in (set_side_capture): round 3's captured fork
-        # faulted on replay when a later, larger request reallocated a scratch arena the graph pointed into
-        # (arenas are now never freed and refuse growth inside a capture: csrc/kernels/workspace.hip)
+    if torch.cuda.is_current_stream_capturing():
+        # captured steps are single-stream: with the side stream inside the capture Inception-v3 ran 6.3 % slower
+        # (profiles/ab/r4_ab_graph_side_inception.log; that capture mode was removed in round 5)
         return None
     dev = torch.cuda.current_device()
     st = _side["stream"]
@@ -223,6 +216,7 @@ def side_stream():
     return st
 
 
+SIDE_CU_FRAC = 0.75
 _side_cu = {"frac": None}
 
 
@@ -231,12 +225,12 @@ def set_side_cu_fraction(frac):
 
 
 def side_cus():
-    """CU count the split-K policy of a side-stream weight gradient sizes its grid for (DTM_SIDE_CU_FRAC x the
-    device's CUs): the side stream shares the chip with the dgrad chain, so fewer splits mean fewer fp32
+    """CU count the split-K policy of a side-stream weight gradient sizes its grid for (SIDE_CU_FRAC x the
+    device's CUs; set_side_cu_fraction for A/B runs): the side stream shares the chip with the dgrad chain, so fewer splits mean fewer fp32
     partial slabs to write and reduce and fewer workgroups taken from the main stream.  Measured on ResNet-50
     (profiles/ab/r3_ab_side_cus.log, r3_ab_dgrp_bnst.log): 0.75 -1.0..-1.5 % step vs 1.0; 0.5 neutral; 0.35 +4 %."""
     if _side_cu["frac"] is None:
-        _side_cu["frac"] = float(os.environ.get("DTM_SIDE_CU_FRAC", "0.75"))
+        _side_cu["frac"] = SIDE_CU_FRAC
     return max(8, int(num_cus() * _side_cu["frac"]))
 
 
@@ -249,11 +243,11 @@ def set_wgrad_cu_percent(kind, pct):
 
 def wgrad_cus(kind="main"):
     """CU count the split-K policy of a main-stream weight gradient sizes its grid for: ``kind`` 'main' (every
-    conv wgrad not on the side stream; DTM_WGRAD_CU percent) or 'stem' (the packed-row stem's BN-fused wgrad,
-    the last kernel of the backward; DTM_STEM_WGRAD_CU percent)."""
+    conv wgrad not on the side stream) or 'stem' (the packed-row stem's BN-fused wgrad, the last kernel of the
+    backward): 100 % of the CUs unless set_wgrad_cu_percent (A/B runs: profiles/ab/r3_ab_wgrad_cus_*.log,
+    r3_ab_stem_wgrad_cus.log)."""
     if _wgrad_cu[kind] is None:
-        env = "DTM_STEM_WGRAD_CU" if kind == "stem" else "DTM_WGRAD_CU"
-        _wgrad_cu[kind] = float(os.environ.get(env, "100"))
+        _wgrad_cu[kind] = 100.0
     return max(8, int(num_cus() * _wgrad_cu[kind] / 100.0))
 
 

@@ -11,11 +11,10 @@ Each piece is an autograd Function with a hand-written backward kernel, so gradi
 exactly to TF's fused BatchNorm gradient (tests/test_fused_gpu.py checks it against torch).
 """
 import ctypes
-import os
 
 import torch
 
-from . import _lib
+from . import _lib, features
 from .geometry import conv_geom
 from .lazy import LazyBN, Subsampled, as_tensor  # noqa: F401
 from .nn import _accum_param_grad, _check, _notify, dgrad_decomposable, grad_target, weight_bf16, weight_flipped
@@ -95,15 +94,13 @@ BNOUT_FUSED = [0]  # count of block-output BN backwards absorbed by a dgrad epil
 
 
 def _bnout_enabled():
-    import os
-    return os.environ.get("DTM_BNOUT_FUSE", "1") != "0"
+    return features.on("bnout_fuse")
 
 
 def _bnout_strided():
-    """A/B knob DTM_BNOUT_STRIDED (default on): the dgrad-epilogue BN-apply backward also for the outputs of
-    stride-2 units (strided identity residual)."""
-    import os
-    return os.environ.get("DTM_BNOUT_STRIDED", "1") != "0"
+    """The dgrad-epilogue BN-apply backward also for the outputs of stride-2 units (strided identity residual):
+    part of feature bnout_fuse (profiles/ab/r3_ab_dgrp_bnst.log)."""
+    return features.on("bnout_fuse")
 
 
 def _slot_register(x):
@@ -422,8 +419,7 @@ BWD1X1_FUSED = [0]  # count of 1x1 conv+BN backwards done by the one-pass kernel
 def _bwd1x1_ok(ctx, g):
     """The one-pass 1x1 backward covers the ResNet 64 -> 256 channel shape (stage-1 expansion conv and
     projection shortcut)."""
-    import os
-    return (os.environ.get("DTM_BWD1X1_FUSE", "1") != "0" and g.R == 1 and g.S == 1 and g.stride == 1 and
+    return (features.on("bwd1x1_fuse") and g.R == 1 and g.S == 1 and g.stride == 1 and
             g.pad_h == 0 and g.pad_w == 0 and g.P == g.H and g.Q == g.W and g.K == 256 and g.C == 64 and
             ctx.needs_input_grad[0] and ctx.needs_input_grad[2])
 
@@ -622,9 +618,7 @@ class _StemConvBNFn(torch.autograd.Function):
         N, Hp, Wp, K, R, S, C, P, Q, st = ctx.d
         dy = dy.contiguous()
         dgamma = dbeta = None
-        import os
-        if (ss is not None and dss is not None and ctx.needs_input_grad[1] and
-                os.environ.get("DTM_STEM_WGRAD_FUSE", "1") != "0"):
+        if (ss is not None and dss is not None and ctx.needs_input_grad[1] and features.on("stem_wgrad_fuse")):
             # no input gradient: comb (the BN backward of dy) has the wgrad as its only reader, so it is
             # formed in the wgrad's operand staging instead of being written and read back
             gmg = grad_target(gamma) if gamma is not None else None
@@ -677,8 +671,7 @@ def _stem_eligible(x, w, stride, g):
     """The packed-row stem path: a plain (non-lazy) input without gradient, <= 4 channels, stride 2,
     S <= 7 taps per kernel row (S x 4 channels fit one 64-byte run), equal top / left pads (explicit,
     'VALID', or TF 'SAME'; the bottom / right zero fill comes from the packed buffer's extent)."""
-    import os
-    if os.environ.get("DTM_STEM", "1") == "0" or isinstance(x, (LazyBN, Subsampled)):
+    if isinstance(x, (LazyBN, Subsampled)):
         return False
     if not (x.is_cuda and x.dim() == 4 and w.dim() == 4) or x.requires_grad:
         return False
@@ -824,7 +817,7 @@ class _SiblingGroup:
         bmg = grad_target(beta) if (ss is not None and beta is not None) else None
         # every BN parameter gradient lands in main_grad: the members' combines are deferred to ONE grouped launch
         # at the last member (dgamma / dbeta written there, then reported); otherwise per member, now
-        grouped = (os.environ.get("DTM_SIBLING_COMBINE", "1") != "0" and len(grp.members) <= 8 and g.K % 8 == 0 and
+        grouped = (features.on("sibling_combine") and len(grp.members) <= 8 and g.K % 8 == 0 and
                    (gamma is None or gmg is not None) and (beta is None or bmg is not None))
         if grouped:
             dyc = dy.contiguous()
@@ -953,17 +946,16 @@ _SIBLINGS = [None]
 
 class sibling_group:
     """Context: the eligible 1x1 conv+BN calls on ``x`` inside it share one backward (see _SiblingGroup).
-    Knob DTM_SIBLING_GROUP (default on: Inception-v3 -4.8 %, ResNet-50 -0.24 % step on one GPU,
+    Feature sibling_group (default on: Inception-v3 -4.8 %, ResNet-50 -0.24 % step on one GPU,
     profiles/ab/r3_ab_sibling_*).  Data-parallel exactness: the step-1 and step-2 per-parameter gradients of 2 ranks
     equal the single-rank ones bit for bit (profiles/r4/r4_diag_resnet_sib_2steps.log, tests/test_distributed.py
     test_bsp_gpu_step1_gradients_match_single_rank); the round-3 2-rank mismatch no longer reproduces
     (profiles/r4/README.md)."""
 
     def __init__(self, x, training=True, heads=None):
-        import os
         on = (training and torch.is_grad_enabled() and isinstance(x, torch.Tensor) and x.is_cuda and
-              x.requires_grad and os.environ.get("DTM_SIBLING_GROUP", "1") != "0")
-        if heads is not None and (len(heads) < 2 or os.environ.get("DTM_SIBLING_FWD", "1") == "0"):
+              x.requires_grad and features.on("sibling_group"))
+        if heads is not None and (len(heads) < 2 or not features.on("sibling_fwd")):
             heads = None
         self.grp = _SiblingGroup(x, heads) if on else None
 
@@ -985,12 +977,17 @@ def _sibling_join(xb, w, g, training, bn, plain=False):
             g.pad_h or g.pad_w or g.P != g.H or g.Q != g.W or g.K % 8 or g.C % 8 or
             getattr(w, "main_grad", None) is None):
         return None
-    if g.K == 256 and g.C == 64 and os.environ.get("DTM_BWD1X1_FUSE", "1") != "0":
+    if g.K == 256 and g.C == 64 and features.on("bwd1x1_fuse"):
         return None  # (the ResNet stage-1 64 -> 256 projection keeps its one-pass backward, dtm_conv1x1_bnbwd)
     h = grp.join(w, g)
     if grp.heads is not None and len(grp.members) == 1 and not grp.forward_all(g, training):
         grp.heads = None  # (not a mergeable head set: per-member forwards)
     return h
+
+
+# How a conv consumes a LazyBN input (see _prologue_mode); None = the measured shape policy.  Tests and the A/B
+# tool pin a mode by setting this attribute (it is not an environment knob).
+PROLOGUE_MODE = None
 
 
 def _prologue_mode(x_shape, w_shape, stride):
@@ -1002,26 +999,21 @@ def _prologue_mode(x_shape, w_shape, stride):
     'mat'   - materialised once by a forward-only BN-apply pass (read raw + write bf16); the conv and its
               wgrad read it plainly, and the dgrad epilogue still does the activation backward from the
               raw tensor, so there is no backward pass for it;
-    'apply' - the autograd BN-apply (its own backward pass) - the pre-'mat' form, kept for A/B runs.
+    'apply' - the autograd BN-apply (its own backward pass).
     Measured per ResNet-50 layer (tools/conv_tile_sweep.py with WGRAD=1, batch 256): the prologue
     costs fwd +13..+66 us and wgrad +12..+68 us per layer, a materialising pass 6..35 us -> 'mat' wins
-    every conv except the stride-2 3x3 at 56x56, where it is neutral.
-    DTM_PROLOGUE = auto (default) | auto0 (auto without the expansion-1x1 rule) | fused | mat | apply | legacy."""
-    import os
-    mode = os.environ.get("DTM_PROLOGUE", "auto")
-    if mode in ("fused", "apply", "mat"):
-        return mode
+    every conv except the stride-2 3x3 at 56x56, where it is neutral (profiles/ab/r2_ab_prologue_fused_vs_mat.log),
+    and the stage-1 expansion 1x1, whose one-pass backward recomputes relu(bn(x)) from the raw x anyway
+    (profiles/ab/r2_ab_prologue_expand.log)."""
+    if PROLOGUE_MODE is not None:
+        return PROLOGUE_MODE
     _, H, W, _ = x_shape
     _, R, S, _ = w_shape
     st = stride if isinstance(stride, int) else stride[0]
-    if mode == "legacy":  # the previous policy: autograd apply for the stride-1 3x3 convs at <= 14x14
-        return "apply" if (R * S > 1 and st == 1 and H * W <= 14 * 14) else "fused"
     if st > 1 and H * W >= 56 * 56:
         return "fused"
     K, C = w_shape[0], w_shape[3]
-    if mode == "auto" and R * S == 1 and st == 1 and C == 64 and K == 256:
-        # the stage-1 expansion 1x1: its backward (dtm_conv1x1_bnbwd) recomputes relu(bn(x)) from the raw x
-        # anyway, so the materialised copy would only feed this forward (streaming kernel, prologue in LDS)
+    if R * S == 1 and st == 1 and C == 64 and K == 256:
         return "fused"
     return "mat"
 
@@ -1040,7 +1032,7 @@ def conv_bn(x, w, bn, stride, padding, training, relu):
             lz = x
             in_ss, in_unscaled, x = x.ss, x.unscaled, x.raw
             if (training and lz.unscaled and torch.is_grad_enabled() and x.requires_grad and x.is_cuda and
-                    os.environ.get("DTM_ACT_HANDOFF", "1") != "0"):
+                    features.on("act_handoff")):
                 # conv consumers of one activation hand the (unscaled, masked) input gradient on: the last one's
                 # act epilogue adds the others' before its mask and sums (Inception's split 1x3 / 3x1 pairs), so
                 # autograd adds neither the gradients nor the BN-gradient sums
@@ -1103,9 +1095,7 @@ class _BNStatsFn(torch.autograd.Function):
         C = y.shape[-1]
         if dstats is None:
             return dalias
-        import os
-        if (y.is_cuda and y.dtype == torch.bfloat16 and C % 8 == 0 and y.is_contiguous() and
-                os.environ.get("DTM_STATS_BWD", "1") != "0"):  # (A/B knob: 0 = the torch expression)
+        if y.is_cuda and y.dtype == torch.bfloat16 and C % 8 == 0 and y.is_contiguous():
             g = None
             if dalias is not None:
                 g = dalias.to(torch.bfloat16).contiguous()
@@ -1123,9 +1113,8 @@ class _BNStatsFn(torch.autograd.Function):
 
 
 def pool_commute_enabled():
-    """A/B knob DTM_POOL_COMMUTE (default on): Inception pool branches as conv -> avg_pool -> BN."""
-    import os
-    return os.environ.get("DTM_POOL_COMMUTE", "1") != "0"
+    """Feature pool_commute (default on): Inception pool branches as conv -> avg_pool -> BN."""
+    return features.on("pool_commute")
 
 
 def conv_avgpool_bn(x, w, bn, training, relu=True):
@@ -1139,8 +1128,7 @@ def conv_avgpool_bn(x, w, bn, training, relu=True):
     from .nn import avg_pool
     xb = as_tensor(x).to(torch.bfloat16).contiguous()
     g = conv_geom(tuple(xb.shape), tuple(w.shape), 1, "SAME")
-    grp = (_sibling_join(xb, w, g, training, None, plain=True)
-           if (xb is x and os.environ.get("DTM_SIBLING_POOL", "1") != "0") else None)
+    grp = _sibling_join(xb, w, g, training, None, plain=True) if xb is x else None
     slot = _slot_register(xb) if (xb is x and grp is None) else None
     z = _ConvBNFn.apply(xb, None, w, None, None, g, None, slot, False, None, grp)
     y = avg_pool(z, 3, 1, "SAME")
@@ -1283,11 +1271,9 @@ def _part_index(meta):
 
 
 def _cat_multi():
-    """A/B knob DTM_CAT_MULTI: 1 (default) = the one-launch multi-part concat BN-apply, plain tensor parts
-    included; 2 = only for concats of BN'd parts; 0 = one launch per part."""
-    import os
-    v = os.environ.get("DTM_CAT_MULTI", "1")
-    return int(v) if v in ("0", "1", "2") else 1
+    """Feature cat_multi: 1 (default) = the one-launch multi-part concat BN-apply, plain tensor parts included;
+    0 = one launch per part."""
+    return 1 if features.on("cat_multi") else 0
 
 
 def concat_channels(parts):

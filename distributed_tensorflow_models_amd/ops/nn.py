@@ -11,7 +11,6 @@ data-parallel engine can launch a bucket's all-reduce while backward continues.
 """
 import ctypes
 
-import os
 
 import torch
 
@@ -135,9 +134,8 @@ FLIP_REGISTRY = {}   # (id(param), dec) -> (param, wt buffer, dec)
 
 def dgrad_decomposable(g):
     """A stride > 1 dgrad runs as one stride-1 conv per output parity class (ConvDesc.dec, the
-    decomposed flipped weight) when every class has taps (R, S >= stride).  DTM_DGRAD_DEC=0: off."""
-    import os
-    return g.stride > 1 and g.R >= g.stride and g.S >= g.stride and os.environ.get("DTM_DGRAD_DEC", "1") != "0"
+    decomposed flipped weight) when every class has taps (R, S >= stride)."""
+    return g.stride > 1 and g.R >= g.stride and g.S >= g.stride
 
 
 def weight_flipped(w, K, R, S, C, dec=None):
@@ -268,12 +266,11 @@ class _Conv2dFn(torch.autograd.Function):
 
 
 _UNIT_SS = {}
-_RELU_BIAS_FUSE = os.environ.get("DTM_RELU_BIAS_FUSE", "1") != "0"  # A/B knob (tools/ab_step.py)
 
 
 def _relu_bias_bwd_ok(dy):
     K = dy.shape[-1]
-    return _RELU_BIAS_FUSE and dy.dtype == torch.bfloat16 and K % 8 == 0 and K // 8 <= 256 and dy.numel() // K < (1 << 31)
+    return dy.dtype == torch.bfloat16 and K % 8 == 0 and K // 8 <= 256 and dy.numel() // K < (1 << 31)
 
 
 def _relu_bias_bwd(dy, y):
@@ -843,7 +840,7 @@ class _LinearHipFn(torch.autograd.Function):
 
 
 class _LinearFn(torch.autograd.Function):
-    """hipBLASLt fallback (input width not a multiple of 8, or DTM_FC_BLAS=1 for A/B runs)."""
+    """hipBLASLt fallback (input width not a multiple of 8)."""
     @staticmethod
     def forward(ctx, x, w, b, relu):
         w16 = weight_bf16(w)
@@ -887,7 +884,6 @@ def linear(x, w, b=None, relu=False):
         if b is not None:
             y = y + b
         return torch.relu(y) if relu else y
-    import os
-    if w.shape[0] % 8 == 0 and x.dim() == 2 and os.environ.get("DTM_FC_BLAS", "0") != "1":
+    if w.shape[0] % 8 == 0 and x.dim() == 2:
         return _LinearHipFn.apply(x, w, b, bool(relu))
     return _LinearFn.apply(x, w, b, bool(relu))

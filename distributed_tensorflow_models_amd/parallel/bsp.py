@@ -64,8 +64,9 @@ class BSPDataParallel:
         # the LAST bucket of backward is the exposed one (nothing is left to overlap it): keep it small
         self.tail = max(0, int(tail_mb * (1 << 20) / self.flat.element_size()))
         # param -> live-tap window (r0, r1, s0, s1): compact bucket (windows announced to an earlier
-        # instance are remembered on the parameter).  DTM_BSP_COMPACT=0 turns compaction off (A/B).
-        self._compact_on = os.environ.get("DTM_BSP_COMPACT", "1") != "0"
+        # instance are remembered on the parameter).  Feature bsp_compact (ops/features.py; off: DTM_DISABLE).
+        from ..ops import features
+        self._compact_on = features.on("bsp_compact")
         self.windows = {p: p._live_win for p in self.params
                         if self._compact_on and getattr(p, "_live_win", None) is not None and p.dim() == 4}
         self._works = []

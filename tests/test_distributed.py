@@ -167,41 +167,49 @@ def test_bsp_gpu_two_ranks_hip_kernels_match_single_rank():
     assert two[0]["losses"] == pytest.approx(single["losses"], rel=1e-4)
 
 
-# Step-1 gradients of every BASELINE data-parallel model, per parameter, W = 2 ranks (same batch) vs 1 rank,
-# over the gradient-routing knobs: deterministic reductions make a correct run bit-exact, the BSP write
-# checker (DTM_BSP_CHECK) raises on a gradient written after its bucket's all-reduce was issued.
-_DP_MATRIX = [
-    ("resnet_v1_50", {}),
-    ("resnet_v1_50", {"DTM_WGRAD_STREAM": "0"}),
-    ("resnet_v1_50", {"DTM_RESNET_SIBLING_FWD": "1"}),
-    ("resnet_v1_50", {"DTM_SIBLING_GROUP": "0"}),
-    ("inception_v3_slim_old", {}),
-    ("inception_v3_slim_old", {"DTM_SIBLING_FWD": "0", "DTM_SIBLING_COMBINE": "0"}),
-    ("inception_v3_slim_old", {"DTM_SIBLING_GROUP": "0", "DTM_ACT_HANDOFF": "0"}),
-    ("inception_v3_slim_old", {"DTM_WGRAD_STREAM": "0"}),
-    ("vgg_16", {}),
-    ("vgg_16", {"DTM_WGRAD_STREAM": "0"}),
-]
+# Step-1 gradients of every BASELINE data-parallel model, per parameter, W = 2 ranks each on ITS OWN batch vs the
+# mean of the two single-rank gradients, over the gradient-routing fused paths (ops/features.py ROUTES_GRADIENTS,
+# each switched off on its own): deterministic reductions make a correct run bit-exact, the BSP write checker
+# (DTM_BSP_CHECK) raises on a gradient written after its bucket's all-reduce was issued.
+_DP_MATRIX = [("resnet_v1_50", ())] + [("resnet_v1_50", (f,)) for f in (
+    "fused_bn", "sibling_group", "bnout_fuse", "bwd1x1_fuse", "stem_wgrad_fuse", "wgrad_stream")] + [
+    ("inception_v3_slim_old", ())] + [("inception_v3_slim_old", (f,)) for f in (
+        "sibling_fwd", "sibling_combine", "sibling_group", "act_handoff", "cat_multi", "pool_commute",
+        "wgrad_stream")] + [
+    ("vgg_16", ()), ("vgg_16", ("wgrad_stream",)), ("vgg_16", ("bsp_compact",))]
 
 
-# the driver's GPU suite runs the default configs; DTM_DP_MATRIX=1 runs every knob combination
+def test_dp_matrix_covers_every_gradient_routing_feature():
+    from distributed_tensorflow_models_amd.ops import features
+    covered = {f for _m, fs in _DP_MATRIX for f in fs}
+    assert covered == set(features.ROUTES_GRADIENTS), set(features.ROUTES_GRADIENTS) ^ covered
+
+
+# the driver's GPU suite runs the default configs; DTM_DP_MATRIX=1 runs every row
 _DP_RUN = _DP_MATRIX if os.environ.get("DTM_DP_MATRIX") == "1" else [c for c in _DP_MATRIX if not c[1]]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("model,knobs", _DP_RUN, ids=lambda v: v if isinstance(v, str) else
-                         ("-".join("%s%s" % (k[4:].lower(), x) for k, x in v.items()) or "defaults"))
-def test_bsp_gpu_step1_gradients_match_single_rank(model, knobs):
-    """Per-parameter step-1 gradients of 2 ranks (the same batch) vs the single-rank run (computed inside the same
-    2-rank job in a singleton group), deterministic reductions, BSP write checker on."""
+@pytest.mark.parametrize("model,off", _DP_RUN, ids=lambda v: v if isinstance(v, str) else
+                         ("no-" + "-".join(v) if v else "defaults"))
+def test_bsp_gpu_step1_gradients_match_single_rank(model, off):
+    """Per-parameter step-1 gradients of 2 ranks, rank r on its own batch b_r, vs the mean over r of the single-rank
+    gradient on b_r (each computed inside the same 2-rank job in a singleton group), deterministic reductions, BSP
+    write checker on.  Distinct batches: a permuted, offset or dropped contribution of one rank cannot hide."""
+    from distributed_tensorflow_models_amd.ops import features
     from distributed_tensorflow_models_amd.utils import dp_check
-    res = run_workers(dp_check.grad_worker_pair, 2, model, knobs)
-    single, two = res[0]["single"], [r["multi"] for r in res]
+    res = run_workers(dp_check.grad_worker_pair, 2, model, features.disable_env(off) if off else None)
+    two = [r["multi"] for r in res]
+    ref = dp_check.mean_grads([r["single"] for r in res])
     assert two[0]["launched"] == two[0]["buckets"] > 1 and two[0]["writes_checked"] > 0
     if model == "vgg_16":
-        assert two[0]["compact"] == 1  # fc6's live window travels alone
-    rows = dp_check.compare(two[0], single)
+        assert two[0]["compact"] == (0 if "bsp_compact" in off else 1)  # fc6's live window travels alone
+    # the two ranks' own gradients differ (distinct batches), so the check can see a mixed-up contribution
+    d01 = dp_check.compare(res[0]["single"], res[1]["single"])
+    assert sorted(r[1] for r in d01)[len(d01) // 2] > 1e-3
+    rows = dp_check.compare(two[0], ref)
     bad = [r for r in rows if r[1] > 1e-5]
+    print("%s %s: %d tensors, max rel err %.3g" % (model, off or "defaults", len(rows), max(r[1] for r in rows)))
     assert not bad, (len(bad), len(rows), bad[:6])
     assert torch.equal(two[0]["params"], two[1]["params"])
 
@@ -406,7 +414,7 @@ class _DeadTapNet(torch.nn.Module):
 
 
 def _dead_tap_worker(rank, world, compact):
-    os.environ["DTM_BSP_COMPACT"] = "1" if compact else "0"
+    os.environ["DTM_DISABLE"] = "" if compact else "bsp_compact"
     from distributed_tensorflow_models_amd.engine import TrainStep
     torch.manual_seed(0)
     model = _DeadTapNet()

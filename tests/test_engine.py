@@ -71,7 +71,7 @@ def test_nan_guard_skips_update_gpu():
     assert all(torch.equal(a, p.detach()) for a, p in zip(before, m.parameters()))
 
 
-def _run_steps(name, use_graph, steps, size, ncls, opt="momentum", ema=None, sched=None, lr=0.05, graph_side=False,
+def _run_steps(name, use_graph, steps, size, ncls, opt="momentum", ema=None, sched=None, lr=0.05,
                reset_seed=False, wgrad_stream=None, **kw):
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
@@ -81,7 +81,7 @@ def _run_steps(name, use_graph, steps, size, ncls, opt="momentum", ema=None, sch
         E.set_base_seed(1234)
     model = nets_factory.build(name, num_classes=ncls, **kw).to(dev)
     step = TrainStep(model, optimizer=opt, lr=lr, momentum=0.9, use_graph=use_graph, ema_decay=ema,
-                     lr_schedule=sched, graph_side_stream=graph_side, wgrad_stream=wgrad_stream)
+                     lr_schedule=sched, wgrad_stream=wgrad_stream)
     g = torch.Generator().manual_seed(3)
     cin = 1 if name == "lenet" else 3
     xs = [torch.randn(4, size, size, cin, generator=g).to(dev, torch.bfloat16) for _ in range(2)]
@@ -95,15 +95,14 @@ def _run_steps(name, use_graph, steps, size, ncls, opt="momentum", ema=None, sch
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,size,ncls,side", [("resnet_v1_50", 64, 16, False), ("cifar10_cnn", 24, 10, False),
-                                                 ("resnet_v1_50", 64, 16, True)])
-def test_hipgraph_step_matches_eager(name, size, ncls, side):
+@pytest.mark.parametrize("name,size,ncls", [("resnet_v1_50", 64, 16), ("cifar10_cnn", 24, 10)])
+def test_hipgraph_step_matches_eager(name, size, ncls):
     """Captured-and-replayed steps (alternating input buffers, lr schedule and EMA decay staged per
-    replay) follow the eager trajectory; ``side``: the weight gradients captured on the side stream
-    (fork / join as graph edges)."""
+    replay) follow the eager trajectory (a captured step is single-stream: the weight-gradient side stream is
+    left out of captures, ops/_lib.py side_stream)."""
     sched = lambda s: 0.05 * (0.5 ** (s // 3))  # noqa: E731
     le, pe, ee, _ = _run_steps(name, False, 6, size, ncls, ema=0.99, sched=sched, reset_seed=True)
-    lg, pg_, eg, st = _run_steps(name, True, 6, size, ncls, ema=0.99, sched=sched, graph_side=side, reset_seed=True)
+    lg, pg_, eg, st = _run_steps(name, True, 6, size, ncls, ema=0.99, sched=sched, reset_seed=True)
     assert st._graph is not None and st.global_step == 6 and st.opt.num_updates == 6
     assert lg == pytest.approx(le, rel=2e-2, abs=2e-3)
     # BN statistics are summed with fp32 atomics, so two runs are not bit-identical, and the 2x2
@@ -113,23 +112,20 @@ def test_hipgraph_step_matches_eager(name, size, ncls, side):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("side", [False, True])
-def test_hipgraph_inception_bit_exact_vs_eager(side):
+def test_hipgraph_inception_bit_exact_vs_eager():
     """Inception-v3 (299, batch 4: the aux head, merged sibling heads, dropout, concat BN) in deterministic mode:
-    the captured step - with the weight gradients on the side stream or not - replays the eager trajectory bit for
-    bit (a random-init Inception at batch 4 is chaotic enough that fp32-atomic reductions alone make two eager runs
+    the captured step replays the eager trajectory bit for bit (a random-init Inception at batch 4 is chaotic enough that fp32-atomic reductions alone make two eager runs
     drift apart, so the comparison is made where every reduction has a fixed order)."""
     from distributed_tensorflow_models_amd.ops import _lib
     _lib.set_deterministic(True)
     side_was = _lib.side_enabled()
     try:
-        # the eager run routes the weight gradients like the captured one (the side stream's split-K sizing
-        # differs from the main stream's: another summation order); no dropout (an eager step draws a new host
-        # seed per step, a replayed graph keeps the captured one and advances the device offset)
+        # the eager run routes the weight gradients like the captured one (main stream: the side stream's split-K
+        # sizing differs, another summation order); no dropout (an eager step draws a new host seed per step, a
+        # replayed graph keeps the captured one and advances the device offset)
         kw = dict(lr=0.005, reset_seed=True, dropout_keep_prob=1.0)
-        le, pe, _, _ = _run_steps("inception_v3_slim_old", False, 5, 299, 11, wgrad_stream=side, **kw)
-        lg, pg_, _, st = _run_steps("inception_v3_slim_old", True, 5, 299, 11, graph_side=side, wgrad_stream=False,
-                                    **kw)
+        le, pe, _, _ = _run_steps("inception_v3_slim_old", False, 5, 299, 11, wgrad_stream=False, **kw)
+        lg, pg_, _, st = _run_steps("inception_v3_slim_old", True, 5, 299, 11, wgrad_stream=False, **kw)
     finally:
         _lib.set_deterministic(False)
         _lib.set_side_enabled(side_was)

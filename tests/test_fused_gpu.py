@@ -6,6 +6,7 @@ import pytest
 import torch
 
 from distributed_tensorflow_models_amd.models.resnet_v1 import ResNetV1
+from distributed_tensorflow_models_amd.ops import features, fused
 
 pytestmark = pytest.mark.gpu
 
@@ -18,8 +19,8 @@ def _rel(a, b):
 @pytest.mark.parametrize("fused,prologue", [("1", "auto"), ("1", "fused"), ("1", "apply"), ("0", "auto")])
 @pytest.mark.parametrize("base,batch", [(16, 16), (16, 32)])
 def test_small_resnet_matches_reference(fused, prologue, base, batch, monkeypatch):
-    monkeypatch.setenv("DTM_FUSED_BN", fused)
-    monkeypatch.setenv("DTM_PROLOGUE", prologue)
+    monkeypatch.setitem(features._override, "fused_bn", (fused) != "0")
+    monkeypatch.setattr(fused, "PROLOGUE_MODE", None if prologue == "auto" else prologue)
     torch.manual_seed(0)
     net_cpu = ResNetV1(blocks=[(base, 2, 2), (2 * base, 2, 1)], num_classes=10, scope="r")
     net_gpu = copy.deepcopy(net_cpu).cuda()

@@ -5,6 +5,7 @@ import torch
 from distributed_tensorflow_models_amd.ops import fused
 from distributed_tensorflow_models_amd.ops import reference as ref
 from distributed_tensorflow_models_amd.models.layers import BatchNorm
+from distributed_tensorflow_models_amd.ops import features
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -351,7 +352,7 @@ def test_stem_packed_row_conv_bn(monkeypatch, H, W, C, N, R, pad, stemw):
     weight/gamma/beta grads; the BN backward either as a stats-combine pass or inside the wgrad operand
     staging (stemw=1)."""
     from distributed_tensorflow_models_amd.ops.geometry import conv_geom
-    monkeypatch.setenv("DTM_STEM_WGRAD_FUSE", stemw)
+    monkeypatch.setitem(features._override, "stem_wgrad_fuse", (stemw) != "0")
     torch.manual_seed(0)
     x = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16)
     w = (torch.randn(64, R, R, C, device=DEV) / (R * R * C) ** 0.5).to(torch.bfloat16).float()
@@ -464,9 +465,9 @@ def test_sibling_1x1_merged_backward(monkeypatch, side, model, S, B, merged, las
     y = torch.randint(0, 11, (B,), device=DEV)
     grads = {}
     try:
-        monkeypatch.setenv("DTM_SIBLING_FWD", "0")  # (the merged forward has its own test)
+        monkeypatch.setitem(features._override, "sibling_fwd", False)  # (the merged forward has its own test)
         for grp in ("0", "1"):
-            monkeypatch.setenv("DTM_SIBLING_GROUP", grp)
+            monkeypatch.setitem(features._override, "sibling_group", (grp) != "0")
             n0 = fused.SIBLING_MERGED[0]
             step._forward_backward(x, y)
             torch.cuda.synchronize()
@@ -501,7 +502,7 @@ def test_sibling_grouped_stats_combine_bit_exact(monkeypatch, model, S, B):
     from distributed_tensorflow_models_amd.ops import elementwise as ew
     monkeypatch.setattr(ew, "advance_seed_offset", lambda device: None)
     monkeypatch.setattr(ew, "next_seed", lambda: 1234)
-    monkeypatch.setenv("DTM_SIBLING_GROUP", "1")
+    monkeypatch.setitem(features._override, "sibling_group", True)
     _lib.lib().dtm_set_deterministic(1)
     try:
         torch.manual_seed(0)
@@ -511,7 +512,7 @@ def test_sibling_grouped_stats_combine_bit_exact(monkeypatch, model, S, B):
         y = torch.randint(0, 11, (B,), device=DEV)
         grads = {}
         for comb in ("1", "0"):
-            monkeypatch.setenv("DTM_SIBLING_COMBINE", comb)
+            monkeypatch.setitem(features._override, "sibling_combine", (comb) != "0")
             step._forward_backward(x, y)
             torch.cuda.synchronize()
             grads[comb] = {k: p.main_grad.detach().clone() for k, p in net.named_parameters()
@@ -522,16 +523,16 @@ def test_sibling_grouped_stats_combine_bit_exact(monkeypatch, model, S, B):
         _lib.lib().dtm_set_deterministic(0)
 
 
-@pytest.mark.parametrize("model,S,B,nmerged,block", [("inception_v3_slim_old", 299, 4, 10, "mixed_35x35x256a"),
-                                                     ("resnet_v1_50", 64, 4, 3, None)])
+@pytest.mark.parametrize("model,S,B,nmerged,block", [("inception_v3_slim_old", 299, 4, 10, "mixed_35x35x256a")])
 def test_sibling_merged_head_forward(monkeypatch, model, S, B, nmerged, block):
-    """Inception-v3 mixed blocks' branch-head 1x1 conv+BNs (and the commuted pool-branch conv), ResNet-50 projection
-    units' shortcut + conv1, as ONE conv over their concatenated bf16 weights (one buffer,
+    """Inception-v3 mixed blocks' branch-head 1x1 conv+BNs (and the commuted pool-branch conv) as ONE conv over their concatenated bf16 weights (one buffer,
     engine.prepare_compute_copies) writing each member's own output plus ONE finalize (dtm_conv_fwd_bn_multi), vs
     one conv + finalize per head.  The conv outputs are bit-identical (test_kernels_gpu.py
     test_conv_fwd_bn_multi_matches_separate); the BatchNorm statistics are summed over other partial rows, so the
     two forwards differ in the last bits of the statistics.  Through a whole random-init Inception-v3 at batch 4 that
-    difference grows into O(1) gradient differences near the stem (profiles/r4/r4_diag_sibfwd_wholenet_b4.log), so
+    difference grows into O(1) gradient differences near the stem (profiles/r4/r4_diag_sibfwd_wholenet_b4.log; the
+    random-init network's gradient is chaotic, profiles/r5/r5_grad_sensitivity_inception_b16.log - the whole-model
+    checks are tests/test_trajectory_inception_gpu.py), so
     Inception is compared where it is not amplified: a fixed gradient backpropagated from the first mixed block's
     output (its merged group's forward and backward, the stem below it).  Per block of depth the statistics-order
     drift grows ~4x (block 1: its parameters' gradients median 8e-5 / max 9e-3, block 2: ~4e-2, block 4: ~0.13 -
@@ -543,7 +544,6 @@ def test_sibling_merged_head_forward(monkeypatch, model, S, B, nmerged, block):
     from distributed_tensorflow_models_amd.ops import elementwise as ew
     monkeypatch.setattr(ew, "advance_seed_offset", lambda device: None)
     monkeypatch.setattr(ew, "next_seed", lambda: 1234)
-    monkeypatch.setenv("DTM_RESNET_SIBLING_FWD", "1")  # (opt-in for ResNet-50: measured +0.41 % step)
     _lib.lib().dtm_set_deterministic(1)
     try:
         torch.manual_seed(0)
@@ -555,7 +555,7 @@ def test_sibling_merged_head_forward(monkeypatch, model, S, B, nmerged, block):
         init = [b.detach().clone() for b in moving_average_buffers(net)]
         out = {}
         for run in ("0", "1", "1b"):
-            monkeypatch.setenv("DTM_SIBLING_FWD", run[0])
+            monkeypatch.setitem(features._override, "sibling_fwd", (run[0]) != "0")
             with torch.no_grad():
                 for b, v in zip(moving_average_buffers(net), init):
                     b.copy_(v)
@@ -600,16 +600,6 @@ def test_sibling_merged_head_forward(monkeypatch, model, S, B, nmerged, block):
         body = [(v, k) for v, k in errs if not (k.endswith("bn.beta") and k.startswith("layers.conv"))]
         assert body[len(body) // 2][0] < 1e-2 and body[-1][0] < 5e-2, body[-5:]
         return
-    # ResNet-50 (64x64, batch 4; its merged forward is opt-in): the whole model - its units pass no end points to the
-    # merged path - so only forward-side quantities: loss, moving statistics (scale-free: max |diff| over max |value|)
-    # and the logits weights' gradient; the per-parameter gradients deeper in drift with the statistics order as in
-    # the Inception whole-net diagnostics (a median of 0.73 once the merged conv moved to the 128x128 tile), and the
-    # merged kernel itself is compared on the projection shapes in test_conv_fwd_bn_multi_matches_separate
-    mv = max(float((a - b).abs().max() / b.abs().max().clamp_min(1e-12)) for a, b in zip(out["1"][1], out["0"][1]))
-    errs = sorted((_rel(out["1"][2][k], out["0"][2][k]), k) for k in out["0"][2])
-    logit = max(v for v, k in errs if (k.startswith("fc.") or "logits" in k) and "aux" not in k)
-    assert abs(out["1"][0] - out["0"][0]) < 1e-2 * abs(out["0"][0]), (out["1"][0], out["0"][0])
-    assert mv < 1e-1 and logit < 1e-1, (mv, logit, errs[-5:])
 
 
 def test_act_input_handoff_between_conv_consumers(monkeypatch):
@@ -626,7 +616,7 @@ def test_act_input_handoff_between_conv_consumers(monkeypatch):
     ga = gb = None
     out = {}
     for on in ("0", "1"):
-        monkeypatch.setenv("DTM_ACT_HANDOFF", on)
+        monkeypatch.setitem(features._override, "act_handoff", (on) != "0")
         for p in (bn1.gamma, bn1.beta):
             p.grad = None
         xk = x.to(torch.bfloat16).requires_grad_()
@@ -656,7 +646,7 @@ def test_block_output_bn_backward_in_dgrad_epilogue(monkeypatch):
     from distributed_tensorflow_models_amd.ops import nn as F
     grads = {}
     for fuse in ("0", "1"):
-        monkeypatch.setenv("DTM_BNOUT_FUSE", fuse)
+        monkeypatch.setitem(features._override, "bnout_fuse", (fuse) != "0")
         for p in net.parameters():
             p.grad = None
         n0 = fused.BNOUT_FUSED[0]
@@ -696,7 +686,7 @@ def test_conv1x1_bn_backward_one_pass(monkeypatch, N, H, relu):
     gy = None
     res = {}
     for fuse in ("0", "1"):
-        monkeypatch.setenv("DTM_BWD1X1_FUSE", fuse)
+        monkeypatch.setitem(features._override, "bwd1x1_fuse", (fuse) != "0")
         for b in (bn1, bn2):
             for p in b.parameters():
                 p.grad = None
@@ -744,7 +734,7 @@ def test_conv1x1_bn_backward_one_pass_plain_input(monkeypatch):
     y = torch.randint(0, 10, (4,), device=DEV)
     grads, counts = {}, {}
     for fuse in ("0", "1"):
-        monkeypatch.setenv("DTM_BWD1X1_FUSE", fuse)
+        monkeypatch.setitem(features._override, "bwd1x1_fuse", (fuse) != "0")
         for p in net.parameters():
             p.grad = None
         n0 = fused.BWD1X1_FUSED[0]

@@ -30,6 +30,7 @@ import sys
 import numpy as np
 import pytest
 import torch
+from distributed_tensorflow_models_amd.ops import features
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -44,7 +45,7 @@ def _fixture():
 
 def _trajectory(monkeypatch, sib_fwd):
     T = _fixture()
-    monkeypatch.setenv("DTM_SIBLING_FWD", sib_fwd)
+    monkeypatch.setitem(features._override, "sibling_fwd", (sib_fwd) != "0")
     net = T.build().to(DEV)
     tr = T.tracked(net)
     w0 = {k: v.detach().clone() for k, (v, _i) in tr.items()}
@@ -114,7 +115,7 @@ def _pct(v):
 def _grads(monkeypatch, net, step, x, y, sib_fwd, det, init):
     from distributed_tensorflow_models_amd.engine import moving_average_buffers
     from distributed_tensorflow_models_amd.ops import _lib
-    monkeypatch.setenv("DTM_SIBLING_FWD", sib_fwd)
+    monkeypatch.setitem(features._override, "sibling_fwd", (sib_fwd) != "0")
     _lib.lib().dtm_set_deterministic(int(det))
     try:
         with torch.no_grad():
@@ -183,7 +184,7 @@ _SEGMENT_EPS = ("pool2", "mixed_35x35x256a", "mixed_35x35x288a", "mixed_35x35x28
 
 def _gpu_step_with_taps(monkeypatch, sib_fwd):
     T = _fixture()
-    monkeypatch.setenv("DTM_SIBLING_FWD", sib_fwd)
+    monkeypatch.setitem(features._override, "sibling_fwd", (sib_fwd) != "0")
     net = T.build().to(DEV)
     step = T.make_step(net)
     x, y = T.batches()[0]

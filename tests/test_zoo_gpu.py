@@ -10,6 +10,7 @@ from distributed_tensorflow_models_amd.compat import slim
 from distributed_tensorflow_models_amd.models import gans, nets_factory
 from distributed_tensorflow_models_amd.ops import nn as dnn
 from distributed_tensorflow_models_amd.ops import reference as ref
+from distributed_tensorflow_models_amd.ops import features
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -204,7 +205,7 @@ def test_zero_copy_concat_one_launch(monkeypatch, Cs):
     dout = torch.randn(N, H, W, sum(Cs), device=DEV).to(torch.bfloat16)
     outs = []
     for mode in ("multi", "parts", "cat"):
-        monkeypatch.setenv("DTM_CAT_MULTI", "0" if mode == "parts" else "1")
+        monkeypatch.setitem(features._override, "cat_multi", mode != "parts")
         rs = [r.clone().requires_grad_() for r in raws]
         ss = [x.clone().requires_grad_() for x in sss]
         lz = [LazyBN(r, s, True, unscaled=(i % 2 == 0)) for i, (r, s) in enumerate(zip(rs, ss))]

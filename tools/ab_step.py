@@ -3,14 +3,20 @@
 median ms/step per variant; one device, one process: MI355X_MICROARCH 'DVFS give-back' / rule 24).
 
 VARIANTS="base=;noW=wtile:-3;noT=tile:-3;fused=prologue:fused" python tools/ab_step.py
-keys: tile (conv_nt tile id), w8 (0/1: the 8-wave 256x256 conv tile in the shape policy), kwide (0/1: 64-channel tiles for K % 128 <= 64), few (0/1: streaming few-row slab reduction), bnout (0/1: block-output BN backward in the consuming dgrad's epilogue), bnst (0/1: also for stride-2 unit outputs), b1x1 (0/1: one-pass 1x1 conv+BN backward), stemw (0/1: stem BN backward in the wgrad operand staging), sact (0/1: streaming 1x1 kernel for act dgrads), pcom (0/1: Inception pool branches as conv -> pool -> BN), sib (0/1: merged backward of sibling 1x1 convs), ahand (0/1: input-gradient hand-off between conv consumers of one activation), sibp (0/1: the commuted pool-branch conv joins the sibling group), sbwd (0/1: HIP backward of the pooled-BN statistics), catm (0/1: one-launch multi-part concat BN-apply), dec (0/1: stride-decomposed strided dgrads), dgrp (0/1: their parity classes as one grouped launch), k32 (0/1: 256x32 tile for <=32-channel spatial convs), cpt (16-B chunks per thread of the BN-stream grids), pol2 (0/1: v2 conv tile-policy rules), sstr (0/1/2: the stem forward as a persistent stream, 3- / 2-slot ring), wgs (0/1: conv+BN weight gradients on a side stream), scu (percent of the CUs the side-stream wgrads size their split-K grid for), wcu / swc (the same for the main-stream / stem wgrads), dir3 (0/1: direct 3x3 kernel for C in {32, 64}), atile (tile id of the dgrads with a fused
-activation-backward epilogue, -1 = policy), rsv (CUs reserved from the compute grids' sizing), sfwd (0/1: merged sibling-head forward), rfwd (0/1: also for ResNet projection units), scomb (0/1: grouped sibling
-stats-combine), lpt (0/1: grouped parity classes of strided dgrads in descending tap
-count), dtile (0/1: grouped strided-dgrad tile chosen for the whole grouped grid), stile (0/1: merged-head convs on the pipelined 128x128 tile), hog (blocks:ms - a
-CU-occupying copy kernel on another stream from every backward start, standing in for RCCL channels), wtile[:occ] (wgrad tile id / blocks-per-CU target), prologue (DTM_PROLOGUE),
-stem (DTM_STEM: 1 = packed-row stem path), red (target_blocks:max_chunks[:direct_max] of the
-partial-sum reductions; 0 = legacy 256 rows per block; direct_max = largest BN-backward grid that
-reduces with atomics in the producer instead of a reduce launch)."""
+keys: tile (conv_nt tile id), w8 (0/1: the 8-wave 256x256 conv tile in the shape policy), kwide (0/1: 64-channel
+tiles for K % 128 <= 64), few (0/1: streaming few-row slab reduction), sact (0/1: streaming 1x1 kernel for act
+dgrads), k32 (0/1: 256x32 tile for <=32-channel spatial convs), cpt (16-B chunks per thread of the BN-stream grids),
+pol2 (0/1: v2 conv tile-policy rules), sstr (0/1/2: the stem forward as a persistent stream, 3- / 2-slot ring), wgs
+(0/1: conv+BN weight gradients on a side stream), scu (percent of the CUs the side-stream wgrads size their split-K
+grid for), wcu / swc (the same for the main-stream / stem wgrads), dir3 (0/1: direct 3x3 kernel for C in {32, 64}),
+dgrp (0/1: strided-dgrad parity classes as one grouped launch), atile (tile id of the dgrads with a fused
+activation-backward epilogue, -1 = policy), rsv (CUs reserved from the compute grids' sizing), lpt (0/1: grouped
+parity classes in descending tap count), dtile (0/1: grouped strided-dgrad tile chosen for the whole grouped grid),
+stile (0/1: merged-head convs on the pipelined 128x128 tile), hog (blocks:ms - a CU-occupying copy kernel on another
+stream from every backward start, standing in for RCCL channels), wtile[:occ] (wgrad tile id / blocks-per-CU target),
+prologue (auto | fused | mat | apply: ops/fused.py PROLOGUE_MODE), red (target_blocks:max_chunks[:direct_max] of the
+partial-sum reductions), off (name+name: fused-path features of ops/features.py switched off, e.g.
+off:sibling_fwd+act_handoff)."""
 import os
 import statistics
 import sys
@@ -21,7 +27,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_tensorflow_models_amd.engine import TrainStep  # noqa: E402
 from distributed_tensorflow_models_amd.models import nets_factory  # noqa: E402
-from distributed_tensorflow_models_amd.ops import _lib  # noqa: E402
+from distributed_tensorflow_models_amd.ops import _lib, features, fused  # noqa: E402
 
 
 HOG = [None]  # "blocks:ms": CU-contention stand-in for RCCL channels launched at every backward start
@@ -40,7 +46,7 @@ def _hog():
 
 
 _HOG_STREAM = [None]
-WGS_DEFAULT = [os.environ.get("DTM_WGRAD_STREAM", "1")]  # (the model preset's choice, set in main)
+WGS_DEFAULT = ["1"]  # (the model preset's choice, set in main)
 
 
 def apply(cfg):
@@ -75,22 +81,10 @@ def apply(cfg):
     HOG[0] = cfg.get("hog")
     sc = cfg.get("sc", "5:4096").split(":")
     L.dtm_set_sc_policy(int(sc[0]), int(sc[1]))
-    os.environ["DTM_PROLOGUE"] = cfg.get("prologue", "auto")
-    os.environ["DTM_STEM"] = cfg.get("stem", "1")
-    os.environ["DTM_BNOUT_FUSE"] = cfg.get("bnout", "1")
-    os.environ["DTM_BNOUT_STRIDED"] = cfg.get("bnst", "1")
-    os.environ["DTM_BWD1X1_FUSE"] = cfg.get("b1x1", "1")
-    os.environ["DTM_STEM_WGRAD_FUSE"] = cfg.get("stemw", "1")
-    os.environ["DTM_DGRAD_DEC"] = cfg.get("dec", "1")
-    os.environ["DTM_CAT_MULTI"] = cfg.get("catm", "1")
-    os.environ["DTM_POOL_COMMUTE"] = cfg.get("pcom", "1")
-    os.environ["DTM_SIBLING_GROUP"] = cfg.get("sib", "1")
-    os.environ["DTM_ACT_HANDOFF"] = cfg.get("ahand", "1")
-    os.environ["DTM_SIBLING_POOL"] = cfg.get("sibp", "1")
-    os.environ["DTM_SIBLING_FWD"] = cfg.get("sfwd", "1")
-    os.environ["DTM_RESNET_SIBLING_FWD"] = cfg.get("rfwd", "0")
-    os.environ["DTM_SIBLING_COMBINE"] = cfg.get("scomb", "1")
-    os.environ["DTM_STATS_BWD"] = cfg.get("sbwd", "1")
+    fused.PROLOGUE_MODE = None if cfg.get("prologue", "auto") == "auto" else cfg["prologue"]
+    # fused-path features (ops/features.py) switched off by this variant: off:<name>+<name>
+    os.environ["DTM_DISABLE"] = ",".join(n for n in cfg.get("off", "").split("+") if n)
+    features.check_env()
 
 
 def main():

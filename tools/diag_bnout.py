@@ -21,7 +21,7 @@ def main():
     y = torch.randint(0, 10, (x.shape[0],), device=dev)
     runs = {}
     for tag, fuse in (("u1", "0"), ("u2", "0"), ("f", "1")):
-        os.environ["DTM_BNOUT_FUSE"] = fuse
+        os.environ["DTM_DISABLE"] = "" if fuse == "1" else "bnout_fuse"
         for p in net.parameters():
             p.grad = None
         n0 = fused.BNOUT_FUSED[0]

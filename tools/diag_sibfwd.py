@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Merged sibling-head forward (DTM_SIBLING_FWD=1) vs per-head forward (0) on Inception-v3: per-parameter main_grad
+"""Merged sibling-head forward (feature sibling_fwd) vs per-head forward (DTM_DISABLE=sibling_fwd) on Inception-v3: per-parameter main_grad
 relative errors of one training step, grouped by mixed block (deterministic reductions, pinned dropout), so a real
 backward difference of the merged path (it would show in the blocks nearest the loss) can be told from random-init
 drift (which grows towards the stem).
@@ -40,7 +40,7 @@ def main():
     init = [b.detach().clone() for b in moving_average_buffers(net)]
     out = {}
     for run in ("0", "1", "0b"):
-        os.environ["DTM_SIBLING_FWD"] = run[0]
+        os.environ["DTM_DISABLE"] = "" if run[0] == "1" else "sibling_fwd"
         with torch.no_grad():
             for b, v in zip(moving_average_buffers(net), init):
                 b.copy_(v)

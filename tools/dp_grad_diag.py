@@ -1,6 +1,6 @@
 """Per-parameter step-1 gradient table: W ranks (same batch) vs 1 rank, in backward order.
 
-  python tools/dp_grad_diag.py resnet_v1_50 DTM_SIBLING_GROUP=1 [--no-overlap] [--world 2] [--steps 1]
+  python tools/dp_grad_diag.py resnet_v1_50 DTM_DISABLE=sibling_group [--no-overlap] [--world 2] [--steps 1]
 
 Two gloo ranks share the one GPU of a test box (RCCL refuses two ranks on one device); deterministic
 reductions make a correct run bit-exact, so any non-zero row is a real data-parallel defect.  The first
