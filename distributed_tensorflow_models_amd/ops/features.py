@@ -33,7 +33,7 @@ FEATURES = {
     "wgrad_stream": ("conv+BN weight gradients on a second HIP stream, concurrent with the dgrad chain "
                      "(TrainStep(wgrad_stream=...) overrides per model)", "profiles/ab/r3_ab_wgrad_side_stream.log"),
     "bsp_compact": ("dead-tap conv weights get a compact all-reduce bucket holding their live window only",
-                    "profiles/r3/r3_vgg_compact_bucket.log"),
+                    "tests/test_distributed.py test_bsp_dead_tap_gradients_left_out_of_the_allreduce"),
 }
 
 ROUTES_GRADIENTS = ("fused_bn", "sibling_group", "sibling_fwd", "sibling_combine", "act_handoff", "bnout_fuse",

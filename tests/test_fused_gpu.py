@@ -6,7 +6,8 @@ import pytest
 import torch
 
 from distributed_tensorflow_models_amd.models.resnet_v1 import ResNetV1
-from distributed_tensorflow_models_amd.ops import features, fused
+from distributed_tensorflow_models_amd.ops import features
+from distributed_tensorflow_models_amd.ops import fused as fused_ops
 
 pytestmark = pytest.mark.gpu
 
@@ -20,7 +21,7 @@ def _rel(a, b):
 @pytest.mark.parametrize("base,batch", [(16, 16), (16, 32)])
 def test_small_resnet_matches_reference(fused, prologue, base, batch, monkeypatch):
     monkeypatch.setitem(features._override, "fused_bn", (fused) != "0")
-    monkeypatch.setattr(fused, "PROLOGUE_MODE", None if prologue == "auto" else prologue)
+    monkeypatch.setattr(fused_ops, "PROLOGUE_MODE", None if prologue == "auto" else prologue)
     torch.manual_seed(0)
     net_cpu = ResNetV1(blocks=[(base, 2, 2), (2 * base, 2, 1)], num_classes=10, scope="r")
     net_gpu = copy.deepcopy(net_cpu).cuda()

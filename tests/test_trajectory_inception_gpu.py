@@ -85,22 +85,32 @@ def test_inception_v3_trajectory_matches_cpu_fp32(monkeypatch):
     for path, sib in (("merged", "1"), ("per-head", "0")):
         got, d1 = _trajectory(monkeypatch, sib)
         errs = _errors(d1, fx)
-        assert len(errs) > 180, len(errs)  # every trainable tensor of the 388-variable layout
-        bad = ["%s: step-1 rel err %.4f (emulation %.4f)" % (k, e, em) for k, (e, em, _r) in errs.items()
-               if e > 1.5 * em + 0.02]
-        msg = "%s\ngpu  %s\nfp32 %s\nemul %s" % ((path,) + tuple(["%.4f" % v for v in t] for t in (got, fp32, emul)))
-        assert not bad, path + "\n" + "\n".join(bad[:20])
+        d_gpu, d_emul = mrel(got, fp32), mrel(emul, fp32)
         ratios = sorted(r for _e, _em, r in errs.values())
         med = ratios[len(ratios) // 2]
+        # per tensor where bf16-scale noise still determines the update (emulation error < 0.1: the logits and the
+        # top blocks); the chaos-dominated rest (emulation error 0.1 .. 1.5) as a distribution
+        sharp = {k: v for k, v in errs.items() if v[1] < 0.1}
+        chaotic = {k: v for k, v in errs.items() if v[1] >= 0.1}
+        print("%s: losses %s (fp32 %s); loss dev %.4g (emulation %.4g); update norm ratio median %.4f; %d sharp "
+              "tensors: GPU rel err median %.3g max %.3g (emulation %.3g / %.3g); %d chaotic tensors: GPU median %.3g "
+              "p90 %.3g (emulation %.3g / %.3g)" % (
+                  path, ["%.4f" % v for v in got], ["%.4f" % v for v in fp32], d_gpu, d_emul, med, len(sharp),
+                  _pct([v[0] for v in sharp.values()])[0], _pct([v[0] for v in sharp.values()])[2],
+                  _pct([v[1] for v in sharp.values()])[0], _pct([v[1] for v in sharp.values()])[2], len(chaotic),
+                  *_pct([v[0] for v in chaotic.values()])[:2], *_pct([v[1] for v in chaotic.values()])[:2]))
+        msg = "%s\ngpu  %s\nfp32 %s\nemul %s" % ((path,) + tuple(["%.4f" % v for v in t] for t in (got, fp32, emul)))
+        assert len(errs) > 180, len(errs)  # every trainable tensor of the 388-variable layout
+        assert len(sharp) >= 4, sorted(sharp)
+        bad = ["%s: step-1 rel err %.4f (emulation %.4f)" % (k, e, em) for k, (e, em, _r) in sharp.items()
+               if e > 1.5 * em + 0.02]
+        assert not bad, path + "\n" + "\n".join(bad[:20])
+        gc, ec = _pct([v[0] for v in chaotic.values()]), _pct([v[1] for v in chaotic.values()])
+        assert gc[0] < 1.25 * ec[0] + 0.02 and gc[1] < 1.25 * ec[1] + 0.02, (path, gc, ec)
         assert abs(med - 1.0) < 0.03, (path, med)  # no systematic scaling of the update
         assert abs(got[0] - fp32[0]) / fp32[0] < 2e-2, msg  # same weights and batch at step 0
-        d_gpu, d_emul = mrel(got, fp32), mrel(emul, fp32)
         assert d_gpu < 1.5 * d_emul + 5e-3, (d_gpu, d_emul, msg)
         res[path] = errs
-        print("%s: losses %s; step-1 rel err median %.4g p90 %.4g max %.4g (emulation median %.4g); loss dev %.4g "
-              "(emulation %.4g)" % (path, ["%.4f" % v for v in got],
-                                    *_pct([e for e, _em, _r in errs.values()]),
-                                    _pct([em for _e, em, _r in errs.values()])[0], d_gpu, d_emul))
     # the merged head forward is no farther from fp32 than the per-head path
     m = _pct([v[0] for v in res["merged"].values()])
     p = _pct([v[0] for v in res["per-head"].values()])
@@ -159,8 +169,10 @@ def test_inception_v3_merged_forward_within_reduction_noise(monkeypatch):
     print("per-head atomic-order vs deterministic (noise floor): median %.3g p90 %.3g max %.3g" % n)
     print("merged vs per-head (both deterministic):              median %.3g p90 %.3g max %.3g" % d)
     assert abs(merged_l - ref_l) < 1e-3 * abs(ref_l), (merged_l, ref_l)
+    # (measured: the floor itself is O(1) - median 1.06 - the reduction order alone decorrelates the deep layers'
+    # gradients of this chaotic network, so this bound only shows the merged path is no worse than that noise;
+    # the discriminating whole-step check is the teacher-forced test below)
     assert d[0] <= 3.0 * n[0] + 1e-4 and d[1] <= 3.0 * n[1] + 1e-3, (d, n)
-    assert d[2] < 0.5, d  # nothing O(1)
 
 
 # ---------------------------------------------------------------------------------------------------------------
