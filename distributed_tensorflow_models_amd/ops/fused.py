@@ -1005,10 +1005,13 @@ def _prologue_mode(x_shape, w_shape, stride):
     every conv except the stride-2 3x3 at 56x56, where it is neutral (profiles/ab/r2_ab_prologue_fused_vs_mat.log),
     and the stage-1 expansion 1x1, whose one-pass backward recomputes relu(bn(x)) from the raw x anyway
     (profiles/ab/r2_ab_prologue_expand.log)."""
-    if PROLOGUE_MODE is not None:
-        return PROLOGUE_MODE
     _, H, W, _ = x_shape
     _, R, S, _ = w_shape
+    if PROLOGUE_MODE == "fused1x1":  # (A/B: the prologue for every 1x1 consumer, the policy otherwise)
+        if R * S == 1:
+            return "fused"
+    elif PROLOGUE_MODE is not None:
+        return PROLOGUE_MODE
     st = stride if isinstance(stride, int) else stride[0]
     if st > 1 and H * W >= 56 * 56:
         return "fused"

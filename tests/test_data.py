@@ -395,3 +395,39 @@ def test_gpu_pipeline_split_decode_host_side(tmp_path):
         assert n == len(descs) and fb is not None  # both kinds present in these batches
         np.testing.assert_array_equal(rgb, bt.numpy()[:total])
         assert int(tab["src_off"][-1] + tab["h"][-1] * tab["w"][-1] * 3) == total
+
+
+def test_decode_capacity_check_warns_when_host_cpus_cannot_feed_the_node(monkeypatch):
+    """a node of 8 ResNet-50 ranks (~120k img/s) needs far more decode CPUs than a 16-CPU host; the
+    startup check says so (with the split-decode alternative), a host with enough CPUs passes silently, and the
+    split JPEG decode is chosen automatically only when the full host decode cannot keep up (DTM_SPLIT_DECODE=0/1
+    overrides)."""
+    from distributed_tensorflow_models_amd.data import capacity
+    msgs = []
+    rate = {"full": 1000.0, "split": 2500.0}
+    need, cpus, ok = capacity.decode_capacity_check("resnet_v1_50", gpus=8, cpus=16, per_cpu=rate, log=msgs.append)
+    assert not ok and cpus == 16 and abs(need - 120.0) < 1e-6
+    assert len(msgs) == 1 and "needs ~120 host CPUs" in msgs[0] and "split decode needs ~48" in msgs[0]
+    msgs.clear()
+    need, _c, ok = capacity.decode_capacity_check("inception_v3_slim_old", gpus=1, cpus=16, per_cpu=rate,
+                                                  log=msgs.append)
+    assert ok and not msgs and need < 16
+    assert capacity.decode_capacity_check("unknown_net", gpus=8, cpus=1, log=msgs.append)[2] and not msgs
+    monkeypatch.delenv("DTM_SPLIT_DECODE", raising=False)
+    assert capacity.choose_split_decode("resnet_v1_50", gpus=8, cpus=16, per_cpu=rate)
+    assert not capacity.choose_split_decode("resnet_v1_50", gpus=1, cpus=64, per_cpu=rate)
+    monkeypatch.setenv("DTM_SPLIT_DECODE", "0")
+    assert not capacity.choose_split_decode("resnet_v1_50", gpus=8, cpus=16, per_cpu=rate)
+    monkeypatch.setenv("DTM_SPLIT_DECODE", "1")
+    assert capacity.choose_split_decode("resnet_v1_50", gpus=1, cpus=64, per_cpu=rate)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert capacity.local_world() == 8 and capacity.node_cpus() >= 1
+
+
+def test_decode_cpu_cost_tool_measures_both_modes():
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from tools import decode_cpu_cost
+    r = decode_cpu_cost.measure(8)
+    assert r["full_us"] > 0 and r["split_us"] > 0 and r["huffman_us"] > 0
+    assert r["split_us"] < r["full_us"]  # the split path leaves dequant / IDCT / colour to the GPU
