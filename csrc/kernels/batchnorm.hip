@@ -612,8 +612,72 @@ __global__ __launch_bounds__(256) void stats_reduce_finalize_kernel(
   if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The same reduction + finalize when ONE block per column group covers every row (no cross-block sum): block b owns
+// channels [32b, 32b + 32) - the 8 column quads of their sums AND the 8 of their sums of squares (16 quads x 16 row
+// lanes) - so it finalizes them itself: no accumulator atomics, no completion counter, no last-block tail (the
+// direct path measured 4-6 us cheaper per launch than the counter hand-off on ResNet-50's 196-row 14x14 / 7x7 maps).
+// Summation order: per row lane a fixed row sequence, then the 16 lanes in order - deterministic.
+template <bool MULTI>
+__global__ __launch_bounds__(256) void stats_finalize_direct_kernel(
+    const float* __restrict__ ws, int rows, int K, const float* __restrict__ gamma, const float* __restrict__ beta,
+    float* __restrict__ mov_mean, float* __restrict__ mov_var, float* __restrict__ out, float count, float eps,
+    float decay, int update, int bessel, FinGroup grp) {
+  __shared__ float4 red[16][16];
+  const int width = 2 * K;
+  const int cg = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int c0 = blockIdx.x * 32;
+  // quads 0..7: sums of channels c0 + 4q .. +3; quads 8..15: their sums of squares
+  const int ch = c0 + (cg & 7) * 4;
+  const int col = (cg < 8 ? 0 : K) + ch;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ch < K) {
+    int r = rl;
+    for (; r + 48 < rows; r += 64) {
+      float4 a = *(const float4*)(ws + (size_t)r * width + col);
+      float4 b = *(const float4*)(ws + (size_t)(r + 16) * width + col);
+      float4 c = *(const float4*)(ws + (size_t)(r + 32) * width + col);
+      float4 d = *(const float4*)(ws + (size_t)(r + 48) * width + col);
+      s.x += (a.x + b.x) + (c.x + d.x); s.y += (a.y + b.y) + (c.y + d.y);
+      s.z += (a.z + b.z) + (c.z + d.z); s.w += (a.w + b.w) + (c.w + d.w);
+    }
+    for (; r < rows; r += 16) {
+      float4 a = *(const float4*)(ws + (size_t)r * width + col);
+      s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+    }
+  }
+  red[rl][cg] = s;
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    float4 t = red[0][threadIdx.x];
+    for (int i = 1; i < 16; ++i) { float4 u = red[i][threadIdx.x]; t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w; }
+    red[0][threadIdx.x] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    const int c = c0 + threadIdx.x;
+    if (c < K) {
+      const float* q = (const float*)&red[0][0];
+      const float sum = q[threadIdx.x], sq = q[32 + threadIdx.x];  // quad j holds channels 4j..4j+3
+      if constexpr (MULTI) {
+        FinMember mb = grp.m[0];
+#pragma unroll
+        for (int j = 1; j < 8; ++j)  // (constant indices: no scratch copy of the argument table)
+          if (j < grp.n && c >= grp.m[j].off) mb = grp.m[j];
+        if (mb.out)
+          bn_fin_channel(sum, sq, c - mb.off, mb.K, mb.gamma, mb.beta, mb.mov_mean, mb.mov_var, mb.out, count, eps,
+                         decay, update, bessel);
+      } else {
+        bn_fin_channel(sum, sq, c, K, gamma, beta, mov_mean, mov_var, out, count, eps, decay, update, bessel);
+      }
+    }
+  }
+}
+
 }  // namespace dtm
 using namespace dtm;
+
+static int g_fin_direct = 1;  // A/B API (dtm_set_fin_direct): the one-block-per-channel-group finalize
+DTM_API void dtm_set_fin_direct(int on) { g_fin_direct = on; }
 
 static int grid_for(long work, int cap = 2048) {
   long b = (work + 255) / 256;
@@ -822,6 +886,19 @@ int dtm_bn_stats_finalize_g(const float* ws, int rows, int K, const float* gamma
   if (K % 2) return -1;  // float4 columns over [2K]
   int rpb, ychunks;
   dtm_reduce_split(rows, (2 * K + 63) / 64, &rpb, &ychunks);
+  if (ychunks == 1 && K % 4 == 0 && g_fin_direct) {
+    // every column's rows in one block: that block finalizes its channels itself
+    if (fg) {
+      hipLaunchKernelGGL(stats_finalize_direct_kernel<true>, dim3((K + 31) / 32), dim3(256), 0, st, ws, rows, K, gamma,
+                         beta, mov_mean, mov_var, ss, count, eps, decay, update, bessel, *fg);
+    } else {
+      FinGroup none;
+      none.n = 0;
+      hipLaunchKernelGGL(stats_finalize_direct_kernel<false>, dim3((K + 31) / 32), dim3(256), 0, st, ws, rows, K, gamma,
+                         beta, mov_mean, mov_var, ss, count, eps, decay, update, bessel, none);
+    }
+    return 0;
+  }
   if (fg) {
     hipLaunchKernelGGL(stats_reduce_finalize_kernel<true>, dim3((2 * K + 63) / 64, ychunks), dim3(256), 0, st, ws, rows,
                        K, rpb, g_fin_acc[k], g_fin_counter[k], gamma, beta, mov_mean, mov_var, ss, count, eps, decay,

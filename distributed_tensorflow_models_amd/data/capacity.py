@@ -7,14 +7,15 @@ r5_decode_cpu_cost*.log):
   full  - Example parse + baseline JPEG decode (PIL / libjpeg-turbo) + distortion parameters,
   split - the same with only the Huffman decode on the host (DTM_SPLIT_DECODE=1: dequantisation, IDCT, upsampling
           and colour conversion run as HIP kernels, csrc/kernels/jpeg.hip).
-The split path needs ~2.4x less host CPU per image; on a box with CPUs to spare the full path sustains more
+The split path needs ~1.8x less host CPU per image on the box (729 vs 410 us; 2.4x on this container's slower cores,
+r5_decode_cpu_cost_container.log); on a box with CPUs to spare the full path sustains more
 images/s (its batch assembly is lighter: profiles/r3/r3_imagenet_pipeline_split_vs_full.log), so it stays the default
 there, and ``choose_split_decode`` switches to split only when full decode cannot keep up."""
 import logging
 import os
 
 # img/s per host CPU core (tools/decode_cpu_cost.py on the MI355X box's host CPUs; see module docstring)
-IMG_S_PER_CPU = {"full": 850.0, "split": 2000.0}
+IMG_S_PER_CPU = {"full": 1370.0, "split": 2440.0}
 
 # expected per-GPU consumption of the training step (bench.py on one MI355X, round 5), images/s
 PER_GPU_IMG_S = {"resnet_v1_50": 15000.0, "inception_v3_slim_old": 7400.0, "mobilenet_v1": 20000.0,

@@ -1004,13 +1004,11 @@ def _prologue_mode(x_shape, w_shape, stride):
     costs fwd +13..+66 us and wgrad +12..+68 us per layer, a materialising pass 6..35 us -> 'mat' wins
     every conv except the stride-2 3x3 at 56x56, where it is neutral (profiles/ab/r2_ab_prologue_fused_vs_mat.log),
     and the stage-1 expansion 1x1, whose one-pass backward recomputes relu(bn(x)) from the raw x anyway
-    (profiles/ab/r2_ab_prologue_expand.log)."""
+    (profiles/ab/r2_ab_prologue_expand.log).  Re-measured in round 5 with the pipelined prologue tiles: the prologue
+    for every 1x1 consumer is still +1.71 % step (profiles/ab/r5_ab_prologue_1x1_fdir.log)."""
     _, H, W, _ = x_shape
     _, R, S, _ = w_shape
-    if PROLOGUE_MODE == "fused1x1":  # (A/B: the prologue for every 1x1 consumer, the policy otherwise)
-        if R * S == 1:
-            return "fused"
-    elif PROLOGUE_MODE is not None:
+    if PROLOGUE_MODE is not None:
         return PROLOGUE_MODE
     st = stride if isinstance(stride, int) else stride[0]
     if st > 1 and H * W >= 56 * 56:

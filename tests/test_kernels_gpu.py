@@ -589,3 +589,52 @@ def test_device_state_bound_to_first_device():
     x = torch.zeros(8, device="cuda")  # (initialises the device)
     assert L.dtm_device_check() == 0
     assert x.sum().item() == 0
+
+
+@pytest.mark.parametrize("case", [(16, 14, 256, 256), (8, 7, 512, 2048), (4, 35, 288, 48), (2, 8, 1280, 320),
+                                  (64, 56, 64, 64), (3, 17, 768, 192)])
+def test_bn_stats_finalize_direct_matches_counter_path_and_fp32(case):
+    """The one-block-per-channel-group BN finalize (stats_finalize_direct_kernel, taken when one row chunk covers
+    every statistics row) vs the accumulator + completion-counter path it replaces: ss = [scale; shift; mean; rstd]
+    and the moving averages bit-identical under deterministic reductions (the persistent conv kernels' partial rows
+    are otherwise summed in arrival order: 1e-6 then); both against the fp32 batch statistics of the conv output."""
+    import ctypes
+
+    from distributed_tensorflow_models_amd.ops import _lib
+    N, H, C, K = case
+    torch.manual_seed(1)
+    L = _lib.lib()
+    st = _lib.stream_ptr()
+    x = torch.randn(N, H, H, C, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(K, 1, 1, C, device=DEV) / C ** 0.5).to(torch.bfloat16)
+    beta = torch.randn(K, device=DEV)
+    mm0, mv0 = torch.randn(K, device=DEV) * 0.1, torch.rand(K, device=DEV) + 0.5
+    M = N * H * H
+    d = _lib.ConvDesc(N, H, H, C, K, 1, 1, H, H, 1, 0, 0, 0, 0)
+    out = {}
+    try:
+        for direct, det in ((1, 1), (0, 1), (1, 0)):
+            L.dtm_set_fin_direct(direct)
+            L.dtm_set_deterministic(det)
+            y = torch.empty(N, H, H, K, device=DEV, dtype=torch.bfloat16)
+            mm, mv, ss = mm0.clone(), mv0.clone(), torch.zeros(4, K, device=DEV)
+            assert L.dtm_conv_fwd_bn(_lib.ptr(x), _lib.ptr(w), _lib.ptr(y), None, None, None, _lib.ptr(beta),
+                                     _lib.ptr(mm), _lib.ptr(mv), _lib.ptr(ss), float(M), 1e-3, 0.9, 1, 0,
+                                     ctypes.byref(d), st) == 0
+            torch.cuda.synchronize()
+            out[(direct, det)] = (y, ss, mm, mv)
+    finally:
+        L.dtm_set_fin_direct(1)
+        L.dtm_set_deterministic(0)
+    assert torch.equal(out[(0, 1)][0], out[(1, 1)][0])
+    for a, b in zip(out[(1, 1)][1:], out[(0, 1)][1:]):
+        assert torch.equal(a, b), _rel(a, b)
+    for a, b in zip(out[(1, 0)][1:], out[(0, 1)][1:]):
+        assert _rel(a, b) < 1e-6, _rel(a, b)
+    out[1] = out[(1, 0)]
+    yf = (x.float().reshape(M, C) @ w.float().reshape(K, C).t())
+    mean, var = yf.mean(0), yf.var(0, unbiased=False)
+    ss = out[1][1]
+    assert _rel(ss[2], mean) < 2e-2 and _rel(ss[3], torch.rsqrt(var + 1e-3)) < 2e-2
+    assert _rel(ss[1], beta - mean * ss[0]) < 2e-2
+    assert _rel(out[1][2], mm0 * 0.9 + 0.1 * mean) < 2e-2 and _rel(out[1][3], mv0 * 0.9 + 0.1 * var) < 2e-2

@@ -22,7 +22,8 @@ of two independent whole backward passes blind below the top layers.  Hence thre
 3. test_inception_v3_step_teacher_forced_per_segment: the discriminating whole-step check - one real GPU
    training step, every segment (stem, 11 mixed blocks, aux head, logits head) recomputed on the CPU from the
    GPU's own segment inputs and output gradients; every parameter gradient and every block's input gradient within
-   1.5x the bf16-emulation floor (+2 %) of that recomputation."""
+   2x the bf16-emulation floor (+3 %) of that recomputation, and the median / p90 over tensors within 1.1x / 1.2x of
+   the emulation's (measured: 0.0805 vs 0.0803, profiles/r5/r5_s3_pytest_fixed.log)."""
 import json
 import os
 import sys
@@ -268,18 +269,21 @@ def test_inception_v3_step_teacher_forced_per_segment(monkeypatch, sib_fwd):
         eg, ee = rel(gpu_pg[k], f), rel(emu_pg[k], f)
         e_g.append(eg)
         e_e.append(ee)
-        if eg > 1.5 * ee + 0.02:
+        if eg > 2.0 * ee + 0.03:
             bad.append("param %s: rel err %.4g (emulation %.4g)" % (k, eg, ee))
     # the gradient each block hands to the one below it (its input gradient, aux head included at 768e)
     for k in _SEGMENT_EPS[:-1]:
         eg, ee = rel(grads[k], f32_dx[k]), rel(emu_dx[k], f32_dx[k])
         e_g.append(eg)
         e_e.append(ee)
-        if eg > 1.5 * ee + 0.02:
+        if eg > 2.0 * ee + 0.03:
             bad.append("input gradient of the block after %s: rel err %.4g (emulation %.4g)" % (k, eg, ee))
     assert len(e_g) > 190, len(e_g)
     print("%s: %d tensors, GPU vs fp32 rel err median %.3g p90 %.3g max %.3g; emulation median %.3g p90 %.3g "
           "max %.3g" % ((sib_fwd, len(e_g)) + _pct(e_g) + _pct(e_e)))
     assert not bad, "\n".join(bad[:20])
-    # and typically as close as the emulation (no systematic error hiding under the per-tensor slack)
-    assert _pct(e_g)[0] < 1.5 * _pct(e_e)[0] + 2e-3, (_pct(e_g), _pct(e_e))
+    # and typically as close as the emulation: no systematic error hiding under the per-tensor slack (the slack is for
+    # single tensors whose rounding points differ from the emulation's - the commuted pool branch rounds the conv
+    # output before the pool, the reference after it - and for atomic-order noise; measured medians agree to 1 %)
+    assert _pct(e_g)[0] < 1.1 * _pct(e_e)[0] + 2e-3 and _pct(e_g)[1] < 1.2 * _pct(e_e)[1] + 5e-3, (
+        _pct(e_g), _pct(e_e))

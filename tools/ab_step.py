@@ -12,7 +12,8 @@ grid for), wcu / swc (the same for the main-stream / stem wgrads), dir3 (0/1: di
 dgrp (0/1: strided-dgrad parity classes as one grouped launch), atile (tile id of the dgrads with a fused
 activation-backward epilogue, -1 = policy), rsv (CUs reserved from the compute grids' sizing), lpt (0/1: grouped
 parity classes in descending tap count), dtile (0/1: grouped strided-dgrad tile chosen for the whole grouped grid),
-stile (0/1: merged-head convs on the pipelined 128x128 tile), hog (blocks:ms - a CU-occupying copy kernel on another
+stile (0/1: merged-head convs on the pipelined 128x128 tile), fdir (0/1: one-block BN finalize when one row
+chunk covers every statistics row), hog (blocks:ms - a CU-occupying copy kernel on another
 stream from every backward start, standing in for RCCL channels), wtile[:occ] (wgrad tile id / blocks-per-CU target),
 prologue (auto | fused | mat | apply: ops/fused.py PROLOGUE_MODE), red (target_blocks:max_chunks[:direct_max] of the
 partial-sum reductions), off (name+name: fused-path features of ops/features.py switched off, e.g.
@@ -78,6 +79,7 @@ def apply(cfg):
     L.dtm_conv_set_dec_lpt(int(cfg.get("lpt", "1")))
     L.dtm_conv_set_dec_tile(int(cfg.get("dtile", "1")))
     L.dtm_conv_set_split_tile(int(cfg.get("stile", "1")))
+    L.dtm_set_fin_direct(int(cfg.get("fdir", "1")))
     HOG[0] = cfg.get("hog")
     sc = cfg.get("sc", "5:4096").split(":")
     L.dtm_set_sc_policy(int(sc[0]), int(sc[1]))
