@@ -2225,6 +2225,9 @@ static TileCfg pick_tile_impl(const ConvNTArgs& a, bool stats) {
   if (id == 24) return {id, 256, 2};              // 256 x 64 pipelined (waves 2x2 of 128x32)
   if (id == 32) return {id, 256, 4};              // 256 x 32 pipelined, waves 4x1 of 64x32
   // 8-wave 256x256 tile (waves 2x4), no prologue
+  // (3-slot 8-wave 256x128 / 128x256 forms of this tile - two k-tiles in flight, 144 KiB of LDS - measured slower
+  // than the 2-slot 256x256 on every ResNet-50 shape, e.g. 14x14 3x3 82.5 / 79.7 vs 65.0 us, and were removed:
+  // profiles/r5/r5_tile_sweep_w8ns3.log)
   if (id == 40 && a.in_scale) id = 0;
   if (id == 40) return {id, 256, 2};
   if (id == 30 || id == 31) {
