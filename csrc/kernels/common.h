@@ -57,6 +57,10 @@ __host__ static inline FastDiv make_fastdiv(uint32_t d) {
 
 // workspace arena + two-stage reduction (workspace.hip)
 void dtm_reduce_rows(const float* ws, int rows, int width, int ld, float* out, hipStream_t st);
+// several row-sum reductions over the same rows (column segments of one partial-sum table, each into its own output:
+// the split-K slabs of a merged sibling weight gradient) in ONE launch (n <= 8)
+void dtm_reduce_rows_multi(const float* const* ws, const int* widths, float* const* outs, int n, int rows, int ld,
+                           hipStream_t st);
 constexpr int DTM_WS_SLOTS = 5;
 float* dtm_ws_get_stream(size_t floats, hipStream_t st);  // scratch arena of the stream's slot
 bool dtm_stream_capturing(hipStream_t st);  // st is being captured into a hipGraph

@@ -2723,9 +2723,14 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   else launch_wgrad<128, 128, 64, 64>(a, (int)splits, (hipStream_t)stream);
   // dW += sum over the split slabs (every slab element is written: tiles cover [K][Kg] exactly)
   if (dst) {
-    for (int i = 0, r0 = 0; i < dst->n; r0 += dst->rows[i], ++i)
-      dtm_reduce_rows(ws + (size_t)r0 * a.Kg, (int)splits, dst->rows[i] * a.Kg, a.K * a.Kg, dst->dw[i],
-                      (hipStream_t)stream);
+    // every member's row range of the slabs in one launch (a merged Inception head group: up to 4 members)
+    const float* src[8];
+    int widths[8];
+    for (int i = 0, r0 = 0; i < dst->n; r0 += dst->rows[i], ++i) {
+      src[i] = ws + (size_t)r0 * a.Kg;
+      widths[i] = dst->rows[i] * a.Kg;
+    }
+    dtm_reduce_rows_multi(src, widths, dst->dw, dst->n, (int)splits, a.K * a.Kg, (hipStream_t)stream);
   } else {
     dtm_reduce_rows(ws, (int)splits, a.K * a.Kg, a.K * a.Kg, dw, (hipStream_t)stream);
   }

@@ -153,6 +153,58 @@ __global__ __launch_bounds__(256) void reduce_rows_few_kernel(const float* __res
   }
 }
 
+// reduce_rows4 over up to 8 column segments in one grid: x-blocks [xb0_i, xb0_{i+1}) reduce segment i (its own
+// source columns and output).  The segment is picked with constant indices (no scratch copy of the argument table).
+struct RedSeg {
+  const float* ws;
+  float* out;
+  int width, xb0;
+};
+struct RedSegs {
+  RedSeg s[8];
+  int n;
+};
+__global__ __launch_bounds__(256) void reduce_rows4_multi_kernel(RedSegs sg, int rows, int ld, int rpb) {
+  __shared__ float4 red[16][16];
+  RedSeg seg = sg.s[0];
+#pragma unroll
+  for (int j = 1; j < 8; ++j)
+    if (j < sg.n && (int)blockIdx.x >= sg.s[j].xb0) seg = sg.s[j];
+  const int cg = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int col = (((int)blockIdx.x - seg.xb0) * 16 + cg) * 4;
+  const int r0 = blockIdx.y * rpb, r1 = min(rows, r0 + rpb);
+  const float* ws = seg.ws;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col < seg.width) {
+    int r = r0 + rl;
+    for (; r + 48 < r1; r += 64) {
+      float4 a = *(const float4*)(ws + (size_t)r * ld + col);
+      float4 b = *(const float4*)(ws + (size_t)(r + 16) * ld + col);
+      float4 c = *(const float4*)(ws + (size_t)(r + 32) * ld + col);
+      float4 d = *(const float4*)(ws + (size_t)(r + 48) * ld + col);
+      s.x += (a.x + b.x) + (c.x + d.x); s.y += (a.y + b.y) + (c.y + d.y);
+      s.z += (a.z + b.z) + (c.z + d.z); s.w += (a.w + b.w) + (c.w + d.w);
+    }
+    for (; r < r1; r += 16) {
+      float4 a = *(const float4*)(ws + (size_t)r * ld + col);
+      s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+    }
+  }
+  red[rl][cg] = s;
+  __syncthreads();
+  if (rl == 0 && col < seg.width) {
+    float4 t = red[0][cg];
+    for (int i = 1; i < 16; ++i) { float4 u = red[i][cg]; t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w; }
+    float* out = seg.out;
+    if (gridDim.y == 1) {
+      out[col] += t.x; out[col + 1] += t.y; out[col + 2] += t.z; out[col + 3] += t.w;
+    } else {
+      atomicAdd(out + col, t.x); atomicAdd(out + col + 1, t.y);
+      atomicAdd(out + col + 2, t.z); atomicAdd(out + col + 3, t.w);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ ws, int rows, int width, int ld,
                                                           float* __restrict__ out, int chunks) {
   const int j = blockIdx.x * 256 + threadIdx.x;
@@ -227,6 +279,30 @@ void dtm_reduce_rows(const float* ws, int rows, int width, int ld, float* out, h
   int chunks = g_red_det ? 1 : (rows >= 512 ? 32 : (rows >= 64 ? 8 : 1));
   hipLaunchKernelGGL(reduce_rows_kernel, dim3((width + 255) / 256, chunks), dim3(256), 0, st, ws, rows, width, ld, out,
                      chunks);
+}
+
+void dtm_reduce_rows_multi(const float* const* ws, const int* widths, float* const* outs, int n, int rows, int ld,
+                           hipStream_t st) {
+  bool ok = n >= 1 && n <= 8 && ld % 4 == 0 && !(g_red_few && rows <= 32);
+  for (int i = 0; ok && i < n; ++i)
+    ok = widths[i] % 4 == 0 && ((uintptr_t)ws[i] & 15) == 0 && ((uintptr_t)outs[i] & 15) == 0;
+  if (!ok) {  // (few-row slabs keep the streaming kernel; odd widths the generic one)
+    for (int i = 0; i < n; ++i) dtm_reduce_rows(ws[i], rows, widths[i], ld, outs[i], st);
+    return;
+  }
+  RedSegs sg;
+  sg.n = n;
+  int xb = 0, maxw = 0;
+  for (int i = 0; i < 8; ++i) {
+    sg.s[i] = RedSeg{i < n ? ws[i] : nullptr, i < n ? outs[i] : nullptr, i < n ? widths[i] : 0, xb};
+    if (i < n) {
+      xb += (widths[i] + 63) / 64;
+      maxw = widths[i] > maxw ? widths[i] : maxw;
+    }
+  }
+  int rpb, ychunks;
+  dtm_reduce_split(rows, xb, &rpb, &ychunks);
+  hipLaunchKernelGGL(reduce_rows4_multi_kernel, dim3(xb, ychunks), dim3(256), 0, st, sg, rows, ld, rpb);
 }
 
 DTM_API int dtm_ws_reserve(long floats) { return dtm_ws_get_stream((size_t)floats, nullptr) ? 0 : -1; }

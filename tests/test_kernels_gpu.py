@@ -638,3 +638,39 @@ def test_bn_stats_finalize_direct_matches_counter_path_and_fp32(case):
     assert _rel(ss[2], mean) < 2e-2 and _rel(ss[3], torch.rsqrt(var + 1e-3)) < 2e-2
     assert _rel(ss[1], beta - mean * ss[0]) < 2e-2
     assert _rel(out[1][2], mm0 * 0.9 + 0.1 * mean) < 2e-2 and _rel(out[1][3], mv0 * 0.9 + 0.1 * var) < 2e-2
+
+
+@pytest.mark.parametrize("case", [(128, 35, 288, [64, 48, 64, 32]), (8, 17, 768, [192, 160, 160, 192]),
+                                  (4, 8, 1280, [320, 384, 448]), (2, 9, 64, [16, 8])])
+@pytest.mark.parametrize("det", [0, 1])
+def test_conv_wgrad_multi_matches_separate(case, det):
+    """The weight gradient of merged sibling 1x1 convs (dtm_conv_wgrad_multi: ONE wgrad over the members' output
+    gradients side by side, its split-K slabs' row ranges reduced into each member's dW in one launch) vs one
+    dtm_conv_wgrad per member, and vs fp32 torch; deterministic mode: bit-identical to the per-member runs' sums of
+    the same slabs is not promised (other split counts), so both are held to the fp32 reference."""
+    import ctypes
+
+    from distributed_tensorflow_models_amd.ops import _lib
+    N, H, C, ks = case
+    torch.manual_seed(3)
+    L = _lib.lib()
+    st = _lib.stream_ptr()
+    x = torch.randn(N, H, H, C, device=DEV).to(torch.bfloat16)
+    K = sum(ks)
+    dy = torch.randn(N, H, H, K, device=DEV).to(torch.bfloat16)
+    L.dtm_set_deterministic(det)
+    try:
+        dws = [torch.zeros(k, 1, 1, C, device=DEV) for k in ks]
+        d = _lib.ConvDesc(N, H, H, C, K, 1, 1, H, H, 1, 0, 0, 0, 0)
+        ptrs = (ctypes.c_void_p * len(ks))(*[t.data_ptr() for t in dws])
+        rows = (ctypes.c_int * len(ks))(*ks)
+        assert L.dtm_conv_wgrad_multi(_lib.ptr(x), _lib.ptr(dy), ptrs, rows, len(ks), ctypes.byref(d),
+                                      _lib.num_cus(), st) == 0
+        torch.cuda.synchronize()
+    finally:
+        L.dtm_set_deterministic(0)
+    ref = (dy.float().reshape(-1, K).t() @ x.float().reshape(-1, C))
+    off = 0
+    for k, got in zip(ks, dws):
+        assert _rel(got.reshape(k, C), ref[off:off + k]) < 1e-4, (k, _rel(got.reshape(k, C), ref[off:off + k]))
+        off += k
