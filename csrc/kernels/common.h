@@ -63,11 +63,6 @@ void dtm_reduce_rows_multi(const float* const* ws, const int* widths, float* con
                            hipStream_t st);
 constexpr int DTM_WS_SLOTS = 5;
 float* dtm_ws_get_stream(size_t floats, hipStream_t st);  // scratch arena of the stream's slot
-// split-K slab reductions off the issuing stream (workspace.hip): the slab buffer of an offloaded reduction (nullptr =
-// not offloaded: use the stream's arena), then begin / end around the reduction launched on dtm_off_stream()
-float* dtm_off_slabs(size_t floats, hipStream_t st, int* slot);
-hipStream_t dtm_off_begin(int slot, hipStream_t st);
-void dtm_off_end(int slot);
 bool dtm_stream_capturing(hipStream_t st);  // st is being captured into a hipGraph
 void dtm_ws_set_error(int e);               // -10: growth refused during capture, -4: out of memory
 void dtm_ws_note_retired();

@@ -2708,9 +2708,7 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   splits = (a.Mpix + a.pix_per_split - 1) / a.pix_per_split;
   // split-K partial slabs, summed into dW below (fp32 atomics straight into dW measured +2.4..+12 % step:
   // profiles/ab/r3_ab_wgrad_atomic_*.log)
-  int off_slot = -1;
-  float* ws = dtm_off_slabs((size_t)splits * a.K * a.Kg, (hipStream_t)stream, &off_slot);
-  if (!ws) ws = dtm_ws_get_stream((size_t)splits * a.K * a.Kg, (hipStream_t)stream);
+  float* ws = dtm_ws_get_stream((size_t)splits * a.K * a.Kg, (hipStream_t)stream);
   if (!ws) return -4;
   a.dw = ws;
   if (wt >= 10) {
@@ -2723,9 +2721,10 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   } else if (wt == 1) launch_wgrad<64, 128, 32, 64>(a, (int)splits, (hipStream_t)stream);
   else if (wt == 6) launch_wgrad<32, 128, 16, 64>(a, (int)splits, (hipStream_t)stream);
   else launch_wgrad<128, 128, 64, 64>(a, (int)splits, (hipStream_t)stream);
-  // dW += sum over the split slabs (every slab element is written: tiles cover [K][Kg] exactly); an offloaded
-  // reduction runs on the offload stream (workspace.hip dtm_off_slabs)
-  const hipStream_t rst = off_slot >= 0 ? dtm_off_begin(off_slot, (hipStream_t)stream) : (hipStream_t)stream;
+  // dW += sum over the split slabs (every slab element is written: tiles cover [K][Kg] exactly).  (Running these
+  // reductions on a second stream under the next conv - slabs in a 2-entry ring, event hand-offs, joined before the
+  // optimizer - measured +5.8 % eager / +6.3 % captured Inception-v3 step and was removed in round 5:
+  // profiles/ab/r5_ab_offload_inception.log, profiles/r5/r5_s6_bench_inc_*.log)
   if (dst) {
     // every member's row range of the slabs in one launch (a merged Inception head group: up to 4 members)
     const float* src[8];
@@ -2734,11 +2733,10 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
       src[i] = ws + (size_t)r0 * a.Kg;
       widths[i] = dst->rows[i] * a.Kg;
     }
-    dtm_reduce_rows_multi(src, widths, dst->dw, dst->n, (int)splits, a.K * a.Kg, rst);
+    dtm_reduce_rows_multi(src, widths, dst->dw, dst->n, (int)splits, a.K * a.Kg, (hipStream_t)stream);
   } else {
-    dtm_reduce_rows(ws, (int)splits, a.K * a.Kg, a.K * a.Kg, dw, rst);
+    dtm_reduce_rows(ws, (int)splits, a.K * a.Kg, a.K * a.Kg, dw, (hipStream_t)stream);
   }
-  if (off_slot >= 0) dtm_off_end(off_slot);
   return 0;
 }
 

@@ -95,80 +95,6 @@ float* dtm_ws_get_stream(size_t floats, hipStream_t st) {
   return g_ws[k];
 }
 
-// ---- split-K slab reductions off the issuing stream -----------------------------------------------------------
-// A weight gradient on the main stream writes split-K partial slabs and a row reduction sums them into dW.  The
-// reduction is small and latency-bound (~5 us per launch, ~100 per Inception-v3 step), and nothing on the main
-// stream reads dW until the optimizer.  With an offload stream set (dtm_set_reduce_offload; single-rank steps
-// whose weight gradients run on the main stream), the slabs go to a 2-entry ring instead of the stream's arena and
-// the reduction runs on the offload stream - concurrently with the next conv on the main stream:
-//   main: wgrad(i) -> record ready[j] ; offload: wait ready[j] -> reduce(i) -> record done[j]
-//   main, before reusing ring[j] (two wgrads later): wait done[j]   (the reduction has finished reading it)
-//   main, before anything reads dW (dtm_reduce_offload_join, called where the engine joins its side streams):
-//   wait done[*].
-// Inside a hipGraph capture the records / waits are graph edges (the offload stream joins the capture through the
-// first wait and is joined back by the join).  Ring growth is refused inside a capture (the reduction then stays on
-// the main stream for that launch: correct, only not overlapped).
-static hipStream_t g_off_stream = nullptr;
-static bool g_off_on = false;
-static float* g_off_ring[2] = {};
-static size_t g_off_floats[2] = {};
-static hipEvent_t g_off_ready[2] = {}, g_off_done[2] = {};
-static bool g_off_pending[2] = {};
-static int g_off_next = 0;
-
-DTM_API int dtm_set_reduce_offload(int on) {
-  if (on && !g_off_stream) {
-    if (hipStreamCreateWithFlags(&g_off_stream, hipStreamNonBlocking) != hipSuccess) return -4;
-    for (int j = 0; j < 2; ++j)
-      if (hipEventCreateWithFlags(&g_off_ready[j], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&g_off_done[j], hipEventDisableTiming) != hipSuccess)
-        return -4;
-    dtm_ws_set_side_stream(DTM_WS_SLOTS - 1, g_off_stream);  // its own scratch slot (reductions need none today)
-  }
-  g_off_on = on != 0;
-  return 0;
-}
-DTM_API int dtm_get_reduce_offload() { return g_off_on ? 1 : 0; }
-
-float* dtm_off_slabs(size_t floats, hipStream_t st, int* slot) {
-  if (!g_off_on || !g_off_stream || st == g_off_stream || dtm_ws_slot(st) != 0 || !dtm_device_ok()) return nullptr;
-  const int j = g_off_next;
-  if (floats > g_off_floats[j]) {
-    if (dtm_stream_capturing(st)) return nullptr;  // (no growth inside a capture: this launch reduces in place)
-    // both ring entries grow together (a step's parity of offloaded launches need not be even)
-    size_t n = floats < (16u << 20) ? (16u << 20) : floats;
-    for (int e = 0; e < 2; ++e) {
-      float* p = nullptr;
-      if (g_off_pending[e]) hipStreamWaitEvent(st, g_off_done[e], 0);
-      if (hipMalloc(&p, n * sizeof(float)) != hipSuccess) return nullptr;
-      if (g_off_ring[e]) ++g_ws_retired;  // (never freed: in-flight reductions and captured graphs may hold it)
-      g_off_ring[e] = p;
-      g_off_floats[e] = n;
-    }
-  }
-  if (g_off_pending[j]) hipStreamWaitEvent(st, g_off_done[j], 0);  // WAR on ring[j]
-  *slot = j;
-  g_off_next ^= 1;
-  return g_off_ring[j];
-}
-hipStream_t dtm_off_begin(int slot, hipStream_t st) {
-  hipEventRecord(g_off_ready[slot], st);
-  hipStreamWaitEvent(g_off_stream, g_off_ready[slot], 0);
-  return g_off_stream;
-}
-void dtm_off_end(int slot) {
-  hipEventRecord(g_off_done[slot], g_off_stream);
-  g_off_pending[slot] = true;
-}
-// make `stream` wait for every offloaded reduction issued so far (before the optimizer / any reader of dW)
-DTM_API void dtm_reduce_offload_join(void* stream) {
-  for (int j = 0; j < 2; ++j)
-    if (g_off_pending[j]) {
-      hipStreamWaitEvent((hipStream_t)stream, g_off_done[j], 0);
-      g_off_pending[j] = false;
-    }
-}
-
 // out[j] (+)= sum_r ws[r*ld + j], j < width.  16 column-quads x 16 row-lanes per block, float4 loads,
 // 4 rows in flight per lane, LDS combine, one atomic per output per block.
 __global__ __launch_bounds__(256) void reduce_rows4_kernel(const float* __restrict__ ws, int rows, int width, int ld,

@@ -128,12 +128,6 @@ class TrainStep:
         self.on_backward = None  # optional callable run right before loss.backward() (tools/ab_step.py 'hog')
         if self.dp.world > 1 and params and params[0].is_cuda:
             _lib.set_reserved_cus(reserved_cus_default())
-        if params and params[0].is_cuda:
-            # single rank with the weight gradients on the main stream: their split-K slab reductions run on their
-            # own stream, under the next conv (joined in side_join before the optimizer); never under data
-            # parallelism, where a bucket's all-reduce may start as soon as its gradients are reported
-            from .ops import features
-            _lib.set_reduce_offload(self.dp.world == 1 and not _lib.side_enabled() and features.on("reduce_offload"))
 
     def loss_fn(self, out, labels):
         aux = None

@@ -271,32 +271,10 @@ def side_active():
 
 
 def side_join():
-    """The current stream waits for everything enqueued on the side stream (and for the offloaded split-K slab
-    reductions, set_reduce_offload)."""
+    """The current stream waits for everything enqueued on the side stream."""
     if _side["used"]:
         torch.cuda.current_stream().wait_stream(_side["stream"])
         _side["used"] = False
-    if _off["on"]:
-        lib().dtm_reduce_offload_join(stream_ptr())
-
-
-# split-K slab reductions of main-stream weight gradients on their own stream (csrc/kernels/workspace.hip
-# dtm_off_slabs): single-rank steps whose weight gradients stay on the main stream (Inception-v3's preset); the
-# engine joins it with the side stream (side_join) before anything reads the gradients
-_off = {"on": False}
-
-
-def set_reduce_offload(on):
-    on = bool(on)
-    if on or _off["on"]:
-        rc = lib().dtm_set_reduce_offload(int(on))
-        if rc != 0:
-            raise RuntimeError("dtm_set_reduce_offload failed (%d)" % rc)
-    _off["on"] = on
-
-
-def reduce_offload():
-    return _off["on"]
 
 
 def ptr(t):

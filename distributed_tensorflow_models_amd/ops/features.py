@@ -32,8 +32,6 @@ FEATURES = {
                      "profiles/ab/r2_ab_pool_commute_inception.log"),
     "wgrad_stream": ("conv+BN weight gradients on a second HIP stream, concurrent with the dgrad chain "
                      "(TrainStep(wgrad_stream=...) overrides per model)", "profiles/ab/r3_ab_wgrad_side_stream.log"),
-    "reduce_offload": ("single rank, weight gradients on the main stream: their split-K slab reductions on an offload "
-                       "stream under the next conv (never with more than one rank)", "profiles/ab/r5_ab_offload_inception.log"),
     "bsp_compact": ("dead-tap conv weights get a compact all-reduce bucket holding their live window only",
                     "tests/test_distributed.py test_bsp_dead_tap_gradients_left_out_of_the_allreduce"),
 }

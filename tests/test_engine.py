@@ -303,27 +303,3 @@ def test_hipgraph_replay_after_larger_eager_step_matches_eager():
     step.dp.close()
     assert losses == pytest.approx(le, rel=2e-2, abs=2e-3)
     assert ((params - pe).norm() / pe.norm()).item() < 1e-3
-
-
-@pytest.mark.gpu
-def test_reduce_offload_bit_exact_vs_in_stream():
-    """Inception-v3's main-stream weight gradients with their split-K slab reductions on the offload stream
-    (feature reduce_offload, csrc/kernels/workspace.hip dtm_off_slabs) vs on the main stream: the same parameters
-    after 3 eager steps, bit for bit under deterministic reductions (same kernels, same order; only the stream and
-    the slab buffer differ)."""
-    from distributed_tensorflow_models_amd.ops import _lib, features
-    _lib.set_deterministic(True)
-    side_was = _lib.side_enabled()
-    try:
-        kw = dict(lr=0.005, reset_seed=True, dropout_keep_prob=1.0, wgrad_stream=False)
-        lo, po, _, st = _run_steps("inception_v3_slim_old", False, 3, 299, 11, **kw)
-        assert _lib.reduce_offload()
-        with features.override(reduce_offload=False):
-            li, pi, _, st2 = _run_steps("inception_v3_slim_old", False, 3, 299, 11, **kw)
-            assert not _lib.reduce_offload()
-    finally:
-        _lib.set_deterministic(False)
-        _lib.set_side_enabled(side_was)
-        _lib.set_reduce_offload(False)
-    assert lo == li
-    assert torch.equal(po, pi)

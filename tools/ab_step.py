@@ -87,8 +87,6 @@ def apply(cfg):
     # fused-path features (ops/features.py) switched off by this variant: off:<name>+<name>
     os.environ["DTM_DISABLE"] = ",".join(n for n in cfg.get("off", "").split("+") if n)
     features.check_env()
-    # (the engine decides the reduction offload at construction; a variant re-decides it the same way)
-    _lib.set_reduce_offload(features.on("reduce_offload") and not _lib.side_enabled())
 
 
 def main():
