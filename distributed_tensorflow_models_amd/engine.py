@@ -83,7 +83,7 @@ class TrainStep:
                  label_smoothing=0.0, aux_weight=0.4, ema_decay=None, lr_schedule=None, use_graph=False,
                  process_group=None, weight_decay=None, batch_weight=1.0, nan_guard=True, timer=None,
                  grad_comm_dtype=None, ema_buffers=True, bn_sync_every=1, wgrad_stream=None, bsp_check=None,
-                 overlap=True):
+                 overlap=True, force_comm=False):
         self.model = model
         if wgrad_stream is not None:
             # conv+BN weight gradients on the side stream (ops/_lib.py side_stream; process-wide): ResNet-50
@@ -93,8 +93,9 @@ class TrainStep:
         prepare_compute_copies(model)
         params = [p for p in model.parameters() if p.requires_grad]
         # bsp_check (or DTM_BSP_CHECK=1): assert every gradient write precedes its bucket's all-reduce (debug)
+        # force_comm: issue the collectives even with one rank (tests of the RCCL path on a one-GPU box)
         self.dp = BSPDataParallel(params, bucket_mb, process_group, comm_dtype=grad_comm_dtype, overlap=overlap,
-                                  check=bsp_check, names=list(model.named_parameters()))
+                                  check=bsp_check, names=list(model.named_parameters()), force_comm=force_comm)
         if use_graph and self.dp.world > 1:
             # a captured step would hold the bucket collectives (and their waits) inside the graph;
             # RCCL-in-hipGraph has never been validated here, so multi-rank runs stay eager
@@ -104,7 +105,7 @@ class TrainStep:
         # keeps ONE PS-resident copy that every worker updates); must precede the optimizer tables
         bufs = moving_average_buffers(model)
         self.bufsync = BufferSync(bufs, process_group, every=bn_sync_every,
-                                  decays=moving_average_decays(model, bufs))
+                                  decays=moving_average_decays(model, bufs), force_comm=force_comm)
         # ema_buffers: whether the statistics also get EMA shadows (slim BN lists them in
         # moving_average_variables(); tf.layers BN - the CIFAR ResNet preset - does not)
         self.opt = FusedOptimizer(params, optimizer, lr, momentum, rho, epsilon, ema_decay, weight_decay,

@@ -41,17 +41,19 @@ from ..utils.profiler import roctx
 
 class BSPDataParallel:
     def __init__(self, params, bucket_mb=32.0, process_group=None, device=None, overlap=True, grad_dtype=torch.float32,
-                 comm_dtype=None, tail_mb=1.0, check=None, names=None):
+                 comm_dtype=None, tail_mb=1.0, check=None, names=None, force_comm=False):
         self.params = [p for p in params if p.requires_grad]
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        # force_comm: issue the bucket collectives even with one rank (tests: the RCCL path on a one-GPU box)
+        self.comm_on = self.world > 1 or bool(force_comm)
         dev = device or self.params[0].device
         total = sum(p.numel() for p in self.params)
         self.flat = torch.zeros(total, dtype=grad_dtype, device=dev)
         self.comm_dtype = comm_dtype if comm_dtype is not None else grad_dtype
         # low-precision shadow of the flat buffer for the wire (only with more than one rank)
         self.comm = (torch.empty(total, dtype=self.comm_dtype, device=dev)
-                     if (self.comm_dtype != grad_dtype and self.world > 1) else None)
+                     if (self.comm_dtype != grad_dtype and self.comm_on) else None)
         # backward order ~ reverse of registration order
         self.order = list(reversed(self.params))
         self.offsets = {}
@@ -229,7 +231,7 @@ class BSPDataParallel:
         if self._launched[bi]:
             return
         self._launched[bi] = True
-        if self.world == 1:
+        if not self.comm_on:
             return
         side = _lib.side_active() if self.flat.is_cuda else None
         if side is not None and torch.cuda.current_stream() != side:
@@ -353,12 +355,13 @@ class BufferSync:
     own values.  EMA shadows of the statistics are updated by the optimizer from the synced values, so they
     stay replica-identical without a collective of their own."""
 
-    def __init__(self, buffers, process_group=None, every=1, decays=None):
+    def __init__(self, buffers, process_group=None, every=1, decays=None, force_comm=False):
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
         self.buffers = [b for b in buffers]
         self.every = max(1, int(every))
-        self.flat = flatten_tensors(self.buffers) if (self.world > 1 and self.buffers) else None
+        comm = self.world > 1 or bool(force_comm)
+        self.flat = flatten_tensors(self.buffers) if (comm and self.buffers) else None
         self.prev = self.send = self.decay = None
         if self.flat is not None:
             # the statistics as of the last sync (every replica holds the same values there)

@@ -36,12 +36,13 @@ def nccl_options(high_priority=True):
 
 
 def init(rank=None, world_size=None, master_addr=None, master_port=None, backend=None, timeout_s=1800,
-         high_priority=True):
+         high_priority=True, force=False):
+    """force: create the process group even for one rank (tests of the RCCL path on a one-GPU box)."""
     if dist.is_available() and dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
     rank = int(os.environ.get("RANK", 0) if rank is None else rank)
     world_size = int(os.environ.get("WORLD_SIZE", 1) if world_size is None else world_size)
-    if world_size <= 1:
+    if world_size <= 1 and not force:
         return 0, 1
     os.environ.setdefault("MASTER_ADDR", master_addr or "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", str(master_port or 29500))

@@ -16,12 +16,14 @@ def free_port():
     return p
 
 
-def _entry(rank, fn, world, port, outdir, args):
+def _entry(rank, fn, world, port, outdir, args, backend="gloo"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), DTM_RUN_ID="t%d" % port)
     torch.set_num_threads(max(1, (os.cpu_count() or 2) // world))
     from ..parallel import process_group as pg
-    pg.init(backend="gloo", timeout_s=120)
+    if backend == "nccl":
+        pg.rccl_env(0, timing=True)  # per-collective durations (bucket_ms)
+    pg.init(backend=backend, timeout_s=120, force=backend == "nccl")
     ok = False
     try:
         out = fn(rank, world, *args)
@@ -35,9 +37,11 @@ def _entry(rank, fn, world, port, outdir, args):
         pg.destroy()
 
 
-def run_workers(fn, world, *args):
-    """Returns [result_rank0, result_rank1, ...]; raises if any rank fails."""
+def run_workers(fn, world, *args, backend="gloo"):
+    """Returns [result_rank0, result_rank1, ...]; raises if any rank fails.  backend "nccl" (RCCL): one rank per GPU
+    (RCCL refuses two ranks on one device)."""
     port = free_port()
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_entry, args=(fn, world, port, d, args), nprocs=world, join=True, start_method="spawn")
+        mp.start_processes(_entry, args=(fn, world, port, d, args, backend), nprocs=world, join=True,
+                           start_method="spawn")
         return [torch.load(os.path.join(d, "r%d.pt" % r), weights_only=True) for r in range(world)]

@@ -689,3 +689,44 @@ def test_ssp_debug_clock_is_read_only():
         obs.tick(1)
     obs.finish()
     assert obs.steps() == [0, 3]
+
+
+def _rccl_single_rank_worker(rank, world):
+    """One rank over RCCL (backend nccl) with the BSP bucket all-reduces and the BN-statistics sync forced on: the
+    communicator, the bucket collectives issued from the backward hooks (side stream included), their timing events
+    and the waits run for real - the part of the data-parallel path a one-GPU box can execute."""
+    import torch.distributed as dist
+
+    from distributed_tensorflow_models_amd.engine import TrainStep, moving_average_buffers
+    from distributed_tensorflow_models_amd.models import nets_factory
+    assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+    dev = torch.device("cuda", 0)
+    out = {}
+    for forced in (False, True):
+        torch.manual_seed(0)
+        model = nets_factory.build("resnet_v1_50", num_classes=16).to(dev)
+        step = TrainStep(model, optimizer="momentum", lr=0.05, momentum=0.9, bucket_mb=2.0, force_comm=forced)
+        g = torch.Generator().manual_seed(5)
+        x = torch.randn(8, 64, 64, 3, generator=g).to(dev, torch.bfloat16)
+        y = torch.randint(0, 16, (8,), generator=g).to(dev)
+        for _ in range(2):
+            step(x, y)
+        torch.cuda.synchronize()
+        out[forced] = {"params": torch.cat([p.detach().float().reshape(-1) for p in model.parameters()]).cpu(),
+                       "bufs": torch.cat([b.detach().reshape(-1) for b in moving_average_buffers(model)]).cpu(),
+                       "works": len(step.dp._done_works), "buckets": len(step.dp.buckets),
+                       "ms": step.dp.bucket_ms(), "bn_flat": step.bufsync.numel()}
+        step.dp.close()
+    return out
+
+
+@pytest.mark.gpu
+def test_bsp_rccl_single_rank_collectives_are_identity():
+    res = run_workers(_rccl_single_rank_worker, 1, backend="nccl")[0]
+    off, on = res[False], res[True]
+    assert off["works"] == 0 and on["works"] == on["buckets"] > 4 and on["bn_flat"] > 0
+    assert len(on["ms"]) == on["works"] and all(v >= 0 for v in on["ms"])
+    # a one-rank all-reduce is the identity: the same parameters as without collectives, bit for bit (BSP buckets);
+    # the BN statistics go through the fp64 combine (d m_prev + (1 - d) B_r with B_r = (m_r - d m_prev) / (1 - d))
+    assert torch.equal(on["params"], off["params"])
+    torch.testing.assert_close(on["bufs"], off["bufs"], rtol=1e-6, atol=1e-7)
