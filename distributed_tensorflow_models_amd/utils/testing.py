@@ -19,7 +19,10 @@ def free_port():
 def _entry(rank, fn, world, port, outdir, args, backend="gloo"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), DTM_RUN_ID="t%d" % port)
-    torch.set_num_threads(max(1, (os.cpu_count() or 2) // world))
+    # the CPU share, not the machine: os.cpu_count() on a GPU box is the whole host (hundreds), and that many OpenMP
+    # threads per rank under a 16-CPU quota turn every CPU op (a model's weight init) into minutes of spin-waiting
+    cpus = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0)) or 2
+    torch.set_num_threads(max(1, cpus // world))
     from ..parallel import process_group as pg
     if backend == "nccl":
         pg.rccl_env(0, timing=True)  # per-collective durations (bucket_ms)

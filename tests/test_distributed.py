@@ -699,19 +699,23 @@ def _rccl_single_rank_worker(rank, world):
 
     from distributed_tensorflow_models_amd.engine import TrainStep, moving_average_buffers
     from distributed_tensorflow_models_amd.models import nets_factory
+    import sys
     assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
     dev = torch.device("cuda", 0)
     out = {}
     for forced in (False, True):
+        print("rccl worker: forced %s" % forced, file=sys.stderr, flush=True)
         torch.manual_seed(0)
         model = nets_factory.build("resnet_v1_50", num_classes=16).to(dev)
         step = TrainStep(model, optimizer="momentum", lr=0.05, momentum=0.9, bucket_mb=2.0, force_comm=forced)
         g = torch.Generator().manual_seed(5)
         x = torch.randn(8, 64, 64, 3, generator=g).to(dev, torch.bfloat16)
         y = torch.randint(0, 16, (8,), generator=g).to(dev)
-        for _ in range(2):
+        for i in range(2):
             step(x, y)
+            print("rccl worker: step %d issued" % i, file=sys.stderr, flush=True)
         torch.cuda.synchronize()
+        print("rccl worker: synchronized", file=sys.stderr, flush=True)
         out[forced] = {"params": torch.cat([p.detach().float().reshape(-1) for p in model.parameters()]).cpu(),
                        "bufs": torch.cat([b.detach().reshape(-1) for b in moving_average_buffers(model)]).cpu(),
                        "works": len(step.dp._done_works), "buckets": len(step.dp.buckets),
