@@ -152,7 +152,10 @@ def lib():
                 "native kernel library %s is missing: run `python tools/build_native.py` "
                 "(or __graft_entry__.build())" % LIB_PATH)
         L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        ab = bool(os.environ.get("DTM_KERNELS_SO"))
         for name, (res, args) in _SIGS.items():
+            if ab and not hasattr(L, name):  # an A/B baseline build older than this binding: its missing entry
+                continue                     # points stay unbound (only the default library is checked in full)
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -126,8 +126,9 @@ def main():
         if os.environ.get("WTILES"):
             wts = [tuple(int(u) for u in t.split(":")) for t in os.environ["WTILES"].split(",")]
             dw = torch.zeros(K, R, S, C, device="cuda")
-            fn = lambda: L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(dw), None, None, ctypes.byref(d),  # noqa
-                                          _lib.num_cus(), st)
+            pro = (_lib.ptr(sc), _lib.ptr(sh)) if os.environ.get("WPRO") else (None, None)  # BN-apply prologue on x
+            fn = lambda: L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(dw), pro[0], pro[1],  # noqa
+                                          ctypes.byref(d), _lib.num_cus(), st)
             res = {t: [] for t in wts}
             for _ in range(ROUNDS):
                 for t in wts:
