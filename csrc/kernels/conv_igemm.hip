@@ -1980,6 +1980,7 @@ static const bf16_t* zero_chunk() {
   }
   return (const bf16_t*)z;
 }
+const void* dtm_zero_chunk() { return zero_chunk(); }  // (the stem-pool kernels' out-of-range tap source)
 
 template <int PT, int CT, int NWP, int NS, int UD, bool SPL = false>
 static void launch_w8(const ConvNTArgs& a, hipStream_t st) {

@@ -319,6 +319,166 @@ __global__ __launch_bounds__(256) void maxpool_bnrelu_bwd_kernel(const bf16_t* _
   col_reduce8(red, a1, a0, prow, prow + a.C, cols, c0);
 }
 
+// ---- 3x3 / stride-2 specialisations (the ResNet-50 and Inception-v3 stem pools) ----
+// Forward: one lane = two vertically adjacent outputs (p, p + 1) of one 8-channel column: their windows share an
+// input row, so 15 16-B loads (5 rows x 3 columns) instead of 18, all issued before any is used (compile-time
+// window, predicated: an out-of-range tap reads a zero chunk and is never selected).  Same scan order and strict
+// comparison as maxpool_bnrelu_fwd_kernel: the same maxima and the same first-maximum argmax bytes.
+__global__ __launch_bounds__(256) void maxpool_bnrelu_fwd_k3s2_kernel(const bf16_t* __restrict__ x,
+                                                                      const float* __restrict__ ss,
+                                                                      bf16_t* __restrict__ y, uint8_t* __restrict__ arg,
+                                                                      PoolArgs a, FastDiv fd_cols, FastDiv fd_Q,
+                                                                      FastDiv fd_P2, const bf16_t* __restrict__ zero) {
+  const uint32_t cols = a.C >> 3, P2 = (a.P + 1) >> 1, total = (uint32_t)a.N * P2 * a.Q * cols;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const uint32_t o = fdiv(i, fd_cols), cv = (i - o * cols) * 8;
+    const uint32_t t = fdiv(o, fd_Q), q = o - t * a.Q;
+    const uint32_t n = fdiv(t, fd_P2), p0 = (t - n * P2) * 2;
+    float sc[8], sh[8];
+    {
+      const float4 s0 = *(const float4*)(ss + cv), s1 = *(const float4*)(ss + cv + 4);
+      const float4 h0 = *(const float4*)(ss + a.C + cv), h1 = *(const float4*)(ss + a.C + cv + 4);
+      sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+      sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w; sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
+    }
+    const int h0 = (int)p0 * 2 - a.PH, w0 = (int)q * 2 - a.PW;
+    uint4 v[5][3];
+    bool ok[5][3];
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int h = h0 + r, w = w0 + c;
+        ok[r][c] = h >= 0 && h < a.H && w >= 0 && w < a.W;
+        v[r][c] = *(const uint4*)(ok[r][c] ? x + (((size_t)n * a.H + h) * a.W + w) * a.C + cv : zero);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const uint32_t p = p0 + u;
+      if (p >= (uint32_t)a.P) break;
+      float best[8];
+      uint32_t bi[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          if (!ok[2 * u + r][c]) continue;
+          const uint4 w4 = v[2 * u + r][c];
+          const float f[8] = {lo_bf(w4.x), hi_bf(w4.x), lo_bf(w4.y), hi_bf(w4.y),
+                              lo_bf(w4.z), hi_bf(w4.z), lo_bf(w4.w), hi_bf(w4.w)};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float val = fmaxf(fmaf(f[e], sc[e], sh[e]), 0.f);
+            if (val > best[e]) { best[e] = val; bi[e] = (uint32_t)(r * 3 + c); }
+          }
+        }
+      }
+      const size_t oo = (((size_t)n * a.P + p) * a.Q + q) * a.C + cv;
+      st<8>(y + oo, best);
+      *(uint2*)(arg + oo) = make_uint2(bi[0] | bi[1] << 8 | bi[2] << 16 | bi[3] << 24,
+                                       bi[4] | bi[5] << 8 | bi[6] << 16 | bi[7] << 24);
+    }
+  }
+}
+
+// Backward: one lane = a 2 x 2 block of input pixels (rows 2bi - PH + {0, 1}, columns 2bj - PW + {0, 1}) of one
+// 8-channel column.  Every window that covers a pixel of the block is one of the 2 x 2 windows (bi - 1 .. bi,
+// bj - 1 .. bj), so their gradient and argmax are loaded once for four pixels (the per-pixel gather of
+// maxpool_bnrelu_bwd_kernel loaded them for each pixel: 4x the L2 traffic); each pixel adds its matching windows
+// in the same ascending (p, q) order as that kernel - bit-identical dx.  BN-apply backward and the per-block
+// partial sums (sum g*x, sum g) as there.
+__global__ __launch_bounds__(256) void maxpool_bnrelu_bwd_k3s2_kernel(const bf16_t* __restrict__ dy,
+                                                                      const uint8_t* __restrict__ arg,
+                                                                      const bf16_t* __restrict__ x,
+                                                                      const float* __restrict__ ss,
+                                                                      bf16_t* __restrict__ dx, float* __restrict__ part,
+                                                                      PoolArgs a, FastDiv fd_BW, FastDiv fd_BH,
+                                                                      int unscaled, int rpb, const bf16_t* __restrict__ zero) {
+  __shared__ float red[2][256][8];
+  const int cols = a.C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t % cols) * 8, lr0 = t / cols;
+  const int BH = (a.H + a.PH + 1) >> 1, BW = (a.W + a.PW + 1) >> 1;
+  float sc[8], sh[8], a1[8], a0[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { sc[e] = ss[c0 + e]; sh[e] = ss[a.C + c0 + e]; a1[e] = 0.f; a0[e] = 0.f; }
+  const int M = a.N * BH * BW;
+  const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
+  for (int blk = lr0 < RP ? r0 + lr0 : r1; blk < r1; blk += RP) {
+    const uint32_t tt = fdiv((uint32_t)blk, fd_BW), bj = blk - tt * BW;
+    const uint32_t n = fdiv(tt, fd_BH), bi = tt - n * BH;
+    uint4 gv[2][2];
+    uint2 av[2][2];
+    bool wv[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int p = (int)bi - 1 + i, q = (int)bj - 1 + j;
+        wv[i][j] = p >= 0 && p < a.P && q >= 0 && q < a.Q;
+        const size_t oo = wv[i][j] ? (((size_t)n * a.P + p) * a.Q + q) * a.C + c0 : 0;
+        gv[i][j] = *(const uint4*)(wv[i][j] ? dy + oo : zero);
+        av[i][j] = wv[i][j] ? *(const uint2*)(arg + oo) : make_uint2(0xffffffffu, 0xffffffffu);
+      }
+    }
+    uint4 xv[2][2];
+    bool pv[2][2];
+    const int hb = (int)bi * 2 - a.PH, wb = (int)bj * 2 - a.PW;
+#pragma unroll
+    for (int di = 0; di < 2; ++di) {
+#pragma unroll
+      for (int dj = 0; dj < 2; ++dj) {
+        const int h = hb + di, w = wb + dj;
+        pv[di][dj] = h >= 0 && h < a.H && w >= 0 && w < a.W;
+        xv[di][dj] = *(const uint4*)(pv[di][dj] ? x + (((size_t)n * a.H + h) * a.W + w) * a.C + c0 : zero);
+      }
+    }
+#pragma unroll
+    for (int di = 0; di < 2; ++di) {
+#pragma unroll
+      for (int dj = 0; dj < 2; ++dj) {
+        if (!pv[di][dj]) continue;
+        float acc[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            // pixel (hb + di, wb + dj) in window (bi - 1 + i, bj - 1 + j): tap r = di + 2 (1 - i), s = dj + 2 (1 - j)
+            const int r = di + 2 * (1 - i), sidx = dj + 2 * (1 - j);
+            if (!wv[i][j] || r > 2 || sidx > 2) continue;
+            const uint32_t want = (uint32_t)(r * 3 + sidx);
+            const uint4 g4 = gv[i][j];
+            const float g[8] = {lo_bf(g4.x), hi_bf(g4.x), lo_bf(g4.y), hi_bf(g4.y),
+                                lo_bf(g4.z), hi_bf(g4.z), lo_bf(g4.w), hi_bf(g4.w)};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const uint32_t b = ((e < 4 ? av[i][j].x : av[i][j].y) >> (8 * (e & 3))) & 0xffu;
+              if (b == want) acc[e] += g[e];
+            }
+          }
+        }
+        const uint4 x4 = xv[di][dj];
+        const float xf[8] = {lo_bf(x4.x), hi_bf(x4.x), lo_bf(x4.y), hi_bf(x4.y),
+                             lo_bf(x4.z), hi_bf(x4.z), lo_bf(x4.w), hi_bf(x4.w)};
+        float d[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float g = fmaf(xf[e], sc[e], sh[e]) > 0.f ? acc[e] : 0.f;
+          d[e] = unscaled ? g : g * sc[e];
+          a1[e] += g * xf[e];
+          a0[e] += g;
+        }
+        st<8>(dx + (((size_t)n * a.H + hb + di) * a.W + wb + dj) * a.C + c0, d);
+      }
+    }
+  }
+  float* prow = part + (size_t)blockIdx.x * 2 * a.C;
+  col_reduce8(red, a1, a0, prow, prow + a.C, cols, c0);
+}
+
 }  // namespace dtm
 using namespace dtm;
 
@@ -373,8 +533,23 @@ DTM_API void dtm_global_avg_bwd(const float* dy, void* dx, int N, int HW, int C,
 }
 
 // y = maxpool(relu(x*scale + shift)) with a uint8 argmax per output element (ss = [scale; shift; ...])
+static int g_pool_k3s2 = 1;  // A/B knob (dtm_pool_set_k3s2): the 3x3 / stride-2 specialised stem-pool kernels
+DTM_API void dtm_pool_set_k3s2(int on) { g_pool_k3s2 = on; }
+static bool k3s2(const PoolArgs* a) {
+  return g_pool_k3s2 && a->KH == 3 && a->KW == 3 && a->SH == 2 && a->SW == 2 && a->PH >= 0 && a->PH <= 1 &&
+         a->PW >= 0 && a->PW <= 1;
+}
+const void* dtm_zero_chunk();  // >= 16 B of device zeros (conv_igemm.hip)
+
 DTM_API int dtm_maxpool_bnrelu_fwd(const void* x, const float* ss, void* y, void* arg, const PoolArgs* a, void* stream) {
   if (a->C % 8 || a->KH * a->KW > 255 || (long)a->N * a->H * a->W * a->C >= (1l << 31)) return -1;
+  if (k3s2(a)) {
+    const long work = (long)a->N * ((a->P + 1) / 2) * a->Q * (a->C / 8);
+    hipLaunchKernelGGL(maxpool_bnrelu_fwd_k3s2_kernel, dim3(pgrid(work)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)x, ss, (bf16_t*)y, (uint8_t*)arg, *a, make_fastdiv(a->C / 8), make_fastdiv(a->Q),
+                       make_fastdiv((a->P + 1) / 2), (const bf16_t*)dtm_zero_chunk());
+    return 0;
+  }
   const long work = (long)a->N * a->P * a->Q * (a->C / 8);
   hipLaunchKernelGGL(maxpool_bnrelu_fwd_kernel, dim3(pgrid(work)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
                      ss, (bf16_t*)y, (uint8_t*)arg, *a, make_fastdiv(a->C / 8), make_fastdiv(a->Q), make_fastdiv(a->P));
@@ -387,6 +562,23 @@ DTM_API int dtm_maxpool_bnrelu_bwd(const void* dy, const void* arg, const void* 
   if (a->C % 8 || a->C / 8 > 256 || (long)a->N * a->H * a->W * a->C >= (1l << 31)) return -1;
   if ((a->KH + a->SH - 1) / a->SH > 3 || (a->KW + a->SW - 1) / a->SW > 3) return -2;
   const int cols = a->C / 8, RP = 256 / cols;
+  if (k3s2(a)) {  // one row = a 2 x 2 block of input pixels
+    const int BH = (a->H + a->PH + 1) / 2, BW = (a->W + a->PW + 1) / 2;
+    const long MB = (long)a->N * BH * BW;
+    long b = MB * cols / (256 * 2);
+    if (b < 1) b = 1;
+    if (b > 2048) b = 2048;
+    long rpb = (MB + b - 1) / b;
+    rpb = (rpb + RP - 1) / RP * RP;
+    const int blocks = (int)((MB + rpb - 1) / rpb);
+    float* ws = dtm_ws_get_stream((size_t)blocks * 2 * a->C, (hipStream_t)stream);
+    if (!ws) return -4;
+    hipLaunchKernelGGL(maxpool_bnrelu_bwd_k3s2_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)dy, (const uint8_t*)arg, (const bf16_t*)x, ss, (bf16_t*)dx, ws, *a,
+                       make_fastdiv(BW), make_fastdiv(BH), unscaled, (int)rpb, (const bf16_t*)dtm_zero_chunk());
+    dtm_reduce_rows(ws, blocks, 2 * a->C, 2 * a->C, sums, (hipStream_t)stream);
+    return 0;
+  }
   const long M = (long)a->N * a->H * a->W;
   long b = M * cols / (256 * 8);
   if (b < 1) b = 1;

@@ -266,6 +266,63 @@ def test_conv_act_dgrad_tiles_match_reference(tile, case):
     assert _rel(sums[1], gref.sum((0, 1, 2))) < 1e-2
 
 
+@pytest.mark.parametrize("case", [(4, 112, 112, 64, "SAME"), (3, 147, 147, 64, "VALID"), (2, 71, 71, 192, "VALID"),
+                                  (2, 15, 14, 16, "SAME"), (3, 9, 10, 8, "VALID"), (2, 13, 13, 24, "SAME")])
+@pytest.mark.parametrize("unscaled", [0, 1])
+def test_maxpool_bnrelu_k3s2_matches_generic(case, unscaled):
+    """The 3x3 / stride-2 stem-pool kernels (two outputs per lane forward, a 2x2 input block per lane backward) vs the
+    generic gather kernels: pooled output and argmax bytes bit-identical (same scan order, strict comparison), input
+    gradient bit-identical (same window order), the BN-gradient sums equal up to the summation order; and both
+    against fp32 torch (max_pool2d of relu(x*scale+shift), its gradient)."""
+    import ctypes
+
+    import torch.nn.functional as tF
+
+    from distributed_tensorflow_models_amd.ops import _lib
+    from distributed_tensorflow_models_amd.ops.geometry import pool_geom
+    N, H, W, C, pad = case
+    torch.manual_seed(7)
+    L = _lib.lib()
+    s = _lib.stream_ptr()
+    raw = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16)
+    sc, sh = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.3
+    ss = torch.stack([sc, sh, sh, sc]).contiguous()
+    g = pool_geom(tuple(raw.shape), 3, 2, pad)
+    a = g.as_args(_lib.PoolArgs)
+    dy = torch.randn(N, g.P, g.Q, C, device=DEV).to(torch.bfloat16)
+    out = {}
+    for fast in (1, 0):
+        L.dtm_pool_set_k3s2(fast)
+        try:
+            y = torch.empty(N, g.P, g.Q, C, device=DEV, dtype=torch.bfloat16)
+            arg = torch.empty(N, g.P, g.Q, C, device=DEV, dtype=torch.uint8)
+            assert L.dtm_maxpool_bnrelu_fwd(_lib.ptr(raw), _lib.ptr(ss), _lib.ptr(y), _lib.ptr(arg), ctypes.byref(a),
+                                            s) == 0
+            dx = torch.empty_like(raw)
+            sums = torch.zeros(4, C, device=DEV)
+            assert L.dtm_maxpool_bnrelu_bwd(_lib.ptr(dy), _lib.ptr(arg), _lib.ptr(raw), _lib.ptr(ss), _lib.ptr(dx),
+                                            _lib.ptr(sums), ctypes.byref(a), unscaled, s) == 0
+            torch.cuda.synchronize()
+        finally:
+            L.dtm_pool_set_k3s2(1)
+        out[fast] = (y, arg, dx, sums)
+    for i in range(3):
+        assert torch.equal(out[1][i], out[0][i]), i
+    assert _rel(out[1][3][:2], out[0][3][:2]) < 1e-5
+    # fp32 reference (NCHW torch pooling; TF SAME padding as explicit -inf pads)
+    act = torch.relu(raw.float() * sc + sh).permute(0, 3, 1, 2).contiguous().requires_grad_()
+    padded = tF.pad(act, (g.PW, g.PR, g.PH, g.PB), value=-1e30)
+    yr = tF.max_pool2d(padded, 3, 2)
+    assert _rel(out[1][0].float().permute(0, 3, 1, 2), yr) < 1e-2
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    m = (raw.float() * sc + sh > 0).float()
+    gref = act.grad.permute(0, 2, 3, 1) * m  # (ties: torch and the kernels may route to different maxima)
+    want = gref if unscaled else gref * sc
+    assert _rel(out[1][2].float(), want) < 2e-2
+    assert _rel(out[1][3][0], (gref * raw.float()).sum((0, 1, 2))) < 2e-2
+    assert _rel(out[1][3][1], gref.sum((0, 1, 2))) < 2e-2
+
+
 @pytest.mark.parametrize("case", [(8, 17, 17, 192, 768, 1, 1, False), (8, 8, 8, 320, 1280, 3, 1, False),
                                   (4, 17, 17, 160, 192, 7, 1, True), (4, 35, 35, 96, 288, 3, 2, False),
                                   (16, 17, 17, 128, 768, 1, 1, True)])
