@@ -61,8 +61,6 @@ struct ConvNTArgs {
   float* act_sums;        //   partial rows per pixel tile: [sum g*act_x (K) | sum g (K)]
   const bf16_t* zero;     // >= 16 B of zeros: the LDS-DMA source of padding / out-of-range chunks
   int act_unscaled;       // act path: out <- g (not g*scale); the producer's conv+BN backward scales it
-  int act_atomic;         // act path: act_sums is the final (zeroed) [g*x | g] (+ [g*r | g] at 4K) buffer and every
-                          //   pixel tile adds its sums with fp32 atomics - no partial rows, no reduction launch
   const uint8_t* act_mask;  // act path, block-output form: the ReLU mask is the forward's bitmask (1 bit per
                             //   element) of relu(bn(act_x) + residual) instead of act_x*scale+shift > 0
   const bf16_t* act_r;      //   + a BN'd residual: also sum g*act_r -> rows [g*x | g | g*r | g] (4K wide)
@@ -365,18 +363,14 @@ __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem
     // every thread finishes one (chunk column, value) output: NT/CPR partials each, instead of CPR
     // threads walking all NT rows of the table serially
     const int rw = (act && a.act_r) ? 4 : 2;  // row width in K units
-    const bool atom = act && a.act_atomic;
-    float* prow = (act ? a.act_sums : a.stats) + (atom ? (size_t)0 : (size_t)by * (rw * a.K));
+    float* prow = (act ? a.act_sums : a.stats) + (size_t)by * (rw * a.K);
     for (int o = tid; o < CPR * 16; o += NT) {
       const int c = o >> 4, e = o & 15;
       float t = 0.f;
 #pragma unroll 4
       for (int k = 0; k < NT / CPR; ++k) t += red[((c + k * CPR) << 4) + e];
       const int kk = c0 + c * 8 + (e & 7);
-      if (kk < a.K) {
-        if (atom) atomicAdd(prow + (e < 8 ? 0 : a.K) + kk, t);
-        else prow[(e < 8 ? 0 : a.K) + kk] = t;
-      }
+      if (kk < a.K) prow[(e < 8 ? 0 : a.K) + kk] = t;
     }
     if (act && a.act_r) {  // second round: [sum g*r | sum g] of the BN'd residual
       epi_barrier<RAWB>();
@@ -389,10 +383,7 @@ __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem
 #pragma unroll 4
         for (int k = 0; k < NT / CPR; ++k) t += red[((c + k * CPR) << 4) + e];
         const int kk = c0 + c * 8 + (e & 7);
-        if (kk < a.K) {  // (the final buffer keeps the residual's pair at rows 4-5: 4K)
-          if (atom) atomicAdd(prow + 4 * a.K + (e < 8 ? 0 : a.K) + kk, t);
-          else prow[2 * a.K + (e < 8 ? 0 : a.K) + kk] = t;
-        }
+        if (kk < a.K) prow[2 * a.K + (e < 8 ? 0 : a.K) + kk] = t;
       }
     }
   }
@@ -2312,7 +2303,6 @@ static int conv_fwd_impl(const void* x, const void* w, void* y, bool stats, cons
   a.act_mask = nullptr; a.act_r = nullptr;
   a.add_stride = 1; a.add_H = a.add_W = 0;
   a.act_unscaled = 0;
-  a.act_atomic = 0;
   a.zero = zero_chunk();
   a.dump = dump_chunk();
   a.pix_bytes = d->pix_bytes > 0 ? d->pix_bytes : d->C * 2;
@@ -2468,9 +2458,6 @@ DTM_API void dtm_conv_set_dec_lpt(int on) { g_dec_lpt = on; }
 static int g_dec_tile = 1;
 DTM_API void dtm_conv_set_dec_tile(int on) { g_dec_tile = on; }
 
-static int g_act_atomic = 1;  // A/B knob (dtm_conv_set_act_atomic)
-DTM_API void dtm_conv_set_act_atomic(int on) { g_act_atomic = on; }
-static constexpr int ACT_ATOMIC_ROWS = 300;  // (512 took ResNet-50's 14x14 act dgrads, 392 tiles: -0.3 % step)
 static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvDesc* d, const void* add_src,
                            int add_stride, const void* act_x, const float* act_ss, float* act_sums, int act_unscaled,
                            const void* act_mask, const void* act_r, void* stream) {
@@ -2487,7 +2474,6 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvD
   a.act_mask = (const uint8_t*)act_mask; a.act_r = (const bf16_t*)act_r;
   a.add_stride = add_stride;
   a.act_unscaled = act_unscaled;
-  a.act_atomic = 0;
   a.zero = zero_chunk();
   a.dump = dump_chunk();
   a.add_H = (d->H - 1) / add_stride + 1; a.add_W = (d->W - 1) / add_stride + 1;
@@ -2567,22 +2553,14 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvD
       }
     }
   }
-  // the BN-gradient sums straight into act_sums with fp32 atomics from every pixel tile when there are few tiles
-  // (one per 128 / 256 output pixels: <= ACT_ATOMIC_ROWS adders per address) - the partial-row table and its
-  // reduction launch disappear (Inception-v3's 17x17 / 8x8 blocks).  Staged-epilogue kernels only (the persistent
-  // kernels keep per-worker rows); deterministic mode keeps the fixed-order table.
-  bool atomic = act_x && !dtm_get_deterministic() && g_act_atomic && rows <= ACT_ATOMIC_ROWS;
-  for (int i = 0; atomic && i < nl; ++i) atomic = lt[i].id != 30 && lt[i].id != 31 && lt[i].id != 33 && lt[i].id != 60;
   float* ws = nullptr;
-  if (act_x && !atomic) {
+  if (act_x) {
     ws = dtm_ws_get_stream((size_t)rows * rw * d->C, (hipStream_t)stream);
     if (!ws) return -4;
   }
-  for (int i = 0, r = 0; i < nl; r += lrows[i], ++i) {
+  for (int i = 0, r = 0; i < nl; r += lrows[i], ++i)
     // every launch's partial-sum rows go to its own slice of one table, reduced together below
-    if (act_x) la[i].act_sums = atomic ? act_sums : ws + (size_t)r * rw * d->C;
-    la[i].act_atomic = atomic;
-  }
+    if (act_x) la[i].act_sums = ws + (size_t)r * rw * d->C;
   if (gi >= 0) {
     ConvNTArgs g = la[gi];
     g.ngrp = nl;
@@ -2604,7 +2582,6 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvD
   } else {
     for (int i = 0; i < nl; ++i) dispatch_nt(la[i], dec ? 1 : st, lt[i], (hipStream_t)stream);
   }
-  if (atomic) return 0;
   if (act_x && act_r) {
     // [sum g*x | sum g] -> act_sums rows 0-1, [sum g*r | sum g] -> rows 4-5 of an [8][C] buffer: rows 0-3
     // and 4-7 are then directly the ss gradients of the two BatchNorms (no copies)

@@ -323,64 +323,6 @@ def test_maxpool_bnrelu_k3s2_matches_generic(case, unscaled):
     assert _rel(out[1][3][1], gref.sum((0, 1, 2))) < 2e-2
 
 
-@pytest.mark.parametrize("case", [(8, 17, 17, 192, 768, 1, 1, False), (8, 8, 8, 320, 1280, 3, 1, False),
-                                  (4, 17, 17, 160, 192, 7, 1, True), (4, 35, 35, 96, 288, 3, 2, False),
-                                  (16, 17, 17, 128, 768, 1, 1, True)])
-def test_conv_dgrad_act_atomic_sums_match_partial_rows(case):
-    """The BN-gradient sums of an act / block-output dgrad added straight into the final buffer with fp32 atomics from
-    every pixel tile (few tiles: Inception's 17x17 / 8x8 maps) vs the per-tile partial-row table + reduction it
-    replaces: dx bit-identical, sums (rows 0-1, and rows 4-5 of the block-output form with a residual) equal up to
-    the summation order; covers the grouped stride-2 parity classes."""
-    import ctypes
-
-    from distributed_tensorflow_models_amd.ops import _lib
-    from distributed_tensorflow_models_amd.ops.geometry import conv_geom
-    N, H, W, K, C, R, st, bnout = case  # K: the dgrad's reduction (conv output channels), C: its output channels
-    torch.manual_seed(5)
-    L = _lib.lib()
-    s = _lib.stream_ptr()
-    x = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16)
-    w = (torch.randn(K, R, R, C, device=DEV) / (R * R * C) ** 0.5).to(torch.bfloat16)
-    pad = "VALID" if st > 1 else "SAME"
-    g = conv_geom(tuple(x.shape), tuple(w.shape), st, pad)
-    d = g.as_desc(_lib.ConvDesc)
-    wt = torch.empty(C, R, R, K, device=DEV, dtype=torch.bfloat16)
-    if st > 1:
-        L.dtm_weight_flip_transpose_dec(_lib.ptr(w), _lib.ptr(wt), K, R, R, C, st, g.pad_h, g.pad_w, s)
-        d.dec = 1
-    else:
-        L.dtm_weight_flip_transpose(_lib.ptr(w), _lib.ptr(wt), K, R, R, C, s)
-    dy = torch.randn(N, g.P, g.Q, K, device=DEV).to(torch.bfloat16)
-    ss4 = torch.stack([torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.3, torch.zeros(C, device=DEV),
-                       torch.ones(C, device=DEV)]).contiguous()
-    rr = torch.randn_like(x)
-    add = torch.randn_like(x)
-    mask = (torch.rand(x.numel() // 8, device=DEV) * 255).to(torch.uint8)
-    out = {}
-    for atomic in (1, 0):
-        L.dtm_conv_set_act_atomic(atomic)
-        try:
-            dx = torch.empty_like(x)
-            sums = torch.zeros(8, C, device=DEV)
-            if bnout:
-                rc = L.dtm_conv_dgrad_bnout(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), _lib.ptr(add), 1,
-                                            _lib.ptr(mask), _lib.ptr(x), _lib.ptr(rr), _lib.ptr(sums), s)
-            else:
-                rc = L.dtm_conv_dgrad_ex(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d), None, 1, _lib.ptr(x),
-                                         _lib.ptr(ss4), _lib.ptr(sums), 1, s)
-            assert rc == 0
-            torch.cuda.synchronize()
-        finally:
-            L.dtm_conv_set_act_atomic(1)
-        out[atomic] = (dx, sums)
-    assert torch.equal(out[1][0], out[0][0])
-    rows = [0, 1, 4, 5] if bnout else [0, 1]
-    for r in rows:
-        assert _rel(out[1][1][r], out[0][1][r]) < 1e-5, (r, _rel(out[1][1][r], out[0][1][r]))
-    assert out[1][1][rows].abs().sum() > 0
-    assert not out[1][1][2:4].any() and (bnout or not out[1][1][4:].any())
-
-
 @pytest.mark.parametrize("case", [(4, 28, 28, 64, 256, True, True), (4, 28, 28, 64, 256, False, True),
                                   (3, 13, 13, 128, 512, True, False), (2, 9, 11, 128, 384, False, True),
                                   (5, 14, 14, 64, 128, True, True), (3, 14, 14, 256, 1024, False, True),
