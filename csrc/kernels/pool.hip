@@ -319,11 +319,13 @@ __global__ __launch_bounds__(256) void maxpool_bnrelu_bwd_kernel(const bf16_t* _
   col_reduce8(red, a1, a0, prow, prow + a.C, cols, c0);
 }
 
-// ---- 3x3 / stride-2 specialisations (the ResNet-50 and Inception-v3 stem pools) ----
+// ---- 3x3 / stride-2 specialisations (the ResNet-50 and Inception-v3 stem pools; BN = false: the plain max pools
+// of Inception's grid-reduction blocks) ----
 // Forward: one lane = two vertically adjacent outputs (p, p + 1) of one 8-channel column: their windows share an
 // input row, so 15 16-B loads (5 rows x 3 columns) instead of 18, all issued before any is used (compile-time
 // window, predicated: an out-of-range tap reads a zero chunk and is never selected).  Same scan order and strict
-// comparison as maxpool_bnrelu_fwd_kernel: the same maxima and the same first-maximum argmax bytes.
+// comparison as maxpool_bnrelu_fwd_kernel / maxpool_fwd_kernel: the same maxima and first-maximum argmax bytes.
+template <bool BN>
 __global__ __launch_bounds__(256) void maxpool_bnrelu_fwd_k3s2_kernel(const bf16_t* __restrict__ x,
                                                                       const float* __restrict__ ss,
                                                                       bf16_t* __restrict__ y, uint8_t* __restrict__ arg,
@@ -335,7 +337,7 @@ __global__ __launch_bounds__(256) void maxpool_bnrelu_fwd_k3s2_kernel(const bf16
     const uint32_t t = fdiv(o, fd_Q), q = o - t * a.Q;
     const uint32_t n = fdiv(t, fd_P2), p0 = (t - n * P2) * 2;
     float sc[8], sh[8];
-    {
+    if constexpr (BN) {
       const float4 s0 = *(const float4*)(ss + cv), s1 = *(const float4*)(ss + cv + 4);
       const float4 h0 = *(const float4*)(ss + a.C + cv), h1 = *(const float4*)(ss + a.C + cv + 4);
       sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
@@ -371,7 +373,7 @@ __global__ __launch_bounds__(256) void maxpool_bnrelu_fwd_k3s2_kernel(const bf16
                               lo_bf(w4.z), hi_bf(w4.z), lo_bf(w4.w), hi_bf(w4.w)};
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const float val = fmaxf(fmaf(f[e], sc[e], sh[e]), 0.f);
+            const float val = BN ? fmaxf(fmaf(f[e], sc[e], sh[e]), 0.f) : f[e];
             if (val > best[e]) { best[e] = val; bi[e] = (uint32_t)(r * 3 + c); }
           }
         }
@@ -389,7 +391,8 @@ __global__ __launch_bounds__(256) void maxpool_bnrelu_fwd_k3s2_kernel(const bf16
 // bj - 1 .. bj), so their gradient and argmax are loaded once for four pixels (the per-pixel gather of
 // maxpool_bnrelu_bwd_kernel loaded them for each pixel: 4x the L2 traffic); each pixel adds its matching windows
 // in the same ascending (p, q) order as that kernel - bit-identical dx.  BN-apply backward and the per-block
-// partial sums (sum g*x, sum g) as there.
+// partial sums (sum g*x, sum g) as there (BN = false: the plain max-pool gradient, maxpool_bwd_kernel's).
+template <bool BN>
 __global__ __launch_bounds__(256) void maxpool_bnrelu_bwd_k3s2_kernel(const bf16_t* __restrict__ dy,
                                                                       const uint8_t* __restrict__ arg,
                                                                       const bf16_t* __restrict__ x,
@@ -397,12 +400,16 @@ __global__ __launch_bounds__(256) void maxpool_bnrelu_bwd_k3s2_kernel(const bf16
                                                                       bf16_t* __restrict__ dx, float* __restrict__ part,
                                                                       PoolArgs a, FastDiv fd_BW, FastDiv fd_BH,
                                                                       int unscaled, int rpb, const bf16_t* __restrict__ zero) {
-  __shared__ float red[2][256][8];
   const int cols = a.C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t % cols) * 8, lr0 = t / cols;
   const int BH = (a.H + a.PH + 1) >> 1, BW = (a.W + a.PW + 1) >> 1;
   float sc[8], sh[8], a1[8], a0[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) { sc[e] = ss[c0 + e]; sh[e] = ss[a.C + c0 + e]; a1[e] = 0.f; a0[e] = 0.f; }
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = BN ? ss[c0 + e] : 1.f;
+    sh[e] = BN ? ss[a.C + c0 + e] : 0.f;
+    a1[e] = 0.f;
+    a0[e] = 0.f;
+  }
   const int M = a.N * BH * BW;
   const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
   for (int blk = lr0 < RP ? r0 + lr0 : r1; blk < r1; blk += RP) {
@@ -431,7 +438,8 @@ __global__ __launch_bounds__(256) void maxpool_bnrelu_bwd_k3s2_kernel(const bf16
       for (int dj = 0; dj < 2; ++dj) {
         const int h = hb + di, w = wb + dj;
         pv[di][dj] = h >= 0 && h < a.H && w >= 0 && w < a.W;
-        xv[di][dj] = *(const uint4*)(pv[di][dj] ? x + (((size_t)n * a.H + h) * a.W + w) * a.C + c0 : zero);
+        if constexpr (BN)
+          xv[di][dj] = *(const uint4*)(pv[di][dj] ? x + (((size_t)n * a.H + h) * a.W + w) * a.C + c0 : zero);
       }
     }
 #pragma unroll
@@ -460,23 +468,31 @@ __global__ __launch_bounds__(256) void maxpool_bnrelu_bwd_k3s2_kernel(const bf16
             }
           }
         }
-        const uint4 x4 = xv[di][dj];
-        const float xf[8] = {lo_bf(x4.x), hi_bf(x4.x), lo_bf(x4.y), hi_bf(x4.y),
-                             lo_bf(x4.z), hi_bf(x4.z), lo_bf(x4.w), hi_bf(x4.w)};
         float d[8];
+        if constexpr (BN) {
+          const uint4 x4 = xv[di][dj];
+          const float xf[8] = {lo_bf(x4.x), hi_bf(x4.x), lo_bf(x4.y), hi_bf(x4.y),
+                               lo_bf(x4.z), hi_bf(x4.z), lo_bf(x4.w), hi_bf(x4.w)};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float g = fmaf(xf[e], sc[e], sh[e]) > 0.f ? acc[e] : 0.f;
-          d[e] = unscaled ? g : g * sc[e];
-          a1[e] += g * xf[e];
-          a0[e] += g;
+          for (int e = 0; e < 8; ++e) {
+            const float g = fmaf(xf[e], sc[e], sh[e]) > 0.f ? acc[e] : 0.f;
+            d[e] = unscaled ? g : g * sc[e];
+            a1[e] += g * xf[e];
+            a0[e] += g;
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) d[e] = acc[e];
         }
         st<8>(dx + (((size_t)n * a.H + hb + di) * a.W + wb + dj) * a.C + c0, d);
       }
     }
   }
-  float* prow = part + (size_t)blockIdx.x * 2 * a.C;
-  col_reduce8(red, a1, a0, prow, prow + a.C, cols, c0);
+  if constexpr (BN) {
+    __shared__ float red[2][256][8];
+    float* prow = part + (size_t)blockIdx.x * 2 * a.C;
+    col_reduce8(red, a1, a0, prow, prow + a.C, cols, c0);
+  }
 }
 
 }  // namespace dtm
@@ -487,8 +503,23 @@ static int pgrid(long work) {
   return (int)(b < 1 ? 1 : (b > 4096 ? 4096 : b));
 }
 
+static int g_pool_k3s2 = 1;  // A/B knob (dtm_pool_set_k3s2): the 3x3 / stride-2 specialised stem-pool kernels
+DTM_API void dtm_pool_set_k3s2(int on) { g_pool_k3s2 = on; }
+static bool k3s2(const PoolArgs* a) {
+  return g_pool_k3s2 && a->KH == 3 && a->KW == 3 && a->SH == 2 && a->SW == 2 && a->PH >= 0 && a->PH <= 1 &&
+         a->PW >= 0 && a->PW <= 1;
+}
+const void* dtm_zero_chunk();  // >= 16 B of device zeros (conv_igemm.hip)
+
 DTM_API void dtm_maxpool_fwd(const void* x, void* y, void* arg, const PoolArgs* a, void* stream) {
   long work = (long)a->N * a->P * a->Q * a->C;
+  if (a->C % 8 == 0 && arg && k3s2(a) && (long)a->N * a->H * a->W * a->C < (1l << 31)) {
+    const long w2 = (long)a->N * ((a->P + 1) / 2) * a->Q * (a->C / 8);
+    hipLaunchKernelGGL(maxpool_bnrelu_fwd_k3s2_kernel<false>, dim3(pgrid(w2)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)x, (const float*)nullptr, (bf16_t*)y, (uint8_t*)arg, *a, make_fastdiv(a->C / 8),
+                       make_fastdiv(a->Q), make_fastdiv((a->P + 1) / 2), (const bf16_t*)dtm_zero_chunk());
+    return;
+  }
   if (a->C % 8 == 0)
     hipLaunchKernelGGL(maxpool_fwd_kernel<8>, dim3(pgrid(work / 8)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
                        (bf16_t*)y, (uint8_t*)arg, *a);
@@ -498,6 +529,22 @@ DTM_API void dtm_maxpool_fwd(const void* x, void* y, void* arg, const PoolArgs* 
 }
 DTM_API void dtm_maxpool_bwd(const void* dy, const void* arg, void* dx, const PoolArgs* a, void* stream) {
   long work = (long)a->N * a->H * a->W * a->C;
+  if (a->C % 8 == 0 && a->C / 8 <= 256 && k3s2(a) && (long)a->N * a->H * a->W * a->C < (1l << 31)) {
+    const int cols = a->C / 8, RP = 256 / cols;  // (the BN kernel's row mapping: one row = a 2 x 2 pixel block)
+    const int BH = (a->H + a->PH + 1) / 2, BW = (a->W + a->PW + 1) / 2;
+    const long MB = (long)a->N * BH * BW;
+    long b = MB * cols / (256 * 2);
+    if (b < 1) b = 1;
+    if (b > 2048) b = 2048;
+    long rpb = (MB + b - 1) / b;
+    rpb = (rpb + RP - 1) / RP * RP;
+    const int blocks = (int)((MB + rpb - 1) / rpb);
+    hipLaunchKernelGGL(maxpool_bnrelu_bwd_k3s2_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)dy, (const uint8_t*)arg, (const bf16_t*)nullptr, (const float*)nullptr,
+                       (bf16_t*)dx, (float*)nullptr, *a, make_fastdiv(BW), make_fastdiv(BH), 0, (int)rpb,
+                       (const bf16_t*)dtm_zero_chunk());
+    return;
+  }
   if (a->C % 8 == 0)
     hipLaunchKernelGGL(maxpool_bwd_kernel<8>, dim3(pgrid(work / 8)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
                        (const uint8_t*)arg, (bf16_t*)dx, *a);
@@ -533,19 +580,11 @@ DTM_API void dtm_global_avg_bwd(const float* dy, void* dx, int N, int HW, int C,
 }
 
 // y = maxpool(relu(x*scale + shift)) with a uint8 argmax per output element (ss = [scale; shift; ...])
-static int g_pool_k3s2 = 1;  // A/B knob (dtm_pool_set_k3s2): the 3x3 / stride-2 specialised stem-pool kernels
-DTM_API void dtm_pool_set_k3s2(int on) { g_pool_k3s2 = on; }
-static bool k3s2(const PoolArgs* a) {
-  return g_pool_k3s2 && a->KH == 3 && a->KW == 3 && a->SH == 2 && a->SW == 2 && a->PH >= 0 && a->PH <= 1 &&
-         a->PW >= 0 && a->PW <= 1;
-}
-const void* dtm_zero_chunk();  // >= 16 B of device zeros (conv_igemm.hip)
-
 DTM_API int dtm_maxpool_bnrelu_fwd(const void* x, const float* ss, void* y, void* arg, const PoolArgs* a, void* stream) {
   if (a->C % 8 || a->KH * a->KW > 255 || (long)a->N * a->H * a->W * a->C >= (1l << 31)) return -1;
   if (k3s2(a)) {
     const long work = (long)a->N * ((a->P + 1) / 2) * a->Q * (a->C / 8);
-    hipLaunchKernelGGL(maxpool_bnrelu_fwd_k3s2_kernel, dim3(pgrid(work)), dim3(256), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(maxpool_bnrelu_fwd_k3s2_kernel<true>, dim3(pgrid(work)), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)x, ss, (bf16_t*)y, (uint8_t*)arg, *a, make_fastdiv(a->C / 8), make_fastdiv(a->Q),
                        make_fastdiv((a->P + 1) / 2), (const bf16_t*)dtm_zero_chunk());
     return 0;
@@ -573,7 +612,7 @@ DTM_API int dtm_maxpool_bnrelu_bwd(const void* dy, const void* arg, const void* 
     const int blocks = (int)((MB + rpb - 1) / rpb);
     float* ws = dtm_ws_get_stream((size_t)blocks * 2 * a->C, (hipStream_t)stream);
     if (!ws) return -4;
-    hipLaunchKernelGGL(maxpool_bnrelu_bwd_k3s2_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(maxpool_bnrelu_bwd_k3s2_kernel<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)dy, (const uint8_t*)arg, (const bf16_t*)x, ss, (bf16_t*)dx, ws, *a,
                        make_fastdiv(BW), make_fastdiv(BH), unscaled, (int)rpb, (const bf16_t*)dtm_zero_chunk());
     dtm_reduce_rows(ws, blocks, 2 * a->C, 2 * a->C, sums, (hipStream_t)stream);

@@ -266,6 +266,47 @@ def test_conv_act_dgrad_tiles_match_reference(tile, case):
     assert _rel(sums[1], gref.sum((0, 1, 2))) < 1e-2
 
 
+@pytest.mark.parametrize("case", [(4, 35, 35, 288, "VALID"), (4, 17, 17, 768, "VALID"), (2, 15, 14, 16, "SAME"),
+                                  (3, 9, 10, 8, "VALID"), (2, 13, 13, 2048, "SAME")])
+def test_maxpool_k3s2_matches_generic(case):
+    """The plain 3x3 / stride-2 max pool (Inception's grid-reduction branches) on the specialised kernels vs the
+    generic ones: output, argmax bytes and input gradient bit-identical; and against fp32 torch."""
+    import ctypes
+
+    import torch.nn.functional as tF
+
+    from distributed_tensorflow_models_amd.ops import _lib
+    from distributed_tensorflow_models_amd.ops.geometry import pool_geom
+    N, H, W, C, pad = case
+    torch.manual_seed(8)
+    L = _lib.lib()
+    s = _lib.stream_ptr()
+    x = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16)
+    g = pool_geom(tuple(x.shape), 3, 2, pad)
+    a = g.as_args(_lib.PoolArgs)
+    dy = torch.randn(N, g.P, g.Q, C, device=DEV).to(torch.bfloat16)
+    out = {}
+    for fast in (1, 0):
+        L.dtm_pool_set_k3s2(fast)
+        try:
+            y = torch.empty(N, g.P, g.Q, C, device=DEV, dtype=torch.bfloat16)
+            arg = torch.empty(N, g.P, g.Q, C, device=DEV, dtype=torch.uint8)
+            L.dtm_maxpool_fwd(_lib.ptr(x), _lib.ptr(y), _lib.ptr(arg), ctypes.byref(a), s)
+            dx = torch.empty_like(x)
+            L.dtm_maxpool_bwd(_lib.ptr(dy), _lib.ptr(arg), _lib.ptr(dx), ctypes.byref(a), s)
+            torch.cuda.synchronize()
+        finally:
+            L.dtm_pool_set_k3s2(1)
+        out[fast] = (y, arg, dx)
+    for i in range(3):
+        assert torch.equal(out[1][i], out[0][i]), i
+    xr = x.float().permute(0, 3, 1, 2).contiguous().requires_grad_()
+    yr = tF.max_pool2d(tF.pad(xr, (g.PW, g.PR, g.PH, g.PB), value=-1e30), 3, 2)
+    assert torch.equal(out[1][0].float().permute(0, 3, 1, 2), yr)
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    assert _rel(out[1][2].float(), xr.grad.permute(0, 2, 3, 1)) < 2e-2  # (bf16 ties may route differently)
+
+
 @pytest.mark.parametrize("case", [(4, 112, 112, 64, "SAME"), (3, 147, 147, 64, "VALID"), (2, 71, 71, 192, "VALID"),
                                   (2, 15, 14, 16, "SAME"), (3, 9, 10, 8, "VALID"), (2, 13, 13, 24, "SAME")])
 @pytest.mark.parametrize("unscaled", [0, 1])
