@@ -266,6 +266,49 @@ def test_conv_act_dgrad_tiles_match_reference(tile, case):
     assert _rel(sums[1], gref.sum((0, 1, 2))) < 1e-2
 
 
+@pytest.mark.parametrize("case", [(4, 35, 35, 64, "SAME"), (4, 17, 17, 192, "SAME"), (3, 8, 8, 192, "SAME"),
+                                  (2, 13, 11, 16, "VALID"), (2, 9, 10, 8, "SAME")])
+@pytest.mark.parametrize("count_pad", [0, 1])
+def test_avgpool_k3s1_matches_generic(case, count_pad):
+    """3x3 / stride-1 average pools (Inception's pool branches) on the strip kernels vs the generic ones: output and
+    input gradient bit-identical (same tap / window order and divisors); and against fp32 torch."""
+    import ctypes
+
+    import torch.nn.functional as tF
+
+    from distributed_tensorflow_models_amd.ops import _lib
+    from distributed_tensorflow_models_amd.ops.geometry import pool_geom
+    N, H, W, C, pad = case
+    torch.manual_seed(9)
+    L = _lib.lib()
+    s = _lib.stream_ptr()
+    x = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16)
+    g = pool_geom(tuple(x.shape), 3, 1, pad)
+    a = g.as_args(_lib.PoolArgs)
+    dy = torch.randn(N, g.P, g.Q, C, device=DEV).to(torch.bfloat16)
+    out = {}
+    for fast in (1, 0):
+        L.dtm_pool_set_k3s2(fast)
+        try:
+            y = torch.empty(N, g.P, g.Q, C, device=DEV, dtype=torch.bfloat16)
+            L.dtm_avgpool_fwd(_lib.ptr(x), _lib.ptr(y), ctypes.byref(a), count_pad, s)
+            dx = torch.empty_like(x)
+            L.dtm_avgpool_bwd(_lib.ptr(dy), _lib.ptr(dx), ctypes.byref(a), count_pad, s)
+            torch.cuda.synchronize()
+        finally:
+            L.dtm_pool_set_k3s2(1)
+        out[fast] = (y, dx)
+    assert torch.equal(out[1][0], out[0][0]) and torch.equal(out[1][1], out[0][1])
+    xr = x.float().permute(0, 3, 1, 2).contiguous().requires_grad_()
+    yr = tF.avg_pool2d(tF.pad(xr, (g.PW, g.PR, g.PH, g.PB)), 3, 1)
+    if not count_pad:  # TF SAME: divide by the in-bounds taps
+        ones = tF.pad(torch.ones_like(xr[:, :1]), (g.PW, g.PR, g.PH, g.PB))
+        yr = yr * 9.0 / (tF.avg_pool2d(ones, 3, 1) * 9.0)
+    assert _rel(out[1][0].float().permute(0, 3, 1, 2), yr) < 1e-2
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    assert _rel(out[1][1].float(), xr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
 @pytest.mark.parametrize("case", [(4, 35, 35, 288, "VALID"), (4, 17, 17, 768, "VALID"), (2, 15, 14, 16, "SAME"),
                                   (3, 9, 10, 8, "VALID"), (2, 13, 13, 2048, "SAME")])
 def test_maxpool_k3s2_matches_generic(case):

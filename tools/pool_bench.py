@@ -62,5 +62,34 @@ def main():
                 100.0 * (m[1] - m[0]) / m[0]), flush=True)
 
 
+def avg_main():
+    """3x3 / stride-1 SAME average pools of Inception-v3's pool branches (batch 128)."""
+    L = _lib.lib()
+    st = _lib.stream_ptr()
+    for name, N, H, C in (("inc 35x35x64", 128, 35, 64), ("inc 35x35x32", 128, 35, 32), ("inc 17x17x192", 128, 17, 192),
+                          ("inc 8x8x192", 128, 8, 192)):
+        x = torch.randn(N, H, H, C, device="cuda").to(torch.bfloat16)
+        g = pool_geom(tuple(x.shape), 3, 1, "SAME")
+        a = g.as_args(_lib.PoolArgs)
+        y = torch.empty_like(x)
+        dy, dx = torch.randn_like(x), torch.empty_like(x)
+        fwd = lambda: L.dtm_avgpool_fwd(_lib.ptr(x), _lib.ptr(y), ctypes.byref(a), 0, st)  # noqa
+        bwd = lambda: L.dtm_avgpool_bwd(_lib.ptr(dy), _lib.ptr(dx), ctypes.byref(a), 0, st)  # noqa
+        for pname, fn in (("fwd", fwd), ("bwd", bwd)):
+            res = {0: [], 1: []}
+            for _ in range(ROUNDS):
+                for fast in (0, 1):
+                    L.dtm_pool_set_k3s2(fast)
+                    res[fast].append(timed(fn))
+            L.dtm_pool_set_k3s2(1)
+            m = {k: statistics.median(v) for k, v in res.items()}
+            b = 2 * x.numel() * 2
+            print("%-16s %s  generic %7.1f us (%4.2f TB/s)  k3s1 %7.1f us (%4.2f TB/s)  %+.1f %%" % (
+                name, pname, m[0], b / m[0] / 1e6, m[1], b / m[1] / 1e6, 100.0 * (m[1] - m[0]) / m[0]), flush=True)
+
+
 if __name__ == "__main__":
+    if os.environ.get("AVG"):
+        avg_main()
+        sys.exit(0)
     main()
