@@ -100,9 +100,10 @@ int dtm_bn_stats_finalize(const float* ws, int rows, int K, const float* gamma, 
 // the per-block partial row out0[c0..c0+7], out1[...] (plain stores; reduced later by reduce_rows).
 // atomic: add into the final [C] sums instead (small grids: one launch fewer, <= a few hundred
 // adders per address).
-__device__ __forceinline__ void col_reduce8(float (*red)[256][8], const float* s, const float* q, float* out0,
+template <int NT = 256>
+__device__ __forceinline__ void col_reduce8(float (*red)[NT][8], const float* s, const float* q, float* out0,
                                             float* out1, int cols, int c0, bool atomic = false) {
-  const int t = threadIdx.x, RP = 256 / cols;
+  const int t = threadIdx.x, RP = NT / cols;  // (NT: the red table's rows; blocks of cols * (NT / cols) lanes)
   if (RP == 1) {
     if (t < cols) {
 #pragma unroll

@@ -336,10 +336,15 @@ __global__ __launch_bounds__(256) void cat_bn_apply_kernel(CatArgs a, bf16_t* __
 // backward: g = d(concat slice) * mask bit; dx = g (unscaled producer) or g*scale; per block a partial row of
 // width 4*Ct laid out as every part's [4][C] (Σg·x | Σg | 0 | 0), so ONE reduction yields the parts' dss
 // buffers back to back
-__global__ __launch_bounds__(256) void cat_bn_apply_bwd_kernel(CatArgs a, const bf16_t* __restrict__ dout,
-                                                               float* __restrict__ ws) {
-  __shared__ float red[2][256][8];
-  const int cols = a.Ct >> 3, t = threadIdx.x, RP = 256 / cols, gc = (t % cols) * 8, lr0 = t / cols;
+// NT lanes per block (cat_bwd_threads): 512 for the wide concats - every lane owns a column (a 768-channel concat
+// at 256 lanes left a quarter of them idle, 1280 channels 38 %) and half the partial rows to reduce
+// (profiles/ab/r5_ab_pool_k3s2.log, session s21: 17x17x768 69.7 -> 56.3 us, 8x8x2048 51.3 -> 40.2 us); 256 for
+// the 35x35 ones (<= 64 columns), which measured 4 % slower on 512.
+template <int NT>
+__global__ __launch_bounds__(NT) void cat_bn_apply_bwd_kernel(CatArgs a, const bf16_t* __restrict__ dout,
+                                                              float* __restrict__ ws) {
+  __shared__ float red[2][NT][8];
+  const int cols = a.Ct >> 3, t = threadIdx.x, RP = NT / cols, gc = (t % cols) * 8, lr0 = t / cols;
   const int k = cat_part(a, gc);
   const CatPart& P = a.p[k];
   const int cl = gc - P.off;
@@ -382,7 +387,7 @@ __global__ __launch_bounds__(256) void cat_bn_apply_bwd_kernel(CatArgs a, const 
     }
   }
   float* row = ws + (size_t)blockIdx.x * 4 * a.Ct + 4 * P.off;  // this part's [4][C] image in the row
-  col_reduce8(red, a1, a0, row - P.off, row + P.C - P.off, cols, gc);
+  col_reduce8<NT>(red, a1, a0, row - P.off, row + P.C - P.off, cols, gc);
   if (t < cols) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) { row[2 * P.C + cl + e] = 0.f; row[3 * P.C + cl + e] = 0.f; }
@@ -391,10 +396,10 @@ __global__ __launch_bounds__(256) void cat_bn_apply_bwd_kernel(CatArgs a, const 
 
 static int g_cpt = 8;  // A/B knob: 16-B chunks per thread the BN-stream grids aim for (dtm_set_grid_cpt)
 DTM_API void dtm_set_grid_cpt(int n) { g_cpt = n > 0 ? n : 8; }
-static void grid2(long M, int C, int* blocks, int* rpb, int cap = 2048) {
-  int cols = C / 8, RP = 256 / cols;
+static void grid2(long M, int C, int* blocks, int* rpb, int cap = 2048, int nt = 256) {
+  int cols = C / 8, RP = nt / cols;
   long chunks = M * cols;
-  long b = chunks / (256 * g_cpt);
+  long b = chunks / ((long)nt * g_cpt);
   if (b < 1) b = 1;
   if (b > cap) b = cap;
   long r = (M + b - 1) / b;
@@ -487,10 +492,12 @@ DTM_API int dtm_cat_bn_apply_bwd(const void* descs, int np, const void* dout, fl
   for (int i = 0; i < np; ++i)
     if (!(a.p[i].flags & 2) && (!a.p[i].mask || !a.p[i].dx)) return -1;
   int blocks;
-  grid2(M, Ct, &blocks, &a.rpb);
+  const int nt = Ct / 8 > 64 ? 512 : 256;
+  grid2(M, Ct, &blocks, &a.rpb, 2048, nt);
   float* ws = dtm_ws_get_stream((size_t)blocks * 4 * Ct, (hipStream_t)stream);
   if (!ws) return -4;
-  hipLaunchKernelGGL(cat_bn_apply_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a,
+  hipLaunchKernelGGL(nt == 512 ? cat_bn_apply_bwd_kernel<512> : cat_bn_apply_bwd_kernel<256>, dim3(blocks),
+                     dim3((Ct / 8) * (nt / (Ct / 8))), 0, (hipStream_t)stream, a,
                      (const bf16_t*)dout, ws);
   dtm_reduce_rows(ws, blocks, 4 * Ct, 4 * Ct, sums, (hipStream_t)stream);
   return 0;

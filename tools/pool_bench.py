@@ -88,7 +88,37 @@ def avg_main():
                 name, pname, m[0], b / m[0] / 1e6, m[1], b / m[1] / 1e6, 100.0 * (m[1] - m[0]) / m[0]), flush=True)
 
 
+def cat_main():
+    """One-launch zero-copy concat of BN'd branch outputs (dtm_cat_bn_apply / _bwd) at Inception-v3's mixed-block
+    widths (batch 128); compare two library builds with DTM_KERNELS_SO."""
+    from distributed_tensorflow_models_amd.ops.fused import _ConcatBNApplyFn as _ConcatFn
+    L = _lib.lib()
+    st = _lib.stream_ptr()
+    for name, N, H, Cs in (("cat 35x35x288", 128, 35, (64, 64, 96, 64)), ("cat 17x17x768", 128, 17, (192,) * 4),
+                           ("cat 8x8x1280", 128, 8, (320, 384, 384, 192)), ("cat 8x8x2048", 128, 8, (320, 768, 768, 192))):
+        M, Ct = N * H * H, sum(Cs)
+        raws = [torch.randn(M, c, device="cuda").to(torch.bfloat16) for c in Cs]
+        sss = [torch.stack([torch.rand(c, device="cuda") + 0.5, torch.randn(c, device="cuda") * 0.3,
+                            torch.zeros(c, device="cuda"), torch.ones(c, device="cuda")]) for c in Cs]
+        masks = [torch.empty(M * c // 8, device="cuda", dtype=torch.uint8) for c in Cs]
+        dxs = [torch.empty_like(r) for r in raws]
+        tab = _ConcatFn._descs([(r, ss, m, dx, c, 1) for r, ss, m, dx, c in zip(raws, sss, masks, dxs, Cs)])
+        out = torch.empty(M, Ct, device="cuda", dtype=torch.bfloat16)
+        dout = torch.randn_like(out)
+        sums = torch.zeros(4 * Ct, device="cuda")
+        fwd = lambda: L.dtm_cat_bn_apply(ctypes.c_void_p(tab.ctypes.data), len(Cs), _lib.ptr(out), M, Ct, st)  # noqa
+        bwd = lambda: L.dtm_cat_bn_apply_bwd(ctypes.c_void_p(tab.ctypes.data), len(Cs), _lib.ptr(dout),  # noqa
+                                             _lib.ptr(sums), M, Ct, st)
+        b = M * Ct * 2
+        for pname, fn, nbytes in (("fwd", fwd, 2 * b + M * Ct // 8), ("bwd", bwd, 3 * b + M * Ct // 8)):
+            v = statistics.median([timed(fn) for _ in range(ROUNDS)])
+            print("%-16s %s %7.1f us (%4.2f TB/s)" % (name, pname, v, nbytes / v / 1e6), flush=True)
+
+
 if __name__ == "__main__":
+    if os.environ.get("CAT"):
+        cat_main()
+        sys.exit(0)
     if os.environ.get("AVG"):
         avg_main()
         sys.exit(0)
