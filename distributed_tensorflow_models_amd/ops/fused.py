@@ -1008,6 +1008,8 @@ def _prologue_mode(x_shape, w_shape, stride):
     for every 1x1 consumer is still +1.71 % step (profiles/ab/r5_ab_prologue_1x1_fdir.log)."""
     _, H, W, _ = x_shape
     _, R, S, _ = w_shape
+    if PROLOGUE_MODE == "spatial":  # (A/B: the prologue for every spatial consumer)
+        return "fused" if R * S > 1 else "mat"
     if PROLOGUE_MODE is not None:
         return PROLOGUE_MODE
     st = stride if isinstance(stride, int) else stride[0]
