@@ -2607,6 +2607,8 @@ static void launch_wgrad(const ConvWgradArgs& a, int splits, hipStream_t st) {
 // kernels (A/B sweeps: tools/conv_tile_sweep.py)
 static int g_wgrad_env = -2;
 static int g_wgrad_occ = 4;
+static int g_wgrad_k64 = 1;  // A/B knob (dtm_conv_set_wgrad_k64): the 64 x 256 pipelined tile for K % 128 != 0
+DTM_API void dtm_conv_set_wgrad_k64(int on) { g_wgrad_k64 = on; }
 DTM_API void dtm_conv_set_wgrad_tile(int id, int occ) {
   g_wgrad_env = id;
   if (occ > 0) g_wgrad_occ = occ;
@@ -2673,7 +2675,8 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   a.P = d->P; a.Q = d->Q; a.stride = d->stride; a.pad_h = d->pad_h; a.pad_w = d->pad_w;
   a.Mpix = d->N * d->P * d->Q; a.Kg = d->R * d->S * d->C;
   a.fd_PQ = make_fastdiv(d->P * d->Q); a.fd_Q = make_fastdiv(d->Q);
-  // wgrad tile variants: 0 = 128 (K) x 128 (RSC) register-staged, 1 = 64 x 128, 6 = 32 x 128, 10 = the
+  // wgrad tile variants: 0 = 128 (K) x 128 (RSC) register-staged, 1 = 64 x 128, 6 = 32 x 128, 11 = the pipelined
+  // LDS-DMA 64 x 256, 10 = the
   // pipelined LDS-DMA 128 x 128, 12 = the 8-wave pipelined 256 x 256 (the rejected variants and their A/B
   // logs: profiles/ab/README.md).  dtm_conv_set_wgrad_tile forces one (A/B experiments).
   if (g_wgrad_env == -2) g_wgrad_env = -1;
@@ -2690,11 +2693,32 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
     // the 8-wave 256x256 tile on the wide deep-reduction layers (profiles/r2_wgrad_tiles_w8.txt:
     // 14x14 / 7x7 3x3 -8..-13 %, 7x7 1024->2048 -7 %; it loses on every K < 256 or short-RSC layer)
     if (g_tile_w8 && d->K >= 256 && a.Kg >= 1024 && (d->R * d->S > 1 || d->K >= 1024)) wt = 12;
+    // merged sibling heads (one wgrad over several 1x1 convs' output gradients, dst): the 256 x 256 tile also wins
+    // at short reductions on <= 160k-pixel maps (profiles/r5/r5_s27_wgrad_heads_sweep.log, Inception-v3 batch 128:
+    // 17x17 768 -> 704 87.9 -> 75.6 us, 35x35 192 -> 208 47.6 -> 42.0 us)
+    if (g_tile_w8 && dst && d->K >= 208 && a.Mpix <= 163840) wt = 12;
   }
+  // the pipelined 64 x 256 tile (tools/conv_tile_sweep.py WTILES, profiles/r5/r5_s25_wgrad_small_k_sweep.log, Inception-v3
+  // at batch 128): the 5x5 48 -> 64 layers (Kg 1200: 79.1 us on the register-staged 64 x 128, 68.6 here) and the
+  // stem's 3x3 80 -> 192 at 73x73 (645k pixels, K % 128 != 0: 389.7 us on 128 x 128, 365.6 here)
+  if (wenv == -1 && g_wgrad_k64 && !in_scale && !bn &&
+      ((wt == 1 && d->R * d->S >= 25 && a.Kg >= 1024) ||
+       (wt == 10 && d->K % 128 != 0 && d->R * d->S > 1 && a.Mpix >= 262144)))
+    wt = 11;
   if (wt >= 10 && (in_scale || bn)) wt = d->K <= 64 ? 1 : 0;  // the pipelined kernels have no operand prologues
-  if (wt != 0 && wt != 1 && wt != 6 && wt != 10 && wt != 12) wt = 0;
+  if (wt != 0 && wt != 1 && wt != 6 && wt != 10 && wt != 11 && wt != 12) wt = 0;
+  {
+    static int log = -1;  // DTM_TILE_LOG=1: one stderr line per weight-gradient decision too
+    if (log < 0) {
+      const char* e = getenv("DTM_TILE_LOG");
+      log = e ? atoi(e) : 0;
+    }
+    if (log)
+      fprintf(stderr, "dtm_wgrad M=%d K=%d C=%d RxS=%dx%d Kg=%d st=%d pro=%d bn=%d dst=%d -> %d\n", a.Mpix, d->K, d->C,
+              d->R, d->S, a.Kg, d->stride, in_scale != nullptr, bn != nullptr, dst ? dst->n : 0, wt);
+  }
   const bool big = wt == 12;  // 8-wave 256x256 (one block per CU)
-  const int MT = wt == 6 ? 32 : (wt == 1 ? 64 : (big ? 256 : 128)), NT = big ? 256 : 128;
+  const int MT = wt == 6 ? 32 : ((wt == 1 || wt == 11) ? 64 : (big ? 256 : 128)), NT = (big || wt == 11) ? 256 : 128;
   if (big) occ = (wenv == 12 && g_wgrad_occ != 4) ? g_wgrad_occ : 1;  // (sweeps: WTILES=12:<occ>)
   long tiles = (long)((a.Kg + NT - 1) / NT) * ((a.K + MT - 1) / MT);
   long target = (long)num_cus * (wt >= 10 ? occ : 3);
@@ -2717,6 +2741,8 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
     dim3 grid((a.Kg + NT - 1) / NT, (a.K + MT - 1) / MT, splits);
     if (wt == 12)
       hipLaunchKernelGGL((conv_wgrad_pipe_kernel<256, 256, 2, 2, 512>), grid, dim3(512), 0, (hipStream_t)stream, a);
+    else if (wt == 11)
+      hipLaunchKernelGGL((conv_wgrad_pipe_kernel<64, 256, 2>), grid, dim3(256), 0, (hipStream_t)stream, a);
     else
       hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 128, 2>), grid, dim3(256), 0, (hipStream_t)stream, a);
   } else if (wt == 1) launch_wgrad<64, 128, 32, 64>(a, (int)splits, (hipStream_t)stream);

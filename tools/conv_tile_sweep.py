@@ -67,6 +67,9 @@ def main():
     which = os.environ.get("SET", "resnet")
     shapes = ([(H, C, K, R, R, s_, (p_, p_), n) for (H, C, K, R, s_, p_, n) in SHAPES[1:]]
               if which == "resnet" else (INCEPTION if which == "inception" else VGG))
+    if which == "custom":  # SHAPES_CUSTOM="H,C,K,R,S,stride,padding,count;..." (e.g. merged sibling-head widths)
+        shapes = [tuple(int(v) if v.lstrip("-").isdigit() else v for v in item.split(","))
+                  for item in os.environ["SHAPES_CUSTOM"].split(";")]
     for (H, C, K, R, S, stride, pad, cnt) in shapes:
         if ONLY and ONLY not in "%d_%d_%d_%d" % (H, C, K, R):
             continue
