@@ -2273,6 +2273,8 @@ static void dispatch_ud(const ConvNTArgs& a, const TileCfg& t, hipStream_t st) {
   else if (t.id == 26) launch_pipe<128, 64, 2, UD>(a, st);
   else if (t.id == 32) launch_pipe<256, 32, 2, UD, 4>(a, st);   // waves 4x1 of 64x32 (32-channel outputs)
   else if (t.id == 40) launch_w8<256, 256, 2, 2, UD>(a, st);
+  // (a stream-K form of this tile for the < 2-round grids - ResNet-50's 196-tile 14x14 layers - was correct but slower:
+  //  a 256x256 fp32 partial is 256 KiB of slab traffic per hand-off; profiles/ab/r5_ab_stream_k_w8.log)
   else launch_nt<128, 128, 64, 64, UD>(a, st);
 }
 
