@@ -2176,6 +2176,9 @@ static TileCfg pick_tile_impl(const ConvNTArgs& a, bool stats) {
   // (dgrad post-op inputs come by LDS-DMA: with per-tile global side loads in the epilogue the compiler's waits
   // drained the halo prefetch - Inception stem dgrads 551 / 252 us vs 355 / 195 on the GEMM tiles)
   if (((id == -1 && a.K == 32) || id == 60) && g_direct3 && direct_ok(a)) return {60, 128, 4};
+  // ... and the 32 -> 64 3x3 of Inception-v3's stem (147x147 at batch 128: 282.6 -> 253.0 us forward with the BN
+  // statistics, profiles/r5/r5_s31_inception_stem_sweep.log; ResNet-50's 64 -> 64 layers lose on it, see above)
+  if (id == -1 && a.K == 64 && a.C == 32 && !a.in_scale && g_direct3 && direct_ok(a)) return {60, 128, 4};
   // the pipelined LDS-DMA 128x128 tile (2 slots, 2 blocks/CU) wins every deep-reduction layer without the
   // prologue (tools/conv_tile_sweep.py: 3x3 at 14x14 / 7x7 -13..-18 %, deep 1x1 -5..-16 %)
   if (id == -4) id = -1;  // (-4: the policy without the streaming kernel, for A/B runs)
@@ -2209,7 +2212,9 @@ static TileCfg pick_tile_impl(const ConvNTArgs& a, bool stats) {
   // 160 ...): 64-channel tiles (A/B knob dtm_conv_set_kwide); v2: 256-pixel tiles on mid-size maps
   // (17x17 at batch 128: 1x7 / 7x1 / 1x1 -> 160 / 192 -19 %), not on small ones (8x8: +33 %)
   if (id == -1 && g_kwide && a.K > 64 && a.K % 128 != 0 && (a.K % 128) <= 64 && a.K % 8 == 0)
-    id = a.in_scale ? 3 : ((g_policy2 && a.M >= 16384 && a.M <= 65536) ? 24 : 26);
+    id = a.in_scale ? 3 : ((g_policy2 && a.M >= 16384 && (a.M <= 65536 || a.M >= 262144)) ? 24 : 26);
+  // (and on the stem-size maps: Inception-v3's 73x73 3x3 80 -> 192, 324.2 -> 306.2 us with statistics,
+  //  profiles/r5/r5_s31_inception_stem_sweep.log)
   if (id == -1 && !a.in_scale && a.Kg >= 1024) {
     id = 21;  // (-3: the policy without it, for A/B runs)
     // v2: no more 128x128 tiles than CUs (8x8 maps at batch 128, VGG's 4x4 at 512): 128x64 tiles fill the
