@@ -149,8 +149,38 @@ __global__ void scale_kernel(float* __restrict__ x, long n, float s) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) x[i] *= s;
 }
 
+// Backward of the per-row loss: out[r][c] = dl[r][c] * gl[r * gstride] for c < N, 0 for N <= c < ldo (the zero
+// columns of the padded logits operand of the FC backward, written here instead of a zero fill + copy).  One pass in
+// place of the float cast, broadcast multiply and bf16 cast autograd would launch; gstride 0: one scale for every row.
+template <typename T>
+__global__ __launch_bounds__(256) void scale_rows_pad_kernel(const T* __restrict__ dl, const float* __restrict__ gl,
+                                                             int gstride, T* __restrict__ out, int N, int ldo) {
+  const int r = blockIdx.y;
+  const float g = gl[(long)r * gstride];
+  const T* src = dl + (long)r * N;
+  T* dst = out + (long)r * ldo;
+  for (int c = blockIdx.x * 256 + threadIdx.x; c < ldo; c += gridDim.x * 256) {
+    const float v = c < N ? ldf(src, c) * g : 0.f;
+    if constexpr (sizeof(T) == 2) dst[c] = f2bf(v);
+    else dst[c] = v;
+  }
+}
+
 }  // namespace dtm
 using namespace dtm;
+
+DTM_API int dtm_scale_rows_pad(const void* dl, int bf16, const float* gl, int gstride, void* out, int B, int N, int ldo,
+                               void* stream) {
+  if (B <= 0 || N <= 0 || ldo < N || B > 65535) return -1;
+  const int bx = (ldo + 255) / 256 > 8 ? 8 : (ldo + 255) / 256;
+  if (bf16)
+    hipLaunchKernelGGL(scale_rows_pad_kernel<bf16_t>, dim3(bx, B), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)dl, gl, gstride, (bf16_t*)out, N, ldo);
+  else
+    hipLaunchKernelGGL(scale_rows_pad_kernel<float>, dim3(bx, B), dim3(256), 0, (hipStream_t)stream, (const float*)dl,
+                       gl, gstride, (float*)out, N, ldo);
+  return 0;
+}
 
 DTM_API void dtm_softmax_xent(const void* logits, int logits_bf16, const int* labels, float* loss, void* dlogits,
                               int B, int K, float smoothing, float gscale, const float* row_weight, void* stream) {

@@ -75,6 +75,7 @@ _SIGS = {
     "dtm_maxpool_bnrelu_bwd": (_I, [_P, _P, _P, _P, _P, _P, ctypes.POINTER(PoolArgs), _I, _P]),
     "dtm_conv_set_tile": (None, [_I]),
     "dtm_conv_set_wgrad_tile": (None, [_I, _I]),
+    "dtm_scale_rows_pad": (_I, [_P, _I, _P, _I, _P, _I, _I, _I, _P]),
     "dtm_conv_set_wgrad_k64": (None, [_I]),
     "dtm_pool_set_k3s2": (None, [_I]),
     "dtm_conv_fwd_bn": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _I, _I, ctypes.POINTER(ConvDesc), _P]),

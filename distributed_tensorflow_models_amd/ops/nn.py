@@ -138,18 +138,32 @@ def dgrad_decomposable(g):
     return g.stride > 1 and g.R >= g.stride and g.S >= g.stride
 
 
-def weight_flipped(w, K, R, S, C, dec=None):
+def _flip_attr(dec):
+    return "_flip" if dec is None else ("_flippad" if dec[0] == "pad" else "_flipdec")
+
+
+def weight_flipped(w, K, R, S, C, dec=None, pad_to=None):
     """Flipped / transposed bf16 dgrad copy [C][R][S][K] of w [K][R][S][C]; with dec = (stride, pad_h,
     pad_w) the same elements in the stride-decomposed layout (per output parity class (a, b) a block
-    [C][Tr][Tu][K] of that class's taps, conv_igemm.hip dec_dim)."""
-    attr = "_flip" if dec is None else "_flipdec"
+    [C][Tr][Tu][K] of that class's taps, conv_igemm.hip dec_dim).  pad_to: the copy lives in the first C rows of a
+    zero-initialised [pad_to][R][S][K] buffer, which is returned (the FC forward's 8-aligned output width: the
+    refresh after every update rewrites the C real rows, the zero rows stay)."""
+    if pad_to is not None and pad_to != C:
+        dec = ("pad", int(pad_to))
+    attr = _flip_attr(dec)
     c = getattr(w, attr, None)
     if c is not None and c[0] == WEIGHT_VERSION[0] and c[1].shape == (C, R, S, K) and c[2] == dec:
-        return c[1]
+        return c[1] if dec is None or dec[0] != "pad" else c[1]._pad_full
     L = _lib.lib()
-    wt = c[1] if (c is not None and c[1].shape == (C, R, S, K)) else \
-        torch.empty((C, R, S, K), device=w.device, dtype=torch.bfloat16)
-    if dec is None:
+    if c is not None and c[1].shape == (C, R, S, K) and c[2] == dec:
+        wt = c[1]
+    elif dec is not None and dec[0] == "pad":
+        full = torch.zeros((dec[1], R, S, K), device=w.device, dtype=torch.bfloat16)
+        wt = full[:C]  # (contiguous: the first C rows)
+        wt._pad_full = full
+    else:
+        wt = torch.empty((C, R, S, K), device=w.device, dtype=torch.bfloat16)
+    if dec is None or dec[0] == "pad":
         L.dtm_weight_flip_transpose(_lib.ptr(weight_bf16(w)), _lib.ptr(wt), K, R, S, C, _lib.stream_ptr())
     else:
         L.dtm_weight_flip_transpose_dec(_lib.ptr(weight_bf16(w)), _lib.ptr(wt), K, R, S, C, int(dec[0]), int(dec[1]),
@@ -160,10 +174,30 @@ def weight_flipped(w, K, R, S, C, dec=None):
             FLIP_REGISTRY[(id(w), dec)] = (w, wt, dec)
         except Exception:
             pass
-    return wt
+    return wt if dec is None or dec[0] != "pad" else wt._pad_full
 
 
 _RETIRED = []  # device tables a captured graph may still point into (kept for the process lifetime)
+
+
+def _padded_copy(src, attr, shape, fill):
+    """A zero-padded copy of src (bf16 weight [Kin][N] -> [Kin][Np], or fp32 bias [N] -> [Np]) kept on the parameter and
+    refreshed once per weights version: one strided copy per step instead of a zero fill + copy per use."""
+    c = getattr(src, attr, None)
+    if c is not None and c[0] == WEIGHT_VERSION[0] and tuple(c[1].shape) == tuple(shape):
+        return c[1]
+    buf = c[1] if (c is not None and tuple(c[1].shape) == tuple(shape)) else \
+        torch.zeros(shape, device=src.device, dtype=fill.dtype)
+    with torch.no_grad():
+        if buf.dim() == 2:
+            buf[:, :fill.shape[1]].copy_(fill)
+        else:
+            buf[:fill.shape[0]].copy_(fill)
+    try:
+        setattr(src, attr, (WEIGHT_VERSION[0], buf))
+    except Exception:
+        pass
+    return buf
 
 
 def refresh_flipped(stream=None):
@@ -184,7 +218,7 @@ def refresh_flipped(stream=None):
             tab[i, 0] = weight_bf16(w).data_ptr()
             tab[i, 1] = wt.data_ptr()
             tab[i, 2:4] = np.array([K, R, S, C], dtype=np.int32).view(np.int64)
-            st, ph, pw = d if d is not None else (1, 0, 0)
+            st, ph, pw = d if (d is not None and d[0] != "pad") else (1, 0, 0)
             tab[i, 4:6] = np.array([st, ph, pw, 0], dtype=np.int32).view(np.int64)
         dev_tab = torch.from_numpy(tab.view(np.uint8).reshape(-1).copy()).to(entries[0][0].device)
         if cache is not None:
@@ -193,7 +227,7 @@ def refresh_flipped(stream=None):
         refresh_flipped.table = cache = (key, dev_tab, len(entries))
     L.dtm_weight_flip_transpose_batched(_lib.ptr(cache[1]), cache[2], stream or _lib.stream_ptr())
     for w, wt, d in entries:
-        setattr(w, "_flip" if d is None else "_flipdec", (WEIGHT_VERSION[0], wt, d))
+        setattr(w, _flip_attr(d), (WEIGHT_VERSION[0], wt, d))
 
 
 def invalidate_weight_copies(params):
@@ -732,7 +766,21 @@ class _SoftmaxXentFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gl):
         (dl,) = ctx.saved_tensors
-        return (dl.float() * gl.view(-1, 1)).to(dl.dtype), None, None, None
+        B, N = dl.shape
+        if not dl.is_cuda or gl.dtype != torch.float32 or gl.dim() != 1 or gl.stride(0) not in (0, 1):
+            return (dl.float() * gl.view(-1, 1)).to(dl.dtype), None, None, None
+        # one HIP pass (dl * gl per row); an FC producer's 8-aligned padded width is written here with zero columns,
+        # and its backward takes that buffer as is (_LinearHipFn: no zero fill + copy of the padded operand)
+        Np = _pad8(N) if dl.dtype == torch.bfloat16 else N
+        out = torch.empty((B, Np), device=dl.device, dtype=dl.dtype)
+        _check(_lib.lib().dtm_scale_rows_pad(_lib.ptr(dl), int(dl.dtype == torch.bfloat16), _lib.ptr(gl),
+                                             int(gl.stride(0)), _lib.ptr(out), B, N, Np, _lib.stream_ptr()),
+               "scale_rows_pad")
+        if Np == N:
+            return out, None, None, None
+        g = out[:, :N]
+        g._dtm_pad_base = out
+        return g, None, None, None
 
 
 def softmax_cross_entropy(logits, labels, smoothing=0.0, row_weight=None):
@@ -753,6 +801,9 @@ def softmax_cross_entropy(logits, labels, smoothing=0.0, row_weight=None):
 #                            dgrad    dx[B][Kin] = conv(dy [B,1,1,N], W [Kin][N]);
 #                            wgrad    dW[Kin][N] = conv_wgrad with the roles of x / dy swapped.
 # Output widths that are not a multiple of 8 (logits: 10, 1001) run on zero-padded copies.
+PAD_BASE_USED = [0]  # FC backwards that took the loss backward's padded gradient buffer as is (tests)
+
+
 def _pad8(n):
     return (n + 7) // 8 * 8
 
@@ -773,13 +824,9 @@ class _LinearHipFn(torch.autograd.Function):
         if Np == N:
             wt = weight_flipped(w, Kin, 1, 1, N).view(N, Kin)
             bias = b.float().contiguous() if b is not None else None
-        else:
-            wt = torch.zeros((Np, Kin), device=x.device, dtype=torch.bfloat16)
-            wt[:N].copy_(weight_bf16(w).t())
-            bias = None
-            if b is not None:
-                bias = torch.zeros(Np, device=x.device, dtype=torch.float32)
-                bias[:N].copy_(b)
+        else:  # (padded copies kept per weights version: no zero fill + copy per step)
+            wt = weight_flipped(w, Kin, 1, 1, N, pad_to=Np).view(Np, Kin)
+            bias = _padded_copy(b, "_pad8", (Np,), b.detach().float()) if b is not None else None
         y = torch.empty((B, Np), device=x.device, dtype=torch.bfloat16)
         d = _fc_desc(B, Kin, Np)
         _check(L.dtm_conv_fwd(_lib.ptr(x16), _lib.ptr(wt), _lib.ptr(y), None, _lib.ptr(bias), None, None, int(relu),
@@ -799,24 +846,31 @@ class _LinearHipFn(torch.autograd.Function):
         Np = _pad8(N)
         B = x16.shape[0]
         gb = None
-        dy = dy.contiguous()
-        if ctx.relu and ctx.b is not None and _relu_bias_bwd_ok(dy):
-            dy, gb = _relu_bias_bwd(dy, y)  # mask + bias-gradient sums in one HIP pass
-        elif ctx.relu:
-            dy = torch.where(y > 0, dy, torch.zeros((), dtype=dy.dtype, device=dy.device))
-        dy16 = dy.to(torch.bfloat16).contiguous()
-        if Np != N:
-            dyp = torch.zeros((B, Np), device=dy.device, dtype=torch.bfloat16)
-            dyp[:, :N].copy_(dy16)
+        base = getattr(dy, "_dtm_pad_base", None)
+        if (base is not None and Np != N and not ctx.relu and base.dtype == torch.bfloat16
+                and tuple(base.shape) == (B, Np)):
+            # the loss backward already wrote this gradient into a zero-padded [B][Np] buffer (_SoftmaxXentFn)
+            PAD_BASE_USED[0] += 1
+            dyp = base
+            dy16 = base[:, :N]
         else:
-            dyp = dy16
+            dy = dy.contiguous()
+            if ctx.relu and ctx.b is not None and _relu_bias_bwd_ok(dy):
+                dy, gb = _relu_bias_bwd(dy, y)  # mask + bias-gradient sums in one HIP pass
+            elif ctx.relu:
+                dy = torch.where(y > 0, dy, torch.zeros((), dtype=dy.dtype, device=dy.device))
+            dy16 = dy.to(torch.bfloat16).contiguous()
+            if Np != N:
+                dyp = torch.zeros((B, Np), device=dy.device, dtype=torch.bfloat16)
+                dyp[:, :N].copy_(dy16)
+            else:
+                dyp = dy16
         dx = None
         if ctx.needs_input_grad[0]:
             if Np == N:
                 w16 = weight_bf16(w)
             else:
-                w16 = torch.zeros((Kin, Np), device=dy.device, dtype=torch.bfloat16)
-                w16[:, :N].copy_(weight_bf16(w))
+                w16 = _padded_copy(w, "_pad8w", (Kin, Np), weight_bf16(w))
             dx = torch.empty((B, Kin), device=dy.device, dtype=torch.bfloat16)
             d = _fc_desc(B, Np, Kin)
             _check(L.dtm_conv_fwd(_lib.ptr(dyp), _lib.ptr(w16), _lib.ptr(dx), None, None, None, None, 0,

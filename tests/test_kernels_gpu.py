@@ -547,6 +547,45 @@ def test_conv_wgrad_pipelined_tiles_match_reference(tile, case):
     assert _rel(dw, wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("N", [1001, 1000, 10])
+def test_fc_softmax_xent_padded_head_matches_torch(N):
+    """Logits FC + label-smoothed softmax cross-entropy (the Inception-v3 / ResNet heads): the loss backward writes the
+    row-scaled gradient in one HIP pass, into an 8-aligned zero-padded buffer that the FC backward takes as its padded
+    operand (N % 8 != 0), and the padded flipped / bf16 weight copies persist per weights version - loss, input, weight
+    and bias gradients against fp32 torch, over two versions of the weights."""
+    from distributed_tensorflow_models_amd.ops import nn as F
+    torch.manual_seed(12)
+    B, Kin = 48, 256
+    x = torch.randn(B, Kin, device=DEV)
+    labels = torch.randint(0, N, (B,), device=DEV)
+    w = torch.nn.Parameter((torch.randn(Kin, N, device=DEV) / Kin ** 0.5))
+    b = torch.nn.Parameter(torch.randn(N, device=DEV) * 0.1)
+    used0 = F.PAD_BASE_USED[0]
+    for version in range(2):
+        if version:
+            with torch.no_grad():
+                w.add_(0.01)
+                b.add_(0.02)
+            F.invalidate_weight_copies([w])
+            F.refresh_flipped()
+        w.grad = b.grad = None
+        xi = x.clone().requires_grad_()
+        logits = F.linear(xi.to(torch.bfloat16), w, b)
+        loss = 0.4 * F.softmax_cross_entropy(logits, labels, 0.1).mean()
+        loss.backward()
+        torch.cuda.synchronize()
+        xr = x.clone().requires_grad_()
+        wr, br = w.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+        lr = xr.to(torch.bfloat16).float() @ wr.to(torch.bfloat16).float() + br
+        lref = 0.4 * ref.softmax_cross_entropy(lr, labels, 0.1).mean()
+        lref.backward()
+        assert abs(float(loss.detach()) - float(lref.detach())) < 2e-2 * max(1.0, abs(float(lref.detach())))
+        assert _rel(xi.grad, xr.grad) < 3e-2
+        assert _rel(w.grad, wr.grad) < 3e-2 and _rel(b.grad, br.grad) < 3e-2
+    if N % 8:
+        assert F.PAD_BASE_USED[0] >= used0 + 2
+
+
 @pytest.mark.parametrize("tile", [10, 11, 12, 13, 14, 15])
 def test_conv_lds_dma_tiles_match_default(tile):
     """The opt-in LDS-DMA conv kernels (DTM_CONV_TILE=10..12) give the default kernel's results
