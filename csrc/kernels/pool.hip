@@ -173,8 +173,10 @@ __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const bf16_t* __restri
   }
 }
 
-// global mean over H*W: x[N][HW][C] -> y[N][C] (fp32 out, feeds the logits GEMM)
-__global__ __launch_bounds__(256) void global_avg_fwd_kernel(const bf16_t* __restrict__ x, float* __restrict__ y, int HW,
+// global mean over H*W: x[N][HW][C] -> y[N][C] (fp32 out, or bf16 when it only feeds the logits GEMM: the cast
+// launch of its input disappears, same rounding)
+template <typename TO>
+__global__ __launch_bounds__(256) void global_avg_fwd_kernel(const bf16_t* __restrict__ x, TO* __restrict__ y, int HW,
                                                              int C) {
   const int n = blockIdx.y;
   const int c = blockIdx.x * 256 + threadIdx.x;
@@ -182,16 +184,21 @@ __global__ __launch_bounds__(256) void global_avg_fwd_kernel(const bf16_t* __res
   const bf16_t* p = x + (long)n * HW * C + c;
   float s = 0.f;
   for (int i = 0; i < HW; ++i) s += bf2f(p[(long)i * C]);
-  y[(long)n * C + c] = s / (float)HW;
+  if constexpr (sizeof(TO) == 2) y[(long)n * C + c] = f2bf(s / (float)HW);
+  else y[(long)n * C + c] = s / (float)HW;
 }
-__global__ __launch_bounds__(256) void global_avg_bwd_kernel(const float* __restrict__ dy, bf16_t* __restrict__ dx, int N,
+template <typename TI>
+__global__ __launch_bounds__(256) void global_avg_bwd_kernel(const TI* __restrict__ dy, bf16_t* __restrict__ dx, int N,
                                                              int HW, int C) {
   const long total = (long)N * HW * C;
   const float inv = 1.f / (float)HW;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     int c = i % C;
     long n = i / ((long)HW * C);
-    dx[i] = f2bf(dy[n * C + c] * inv);
+    float g;
+    if constexpr (sizeof(TI) == 2) g = bf2f(dy[n * C + c]);
+    else g = dy[n * C + c];
+    dx[i] = f2bf(g * inv);
   }
 }
 
@@ -695,12 +702,21 @@ DTM_API void dtm_avgpool_bwd(const void* dy, void* dx, const PoolArgs* a, int co
                        (bf16_t*)dx, *a, count_pad);
 }
 DTM_API void dtm_global_avg_fwd(const void* x, float* y, int N, int HW, int C, void* stream) {
-  hipLaunchKernelGGL(global_avg_fwd_kernel, dim3((C + 255) / 256, N), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(global_avg_fwd_kernel<float>, dim3((C + 255) / 256, N), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)x, y, HW, C);
 }
 DTM_API void dtm_global_avg_bwd(const float* dy, void* dx, int N, int HW, int C, void* stream) {
-  hipLaunchKernelGGL(global_avg_bwd_kernel, dim3(pgrid((long)N * HW * C)), dim3(256), 0, (hipStream_t)stream, dy,
-                     (bf16_t*)dx, N, HW, C);
+  hipLaunchKernelGGL(global_avg_bwd_kernel<float>, dim3(pgrid((long)N * HW * C)), dim3(256), 0, (hipStream_t)stream,
+                     dy, (bf16_t*)dx, N, HW, C);
+}
+// bf16 output / bf16 incoming gradient (the pooled features feed a bf16 logits layer)
+DTM_API void dtm_global_avg_fwd_bf16(const void* x, void* y, int N, int HW, int C, void* stream) {
+  hipLaunchKernelGGL(global_avg_fwd_kernel<bf16_t>, dim3((C + 255) / 256, N), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)x, (bf16_t*)y, HW, C);
+}
+DTM_API void dtm_global_avg_bwd_bf16(const void* dy, void* dx, int N, int HW, int C, void* stream) {
+  hipLaunchKernelGGL(global_avg_bwd_kernel<bf16_t>, dim3(pgrid((long)N * HW * C)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)dy, (bf16_t*)dx, N, HW, C);
 }
 
 // y = maxpool(relu(x*scale + shift)) with a uint8 argmax per output element (ss = [scale; shift; ...])

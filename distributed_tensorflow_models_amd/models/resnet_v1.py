@@ -197,7 +197,8 @@ class ResNetV1(Layer):
                     end_points[name] = net
                 net = subsample(net, sub)
         if self.global_pool:
-            net = F.global_avg_pool(net).reshape(net.shape[0], 1, 1, -1)
+            # (bf16 when the logits layer follows: it computes in bf16, the cast launch disappears)
+            net = F.global_avg_pool(net, out_bf16=self.logits is not None).reshape(net.shape[0], 1, 1, -1)
             if end_points is not None:
                 end_points["global_pool"] = net
         if self.logits is not None:

@@ -294,12 +294,27 @@ class _Conv2dFn(torch.autograd.Function):
         db = None
         if ctx.has_b and ctx.needs_input_grad[2]:
             if gb is None:
-                gb = dy.reshape(-1, g.K).float().sum(0)
+                gb = _col_sums(dy.reshape(-1, g.K), ctx.bias_param)
             db = _accum_param_grad(ctx.bias_param, gb)
         return dx, dw, db, None, None
 
 
 _UNIT_SS = {}
+
+
+def _col_sums(g, param):
+    """fp32 column sums of a [M][K] gradient (a bias gradient).  bf16 with K % 8 == 0 and a data-parallel gradient
+    slot on the parameter (consumed at once by _accum_param_grad): one BN-statistics pass + its row reduction into the
+    step's zero arena instead of a float cast + torch reduction; otherwise the torch form (its result may become
+    param.grad, which must not live in the arena)."""
+    K = g.shape[-1]
+    if (g.is_cuda and g.dtype == torch.bfloat16 and K % 8 == 0 and K // 8 <= 256 and g.is_contiguous()
+            and getattr(param, "main_grad", None) is not None):
+        from .fused import arena
+        st = arena.zeros((2, K), g.device)
+        _lib.lib().dtm_bn_stats(_lib.ptr(g), _lib.ptr(st), g.numel() // K, K, _lib.stream_ptr())
+        return st[0]
+    return g.reshape(-1, K).float().sum(0)
 
 
 def _relu_bias_bwd_ok(dy):
@@ -720,11 +735,12 @@ def avg_pool(x, kernel, stride, padding="VALID", count_pad=False, grad_handoff=F
 
 class _GlobalAvgFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, out_bf16):
         L = _lib.lib()
         N, H, W, C = x.shape
-        y = torch.empty((N, C), device=x.device, dtype=torch.float32)
-        L.dtm_global_avg_fwd(_lib.ptr(x.contiguous()), _lib.ptr(y), N, H * W, C, _lib.stream_ptr())
+        y = torch.empty((N, C), device=x.device, dtype=torch.bfloat16 if out_bf16 else torch.float32)
+        (L.dtm_global_avg_fwd_bf16 if out_bf16 else L.dtm_global_avg_fwd)(_lib.ptr(x.contiguous()), _lib.ptr(y), N,
+                                                                          H * W, C, _lib.stream_ptr())
         ctx.shape = x.shape
         return y
 
@@ -733,16 +749,20 @@ class _GlobalAvgFn(torch.autograd.Function):
         L = _lib.lib()
         N, H, W, C = ctx.shape
         dx = torch.empty((N, H, W, C), device=dy.device, dtype=torch.bfloat16)
-        L.dtm_global_avg_bwd(_lib.ptr(dy.float().contiguous()), _lib.ptr(dx), N, H * W, C, _lib.stream_ptr())
-        return dx
+        if dy.dtype == torch.bfloat16:  # (the bf16-output form: its gradient comes back in bf16)
+            L.dtm_global_avg_bwd_bf16(_lib.ptr(dy.contiguous()), _lib.ptr(dx), N, H * W, C, _lib.stream_ptr())
+        else:
+            L.dtm_global_avg_bwd(_lib.ptr(dy.float().contiguous()), _lib.ptr(dx), N, H * W, C, _lib.stream_ptr())
+        return dx, None
 
 
-def global_avg_pool(x):
-    """mean over H, W -> [N, C] fp32."""
+def global_avg_pool(x, out_bf16=False):
+    """mean over H, W -> [N, C] fp32 (out_bf16: bf16, rounded as a cast of the fp32 mean would be - for a consumer that
+    computes in bf16 anyway, e.g. the logits layer)."""
     x = as_tensor(x)
     if not x.is_cuda:
         return ref.global_avg_pool(x)
-    return _GlobalAvgFn.apply(x.to(torch.bfloat16))
+    return _GlobalAvgFn.apply(x.to(torch.bfloat16), bool(out_bf16))
 
 
 # ---------------------------------------------------------------------------------------------
@@ -889,7 +909,9 @@ class _LinearHipFn(torch.autograd.Function):
                 dw = _accum_param_grad(w, target[:, :N] if Np != N else target)
         db = None
         if ctx.b is not None and ctx.needs_input_grad[2]:
-            db = _accum_param_grad(ctx.b, gb if gb is not None else dy16.float().sum(0))
+            if gb is None:
+                gb = _col_sums(dyp, ctx.b)[:N] if Np != N else _col_sums(dy16, ctx.b)
+            db = _accum_param_grad(ctx.b, gb)
         return dx, dw, db, None
 
 

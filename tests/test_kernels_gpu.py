@@ -547,6 +547,45 @@ def test_conv_wgrad_pipelined_tiles_match_reference(tile, case):
     assert _rel(dw, wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("shape", [(256, 1000), (48, 1008), (4, 7, 7, 64), (3, 24)])
+def test_bias_column_sums_match_torch(shape):
+    """Bias gradients (column sums of a bf16 [.., K] gradient) on the BN-statistics kernel into the step's zero arena
+    when the parameter has a data-parallel gradient slot, vs the fp32 torch reduction; other cases take torch."""
+    from distributed_tensorflow_models_amd.ops import nn as F
+    from distributed_tensorflow_models_amd.ops.fused import arena
+    torch.manual_seed(13)
+    g = torch.randn(*shape, device=DEV).to(torch.bfloat16)
+    K = shape[-1]
+    p = torch.nn.Parameter(torch.zeros(K, device=DEV))
+    want = g.reshape(-1, K).float().sum(0)
+    assert _rel(F._col_sums(g.reshape(-1, K), p), want) < 1e-5  # (no slot: torch)
+    p.main_grad = torch.zeros(K, device=DEV)
+    arena.begin_step(g.device)
+    try:
+        got = F._col_sums(g.reshape(-1, K), p).clone()
+        torch.cuda.synchronize()
+    finally:
+        arena.end_step()
+    assert _rel(got, want) < 1e-5
+
+
+@pytest.mark.parametrize("C", [2048, 64])
+def test_global_avg_pool_bf16_output_matches_cast(C):
+    """The bf16-output global average pool (the ResNet logits input) == the fp32 pool cast to bf16, forward and
+    backward (a bf16 incoming gradient)."""
+    from distributed_tensorflow_models_amd.ops import nn as F
+    torch.manual_seed(14)
+    x = torch.randn(8, 7, 7, C, device=DEV).to(torch.bfloat16)
+    xa, xb = x.clone().requires_grad_(), x.clone().requires_grad_()
+    ya = F.global_avg_pool(xa).to(torch.bfloat16)
+    yb = F.global_avg_pool(xb, out_bf16=True)
+    assert yb.dtype == torch.bfloat16 and torch.equal(ya, yb)
+    dy = torch.randn_like(yb)
+    ya.backward(dy)
+    yb.backward(dy)
+    assert torch.equal(xa.grad, xb.grad)
+
+
 @pytest.mark.parametrize("N", [1001, 1000, 10])
 def test_fc_softmax_xent_padded_head_matches_torch(N):
     """Logits FC + label-smoothed softmax cross-entropy (the Inception-v3 / ResNet heads): the loss backward writes the
