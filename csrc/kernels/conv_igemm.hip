@@ -2700,6 +2700,8 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
     // the 8-wave 256x256 tile on the wide deep-reduction layers (profiles/r2_wgrad_tiles_w8.txt:
     // 14x14 / 7x7 3x3 -8..-13 %, 7x7 1024->2048 -7 %; it loses on every K < 256 or short-RSC layer)
     if (g_tile_w8 && d->K >= 256 && a.Kg >= 1024 && (d->R * d->S > 1 || d->K >= 1024)) wt = 12;
+    // (per-shape wins of the 256x256 tile on Inception's 17x17 1x7 / 7x1 layers and of 128x128 on its 8x8 1x3 / 3x1
+    //  ones, profiles/r5/r5_s37_wgrad_occ_sweep.log, measured neutral on the step together: not adopted)
     // merged sibling heads (one wgrad over several 1x1 convs' output gradients, dst): the 256 x 256 tile also wins
     // at short reductions on <= 160k-pixel maps (profiles/r5/r5_s27_wgrad_heads_sweep.log, Inception-v3 batch 128:
     // 17x17 768 -> 704 87.9 -> 75.6 us, 35x35 192 -> 208 47.6 -> 42.0 us)
