@@ -406,7 +406,9 @@ __global__ __launch_bounds__(256) void maxpool_bnrelu_bwd_k3s2_kernel(const bf16
                                                                       const float* __restrict__ ss,
                                                                       bf16_t* __restrict__ dx, float* __restrict__ part,
                                                                       PoolArgs a, FastDiv fd_BW, FastDiv fd_BH,
-                                                                      int unscaled, int rpb, const bf16_t* __restrict__ zero) {
+                                                                      int unscaled, int rpb, const bf16_t* __restrict__ zero,
+                                                                      int ldy) {
+  // ldy: dy's pixel pitch in elements (a.C; more when dy is the channel slice of a concat's gradient, read in place)
   const int cols = a.C >> 3, t = threadIdx.x, RP = 256 / cols, c0 = (t % cols) * 8, lr0 = t / cols;
   const int BH = (a.H + a.PH + 1) >> 1, BW = (a.W + a.PW + 1) >> 1;
   float sc[8], sh[8], a1[8], a0[8];
@@ -431,9 +433,9 @@ __global__ __launch_bounds__(256) void maxpool_bnrelu_bwd_k3s2_kernel(const bf16
       for (int j = 0; j < 2; ++j) {
         const int p = (int)bi - 1 + i, q = (int)bj - 1 + j;
         wv[i][j] = p >= 0 && p < a.P && q >= 0 && q < a.Q;
-        const size_t oo = wv[i][j] ? (((size_t)n * a.P + p) * a.Q + q) * a.C + c0 : 0;
-        gv[i][j] = *(const uint4*)(wv[i][j] ? dy + oo : zero);
-        av[i][j] = wv[i][j] ? *(const uint2*)(arg + oo) : make_uint2(0xffffffffu, 0xffffffffu);
+        const size_t po = wv[i][j] ? ((size_t)n * a.P + p) * a.Q + q : 0;
+        gv[i][j] = *(const uint4*)(wv[i][j] ? dy + po * ldy + c0 : zero);
+        av[i][j] = wv[i][j] ? *(const uint2*)(arg + po * a.C + c0) : make_uint2(0xffffffffu, 0xffffffffu);
       }
     }
     uint4 xv[2][2];
@@ -640,22 +642,11 @@ DTM_API void dtm_maxpool_fwd(const void* x, void* y, void* arg, const PoolArgs* 
     hipLaunchKernelGGL(maxpool_fwd_kernel<1>, dim3(pgrid(work)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
                        (bf16_t*)y, (uint8_t*)arg, *a);
 }
+static void maxpool_bwd_k3s2(const void* dy, int ldy, const void* arg, void* dx, const PoolArgs* a, void* stream);
 DTM_API void dtm_maxpool_bwd(const void* dy, const void* arg, void* dx, const PoolArgs* a, void* stream) {
   long work = (long)a->N * a->H * a->W * a->C;
   if (a->C % 8 == 0 && a->C / 8 <= 256 && k3s2(a) && (long)a->N * a->H * a->W * a->C < (1l << 31)) {
-    const int cols = a->C / 8, RP = 256 / cols;  // (the BN kernel's row mapping: one row = a 2 x 2 pixel block)
-    const int BH = (a->H + a->PH + 1) / 2, BW = (a->W + a->PW + 1) / 2;
-    const long MB = (long)a->N * BH * BW;
-    long b = MB * cols / (256 * 2);
-    if (b < 1) b = 1;
-    if (b > 2048) b = 2048;
-    long rpb = (MB + b - 1) / b;
-    rpb = (rpb + RP - 1) / RP * RP;
-    const int blocks = (int)((MB + rpb - 1) / rpb);
-    hipLaunchKernelGGL(maxpool_bnrelu_bwd_k3s2_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
-                       (const bf16_t*)dy, (const uint8_t*)arg, (const bf16_t*)nullptr, (const float*)nullptr,
-                       (bf16_t*)dx, (float*)nullptr, *a, make_fastdiv(BW), make_fastdiv(BH), 0, (int)rpb,
-                       (const bf16_t*)dtm_zero_chunk());
+    maxpool_bwd_k3s2(dy, a->C, arg, dx, a, stream);
     return;
   }
   if (a->C % 8 == 0)
@@ -664,6 +655,30 @@ DTM_API void dtm_maxpool_bwd(const void* dy, const void* arg, void* dx, const Po
   else
     hipLaunchKernelGGL(maxpool_bwd_kernel<1>, dim3(pgrid(work)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
                        (const uint8_t*)arg, (bf16_t*)dx, *a);
+}
+// dy read in place with a pixel pitch of ldy elements (the max-pool branch's slice of a concat gradient): 3x3 / stride 2
+// only (-1 otherwise: the caller makes dy contiguous)
+DTM_API int dtm_maxpool_bwd_ld(const void* dy, int ldy, const void* arg, void* dx, const PoolArgs* a, void* stream) {
+  if (!(a->C % 8 == 0 && a->C / 8 <= 256 && k3s2(a) && (long)a->N * a->H * a->W * a->C < (1l << 31)) || ldy < a->C ||
+      ldy % 8 || ((uintptr_t)dy & 15) || (long)a->N * a->P * a->Q * ldy >= (1l << 31))
+    return -1;
+  maxpool_bwd_k3s2(dy, ldy, arg, dx, a, stream);
+  return 0;
+}
+static void maxpool_bwd_k3s2(const void* dy, int ldy, const void* arg, void* dx, const PoolArgs* a, void* stream) {
+  const int cols = a->C / 8, RP = 256 / cols;  // (the BN kernel's row mapping: one row = a 2 x 2 pixel block)
+  const int BH = (a->H + a->PH + 1) / 2, BW = (a->W + a->PW + 1) / 2;
+  const long MB = (long)a->N * BH * BW;
+  long b = MB * cols / (256 * 2);
+  if (b < 1) b = 1;
+  if (b > 2048) b = 2048;
+  long rpb = (MB + b - 1) / b;
+  rpb = (rpb + RP - 1) / RP * RP;
+  const int blocks = (int)((MB + rpb - 1) / rpb);
+  hipLaunchKernelGGL(maxpool_bnrelu_bwd_k3s2_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)dy, (const uint8_t*)arg, (const bf16_t*)nullptr, (const float*)nullptr,
+                     (bf16_t*)dx, (float*)nullptr, *a, make_fastdiv(BW), make_fastdiv(BH), 0, (int)rpb,
+                     (const bf16_t*)dtm_zero_chunk(), ldy);
 }
 static bool k3s1(const PoolArgs* a) {
   return g_pool_k3s2 && a->KH == 3 && a->KW == 3 && a->SH == 1 && a->SW == 1 && a->PH >= 0 && a->PH <= 1 &&
@@ -754,7 +769,7 @@ DTM_API int dtm_maxpool_bnrelu_bwd(const void* dy, const void* arg, const void* 
     if (!ws) return -4;
     hipLaunchKernelGGL(maxpool_bnrelu_bwd_k3s2_kernel<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)dy, (const uint8_t*)arg, (const bf16_t*)x, ss, (bf16_t*)dx, ws, *a,
-                       make_fastdiv(BW), make_fastdiv(BH), unscaled, (int)rpb, (const bf16_t*)dtm_zero_chunk());
+                       make_fastdiv(BW), make_fastdiv(BH), unscaled, (int)rpb, (const bf16_t*)dtm_zero_chunk(), a->C);
     dtm_reduce_rows(ws, blocks, 2 * a->C, 2 * a->C, sums, (hipStream_t)stream);
     return 0;
   }

@@ -215,7 +215,12 @@ class InceptionV3Slim(Layer):
 
     def run_logits(self, net, training=True):
         k = net.shape[1]
-        net = F.avg_pool(net, (k, net.shape[2]), 1, "VALID")
+        if _t(net).is_cuda:
+            # the whole-map VALID average pool = the global mean (its kernel: one block per 256 channels and image
+            # instead of one lane per output chunk, 128 blocks for the 8x8x2048 map; bf16 as the pool would store)
+            net = F.global_avg_pool(net, out_bf16=True)
+        else:
+            net = F.avg_pool(net, (k, net.shape[2]), 1, "VALID")
         net = self.dropout(_t(net).reshape(net.shape[0], -1), training)
         return self.fc(net, training)
 

@@ -87,6 +87,7 @@ _SIGS = {
     "dtm_bn_param_grad": (None, [_P, _P, _P, _I, _P]),
     "dtm_maxpool_fwd": (None, [_P, _P, _P, ctypes.POINTER(PoolArgs), _P]),
     "dtm_maxpool_bwd": (None, [_P, _P, _P, ctypes.POINTER(PoolArgs), _P]),
+    "dtm_maxpool_bwd_ld": (_I, [_P, _I, _P, _P, ctypes.POINTER(PoolArgs), _P]),
     "dtm_avgpool_fwd": (None, [_P, _P, ctypes.POINTER(PoolArgs), _I, _P]),
     "dtm_avgpool_bwd": (None, [_P, _P, ctypes.POINTER(PoolArgs), _I, _P]),
     "dtm_global_avg_fwd": (None, [_P, _P, _I, _I, _I, _P]),

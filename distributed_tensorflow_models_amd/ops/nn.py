@@ -625,6 +625,17 @@ def _pool_grad_out(slot, dx):
     return dx
 
 
+def _pixel_pitch(t):
+    """Element pitch between consecutive pixels of an NHWC bf16 tensor whose channels are contiguous (a concat
+    gradient's channel slice: pitch = the concat width), or None."""
+    if t.dim() != 4 or t.dtype != torch.bfloat16 or t.stride(3) != 1:
+        return None
+    ld = t.stride(2)
+    if t.stride(1) != ld * t.shape[2] or t.stride(0) != t.stride(1) * t.shape[1]:
+        return None
+    return ld
+
+
 class _MaxPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, g, slot=None):
@@ -645,7 +656,11 @@ class _MaxPoolFn(torch.autograd.Function):
         g = ctx.g
         dx = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
         a = g.as_args(_lib.PoolArgs)
-        L.dtm_maxpool_bwd(_lib.ptr(dy.contiguous()), _lib.ptr(arg), _lib.ptr(dx), ctypes.byref(a), _lib.stream_ptr())
+        ld = _pixel_pitch(dy)
+        if ld is None or L.dtm_maxpool_bwd_ld(_lib.ptr(dy), ld, _lib.ptr(arg), _lib.ptr(dx), ctypes.byref(a),
+                                              _lib.stream_ptr()) != 0:
+            L.dtm_maxpool_bwd(_lib.ptr(dy.contiguous()), _lib.ptr(arg), _lib.ptr(dx), ctypes.byref(a),
+                              _lib.stream_ptr())
         return _pool_grad_out(ctx.slot, dx), None, None
 
 

@@ -343,6 +343,14 @@ def test_maxpool_k3s2_matches_generic(case):
         out[fast] = (y, arg, dx)
     for i in range(3):
         assert torch.equal(out[1][i], out[0][i]), i
+    if C % 8 == 0:  # dy read in place as the channel slice of a wider (concat) gradient
+        wide = torch.randn(N, g.P, g.Q, C + 24, device=DEV).to(torch.bfloat16)
+        wide[..., 8:8 + C] = dy
+        dxs = torch.empty_like(x)
+        assert L.dtm_maxpool_bwd_ld(_lib.ptr(wide[..., 8:8 + C]), C + 24, _lib.ptr(out[1][1]), _lib.ptr(dxs),
+                                    ctypes.byref(a), s) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(dxs, out[1][2])
     xr = x.float().permute(0, 3, 1, 2).contiguous().requires_grad_()
     yr = tF.max_pool2d(tF.pad(xr, (g.PW, g.PR, g.PH, g.PB), value=-1e30), 3, 2)
     assert torch.equal(out[1][0].float().permute(0, 3, 1, 2), yr)
