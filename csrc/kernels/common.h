@@ -39,6 +39,15 @@ __device__ __forceinline__ float warp_sum(float v) {
   return v;
 }
 
+// XCD-aware block remap (8 XCDs, each with its own L2; the hardware deals workgroup L to XCD L % 8):
+// returns a logical tile id such that the workgroups of one XCD get a contiguous logical range, so
+// the tiles that share an operand (all channel tiles of one pixel tile, all tiles of one split, the
+// overlapping windows of a pool) hit the same L2.  Bijective for any count (guide T1).
+__device__ __forceinline__ int xcd_remap(int L, int nwg) {
+  const int xcd = L & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
+}
+
 // magic-number unsigned division (host computes m, s): q = mulhi(n, m) >> s  for n < 2^31
 struct FastDiv {
   uint32_t d, m, s;

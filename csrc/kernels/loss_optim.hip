@@ -166,6 +166,26 @@ __global__ __launch_bounds__(256) void scale_rows_pad_kernel(const T* __restrict
   }
 }
 
+// The scalar training loss from up to 4 per-row loss vectors: out = sum_h w_h * sum_r loss[h][r] (w_h = the head's
+// weight / batch: the mean, the aux-head weight and the batch weight in one launch, one block, fixed order).
+struct LossW {
+  float w[4];
+};
+__global__ __launch_bounds__(256) void loss_combine_kernel(const float* __restrict__ loss, int heads, int B, LossW lw,
+                                                           float* __restrict__ out) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (int h = 0; h < heads; ++h) {
+    float s = 0.f;
+    for (int r = threadIdx.x; r < B; r += 256) s += loss[(long)h * B + r];
+    acc += s * lw.w[h];
+  }
+  acc = warp_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 }  // namespace dtm
 using namespace dtm;
 
@@ -190,6 +210,14 @@ DTM_API void dtm_softmax_xent(const void* logits, int logits_bf16, const int* la
   else
     hipLaunchKernelGGL(softmax_xent_kernel<float>, dim3(B), dim3(256), 0, (hipStream_t)stream, (const float*)logits,
                        labels, loss, (float*)dlogits, K, smoothing, gscale, row_weight);
+}
+
+DTM_API int dtm_loss_combine(const float* loss, int heads, int B, const float* w, float* out, void* stream) {
+  if (heads < 1 || heads > 4 || B < 1) return -1;
+  LossW lw{};
+  for (int h = 0; h < heads; ++h) lw.w[h] = w[h];
+  hipLaunchKernelGGL(loss_combine_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, loss, heads, B, lw, out);
+  return 0;
 }
 
 DTM_API int dtm_opt_chunk_size() { return OPT_CHUNK; }

@@ -173,6 +173,163 @@ __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const bf16_t* __restri
   }
 }
 
+// The generic avg pool with 8 channels per lane and 32-bit magic-number index math (the 64-bit divisions of the
+// V-template forms above dominated their time: 30 us for the backward of Inception's 5x5/3 aux-head pool over
+// 17x17x768).  Same tap order and divisor as those, so the results match them exactly.  The backward can add into
+// dx (accum != 0): the aux head's pool gradient folded into the block-input gradient the main path produced
+// (ops/nn.py avg_pool grad_tail) instead of a separate add over the whole map.
+__global__ __launch_bounds__(256) void avgpool_fwd8_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                           PoolArgs a, int count_pad, FastDiv fcols, FastDiv fQ,
+                                                           FastDiv fP, int total) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const uint32_t o = fdiv(i, fcols);
+    const int cv = (int)(i - o * fcols.d) * 8;
+    const uint32_t t = fdiv(o, fQ);
+    const int q = (int)(o - t * fQ.d);
+    const int n = (int)fdiv(t, fP), p = (int)(t - n * fP.d);
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    int cnt = 0;
+    for (int r = 0; r < a.KH; ++r) {
+      const int h = p * a.SH - a.PH + r;
+      if (h < 0 || h >= a.H) continue;
+      for (int s = 0; s < a.KW; ++s) {
+        const int w = q * a.SW - a.PW + s;
+        if (w < 0 || w >= a.W) continue;
+        float f[8];
+        ld<8>(x + ((n * a.H + h) * a.W + w) * a.C + cv, f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += f[e];
+        ++cnt;
+      }
+    }
+    const float inv = 1.f / (float)(count_pad ? a.KH * a.KW : max(cnt, 1));
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= inv;
+    st<8>(y + o * a.C + cv, acc);
+  }
+}
+__global__ __launch_bounds__(256) void avgpool_bwd8_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx,
+                                                           PoolArgs a, int count_pad, int accum, FastDiv fcols,
+                                                           FastDiv fW, FastDiv fH, int total) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const uint32_t o = fdiv(i, fcols);
+    const int cv = (int)(i - o * fcols.d) * 8;
+    const uint32_t t = fdiv(o, fW);
+    const int w = (int)(o - t * fW.d);
+    const int n = (int)fdiv(t, fH), h = (int)(t - n * fH.d);
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    const int plo = first_win(h + a.PH - a.KH + 1, a.SH), phi = min(a.P - 1, (h + a.PH) / a.SH);
+    const int qlo = first_win(w + a.PW - a.KW + 1, a.SW), qhi = min(a.Q - 1, (w + a.PW) / a.SW);
+    for (int p = plo; p <= phi; ++p) {
+      const int h0 = p * a.SH - a.PH;
+      if (h < h0 || h >= h0 + a.KH) continue;
+      const int hc = min(h0 + a.KH, a.H) - max(h0, 0);
+      for (int q = qlo; q <= qhi; ++q) {
+        const int w0 = q * a.SW - a.PW;
+        if (w < w0 || w >= w0 + a.KW) continue;
+        const int wcnt = min(w0 + a.KW, a.W) - max(w0, 0);
+        const float inv = 1.f / (float)(count_pad ? a.KH * a.KW : max(hc * wcnt, 1));
+        float g[8];
+        ld<8>(dy + ((n * a.P + p) * a.Q + q) * a.C + cv, g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += g[e] * inv;
+      }
+    }
+    if (accum) {
+      float f[8];
+      ld<8>(dx + o * a.C + cv, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += f[e];
+    }
+    st<8>(dx + o * a.C + cv, acc);
+  }
+}
+
+// VALID K x K / stride S average pool with every window in bounds (Inception's 5x5/3 aux-head pool): the tap
+// loops are compile-time, so a lane issues all its loads back to back instead of one dependent load per runtime
+// loop trip (the generic kernels above were load-latency bound: 18 us forward / 29 us backward for that pool).
+// One lane per output (forward) or input (backward) 8-channel chunk, no grid-stride loop; same tap order and
+// divisor as the generic kernels, so the results match them bit for bit.
+template <int K>
+__global__ __launch_bounds__(256) void avgpool_fwd_valid_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                                PoolArgs a, FastDiv fcols, FastDiv fQ, FastDiv fP,
+                                                                int total) {
+  const int i = xcd_remap(blockIdx.x, gridDim.x) * 256 + threadIdx.x;  // (overlapping windows: one L2)
+  if (i >= total) return;
+  const uint32_t o = fdiv(i, fcols);
+  const int cv = (int)(i - o * fcols.d) * 8;
+  const uint32_t t = fdiv(o, fQ);
+  const int q = (int)(o - t * fQ.d);
+  const int n = (int)fdiv(t, fP), p = (int)(t - n * fP.d);
+  const bf16_t* base = x + ((n * a.H + p * a.SH) * a.W + q * a.SW) * a.C + cv;
+  uint4 v[K * K];
+#pragma unroll
+  for (int r = 0; r < K; ++r)
+#pragma unroll
+    for (int s = 0; s < K; ++s) v[r * K + s] = *(const uint4*)(base + (r * a.W + s) * a.C);
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+#pragma unroll
+  for (int k = 0; k < K * K; ++k) {
+    const uint4 u = v[k];
+    acc[0] += lo_bf(u.x); acc[1] += hi_bf(u.x); acc[2] += lo_bf(u.y); acc[3] += hi_bf(u.y);
+    acc[4] += lo_bf(u.z); acc[5] += hi_bf(u.z); acc[6] += lo_bf(u.w); acc[7] += hi_bf(u.w);
+  }
+  const float inv = 1.f / (float)(K * K);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] *= inv;
+  st<8>(y + o * a.C + cv, acc);
+}
+template <int K, int S>
+__global__ __launch_bounds__(256) void avgpool_bwd_valid_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx,
+                                                                PoolArgs a, int accum, FastDiv fcols, FastDiv fW,
+                                                                FastDiv fH, int total, const bf16_t* __restrict__ zero) {
+  constexpr int MW = (K + S - 1) / S;  // windows covering a pixel, per dimension, at most
+  const int i = xcd_remap(blockIdx.x, gridDim.x) * 256 + threadIdx.x;  // (a dy chunk's 25 readers: one L2)
+  if (i >= total) return;
+  const uint32_t o = fdiv(i, fcols);
+  const int cv = (int)(i - o * fcols.d) * 8;
+  const uint32_t t = fdiv(o, fW);
+  const int w = (int)(o - t * fW.d);
+  const int n = (int)fdiv(t, fH), h = (int)(t - n * fH.d);
+  const int plo = first_win(h - K + 1, S), phi = min(a.P - 1, h / S);
+  const int qlo = first_win(w - K + 1, S), qhi = min(a.Q - 1, w / S);
+  uint4 g[MW * MW];
+#pragma unroll
+  for (int dp = 0; dp < MW; ++dp)
+#pragma unroll
+    for (int dq = 0; dq < MW; ++dq) {
+      const bool ok = plo + dp <= phi && qlo + dq <= qhi;
+      const bf16_t* src = ok ? dy + ((n * a.P + plo + dp) * a.Q + qlo + dq) * a.C + cv : zero;
+      g[dp * MW + dq] = *(const uint4*)src;
+    }
+  uint4 prev = make_uint4(0, 0, 0, 0);
+  if (accum) prev = *(const uint4*)(dx + o * a.C + cv);
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  const float inv = 1.f / (float)(K * K);
+#pragma unroll
+  for (int dp = 0; dp < MW; ++dp)
+#pragma unroll
+    for (int dq = 0; dq < MW; ++dq) {
+      if (plo + dp > phi || qlo + dq > qhi) continue;
+      const uint4 u = g[dp * MW + dq];
+      acc[0] += lo_bf(u.x) * inv; acc[1] += hi_bf(u.x) * inv; acc[2] += lo_bf(u.y) * inv; acc[3] += hi_bf(u.y) * inv;
+      acc[4] += lo_bf(u.z) * inv; acc[5] += hi_bf(u.z) * inv; acc[6] += lo_bf(u.w) * inv; acc[7] += hi_bf(u.w) * inv;
+    }
+  if (accum) {
+    acc[0] += lo_bf(prev.x); acc[1] += hi_bf(prev.x); acc[2] += lo_bf(prev.y); acc[3] += hi_bf(prev.y);
+    acc[4] += lo_bf(prev.z); acc[5] += hi_bf(prev.z); acc[6] += lo_bf(prev.w); acc[7] += hi_bf(prev.w);
+  }
+  st<8>(dx + o * a.C + cv, acc);
+}
+
 // global mean over H*W: x[N][HW][C] -> y[N][C] (fp32 out, or bf16 when it only feeds the logits GEMM: the cast
 // launch of its input disappears, same rounding)
 template <typename TO>
@@ -200,6 +357,78 @@ __global__ __launch_bounds__(256) void global_avg_bwd_kernel(const TI* __restric
     else g = dy[n * C + c];
     dx[i] = f2bf(g * inv);
   }
+}
+
+// The same two with 8 channels per lane (C % 8 == 0).  Forward: a block is one image and 512 channels, its four
+// waves split the H*W rows (16-B loads, four in flight per lane) and combine through LDS in a fixed order (the
+// one-lane-per-channel form ran H*W dependent 2-B loads per lane: 17.6 us for Inception's 8x8x2048 logits pool).
+// Backward: one lane per 8-channel output chunk, 32-bit magic-number indexing, no grid-stride loop (the form above
+// spent its time in 64-bit divisions: 27 us Inception / 40 us ResNet-50 for a write of 17 / 51 MB).
+template <typename TO>
+__global__ __launch_bounds__(256) void global_avg_fwd8_kernel(const bf16_t* __restrict__ x, TO* __restrict__ y, int HW,
+                                                              int C) {
+  __shared__ float red[3][8][64];
+  const int n = blockIdx.y, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = (blockIdx.x * 64 + lane) * 8;
+  const bool live = c < C;
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  if (live) {
+    const bf16_t* p = x + (long)n * HW * C + c;
+    int i = wv;
+    for (; i + 12 < HW; i += 16) {
+      uint4 u[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) u[k] = *(const uint4*)(p + (long)(i + 4 * k) * C);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc[0] += lo_bf(u[k].x); acc[1] += hi_bf(u[k].x); acc[2] += lo_bf(u[k].y); acc[3] += hi_bf(u[k].y);
+        acc[4] += lo_bf(u[k].z); acc[5] += hi_bf(u[k].z); acc[6] += lo_bf(u[k].w); acc[7] += hi_bf(u[k].w);
+      }
+    }
+    for (; i < HW; i += 4) {
+      const uint4 u = *(const uint4*)(p + (long)i * C);
+      acc[0] += lo_bf(u.x); acc[1] += hi_bf(u.x); acc[2] += lo_bf(u.y); acc[3] += hi_bf(u.y);
+      acc[4] += lo_bf(u.z); acc[5] += hi_bf(u.z); acc[6] += lo_bf(u.w); acc[7] += hi_bf(u.w);
+    }
+  }
+  if (wv) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[wv - 1][e][lane] = acc[e];
+  }
+  __syncthreads();
+  if (wv || !live) return;
+  float o[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = ((acc[e] + red[0][e][lane]) + (red[1][e][lane] + red[2][e][lane])) / (float)HW;
+  if constexpr (sizeof(TO) == 2) {
+    st<8>((bf16_t*)y + (long)n * C + c, o);
+  } else {
+    float4* q = (float4*)((float*)y + (long)n * C + c);
+    q[0] = make_float4(o[0], o[1], o[2], o[3]);
+    q[1] = make_float4(o[4], o[5], o[6], o[7]);
+  }
+}
+template <typename TI>
+__global__ __launch_bounds__(256) void global_avg_bwd8_kernel(const TI* __restrict__ dy, bf16_t* __restrict__ dx, int C,
+                                                              FastDiv fcols, FastDiv fHW, int total, float inv) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const uint32_t o = fdiv(i, fcols);  // pixel n*HW + hw
+  const int cv = (int)(i - o * fcols.d) * 8;
+  const int n = (int)fdiv(o, fHW);
+  float g[8];
+  if constexpr (sizeof(TI) == 2) {
+    ld<8>((const bf16_t*)dy + (long)n * C + cv, g);
+  } else {
+    const float4* q = (const float4*)((const float*)dy + (long)n * C + cv);
+    const float4 a = q[0], b = q[1];
+    g[0] = a.x; g[1] = a.y; g[2] = a.z; g[3] = a.w; g[4] = b.x; g[5] = b.y; g[6] = b.z; g[7] = b.w;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) g[e] *= inv;
+  st<8>(dx + (long)o * C + cv, g);
 }
 
 // ---- BatchNorm-apply + ReLU fused into a max pool (ResNet stem: conv1 -> BN -> ReLU -> 3x3/2 pool) ----
@@ -684,6 +913,31 @@ static bool k3s1(const PoolArgs* a) {
   return g_pool_k3s2 && a->KH == 3 && a->KW == 3 && a->SH == 1 && a->SW == 1 && a->PH >= 0 && a->PH <= 1 &&
          a->PW >= 0 && a->PW <= 1 && a->C % 8 == 0 && (long)a->N * a->H * a->W * a->C < (1l << 31);
 }
+static bool avg8(const PoolArgs* a) {  // the 32-bit-index 8-channel kernels apply
+  return a->C % 8 == 0 && (long)a->N * a->H * a->W * a->C < (1l << 31) && (long)a->N * a->P * a->Q * a->C < (1l << 31);
+}
+static bool valid53(const PoolArgs* a) {  // the 5x5/3 VALID pool with every window in bounds (aux head)
+  return a->KH == 5 && a->KW == 5 && a->SH == 3 && a->SW == 3 && a->PH == 0 && a->PW == 0 &&
+         (a->P - 1) * 3 + 5 <= a->H && (a->Q - 1) * 3 + 5 <= a->W;
+}
+static void avgpool_bwd8(const void* dy, void* dx, const PoolArgs* a, int count_pad, int accum, void* stream) {
+  const long work = (long)a->N * a->H * a->W * a->C;
+  if (valid53(a)) {
+    hipLaunchKernelGGL((avgpool_bwd_valid_kernel<5, 3>), dim3((unsigned)((work / 8 + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, (const bf16_t*)dy, (bf16_t*)dx, *a, accum, make_fastdiv(a->C / 8),
+                       make_fastdiv(a->W), make_fastdiv(a->H), (int)(work / 8), (const bf16_t*)dtm_zero_chunk());
+    return;
+  }
+  hipLaunchKernelGGL(avgpool_bwd8_kernel, dim3(pgrid(work / 8)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
+                     (bf16_t*)dx, *a, count_pad, accum, make_fastdiv(a->C / 8), make_fastdiv(a->W), make_fastdiv(a->H),
+                     (int)(work / 8));
+}
+// dx += avgpool_bwd(dy) (-1 when the 8-channel kernel does not apply: the caller adds itself)
+DTM_API int dtm_avgpool_bwd_acc(const void* dy, void* dx, const PoolArgs* a, int count_pad, void* stream) {
+  if (!avg8(a) || ((uintptr_t)dy & 15) || ((uintptr_t)dx & 15)) return -1;
+  avgpool_bwd8(dy, dx, a, count_pad, 1, stream);
+  return 0;
+}
 DTM_API void dtm_avgpool_fwd(const void* x, void* y, const PoolArgs* a, int count_pad, void* stream) {
   long work = (long)a->N * a->P * a->Q * a->C;
   if (k3s1(a)) {
@@ -693,7 +947,15 @@ DTM_API void dtm_avgpool_fwd(const void* x, void* y, const PoolArgs* a, int coun
                        make_fastdiv(a->Q), make_fastdiv(PR), (const bf16_t*)dtm_zero_chunk());
     return;
   }
-  if (a->C % 8 == 0)
+  if (avg8(a) && valid53(a))
+    hipLaunchKernelGGL(avgpool_fwd_valid_kernel<5>, dim3((unsigned)((work / 8 + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, (const bf16_t*)x, (bf16_t*)y, *a, make_fastdiv(a->C / 8),
+                       make_fastdiv(a->Q), make_fastdiv(a->P), (int)(work / 8));
+  else if (avg8(a))
+    hipLaunchKernelGGL(avgpool_fwd8_kernel, dim3(pgrid(work / 8)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                       (bf16_t*)y, *a, count_pad, make_fastdiv(a->C / 8), make_fastdiv(a->Q), make_fastdiv(a->P),
+                       (int)(work / 8));
+  else if (a->C % 8 == 0)
     hipLaunchKernelGGL(avgpool_fwd_kernel<8>, dim3(pgrid(work / 8)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
                        (bf16_t*)y, *a, count_pad);
   else
@@ -709,29 +971,50 @@ DTM_API void dtm_avgpool_bwd(const void* dy, void* dx, const PoolArgs* a, int co
                        make_fastdiv(a->W), make_fastdiv(HR), (const bf16_t*)dtm_zero_chunk());
     return;
   }
-  if (a->C % 8 == 0)
+  if (avg8(a))
+    avgpool_bwd8(dy, dx, a, count_pad, 0, stream);
+  else if (a->C % 8 == 0)
     hipLaunchKernelGGL(avgpool_bwd_kernel<8>, dim3(pgrid(work / 8)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
                        (bf16_t*)dx, *a, count_pad);
   else
     hipLaunchKernelGGL(avgpool_bwd_kernel<1>, dim3(pgrid(work)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
                        (bf16_t*)dx, *a, count_pad);
 }
+static bool gavg8(const void* x, const void* y, long N, long HW, int C) {
+  return C % 8 == 0 && !((uintptr_t)x & 15) && !((uintptr_t)y & 15) && N * HW * C < (1l << 31) && N <= 65535;
+}
+template <typename TO>
+static void global_avg_fwd(const void* x, TO* y, int N, int HW, int C, void* stream) {
+  if (gavg8(x, y, N, HW, C))
+    hipLaunchKernelGGL(global_avg_fwd8_kernel<TO>, dim3((C / 8 + 63) / 64, N), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)x, y, HW, C);
+  else
+    hipLaunchKernelGGL(global_avg_fwd_kernel<TO>, dim3((C + 255) / 256, N), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)x, y, HW, C);
+}
+template <typename TI>
+static void global_avg_bwd(const TI* dy, void* dx, int N, int HW, int C, void* stream) {
+  if (gavg8(dy, dx, N, HW, C)) {
+    const int total = N * HW * (C / 8);
+    hipLaunchKernelGGL(global_avg_bwd8_kernel<TI>, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, dy,
+                       (bf16_t*)dx, C, make_fastdiv(C / 8), make_fastdiv(HW), total, 1.f / (float)HW);
+  } else {
+    hipLaunchKernelGGL(global_avg_bwd_kernel<TI>, dim3(pgrid((long)N * HW * C)), dim3(256), 0, (hipStream_t)stream,
+                       dy, (bf16_t*)dx, N, HW, C);
+  }
+}
 DTM_API void dtm_global_avg_fwd(const void* x, float* y, int N, int HW, int C, void* stream) {
-  hipLaunchKernelGGL(global_avg_fwd_kernel<float>, dim3((C + 255) / 256, N), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16_t*)x, y, HW, C);
+  global_avg_fwd<float>(x, y, N, HW, C, stream);
 }
 DTM_API void dtm_global_avg_bwd(const float* dy, void* dx, int N, int HW, int C, void* stream) {
-  hipLaunchKernelGGL(global_avg_bwd_kernel<float>, dim3(pgrid((long)N * HW * C)), dim3(256), 0, (hipStream_t)stream,
-                     dy, (bf16_t*)dx, N, HW, C);
+  global_avg_bwd<float>(dy, dx, N, HW, C, stream);
 }
 // bf16 output / bf16 incoming gradient (the pooled features feed a bf16 logits layer)
 DTM_API void dtm_global_avg_fwd_bf16(const void* x, void* y, int N, int HW, int C, void* stream) {
-  hipLaunchKernelGGL(global_avg_fwd_kernel<bf16_t>, dim3((C + 255) / 256, N), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16_t*)x, (bf16_t*)y, HW, C);
+  global_avg_fwd<bf16_t>(x, (bf16_t*)y, N, HW, C, stream);
 }
 DTM_API void dtm_global_avg_bwd_bf16(const void* dy, void* dx, int N, int HW, int C, void* stream) {
-  hipLaunchKernelGGL(global_avg_bwd_kernel<bf16_t>, dim3(pgrid((long)N * HW * C)), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16_t*)dy, (bf16_t*)dx, N, HW, C);
+  global_avg_bwd<bf16_t>((const bf16_t*)dy, dx, N, HW, C, stream);
 }
 
 // y = maxpool(relu(x*scale + shift)) with a uint8 argmax per output element (ss = [scale; shift; ...])

@@ -134,12 +134,9 @@ class TrainStep:
         aux = None
         if isinstance(out, tuple):
             out, aux = out
-        loss = F.softmax_cross_entropy(out, labels, self.smoothing).mean()
-        if aux is not None and self.aux_weight:
-            loss = loss + self.aux_weight * F.softmax_cross_entropy(aux, labels, self.smoothing).mean()
-        if self.batch_weight != 1.0:
-            loss = loss * self.batch_weight
-        return loss
+        bw = self.batch_weight
+        heads = [(out, bw)] + ([(aux, self.aux_weight * bw)] if aux is not None and self.aux_weight else [])
+        return F.mean_xent_loss(heads, labels, self.smoothing)
 
     def current_lr(self):
         if self.lr_schedule is not None:

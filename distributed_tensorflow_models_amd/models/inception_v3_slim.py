@@ -209,7 +209,8 @@ class InceptionV3Slim(Layer):
         return concat_channels(parts)
 
     def run_aux(self, net, training=True):
-        a = F.avg_pool(net, 5, 3, "VALID")
+        # (a tail consumer of the Mixed_6e output: its gradient is added into the one Mixed_7a's backward returns)
+        a = F.avg_pool(net, 5, 3, "VALID", grad_tail=True)
         a = self.aux_conv(self.aux_proj(a, training), training)
         return self.aux_fc(_t(a).reshape(a.shape[0], -1), training)
 

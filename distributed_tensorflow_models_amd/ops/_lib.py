@@ -75,6 +75,7 @@ _SIGS = {
     "dtm_maxpool_bnrelu_bwd": (_I, [_P, _P, _P, _P, _P, _P, ctypes.POINTER(PoolArgs), _I, _P]),
     "dtm_conv_set_tile": (None, [_I]),
     "dtm_conv_set_wgrad_tile": (None, [_I, _I]),
+    "dtm_loss_combine": (_I, [_P, _I, _I, _P, _P, _P]),
     "dtm_scale_rows_pad": (_I, [_P, _I, _P, _I, _P, _I, _I, _I, _P]),
     "dtm_conv_set_wgrad_k64": (None, [_I]),
     "dtm_pool_set_k3s2": (None, [_I]),
@@ -90,6 +91,7 @@ _SIGS = {
     "dtm_maxpool_bwd_ld": (_I, [_P, _I, _P, _P, ctypes.POINTER(PoolArgs), _P]),
     "dtm_avgpool_fwd": (None, [_P, _P, ctypes.POINTER(PoolArgs), _I, _P]),
     "dtm_avgpool_bwd": (None, [_P, _P, ctypes.POINTER(PoolArgs), _I, _P]),
+    "dtm_avgpool_bwd_acc": (_I, [_P, _P, ctypes.POINTER(PoolArgs), _I, _P]),
     "dtm_global_avg_fwd": (None, [_P, _P, _I, _I, _I, _P]),
     "dtm_global_avg_bwd": (None, [_P, _P, _I, _I, _I, _P]),
     "dtm_global_avg_fwd_bf16": (None, [_P, _P, _I, _I, _I, _P]),

@@ -32,6 +32,8 @@ FEATURES = {
                      "profiles/ab/r2_ab_pool_commute_inception.log"),
     "wgrad_stream": ("conv+BN weight gradients on a second HIP stream, concurrent with the dgrad chain "
                      "(TrainStep(wgrad_stream=...) overrides per model)", "profiles/ab/r3_ab_wgrad_side_stream.log"),
+    "pool_tail": ("Inception's aux-head pool gradient added in place into the Mixed_6e-output gradient the main path "
+                  "returned (no separate add over the 17x17x768 map)", "profiles/ab/r5_ab_pool_tail.log"),
     "bsp_compact": ("dead-tap conv weights get a compact all-reduce bucket holding their live window only",
                     "tests/test_distributed.py test_bsp_dead_tap_gradients_left_out_of_the_allreduce"),
 }

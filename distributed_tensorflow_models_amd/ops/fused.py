@@ -69,13 +69,15 @@ class _GradSlot:
     autograd engine never launches a separate add over the whole activation.  A stash may be the
     gradient of a stride-s subsample of the tensor (``stride`` > 1): the dgrad epilogue adds it at
     the subsampled pixels."""
-    __slots__ = ("pending", "buf", "stride", "shape")
+    __slots__ = ("pending", "buf", "stride", "shape", "main", "tail")
 
     def __init__(self, shape):
         self.pending = 0
         self.buf = None
         self.stride = 1
         self.shape = tuple(shape)
+        self.main = None  # the gradient the last consumer returned (a tail consumer may still add into it)
+        self.tail = False  # a tail consumer is registered (only then is main kept)
 
 
 class _BNOutInfo:
@@ -115,6 +117,32 @@ def _slot_register(x):
             return None
     s.pending += 1
     return s
+
+
+def _slot_tail(x):
+    """The slot of x for a tail consumer (Inception's aux-head pool): one whose backward the engine runs after
+    every registered consumer's (it was recorded before them) and that is not counted as pending.  It adds its
+    gradient in place into the one the last consumer returned (``_slot_done``) and returns None; when that is
+    absent (the order differs, or no consumer recorded one) it returns its own gradient as usual.  Only for a
+    tensor whose other consumers all use the slot: an autograd-added gradient would make the recorded one stale."""
+    if not (torch.is_grad_enabled() and x.requires_grad and x.is_cuda):
+        return None
+    s = getattr(x, "_dtm_slot", None)
+    if s is None:
+        s = _GradSlot(x.shape)
+        try:
+            x._dtm_slot = s
+        except Exception:
+            return None
+    s.tail = True
+    return s
+
+
+def _slot_done(slot, dx):
+    """Record the full gradient the last consumer returns (for a tail consumer)."""
+    if slot is not None and slot.tail and dx is not None and slot.pending == 0:
+        slot.main = dx
+    return dx
 
 
 def _unstride(slot, g, stride):
@@ -339,6 +367,8 @@ class _ConvBNFn(torch.autograd.Function):
                 if not last:
                     ctx.slot.buf, ctx.slot.stride = dx, 1
                     dx = None
+                else:
+                    _slot_done(ctx.slot, dx)
             if in_ss is not None and not last:
                 # act hand-off (conv_bn): the cumulative masked gradient waits for the next conv consumer, whose
                 # BN-gradient sums cover every consumer
@@ -406,6 +436,8 @@ class _ConvBNFn(torch.autograd.Function):
             # (the kernel already folded the pending stash in: dx is the cumulative gradient)
             ctx.slot.buf, ctx.slot.stride = dx, 1
             dx = None
+        elif not act:
+            _slot_done(ctx.slot, dx)
         BWD1X1_FUSED[0] += 1
         for p, m in ((gamma, gmg), (beta, bmg), (w, mg)):
             if m is not None:
@@ -906,6 +938,8 @@ class _SiblingGroup:
         if not last:
             grp.slot.buf, grp.slot.stride = dx, 1
             dx = None
+        else:
+            _slot_done(grp.slot, dx)
         grp.buf = None
         SIBLING_MERGED[0] += 1
         # member weights whose gradient has no main_grad: hand the fresh tensors back through this member only

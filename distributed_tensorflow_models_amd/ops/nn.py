@@ -14,7 +14,7 @@ import ctypes
 
 import torch
 
-from . import _lib
+from . import _lib, features
 from . import reference as ref
 from .geometry import conv_geom, cropped_geom, live_taps, pool_geom
 from .lazy import LazyBN, as_tensor
@@ -613,7 +613,7 @@ def _pool_grad_out(slot, dx):
     """Pool backward's input gradient under the hand-off: the pool branch is built last in an
     Inception block, so its backward runs first and stashes; the last conv consumer folds the stash
     into its dgrad epilogue - no separate add over the block input."""
-    from .fused import _slot_stash, _slot_take, _unstride
+    from .fused import _slot_done, _slot_stash, _slot_take, _unstride
     if slot is None:
         return dx
     last, buf, bst = _slot_take(slot)
@@ -622,7 +622,10 @@ def _pool_grad_out(slot, dx):
         return None
     if buf is not None:
         dx = dx + _unstride(slot, buf, bst)
-    return dx
+    return _slot_done(slot, dx)
+
+
+TAIL_FUSED = [0]  # tail avg-pool gradients added in place into the main-path gradient (tests / diagnostics)
 
 
 def _pixel_pitch(t):
@@ -718,34 +721,48 @@ def max_pool(x, kernel, stride, padding="VALID", grad_handoff=False):
 
 class _AvgPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, g, count_pad, slot=None):
+    def forward(ctx, x, g, count_pad, slot=None, tail=None):
         L = _lib.lib()
         y = torch.empty((g.N, g.P, g.Q, g.C), device=x.device, dtype=torch.bfloat16)
         a = g.as_args(_lib.PoolArgs)
         L.dtm_avgpool_fwd(_lib.ptr(x.contiguous()), _lib.ptr(y), ctypes.byref(a), int(count_pad), _lib.stream_ptr())
-        ctx.g, ctx.cp, ctx.slot = g, count_pad, slot
+        ctx.g, ctx.cp, ctx.slot, ctx.tail = g, count_pad, slot, tail
         return y
 
     @staticmethod
     def backward(ctx, dy):
         L = _lib.lib()
         g = ctx.g
-        dx = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
         a = g.as_args(_lib.PoolArgs)
+        main = ctx.tail.main if ctx.tail is not None else None
+        if main is not None and tuple(main.shape) == (g.N, g.H, g.W, g.C) and main.dtype == torch.bfloat16 \
+                and main.is_contiguous() and L.dtm_avgpool_bwd_acc(_lib.ptr(dy.contiguous()), _lib.ptr(main),
+                                                                    ctypes.byref(a), int(ctx.cp),
+                                                                    _lib.stream_ptr()) == 0:
+            # (tail consumer: its gradient added into the main path's, which autograd still holds for x)
+            ctx.tail.main = None
+            TAIL_FUSED[0] += 1
+            return None, None, None, None, None
+        dx = torch.empty((g.N, g.H, g.W, g.C), device=dy.device, dtype=torch.bfloat16)
         L.dtm_avgpool_bwd(_lib.ptr(dy.contiguous()), _lib.ptr(dx), ctypes.byref(a), int(ctx.cp), _lib.stream_ptr())
-        return _pool_grad_out(ctx.slot, dx), None, None, None
+        return _pool_grad_out(ctx.slot, dx), None, None, None, None
 
 
-def avg_pool(x, kernel, stride, padding="VALID", count_pad=False, grad_handoff=False):
+def avg_pool(x, kernel, stride, padding="VALID", count_pad=False, grad_handoff=False, grad_tail=False):
     """TF avg pool (SAME excludes the padding from the divisor unless count_pad); grad_handoff as in
-    max_pool."""
+    max_pool.  ``grad_tail``: x's other consumers are all slot consumers recorded AFTER this pool (Inception's
+    aux head on the Mixed_6e output): the backward adds into their gradient in place (ops.fused._slot_tail)."""
     x = as_tensor(x)
     if not x.is_cuda:
         return ref.avg_pool(x, kernel, stride, padding, count_pad)
     g = pool_geom(tuple(x.shape), kernel, stride, padding)
     xb = x.to(torch.bfloat16)
     share = grad_handoff and xb is x and xb.is_contiguous()
-    return _AvgPoolFn.apply(xb, g, bool(count_pad), _pool_slot(xb) if share else None)
+    tail = None
+    if grad_tail and not share and xb is x and xb.is_contiguous() and features.on("pool_tail"):
+        from .fused import _slot_tail
+        tail = _slot_tail(xb)
+    return _AvgPoolFn.apply(xb, g, bool(count_pad), _pool_slot(xb) if share else None, tail)
 
 
 class _GlobalAvgFn(torch.autograd.Function):
@@ -825,6 +842,68 @@ def softmax_cross_entropy(logits, labels, smoothing=0.0, row_weight=None):
     if logits.dtype not in (torch.float32, torch.bfloat16):
         logits = logits.float()
     return _SoftmaxXentFn.apply(logits, labels, float(smoothing), row_weight)
+
+
+def _scaled_rows_grad(dl, gl):
+    """dl * gl[0] for every row (gl: the 0-dim upstream gradient) in one HIP pass, written into the FC producer's
+    8-aligned padded width as _SoftmaxXentFn.backward does."""
+    B, N = dl.shape
+    Np = _pad8(N) if dl.dtype == torch.bfloat16 else N
+    out = torch.empty((B, Np), device=dl.device, dtype=dl.dtype)
+    _check(_lib.lib().dtm_scale_rows_pad(_lib.ptr(dl), int(dl.dtype == torch.bfloat16), _lib.ptr(gl), 0, _lib.ptr(out),
+                                         B, N, Np, _lib.stream_ptr()), "scale_rows_pad")
+    if Np == N:
+        return out
+    g = out[:, :N]
+    g._dtm_pad_base = out
+    return g
+
+
+class _MeanXentFn(torch.autograd.Function):
+    """sum_h w_h * mean_r xent(logits_h[r], labels[r]) as ONE scalar op: each head's xent kernel writes its gradient
+    pre-scaled by w_h / B, one launch combines the per-row losses (dtm_loss_combine), and the backward is one
+    scale pass per head - in place of the per-head mean, the weight multiply, the add and their backwards
+    (eight small launches at ~4.7 us each in a captured Inception step)."""
+
+    @staticmethod
+    def forward(ctx, labels, smoothing, weights, *logits):
+        L = _lib.lib()
+        B = labels.shape[0]
+        lab = labels.to(torch.int32).contiguous()
+        losses = torch.empty((len(logits), B), device=lab.device, dtype=torch.float32)
+        dls = []
+        for i, (lg, w) in enumerate(zip(logits, weights)):
+            lg = lg.contiguous()
+            dl = torch.empty_like(lg)
+            L.dtm_softmax_xent(_lib.ptr(lg), int(lg.dtype == torch.bfloat16), _lib.ptr(lab), _lib.ptr(losses[i]),
+                               _lib.ptr(dl), B, lg.shape[1], float(smoothing), float(w) / B, None, _lib.stream_ptr())
+            dls.append(dl)
+        out = torch.empty((), device=lab.device, dtype=torch.float32)
+        ws = (ctypes.c_float * len(weights))(*[float(w) / B for w in weights])
+        _check(L.dtm_loss_combine(_lib.ptr(losses), len(logits), B, ctypes.cast(ws, ctypes.c_void_p), _lib.ptr(out),
+                                  _lib.stream_ptr()), "loss_combine")
+        ctx.save_for_backward(*dls)
+        return out
+
+    @staticmethod
+    def backward(ctx, gl):
+        gl = gl.float().reshape(1).contiguous()
+        return (None, None, None) + tuple(_scaled_rows_grad(dl, gl) for dl in ctx.saved_tensors)
+
+
+def mean_xent_loss(heads, labels, smoothing=0.0):
+    """sum over (logits, weight) heads of weight * mean softmax cross-entropy (the training loss with Inception's
+    weighted aux head); one fused op on the GPU, the plain composition elsewhere."""
+    heads = [(lg, float(w)) for lg, w in heads]
+    ok = all(lg.is_cuda and lg.dim() == 2 and lg.dtype in (torch.float32, torch.bfloat16) for lg, _ in heads)
+    if ok and labels.is_cuda and 1 <= len(heads) <= 4 and labels.shape[0] <= 65535:
+        return _MeanXentFn.apply(labels, float(smoothing), [w for _, w in heads], *[lg for lg, _ in heads])
+    loss = None
+    for lg, w in heads:
+        term = softmax_cross_entropy(lg, labels, smoothing).mean()
+        term = term if w == 1.0 else w * term
+        loss = term if loss is None else loss + term
+    return loss
 
 
 # ---------------------------------------------------------------------------------------------

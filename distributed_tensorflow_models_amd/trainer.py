@@ -209,10 +209,10 @@ def make_loss_fn(label_smoothing=0.0, aux_weight=0.4, batch_weight=1.0):
         aux = None
         if isinstance(out, tuple):
             out, aux = out
-        loss = F.softmax_cross_entropy(out, labels, label_smoothing).mean()
+        heads = [(out, batch_weight)]
         if aux is not None and aux_weight:
-            loss = loss + aux_weight * F.softmax_cross_entropy(aux, labels, label_smoothing).mean()
-        return loss * batch_weight if batch_weight != 1.0 else loss
+            heads.append((aux, aux_weight * batch_weight))
+        return F.mean_xent_loss(heads, labels, label_smoothing)
     return loss_fn
 
 

@@ -309,6 +309,50 @@ def test_avgpool_k3s1_matches_generic(case, count_pad):
     assert _rel(out[1][1].float(), xr.grad.permute(0, 2, 3, 1)) < 1e-2
 
 
+@pytest.mark.parametrize("case", [(4, 17, 17, 768, 5, 3, "VALID"), (3, 8, 8, 2048, 8, 1, "VALID"),
+                                  (2, 11, 9, 24, 3, 2, "SAME"), (2, 12, 12, 16, 2, 2, "SAME")])
+@pytest.mark.parametrize("count_pad", [0, 1])
+def test_avgpool_generic8_and_accumulating_backward(case, count_pad):
+    """The generic 8-channel avg pool (32-bit index kernels: Inception's 5x5/3 aux-head pool) against fp32 torch,
+    and its accumulating backward dx += pool_bwd(dy) (the aux head's gradient added into the main path's) against
+    the plain backward plus the prior dx."""
+    import ctypes
+
+    import torch.nn.functional as tF
+
+    from distributed_tensorflow_models_amd.ops import _lib
+    from distributed_tensorflow_models_amd.ops.geometry import pool_geom
+    N, H, W, C, k, st, pad = case
+    torch.manual_seed(4)
+    L = _lib.lib()
+    s = _lib.stream_ptr()
+    x = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16)
+    g = pool_geom(tuple(x.shape), k, st, pad)
+    a = g.as_args(_lib.PoolArgs)
+    dy = torch.randn(N, g.P, g.Q, C, device=DEV).to(torch.bfloat16)
+    y = torch.empty(N, g.P, g.Q, C, device=DEV, dtype=torch.bfloat16)
+    L.dtm_avgpool_fwd(_lib.ptr(x), _lib.ptr(y), ctypes.byref(a), count_pad, s)
+    dx = torch.empty_like(x)
+    L.dtm_avgpool_bwd(_lib.ptr(dy), _lib.ptr(dx), ctypes.byref(a), count_pad, s)
+    prior = torch.randn_like(x, dtype=torch.float32).to(torch.bfloat16)
+    acc = prior.clone()
+    assert L.dtm_avgpool_bwd_acc(_lib.ptr(dy), _lib.ptr(acc), ctypes.byref(a), count_pad, s) == 0
+    torch.cuda.synchronize()
+    xr = x.float().permute(0, 3, 1, 2).contiguous().requires_grad_()
+    yr = tF.avg_pool2d(tF.pad(xr, (g.PW, g.PR, g.PH, g.PB)), k, st)
+    if not count_pad:
+        ones = tF.pad(torch.ones_like(xr[:, :1]), (g.PW, g.PR, g.PH, g.PB))
+        yr = yr / tF.avg_pool2d(ones, k, st)
+    assert _rel(y.float().permute(0, 3, 1, 2), yr) < 1e-2
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    gx = xr.grad.permute(0, 2, 3, 1)
+    assert _rel(dx.float(), gx) < 1e-2
+    assert _rel(acc.float(), prior.float() + gx) < 1e-2
+    # one rounding of (prior + exact fp32 pool gradient): within half a bf16 ulp of it
+    ref = prior.float() + dx.float()
+    assert float((acc.float() - ref).abs().max()) <= float(ref.abs().max()) * 2 ** -7
+
+
 @pytest.mark.parametrize("case", [(4, 35, 35, 288, "VALID"), (4, 17, 17, 768, "VALID"), (2, 15, 14, 16, "SAME"),
                                   (3, 9, 10, 8, "VALID"), (2, 13, 13, 2048, "SAME")])
 def test_maxpool_k3s2_matches_generic(case):
@@ -577,6 +621,26 @@ def test_bias_column_sums_match_torch(shape):
     assert _rel(got, want) < 1e-5
 
 
+@pytest.mark.parametrize("shape", [(64, 8, 8, 2048), (16, 7, 7, 2048), (3, 5, 3, 24), (2, 3, 3, 12)])
+@pytest.mark.parametrize("out_bf16", [False, True])
+def test_global_avg_pool_shapes_match_torch(shape, out_bf16):
+    """Global mean pool (8-channel split-row kernel when C % 8 == 0, the per-channel one otherwise) forward and
+    backward against fp32 torch, for fp32 and bf16 outputs."""
+    from distributed_tensorflow_models_amd.ops import nn as F
+    torch.manual_seed(15)
+    x = torch.randn(*shape, device=DEV).to(torch.bfloat16)
+    xk = x.clone().requires_grad_()
+    y = F.global_avg_pool(xk, out_bf16=out_bf16)
+    xr = x.float().requires_grad_()
+    yr = xr.mean(dim=(1, 2))
+    assert y.shape == yr.shape
+    assert _rel(y.float(), yr) < (4e-3 if out_bf16 else 1e-5)
+    dy = torch.randn_like(yr)
+    y.backward(dy.to(y.dtype))
+    yr.backward(dy.to(y.dtype).float())
+    assert _rel(xk.grad.float(), xr.grad) < 4e-3
+
+
 @pytest.mark.parametrize("C", [2048, 64])
 def test_global_avg_pool_bf16_output_matches_cast(C):
     """The bf16-output global average pool (the ResNet logits input) == the fp32 pool cast to bf16, forward and
@@ -631,6 +695,40 @@ def test_fc_softmax_xent_padded_head_matches_torch(N):
         assert _rel(w.grad, wr.grad) < 3e-2 and _rel(b.grad, br.grad) < 3e-2
     if N % 8:
         assert F.PAD_BASE_USED[0] >= used0 + 2
+
+
+@pytest.mark.parametrize("bw", [1.0, 0.5])
+def test_mean_xent_loss_fused_matches_composition(bw):
+    """The fused training loss (main head + 0.4-weighted aux head, batch weight bw) against the composition of
+    per-row xent, means and weights: the loss to fp32 rounding, and both heads' logits gradients and the FCs' padded
+    backward hand-off (PAD_BASE_USED) through a real FC pair."""
+    from distributed_tensorflow_models_amd.ops import nn as F
+    torch.manual_seed(13)
+    B, Kin, N = 64, 128, 1001
+    x = torch.randn(B, Kin, device=DEV).to(torch.bfloat16)
+    labels = torch.randint(0, N, (B,), device=DEV)
+    ws = [torch.nn.Parameter(torch.randn(Kin, N, device=DEV) / Kin ** 0.5) for _ in range(2)]
+    out = []
+    for fused in (True, False):
+        for w in ws:
+            w.grad = None
+        xi = x.clone().requires_grad_()
+        used0 = F.PAD_BASE_USED[0]
+        la, lb = F.linear(xi, ws[0], None), F.linear(xi * 2, ws[1], None)
+        if fused:
+            loss = F.mean_xent_loss([(la, bw), (lb, 0.4 * bw)], labels, 0.1)
+        else:
+            loss = (F.softmax_cross_entropy(la, labels, 0.1).mean()
+                    + 0.4 * F.softmax_cross_entropy(lb, labels, 0.1).mean()) * bw
+        loss.backward()
+        torch.cuda.synchronize()
+        out.append((float(loss.detach()), xi.grad.float(), [w.grad.clone() for w in ws], F.PAD_BASE_USED[0] - used0))
+    (l1, gx1, gw1, u1), (l2, gx2, gw2, u2) = out
+    assert abs(l1 - l2) <= 1e-5 * abs(l2), (l1, l2)
+    assert _rel(gx1, gx2) < 1e-2
+    for a, b in zip(gw1, gw2):
+        assert _rel(a, b) < 1e-2
+    assert u1 == 2 and u2 == 2
 
 
 @pytest.mark.parametrize("tile", [10, 11, 12, 13, 14, 15])

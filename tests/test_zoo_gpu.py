@@ -281,6 +281,42 @@ def test_pool_joins_shared_input_grad_handoff(pool):
     assert _rel(grads[0], grads[1]) < 1e-2
 
 
+@pytest.mark.parametrize("aux_in_loss", [True, False])
+def test_aux_pool_tail_adds_into_main_gradient(aux_in_loss):
+    """Inception's aux-head pool as a tail consumer (avg_pool grad_tail=True, recorded before the block's slot
+    consumers): its gradient is added in place into the one the last consumer returns - same x.grad as autograd's
+    add; and with the aux output left out of the loss (its backward never runs) x.grad is exactly the no-tail one."""
+    from distributed_tensorflow_models_amd.models.layers import Conv2d
+    from distributed_tensorflow_models_amd.ops import features
+    from distributed_tensorflow_models_amd.ops import nn as F
+    from distributed_tensorflow_models_amd.ops.lazy import as_tensor
+    torch.manual_seed(0)
+    bn = dict(decay=0.9997, epsilon=1e-3, scale=False, bessel=False)
+    convs = [Conv2d("c%d" % i, 64, 32, k, 1, "SAME", "relu", dict(bn), False, 0.0, ("truncated_normal", 0.1)).to(DEV)
+             for i, k in enumerate((1, 3))]
+    x0 = torch.randn(4, 17, 17, 64, device=DEV).to(torch.bfloat16)
+    grads, fused = [], []
+    for tail in (True, False):
+        with features.override(pool_tail=tail):
+            x = x0.clone().requires_grad_()
+            before = F.TAIL_FUSED[0]
+            aux = F.avg_pool(x, 5, 3, "VALID", grad_tail=True)
+            outs = [as_tensor(c(x, True)) for c in convs]
+            p = F.max_pool(x, 3, 2, "VALID", grad_handoff=True)
+            loss = sum(o.float().square().mean() for o in outs) + p.float().square().mean() * 3
+            if aux_in_loss:
+                loss = loss + aux.float().square().mean() * 5
+            loss.backward()
+            torch.cuda.synchronize()
+            grads.append(x.grad.float())
+            fused.append(F.TAIL_FUSED[0] - before)
+    assert fused == [1 if aux_in_loss else 0, 0], fused
+    if aux_in_loss:
+        assert _rel(grads[0], grads[1]) < 1e-2
+    else:
+        assert torch.equal(grads[0], grads[1])
+
+
 @pytest.mark.parametrize("C,K,H", [(288, 64, 35), (768, 192, 17), (2048, 192, 8)])
 def test_pool_branch_commuted(C, K, H):
     """Inception pool branch avg_pool(3x3/1 SAME) -> 1x1 conv -> BN+ReLU computed as 1x1 conv -> avg_pool ->
