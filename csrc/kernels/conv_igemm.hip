@@ -2723,7 +2723,9 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   const int MT = wt == 6 ? 32 : ((wt == 1 || wt == 11) ? 64 : (big ? 256 : 128)), NT = (big || wt == 11) ? 256 : 128;
   if (big) occ = (wenv == 12 && g_wgrad_occ != 4) ? g_wgrad_occ : 1;  // (sweeps: WTILES=12:<occ>)
   long tiles = (long)((a.Kg + NT - 1) / NT) * ((a.K + MT - 1) / MT);
-  long target = (long)num_cus * (wt >= 10 ? occ : 3);
+  // register-staged tiles: 3 blocks' worth of splits per CU (sweeps: WTILES=<1|6|0>:<occ>, occ != 4)
+  const int rs_occ = (wenv >= 0 && g_wgrad_occ != 4) ? g_wgrad_occ : 3;
+  long target = (long)num_cus * (wt >= 10 ? occ : rs_occ);
   long ksteps = (a.Mpix + 63) / 64;
   // the pipelined kernels run 2 blocks/CU: fill whole rounds of resident blocks (floor), a last
   // round with a few blocks doubles a layer's time
