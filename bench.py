@@ -51,6 +51,8 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--grad-comm", default="fp32", choices=("fp32", "bf16"),
                     help="dtype of the gradient all-reduce on the wire (bf16 halves the xGMI bytes)")
+    ap.add_argument("--wgrad-stream", type=int, default=-1,
+                    help="weight gradients on the side stream: 1 / 0, -1 = the preset's choice")
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the step in a hipGraph (1/0); -1 = auto: on for launch-bound models on 1 GPU")
     ap.add_argument("--profile-steps", type=int, default=0)
@@ -112,6 +114,8 @@ def main():
         sys.exit(2)
     torch.manual_seed(1234)  # identical replicas: every rank builds the same initial weights
     S0, ncls, B0, opt, extra = PRESETS[args.model]
+    if args.wgrad_stream >= 0:
+        extra = dict(extra, wgrad_stream=bool(args.wgrad_stream))
     S = args.image_size or S0
     B = args.batch or B0
     kw = {"fc_conv_padding": "SAME"} if args.model == "vgg_16" else {}
