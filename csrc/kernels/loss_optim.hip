@@ -27,10 +27,11 @@ __device__ __forceinline__ float ldf<bf16_t>(const bf16_t* p, long i) { return b
 template <typename T>
 __global__ __launch_bounds__(256) void softmax_xent_kernel(const T* __restrict__ logits, const int* __restrict__ labels,
                                                            float* __restrict__ loss, T* __restrict__ dlogits, int K,
-                                                           float smoothing, float gscale, const float* row_weight) {
+                                                           float smoothing, float gscale, const float* row_weight,
+                                                           int ldx) {
   __shared__ float red[8];
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const T* x = logits + (long)row * K;
+  const T* x = logits + (long)row * ldx;  // (ldx: row pitch - an FC's padded output read in place)
   float m = -INFINITY;
   for (int k = tid; k < K; k += 256) m = fmaxf(m, ldf(x, k));
 #pragma unroll
@@ -203,13 +204,15 @@ DTM_API int dtm_scale_rows_pad(const void* dl, int bf16, const float* gl, int gs
 }
 
 DTM_API void dtm_softmax_xent(const void* logits, int logits_bf16, const int* labels, float* loss, void* dlogits,
-                              int B, int K, float smoothing, float gscale, const float* row_weight, void* stream) {
+                              int B, int K, float smoothing, float gscale, const float* row_weight, int ldx,
+                              void* stream) {
+  if (ldx < K) ldx = K;
   if (logits_bf16)
     hipLaunchKernelGGL(softmax_xent_kernel<bf16_t>, dim3(B), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)logits,
-                       labels, loss, (bf16_t*)dlogits, K, smoothing, gscale, row_weight);
+                       labels, loss, (bf16_t*)dlogits, K, smoothing, gscale, row_weight, ldx);
   else
     hipLaunchKernelGGL(softmax_xent_kernel<float>, dim3(B), dim3(256), 0, (hipStream_t)stream, (const float*)logits,
-                       labels, loss, (float*)dlogits, K, smoothing, gscale, row_weight);
+                       labels, loss, (float*)dlogits, K, smoothing, gscale, row_weight, ldx);
 }
 
 DTM_API int dtm_loss_combine(const float* loss, int heads, int B, const float* w, float* out, void* stream) {

@@ -96,7 +96,7 @@ _SIGS = {
     "dtm_global_avg_bwd": (None, [_P, _P, _I, _I, _I, _P]),
     "dtm_global_avg_fwd_bf16": (None, [_P, _P, _I, _I, _I, _P]),
     "dtm_global_avg_bwd_bf16": (None, [_P, _P, _I, _I, _I, _P]),
-    "dtm_softmax_xent": (None, [_P, _I, _P, _P, _P, _I, _I, _F, _F, _P, _P]),
+    "dtm_softmax_xent": (None, [_P, _I, _P, _P, _P, _I, _I, _F, _F, _P, _I, _P]),
     "dtm_opt_chunk_size": (_I, []),
     "dtm_opt_tensor_bytes": (_I, []),
     "dtm_opt_chunk_bytes": (_I, []),

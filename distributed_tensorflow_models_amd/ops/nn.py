@@ -799,18 +799,27 @@ def global_avg_pool(x, out_bf16=False):
 
 # ---------------------------------------------------------------------------------------------
 # loss
+def _rows(t):
+    """(t, row pitch): a [B][K] tensor with unit column stride is read in place (an FC's padded output viewed as its
+    first K columns), anything else made contiguous."""
+    if t.dim() == 2 and t.stride(1) == 1 and t.stride(0) >= t.shape[1]:
+        return t, t.stride(0)
+    t = t.contiguous()
+    return t, t.shape[1]
+
+
 class _SoftmaxXentFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, labels, smoothing, row_weight):
         L = _lib.lib()
-        logits = logits.contiguous()
+        logits, ld = _rows(logits)
         B, K = logits.shape
         loss = torch.empty((B,), device=logits.device, dtype=torch.float32)
-        dl = torch.empty_like(logits)
+        dl = torch.empty((B, K), device=logits.device, dtype=logits.dtype)
         lab = labels.to(torch.int32).contiguous()
         L.dtm_softmax_xent(_lib.ptr(logits), int(logits.dtype == torch.bfloat16), _lib.ptr(lab), _lib.ptr(loss),
                            _lib.ptr(dl), B, K, float(smoothing), 1.0,
-                           _lib.ptr(row_weight.float().contiguous()) if row_weight is not None else None,
+                           _lib.ptr(row_weight.float().contiguous()) if row_weight is not None else None, ld,
                            _lib.stream_ptr())
         ctx.save_for_backward(dl)
         return loss
@@ -873,10 +882,11 @@ class _MeanXentFn(torch.autograd.Function):
         losses = torch.empty((len(logits), B), device=lab.device, dtype=torch.float32)
         dls = []
         for i, (lg, w) in enumerate(zip(logits, weights)):
-            lg = lg.contiguous()
-            dl = torch.empty_like(lg)
+            lg, ld = _rows(lg)
+            dl = torch.empty(lg.shape, device=lg.device, dtype=lg.dtype)
             L.dtm_softmax_xent(_lib.ptr(lg), int(lg.dtype == torch.bfloat16), _lib.ptr(lab), _lib.ptr(losses[i]),
-                               _lib.ptr(dl), B, lg.shape[1], float(smoothing), float(w) / B, None, _lib.stream_ptr())
+                               _lib.ptr(dl), B, lg.shape[1], float(smoothing), float(w) / B, None, ld,
+                               _lib.stream_ptr())
             dls.append(dl)
         out = torch.empty((), device=lab.device, dtype=torch.float32)
         ws = (ctypes.c_float * len(weights))(*[float(w) / B for w in weights])
@@ -946,7 +956,8 @@ class _LinearHipFn(torch.autograd.Function):
         _check(L.dtm_conv_fwd(_lib.ptr(x16), _lib.ptr(wt), _lib.ptr(y), None, _lib.ptr(bias), None, None, int(relu),
                               ctypes.byref(d), s), "fc_fwd")
         if Np != N:
-            y = y[:, :N].contiguous()
+            # the first N columns, read in place by the loss (ops.nn._rows); a consumer needing a dense tensor copies
+            y = y[:, :N] if not relu else y[:, :N].contiguous()
         ctx.save_for_backward(x16, w, y if relu else None)
         ctx.b, ctx.relu = b, relu
         return y

@@ -682,6 +682,7 @@ def test_fc_softmax_xent_padded_head_matches_torch(N):
         w.grad = b.grad = None
         xi = x.clone().requires_grad_()
         logits = F.linear(xi.to(torch.bfloat16), w, b)
+        assert logits.is_contiguous() == (N % 8 == 0)  # (a padded head's output is read in place by the loss)
         loss = 0.4 * F.softmax_cross_entropy(logits, labels, 0.1).mean()
         loss.backward()
         torch.cuda.synchronize()
