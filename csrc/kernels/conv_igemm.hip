@@ -990,6 +990,273 @@ __global__ __launch_bounds__(512) void conv_nt_w8_kernel(ConvNTArgs a) {
   else conv_nt_epilogue<PT, CT, WP, WC, 2, false, false, false, false, NT>(a, acc, smem, p0, c0, by);
 }
 
+// 8-wave ping-pong ("8-phase") main loop of the 256 x 256 tiles (conv_nt_pp_kernel, conv_wgrad_pp_kernel): BK = 64,
+// LDS-DMA operand staging, the k-loop split into 4 phases per k-tile, and the two wave groups (waves 0-3, 4-7: one
+// wave of each on every SIMD) running one barrier apart, so on each SIMD one wave's 16 MFMAs overlap the other
+// wave's LDS fragment reads and DMA issue (the w8 kernels: all 8 waves read, then all 8 multiply - the MFMA pipe
+// idles during the read burst and the per-k-tile vmcnt(0) drain).
+//   * k-tile slot = 4 half-tiles of 16 KiB: P0 / P1 (rows 0-127 / 128-255 of the operand whose rows are split over
+//     the wave groups) and W0 / W1 (rows 0-127 / 128-255 of the other); 2 slots (128 KiB).  Wave (g = wave >> 2,
+//     q = wave & 3) owns P rows {mi*128 + g*64 + 0..63} and W rows {ni*128 + q*32 + 0..31}, mi, ni in {0, 1}, so
+//     the quadrant (ni, mi) of a phase reads ONE P half and ONE W half, and each half is consumed early in its
+//     k-tile and restaged with k-tile t+2:
+//       phase 0: read P(mi=0) + W(ni=0)      MFMA (0,0)   issue W1(t+1)
+//       phase 1: read W(ni=1)                MFMA (1,0)   issue P1(t+1)
+//       phase 2: read P(mi=1)                MFMA (1,1)   issue P0(t+2)
+//       phase 3: (registers)                 MFMA (0,1)   issue W0(t+2)
+//     (16 MFMAs of 16x16x32 per wave per phase.)
+//   * every half is restaged >= 2 phases after its last read (the WAR distance two staggered groups need) and read
+//     >= 1 phase after the vmcnt that retires it (RAW across the stagger); each phase waits with a counted vmcnt for
+//     everything but the last 4 phases' DMAs (8 instructions in steady state, fewer in the tail, where the
+//     past-the-end issues are skipped), so a half has ~8 barrier intervals to land.
+//   * all LDS in ONE __shared__ array (the caller's), raw s_barrier, sched_barrier fences so the compiler keeps each
+//     phase's reads / DMA / MFMAs on their side of the barriers.
+// issue(kt, h): DMA of half h (0 W1, 1 P1, 2 P0, 3 W0) of k-tile kt into slot kt & 1 (2 LDS-DMA instructions per wave);
+// rd_p(slot, mi) / rd_w(slot, ni): fragment reads; mma(ni, mi): the quadrant's 16 MFMAs.
+template <class IssueF, class RdPF, class RdWF, class MmaF>
+__device__ __forceinline__ void pp_mainloop(const char* smem, int slot_bytes, int nk, int grp, IssueF issue, RdPF rd_p,
+                                            RdWF rd_w, MmaF mma) {
+  // the DMA of global phase p (p = 4 t + q; the prologue is p = -6 .. -1): q 0 W1(t+1), 1 P1(t+1), 2 P0(t+2),
+  // 3 W0(t+2); issued only for k-tiles < nk
+  auto phase_kt = [&](int p) { return ((p + 8) >> 2) - 2 + ((p & 3) >= 2 ? 2 : 1); };
+  auto issue_phase = [&](int p) {
+    const int kt = phase_kt(p);
+    if (kt < nk) issue(kt, p & 3);
+  };
+  // counted wait after phase p's issue: everything but the DMAs of phases p-3 .. p (2 per issuing phase)
+  auto wait_phase = [&](int p) {
+    int n = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) n += (p - d >= -6 && phase_kt(p - d) < nk) ? 2 : 0;
+    if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (n == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (n == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  auto bar = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // prologue: phases -6 .. -1 (k-tile 0 whole, P0 / W0 of k-tile 1), then wait for k-tile 0's P0 / W0
+#pragma unroll
+  for (int p = -6; p < 0; ++p) issue_phase(p);
+  wait_phase(-1);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  bar();
+  if (grp == 1) bar();  // the stagger: group 1 runs one barrier behind group 0
+  for (int t = 0; t < nk; ++t) {
+    const char* s = smem + (t & 1) * slot_bytes;
+    const int pb = 4 * t;
+    rd_w(s, 0);  // phase 0
+    rd_p(s, 0);
+    issue_phase(pb);
+    wait_phase(pb);
+    bar();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+    mma(0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    rd_w(s, 1);  // phase 1
+    issue_phase(pb + 1);
+    wait_phase(pb + 1);
+    bar();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+    mma(1, 0);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    rd_p(s, 1);  // phase 2
+    issue_phase(pb + 2);
+    wait_phase(pb + 2);
+    bar();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+    mma(1, 1);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    issue_phase(pb + 3);  // phase 3
+    wait_phase(pb + 3);
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+    mma(0, 1);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+  }
+  if (grp == 0) bar();  // match group 1's extra barrier
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Ping-pong form of conv_nt_w8_kernel<256, 256>: the same GEMM (256 pixels x 256 channels per 512-thread block, the
+// source-swizzled [row][128 B] LDS image), pixels as the P operand (A0 / A1), weight rows as W.  Epilogue: the shared
+// staged-store tail (statistics, dgrad post-ops, split store) after a register -> LDS pass for this wave layout.
+// No input prologue (like w8).
+template <int UD, bool SPL = false>
+__global__ __launch_bounds__(512) void conv_nt_pp_kernel(ConvNTArgs a) {
+  constexpr int PT = 256, CT = 256, NW = 8, BK = 64;
+  constexpr int HALF = 128 * 128;  // one half-tile: 128 rows x 64 k bf16
+  constexpr int BUF = 4 * HALF;    // one k-tile slot [P0 | P1 | W0 | W1]
+  constexpr int OROW = CT * 2 + 16;
+  constexpr int RING = 2 * BUF > PT * OROW ? 2 * BUF : PT * OROW;
+  static_assert(RING <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char smem[RING];
+  typedef __attribute__((address_space(1))) const void gvoid;
+  typedef __attribute__((address_space(3))) void lvoid;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = wave >> 2, wq = wave & 3;
+  const int tile = grp_tile(a);
+  const int bx = tile % gridDim.x, by = tile / gridDim.x;
+  const int p0 = by * PT, c0 = bx * CT;
+  const int lr = lane >> 3;
+  const int ch = (lane & 7) ^ lr;  // logical 16-B chunk this lane moves (source-side swizzle)
+
+  // pixel decode of this lane's 4 DMA rows 8 * (wave + 8 j) + lr (j = 0, 1: half P0; j = 2, 3: half P1)
+  int ih0[4], iw0[4], pixbase[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = p0 + 8 * (wave + NW * j) + lr;
+    if (m < a.M) {
+      uint32_t n = fdiv((uint32_t)m, a.fd_PQ);
+      uint32_t rem = m - n * (a.P * a.Q);
+      uint32_t p = fdiv(rem, a.fd_Q);
+      uint32_t q = rem - p * a.Q;
+      ih0[j] = (int)p * a.stride - a.pad_h;
+      iw0[j] = (int)q * a.stride - a.pad_w;
+      pixbase[j] = (int)n * a.Hin * a.Win;
+    } else {
+      ih0[j] = -(1 << 28);
+      iw0[j] = -(1 << 28);
+      pixbase[j] = 0;
+    }
+  }
+  // (r, s, c) iterators of this lane's chunk for the next P0 / P1 issue (the halves run a k-tile apart)
+  int cc0 = (ch * 8) % a.C, rr0, ss0;
+  {
+    const int tap = (ch * 8) / a.C;
+    rr0 = tap / a.S;
+    ss0 = tap - rr0 * a.S;
+  }
+  int cc1 = cc0, rr1 = rr0, ss1 = ss0;
+  const char* xg = (const char*)a.x;
+  const char* wg = (const char*)a.w;
+  const char* zg = (const char*)a.zero;
+  const int nk = (a.Kg + BK - 1) / BK;
+
+  auto issue_p = [&](int kt, int h, int& cc, int& rr, int& ss) {
+    char* base = smem + (kt & 1) * BUF + h * HALF;
+    const bool kin = kt * BK + ch * 8 < a.Kg;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = 2 * h + jj;
+      const int ihv = ih0[j] + rr, iwv = iw0[j] + ss;
+      bool v = kin & ((unsigned)ihv < (unsigned)a.Hv) & ((unsigned)iwv < (unsigned)a.Wv);
+      if (UD > 1) v = v & (((ihv | iwv) & (UD - 1)) == 0);
+      const int ih = UD > 1 ? ihv / UD : ihv, iw = UD > 1 ? iwv / UD : iwv;
+      const char* src = xg + (size_t)(uint32_t)((pixbase[j] + ih * a.Win + iw) * a.pix_bytes + cc * 2);
+      __builtin_amdgcn_global_load_lds((gvoid*)(v ? src : zg), (lvoid*)(base + (wave + NW * jj) * 1024), 16, 0, 0);
+    }
+    cc += BK;
+    while (cc >= a.C) {
+      cc -= a.C;
+      if (++ss == a.S) { ss = 0; ++rr; }
+    }
+  };
+  auto issue_w = [&](int kt, int h) {
+    char* base = smem + (kt & 1) * BUF + (2 + h) * HALF;
+    const int k = kt * BK + ch * 8;
+    const bool kin = k < a.Kg;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int row = c0 + h * 128 + 8 * (wave + NW * jj) + lr;
+      const bool v = kin & (row < a.K);
+      const char* src = wg + (size_t)(uint32_t)((row * a.Kg + k) * 2);
+      __builtin_amdgcn_global_load_lds((gvoid*)(v ? src : zg), (lvoid*)(base + (wave + NW * jj) * 1024), 16, 0, 0);
+    }
+  };
+  auto issue = [&](int kt, int h) {
+    if (h == 0) issue_w(kt, 1);
+    else if (h == 1) issue_p(kt, 1, cc1, rr1, ss1);
+    else if (h == 2) issue_p(kt, 0, cc0, rr0, ss0);
+    else issue_w(kt, 0);
+  };
+
+  f32x4 acc[2][2][2][4];  // [ni][ii][mi][jj]
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) acc[ni][ii][mi][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fk = lane >> 4;
+  short8 P[2][4], Wa[2][2], Wb[2][2];  // [ks][frag]
+  auto rd_p = [&](const char* s, int mi) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int row = mi * 128 + grp * 64 + jj * 16 + fr;
+        P[ks][jj] = *(const short8*)(s + row * 128 + (((ks * 4 + fk) ^ (row & 7)) << 4));
+      }
+  };
+  auto rd_w = [&](const char* s, int ni) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        const int row = ni * 128 + wq * 32 + ii * 16 + fr;
+        const short8 v = *(const short8*)(s + 2 * HALF + row * 128 + (((ks * 4 + fk) ^ (row & 7)) << 4));
+        if (ni == 0) Wa[ks][ii] = v;
+        else Wb[ks][ii] = v;
+      }
+  };
+  auto mma = [&](int ni, int mi) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          acc[ni][ii][mi][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ni == 0 ? Wa[ks][ii] : Wb[ks][ii], P[ks][jj],
+                                                                        acc[ni][ii][mi][jj], 0, 0, 0);
+  };
+  pp_mainloop(smem, BUF, nk, grp, issue, rd_p, rd_w, mma);
+  __syncthreads();  // the epilogue reuses the ring
+
+  // register -> LDS staging of the bf16 tile (lane: channels fk*4 .. +3 of pixel fr per 16x16 subtile), then the
+  // shared staged-store tail; bias / ReLU applied here like conv_nt_epilogue
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) {
+      const int kloc = ni * 128 + wq * 32 + ii * 16 + fk * 4;
+      float bia[4] = {0.f, 0.f, 0.f, 0.f};
+      if (a.bias && c0 + kloc < a.K) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bia[r] = a.bias[c0 + kloc + r];
+      }
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int mloc = mi * 128 + grp * 64 + jj * 16 + fr;
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = acc[ni][ii][mi][jj][r] + bia[r];
+            if (a.relu) v[r] = fmaxf(v[r], 0.f);
+          }
+          *(uint2*)(smem + mloc * OROW + kloc * 2) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+        }
+    }
+  conv_nt_epi_tail<PT, CT, false, false, false, 512, true, false, SPL>(a, smem, p0, c0, by, nullptr, nullptr);
+}
+
 // Persistent streaming kernel for the short-reduction 1x1 stride-1 convs (K*R*S*C = 64 * NKT <= 256:
 // the 56x56 / 28x28 expand and reduce layers and their dgrads).  They are pure HBM streams (read
 // M x Kg, write M x K), so each block keeps its channel tile of the weights resident in LDS and walks
@@ -1849,6 +2116,160 @@ __global__ __launch_bounds__(NTH) void conv_wgrad_pipe_kernel(ConvWgradArgs a) {
   }
 }
 
+// Ping-pong form of conv_wgrad_pipe_kernel<256, 256> (pp_mainloop): dW rows ko as the P operand (dy), columns
+// (r, s, c) as W (the gathered input), 64 pixels per k-tile.  Each half-tile is its own [k/4][m/16][4][16]
+// transposed-read image of 128 rows (tr_off<128>), filled by LDS-DMA at the lane's inverse-image position (tr_inv<128>)
+// and read with ds_read_b64_tr_b16.  Split-K slab epilogue as conv_wgrad_pipe_kernel.
+__global__ __launch_bounds__(512) void conv_wgrad_pp_kernel(ConvWgradArgs a) {
+  constexpr int NW = 8, BK = 64;
+  constexpr int HALF = BK * 128 * 2;
+  constexpr int BUF = 4 * HALF;  // [P0 | P1 | W0 | W1]
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  typedef __attribute__((address_space(1))) const void gvoid;
+  typedef __attribute__((address_space(3))) void lvoid;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = wave >> 2, wq = wave & 3;
+  const int gxy = gridDim.x * gridDim.y;
+  const int tile = xcd_remap((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x, gxy * gridDim.z);
+  const int bz = tile / gxy, by = (tile % gxy) / gridDim.x, bx = tile % gridDim.x;
+  const int n0 = bx * 256, m0 = by * 256;
+  const int pix_lo = bz * a.pix_per_split;
+  const int pix_hi = min(a.Mpix, pix_lo + a.pix_per_split);
+
+  // per-lane chunk coordinates of its DMA slots: piece (wave + 8 jj) of a half, j = 2 h + jj for half h
+  int a_k[4], a_off[4];
+  bool a_colv[4];
+  int b_k[4], b_r[4], b_s[4], b_c[4];
+  bool b_colv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    int k, m;
+    tr_inv<128>((wave + NW * (j & 1)) * 64 + lane, k, m);
+    const int h = j >> 1;
+    a_k[j] = k;
+    a_off[j] = m0 + h * 128 + m;
+    a_colv[j] = a_off[j] < a.K;
+    b_k[j] = k;
+    const int col = n0 + h * 128 + m;
+    b_colv[j] = col < a.Kg;
+    const int tap = col / a.C;
+    b_c[j] = col - tap * a.C;
+    b_r[j] = tap / a.S;
+    b_s[j] = tap - b_r[j] * a.S;
+  }
+  const char* xg = (const char*)a.x;
+  const char* dg = (const char*)a.dy;
+  const char* zg = (const char*)a.in_shift;  // the host passes a zero chunk here (no prologue in this kernel)
+  const int nk = (pix_hi - pix_lo + BK - 1) / BK;
+
+  auto issue_p = [&](int kt, int h) {
+    char* base = smem + (kt & 1) * BUF + h * HALF;
+    const int pbase = pix_lo + kt * BK;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = 2 * h + jj;
+      const int pix = pbase + a_k[j];
+      const bool v = (pix < pix_hi) & a_colv[j];
+      const char* src = dg + (size_t)(uint32_t)((pix * a.K + a_off[j]) * 2);
+      __builtin_amdgcn_global_load_lds((gvoid*)(v ? src : zg), (lvoid*)(base + (wave + NW * jj) * 1024), 16, 0, 0);
+    }
+  };
+  auto issue_w = [&](int kt, int h) {
+    char* base = smem + (kt & 1) * BUF + (2 + h) * HALF;
+    const int pbase = pix_lo + kt * BK;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = 2 * h + jj;
+      const int pix = pbase + b_k[j];
+      const uint32_t n = fdiv((uint32_t)pix, a.fd_PQ);
+      const uint32_t rem = pix - n * (a.P * a.Q);
+      const uint32_t p = fdiv(rem, a.fd_Q);
+      const uint32_t q = rem - p * a.Q;
+      const int ih = (int)p * a.stride - a.pad_h + b_r[j];
+      const int iw = (int)q * a.stride - a.pad_w + b_s[j];
+      const bool v = (pix < pix_hi) & b_colv[j] & ((unsigned)ih < (unsigned)a.H) & ((unsigned)iw < (unsigned)a.W);
+      const char* src = xg + (size_t)(uint32_t)((((int)n * a.H + ih) * a.W + iw) * a.pix_bytes + b_c[j] * 2);
+      __builtin_amdgcn_global_load_lds((gvoid*)(v ? src : zg), (lvoid*)(base + (wave + NW * jj) * 1024), 16, 0, 0);
+    }
+  };
+  auto issue = [&](int kt, int h) {
+    if (h == 0) issue_w(kt, 1);
+    else if (h == 1) issue_p(kt, 1);
+    else if (h == 2) issue_p(kt, 0);
+    else issue_w(kt, 0);
+  };
+
+  f32x4 acc[2][2][2][4];  // [ni][ii][mi][jj]
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) acc[ni][ii][mi][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int lg = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
+  typedef __attribute__((address_space(3))) short4v lds_s4;
+  typedef __attribute__((address_space(3))) char lds_c;
+  short8 P[2][4], Wa[2][2], Wb[2][2];  // [ks][frag]
+  auto frag = [&](const char* half, int ks, int m) -> short8 {
+    lds_c* lb = (lds_c*)half;
+    const int kb = ks * 32 + 8 * lg;
+    const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lb + tr_off<128>(kb + tq, m)));
+    const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lb + tr_off<128>(kb + 4 + tq, m)));
+    return (short8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  auto rd_p = [&](const char* s, int mi) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) P[ks][jj] = frag(s + mi * HALF, ks, grp * 64 + jj * 16 + 4 * tp);
+  };
+  auto rd_w = [&](const char* s, int ni) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        const short8 v = frag(s + (2 + ni) * HALF, ks, wq * 32 + ii * 16 + 4 * tp);
+        if (ni == 0) Wa[ks][ii] = v;
+        else Wb[ks][ii] = v;
+      }
+  };
+  auto mma = [&](int ni, int mi) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          acc[ni][ii][mi][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(P[ks][jj], ni == 0 ? Wa[ks][ii] : Wb[ks][ii],
+                                                                        acc[ni][ii][mi][jj], 0, 0, 0);
+  };
+  pp_mainloop(smem, BUF, nk, grp, issue, rd_p, rd_w, mma);
+
+  // lane: rows ko .. +3 (lg * 4 + r) of column li per 16x16 subtile -> this split's slab
+  float* slab = a.dw + (size_t)bz * a.K * a.Kg;
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) {
+      const int col = n0 + ni * 128 + wq * 32 + ii * 16 + li;
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int ko = m0 + mi * 128 + grp * 64 + jj * 16 + lg * 4;
+          if (col < a.Kg) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (ko + r < a.K) slab[(size_t)(ko + r) * a.Kg + col] = acc[ni][ii][mi][jj][r];
+          }
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // weight re-layouts
 // dgrad weight: Wt[c][R-1-r][S-1-s][k] = W[k][r][s][c]   (bf16 -> bf16)
@@ -1970,6 +2391,12 @@ template <int PT, int CT, int NWP, int NS, int UD, bool SPL = false>
 static void launch_w8(const ConvNTArgs& a, hipStream_t st) {
   dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT, a.ngrp > 1 ? a.ngrp : 1);
   hipLaunchKernelGGL((conv_nt_w8_kernel<PT, CT, NWP, NS, UD, SPL>), grid, dim3(512), 0, st, a);
+}
+
+template <int UD, bool SPL = false>
+static void launch_pp(const ConvNTArgs& a, hipStream_t st) {
+  dim3 grid((a.K + 255) / 256, (a.M + 255) / 256, a.ngrp > 1 ? a.ngrp : 1);
+  hipLaunchKernelGGL((conv_nt_pp_kernel<UD, SPL>), grid, dim3(512), 0, st, a);
 }
 
 template <int PT, int CT, int NS, int UD, int NWP = 2, bool SPL = false>
@@ -2132,6 +2559,10 @@ DTM_API void dtm_conv_set_stream_act(int on) { g_stream_act = on; }
 static int g_kwide = 1;    // A/B knob: 64-channel tiles for K % 128 in (0, 64] (dtm_conv_set_kwide)
 DTM_API void dtm_conv_set_kwide(int on) { g_kwide = on; }
 DTM_API void dtm_conv_set_w8(int on) { g_tile_w8 = on; }
+// A/B knob: the ping-pong 256x256 tile (conv_nt_pp_kernel) in place of the 8-wave w8 tile wherever the policy picks it
+// (DTM_PP=0/1 sets the initial value: profiling runs of whole programs)
+static int g_tile_pp = getenv("DTM_PP") ? atoi(getenv("DTM_PP")) : 0;
+DTM_API void dtm_conv_set_pp(int on) { g_tile_pp = on; }
 static int g_k64_tile = 3;  // tile of the 64-output-channel layers (A/B knob: dtm_conv_set_k64_tile)
 DTM_API void dtm_conv_set_k64_tile(int id) { g_k64_tile = id; }
 static int g_k32_tile = 1;  // A/B knob: the 256x32 tile for <= 32-channel spatial convs (dtm_conv_set_k32)
@@ -2227,8 +2658,10 @@ static TileCfg pick_tile_impl(const ConvNTArgs& a, bool stats) {
   // (3-slot 8-wave 256x128 / 128x256 forms of this tile - two k-tiles in flight, 144 KiB of LDS - measured slower
   // than the 2-slot 256x256 on every ResNet-50 shape, e.g. 14x14 3x3 82.5 / 79.7 vs 65.0 us, and were removed:
   // profiles/r5/r5_tile_sweep_w8ns3.log)
-  if (id == 40 && a.in_scale) id = 0;
-  if (id == 40) return {id, 256, 2};
+  if ((id == 40 || id == 41) && a.in_scale) id = 0;
+  if (id == 40 && g_tile_pp && g_tile_env != 40) id = 41;
+  if (id == 41 && a.K % 8) id = 40;  // (the ping-pong tile has only the LDS-staged epilogue)
+  if (id == 40 || id == 41) return {id, 256, 2};
   if (id == 30 || id == 31) {
     if (stream_ok(a)) return {id, 64, 2};
     id = a.K <= 64 ? 3 : 4;
@@ -2247,6 +2680,7 @@ static void dispatch_split(const ConvNTArgs& a, const TileCfg& t, hipStream_t st
   else if (t.id == 26) launch_pipe<128, 64, 2, 1, 2, true>(a, st);
   else if (t.id == 32) launch_pipe<256, 32, 2, 1, 4, true>(a, st);
   else if (t.id == 40) launch_w8<256, 256, 2, 2, 1, true>(a, st);
+  else if (t.id == 41) launch_pp<1, true>(a, st);
   else launch_nt<128, 128, 64, 64, 1, 2, true>(a, st);
 }
 
@@ -2271,6 +2705,7 @@ static void dispatch_ud(const ConvNTArgs& a, const TileCfg& t, hipStream_t st) {
   else if (t.id == 26) launch_pipe<128, 64, 2, UD>(a, st);
   else if (t.id == 32) launch_pipe<256, 32, 2, UD, 4>(a, st);   // waves 4x1 of 64x32 (32-channel outputs)
   else if (t.id == 40) launch_w8<256, 256, 2, 2, UD>(a, st);
+  else if (t.id == 41) launch_pp<UD>(a, st);
   // (a stream-K form of this tile for the < 2-round grids - ResNet-50's 196-tile 14x14 layers - was correct but slower:
   //  a 256x256 fp32 partial is 256 KiB of slab traffic per hand-off; profiles/ab/r5_ab_stream_k_w8.log)
   else launch_nt<128, 128, 64, 64, UD>(a, st);
@@ -2539,11 +2974,11 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, const ConvD
     }
     int id = gi >= 0 ? lt[gi].id : -1;
     if (gi >= 0 && g_dec_tile && (id == 21 || id == 26) && g_tile_env < 0 && g_act_tile < 0) {
-      if (la[gi].K % 256 == 0 && g_tile_w8) lt[gi] = {40, 256, 2};
+      if (la[gi].K % 256 == 0 && g_tile_w8) lt[gi] = {g_tile_pp ? 41 : 40, 256, 2};
       else if (la[gi].K <= 128) lt[gi] = {26, 128, 2};
       id = lt[gi].id;
     }
-    if (!(id == 0 || id == 3 || id == 4 || id == 21 || id == 24 || id == 26 || id == 32 || id == 40)) gi = -1;
+    if (!(id == 0 || id == 3 || id == 4 || id == 21 || id == 24 || id == 26 || id == 32 || id == 40 || id == 41)) gi = -1;
     if (gi >= 0) {  // every class on that tile: one partial-sum row per pixel tile of it
       rows = 0;
       for (int i = 0; i < nl; ++i) {
@@ -2708,7 +3143,8 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
        (wt == 10 && d->K % 128 != 0 && d->R * d->S > 1 && a.Mpix >= 262144)))
     wt = 11;
   if (wt >= 10 && (in_scale || bn)) wt = d->K <= 64 ? 1 : 0;  // the pipelined kernels have no operand prologues
-  if (wt != 0 && wt != 1 && wt != 6 && wt != 10 && wt != 11 && wt != 12) wt = 0;
+  if (wt == 12 && g_tile_pp && wenv == -1) wt = 13;  // (the ping-pong form of the 256x256 tile, A/B knob dtm_conv_set_pp)
+  if (wt != 0 && wt != 1 && wt != 6 && wt != 10 && wt != 11 && wt != 12 && wt != 13) wt = 0;
   {
     static int log = -1;  // DTM_TILE_LOG=1: one stderr line per weight-gradient decision too
     if (log < 0) {
@@ -2719,9 +3155,9 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
       fprintf(stderr, "dtm_wgrad M=%d K=%d C=%d RxS=%dx%d Kg=%d st=%d pro=%d bn=%d dst=%d -> %d\n", a.Mpix, d->K, d->C,
               d->R, d->S, a.Kg, d->stride, in_scale != nullptr, bn != nullptr, dst ? dst->n : 0, wt);
   }
-  const bool big = wt == 12;  // 8-wave 256x256 (one block per CU)
+  const bool big = wt == 12 || wt == 13;  // 8-wave 256x256 (one block per CU)
   const int MT = wt == 6 ? 32 : ((wt == 1 || wt == 11) ? 64 : (big ? 256 : 128)), NT = (big || wt == 11) ? 256 : 128;
-  if (big) occ = (wenv == 12 && g_wgrad_occ != 4) ? g_wgrad_occ : 1;  // (sweeps: WTILES=12:<occ>)
+  if (big) occ = ((wenv == 12 || wenv == 13) && g_wgrad_occ != 4) ? g_wgrad_occ : 1;  // (sweeps: WTILES=12:<occ>)
   long tiles = (long)((a.Kg + NT - 1) / NT) * ((a.K + MT - 1) / MT);
   // register-staged tiles: 3 blocks' worth of splits per CU (sweeps: WTILES=<1|6|0>:<occ>, occ != 4)
   const int rs_occ = (wenv >= 0 && g_wgrad_occ != 4) ? g_wgrad_occ : 3;
@@ -2743,7 +3179,8 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   if (wt >= 10) {
     a.in_shift = (const float*)zero_chunk();  // the zero DMA source
     dim3 grid((a.Kg + NT - 1) / NT, (a.K + MT - 1) / MT, splits);
-    if (wt == 12)
+    if (wt == 13) hipLaunchKernelGGL(conv_wgrad_pp_kernel, grid, dim3(512), 0, (hipStream_t)stream, a);
+    else if (wt == 12)
       hipLaunchKernelGGL((conv_wgrad_pipe_kernel<256, 256, 2, 2, 512>), grid, dim3(512), 0, (hipStream_t)stream, a);
     else if (wt == 11)
       hipLaunchKernelGGL((conv_wgrad_pipe_kernel<64, 256, 2>), grid, dim3(256), 0, (hipStream_t)stream, a);

@@ -218,7 +218,7 @@ def test_conv_pipelined_tiles_match_reference(tile, prologue, case):
     assert _rel(stats[0], yf.sum(0)) < 1e-3 and _rel(stats[1], yf.square().sum(0)) < 1e-3
 
 
-@pytest.mark.parametrize("tile", [-1, 4, 21, 24, 26, 32])
+@pytest.mark.parametrize("tile", [-1, 4, 21, 24, 26, 32, 40, 41])
 @pytest.mark.parametrize("case", [(2, 14, 14, 128, 256, 3, 1), (3, 7, 7, 512, 200, 1, 1), (4, 15, 15, 96, 64, 3, 2),
                                   (2, 28, 28, 128, 128, 3, 2), (2, 9, 9, 64, 40, 3, 1), (2, 30, 30, 64, 128, 1, 1)])
 def test_conv_act_dgrad_tiles_match_reference(tile, case):
@@ -564,13 +564,13 @@ def test_conv_fwd_bn_multi_matches_separate(case):
             assert not sss[i].any()
 
 
-@pytest.mark.parametrize("tile", [0, 1, 6, 10, 11, 12])
+@pytest.mark.parametrize("tile", [0, 1, 6, 10, 11, 12, 13])
 @pytest.mark.parametrize("case", [(4, 15, 15, 64, 96, 3, 2), (2, 14, 14, 128, 256, 3, 1), (3, 7, 7, 512, 200, 1, 1),
                                   (2, 9, 9, 24, 40, 3, 1), (5, 8, 8, 64, 64, 1, 1), (4, 9, 9, 256, 512, 3, 1),
-                                  (3, 13, 13, 32, 32, 3, 1), (2, 11, 11, 32, 24, 3, 2)])
+                                  (3, 13, 13, 32, 32, 3, 1), (2, 11, 11, 32, 24, 3, 2), (16, 14, 14, 512, 512, 3, 1)])
 def test_conv_wgrad_pipelined_tiles_match_reference(tile, case):
-    """The wgrad kernels - register-staged tiles 0 / 1 / 6 (128 / 64 / 32 rows x 128 columns) and the pipelined (10: 128 x 128, 11: 64 x 256, 12: 256 x 256)
-    LDS-DMA ones (inverse transposed-read image mapping for the DMA slots) - with split-K slabs against the
+    """The wgrad kernels - register-staged tiles 0 / 1 / 6 (128 / 64 / 32 rows x 128 columns) and the pipelined (10: 128 x 128, 11: 64 x 256, 12: 256 x 256,
+    13: its ping-pong form) LDS-DMA ones (inverse transposed-read image mapping for the DMA slots) - with split-K slabs against the
     fp32 reference, including K / R*S*C tails and empty splits."""
     import ctypes
 
