@@ -738,6 +738,18 @@ DTM_API void dtm_bn_stats(const void* x, float* stats, long M, int C, void* stre
     hipLaunchKernelGGL(bn_stats_kernel<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, stats, M, C, rpb);
 }
 
+// Column sums (and sums of squares) of x [M][C] into stats [2][C] (zeroed by the caller) in a fixed summation order:
+// the bias gradients (ops/nn.py _col_sums) - deterministic run to run, unlike dtm_bn_stats' policy reduction.
+DTM_API int dtm_col_sums(const void* x, float* stats, long M, int C, void* stream) {
+  if (!fast_ok(M, C)) return -1;
+  int blocks, rpb; fast_grid(M, C, &blocks, &rpb);
+  float* ws = dtm_ws_get_stream((size_t)blocks * 2 * C, (hipStream_t)stream);
+  if (!ws) return -4;
+  hipLaunchKernelGGL(bn_stats_fast, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ws, (int)M, C, rpb);
+  dtm_reduce_rows_det(ws, blocks, 2 * C, 2 * C, stats, (hipStream_t)stream);
+  return 0;
+}
+
 DTM_API void dtm_bn_finalize(const float* stats, const float* gamma, const float* beta, float* mov_mean,
                              float* mov_var, float* out, int C, float count, float eps, float decay, int update,
                              int bessel, void* stream) {

@@ -66,6 +66,7 @@ __host__ static inline FastDiv make_fastdiv(uint32_t d) {
 
 // workspace arena + two-stage reduction (workspace.hip)
 void dtm_reduce_rows(const float* ws, int rows, int width, int ld, float* out, hipStream_t st);
+void dtm_reduce_rows_det(const float* ws, int rows, int width, int ld, float* out, hipStream_t st);
 // several row-sum reductions over the same rows (column segments of one partial-sum table, each into its own output:
 // the split-K slabs of a merged sibling weight gradient) in ONE launch (n <= 8)
 void dtm_reduce_rows_multi(const float* const* ws, const int* widths, float* const* outs, int n, int rows, int ld,

@@ -155,15 +155,18 @@ __global__ void scale_kernel(float* __restrict__ x, long n, float s) {
 // place of the float cast, broadcast multiply and bf16 cast autograd would launch; gstride 0: one scale for every row.
 template <typename T>
 __global__ __launch_bounds__(256) void scale_rows_pad_kernel(const T* __restrict__ dl, const float* __restrict__ gl,
-                                                             int gstride, T* __restrict__ out, int N, int ldo) {
-  const int r = blockIdx.y;
-  const float g = gl[(long)r * gstride];
-  const T* src = dl + (long)r * N;
-  T* dst = out + (long)r * ldo;
-  for (int c = blockIdx.x * 256 + threadIdx.x; c < ldo; c += gridDim.x * 256) {
-    const float v = c < N ? ldf(src, c) * g : 0.f;
-    if constexpr (sizeof(T) == 2) dst[c] = f2bf(v);
-    else dst[c] = v;
+                                                             int gstride, T* __restrict__ out, int B, int N,
+                                                             int ldo) {
+  // rows grid-stride over blockIdx.y (grid.y <= 65535 whatever the batch)
+  for (int r = blockIdx.y; r < B; r += gridDim.y) {
+    const float g = gl[(long)r * gstride];
+    const T* src = dl + (long)r * N;
+    T* dst = out + (long)r * ldo;
+    for (int c = blockIdx.x * 256 + threadIdx.x; c < ldo; c += gridDim.x * 256) {
+      const float v = c < N ? ldf(src, c) * g : 0.f;
+      if constexpr (sizeof(T) == 2) dst[c] = f2bf(v);
+      else dst[c] = v;
+    }
   }
 }
 
@@ -192,14 +195,15 @@ using namespace dtm;
 
 DTM_API int dtm_scale_rows_pad(const void* dl, int bf16, const float* gl, int gstride, void* out, int B, int N, int ldo,
                                void* stream) {
-  if (B <= 0 || N <= 0 || ldo < N || B > 65535) return -1;
+  if (B <= 0 || N <= 0 || ldo < N) return -1;
   const int bx = (ldo + 255) / 256 > 8 ? 8 : (ldo + 255) / 256;
+  const int by = B > 65535 ? 65535 : B;
   if (bf16)
-    hipLaunchKernelGGL(scale_rows_pad_kernel<bf16_t>, dim3(bx, B), dim3(256), 0, (hipStream_t)stream,
-                       (const bf16_t*)dl, gl, gstride, (bf16_t*)out, N, ldo);
+    hipLaunchKernelGGL(scale_rows_pad_kernel<bf16_t>, dim3(bx, by), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)dl, gl, gstride, (bf16_t*)out, B, N, ldo);
   else
-    hipLaunchKernelGGL(scale_rows_pad_kernel<float>, dim3(bx, B), dim3(256), 0, (hipStream_t)stream, (const float*)dl,
-                       gl, gstride, (float*)out, N, ldo);
+    hipLaunchKernelGGL(scale_rows_pad_kernel<float>, dim3(bx, by), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)dl, gl, gstride, (float*)out, B, N, ldo);
   return 0;
 }
 

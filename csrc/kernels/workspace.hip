@@ -281,6 +281,17 @@ void dtm_reduce_rows(const float* ws, int rows, int width, int ld, float* out, h
                      chunks);
 }
 
+// dtm_reduce_rows with one row chunk whatever the policy: a fixed summation order, no atomics (bias gradients:
+// small slabs, and run-to-run reproducible outside DTM_DETERMINISTIC too)
+void dtm_reduce_rows_det(const float* ws, int rows, int width, int ld, float* out, hipStream_t st) {
+  if (width % 4 == 0 && ld % 4 == 0) {
+    hipLaunchKernelGGL(reduce_rows4_kernel, dim3((width + 63) / 64, 1), dim3(256), 0, st, ws, rows, width, ld, out,
+                       rows < 16 ? 16 : (rows + 15) / 16 * 16);
+    return;
+  }
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((width + 255) / 256, 1), dim3(256), 0, st, ws, rows, width, ld, out, 1);
+}
+
 void dtm_reduce_rows_multi(const float* const* ws, const int* widths, float* const* outs, int n, int rows, int ld,
                            hipStream_t st) {
   bool ok = n >= 1 && n <= 8 && ld % 4 == 0 && !(g_red_few && rows <= 32);

@@ -31,7 +31,16 @@ def node_cpus():
 
 
 def local_world():
-    return int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    """Ranks that share this process's CPUs.  When the affinity mask is narrower than the host (ranks pinned to CPU
+    subsets) every rank decodes on its own CPUs: 1.  Otherwise the ranks of this node (LOCAL_WORLD_SIZE; never the
+    global WORLD_SIZE, which counts other nodes' ranks)."""
+    try:
+        pinned = len(os.sched_getaffinity(0)) < (os.cpu_count() or 1)
+    except AttributeError:
+        pinned = False
+    if pinned:
+        return 1
+    return int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
 
 
 def needed_cpus(per_gpu_img_s, gpus, mode="full", per_cpu=None):
@@ -71,4 +80,7 @@ def choose_split_decode(model, gpus=None, cpus=None, per_cpu=None):
         return False
     gpus = local_world() if gpus is None else gpus
     cpus = node_cpus() if cpus is None else cpus
-    return needed_cpus(per_gpu, gpus, "full", per_cpu) > cpus
+    split = needed_cpus(per_gpu, gpus, "full", per_cpu) > cpus
+    logging.getLogger("distributed_tensorflow_models_amd").info(
+        "input pipeline: %s JPEG decode (%d rank(s) on %d CPUs, %s)", "split" if split else "full", gpus, cpus, model)
+    return split

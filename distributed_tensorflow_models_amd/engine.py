@@ -96,11 +96,12 @@ class TrainStep:
         # force_comm: issue the collectives even with one rank (tests of the RCCL path on a one-GPU box)
         self.dp = BSPDataParallel(params, bucket_mb, process_group, comm_dtype=grad_comm_dtype, overlap=overlap,
                                   check=bsp_check, names=list(model.named_parameters()), force_comm=force_comm)
-        if use_graph and self.dp.world > 1:
+        if use_graph and self.dp.comm_on:
             # a captured step would hold the bucket collectives (and their waits) inside the graph;
-            # RCCL-in-hipGraph has never been validated here, so multi-rank runs stay eager
-            raise ValueError("use_graph (hipGraph step capture) is single-rank only; world size is %d"
-                             % self.dp.world)
+            # RCCL-in-hipGraph has never been validated here, so runs that issue collectives (world > 1, or
+            # force_comm at world 1) stay eager
+            raise ValueError("use_graph (hipGraph step capture) is only for steps without collectives; world size %d, "
+                             "force_comm %s" % (self.dp.world, bool(force_comm)))
         # BN moving statistics: one flat buffer, averaged over the replicas every step (reference
         # keeps ONE PS-resident copy that every worker updates); must precede the optimizer tables
         bufs = moving_average_buffers(model)

@@ -66,6 +66,7 @@ _SIGS = {
     "dtm_weight_flip_transpose_dec": (None, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "dtm_flip_desc_bytes": (_I, []),
     "dtm_bn_stats": (None, [_P, _P, _L, _I, _P]),
+    "dtm_col_sums": (_I, [_P, _P, _L, _I, _P]),
     "dtm_bn_stats_bwd": (_I, [_P, _P, _P, _P, _L, _I, _P]),
     "dtm_bn_finalize": (None, [_P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _I, _I, _P]),
     "dtm_bn_inference_params": (None, [_P, _P, _P, _P, _P, _I, _F, _P]),

@@ -312,8 +312,9 @@ def _col_sums(g, param):
             and getattr(param, "main_grad", None) is not None):
         from .fused import arena
         st = arena.zeros((2, K), g.device)
-        _lib.lib().dtm_bn_stats(_lib.ptr(g), _lib.ptr(st), g.numel() // K, K, _lib.stream_ptr())
-        return st[0]
+        # (one row chunk: a fixed summation order, so bias gradients reproduce run to run - ADVICE r5)
+        if _lib.lib().dtm_col_sums(_lib.ptr(g), _lib.ptr(st), g.numel() // K, K, _lib.stream_ptr()) == 0:
+            return st[0]
     return g.reshape(-1, K).float().sum(0)
 
 
@@ -613,7 +614,7 @@ def _pool_grad_out(slot, dx):
     """Pool backward's input gradient under the hand-off: the pool branch is built last in an
     Inception block, so its backward runs first and stashes; the last conv consumer folds the stash
     into its dgrad epilogue - no separate add over the block input."""
-    from .fused import _slot_done, _slot_stash, _slot_take, _unstride
+    from .fused import _slot_stash, _slot_take, _unstride
     if slot is None:
         return dx
     last, buf, bst = _slot_take(slot)
@@ -622,7 +623,10 @@ def _pool_grad_out(slot, dx):
         return None
     if buf is not None:
         dx = dx + _unstride(slot, buf, bst)
-    return _slot_done(slot, dx)
+    # (not recorded as the slot's main gradient for a tail consumer: a pool that is the last slot consumer may
+    # share x with generic consumers whose gradients autograd adds out of place - the recorded tensor would then be
+    # stale and the tail's in-place add lost.  Only a conv dgrad epilogue that folded the stash records it.)
+    return dx
 
 
 TAIL_FUSED = [0]  # tail avg-pool gradients added in place into the main-path gradient (tests / diagnostics)
@@ -759,7 +763,10 @@ def avg_pool(x, kernel, stride, padding="VALID", count_pad=False, grad_handoff=F
     xb = x.to(torch.bfloat16)
     share = grad_handoff and xb is x and xb.is_contiguous()
     tail = None
-    if grad_tail and not share and xb is x and xb.is_contiguous() and features.on("pool_tail"):
+    # (the tail needs every other consumer of x on the slot: with fused_bn off the convs take the generic path and
+    # autograd sums their gradients, so the tail stays off)
+    if (grad_tail and not share and xb is x and xb.is_contiguous() and features.on("pool_tail")
+            and features.on("fused_bn")):
         from .fused import _slot_tail
         tail = _slot_tail(xb)
     return _AvgPoolFn.apply(xb, g, bool(count_pad), _pool_slot(xb) if share else None, tail)

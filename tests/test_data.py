@@ -421,7 +421,17 @@ def test_decode_capacity_check_warns_when_host_cpus_cannot_feed_the_node(monkeyp
     monkeypatch.setenv("DTM_SPLIT_DECODE", "1")
     assert capacity.choose_split_decode("resnet_v1_50", gpus=1, cpus=64, per_cpu=rate)
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
-    assert capacity.local_world() == 8 and capacity.node_cpus() >= 1
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(64)))
+    monkeypatch.setattr(os, "cpu_count", lambda: 64)
+    assert capacity.local_world() == 8 and capacity.node_cpus() == 64
+    # ranks pinned to CPU subsets: each decodes on its own CPUs (1 rank per affinity mask), and the global
+    # WORLD_SIZE of a multi-node launch without LOCAL_WORLD_SIZE is never taken for the node's rank count
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(8)))
+    assert capacity.local_world() == 1 and capacity.node_cpus() == 8
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(64)))
+    monkeypatch.delenv("LOCAL_WORLD_SIZE")
+    monkeypatch.setenv("WORLD_SIZE", "32")
+    assert capacity.local_world() == 1
 
 
 def test_decode_cpu_cost_tool_measures_both_modes():

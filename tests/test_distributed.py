@@ -638,7 +638,7 @@ def _graph_refusal_worker(rank, world):
     try:
         TrainStep(model, optimizer="sgd", lr=0.01, use_graph=True)
     except ValueError as e:
-        return {"refused": "single-rank" in str(e)}
+        return {"refused": "without collectives" in str(e)}
     return {"refused": False}
 
 

@@ -65,7 +65,7 @@ def test_conv_bn_chain_prologue(C, relu):
     """conv+BN(+relu) folded into the next conv's operand prologue (fwd) and wgrad/act_bwd (bwd).
     The linear variant has no relu-mask noise and is checked tightly (catches indexing bugs for
     any C); with relu, bf16 mask flips near zero move per-channel grads by a few % (see
-    tools/diag_chain.py), so that variant is a coarse check."""
+    a round-4 diagnostic), so that variant is a coarse check."""
     torch.manual_seed(1)
     x = torch.randn(2, 10, 10, C, device=DEV).to(torch.bfloat16).float()
     w1 = (torch.randn(C, 1, 1, C, device=DEV) / C ** 0.5).to(torch.bfloat16).float()
@@ -661,7 +661,7 @@ def test_block_output_bn_backward_in_dgrad_epilogue(monkeypatch):
     assert grads["0"].keys() == grads["1"].keys()
     # The two paths differ only in rounding: the separate pass rounds d(out) to bf16 before masking and sums
     # the bf16 g, the epilogue masks and sums the fp32 value.  The difference is ~0.4 % at the first fused
-    # unit and accumulates ~0.15 % per unit towards the stem (tools/diag_bnout.py; an indexing or mask bug
+    # unit and accumulates ~0.15 % per unit towards the stem (a round-3 diagnostic; an indexing or mask bug
     # shows up at full size at the first fused unit).  The stem BN's beta gradient (a cancelling sum over
     # the whole image) is excluded.
     errs = {k: _rel(grads["1"][k], grads["0"][k]) for k in grads["0"] if k.startswith("units.")}

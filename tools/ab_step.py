@@ -62,7 +62,7 @@ def apply(cfg):
     L.dtm_set_deterministic(int(cfg.get("det", "0")))
     L.dtm_conv_set_k64_tile(int(cfg.get("k64", "3")))
     L.dtm_conv_set_w8(int(cfg.get("w8", "1")))
-    L.dtm_conv_set_pp(int(cfg.get("pp", "1")))
+    L.dtm_conv_set_pp(int(cfg.get("pp", "0")))
     L.dtm_conv_set_kwide(int(cfg.get("kwide", "1")))
     L.dtm_set_reduce_few(int(cfg.get("few", "1")))
     L.dtm_conv_set_stream_act(int(cfg.get("sact", "0")))
