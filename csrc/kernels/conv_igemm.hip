@@ -1965,7 +1965,11 @@ __device__ __forceinline__ void tr_inv(int q, int& k, int& m) {
 
 // NTH threads (256 = 4 waves 2x2; 512 = the 8-wave 256x256 variant, waves NWM x 8/NWM): the bigger tile
 // halves the L2 operand bytes per MFMA (same reasoning as conv_nt_w8_kernel)
-template <int MT, int NT, int NS, int NWM = 2, int NTH = 256>
+// BNA: the BatchNorm backward of dy fused into the A operand (ConvWgradArgs::ay, the stem's conv+BN with no input
+// gradient): the raw BN input y is LDS-DMA'd beside g into a parallel image and, once this wave's DMAs of the k-tile
+// have landed, each lane rewrites ITS OWN chunks to comb = g*scale + dsum + 2*dsumsq*y (stats_combine_fin's algebra)
+// before the barrier that publishes the stage - the register-staged kernel's fusion on the pipelined tile.
+template <int MT, int NT, int NS, int NWM = 2, int NTH = 256, bool BNA = false>
 __global__ __launch_bounds__(NTH) void conv_wgrad_pipe_kernel(ConvWgradArgs a) {
   constexpr int BK = 64;
   constexpr int NW = NTH / 64;
@@ -1973,9 +1977,11 @@ __global__ __launch_bounds__(NTH) void conv_wgrad_pipe_kernel(ConvWgradArgs a) {
   constexpr int WM = MT / NWM, WN = NT / NWN;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int AI = MT / (8 * NW), BI = NT / (8 * NW);  // 1-KiB DMA pieces per wave per k-tile
-  constexpr int G = AI + BI;
+  constexpr int G = AI + BI + (BNA ? AI : 0);
   constexpr int BUF = BK * (MT + NT) * 2;
-  __shared__ __attribute__((aligned(16))) char smem[NS * BUF];
+  constexpr int YBUF = BNA ? BK * MT * 2 : 0;  // the y image of one slot
+  constexpr int OFF_Y = NS * BUF, OFF_C = OFF_Y + NS * YBUF;
+  __shared__ __attribute__((aligned(16))) char smem[OFF_C + (BNA ? MT * 12 : 0)];
   typedef __attribute__((address_space(1))) const void gvoid;
   typedef __attribute__((address_space(3))) void lvoid;
   static_assert(G <= 31 && NS >= 2 && NS <= 3, "vmcnt range");
@@ -1989,6 +1995,27 @@ __global__ __launch_bounds__(NTH) void conv_wgrad_pipe_kernel(ConvWgradArgs a) {
   const int n0 = bx * NT, m0 = by * MT;
   const int pix_lo = bz * a.pix_per_split;
   const int pix_hi = min(a.Mpix, pix_lo + a.pix_per_split);
+  float* s_cs = (float*)(smem + OFF_C);  // BNA: comb = g*s_cs + s_ca + s_cb*y per row ko of this block
+  float* s_ca = s_cs + MT;
+  float* s_cb = s_ca + MT;
+  if constexpr (BNA) {
+    for (int j = tid; j < MT; j += NTH) {
+      const int ko = m0 + j;
+      float ds = 0.f, dq = 0.f, dg, db, sc = 0.f;
+      if (ko < a.K) {
+        fin_bwd_channel(a.dss, a.ss, a.gamma, a.K, ko, a.count, &ds, &dq, &dg, &db);
+        sc = a.ss[ko];
+        if (bx == 0 && bz == 0) {
+          if (a.dgamma) a.dgamma[ko] += dg;
+          if (a.dbeta) a.dbeta[ko] += db;
+        }
+      }
+      s_cs[j] = sc;
+      s_ca[j] = ds;
+      s_cb[j] = 2.f * dq;
+    }
+    __syncthreads();
+  }
 
   // per-lane chunk coordinates of its DMA slots
   int a_k[AI], a_off[AI];
@@ -2017,6 +2044,7 @@ __global__ __launch_bounds__(NTH) void conv_wgrad_pipe_kernel(ConvWgradArgs a) {
   }
   const char* xg = (const char*)a.x;
   const char* dg = (const char*)a.dy;
+  const char* yg = (const char*)a.ay;
   const char* zg = (const char*)a.in_shift;  // the host passes a zero chunk here (no prologue in this kernel)
 
   auto issue = [&](int pbase, int slot) {
@@ -2025,8 +2053,12 @@ __global__ __launch_bounds__(NTH) void conv_wgrad_pipe_kernel(ConvWgradArgs a) {
     for (int j = 0; j < AI; ++j) {
       const int pix = pbase + a_k[j];
       const bool v = (pix < pix_hi) & a_colv[j];
-      const char* src = dg + (size_t)(uint32_t)((pix * a.K + a_off[j]) * 2);
-      __builtin_amdgcn_global_load_lds((gvoid*)(v ? src : zg), (lvoid*)(base + (wave + NW * j) * 1024), 16, 0, 0);
+      const uint32_t off = (uint32_t)((pix * a.K + a_off[j]) * 2);
+      __builtin_amdgcn_global_load_lds((gvoid*)(v ? dg + (size_t)off : zg), (lvoid*)(base + (wave + NW * j) * 1024),
+                                       16, 0, 0);
+      if constexpr (BNA)
+        __builtin_amdgcn_global_load_lds((gvoid*)(v ? yg + (size_t)off : zg),
+                                         (lvoid*)(smem + OFF_Y + slot * YBUF + (wave + NW * j) * 1024), 16, 0, 0);
     }
 #pragma unroll
     for (int j = 0; j < BI; ++j) {
@@ -2082,6 +2114,31 @@ __global__ __launch_bounds__(NTH) void conv_wgrad_pipe_kernel(ConvWgradArgs a) {
     }
   };
 
+  // BNA: this lane's landed A chunks of k-tile kt -> comb in place (padding / out-of-range pixels stay 0)
+  auto transform = [&](int kt, int slot) {
+    const int pbase = pix_lo + kt * BK;
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+      const int pix = pbase + a_k[j];
+      if ((pix < pix_hi) & a_colv[j]) {
+        uint4* pg = (uint4*)(smem + slot * BUF + (wave + NW * j) * 1024 + lane * 16);
+        const uint4 gq = *pg;
+        const uint4 yq = *(const uint4*)(smem + OFF_Y + slot * YBUF + (wave + NW * j) * 1024 + lane * 16);
+        const uint32_t gu[4] = {gq.x, gq.y, gq.z, gq.w}, yu[4] = {yq.x, yq.y, yq.z, yq.w};
+        uint32_t u[4];
+        const int m = a_off[j] - m0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c0 = m + 2 * e, c1 = c0 + 1;
+          const float lo = fmaf(lo_bf(gu[e]), s_cs[c0], s_ca[c0] + s_cb[c0] * lo_bf(yu[e]));
+          const float hi = fmaf(hi_bf(gu[e]), s_cs[c1], s_ca[c1] + s_cb[c1] * hi_bf(yu[e]));
+          u[e] = pack2bf(lo, hi);
+        }
+        *pg = make_uint4(u[0], u[1], u[2], u[3]);
+      }
+    }
+  };
+
   const int nk = (pix_hi - pix_lo + BK - 1) / BK;
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
@@ -2091,6 +2148,7 @@ __global__ __launch_bounds__(NTH) void conv_wgrad_pipe_kernel(ConvWgradArgs a) {
     const int ahead = min(nk - 1, kt + NS - 2) - kt;
     if (NS >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (BNA) transform(kt, slot);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (kt + NS - 1 < nk) issue(pix_lo + (kt + NS - 1) * BK, slot == 0 ? NS - 1 : slot - 1);
@@ -3044,6 +3102,8 @@ static int g_wgrad_env = -2;
 static int g_wgrad_occ = 4;
 static int g_wgrad_k64 = 1;  // A/B knob (dtm_conv_set_wgrad_k64): the 64 x 256 pipelined tile for K % 128 != 0
 DTM_API void dtm_conv_set_wgrad_k64(int on) { g_wgrad_k64 = on; }
+static int g_stem_bna = 1;  // A/B knob: the stem's BN-fused weight gradient on the pipelined tile 15 (dtm_conv_set_stem_bna)
+DTM_API void dtm_conv_set_stem_bna(int on) { g_stem_bna = on; }
 DTM_API void dtm_conv_set_wgrad_tile(int id, int occ) {
   g_wgrad_env = id;
   if (occ > 0) g_wgrad_occ = occ;
@@ -3142,9 +3202,15 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
       ((wt == 1 && d->R * d->S >= 25 && a.Kg >= 1024) ||
        (wt == 10 && d->K % 128 != 0 && d->R * d->S > 1 && a.Mpix >= 262144)))
     wt = 11;
-  if (wt >= 10 && (in_scale || bn)) wt = d->K <= 64 ? 1 : 0;  // the pipelined kernels have no operand prologues
+  if (wt >= 10 && wt <= 13 && (in_scale || bn)) wt = d->K <= 64 ? 1 : 0;  // (no x prologue in the pipelined kernels)
+  // the pipelined 64 x 256 tile with the BN backward fused into its A staging (BNA): 14 = 4 waves 2 slots, 15 = 8
+  // waves 2 slots, 16 = 8 waves 3 slots
+  if (wt >= 14 && wt <= 16 && (in_scale || !bn || d->K > 64)) wt = d->K <= 64 ? 1 : 0;
+  // the stem (BN backward fused, 64 x <= 256): tile 15 - the g / y operand read once and pipelined, 385.7 -> 357.1 us
+  // at batch 256 (tools/stem_sweep.py, profiles/r6/r6_s10_stem_wgrad.log)
+  if (wenv == -1 && g_stem_bna && bn && !in_scale && d->K <= 64 && a.Kg <= 256) wt = 15;
   if (wt == 12 && g_tile_pp && wenv == -1) wt = 13;  // (the ping-pong form of the 256x256 tile, A/B knob dtm_conv_set_pp)
-  if (wt != 0 && wt != 1 && wt != 6 && wt != 10 && wt != 11 && wt != 12 && wt != 13) wt = 0;
+  if (wt != 0 && wt != 1 && wt != 6 && wt != 7 && wt != 8 && !(wt >= 10 && wt <= 16)) wt = 0;
   {
     static int log = -1;  // DTM_TILE_LOG=1: one stderr line per weight-gradient decision too
     if (log < 0) {
@@ -3156,8 +3222,10 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
               d->R, d->S, a.Kg, d->stride, in_scale != nullptr, bn != nullptr, dst ? dst->n : 0, wt);
   }
   const bool big = wt == 12 || wt == 13;  // 8-wave 256x256 (one block per CU)
-  const int MT = wt == 6 ? 32 : ((wt == 1 || wt == 11) ? 64 : (big ? 256 : 128)), NT = (big || wt == 11) ? 256 : 128;
-  if (big) occ = ((wenv == 12 || wenv == 13) && g_wgrad_occ != 4) ? g_wgrad_occ : 1;  // (sweeps: WTILES=12:<occ>)
+  const bool k64w = wt == 1 || wt == 7 || wt == 8 || wt == 11 || wt >= 14;  // 64-row tiles
+  const int MT = wt == 6 ? 32 : (k64w ? 64 : (big ? 256 : 128)), NT = (big || (k64w && wt != 1)) ? 256 : 128;
+  if (big) occ = ((wenv == 12 || wenv == 13) && g_wgrad_occ != 4) ? g_wgrad_occ : 1;
+  if (wt >= 14) occ = (wenv >= 14 && g_wgrad_occ != 4) ? g_wgrad_occ : 1;  // (the BNA tiles: 1 block per CU)  // (sweeps: WTILES=12:<occ>)
   long tiles = (long)((a.Kg + NT - 1) / NT) * ((a.K + MT - 1) / MT);
   // register-staged tiles: 3 blocks' worth of splits per CU (sweeps: WTILES=<1|6|0>:<occ>, occ != 4)
   const int rs_occ = (wenv >= 0 && g_wgrad_occ != 4) ? g_wgrad_occ : 3;
@@ -3180,6 +3248,12 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
     a.in_shift = (const float*)zero_chunk();  // the zero DMA source
     dim3 grid((a.Kg + NT - 1) / NT, (a.K + MT - 1) / MT, splits);
     if (wt == 13) hipLaunchKernelGGL(conv_wgrad_pp_kernel, grid, dim3(512), 0, (hipStream_t)stream, a);
+    else if (wt == 14)
+      hipLaunchKernelGGL((conv_wgrad_pipe_kernel<64, 256, 2, 2, 256, true>), grid, dim3(256), 0, (hipStream_t)stream, a);
+    else if (wt == 15)
+      hipLaunchKernelGGL((conv_wgrad_pipe_kernel<64, 256, 2, 2, 512, true>), grid, dim3(512), 0, (hipStream_t)stream, a);
+    else if (wt == 16)
+      hipLaunchKernelGGL((conv_wgrad_pipe_kernel<64, 256, 3, 2, 512, true>), grid, dim3(512), 0, (hipStream_t)stream, a);
     else if (wt == 12)
       hipLaunchKernelGGL((conv_wgrad_pipe_kernel<256, 256, 2, 2, 512>), grid, dim3(512), 0, (hipStream_t)stream, a);
     else if (wt == 11)
@@ -3188,6 +3262,10 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
       hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 128, 2>), grid, dim3(256), 0, (hipStream_t)stream, a);
   } else if (wt == 1) launch_wgrad<64, 128, 32, 64>(a, (int)splits, (hipStream_t)stream);
   else if (wt == 6) launch_wgrad<32, 128, 16, 64>(a, (int)splits, (hipStream_t)stream);
+  // 64 x 256 register-staged (7: one LDS buffer, 8: two): every column of a <= 256-wide reduction in one tile, so the
+  // dy operand (and the stem's fused BN backward inputs g, y) is read once instead of once per 128-column tile
+  else if (wt == 7) launch_wgrad<64, 256, 32, 128, 1>(a, (int)splits, (hipStream_t)stream);
+  else if (wt == 8) launch_wgrad<64, 256, 32, 128, 2>(a, (int)splits, (hipStream_t)stream);
   else launch_wgrad<128, 128, 64, 64>(a, (int)splits, (hipStream_t)stream);
   // dW += sum over the split slabs (every slab element is written: tiles cover [K][Kg] exactly).  (Running these
   // reductions on a second stream under the next conv - slabs in a 2-entry ring, event hand-offs, joined before the

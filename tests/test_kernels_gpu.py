@@ -1021,3 +1021,49 @@ def test_conv_wgrad_multi_matches_separate(case, det):
     for k, got in zip(ks, dws):
         assert _rel(got.reshape(k, C), ref[off:off + k]) < 1e-4, (k, _rel(got.reshape(k, C), ref[off:off + k]))
         off += k
+
+
+@pytest.mark.parametrize("tile", [1, 7, 8, 14, 15, 16])
+@pytest.mark.parametrize("N", [2, 5])
+def test_stem_wgrad_bn_fused_tiles_match_unfused(tile, N):
+    """The stem's weight gradient with its BN backward fused into the A-operand staging (dtm_conv_wgrad_bnbwd) on
+    every tile that can take it - register-staged 64 x 128 (1) / 64 x 256 (7, 8) and the pipelined 64 x 256 with the
+    in-LDS transform (14, 15, 16) - against the unfused form (stats_combine_fin -> comb, then a plain wgrad), and
+    dgamma / dbeta against the combine's: packed-row 7x7/2 view at 224 x 224."""
+    import ctypes
+
+    from distributed_tensorflow_models_amd.ops import _lib
+    torch.manual_seed(21)
+    L = _lib.lib()
+    st = _lib.stream_ptr()
+    Hp = Wp = 230
+    P = Q = 112
+    xp = torch.randn(N, Hp, Wp, 4, device=DEV).to(torch.bfloat16)
+    d = _lib.ConvDesc(N, Hp, Wp, 32, 64, 7, 1, P, Q, 2, 0, 0, 8)
+    g = torch.randn(N, P, Q, 64, device=DEV).to(torch.bfloat16)
+    y = torch.randn(N, P, Q, 64, device=DEV).to(torch.bfloat16)
+    count = float(N * P * Q)
+    dss = torch.randn(4, 64, device=DEV) * 1e-2 * count
+    ss = torch.cat([torch.rand(1, 64, device=DEV) + 0.5, torch.randn(1, 64, device=DEV),
+                    torch.randn(1, 64, device=DEV) * 0.1, torch.rand(1, 64, device=DEV) + 0.5]).contiguous()
+    gamma = torch.rand(64, device=DEV) + 0.5
+    comb = torch.empty_like(g)
+    dg0, db0 = torch.zeros(64, device=DEV), torch.zeros(64, device=DEV)
+    assert L.dtm_stats_combine_fin(_lib.ptr(g), _lib.ptr(y), _lib.ptr(dss), _lib.ptr(ss), _lib.ptr(gamma), count,
+                                   _lib.ptr(dg0), _lib.ptr(db0), _lib.ptr(comb), N * P * Q, 64, 1, st) == 0
+    dw0 = torch.zeros(64, 7, 8, 4, device=DEV)
+    L.dtm_conv_set_wgrad_tile(1, 0)
+    try:
+        assert L.dtm_conv_wgrad(_lib.ptr(xp), _lib.ptr(comb), _lib.ptr(dw0), None, None, ctypes.byref(d),
+                                _lib.num_cus(), st) == 0
+        dw = torch.zeros(64, 7, 8, 4, device=DEV)
+        dg, db = torch.zeros(64, device=DEV), torch.zeros(64, device=DEV)
+        L.dtm_conv_set_wgrad_tile(tile, 0)
+        assert L.dtm_conv_wgrad_bnbwd(_lib.ptr(xp), _lib.ptr(g), _lib.ptr(y), _lib.ptr(dss), _lib.ptr(ss),
+                                      _lib.ptr(gamma), count, _lib.ptr(dg), _lib.ptr(db), _lib.ptr(dw),
+                                      ctypes.byref(d), _lib.num_cus(), st) == 0
+        torch.cuda.synchronize()
+    finally:
+        L.dtm_conv_set_wgrad_tile(-1, 4)
+    assert _rel(dw, dw0) < 2e-3, _rel(dw, dw0)
+    assert _rel(dg, dg0) < 1e-5 and _rel(db, db0) < 1e-5

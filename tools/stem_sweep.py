@@ -43,6 +43,12 @@ def main():
     dw = torch.zeros(64, 7, 8, 4, device="cuda")
     res = {("fwd+s", t): [] for t in TILES}
     res.update({("wgrad", w): [] for w in WTILES})
+    res.update({("wg+bn", w): [] for w in WTILES})
+    # the training form: the BN backward of dy fused into the wgrad's operand staging (dtm_conv_wgrad_bnbwd)
+    dss = torch.randn(4, 64, device="cuda") * 1e-3
+    ss = torch.cat([torch.rand(1, 64, device="cuda") + 0.5, torch.randn(3, 64, device="cuda")]).contiguous()
+    gamma = torch.rand(64, device="cuda") + 0.5
+    dg, db = torch.zeros(64, device="cuda"), torch.zeros(64, device="cuda")
     for _ in range(ROUNDS):
         for t in TILES:
             L.dtm_conv_set_tile(t)
@@ -55,6 +61,9 @@ def main():
             L.dtm_conv_set_wgrad_tile(int(i), int(o or 0))
             res[("wgrad", w)].append(timed(lambda: L.dtm_conv_wgrad(_lib.ptr(xp), _lib.ptr(dy), _lib.ptr(dw), None,
                                                                      None, ctypes.byref(d), _lib.num_cus(), st)))
+            res[("wg+bn", w)].append(timed(lambda: L.dtm_conv_wgrad_bnbwd(
+                _lib.ptr(xp), _lib.ptr(dy), _lib.ptr(y), _lib.ptr(dss), _lib.ptr(ss), _lib.ptr(gamma), float(B * P * Q),
+                _lib.ptr(dg), _lib.ptr(db), _lib.ptr(dw), ctypes.byref(d), _lib.num_cus(), st)))
         L.dtm_conv_set_wgrad_tile(-1, 4)
     for (p, t), v in res.items():
         print("stem %-6s %-6s %8.1f us" % (p, t, statistics.median(v)), flush=True)
