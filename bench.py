@@ -108,10 +108,9 @@ def main():
         # captured step, Inception-v3 +0.5 % (885 launches per step), VGG-16 +0.2 %; ResNet-50 is
         # GPU-bound (+0.1 %, within noise) and stays eager
         args.graph = int(args.model in ("lenet", "inception_v3_slim_old", "vgg_16") and world == 1 and not cpu)
-    if args.graph and world > 1:
-        print("bench.py: --graph 1 is single-rank only (hipGraph capture of RCCL collectives is not "
-              "supported here); use --graph 0 or -1 with --gpus %d" % world, file=sys.stderr, flush=True)
-        sys.exit(2)
+    # --graph 1 with several ranks: the step is captured WITH its RCCL bucket all-reduces and BN-statistics sync
+    # (TrainStep graph_comm; bit-identical to eager at world 1, tests/test_distributed.py::
+    # test_bsp_rccl_captured_step_matches_eager).  Opt-in: the auto policy keeps multi-rank steps eager.
     torch.manual_seed(1234)  # identical replicas: every rank builds the same initial weights
     S0, ncls, B0, opt, extra = PRESETS[args.model]
     if args.wgrad_stream >= 0:
@@ -130,6 +129,7 @@ def main():
     # update math at 1..8 GPUs, and no early divergence of a random-init net at lr 0.8 on random labels
     step = TrainStep(net, optimizer=opt, lr=0.1 if opt == "momentum" else 0.01, momentum=0.9,
                      bucket_mb=args.bucket_mb, use_graph=bool(args.graph),
+                     graph_comm=bool(args.graph) and world > 1,
                      grad_comm_dtype=torch.bfloat16 if args.grad_comm == "bf16" else None, **extra)
     cin = 1 if args.model == "lenet" else 3
     images = torch.randn(B, S, S, cin, device=dev).to(torch.float32 if cpu else torch.bfloat16)

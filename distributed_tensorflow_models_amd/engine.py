@@ -83,7 +83,7 @@ class TrainStep:
                  label_smoothing=0.0, aux_weight=0.4, ema_decay=None, lr_schedule=None, use_graph=False,
                  process_group=None, weight_decay=None, batch_weight=1.0, nan_guard=True, timer=None,
                  grad_comm_dtype=None, ema_buffers=True, bn_sync_every=1, wgrad_stream=None, bsp_check=None,
-                 overlap=True, force_comm=False):
+                 overlap=True, force_comm=False, graph_comm=False):
         self.model = model
         if wgrad_stream is not None:
             # conv+BN weight gradients on the side stream (ops/_lib.py side_stream; process-wide): ResNet-50
@@ -96,12 +96,13 @@ class TrainStep:
         # force_comm: issue the collectives even with one rank (tests of the RCCL path on a one-GPU box)
         self.dp = BSPDataParallel(params, bucket_mb, process_group, comm_dtype=grad_comm_dtype, overlap=overlap,
                                   check=bsp_check, names=list(model.named_parameters()), force_comm=force_comm)
-        if use_graph and self.dp.comm_on:
-            # a captured step would hold the bucket collectives (and their waits) inside the graph;
-            # RCCL-in-hipGraph has never been validated here, so runs that issue collectives (world > 1, or
-            # force_comm at world 1) stay eager
-            raise ValueError("use_graph (hipGraph step capture) is only for steps without collectives; world size %d, "
-                             "force_comm %s" % (self.dp.world, bool(force_comm)))
+        if use_graph and self.dp.comm_on and not graph_comm:
+            # a captured step holds the bucket all-reduces, the BN-statistics sync and their waits inside the graph
+            # (RCCL collectives captured on the current stream, replayed every step): opt in with graph_comm=True -
+            # validated bit-identical to the eager step at world 1 over RCCL
+            # (tests/test_distributed.py::test_bsp_rccl_captured_step_matches_eager)
+            raise ValueError("use_graph (hipGraph step capture) is only for steps without collectives unless "
+                             "graph_comm=True; world size %d, force_comm %s" % (self.dp.world, bool(force_comm)))
         # BN moving statistics: one flat buffer, averaged over the replicas every step (reference
         # keeps ONE PS-resident copy that every worker updates); must precede the optimizer tables
         bufs = moving_average_buffers(model)

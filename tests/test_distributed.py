@@ -638,7 +638,7 @@ def _graph_refusal_worker(rank, world):
     try:
         TrainStep(model, optimizer="sgd", lr=0.01, use_graph=True)
     except ValueError as e:
-        return {"refused": "without collectives" in str(e)}
+        return {"refused": "without collectives unless graph_comm" in str(e)}
     return {"refused": False}
 
 
@@ -722,6 +722,56 @@ def _rccl_single_rank_worker(rank, world):
                        "ms": step.dp.bucket_ms(), "bn_flat": step.bufsync.numel()}
         step.dp.close()
     return out
+
+
+def _rccl_graph_worker(rank, world):
+    """One rank over RCCL with every collective forced on (bucket all-reduces from the backward hooks, the BN-statistics
+    sync): the eager step vs the step captured in a hipGraph WITH those collectives inside (graph_comm=True) and
+    replayed - 2 eager warm-up steps, then the capture and 3 replays."""
+    import sys
+
+    import torch.distributed as dist
+
+    from distributed_tensorflow_models_amd.engine import TrainStep, moving_average_buffers
+    from distributed_tensorflow_models_amd.models import nets_factory
+    from distributed_tensorflow_models_amd.ops import _lib
+    assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+    dev = torch.device("cuda", 0)
+    _lib.set_deterministic(True)
+    out = {}
+    try:
+        for graph in (False, True):
+            print("rccl graph worker: graph %s" % graph, file=sys.stderr, flush=True)
+            torch.manual_seed(0)
+            model = nets_factory.build("resnet_v1_50", num_classes=16).to(dev)
+            step = TrainStep(model, optimizer="momentum", lr=0.05, momentum=0.9, bucket_mb=2.0, force_comm=True,
+                             use_graph=graph, graph_comm=True)
+            g = torch.Generator().manual_seed(5)
+            xs = [torch.randn(8, 64, 64, 3, generator=g).to(dev, torch.bfloat16) for _ in range(2)]
+            ys = [torch.randint(0, 16, (8,), generator=g).to(dev) for _ in range(2)]
+            losses = []
+            for i in range(5):
+                losses.append(float(step(xs[i % 2], ys[i % 2])))
+                print("rccl graph worker: step %d" % i, file=sys.stderr, flush=True)
+            torch.cuda.synchronize()
+            out[graph] = {"params": torch.cat([p.detach().float().reshape(-1) for p in model.parameters()]).cpu(),
+                          "bufs": torch.cat([b.detach().reshape(-1) for b in moving_average_buffers(model)]).cpu(),
+                          "losses": losses, "captured": step._graph is not None}
+            step.dp.close()
+    finally:
+        _lib.set_deterministic(False)
+    return out
+
+
+@pytest.mark.gpu
+def test_bsp_rccl_captured_step_matches_eager():
+    """RCCL collectives inside a captured hipGraph step (graph_comm=True): at world 1 with every collective forced on,
+    the captured-and-replayed steps are bit-identical to the eager ones (losses, parameters, BN moving statistics)."""
+    res = run_workers(_rccl_graph_worker, 1, backend="nccl")[0]
+    eager, graph = res[False], res[True]
+    assert graph["captured"] and not eager["captured"]
+    assert eager["losses"] == graph["losses"], (eager["losses"], graph["losses"])
+    assert torch.equal(eager["params"], graph["params"]) and torch.equal(eager["bufs"], graph["bufs"])
 
 
 @pytest.mark.gpu
