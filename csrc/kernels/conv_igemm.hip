@@ -176,7 +176,8 @@ __device__ __forceinline__ void epi_barrier() {
 // SPL: the merged-sibling split store (ConvNTArgs::split) - a separate instantiation, so the kernels without it
 // carry no per-chunk branch or split-table kernel arguments in their store loop (measured +3.6 % ResNet-50 step
 // when it was a runtime branch in every kernel: profiles/r4/README.md).
-template <int PT, int CT, bool RAWB, bool EXACT, bool SACC, int NT, bool SIDE = true, bool PRE = false, bool SPL = false>
+template <int PT, int CT, bool RAWB, bool EXACT, bool SACC, int NT, bool SIDE = true, bool PRE = false, bool SPL = false,
+          int EG = 4>
 __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem, int p0, int c0, int by,
                                                  float* ssum, float* ssq, const char* pre = nullptr,
                                                  const float* pre_ss = nullptr, float* aacc = nullptr) {
@@ -209,7 +210,7 @@ __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem
   }
   // side inputs of the dgrad post-ops (add_src, act_x, act_r, mask bytes) are loaded for a group of
   // GRP rows before any of them is used, so their latencies overlap instead of serialising per row
-  constexpr int GRP = NIT < 4 ? NIT : 4;
+  constexpr int GRP = NIT < EG ? NIT : EG;  // (EG: rows whose side inputs are in flight together - registers)
   static_assert(NIT % GRP == 0, "epilogue row groups");
   const bool side = SIDE && (a.add_src != nullptr || act);
 #pragma unroll
@@ -383,7 +384,7 @@ __device__ __forceinline__ void conv_nt_epi_tail(const ConvNTArgs& a, char* smem
 }
 
 template <int PT, int CT, int WP, int WC, int STG, bool RAWB = false, bool EXACT = false, bool NOBIAS = false,
-          bool SACC = false, int NT = 256, bool SIDE = true, bool PRE = false, bool SPL = false>
+          bool SACC = false, int NT = 256, bool SIDE = true, bool PRE = false, bool SPL = false, int EG = 4>
 __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&acc)[WC / 16][WP / 16], char* smem,
                                                  int p0, int c0, int by, float* ssum = nullptr,
                                                  float* ssq = nullptr, const char* pre = nullptr,
@@ -452,11 +453,14 @@ __device__ __forceinline__ void conv_nt_epilogue(const ConvNTArgs& a, f32x4 (&ac
     }
   }
   if constexpr (staged)
-    conv_nt_epi_tail<PT, CT, RAWB, EXACT, SACC, NT, SIDE, PRE, SPL>(a, smem, p0, c0, by, ssum, ssq, pre, pre_ss, aacc);
+    conv_nt_epi_tail<PT, CT, RAWB, EXACT, SACC, NT, SIDE, PRE, SPL, EG>(a, smem, p0, c0, by, ssum, ssq, pre, pre_ss,
+                                                                        aacc);
 }
 
-template <int PT, int CT, int WP, int WC, int UD, int NBUF, bool SPL = false>
-__global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
+// LBW: minimum waves per SIMD the register allocation must allow (__launch_bounds__; 0 = none), EG: epilogue side-input
+// row group - the occupancy variants of the register-staged dgrads with post-ops (A/B knob dtm_conv_set_act_occ)
+template <int PT, int CT, int WP, int WC, int UD, int NBUF, bool SPL = false, int LBW = 0, int EG = 4>
+__global__ __launch_bounds__(256, LBW > 0 ? LBW : 1) void conv_nt_kernel(ConvNTArgs a) {
   constexpr int BK = 64;
   constexpr int NWP = PT / WP;
   constexpr int NWC = CT / WC;
@@ -645,7 +649,8 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(ConvNTArgs a) {
 
   static_assert(PT * (CT * 2 + 16) <= NBUF * BUF, "output staging fits in the operand buffers");
   if ((a.K & 7) == 0)
-    conv_nt_epilogue<PT, CT, WP, WC, 1, false, false, false, false, 256, true, false, SPL>(a, acc, smem, p0, c0, by);
+    conv_nt_epilogue<PT, CT, WP, WC, 1, false, false, false, false, 256, true, false, SPL, EG>(a, acc, smem, p0, c0,
+                                                                                             by);
   else conv_nt_epilogue<PT, CT, WP, WC, 2>(a, acc, smem, p0, c0, by);
 }
 
@@ -2545,10 +2550,30 @@ static bool stream_ok(const ConvNTArgs& a) {
          (!a.in_scale || a.C <= 512) && a.dump != nullptr && a.ostr == 1;
 }
 
-template <int PT, int CT, int WP, int WC, int UD, int NBUF = 2, bool SPL = false>
+template <int PT, int CT, int WP, int WC, int UD, int NBUF = 2, bool SPL = false, int LBW = 0, int EG = 4>
 static void launch_nt(const ConvNTArgs& a, hipStream_t st) {
   dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT, a.ngrp > 1 ? a.ngrp : 1);
-  hipLaunchKernelGGL((conv_nt_kernel<PT, CT, WP, WC, UD, NBUF, SPL>), grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((conv_nt_kernel<PT, CT, WP, WC, UD, NBUF, SPL, LBW, EG>), grid, dim3(256), 0, st, a);
+}
+// Occupancy variants of the register-staged 64x128 / 128x64 tiles (A/B knobs; DTM_ACT_OCC / DTM_NT_OCC set the initial
+// values): 0 = as compiled (128 VGPR + 32 AGPR: 3 waves/SIMD), 1 = epilogue side rows 2 at a time, 2 = 4 waves/SIMD
+// forced (__launch_bounds__(256, 4): 128 registers, no spill), 3 = both.  The memory-bound dgrads with post-ops (the
+// block-output / act dgrads, side inputs) gain from the 4th resident block: 56x56 318.9 -> 268.9 us, 28x28 178.6 ->
+// 158.9, 14x14 111.5 -> 102.0, 7x7 70.2 -> 65.6, ResNet-50 step -0.99 % (profiles/r6/r6_s17_act_occ.log,
+// r6_s17_ab_aocc.log); so do the plain dgrads (28x28 87.4 -> 73.7 us), while forwards with BN statistics lose
+// (56x56 256 -> 64: 111.3 -> 119.0 us, r6_s17_nt_occ.log): g_nt_occ applies to launches without statistics only.
+static int g_act_occ = getenv("DTM_ACT_OCC") ? atoi(getenv("DTM_ACT_OCC")) : 2;
+DTM_API void dtm_conv_set_act_occ(int v) { g_act_occ = v; }
+static int g_nt_occ = getenv("DTM_NT_OCC") ? atoi(getenv("DTM_NT_OCC")) : 2;
+DTM_API void dtm_conv_set_nt_occ(int v) { g_nt_occ = v; }
+template <int PT, int CT, int UD>
+static void launch_nt_act(const ConvNTArgs& a, hipStream_t st) {
+  const bool side = (a.K & 7) == 0 && (a.add_src != nullptr || a.act_x != nullptr);
+  const int v = side ? g_act_occ : (a.stats ? 0 : g_nt_occ);
+  if (v == 1) launch_nt<PT, CT, 32, 64, UD, 1, false, 0, 2>(a, st);
+  else if (v == 2) launch_nt<PT, CT, 32, 64, UD, 1, false, 4, 4>(a, st);
+  else if (v == 3) launch_nt<PT, CT, 32, 64, UD, 1, false, 4, 2>(a, st);
+  else launch_nt<PT, CT, 32, 64, UD, 1>(a, st);
 }
 
 // tile variants (the ones the shape policy uses; the rejected ones and their A/B logs are listed in
@@ -2745,8 +2770,8 @@ static void dispatch_split(const ConvNTArgs& a, const TileCfg& t, hipStream_t st
 template <int UD>
 static void dispatch_ud(const ConvNTArgs& a, const TileCfg& t, hipStream_t st) {
   if (UD == 1 && a.nsplit > 0) dispatch_split(a, t, st);
-  else if (t.id == 3) launch_nt<128, 64, 32, 64, UD, 1>(a, st);
-  else if (t.id == 4) launch_nt<64, 128, 32, 64, UD, 1>(a, st);
+  else if (t.id == 3) launch_nt_act<128, 64, UD>(a, st);
+  else if (t.id == 4) launch_nt_act<64, 128, UD>(a, st);
   else if (t.id == 30 && UD == 1) {
     if (a.Kg <= 64) launch_stream<128, 1>(a, st);
     else launch_stream<128, 2>(a, st);

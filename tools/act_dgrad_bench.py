@@ -16,6 +16,9 @@ from distributed_tensorflow_models_amd.ops.geometry import conv_geom  # noqa: E4
 
 B = int(os.environ.get("B", "256"))
 TILES = [int(t) for t in os.environ.get("TILES", "-1,4,40,21,24").split(",")]
+# optional knob sweep: KNOB=<dtm_* setter> VALUES=a,b,...: every tile is timed under every value
+KNOB = os.environ.get("KNOB")
+VALUES = [int(v) for v in os.environ.get("VALUES", "0").split(",")]
 # forward conv1 shapes (H, C = block width, K = bottleneck width): its dgrad writes the C-channel block gradient
 SHAPES = [(56, 256, 64), (28, 512, 128), (14, 1024, 256), (7, 2048, 512)]
 
@@ -34,7 +37,9 @@ def timed(fn, n=10):
 def main():
     L = _lib.lib()
     st = _lib.stream_ptr()
-    print("%-18s %8s " % ("shape", "floor") + " ".join("%8s" % ("t%d" % t) for t in TILES))
+    knob = getattr(L, KNOB) if KNOB else (lambda v: None)
+    cols = [(t, v) for t in TILES for v in VALUES]
+    print("%-18s %8s " % ("shape", "floor") + " ".join("%8s" % ("t%dv%d" % c) for c in cols))
     for (H, C, K) in SHAPES:
         x = torch.randn(B, H, H, C, device="cuda").to(torch.bfloat16)
         w = (torch.randn(K, 1, 1, C, device="cuda") * 0.05).to(torch.bfloat16)
@@ -50,14 +55,16 @@ def main():
         nbytes = dy.numel() * 2 + 3 * x.numel() * 2 + mask.numel()
         fn = lambda: L.dtm_conv_dgrad_bnout(_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), ctypes.byref(d),  # noqa: E731
                                             _lib.ptr(add), 1, _lib.ptr(mask), _lib.ptr(x), None, _lib.ptr(sums), st)
-        res = {t: [] for t in TILES}
+        res = {c: [] for c in cols}
         for _ in range(int(os.environ.get("ROUNDS", "3"))):
-            for t in TILES:
-                L.dtm_conv_set_tile(t)
-                res[t].append(timed(fn))
+            for c in cols:
+                L.dtm_conv_set_tile(c[0])
+                knob(c[1])
+                res[c].append(timed(fn))
         L.dtm_conv_set_tile(-1)
+        knob(VALUES[0])
         print("H%-2d C%-4d K%-4d    %8.1f " % (H, C, K, nbytes / 5.5e12 * 1e6) +
-              " ".join("%8.1f" % statistics.median(res[t]) for t in TILES), flush=True)
+              " ".join("%8.1f" % statistics.median(res[c]) for c in cols), flush=True)
 
 
 if __name__ == "__main__":
