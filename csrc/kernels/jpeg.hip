@@ -178,6 +178,355 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(const JpegDesc* __restr
   }
 }
 
+
+// ---- entropy (Huffman) decode ----------------------------------------------------------------------------
+// One workgroup per image decodes the unstuffed entropy-coded bytes (host: dtm_jpeg_scan, csrc/runtime/jpeg.cpp)
+// into the zeroed [comp][bh][bw][64] int16 coefficient layout jpeg_idct_kernel reads - exactly what the host
+// decoder (decode_scan) writes.
+//  * restart interval > 0: every restart segment is an independent run with a known start (MCU s * RI, block 0,
+//    coefficient 0, DC predictors 0): thread t decodes segments t, t + 256, ...
+//  * no restart markers (the common case): the bit stream is cut into 256 subsequences of L bits.  Thread t decodes
+//    from a start state S_t = (bit, block-in-MCU, coefficient) to the first codeword boundary past its end, giving
+//    the exit state E_t, its block count and per-component DC-difference sums.  S_0 is exact; S_t starts as a guess
+//    (bit t * L, block 0, coefficient 0) and is replaced by E_{t-1} until nothing changes - a fixed point that is
+//    exact by induction (after pass j the first j + 1 starts are), and in practice reached in 2-3 passes because a
+//    Huffman decode started at a wrong bit falls back into step with the true one within a few codewords.  Scans of
+//    the counts and DC sums then place every thread's blocks and DC predictors, and a last pass writes them.
+// Tables: each of the image's (<= 4) DHT tables becomes an 11-bit lookup in LDS (code length + symbol, or for
+// short codes the code + magnitude bits -> the value, run and total length in one entry; the host decoder's
+// fast_ac), longer codes walk the canonical maxcode table.
+
+// mirror of csrc/runtime/jpeg.cpp JpegScan
+struct JpegScan {
+  int nbytes, nseg, restart;
+  int ncomp, bpm, mcux, nmcu, nslot;
+  int bcomp[12], bdy[12], bdx[12];
+  int h[3], v[3], bw[3], coef_off[3];
+  int dc_slot[3], ac_slot[3];
+  int slot_dc[4];
+  unsigned char counts[4][16];
+  unsigned char vals[4][256];
+};
+
+// one image of the batch (mirrored in data/jpeg.py HUFF_DESC_DT)
+struct HuffDesc {
+  long long stream_off;  // byte offset (4-aligned) of the image's unstuffed bytes in the batch stream buffer
+  long long coef_base;   // int16 offset of its coefficients (JpegDesc.coef_base)
+  int coef_count;        // int16 coefficients of the image (zeroed here first)
+  int seg_off;           // its first restart segment in the batch segment table
+  int min_bits;          // floor of the subsequence length L (0: 1024)
+  int overlap;           // warm-up bits decoded before a subsequence to guess its start state (< 0: none, 0: L / 2)
+  JpegScan s;
+};
+
+constexpr int HT = 256, LOOK = 11;
+// lookup entry, one per 11-bit prefix (0: a code longer than 11 bits - huff_slow_entry builds the same form):
+//   bits 0-4   code length, or code + magnitude bits of a value entry
+//   bit 5      value entry: bits 16-31 hold the signed coefficient (code + magnitude fit the 11 bits)
+//   bit 6      the symbol places a coefficient (a DC difference, or an AC value of size > 0)
+//   bit 7      invalid (no such code / DC category > 15): 1 bit is skipped, an AC block ends
+//   bits 8-14  coefficient-index advance: run + 1 for a placed value (DC: 1), 16 for ZRL, 64 for EOB
+//   bits 16-19 magnitude bit count of a symbol (non-value) entry
+// so DC and AC symbols take one branch-light path.
+constexpr unsigned HE_VAL = 32u, HE_PUT = 64u, HE_BAD = 128u;
+
+struct HuffLds {
+  unsigned lut[4][1 << LOOK];
+  int maxcode[4][18];
+  int valoff[4][17];
+  unsigned char vals[4][256];
+  unsigned char zz[64];
+  int bcomp[12], bdy[12], bdx[12], dcs[3], acs[3];
+  int bctx[12];  // component | DC slot << 4 | AC slot << 8 of the b-th block of an MCU
+  int ep[HT], eb[HT], ek[HT], cnt[HT], ds[3][HT];
+  int flag[3], err, passes;
+};
+
+__constant__ unsigned char c_zigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                                           12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                                           35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                                           58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+__device__ __forceinline__ int hextend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
+
+// entry for symbol `sym` of code length len (dc: a DC table); bits: the 11-bit prefix (value entries read the
+// magnitude bits that follow the code in it), or -1 (longer codes: no value entry)
+__device__ __forceinline__ unsigned huff_entry(int len, int sym, bool dc, int bits) {
+  if (dc && sym > 15) return 1u | HE_BAD;  // (advance 0: the DC is retried one bit later)
+  const int run = dc ? 0 : sym >> 4, size = dc ? sym : sym & 15;
+  if (!dc && !size) return (unsigned)len | ((run == 15 ? 16u : 64u) << 8);  // ZRL / EOB
+  const unsigned adv = (unsigned)(run + 1) << 8;
+  if (bits >= 0 && len + size <= LOOK) {
+    const int v = size ? hextend((bits >> (LOOK - len - size)) & ((1 << size) - 1), size) : 0;
+    return (unsigned)(len + size) | HE_VAL | HE_PUT | adv | ((unsigned)v << 16);
+  }
+  return (unsigned)len | HE_PUT | adv | ((unsigned)size << 16);
+}
+
+// a code longer than LOOK bits (canonical maxcode walk over the next 16 bits)
+__device__ __forceinline__ unsigned huff_slow_entry(const HuffLds& L, int slot, unsigned code16, bool dc) {
+  int m[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) m[i] = L.maxcode[slot][LOOK + 1 + i];
+  int l = 0, c = 0;
+#pragma unroll
+  for (int i = 4; i >= 0; --i) {  // the shortest matching length wins
+    const int ci = (int)(code16 >> (16 - (LOOK + 1 + i)));
+    if (ci <= m[i]) {
+      l = LOOK + 1 + i;
+      c = ci;
+    }
+  }
+  if (!l) return 1u | HE_BAD | (dc ? 0u : 64u << 8);
+  return huff_entry(l, L.vals[slot][(c + L.valoff[slot][l]) & 255], dc, -1);
+}
+
+// MSB-first bit reader over big-endian 32-bit words; one word is always in flight (nxt) so a refill never waits on
+// memory
+struct BitReader {
+  const unsigned* w;
+  unsigned long long buf;
+  int nb, wi, p;
+  unsigned nxt;
+  __device__ __forceinline__ void init(const unsigned* words, int pos) {
+    w = words;
+    wi = pos >> 5;
+    const unsigned long long hi = __builtin_bswap32(w[wi]), lo = __builtin_bswap32(w[wi + 1]);
+    buf = ((hi << 32) | lo) << (pos & 31);
+    nb = 64 - (pos & 31);
+    wi += 2;
+    nxt = w[wi];  // (raw: swapped when used, so nothing waits for the load before the next refill)
+    p = pos;
+  }
+  __device__ __forceinline__ void fill() {
+    if (nb < 32) {
+      buf |= (unsigned long long)__builtin_bswap32(nxt) << (32 - nb);
+      nb += 32;
+      nxt = w[++wi];
+    }
+  }
+  __device__ __forceinline__ unsigned peek(int n) const { return (unsigned)(buf >> (64 - n)); }
+  __device__ __forceinline__ void skip(int n) { buf <<= n; nb -= n; p += n; }
+};
+
+struct HuffState {
+  int p, b, k;
+};
+
+__device__ __forceinline__ short* block_at(const HuffLds& L, const JpegScan& s, short* img, int g) {
+  const int mcu = g / s.bpm, bb = g - mcu * s.bpm, my = mcu / s.mcux, mx = mcu - my * s.mcux, c = L.bcomp[bb];
+  return img + s.coef_off[c] + ((long long)(my * s.v[c] + L.bdy[bb]) * s.bw[c] + mx * s.h[c] + L.bdx[bb]) * 64;
+}
+
+// Decode from st until the first codeword boundary at or past `stop` (or, with gstop >= 0, until block gstop would
+// start).  OUT = false: count blocks started (DC symbols) and sum the DC differences per component into acc.
+// OUT = true: write the coefficients of blocks g < total (g: the block being decoded; acc: the DC predictors).
+// A decode error in a block < total sets err (chains started from a wrong guess may hit them; only the exact,
+// final pass reports).  Every iteration consumes >= 1 bit.
+template <bool OUT>
+__device__ void huff_run(const HuffLds& L, const JpegScan& s, const unsigned* words, HuffState& st, int stop,
+                         int gstop, int total, int& g, int* acc, int& nblk, int& err, short* img) {
+  BitReader br;
+  br.init(words, st.p);
+  int b = st.b, k = st.k;
+  short* blk = nullptr;
+  if (OUT && k > 0 && g < total) blk = block_at(L, s, img, g);
+  int ctx = L.bctx[b];  // this block's component and table slots (re-read once per block)
+  while (br.p < stop) {
+    if (gstop >= 0 && k == 0 && g >= gstop) break;
+    br.fill();
+    const int c = ctx & 15;
+    const int slot = k == 0 ? (ctx >> 4) & 15 : ctx >> 8;
+    unsigned e = L.lut[slot][br.peek(LOOK)];
+    if (!e) e = huff_slow_entry(L, slot, br.peek(16), k == 0);
+    const int size = (e & HE_VAL) ? 0 : (e >> 16) & 15;
+    const int used = (e & 31) + size;
+    int val = (e & HE_VAL) ? (int)e >> 16 : (size ? hextend((int)(br.peek(used) & ((1u << size) - 1)), size) : 0);
+    br.skip(used);
+    const int adv = (e >> 8) & 127;
+    if ((e & HE_BAD) && (!OUT || g < total)) err = 1;
+    if (e & HE_PUT) {
+      const int pos = k + adv - 1;
+      if (k == 0) {
+        acc[c] += val;
+        val = acc[c];
+        if (!OUT) ++nblk;
+        else if (g < total) blk = block_at(L, s, img, g);
+      }
+      if (pos > 63) {
+        if (!OUT || g < total) err = 1;
+        k = 64;
+      } else {
+        if (OUT && g < total) blk[L.zz[pos]] = (short)val;
+        k = pos + 1;
+      }
+    } else {
+      k += adv;
+    }
+    if (k >= 64) {
+      k = 0;
+      b = b + 1 == s.bpm ? 0 : b + 1;
+      ctx = L.bctx[b];
+      if (OUT) ++g;
+    }
+  }
+  st.p = br.p;
+  st.b = b;
+  st.k = k;
+}
+
+__device__ __forceinline__ int block_scan_excl(int* a, int v) {  // exclusive prefix sum over the HT threads
+  const int t = threadIdx.x;
+  a[t] = v;
+  __syncthreads();
+  for (int o = 1; o < HT; o <<= 1) {
+    const int x = t >= o ? a[t - o] : 0;
+    __syncthreads();
+    a[t] += x;
+    __syncthreads();
+  }
+  const int r = a[t] - v;
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(HT) void jpeg_huff_kernel(const unsigned char* __restrict__ stream,
+                                                       const int* __restrict__ segs, const HuffDesc* __restrict__ descs,
+                                                       short* __restrict__ coefs, int* __restrict__ status) {
+  __shared__ HuffLds L;
+  const HuffDesc& d = descs[blockIdx.x];
+  const JpegScan& s = d.s;
+  const int t = threadIdx.x;
+  short* img = coefs + d.coef_base;
+  // zero the image's coefficients (blocks only get their nonzero entries written)
+  {
+    uint4* z = (uint4*)img;  // (coef_base and every image's capacity are 8-int16 aligned)
+    for (int i = t; i < (d.coef_count + 7) / 8; i += HT) z[i] = make_uint4(0, 0, 0, 0);
+  }
+  // tables
+  if (t < s.nslot) {
+    int code = 0, kk = 0;
+    for (int len = 1; len <= 16; ++len) {
+      const int n = s.counts[t][len - 1];
+      L.valoff[t][len] = kk - code;
+      code += n;
+      kk += n;
+      L.maxcode[t][len] = n ? code - 1 : -1;
+      code <<= 1;
+    }
+    L.maxcode[t][17] = 0x7fffffff;
+  }
+  for (int i = t; i < 4 * 256; i += HT) (&L.vals[0][0])[i] = (&s.vals[0][0])[i];
+  if (t < 64) L.zz[t] = c_zigzag[t];
+  if (t < 12) {
+    L.bcomp[t] = s.bcomp[t];
+    L.bdy[t] = s.bdy[t];
+    L.bdx[t] = s.bdx[t];
+  }
+  if (t < 3) {
+    L.dcs[t] = s.dc_slot[t];
+    L.acs[t] = s.ac_slot[t];
+  }
+  if (t < 12) {
+    const int c = s.bcomp[t];
+    L.bctx[t] = c | (s.dc_slot[c] << 4) | (s.ac_slot[c] << 8);
+  }
+  if (t == 0) {
+    L.err = 0;
+    L.flag[0] = L.flag[1] = L.flag[2] = 0;
+  }
+  __syncthreads();
+  for (int i = t; i < s.nslot << LOOK; i += HT) {
+    const int slot = i >> LOOK, f = i & ((1 << LOOK) - 1);
+    unsigned e = 0;
+    for (int len = 1; len <= LOOK; ++len) {
+      const int code = f >> (LOOK - len);
+      if (code <= L.maxcode[slot][len]) {
+        e = huff_entry(len, L.vals[slot][(code + L.valoff[slot][len]) & 255], s.slot_dc[slot] != 0, f);
+        break;
+      }
+    }
+    L.lut[slot][f] = e;
+  }
+  __threadfence_block();
+  __syncthreads();
+
+  const unsigned* words = (const unsigned*)(stream + d.stream_off);
+  const int nbits = s.nbytes * 8, total = s.nmcu * s.bpm;
+  int err = 0;
+  if (s.restart > 0) {
+    // independent restart segments
+    const int per = s.restart * s.bpm;
+    for (int sg = t; sg < s.nseg; sg += HT) {
+      HuffState st{segs[d.seg_off + sg] * 8, 0, 0};
+      int g = sg * per, nb = 0, pred[3] = {0, 0, 0};
+      const int gstop = min(g + per, total);
+      huff_run<true>(L, s, words, st, nbits + 64, gstop, total, g, pred, nb, err, img);
+      if (g < gstop) err = 1;  // ran out of data
+    }
+    if (t == 0) L.passes = 0;
+  } else {
+    int Lb = d.min_bits > 0 ? d.min_bits : 1024;
+    Lb = max(Lb, (nbits + HT - 1) / HT);
+    Lb = (Lb + 31) & ~31;
+    const int nact = (nbits + Lb - 1) / Lb;
+    const int stop = min((t + 1) * Lb, nbits);
+    HuffState st{t * Lb, 0, 0};
+    const int ov = d.overlap == 0 ? Lb / 2 : d.overlap;
+    if (t > 0 && t < nact && ov > 0) {
+      // warm-up: decode from a guess `ov` bits earlier; the state it reaches at t * L is most often already exact
+      // (the decode has fallen into step), so most subsequences need no second pass
+      HuffState w{max(0, t * Lb - ov), 0, 0};
+      int g = 0, nb = 0, e2 = 0, acc[3] = {0, 0, 0};
+      huff_run<false>(L, s, words, w, t * Lb, -1, total, g, acc, nb, e2, img);
+      st = w;
+    }
+    bool dirty = t < nact;
+    int pass = 0;
+    for (; pass <= HT; ++pass) {
+      if (dirty) {
+        HuffState e = st;
+        int g = 0, nb = 0, e2 = 0, acc[3] = {0, 0, 0};
+        huff_run<false>(L, s, words, e, stop, -1, total, g, acc, nb, e2, img);
+        L.ep[t] = e.p;
+        L.eb[t] = e.b;
+        L.ek[t] = e.k;
+        L.cnt[t] = nb;
+        L.ds[0][t] = acc[0];
+        L.ds[1][t] = acc[1];
+        L.ds[2][t] = acc[2];
+      }
+      if (t == 0) L.flag[(pass + 1) % 3] = 0;  // (3 flags: a slow thread may still read the previous pass's)
+      __syncthreads();
+      dirty = false;
+      if (t >= 1 && t < nact && (L.ep[t - 1] != st.p || L.eb[t - 1] != st.b || L.ek[t - 1] != st.k)) {
+        st = HuffState{L.ep[t - 1], L.eb[t - 1], L.ek[t - 1]};
+        dirty = true;
+        L.flag[pass % 3] = 1;
+      }
+      __syncthreads();
+      if (!L.flag[pass % 3]) break;
+    }
+    const bool act = t < nact;
+    const int nb = act ? L.cnt[t] : 0;
+    const int d0 = act ? L.ds[0][t] : 0, d1 = act ? L.ds[1][t] : 0, d2 = act ? L.ds[2][t] : 0;
+    __syncthreads();
+    const int G = block_scan_excl(L.cnt, nb);
+    int pred[3];
+    pred[0] = block_scan_excl(L.ds[0], d0);
+    pred[1] = block_scan_excl(L.ds[1], d1);
+    pred[2] = block_scan_excl(L.ds[2], d2);
+    if (t == HT - 1 && G + nb < total) L.err = 1;  // the stream ended before the last block
+    if (act) {
+      int g = st.k > 0 ? G - 1 : G, unused = 0;
+      huff_run<true>(L, s, words, st, stop, -1, total, g, pred, unused, err, img);
+    }
+    if (t == 0) L.passes = pass + 1;
+  }
+  if (err) L.err = 1;
+  __syncthreads();
+  if (t == 0) status[blockIdx.x] = L.err ? -1 : L.passes;
+}
 }  // namespace dtm
 using namespace dtm;
 
@@ -195,5 +544,19 @@ DTM_API int dtm_jpeg_decode_gpu(const void* coefs, const void* descs, int n, int
   if (gx > 0x7fffffff) return -1;
   hipLaunchKernelGGL(jpeg_color_kernel, dim3((unsigned)gx, n), dim3(256), 0, (hipStream_t)stream,
                      (const JpegDesc*)descs, (const unsigned char*)planes, (unsigned char*)rgb);
+  return 0;
+}
+
+DTM_API int dtm_jpeg_huff_desc_bytes() { return (int)sizeof(HuffDesc); }
+
+// Entropy-decode a batch: stream = the images' unstuffed bytes (each 4-aligned, 32 zero bytes after), segs = the
+// restart segment table, descs = device [n] HuffDesc.  coefs receives every image's zero-filled coefficients;
+// status[i] = passes of the subsequence fixed point (0: restart segments), -1: the image's data is corrupt.
+DTM_API int dtm_jpeg_huff_gpu(const void* stream, const void* segs, const void* descs, int n, void* coefs,
+                              void* status, void* st) {
+  if (n <= 0) return 0;
+  if (n > 0x7fffffff / HT) return -1;
+  hipLaunchKernelGGL(jpeg_huff_kernel, dim3(n), dim3(HT), 0, (hipStream_t)st, (const unsigned char*)stream,
+                     (const int*)segs, (const HuffDesc*)descs, (short*)coefs, (int*)status);
   return 0;
 }

@@ -80,6 +80,25 @@ bool build_huff(Huff& h, const uint8_t* counts, const uint8_t* symbols, int nsym
 
 inline int extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
 
+// a DHT table as transmitted (code-length counts + symbols): what the GPU entropy decoder builds its tables from
+struct RawHuff {
+  bool defined = false;
+  uint8_t counts[16];
+  uint8_t vals[256];
+};
+
+// canonical-code sanity of a DHT table (build_huff's over-subscription check without building anything)
+bool check_huff(const uint8_t* counts, int nsym) {
+  if (nsym > 256) return false;
+  int code = 0;
+  for (int len = 1; len <= 16; ++len) {
+    code += counts[len - 1];
+    if (code > (1 << len)) return false;
+    code <<= 1;
+  }
+  return true;
+}
+
 struct Comp {
   int id, h, v, tq, td, ta;
 };
@@ -226,20 +245,35 @@ __attribute__((noinline)) static int decode_scan(const uint8_t* p, const uint8_t
   return 0;
 }
 
-// Parse + Huffman-decode `data` into `coefs` (int16, natural order, [comp][bh][bw][64]) of capacity
-// `cap` int16.  Returns 0, or: -1 corrupt, -2 unsupported (caller falls back to PIL), -3 capacity too
-// small (info is filled: info->coef_count is the need).
-API int dtm_jpeg_decode(const uint8_t* data, long n, JpegInfo* info, int16_t* coefs, long cap) {
+namespace {
+// Everything the marker parser hands to an entropy decoder: the components and their table selectors, the
+// restart interval, the entropy-coded segment [scan, end) and the tables - built for the host decoder (dc/ac,
+// when asked for) and raw (for the GPU one).
+struct Parsed {
+  Comp comp[3];
+  int ncomp = 0, restart = 0;
+  const uint8_t* scan = nullptr;
+  const uint8_t* end = nullptr;
+  RawHuff rdc[4], rac[4];
+};
+
+// Marker parse up to the (single, interleaved) scan: fills info's layout and ps.  Returns 0, -1 corrupt,
+// -2 unsupported.  dc / ac: host decode tables to build (nullptr: only the raw tables are kept).
+int parse_jpeg(const uint8_t* data, long n, JpegInfo* info, Parsed& ps, Huff* dc, Huff* ac) {
   memset(info, 0, sizeof(*info));
   if (n < 4 || data[0] != 0xFF || data[1] != 0xD8) return -1;
   const uint8_t* p = data + 2;
   const uint8_t* end = data + n;
   uint16_t qtab[4][64];
   bool qdef[4] = {false, false, false, false};
-  static thread_local Huff dc[4], ac[4];
-  for (int i = 0; i < 4; ++i) dc[i].defined = ac[i].defined = false;
-  Comp comp[3];
-  int ncomp = 0, restart_interval = 0;
+  if (dc)
+    for (int i = 0; i < 4; ++i) dc[i].defined = ac[i].defined = false;
+  for (int i = 0; i < 4; ++i) ps.rdc[i].defined = ps.rac[i].defined = false;
+  ps.ncomp = ps.restart = 0;
+  ps.scan = ps.end = nullptr;
+  Comp* comp = ps.comp;
+  int& ncomp = ps.ncomp;
+  int& restart_interval = ps.restart;
   bool have_frame = false;
   while (p + 4 <= end) {
     if (p[0] != 0xFF) return -1;
@@ -286,7 +320,16 @@ API int dtm_jpeg_decode(const uint8_t* data, long n, JpegInfo* info, int16_t* co
           int nsym = 0;
           for (int i = 0; i < 16; ++i) nsym += counts[i];
           if (seg + 17 + nsym > segend) return -1;
-          if (!build_huff(tc ? ac[th] : dc[th], counts, seg + 17, nsym)) return -1;
+          if (dc) {
+            if (!build_huff(tc ? ac[th] : dc[th], counts, seg + 17, nsym)) return -1;
+          } else if (!check_huff(counts, nsym)) {
+            return -1;
+          }
+          RawHuff& r = tc ? ps.rac[th] : ps.rdc[th];
+          memcpy(r.counts, counts, 16);
+          memset(r.vals, 0, sizeof(r.vals));
+          memcpy(r.vals, seg + 17, nsym);
+          r.defined = true;
           seg += 17 + nsym;
         }
         break;
@@ -326,7 +369,7 @@ API int dtm_jpeg_decode(const uint8_t* data, long n, JpegInfo* info, int16_t* co
           if (c != i) return -2;
           comp[c].td = seg[2 + 2 * i] >> 4;
           comp[c].ta = seg[2 + 2 * i] & 15;
-          if (comp[c].td > 3 || comp[c].ta > 3 || !dc[comp[c].td].defined || !ac[comp[c].ta].defined) return -1;
+          if (comp[c].td > 3 || comp[c].ta > 3 || !ps.rdc[comp[c].td].defined || !ps.rac[comp[c].ta].defined) return -1;
         }
         const int ss = seg[1 + 2 * ns], se = seg[2 + 2 * ns], ahal = seg[3 + 2 * ns];
         if (ss != 0 || se != 63 || ahal != 0) return -2;
@@ -356,9 +399,9 @@ API int dtm_jpeg_decode(const uint8_t* data, long n, JpegInfo* info, int16_t* co
         }
         if (total > (1l << 30)) return -2;
         info->coef_count = (int32_t)total;
-        if (total > cap) return -3;
-        // entropy-coded segment
-        return decode_scan(segend, end, info, comp, ncomp, dc, ac, restart_interval, coefs);
+        ps.scan = segend;
+        ps.end = end;
+        return 0;
       }
       default:  // APPn, COM, DNL, ...: skip
         break;
@@ -366,8 +409,130 @@ API int dtm_jpeg_decode(const uint8_t* data, long n, JpegInfo* info, int16_t* co
   }
   return -1;
 }
+}  // namespace
+
+// Parse + Huffman-decode `data` into `coefs` (int16, natural order, [comp][bh][bw][64]) of capacity
+// `cap` int16.  Returns 0, or: -1 corrupt, -2 unsupported (caller falls back to PIL), -3 capacity too
+// small (info is filled: info->coef_count is the need).
+API int dtm_jpeg_decode(const uint8_t* data, long n, JpegInfo* info, int16_t* coefs, long cap) {
+  static thread_local Huff dc[4], ac[4];
+  static thread_local Parsed ps;
+  const int rc = parse_jpeg(data, n, info, ps, dc, ac);
+  if (rc) return rc;
+  if (info->coef_count > cap) return -3;
+  return decode_scan(ps.scan, ps.end, info, ps.comp, ps.ncomp, dc, ac, ps.restart, coefs);
+}
 
 API int dtm_jpeg_info_bytes() { return (int)sizeof(JpegInfo); }
+
+// ---- host share of the GPU entropy decode (csrc/kernels/jpeg.hip jpeg_huff_kernel) ----------------------
+// What the device needs to Huffman-decode one image: the MCU layout, up to 4 distinct tables as transmitted and
+// the restart segments of the unstuffed entropy-coded bytes (mirrored in jpeg.hip JpegScan and data/jpeg.py).
+struct JpegScan {
+  int32_t nbytes;             // unstuffed entropy-coded bytes (0xFF00 -> 0xFF, RSTn removed), 32 zero bytes follow
+  int32_t nseg;               // restart segments (restart interval > 0), else 0
+  int32_t restart;            // restart interval in MCUs (0: none)
+  int32_t ncomp, bpm, mcux, nmcu, nslot;  // blocks per MCU, MCUs per row, MCUs, distinct tables
+  int32_t bcomp[12], bdy[12], bdx[12];    // component of the b-th block of an MCU, its block row / column in the MCU
+  int32_t h[3], v[3], bw[3], coef_off[3];
+  int32_t dc_slot[3], ac_slot[3];         // table slot of each component's DC / AC table
+  int32_t slot_dc[4];                     // 1: the slot holds a DC table
+  uint8_t counts[4][16];
+  uint8_t vals[4][256];
+};
+
+// Marker parse + byte unstuffing of `data` for the GPU entropy decoder: the host work per image is a header walk
+// and a memchr/memcpy pass over the scan (no bit-level work).  `stream` (capacity cap >= n + 32 bytes) receives the
+// unstuffed entropy-coded bytes and 32 zero bytes; `segs` (capacity seg_cap) the byte offset of every restart
+// segment in it.  Returns 0, -1 corrupt, -2 unsupported (the caller decodes on the host / with PIL), -3 capacity
+// (scan->nseg holds the segment need).
+API int dtm_jpeg_scan(const uint8_t* data, long n, JpegInfo* info, JpegScan* scan, uint8_t* stream, long cap,
+                      int32_t* segs, long seg_cap) {
+  static thread_local Parsed ps;
+  memset(scan, 0, sizeof(*scan));
+  const int rc = parse_jpeg(data, n, info, ps, nullptr, nullptr);
+  if (rc) return rc;
+  JpegScan& d = *scan;
+  d.ncomp = info->ncomp;
+  d.mcux = info->mcux;
+  d.nmcu = info->mcux * info->mcuy;
+  d.restart = ps.restart;
+  int bpm = 0;
+  for (int c = 0; c < info->ncomp; ++c) {
+    d.h[c] = info->h[c];
+    d.v[c] = info->v[c];
+    d.bw[c] = info->bw[c];
+    d.coef_off[c] = info->coef_off[c];
+    for (int by = 0; by < info->v[c]; ++by)
+      for (int bx = 0; bx < info->h[c]; ++bx) {
+        if (bpm >= 12) return -2;
+        d.bcomp[bpm] = c;
+        d.bdy[bpm] = by;
+        d.bdx[bpm] = bx;
+        ++bpm;
+      }
+  }
+  d.bpm = bpm;
+  // distinct (class, id) tables -> slots
+  int key[4], ns = 0;
+  auto slot = [&](int cls, int id) -> int {
+    const int k = cls * 4 + id;
+    for (int i = 0; i < ns; ++i)
+      if (key[i] == k) return i;
+    if (ns == 4) return -1;
+    const RawHuff& r = cls ? ps.rac[id] : ps.rdc[id];
+    key[ns] = k;
+    d.slot_dc[ns] = cls ? 0 : 1;
+    memcpy(d.counts[ns], r.counts, 16);
+    memcpy(d.vals[ns], r.vals, 256);
+    return ns++;
+  };
+  for (int c = 0; c < info->ncomp; ++c) {
+    d.dc_slot[c] = slot(0, ps.comp[c].td);
+    d.ac_slot[c] = slot(1, ps.comp[c].ta);
+    if (d.dc_slot[c] < 0 || d.ac_slot[c] < 0) return -2;
+  }
+  d.nslot = ns;
+  const long need_seg = ps.restart ? (d.nmcu + ps.restart - 1) / ps.restart : 0;
+  d.nseg = (int32_t)need_seg;
+  if (cap < (ps.end - ps.scan) + 32 || seg_cap < need_seg || (ps.end - ps.scan) >= (1l << 28)) return -3;
+  // unstuff: 0xFF 0x00 -> 0xFF, fill bytes dropped, RSTn -> a segment boundary, any other marker ends the scan
+  const uint8_t* p = ps.scan;
+  const uint8_t* end = ps.end;
+  uint8_t* o = stream;
+  long nseg = 0;
+  if (ps.restart) segs[nseg++] = 0;
+  while (p < end) {
+    const uint8_t* q = (const uint8_t*)memchr(p, 0xFF, end - p);
+    if (!q) {
+      memcpy(o, p, end - p);
+      o += end - p;
+      break;
+    }
+    memcpy(o, p, q - p);
+    o += q - p;
+    p = q + 1;
+    while (p < end && *p == 0xFF) ++p;
+    if (p >= end) break;
+    if (*p == 0) {
+      *o++ = 0xFF;
+      ++p;
+      continue;
+    }
+    if (ps.restart && *p >= 0xD0 && *p <= 0xD7) {
+      ++p;
+      if (nseg < need_seg) segs[nseg++] = (int32_t)(o - stream);
+      continue;
+    }
+    break;
+  }
+  if (nseg < need_seg) return -1;  // missing restart markers (the host decoder fails such a file the same way)
+  d.nbytes = (int32_t)(o - stream);
+  memset(o, 0, 32);
+  return 0;
+}
+
+API int dtm_jpeg_scan_bytes() { return (int)sizeof(JpegScan); }
 
 // ---- CPU reference of the GPU stage (libjpeg's islow IDCT + fancy upsampling + YCbCr->RGB) ------------
 namespace {

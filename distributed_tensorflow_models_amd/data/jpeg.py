@@ -1,10 +1,14 @@
-"""Split JPEG decoding: host Huffman decode (csrc/runtime/jpeg.cpp) + device IDCT / upsampling / colour
-(csrc/kernels/jpeg.hip), bit-exact with libjpeg(-turbo)'s default decompression (the reference's
-tf.image.decode_jpeg, inception/image_processing.py:339-407, and PIL both use it).
+"""Split JPEG decoding, bit-exact with libjpeg(-turbo)'s default decompression (the reference's
+tf.image.decode_jpeg, inception/image_processing.py:339-407, and PIL both use it).  Two splits:
 
-``huffman_decode(data)`` -> (JpegInfo numpy record, int16 coefficients) or None when the file is outside
-the supported subset (progressive, CMYK, ...: decode those with PIL).  ``pixels_cpu`` is the host form of
-the device stage (the oracle of the HIP kernel); ``decode_batch_gpu`` runs the device stage for a batch.
+* host Huffman (csrc/runtime/jpeg.cpp) + device IDCT / upsampling / colour (csrc/kernels/jpeg.hip):
+  ``huffman_decode(data)`` -> (JpegInfo numpy record, int16 coefficients) or None when the file is outside
+  the supported subset (progressive, CMYK, ...: decode those with PIL).  ``pixels_cpu`` is the host form of
+  the device stage (the oracle of the HIP kernel); ``decode_batch_gpu`` runs the device stage for a batch.
+* everything past the marker parse on the device: ``scan_prep(data)`` walks the markers and unstuffs the
+  entropy-coded bytes on the host (no bit-level work); ``decode_batch_gpu_full`` Huffman-decodes the batch with
+  jpeg_huff_kernel (one workgroup per image, self-synchronising subsequence decode) and runs the same IDCT /
+  colour stage.
 """
 import ctypes
 
@@ -19,6 +23,14 @@ INFO_DT = np.dtype([("width", "<i4"), ("height", "<i4"), ("ncomp", "<i4"), ("hma
 
 UNSUPPORTED, CORRUPT, TOO_SMALL = -2, -1, -3
 
+# mirror of struct JpegScan (csrc/runtime/jpeg.cpp, csrc/kernels/jpeg.hip)
+SCAN_DT = np.dtype([("nbytes", "<i4"), ("nseg", "<i4"), ("restart", "<i4"), ("ncomp", "<i4"), ("bpm", "<i4"),
+                    ("mcux", "<i4"), ("nmcu", "<i4"), ("nslot", "<i4"), ("bcomp", "<i4", 12), ("bdy", "<i4", 12),
+                    ("bdx", "<i4", 12), ("h", "<i4", 3), ("v", "<i4", 3), ("bw", "<i4", 3), ("coef_off", "<i4", 3),
+                    ("dc_slot", "<i4", 3), ("ac_slot", "<i4", 3), ("slot_dc", "<i4", 4), ("counts", "u1", (4, 16)),
+                    ("vals", "u1", (4, 256))])
+STREAM_PAD = 32  # zero bytes after every image's unstuffed stream
+
 
 def _rt():
     L = native.rt()
@@ -29,6 +41,11 @@ def _rt():
         L.dtm_jpeg_pixels.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.dtm_jpeg_info_bytes.restype = ctypes.c_int
         assert L.dtm_jpeg_info_bytes() == INFO_DT.itemsize, (L.dtm_jpeg_info_bytes(), INFO_DT.itemsize)
+        L.dtm_jpeg_scan.restype = ctypes.c_int
+        L.dtm_jpeg_scan.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_long, ctypes.c_void_p, ctypes.c_long]
+        L.dtm_jpeg_scan_bytes.restype = ctypes.c_int
+        assert L.dtm_jpeg_scan_bytes() == SCAN_DT.itemsize, (L.dtm_jpeg_scan_bytes(), SCAN_DT.itemsize)
         L._jpeg_bound = True
     return L
 
@@ -129,3 +146,97 @@ def decode_batch_gpu(items, device, stream=None):
     if rc != 0:
         raise RuntimeError("dtm_jpeg_decode_gpu failed (%d)" % rc)
     return rgb, d
+
+
+# ---- device entropy decode -----------------------------------------------------------------------------
+# mirror of struct HuffDesc (csrc/kernels/jpeg.hip)
+HUFF_DESC_DT = np.dtype([("stream_off", "<i8"), ("coef_base", "<i8"), ("coef_count", "<i4"), ("seg_off", "<i4"),
+                         ("min_bits", "<i4"), ("overlap", "<i4"), ("s", SCAN_DT)])
+
+
+def scan_prep(data, stream=None, segs=None):
+    """Host share of the device entropy decode: marker parse + byte unstuffing.  ``stream`` / ``segs``: optional
+    uint8 / int32 scratch to write into (their prefix is used).  Returns (JpegInfo, JpegScan, unstuffed bytes +
+    STREAM_PAD zeros, restart segment offsets) - views of the scratch - or None (unsupported / corrupt: the host
+    decoders take the file)."""
+    L = _rt()
+    info = np.zeros(1, INFO_DT)
+    sc = np.zeros(1, SCAN_DT)
+    buf = np.frombuffer(data, np.uint8)
+    if stream is None or stream.size < buf.size + STREAM_PAD:
+        stream = np.empty(buf.size + STREAM_PAD, np.uint8)
+    if segs is None:
+        segs = np.empty(64, np.int32)
+    rc = L.dtm_jpeg_scan(buf.ctypes.data, buf.size, info.ctypes.data, sc.ctypes.data, stream.ctypes.data,
+                         stream.size, segs.ctypes.data, segs.size)
+    if rc == TOO_SMALL:
+        segs = np.empty(max(1, int(sc["nseg"][0])), np.int32)
+        rc = L.dtm_jpeg_scan(buf.ctypes.data, buf.size, info.ctypes.data, sc.ctypes.data, stream.ctypes.data,
+                             stream.size, segs.ctypes.data, segs.size)
+    if rc != 0:
+        return None
+    n = int(sc["nbytes"][0])
+    return info[0], sc[0], stream[:n + STREAM_PAD], segs[:int(sc["nseg"][0])]
+
+
+def huff_batch_table(scans, descs, min_bits=0, overlap=0):
+    """Entropy-decode descriptors for a batch prepared by scan_prep: [(JpegScan, stream bytes, segments)] and the
+    JpegDesc table of the same images (batch_table) -> (HuffDesc table, stream bytes, segment count).  Streams are
+    4-byte aligned."""
+    n = len(scans)
+    h = np.zeros(n, HUFF_DESC_DT)
+    off = nseg = 0
+    for i, (sc, st, sg) in enumerate(scans):
+        h[i]["s"] = sc
+        h[i]["stream_off"] = off
+        h[i]["coef_base"] = descs[i]["coef_base"]
+        nb = int(descs[i]["nblocks"]) * 64
+        h[i]["coef_count"] = nb
+        h[i]["seg_off"] = nseg
+        h[i]["min_bits"] = min_bits
+        h[i]["overlap"] = overlap
+        off += (st.size + 3) // 4 * 4
+        nseg += sg.size
+    return h, off, nseg
+
+
+def decode_batch_gpu_full(datas, device, min_bits=0, overlap=0, stream=None):
+    """Device decode of a batch of JPEG files (bytes): host marker parse + unstuffing, then jpeg_huff_kernel +
+    jpeg_idct_kernel + jpeg_color_kernel.  Returns (device uint8 RGB ragged buffer, JpegDesc table, per-image
+    status: passes of the subsequence fixed point, 0 for restart-segment images, -1 corrupt) - or None for a file
+    scan_prep declines (the caller decodes those on the host)."""
+    import torch
+
+    from ..ops import _lib
+    L = _lib.lib()
+    assert L.dtm_jpeg_huff_desc_bytes() == HUFF_DESC_DT.itemsize, (L.dtm_jpeg_huff_desc_bytes(),
+                                                                   HUFF_DESC_DT.itemsize)
+    preps = [scan_prep(d) for d in datas]
+    if any(p is None for p in preps):
+        return None
+    d, ncoef, nplane, nrgb, maxb, maxp = batch_table([p[0] for p in preps])
+    h, nbytes, nseg = huff_batch_table([p[1:] for p in preps], d, min_bits, overlap)
+    host = torch.zeros(max(nbytes, 16), dtype=torch.uint8, pin_memory=True)
+    hv = host.numpy()
+    segs = np.zeros(max(nseg, 1), np.int32)
+    for (inf, sc, st, sg), hd in zip(preps, h):
+        o = int(hd["stream_off"])
+        hv[o:o + st.size] = st
+        segs[int(hd["seg_off"]):int(hd["seg_off"]) + sg.size] = sg
+    dstream = host.to(device, non_blocking=True)
+    dsegs = torch.from_numpy(segs).to(device)
+    dh = torch.from_numpy(h.view(np.uint8)).to(device)
+    dd = torch.from_numpy(d.view(np.uint8)).to(device)
+    coefs = torch.empty(max(ncoef, 8), dtype=torch.int16, device=device)
+    status = torch.empty(len(datas), dtype=torch.int32, device=device)
+    planes = torch.empty(max(nplane, 8), dtype=torch.uint8, device=device)
+    rgb = torch.empty(max(nrgb, 1), dtype=torch.uint8, device=device)
+    sp = _lib.stream_ptr() if stream is None else stream
+    rc = L.dtm_jpeg_huff_gpu(_lib.ptr(dstream), _lib.ptr(dsegs), _lib.ptr(dh), len(datas), _lib.ptr(coefs),
+                             _lib.ptr(status), sp)
+    if rc == 0:
+        rc = L.dtm_jpeg_decode_gpu(_lib.ptr(coefs), _lib.ptr(dd), len(datas), int(maxb), int(maxp), _lib.ptr(planes),
+                                   _lib.ptr(rgb), sp)
+    if rc != 0:
+        raise RuntimeError("device JPEG decode failed (%d)" % rc)
+    return rgb, d, status, coefs

@@ -37,6 +37,8 @@ _SIGS = {
     "dtm_prep_params_bytes": (_I, []),
     "dtm_jpeg_desc_bytes": (_I, []),
     "dtm_jpeg_decode_gpu": (_I, [_P, _P, _I, _I, _L, _P, _P, _P]),
+    "dtm_jpeg_huff_desc_bytes": (_I, []),
+    "dtm_jpeg_huff_gpu": (_I, [_P, _P, _P, _I, _P, _P, _P]),
     "dtm_imagenet_prep": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P]),
     "dtm_act_bwd": (_I, [_P, _P, _P, _L, _I, _F, _I, _P]),
     "dtm_instnorm_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _I, _P]),

@@ -78,3 +78,100 @@ def test_split_decode_gpu_is_bit_exact_with_pil():
     for (name, data), dsc in zip(cases, descs):
         h, w, o = int(dsc["height"]), int(dsc["width"]), int(dsc["rgb_off"])
         np.testing.assert_array_equal(host[o:o + h * w * 3].reshape(h, w, 3), _pil(data), err_msg=name)
+
+
+def _restuff(st, segs, marker_base=0xD0):
+    """Inverse of the host unstuffing: 0xFF -> 0xFF 0x00 and an RSTn marker before every segment but the first."""
+    out, cuts = bytearray(), set(int(x) for x in segs[1:])
+    for i, b in enumerate(bytes(st)):
+        if i in cuts:
+            out += bytes([0xFF, marker_base + (sorted(cuts).index(i) % 8)])
+        out.append(b)
+        if b == 0xFF:
+            out.append(0)
+    return bytes(out)
+
+
+def test_scan_prep_unstuffs_the_entropy_coded_segment():
+    """dtm_jpeg_scan (the host share of the device entropy decode): the unstuffed bytes + restart segment table
+    re-stuff to exactly the file's scan, the layout matches the host decoder's and the zero padding follows."""
+    for name, data in _cases():
+        r = jpeg.scan_prep(data)
+        assert r is not None, name
+        info, sc, st, segs = r
+        hinfo, _cf = jpeg.huffman_decode(data)
+        assert info.tobytes() == hinfo.tobytes(), name
+        n = int(sc["nbytes"])
+        assert st.size == n + jpeg.STREAM_PAD and not st[n:].any(), name
+        assert int(sc["bpm"]) == sum(int(info["h"][c]) * int(info["v"][c]) for c in range(int(info["ncomp"]))), name
+        assert int(sc["nmcu"]) == int(info["mcux"]) * int(info["mcuy"]), name
+        if int(sc["restart"]):
+            assert segs.size == -(-int(sc["nmcu"]) // int(sc["restart"])) and segs[0] == 0, name
+            assert (np.diff(segs) > 0).all(), name
+        else:
+            assert segs.size == 0, name
+        # the scan as stored: after the SOS segment, up to the EOI marker
+        sos = data.index(b"\xff\xda")
+        start = sos + 2 + (data[sos + 2] << 8 | data[sos + 3])
+        stuffed = data[start:data.rindex(b"\xff\xd9")]
+        assert _restuff(st[:n], segs) == stuffed, name
+    assert jpeg.scan_prep(b"\xff\xd8\xff\xd9") is None
+    from PIL import Image
+    b = io.BytesIO()
+    Image.fromarray(_image(np.random.RandomState(1), 64, 64)).save(b, format="JPEG", progressive=True)
+    assert jpeg.scan_prep(b.getvalue()) is None
+
+
+def _big_cases(n=6):
+    """ImageNet-like geometry (the generator of tools/decode_cpu_cost.py): ~300-500 px sides, 4:2:0, quality 90."""
+    from PIL import Image
+    rng = np.random.RandomState(3)
+    out = []
+    for i in range(n):
+        h, w = int(rng.randint(300, 500)), int(rng.randint(300, 500))
+        b = io.BytesIO()
+        Image.fromarray(_image(rng, h, w)).save(b, format="JPEG", quality=int(rng.choice([75, 90, 95])))
+        out.append(("big%d" % i, b.getvalue()))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("min_bits", [0, 32, 256])
+def test_device_entropy_decode_matches_host_and_pil(min_bits):
+    """jpeg_huff_kernel: the device-decoded coefficients equal the host decoder's int16 for int16 and the RGB equals
+    PIL's, for every case (4:4:4 / 4:2:2 / 4:2:0 / 4:4:0, restart intervals, optimized tables, gray, ImageNet-size
+    files).  min_bits 32 / 256 cut the streams into many short subsequences, so most start states are wrong guesses
+    the fixed point has to repair."""
+    cases = _cases() + _big_cases()
+    r = jpeg.decode_batch_gpu_full([d for _n, d in cases], torch.device("cuda", 0), min_bits=min_bits)
+    assert r is not None
+    rgb, descs, status, coefs = r
+    torch.cuda.synchronize()
+    st = status.cpu().numpy()
+    host = rgb.cpu().numpy()
+    cf = coefs.cpu().numpy()
+    for (name, data), dsc, s in zip(cases, descs, st):
+        assert s >= 0, (name, s)
+        info, hc = jpeg.huffman_decode(data)
+        b = int(dsc["coef_base"])
+        np.testing.assert_array_equal(cf[b:b + hc.size], hc, err_msg=name)
+        h, w, o = int(dsc["height"]), int(dsc["width"]), int(dsc["rgb_off"])
+        np.testing.assert_array_equal(host[o:o + h * w * 3].reshape(h, w, 3), _pil(data), err_msg=name)
+    print("fixed-point passes per image:", list(st))
+
+
+@pytest.mark.gpu
+def test_device_entropy_decode_flags_corrupt_data():
+    """A scan cut short or overwritten with garbage is reported (status -1); the other images of the batch are
+    unaffected."""
+    good = _big_cases(2)
+    bad = bytearray(good[0][1])
+    sos = bad.index(b"\xff\xda")
+    cut = bytes(bad[:sos + 300]) + b"\xff\xd9"  # truncated scan
+    r = jpeg.decode_batch_gpu_full([good[1][1], cut], torch.device("cuda", 0))
+    assert r is not None
+    rgb, descs, status, _cf = r
+    st = status.cpu().numpy()
+    assert st[0] >= 1 and st[1] == -1, st
+    h, w, o = int(descs[0]["height"]), int(descs[0]["width"]), int(descs[0]["rgb_off"])
+    np.testing.assert_array_equal(rgb.cpu().numpy()[o:o + h * w * 3].reshape(h, w, 3), _pil(good[1][1]))

@@ -1,0 +1,7 @@
+#!/bin/bash
+# device entropy decode (unified DC/AC entry path, warm-up overlap): numerics + throughput per overlap
+set -o pipefail
+mkdir -p gpurun_out/r6
+timeout -k 10 300 python -u -m pytest -x -v -s --timeout 120 --timeout-method thread tests/test_jpeg.py -m gpu > gpurun_out/r6/r6_s19_pytest_jpeg.log 2>&1 &&
+timeout -k 10 200 python -u tools/jpeg_gpu_bench.py --images 128 --overlap -1 0 512 2048 > gpurun_out/r6/r6_s19_jpeg_bench.log 2>&1 &&
+timeout -k 10 200 python -u tools/jpeg_gpu_bench.py --images 768 --overlap -1 0 2048 > gpurun_out/r6/r6_s19_jpeg_bench768.log 2>&1
