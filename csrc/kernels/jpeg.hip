@@ -215,11 +215,10 @@ struct HuffDesc {
   int coef_count;        // int16 coefficients of the image (zeroed here first)
   int seg_off;           // its first restart segment in the batch segment table
   int min_bits;          // floor of the subsequence length L (0: 1024)
-  int overlap;           // warm-up bits decoded before a subsequence to guess its start state (< 0: none, 0: L / 2)
+  int pad;
   JpegScan s;
 };
 
-constexpr int HT = 256, LOOK = 11;
 // lookup entry, one per 11-bit prefix (0: a code longer than 11 bits - huff_slow_entry builds the same form):
 //   bits 0-4   code length, or code + magnitude bits of a value entry
 //   bit 5      value entry: bits 16-31 hold the signed coefficient (code + magnitude fit the 11 bits)
@@ -229,16 +228,24 @@ constexpr int HT = 256, LOOK = 11;
 //   bits 16-19 magnitude bit count of a symbol (non-value) entry
 // so DC and AC symbols take one branch-light path.
 constexpr unsigned HE_VAL = 32u, HE_PUT = 64u, HE_BAD = 128u;
+// A subsequence pass reads its bits from LDS, staged in phases of HPW words per thread: the loads of phase j + 1
+// are issued as phase j starts and written to LDS after it, so no refill waits on memory (a per-thread refill from
+// global memory stalls the whole wave on the latest load of whichever lane refilled last).
+constexpr int HPW = 16;
 
+template <int NT, int LK>
 struct HuffLds {
-  unsigned lut[4][1 << LOOK];
+  static constexpr int kLook = LK;
+  unsigned lut[4][1 << LK];
   int maxcode[4][18];
   int valoff[4][17];
   unsigned char vals[4][256];
   unsigned char zz[64];
   int bcomp[12], bdy[12], bdx[12], dcs[3], acs[3];
   int bctx[12];  // component | DC slot << 4 | AC slot << 8 of the b-th block of an MCU
-  int ep[HT], eb[HT], ek[HT], cnt[HT], ds[3][HT];
+  unsigned win[HPW + 4][NT];  // each thread's stream words of the current phase (+ a 4-word tail), thread-minor:
+                              // lanes at similar offsets read distinct banks
+  int ep[NT], eb[NT], ek[NT], cnt[NT], ds[3][NT];
   int flag[3], err, passes;
 };
 
@@ -251,39 +258,42 @@ __device__ __forceinline__ int hextend(int v, int s) { return v < (1 << (s - 1))
 
 // entry for symbol `sym` of code length len (dc: a DC table); bits: the 11-bit prefix (value entries read the
 // magnitude bits that follow the code in it), or -1 (longer codes: no value entry)
+template <int LK>
 __device__ __forceinline__ unsigned huff_entry(int len, int sym, bool dc, int bits) {
   if (dc && sym > 15) return 1u | HE_BAD;  // (advance 0: the DC is retried one bit later)
   const int run = dc ? 0 : sym >> 4, size = dc ? sym : sym & 15;
   if (!dc && !size) return (unsigned)len | ((run == 15 ? 16u : 64u) << 8);  // ZRL / EOB
   const unsigned adv = (unsigned)(run + 1) << 8;
-  if (bits >= 0 && len + size <= LOOK) {
-    const int v = size ? hextend((bits >> (LOOK - len - size)) & ((1 << size) - 1), size) : 0;
+  if (bits >= 0 && len + size <= LK) {
+    const int v = size ? hextend((bits >> (LK - len - size)) & ((1 << size) - 1), size) : 0;
     return (unsigned)(len + size) | HE_VAL | HE_PUT | adv | ((unsigned)v << 16);
   }
   return (unsigned)len | HE_PUT | adv | ((unsigned)size << 16);
 }
 
-// a code longer than LOOK bits (canonical maxcode walk over the next 16 bits)
-__device__ __forceinline__ unsigned huff_slow_entry(const HuffLds& L, int slot, unsigned code16, bool dc) {
-  int m[5];
+// a code longer than LK bits (canonical maxcode walk over the next 16 bits)
+template <int NT, int LK>
+__device__ __forceinline__ unsigned huff_slow_entry(const HuffLds<NT, LK>& L, int slot, unsigned code16, bool dc) {
+  constexpr int NL = 16 - LK;
+  int m[NL];
 #pragma unroll
-  for (int i = 0; i < 5; ++i) m[i] = L.maxcode[slot][LOOK + 1 + i];
+  for (int i = 0; i < NL; ++i) m[i] = L.maxcode[slot][LK + 1 + i];
   int l = 0, c = 0;
 #pragma unroll
-  for (int i = 4; i >= 0; --i) {  // the shortest matching length wins
-    const int ci = (int)(code16 >> (16 - (LOOK + 1 + i)));
+  for (int i = NL - 1; i >= 0; --i) {  // the shortest matching length wins
+    const int ci = (int)(code16 >> (16 - (LK + 1 + i)));
     if (ci <= m[i]) {
-      l = LOOK + 1 + i;
+      l = LK + 1 + i;
       c = ci;
     }
   }
   if (!l) return 1u | HE_BAD | (dc ? 0u : 64u << 8);
-  return huff_entry(l, L.vals[slot][(c + L.valoff[slot][l]) & 255], dc, -1);
+  return huff_entry<LK>(l, L.vals[slot][(c + L.valoff[slot][l]) & 255], dc, -1);
 }
 
-// MSB-first bit reader over big-endian 32-bit words; one word is always in flight (nxt) so a refill never waits on
-// memory
-struct BitReader {
+// MSB-first bit reader over big-endian 32-bit words in global memory (restart segments: arbitrary starts and
+// lengths); one word is always in flight
+struct GReader {
   const unsigned* w;
   unsigned long long buf;
   int nb, wi, p;
@@ -309,35 +319,80 @@ struct BitReader {
   __device__ __forceinline__ void skip(int n) { buf <<= n; nb -= n; p += n; }
 };
 
+// the same over this thread's LDS phase window: win[i * stride] holds absolute word base + i
+template <int NT>
+struct LReader {
+  const unsigned* win;
+  int base;
+  unsigned long long buf;
+  int nb, wi, p;
+  __device__ __forceinline__ unsigned word(int i) const { return __builtin_bswap32(win[(i - base) * NT]); }
+  __device__ __forceinline__ void init(int pos) {
+    wi = pos >> 5;
+    buf = (((unsigned long long)word(wi) << 32) | word(wi + 1)) << (pos & 31);
+    nb = 64 - (pos & 31);
+    wi += 2;
+    p = pos;
+  }
+  __device__ __forceinline__ void fill() {
+    if (nb < 32) {
+      buf |= (unsigned long long)word(wi) << (32 - nb);
+      nb += 32;
+      ++wi;
+    }
+  }
+  __device__ __forceinline__ unsigned peek(int n) const { return (unsigned)(buf >> (64 - n)); }
+  __device__ __forceinline__ void skip(int n) { buf <<= n; nb -= n; p += n; }
+};
+
 struct HuffState {
   int p, b, k;
 };
 
-__device__ __forceinline__ short* block_at(const HuffLds& L, const JpegScan& s, short* img, int g) {
+template <class LDS>
+__device__ __forceinline__ short* block_at(const LDS& L, const JpegScan& s, short* img, int g) {
   const int mcu = g / s.bpm, bb = g - mcu * s.bpm, my = mcu / s.mcux, mx = mcu - my * s.mcux, c = L.bcomp[bb];
   return img + s.coef_off[c] + ((long long)(my * s.v[c] + L.bdy[bb]) * s.bw[c] + mx * s.h[c] + L.bdx[bb]) * 64;
 }
 
-// Decode from st until the first codeword boundary at or past `stop` (or, with gstop >= 0, until block gstop would
-// start).  OUT = false: count blocks started (DC symbols) and sum the DC differences per component into acc.
-// OUT = true: write the coefficients of blocks g < total (g: the block being decoded; acc: the DC predictors).
-// A decode error in a block < total sets err (chains started from a wrong guess may hit them; only the exact,
-// final pass reports).  Every iteration consumes >= 1 bit.
-template <bool OUT>
-__device__ void huff_run(const HuffLds& L, const JpegScan& s, const unsigned* words, HuffState& st, int stop,
-                         int gstop, int total, int& g, int* acc, int& nblk, int& err, short* img) {
-  BitReader br;
-  br.init(words, st.p);
-  int b = st.b, k = st.k;
-  short* blk = nullptr;
-  if (OUT && k > 0 && g < total) blk = block_at(L, s, img, g);
-  int ctx = L.bctx[b];  // this block's component and table slots (re-read once per block)
+// decoder state that survives between phases
+struct HuffDec {
+  int b, k, ctx, g, nblk, err;
+  int a0, a1, a2;  // count passes: DC-difference sums per component; output pass: the DC predictors (no array:
+                   // a lane-indexed one goes to scratch)
+  short* blk;
+};
+
+template <class LDS>
+__device__ __forceinline__ void dec_start(HuffDec& d, const LDS& L, const JpegScan& s, short* img, HuffState st,
+                                          int g, const int* acc, bool out, int total) {
+  d.b = st.b;
+  d.k = st.k;
+  d.ctx = L.bctx[st.b];
+  d.g = g;
+  d.nblk = 0;
+  d.err = 0;
+  d.a0 = acc[0];
+  d.a1 = acc[1];
+  d.a2 = acc[2];
+  d.blk = (out && st.k > 0 && g < total) ? block_at(L, s, img, g) : nullptr;
+}
+
+// Decode until the first codeword boundary at or past `stop` (or, with gstop >= 0, until block gstop would start).
+// OUT = false: count blocks started (DC symbols) and sum the DC differences per component.  OUT = true: write the
+// coefficients of blocks g < total.  A decode error in a block < total sets err (chains started from a wrong
+// guess may hit them; only the exact, final pass reports).  Every iteration consumes >= 1 bit.
+template <bool OUT, class R, class LDS>
+__device__ __forceinline__ void huff_steps(const LDS& L, const JpegScan& s, R& br, HuffDec& d, int stop, int gstop, int total,
+                           short* img) {
+  int b = d.b, k = d.k, ctx = d.ctx, g = d.g, a0 = d.a0, a1 = d.a1, a2 = d.a2, nblk = d.nblk, err = d.err;
+  short* blk = d.blk;
   while (br.p < stop) {
     if (gstop >= 0 && k == 0 && g >= gstop) break;
     br.fill();
     const int c = ctx & 15;
     const int slot = k == 0 ? (ctx >> 4) & 15 : ctx >> 8;
-    unsigned e = L.lut[slot][br.peek(LOOK)];
+    unsigned e = L.lut[slot][br.peek(LDS::kLook)];
     if (!e) e = huff_slow_entry(L, slot, br.peek(16), k == 0);
     const int size = (e & HE_VAL) ? 0 : (e >> 16) & 15;
     const int used = (e & 31) + size;
@@ -348,8 +403,11 @@ __device__ void huff_run(const HuffLds& L, const JpegScan& s, const unsigned* wo
     if (e & HE_PUT) {
       const int pos = k + adv - 1;
       if (k == 0) {
-        acc[c] += val;
-        val = acc[c];
+        const int a = (c == 0 ? a0 : c == 1 ? a1 : a2) + val;
+        a0 = c == 0 ? a : a0;
+        a1 = c == 1 ? a : a1;
+        a2 = c == 2 ? a : a2;
+        val = a;
         if (!OUT) ++nblk;
         else if (g < total) blk = block_at(L, s, img, g);
       }
@@ -370,16 +428,24 @@ __device__ void huff_run(const HuffLds& L, const JpegScan& s, const unsigned* wo
       if (OUT) ++g;
     }
   }
-  st.p = br.p;
-  st.b = b;
-  st.k = k;
+  d.b = b;
+  d.k = k;
+  d.ctx = ctx;
+  d.g = g;
+  d.blk = blk;
+  d.a0 = a0;
+  d.a1 = a1;
+  d.a2 = a2;
+  d.nblk = nblk;
+  d.err = err;
 }
 
-__device__ __forceinline__ int block_scan_excl(int* a, int v) {  // exclusive prefix sum over the HT threads
+template <int NT>
+__device__ __forceinline__ int block_scan_excl(int* a, int v) {  // exclusive prefix sum over the NT threads
   const int t = threadIdx.x;
   a[t] = v;
   __syncthreads();
-  for (int o = 1; o < HT; o <<= 1) {
+  for (int o = 1; o < NT; o <<= 1) {
     const int x = t >= o ? a[t - o] : 0;
     __syncthreads();
     a[t] += x;
@@ -390,18 +456,62 @@ __device__ __forceinline__ int block_scan_excl(int* a, int v) {  // exclusive pr
   return r;
 }
 
-__global__ __launch_bounds__(HT) void jpeg_huff_kernel(const unsigned char* __restrict__ stream,
+// the HPW + 4 words of phase j of a thread whose subsequence starts at word w0 (zeros past the image's stream)
+__device__ __forceinline__ void stage_load(uint4 (&r)[(HPW + 4) / 4], const unsigned* words, int w0, int j, int nw) {
+#pragma unroll
+  for (int i = 0; i < (HPW + 4) / 4; ++i) {
+    const int w = w0 + j * HPW + 4 * i;
+    r[i] = w + 4 <= nw ? *(const uint4*)(words + w) : make_uint4(0, 0, 0, 0);
+  }
+}
+
+// One subsequence pass over the LDS phases: every thread takes part in the staging barriers; `run` threads decode
+// from st up to `stop`.  Returns the exit state (for OUT = false, with the counts in d).
+template <bool OUT, int NT, int LK>
+__device__ __forceinline__ HuffState huff_pass(HuffLds<NT, LK>& L, const JpegScan& s, const unsigned* words, int nw, int w0,
+                               int nphase, bool run, HuffState st, int stop, int g, const int* acc, int total,
+                               short* img, HuffDec& d) {
+  const int t = threadIdx.x;
+  uint4 r[(HPW + 4) / 4];
+  if (run) stage_load(r, words, w0, 0, nw);
+  dec_start(d, L, s, img, st, g, acc, OUT, total);
+  LReader<NT> br;
+  br.win = &L.win[0][t];
+  br.base = w0;
+  for (int j = 0; j < nphase; ++j) {
+    if (run) {
+#pragma unroll
+      for (int i = 0; i < (HPW + 4) / 4; ++i) {
+        L.win[4 * i][t] = r[i].x;
+        L.win[4 * i + 1][t] = r[i].y;
+        L.win[4 * i + 2][t] = r[i].z;
+        L.win[4 * i + 3][t] = r[i].w;
+      }
+    }
+    __syncthreads();
+    if (run && j + 1 < nphase) stage_load(r, words, w0, j + 1, nw);  // (in flight during this phase)
+    if (run) {
+      br.base = w0 + j * HPW;
+      if (j == 0) br.init(st.p);
+      huff_steps<OUT>(L, s, br, d, min(stop, (w0 + (j + 1) * HPW) * 32), -1, total, img);
+    }
+    __syncthreads();
+  }
+  return HuffState{br.p, d.b, d.k};
+}
+
+template <int NT, int LK>
+__global__ __launch_bounds__(NT) void jpeg_huff_kernel(const unsigned char* __restrict__ stream,
                                                        const int* __restrict__ segs, const HuffDesc* __restrict__ descs,
                                                        short* __restrict__ coefs, int* __restrict__ status) {
-  __shared__ HuffLds L;
+  __shared__ HuffLds<NT, LK> L;
   const HuffDesc& d = descs[blockIdx.x];
   const JpegScan& s = d.s;
   const int t = threadIdx.x;
   short* img = coefs + d.coef_base;
-  // zero the image's coefficients (blocks only get their nonzero entries written)
   {
     uint4* z = (uint4*)img;  // (coef_base and every image's capacity are 8-int16 aligned)
-    for (int i = t; i < (d.coef_count + 7) / 8; i += HT) z[i] = make_uint4(0, 0, 0, 0);
+    for (int i = t; i < (d.coef_count + 7) / 8; i += NT) z[i] = make_uint4(0, 0, 0, 0);
   }
   // tables
   if (t < s.nslot) {
@@ -416,18 +526,12 @@ __global__ __launch_bounds__(HT) void jpeg_huff_kernel(const unsigned char* __re
     }
     L.maxcode[t][17] = 0x7fffffff;
   }
-  for (int i = t; i < 4 * 256; i += HT) (&L.vals[0][0])[i] = (&s.vals[0][0])[i];
+  for (int i = t; i < 4 * 256; i += NT) (&L.vals[0][0])[i] = (&s.vals[0][0])[i];
   if (t < 64) L.zz[t] = c_zigzag[t];
   if (t < 12) {
     L.bcomp[t] = s.bcomp[t];
     L.bdy[t] = s.bdy[t];
     L.bdx[t] = s.bdx[t];
-  }
-  if (t < 3) {
-    L.dcs[t] = s.dc_slot[t];
-    L.acs[t] = s.ac_slot[t];
-  }
-  if (t < 12) {
     const int c = s.bcomp[t];
     L.bctx[t] = c | (s.dc_slot[c] << 4) | (s.ac_slot[c] << 8);
   }
@@ -436,13 +540,13 @@ __global__ __launch_bounds__(HT) void jpeg_huff_kernel(const unsigned char* __re
     L.flag[0] = L.flag[1] = L.flag[2] = 0;
   }
   __syncthreads();
-  for (int i = t; i < s.nslot << LOOK; i += HT) {
-    const int slot = i >> LOOK, f = i & ((1 << LOOK) - 1);
+  for (int i = t; i < s.nslot << LK; i += NT) {
+    const int slot = i >> LK, f = i & ((1 << LK) - 1);
     unsigned e = 0;
-    for (int len = 1; len <= LOOK; ++len) {
-      const int code = f >> (LOOK - len);
+    for (int len = 1; len <= LK; ++len) {
+      const int code = f >> (LK - len);
       if (code <= L.maxcode[slot][len]) {
-        e = huff_entry(len, L.vals[slot][(code + L.valoff[slot][len]) & 255], s.slot_dc[slot] != 0, f);
+        e = huff_entry<LK>(len, L.vals[slot][(code + L.valoff[slot][len]) & 255], s.slot_dc[slot] != 0, f);
         break;
       }
     }
@@ -452,49 +556,45 @@ __global__ __launch_bounds__(HT) void jpeg_huff_kernel(const unsigned char* __re
   __syncthreads();
 
   const unsigned* words = (const unsigned*)(stream + d.stream_off);
-  const int nbits = s.nbytes * 8, total = s.nmcu * s.bpm;
+  const int nbits = s.nbytes * 8, total = s.nmcu * s.bpm, nw = (s.nbytes + 32) / 4;
   int err = 0;
   if (s.restart > 0) {
-    // independent restart segments
+    // independent restart segments, read straight from global memory
     const int per = s.restart * s.bpm;
-    for (int sg = t; sg < s.nseg; sg += HT) {
-      HuffState st{segs[d.seg_off + sg] * 8, 0, 0};
-      int g = sg * per, nb = 0, pred[3] = {0, 0, 0};
-      const int gstop = min(g + per, total);
-      huff_run<true>(L, s, words, st, nbits + 64, gstop, total, g, pred, nb, err, img);
-      if (g < gstop) err = 1;  // ran out of data
+    for (int sg = t; sg < s.nseg; sg += NT) {
+      GReader br;
+      br.init(words, segs[d.seg_off + sg] * 8);
+      HuffDec dd;
+      const int zero[3] = {0, 0, 0};
+      dec_start(dd, L, s, img, HuffState{br.p, 0, 0}, sg * per, zero, true, total);
+      const int gstop = min(sg * per + per, total);
+      huff_steps<true>(L, s, br, dd, nbits + 64, gstop, total, img);
+      if (dd.err || dd.g < gstop) err = 1;  // (g < gstop: ran out of data)
     }
     if (t == 0) L.passes = 0;
   } else {
+    // subsequences of Lb bits (a multiple of 128: 16-byte aligned phase loads)
     int Lb = d.min_bits > 0 ? d.min_bits : 1024;
-    Lb = max(Lb, (nbits + HT - 1) / HT);
-    Lb = (Lb + 31) & ~31;
+    Lb = max(Lb, (nbits + NT - 1) / NT);
+    Lb = (Lb + 127) & ~127;
     const int nact = (nbits + Lb - 1) / Lb;
-    const int stop = min((t + 1) * Lb, nbits);
+    const int stop = min((t + 1) * Lb, nbits), w0 = t * Lb / 32;
+    const int nphase = (Lb + HPW * 32 - 1) / (HPW * 32);
     HuffState st{t * Lb, 0, 0};
-    const int ov = d.overlap == 0 ? Lb / 2 : d.overlap;
-    if (t > 0 && t < nact && ov > 0) {
-      // warm-up: decode from a guess `ov` bits earlier; the state it reaches at t * L is most often already exact
-      // (the decode has fallen into step), so most subsequences need no second pass
-      HuffState w{max(0, t * Lb - ov), 0, 0};
-      int g = 0, nb = 0, e2 = 0, acc[3] = {0, 0, 0};
-      huff_run<false>(L, s, words, w, t * Lb, -1, total, g, acc, nb, e2, img);
-      st = w;
-    }
+    const int zero[3] = {0, 0, 0};
     bool dirty = t < nact;
     int pass = 0;
-    for (; pass <= HT; ++pass) {
+    for (; pass <= NT; ++pass) {
+      HuffDec dd;
+      const HuffState e = huff_pass<false>(L, s, words, nw, w0, nphase, dirty, st, stop, 0, zero, total, img, dd);
       if (dirty) {
-        HuffState e = st;
-        int g = 0, nb = 0, e2 = 0, acc[3] = {0, 0, 0};
-        huff_run<false>(L, s, words, e, stop, -1, total, g, acc, nb, e2, img);
         L.ep[t] = e.p;
         L.eb[t] = e.b;
         L.ek[t] = e.k;
-        L.cnt[t] = nb;
-        L.ds[0][t] = acc[0];
-        L.ds[1][t] = acc[1];
-        L.ds[2][t] = acc[2];
+        L.cnt[t] = dd.nblk;
+        L.ds[0][t] = dd.a0;
+        L.ds[1][t] = dd.a1;
+        L.ds[2][t] = dd.a2;
       }
       if (t == 0) L.flag[(pass + 1) % 3] = 0;  // (3 flags: a slow thread may still read the previous pass's)
       __syncthreads();
@@ -511,22 +611,22 @@ __global__ __launch_bounds__(HT) void jpeg_huff_kernel(const unsigned char* __re
     const int nb = act ? L.cnt[t] : 0;
     const int d0 = act ? L.ds[0][t] : 0, d1 = act ? L.ds[1][t] : 0, d2 = act ? L.ds[2][t] : 0;
     __syncthreads();
-    const int G = block_scan_excl(L.cnt, nb);
+    const int G = block_scan_excl<NT>(L.cnt, nb);
     int pred[3];
-    pred[0] = block_scan_excl(L.ds[0], d0);
-    pred[1] = block_scan_excl(L.ds[1], d1);
-    pred[2] = block_scan_excl(L.ds[2], d2);
-    if (t == HT - 1 && G + nb < total) L.err = 1;  // the stream ended before the last block
-    if (act) {
-      int g = st.k > 0 ? G - 1 : G, unused = 0;
-      huff_run<true>(L, s, words, st, stop, -1, total, g, pred, unused, err, img);
-    }
+    pred[0] = block_scan_excl<NT>(L.ds[0], d0);
+    pred[1] = block_scan_excl<NT>(L.ds[1], d1);
+    pred[2] = block_scan_excl<NT>(L.ds[2], d2);
+    if (t == NT - 1 && G + nb < total) L.err = 1;  // the stream ended before the last block
+    HuffDec dd;
+    huff_pass<true>(L, s, words, nw, w0, nphase, act, st, stop, st.k > 0 ? G - 1 : G, pred, total, img, dd);
+    if (act && dd.err) err = 1;
     if (t == 0) L.passes = pass + 1;
   }
   if (err) L.err = 1;
   __syncthreads();
   if (t == 0) status[blockIdx.x] = L.err ? -1 : L.passes;
 }
+
 }  // namespace dtm
 using namespace dtm;
 
@@ -552,11 +652,27 @@ DTM_API int dtm_jpeg_huff_desc_bytes() { return (int)sizeof(HuffDesc); }
 // Entropy-decode a batch: stream = the images' unstuffed bytes (each 4-aligned, 32 zero bytes after), segs = the
 // restart segment table, descs = device [n] HuffDesc.  coefs receives every image's zero-filled coefficients;
 // status[i] = passes of the subsequence fixed point (0: restart segments), -1: the image's data is corrupt.
+// threads per image (64 / 128 / 256) and lookup bits (9 / 10 / 11) of the entropy decoder
+static int g_huff_nt = getenv("DTM_JPEG_NT") ? atoi(getenv("DTM_JPEG_NT")) : 256;
+static int g_huff_lk = getenv("DTM_JPEG_LOOK") ? atoi(getenv("DTM_JPEG_LOOK")) : 11;
+DTM_API void dtm_jpeg_set_huff(int nt, int lk) {
+  g_huff_nt = nt;
+  g_huff_lk = lk;
+}
+
 DTM_API int dtm_jpeg_huff_gpu(const void* stream, const void* segs, const void* descs, int n, void* coefs,
                               void* status, void* st) {
   if (n <= 0) return 0;
-  if (n > 0x7fffffff / HT) return -1;
-  hipLaunchKernelGGL(jpeg_huff_kernel, dim3(n), dim3(HT), 0, (hipStream_t)st, (const unsigned char*)stream,
-                     (const int*)segs, (const HuffDesc*)descs, (short*)coefs, (int*)status);
-  return 0;
+  const int nt = g_huff_nt, lk = g_huff_lk;
+#define DTM_HUFF(NT_, LK_)                                                                                         \
+  if (nt == NT_ && lk == LK_) {                                                                                    \
+    hipLaunchKernelGGL((jpeg_huff_kernel<NT_, LK_>), dim3(n), dim3(NT_), 0, (hipStream_t)st,                        \
+                       (const unsigned char*)stream, (const int*)segs, (const HuffDesc*)descs, (short*)coefs,      \
+                       (int*)status);                                                                              \
+    return 0;                                                                                                      \
+  }
+  DTM_HUFF(256, 11) DTM_HUFF(256, 10) DTM_HUFF(256, 9) DTM_HUFF(128, 11) DTM_HUFF(128, 10) DTM_HUFF(128, 9)
+  DTM_HUFF(64, 11) DTM_HUFF(64, 10) DTM_HUFF(64, 9)
+#undef DTM_HUFF
+  return -2;
 }

@@ -35,6 +35,7 @@ _PARAM_DT = np.dtype([("src_off", "<i8"), ("h", "<i4"), ("w", "<i4"), ("y0", "<i
 
 
 _COEF_SCRATCH = {}
+_SCAN_SCRATCH = {}
 
 
 def _decode_chunk(tasks, split=False):
@@ -43,9 +44,11 @@ def _decode_chunk(tasks, split=False):
     drawn here, from a per-image seed the assembler assigned in submission order, so the stream is
     reproducible for a given seed and the assembler thread does no per-image sampling.
 
-    ``split``: only the entropy decode runs here (data/jpeg.py, ~2x cheaper than a full PIL decode);
-    the item carries (JpegInfo bytes, int16 coefficients) and the device finishes the decode bit-exactly.
-    Files outside the split decoder's subset (progressive, CMYK, ...) are decoded by PIL as before."""
+    ``split`` (decode mode): 0 = full PIL decode here; 1 = only the entropy decode runs here (data/jpeg.py, ~2x
+    cheaper than a full PIL decode), the item carries (JpegInfo bytes, int16 coefficients) and the device finishes
+    the decode bit-exactly; 2 = only the marker parse + byte unstuffing runs here (~30x cheaper than the entropy
+    decode), the item carries (JpegInfo + JpegScan bytes, unstuffed stream) and the device does the rest, Huffman
+    decode included.  Files outside the decoders' subset (progressive, CMYK, ...) are decoded by PIL as before."""
     out = []
     for rec, tid, seed, train in tasks:
         try:
@@ -62,7 +65,18 @@ def _decode_one(rec, tid, seed, train, split, copy=True):
     ``copy=False``: the coefficients are a view of this thread's scratch (valid until its next call)."""
     data, label, bbox, _ = imagenet.parse_example_proto(rec)
     coef = img = None
-    if split:
+    if split == 2:
+        from . import jpeg
+        key = threading.get_ident()
+        st = _SCAN_SCRATCH.get(key)
+        if st is None or st[0].size < len(data) + jpeg.STREAM_PAD:
+            st = _SCAN_SCRATCH[key] = (np.empty(max(1 << 22, len(data) + jpeg.STREAM_PAD), np.uint8),
+                                       np.empty(1 << 14, np.int32))
+        coef = jpeg.scan_item(data, *st)
+        if coef is not None:
+            info = np.frombuffer(coef[0], jpeg.INFO_DT, count=1)[0]
+            h, w = int(info["height"]), int(info["width"])
+    elif split:
         from . import jpeg
         key = threading.get_ident()
         buf = _COEF_SCRATCH.get(key)
@@ -217,8 +231,8 @@ class _ShmDecoders:
                 _k, info, o, nb, label, p, shape = m
                 b = slot * self.slot_bytes + o
                 pay = ring[b:b + nb]
-            if info is not None:
-                item = (None, label, p, (info, pay.view(np.int16)))
+            if info is not None:  # (device-decode items carry JpegInfo + JpegScan and the raw stream bytes)
+                item = (None, label, p, (info, pay if len(info) > jpeg.INFO_DT.itemsize else pay.view(np.int16)))
             else:
                 item = (pay.reshape(shape), label, p, None)
             out.append(item + ((wid, slot) if m[0] == "shm" else None,))
@@ -276,7 +290,7 @@ def _item_hw(d):
     if d[0] is not None:
         return d[0].shape[0], d[0].shape[1]
     from . import jpeg
-    info = np.frombuffer(d[3][0], jpeg.INFO_DT)[0]
+    info = np.frombuffer(d[3][0], jpeg.INFO_DT, count=1)[0]
     return int(info["height"]), int(info["width"])
 
 
@@ -338,10 +352,16 @@ class GPUBatchInputs:
         # (profiles/r3/r3_imagenet_pipeline_split_vs_full.log): full host decode 12.2-13.6k img/s, split
         # 9.7-10.3k - with the shared-memory decoder processes the host decode is no longer the bottleneck,
         # and the split path's larger per-batch table work in the assembler thread costs more than it saves.
+        # DTM_SPLIT_DECODE=2 / split_decode="device": the device decode (host marker parse + unstuffing only,
+        # data/jpeg.py scan_prep; Huffman decode, IDCT and colour as HIP kernels)
         if split_decode is None:
             import os
-            split_decode = os.environ.get("DTM_SPLIT_DECODE", "0") == "1" and torch.device(device).type == "cuda"
-        self.split = bool(split_decode)
+            env = os.environ.get("DTM_SPLIT_DECODE", "0")
+            split_decode = {"1": 1, "2": 2, "device": 2}.get(env, 0) if torch.device(device).type == "cuda" else 0
+        self.split = {"full": 0, "split": 1, "device": 2}.get(split_decode, split_decode)
+        self.split = int(self.split)  # 0 full host decode, 1 host Huffman + device IDCT, 2 device decode
+        self.decode_errors = 0  # device-decoded images whose entropy-coded data was corrupt
+        self._status = []
         self.B, self.S, self.train = batch_size, image_size, train
         self.device = torch.device(device)
         self.nthreads = max(1, num_preprocess_threads)
@@ -551,6 +571,11 @@ class GPUBatchInputs:
         hw = [_item_hw(d) for d in dec]
         tab, total = param_table(None, params, hw)
         split_idx = [i for i, d in enumerate(dec) if d[3] is not None]
+        if len(dec[split_idx[0]][3][0]) > jpeg.INFO_DT.itemsize:  # device decode items
+            batch = jpeg.DeviceBatch([jpeg.unpack_scan_item(*dec[i][3]) for i in split_idx],
+                                     rgb_offs=tab["src_off"][split_idx], rgb_bytes=int(total), pin=self.pin)
+            return batch, torch.from_numpy(tab.view(np.uint8)), ("device", self._fallbacks(dec, tab), int(total),
+                                                                len(split_idx))
         infos = [np.frombuffer(dec[i][3][0], jpeg.INFO_DT)[0] for i in split_idx]
         descs, ncoef, nplane, _nrgb, maxb, maxp = jpeg.batch_table(infos)
         descs["rgb_off"] = tab["src_off"][split_idx]
@@ -560,22 +585,43 @@ class GPUBatchInputs:
             cf = dec[i][3][1]
             b = int(descs[j]["coef_base"])
             np.copyto(cv[b:b + cf.size], cf)
-        falls = [(int(tab[i]["src_off"]), dec[i][0]) for i in range(len(dec)) if dec[i][3] is None]
-        fb = None
-        if falls:
-            nb = sum(im.nbytes for _o, im in falls)
-            fb_t, fv = self._host_buffer(nb)
-            off, lst = 0, []
-            for o, im in falls:
-                np.copyto(fv[off:off + im.nbytes], im.reshape(-1))
-                lst.append((o, off, im.nbytes))
-                off += im.nbytes
-            fb = (fb_t, lst)
+        fb = self._fallbacks(dec, tab)
         dt = torch.from_numpy(descs.view(np.uint8))
         if self.pin:
             dt = dt.pin_memory()
         return coefs, torch.from_numpy(tab.view(np.uint8)), (dt, len(split_idx), int(maxb), int(maxp), int(nplane),
                                                             int(total), fb)
+
+    def _fallbacks(self, dec, tab):
+        """PIL-decoded items of a split / device batch: (pinned pixel buffer, [(rgb offset, buffer offset, bytes)])
+        or None."""
+        falls = [(int(tab[i]["src_off"]), dec[i][0]) for i in range(len(dec)) if dec[i][3] is None]
+        if not falls:
+            return None
+        fb_t, fv = self._host_buffer(sum(im.nbytes for _o, im in falls))
+        off, lst = 0, []
+        for o, im in falls:
+            np.copyto(fv[off:off + im.nbytes], im.reshape(-1))
+            lst.append((o, off, im.nbytes))
+            off += im.nbytes
+        return fb_t, lst
+
+    def _check_status(self, block=False):
+        """Count the corrupt images of device-decoded batches whose status copy has landed (no sync)."""
+        keep = []
+        for host, ev in self._status:
+            if block or ev.query():
+                ev.synchronize()
+                bad = int((host < 0).sum())
+                if bad:
+                    self.decode_errors += bad
+                    import logging
+                    logging.getLogger("distributed_tensorflow_models_amd").warning(
+                        "input pipeline: %d device-decoded image(s) had corrupt entropy-coded data (%d so far)",
+                        bad, self.decode_errors)
+            else:
+                keep.append((host, ev))
+        self._status = keep
 
     def _fail(self, msg):
         """A pipeline thread died: hand the error to the consumer (no silent hang in next_batch)."""
@@ -601,7 +647,28 @@ class GPUBatchInputs:
     def _device_decode(self, coefs, split):
         """IDCT + upsampling + colour of the batch's split items on the device -> the RGB ragged buffer
         (device) that the preprocessing kernel reads; fallback (PIL) pixels are copied into their slots."""
-        dt, n, maxb, maxp, nplane, total, fb = split
+        if split[0] == "device":  # coefs: the jpeg.DeviceBatch
+            _k, fb, total, n = split
+            rgb = torch.empty(max(total, 1), dtype=torch.uint8, device=self.device)
+            if n:
+                rgb, status = coefs.launch(self.device, rgb=rgb)
+                host = torch.empty(n, dtype=torch.int32, pin_memory=self.pin)
+                host.copy_(status, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                self._check_status()
+                self._status.append((host, ev))
+        else:
+            dt, n, maxb, maxp, nplane, total, fb = split
+            rgb = self._coef_decode(coefs, dt, n, maxb, maxp, nplane, total)
+        if fb is not None:
+            fb_t, lst = fb
+            src = fb_t.to(self.device, non_blocking=True)
+            for o, so, nb in lst:
+                rgb[o:o + nb].copy_(src[so:so + nb])
+        return rgb
+
+    def _coef_decode(self, coefs, dt, n, maxb, maxp, nplane, total):
         L = _lib.lib()
         rgb = torch.empty(max(total, 1), dtype=torch.uint8, device=self.device)
         if n:
@@ -612,11 +679,6 @@ class GPUBatchInputs:
                                        _lib.stream_ptr())
             if rc != 0:
                 raise RuntimeError("dtm_jpeg_decode_gpu failed (%d)" % rc)
-        if fb is not None:
-            fb_t, lst = fb
-            src = fb_t.to(self.device, non_blocking=True)
-            for o, so, nb in lst:
-                rgb[o:o + nb].copy_(src[so:so + nb])
         return rgb
 
     def close(self):

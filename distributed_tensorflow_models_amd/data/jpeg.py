@@ -151,7 +151,7 @@ def decode_batch_gpu(items, device, stream=None):
 # ---- device entropy decode -----------------------------------------------------------------------------
 # mirror of struct HuffDesc (csrc/kernels/jpeg.hip)
 HUFF_DESC_DT = np.dtype([("stream_off", "<i8"), ("coef_base", "<i8"), ("coef_count", "<i4"), ("seg_off", "<i4"),
-                         ("min_bits", "<i4"), ("overlap", "<i4"), ("s", SCAN_DT)])
+                         ("min_bits", "<i4"), ("pad", "<i4"), ("s", SCAN_DT)])
 
 
 def scan_prep(data, stream=None, segs=None):
@@ -179,10 +179,36 @@ def scan_prep(data, stream=None, segs=None):
     return info[0], sc[0], stream[:n + STREAM_PAD], segs[:int(sc["nseg"][0])]
 
 
-def huff_batch_table(scans, descs, min_bits=0, overlap=0):
+HDR_SCAN_BYTES = INFO_DT.itemsize + SCAN_DT.itemsize
+
+
+def scan_item(data, stream=None, segs=None):
+    """scan_prep packed for the input pipeline: (JpegInfo + JpegScan bytes, one uint8 payload = the unstuffed
+    stream, 4-byte aligned, then the restart segment table) or None."""
+    r = scan_prep(data, stream, segs)
+    if r is None:
+        return None
+    info, sc, st, sg = r
+    a = (st.size + 3) // 4 * 4
+    pay = np.zeros(a + 4 * sg.size, np.uint8)
+    pay[:st.size] = st
+    pay[a:].view(np.int32)[:] = sg
+    return info.tobytes() + sc.tobytes(), pay
+
+
+def unpack_scan_item(hdr, pay):
+    """Inverse of scan_item -> (JpegInfo, JpegScan, stream bytes, segments): scan_prep's result."""
+    info = np.frombuffer(hdr, INFO_DT, count=1)[0]
+    sc = np.frombuffer(hdr, SCAN_DT, count=1, offset=INFO_DT.itemsize)[0]
+    n = int(sc["nbytes"]) + STREAM_PAD
+    a = (n + 3) // 4 * 4
+    return info, sc, pay[:n], pay[a:a + 4 * int(sc["nseg"])].view(np.int32)
+
+
+def huff_batch_table(scans, descs, min_bits=0):
     """Entropy-decode descriptors for a batch prepared by scan_prep: [(JpegScan, stream bytes, segments)] and the
     JpegDesc table of the same images (batch_table) -> (HuffDesc table, stream bytes, segment count).  Streams are
-    4-byte aligned."""
+    16-byte aligned."""
     n = len(scans)
     h = np.zeros(n, HUFF_DESC_DT)
     off = nseg = 0
@@ -194,49 +220,75 @@ def huff_batch_table(scans, descs, min_bits=0, overlap=0):
         h[i]["coef_count"] = nb
         h[i]["seg_off"] = nseg
         h[i]["min_bits"] = min_bits
-        h[i]["overlap"] = overlap
-        off += (st.size + 3) // 4 * 4
+        off += (st.size + 15) // 16 * 16  # (16-byte aligned: the kernel stages subsequences with 16-byte loads)
         nseg += sg.size
     return h, off, nseg
 
 
-def decode_batch_gpu_full(datas, device, min_bits=0, overlap=0, stream=None):
+class DeviceBatch:
+    """A batch prepared by scan_prep for the device decode: the pinned host staging (unstuffed streams, restart
+    segment table, HuffDesc / JpegDesc tables) and, after ``launch``, the device buffers.  ``rgb_offs``: where each
+    image's HxWx3 output goes in the RGB buffer (default: packed in order); ``rgb_bytes``: that buffer's size."""
+
+    def __init__(self, preps, min_bits=0, rgb_offs=None, rgb_bytes=None, pin=True):
+        import torch
+        d, ncoef, nplane, nrgb, maxb, maxp = batch_table([p[0] for p in preps])
+        if rgb_offs is not None:
+            d["rgb_off"] = rgb_offs
+        h, nbytes, nseg = huff_batch_table([p[1:] for p in preps], d, min_bits)
+        self.n, self.ncoef, self.nplane, self.maxb, self.maxp = len(preps), ncoef, nplane, int(maxb), int(maxp)
+        self.nrgb = nrgb if rgb_bytes is None else rgb_bytes
+        self.descs = d
+        self.stream = torch.empty(max(nbytes, 16) + max(nseg, 1) * 4, dtype=torch.uint8, pin_memory=pin)
+        hv = self.stream.numpy()
+        self.seg_byte_off = max(nbytes, 16)
+        segs = hv[self.seg_byte_off:].view(np.int32)
+        for (_inf, _sc, st, sg), hd in zip(preps, h):
+            o = int(hd["stream_off"])
+            hv[o:o + st.size] = st
+            segs[int(hd["seg_off"]):int(hd["seg_off"]) + sg.size] = sg
+        self.tables = torch.from_numpy(np.concatenate([h.view(np.uint8), d.view(np.uint8)]))
+        if pin:
+            self.tables = self.tables.pin_memory()
+        self.hbytes = h.nbytes
+
+    def launch(self, device, stream_ptr=None, rgb=None):
+        """Upload + jpeg_huff_kernel + jpeg_idct_kernel + jpeg_color_kernel on the current (or the given) stream.
+        Returns (device RGB buffer, device int32 status per image: fixed-point passes, 0 = restart segments, -1 =
+        corrupt data)."""
+        import torch
+
+        from ..ops import _lib
+        L = _lib.lib()
+        assert L.dtm_jpeg_huff_desc_bytes() == HUFF_DESC_DT.itemsize, (L.dtm_jpeg_huff_desc_bytes(),
+                                                                       HUFF_DESC_DT.itemsize)
+        ds = self.stream.to(device, non_blocking=True)
+        dt = self.tables.to(device, non_blocking=True)
+        coefs = torch.empty(max(self.ncoef, 8), dtype=torch.int16, device=device)
+        status = torch.empty(self.n, dtype=torch.int32, device=device)
+        planes = torch.empty(max(self.nplane, 8), dtype=torch.uint8, device=device)
+        if rgb is None:
+            rgb = torch.empty(max(self.nrgb, 1), dtype=torch.uint8, device=device)
+        sp = _lib.stream_ptr() if stream_ptr is None else stream_ptr
+        rc = L.dtm_jpeg_huff_gpu(_lib.ptr(ds), _lib.ptr(ds[self.seg_byte_off:]), _lib.ptr(dt), self.n,
+                                 _lib.ptr(coefs), _lib.ptr(status), sp)
+        if rc == 0:
+            rc = L.dtm_jpeg_decode_gpu(_lib.ptr(coefs), _lib.ptr(dt[self.hbytes:]), self.n, self.maxb, self.maxp,
+                                       _lib.ptr(planes), _lib.ptr(rgb), sp)
+        if rc != 0:
+            raise RuntimeError("device JPEG decode failed (%d)" % rc)
+        self.coefs = coefs  # (kept for tests: the entropy decoder's output)
+        return rgb, status
+
+
+def decode_batch_gpu_full(datas, device, min_bits=0, stream=None):
     """Device decode of a batch of JPEG files (bytes): host marker parse + unstuffing, then jpeg_huff_kernel +
     jpeg_idct_kernel + jpeg_color_kernel.  Returns (device uint8 RGB ragged buffer, JpegDesc table, per-image
-    status: passes of the subsequence fixed point, 0 for restart-segment images, -1 corrupt) - or None for a file
-    scan_prep declines (the caller decodes those on the host)."""
-    import torch
-
-    from ..ops import _lib
-    L = _lib.lib()
-    assert L.dtm_jpeg_huff_desc_bytes() == HUFF_DESC_DT.itemsize, (L.dtm_jpeg_huff_desc_bytes(),
-                                                                   HUFF_DESC_DT.itemsize)
+    status: passes of the subsequence fixed point, 0 for restart-segment images, -1 corrupt, device coefficients)
+    - or None when scan_prep declines a file (the caller decodes those on the host)."""
     preps = [scan_prep(d) for d in datas]
     if any(p is None for p in preps):
         return None
-    d, ncoef, nplane, nrgb, maxb, maxp = batch_table([p[0] for p in preps])
-    h, nbytes, nseg = huff_batch_table([p[1:] for p in preps], d, min_bits, overlap)
-    host = torch.zeros(max(nbytes, 16), dtype=torch.uint8, pin_memory=True)
-    hv = host.numpy()
-    segs = np.zeros(max(nseg, 1), np.int32)
-    for (inf, sc, st, sg), hd in zip(preps, h):
-        o = int(hd["stream_off"])
-        hv[o:o + st.size] = st
-        segs[int(hd["seg_off"]):int(hd["seg_off"]) + sg.size] = sg
-    dstream = host.to(device, non_blocking=True)
-    dsegs = torch.from_numpy(segs).to(device)
-    dh = torch.from_numpy(h.view(np.uint8)).to(device)
-    dd = torch.from_numpy(d.view(np.uint8)).to(device)
-    coefs = torch.empty(max(ncoef, 8), dtype=torch.int16, device=device)
-    status = torch.empty(len(datas), dtype=torch.int32, device=device)
-    planes = torch.empty(max(nplane, 8), dtype=torch.uint8, device=device)
-    rgb = torch.empty(max(nrgb, 1), dtype=torch.uint8, device=device)
-    sp = _lib.stream_ptr() if stream is None else stream
-    rc = L.dtm_jpeg_huff_gpu(_lib.ptr(dstream), _lib.ptr(dsegs), _lib.ptr(dh), len(datas), _lib.ptr(coefs),
-                             _lib.ptr(status), sp)
-    if rc == 0:
-        rc = L.dtm_jpeg_decode_gpu(_lib.ptr(coefs), _lib.ptr(dd), len(datas), int(maxb), int(maxp), _lib.ptr(planes),
-                                   _lib.ptr(rgb), sp)
-    if rc != 0:
-        raise RuntimeError("device JPEG decode failed (%d)" % rc)
-    return rgb, d, status, coefs
+    b = DeviceBatch(preps, min_bits)
+    rgb, status = b.launch(device, stream)
+    return rgb, b.descs, status, b.coefs

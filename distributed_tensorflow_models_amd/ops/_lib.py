@@ -39,6 +39,7 @@ _SIGS = {
     "dtm_jpeg_decode_gpu": (_I, [_P, _P, _I, _I, _L, _P, _P, _P]),
     "dtm_jpeg_huff_desc_bytes": (_I, []),
     "dtm_jpeg_huff_gpu": (_I, [_P, _P, _P, _I, _P, _P, _P]),
+    "dtm_jpeg_set_huff": (None, [_I, _I]),
     "dtm_imagenet_prep": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P]),
     "dtm_act_bwd": (_I, [_P, _P, _P, _L, _I, _F, _I, _P]),
     "dtm_instnorm_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _I, _P]),

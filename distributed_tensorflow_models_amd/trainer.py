@@ -185,11 +185,11 @@ def make_input(cfg, batch_size, device, flags, rank):
         from .data import imagenet
         if torch.device(device).type == "cuda":
             # decode on host threads, crop / resize / flip / colour on the GPU (data/imagenet_gpu.py); the node's
-            # host CPUs are checked against what its ranks consume (data/capacity.py), and the split JPEG decode
-            # (host Huffman + HIP IDCT / colour) is chosen when the full host decode cannot keep up
+            # host CPUs are checked against what its ranks consume (data/capacity.py), and the device JPEG decode
+            # (host marker parse only; HIP Huffman / IDCT / colour) is chosen when the full host decode cannot keep up
             from .data import capacity, imagenet_gpu
             split = capacity.choose_split_decode(cfg["model"])
-            capacity.decode_capacity_check(cfg["model"], mode="split" if split else "full", log=logging.warning)
+            capacity.decode_capacity_check(cfg["model"], mode=split, log=logging.warning)
             return imagenet_gpu.distorted_inputs(imagenet.ImagenetData("train", flags.data_dir), batch_size,
                                                  image_size=S, device=device, seed=flags.seed + rank,
                                                  split_decode=split)

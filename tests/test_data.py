@@ -397,17 +397,61 @@ def test_gpu_pipeline_split_decode_host_side(tmp_path):
         assert int(tab["src_off"][-1] + tab["h"][-1] * tab["w"][-1] * 3) == total
 
 
+def test_gpu_pipeline_device_decode_host_side(tmp_path):
+    """Device decode mode (split_decode=2: the decoders only parse markers and unstuff the scan, data/jpeg.py
+    scan_item): the assembler stages every baseline image's stream + tables (jpeg.DeviceBatch) with its RGB output at
+    the parameter-table slot, and progressive files fall back to PIL pixels; parameters and labels equal the full
+    pipeline's.  (The device side: tests/test_jpeg.py, tests/test_data_gpu.py.)"""
+    from distributed_tensorflow_models_amd.data import imagenet_gpu, jpeg
+    from distributed_tensorflow_models_amd.data.tfrecord import tf_record_iterator
+    ds = _jpeg_shard(tmp_path)
+    streams = {}
+    for rec in tf_record_iterator(ds.data_files()[0]):
+        data = imagenet.parse_example_proto(rec)[0]
+        r = jpeg.scan_prep(data)
+        if r is not None:
+            streams[bytes(r[2])] = (int(r[0]["height"]), int(r[0]["width"]))
+    full = _assembled(ds, False, 2, 2, split=False)
+    dev = _assembled(ds, False, 2, 2, split=2)
+    procs = _assembled(ds, True, 2, 2, split=2)  # decoder processes: the shared-memory item format
+    assert all(p[3][0] == "device" and isinstance(p[0], jpeg.DeviceBatch) for p in procs)
+    for (bt, tt, lab, _n), (batch, tt2, lab2, split) in zip(full, dev):
+        assert torch.equal(lab, lab2) and torch.equal(tt, tt2)
+        assert split[0] == "device"
+        _k, fb, total, n = split
+        tab = tt2.numpy().view(imagenet_gpu._PARAM_DT)
+        assert isinstance(batch, jpeg.DeviceBatch) and batch.n == n and batch.nrgb == total
+        h = batch.tables.numpy()[:batch.hbytes].view(jpeg.HUFF_DESC_DT)
+        st = batch.stream.numpy()
+        slots = set()
+        for hd, d in zip(h, batch.descs):
+            o, nb = int(hd["stream_off"]), int(hd["s"]["nbytes"]) + jpeg.STREAM_PAD
+            assert o % 16 == 0
+            assert streams.get(bytes(st[o:o + nb])) == (int(d["height"]), int(d["width"]))
+            slot = int(np.nonzero(tab["src_off"] == d["rgb_off"])[0][0])
+            assert (int(tab["h"][slot]), int(tab["w"][slot])) == (int(d["height"]), int(d["width"]))
+            slots.add(slot)
+        assert fb is not None  # progressive files: PIL pixels at their own slots
+        fb_t, lst = fb
+        for o, so, nbytes in lst:
+            slot = int(np.nonzero(tab["src_off"] == o)[0][0])
+            assert slot not in slots
+            np.testing.assert_array_equal(fb_t.numpy()[so:so + nbytes], bt.numpy()[o:o + nbytes])
+        assert len(slots) + len(lst) == len(tab)
+
+
 def test_decode_capacity_check_warns_when_host_cpus_cannot_feed_the_node(monkeypatch):
     """a node of 8 ResNet-50 ranks (~120k img/s) needs far more decode CPUs than a 16-CPU host; the
-    startup check says so (with the split-decode alternative), a host with enough CPUs passes silently, and the
-    split JPEG decode is chosen automatically only when the full host decode cannot keep up (DTM_SPLIT_DECODE=0/1
-    overrides)."""
+    startup check says so (with the split- and device-decode alternatives), a host with enough CPUs passes silently,
+    and the device JPEG decode is chosen automatically only when the full host decode cannot keep up
+    (DTM_SPLIT_DECODE=0/1/2 overrides)."""
     from distributed_tensorflow_models_amd.data import capacity
     msgs = []
-    rate = {"full": 1000.0, "split": 2500.0}
+    rate = {"full": 1000.0, "split": 2500.0, "device": 25000.0}
     need, cpus, ok = capacity.decode_capacity_check("resnet_v1_50", gpus=8, cpus=16, per_cpu=rate, log=msgs.append)
     assert not ok and cpus == 16 and abs(need - 120.0) < 1e-6
     assert len(msgs) == 1 and "needs ~120 host CPUs" in msgs[0] and "split decode needs ~48" in msgs[0]
+    assert "device decode needs ~5" in msgs[0]
     msgs.clear()
     need, _c, ok = capacity.decode_capacity_check("inception_v3_slim_old", gpus=1, cpus=16, per_cpu=rate,
                                                   log=msgs.append)
@@ -419,7 +463,14 @@ def test_decode_capacity_check_warns_when_host_cpus_cannot_feed_the_node(monkeyp
     monkeypatch.setenv("DTM_SPLIT_DECODE", "0")
     assert not capacity.choose_split_decode("resnet_v1_50", gpus=8, cpus=16, per_cpu=rate)
     monkeypatch.setenv("DTM_SPLIT_DECODE", "1")
-    assert capacity.choose_split_decode("resnet_v1_50", gpus=1, cpus=64, per_cpu=rate)
+    assert capacity.choose_split_decode("resnet_v1_50", gpus=1, cpus=64, per_cpu=rate) == 1
+    monkeypatch.setenv("DTM_SPLIT_DECODE", "2")
+    assert capacity.choose_split_decode("resnet_v1_50", gpus=1, cpus=64, per_cpu=rate) == 2
+    monkeypatch.delenv("DTM_SPLIT_DECODE")
+    # the device decode's host share: one node's CPUs (e.g. 2 x 64 cores) feed 8 ResNet-50 ranks
+    assert capacity.choose_split_decode("resnet_v1_50", gpus=8, cpus=16, per_cpu=rate) == 2
+    need, _c, ok = capacity.decode_capacity_check("resnet_v1_50", gpus=8, cpus=128, mode="device")
+    assert ok and need < 16, need
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
     monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(64)))
     monkeypatch.setattr(os, "cpu_count", lambda: 64)

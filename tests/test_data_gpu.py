@@ -58,8 +58,9 @@ def test_gpu_batch_inputs_from_tfrecords(tmp_path):
 
 
 def test_split_decode_pipeline_matches_full_decode(tmp_path):
-    """Device batches through the split JPEG decode (host Huffman + HIP IDCT / upsampling / colour) equal
-    the full host-decode pipeline's (same seeds -> same crops and colour parameters), including a
+    """Device batches through the split JPEG decode (host Huffman + HIP IDCT / upsampling / colour) and through the
+    device decode (host marker parse only + HIP Huffman / IDCT / colour, split_decode=2) equal the full host-decode
+    pipeline's (same seeds -> same crops and colour parameters), including a
     progressive file that takes the PIL fallback inside a split batch.  (The decoded pixels are bit-exact -
     tests/test_jpeg.py; the preprocessing's per-image contrast mean is an fp32 atomic sum, so the bf16
     batches agree to rounding.)"""
@@ -80,7 +81,7 @@ def test_split_decode_pipeline_matches_full_decode(tmp_path):
                                     "image/object/bbox/xmax": [0.9], "image/object/bbox/ymax": [0.95]}))
     ds = imagenet.ImagenetData("train", str(out))
     res = []
-    for split in (False, True):
+    for split in (False, True, 2):
         bi = G.GPUBatchInputs(ds, 8, train=True, image_size=64, num_readers=1, num_decoders=2, seed=11, device="cuda",
                               decode_processes=False, shuffle_buffer=32, split_decode=split)
         try:
@@ -88,7 +89,8 @@ def test_split_decode_pipeline_matches_full_decode(tmp_path):
         finally:
             bi.close()
     torch.cuda.synchronize()
-    for (x0, y0), (x1, y1) in zip(*res):
-        assert torch.equal(y0, y1)
-        torch.testing.assert_close(x0.float(), x1.float(), rtol=0, atol=1e-2)
-        assert (x0 != x1).float().mean().item() < 0.01
+    for other in res[1:]:
+        for (x0, y0), (x1, y1) in zip(res[0], other):
+            assert torch.equal(y0, y1)
+            torch.testing.assert_close(x0.float(), x1.float(), rtol=0, atol=1e-2)
+            assert (x0 != x1).float().mean().item() < 0.01

@@ -136,14 +136,21 @@ def _big_cases(n=6):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("min_bits", [0, 32, 256])
-def test_device_entropy_decode_matches_host_and_pil(min_bits):
+@pytest.mark.parametrize("cfg,min_bits", [((256, 11), 0), ((256, 11), 128), ((256, 9), 256), ((64, 9), 0),
+                                          ((64, 9), 128), ((128, 10), 0)])
+def test_device_entropy_decode_matches_host_and_pil(cfg, min_bits):
     """jpeg_huff_kernel: the device-decoded coefficients equal the host decoder's int16 for int16 and the RGB equals
     PIL's, for every case (4:4:4 / 4:2:2 / 4:2:0 / 4:4:0, restart intervals, optimized tables, gray, ImageNet-size
-    files).  min_bits 32 / 256 cut the streams into many short subsequences, so most start states are wrong guesses
-    the fixed point has to repair."""
+    files), for every threads-per-image x lookup-bits variant of the kernel.  min_bits 128 / 256 cut the streams into
+    many short subsequences (and phases), so most start states are wrong guesses the fixed point has to repair."""
+    from distributed_tensorflow_models_amd.ops import _lib
     cases = _cases() + _big_cases()
-    r = jpeg.decode_batch_gpu_full([d for _n, d in cases], torch.device("cuda", 0), min_bits=min_bits)
+    _lib.lib().dtm_jpeg_set_huff(*cfg)
+    try:
+        r = jpeg.decode_batch_gpu_full([d for _n, d in cases], torch.device("cuda", 0), min_bits=min_bits)
+        torch.cuda.synchronize()
+    finally:
+        _lib.lib().dtm_jpeg_set_huff(256, 11)
     assert r is not None
     rgb, descs, status, coefs = r
     torch.cuda.synchronize()

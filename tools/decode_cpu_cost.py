@@ -10,6 +10,8 @@ stream per worker host).
   split  : the DTM_SPLIT_DECODE=1 host share - the same parse and parameter sampling, and only the Huffman decode
            to DCT coefficients (csrc/runtime/jpeg.cpp); dequantisation, IDCT, upsampling and colour conversion run as
            HIP kernels (csrc/kernels/jpeg.hip).
+  device : the DTM_SPLIT_DECODE=2 host share - the same parse and parameter sampling, and only the JPEG marker parse +
+           byte unstuffing (data/jpeg.py scan_item); the Huffman decode runs on the GPU too (jpeg_huff_kernel).
   huffman: the Huffman decode alone (the part of the split host work that is inherently serial).
 
 Synthetic JPEGs with ImageNet-like geometry (300-500 px sides, quality 90, smooth content + noise; ~70 KB -
@@ -84,11 +86,19 @@ def measure(n=512):
         jpeg.huffman_decode(ex["image/encoded"][0], coefs)
         sample_params()
 
+    stream, segs = np.empty(1 << 22, np.uint8), np.empty(1 << 14, np.int32)
+
+    def device(rec):
+        ex = decode_example(rec)
+        jpeg.scan_item(ex["image/encoded"][0], stream, segs)
+        sample_params()
+
     res = {"avg_kb": sum(len(j) for j in jp) / len(jp) / 1024.0,
            "full_us": per_image_us(full, recs), "split_us": per_image_us(split, recs),
+           "device_us": per_image_us(device, recs),
            "huffman_us": per_image_us(lambda j: jpeg.huffman_decode(j, coefs), jp)}
-    res["full_img_s_per_cpu"] = 1e6 / res["full_us"]
-    res["split_img_s_per_cpu"] = 1e6 / res["split_us"]
+    for m in ("full", "split", "device"):
+        res[m + "_img_s_per_cpu"] = 1e6 / res[m + "_us"]
     return res
 
 
@@ -102,10 +112,12 @@ def main():
                                                                                       r["full_img_s_per_cpu"]))
     print("  split (parse + Huffman + params)   : %7.0f us  -> %6.0f img/s per CPU" % (r["split_us"],
                                                                                       r["split_img_s_per_cpu"]))
+    print("  device (parse + unstuff + params)  : %7.0f us  -> %6.0f img/s per CPU" % (r["device_us"],
+                                                                                      r["device_img_s_per_cpu"]))
     print("  huffman alone                      : %7.0f us  (%.0f %% of the full decode)" % (
         r["huffman_us"], 100.0 * r["huffman_us"] / r["full_us"]))
     for name, per_gpu in (("ResNet-50 224", 15000), ("Inception-v3 299", 7400)):
-        for mode in ("full", "split"):
+        for mode in ("full", "split", "device"):
             print("  %-17s x 8 GPUs = %6.0f img/s needs %4.0f CPUs (%s)" % (
                 name, 8 * per_gpu, 8 * per_gpu / r[mode + "_img_s_per_cpu"], mode))
 

@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--images", type=int, default=128)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--min-bits", type=int, default=0)
-    ap.add_argument("--overlap", type=int, nargs="+", default=[0])
+    ap.add_argument("--cfg", nargs="+", default=["256x11"], help="threads-per-image x lookup-bits variants")
     a = ap.parse_args()
     import torch
 
@@ -51,25 +51,29 @@ def main():
     print("%d JPEGs, avg %.0f KB; host per image: scan prep %.1f us (host Huffman decode %.1f us)" % (
         len(jp), sum(map(len, jp)) / len(jp) / 1024.0, best, hb))
     dev = torch.device("cuda", 0)
-    for ov in a.overlap:
-        run(jp, dev, a, ov)
+    from distributed_tensorflow_models_amd.ops import _lib
+    for cfg in a.cfg:
+        nt, lk = (int(x) for x in cfg.split("x"))
+        _lib.lib().dtm_jpeg_set_huff(nt, lk)
+        print("-- %d threads per image, %d-bit lookup" % (nt, lk))
+        run(jp, dev, a)
 
 
-def run(jp, dev, a, ov):
+def run(jp, dev, a):
     import torch
 
     from distributed_tensorflow_models_amd.data import jpeg
     from distributed_tensorflow_models_amd.ops import _lib
-    r = jpeg.decode_batch_gpu_full(jp, dev, min_bits=a.min_bits, overlap=ov)
+    r = jpeg.decode_batch_gpu_full(jp, dev, min_bits=a.min_bits)
     torch.cuda.synchronize()
     stt = r[2].cpu().numpy()
-    print("overlap %d: status (fixed-point passes) histogram: %s" % (
-        ov, {int(k): int(v) for k, v in zip(*np.unique(stt, return_counts=True))}))
+    print("status (fixed-point passes) histogram: %s" % (
+        {int(k): int(v) for k, v in zip(*np.unique(stt, return_counts=True))}))
     # time the device stages alone on the uploaded batch
     L = _lib.lib()
     preps = [jpeg.scan_prep(d) for d in jp]
     d, ncoef, nplane, nrgb, maxb, maxp = jpeg.batch_table([p[0] for p in preps])
-    h, nbytes, nseg = jpeg.huff_batch_table([p[1:] for p in preps], d, a.min_bits, ov)
+    h, nbytes, nseg = jpeg.huff_batch_table([p[1:] for p in preps], d, a.min_bits)
     hv = np.zeros(max(nbytes, 16), np.uint8)
     for (inf, sc, s, g), hd in zip(preps, h):
         hv[int(hd["stream_off"]):int(hd["stream_off"]) + s.size] = s
