@@ -189,12 +189,17 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(const JpegDesc* __restr
 //    from a start state S_t = (bit, block-in-MCU, coefficient) to the first codeword boundary past its end, giving
 //    the exit state E_t, its block count and per-component DC-difference sums.  S_0 is exact; S_t starts as a guess
 //    (bit t * L, block 0, coefficient 0) and is replaced by E_{t-1} until nothing changes - a fixed point that is
-//    exact by induction (after pass j the first j + 1 starts are), and in practice reached in 2-3 passes because a
-//    Huffman decode started at a wrong bit falls back into step with the true one within a few codewords.  Scans of
+//    exact by induction (after pass j the first j + 1 starts are), and in practice reached in a few passes because a
+//    Huffman decode started at a wrong bit falls back into step with the true one (see the measurements below).  Scans of
 //    the counts and DC sums then place every thread's blocks and DC predictors, and a last pass writes them.
-// Tables: each of the image's (<= 4) DHT tables becomes an 11-bit lookup in LDS (code length + symbol, or for
+// Tables: each of the image's (<= 4) DHT tables becomes a 9..11-bit lookup in LDS (code length + symbol, or for
 // short codes the code + magnitude bits -> the value, run and total length in one entry; the host decoder's
 // fast_ac), longer codes walk the canonical maxcode table.
+// Measured (tools/jpeg_gpu_bench.py, ImageNet-like 300-500 px q90 files): the fixed point takes 3-5 passes at
+// 256 threads per image (a wrong-start decode regains bit sync within ~15-80 bits but the block-in-MCU / coefficient
+// state only after ~800 bits median, ~6000 worst), ~430k images/s on the whole GPU with 3 images per CU; 256 images
+// decoded under the ResNet-50 step cost it ~1 ms (6 %), which is why the full host decode stays the default
+// wherever the host CPUs keep up (data/capacity.py).
 
 // mirror of csrc/runtime/jpeg.cpp JpegScan
 struct JpegScan {
@@ -652,9 +657,12 @@ DTM_API int dtm_jpeg_huff_desc_bytes() { return (int)sizeof(HuffDesc); }
 // Entropy-decode a batch: stream = the images' unstuffed bytes (each 4-aligned, 32 zero bytes after), segs = the
 // restart segment table, descs = device [n] HuffDesc.  coefs receives every image's zero-filled coefficients;
 // status[i] = passes of the subsequence fixed point (0: restart segments), -1: the image's data is corrupt.
-// threads per image (64 / 128 / 256) and lookup bits (9 / 10 / 11) of the entropy decoder
+// threads per image (64 / 128 / 256) and lookup bits (9 / 10 / 11) of the entropy decoder.  256 x 10 measured
+// fastest on ImageNet-like files, alone and co-running with the ResNet-50 step (profiles/r6/r6_s23_jpeg_bench*.log,
+// r6_s24_decode_overlap.log): fewer threads per image sync in fewer passes but leave the CU latency-bound; an
+// 11-bit lookup costs LDS occupancy.
 static int g_huff_nt = getenv("DTM_JPEG_NT") ? atoi(getenv("DTM_JPEG_NT")) : 256;
-static int g_huff_lk = getenv("DTM_JPEG_LOOK") ? atoi(getenv("DTM_JPEG_LOOK")) : 11;
+static int g_huff_lk = getenv("DTM_JPEG_LOOK") ? atoi(getenv("DTM_JPEG_LOOK")) : 10;
 DTM_API void dtm_jpeg_set_huff(int nt, int lk) {
   g_huff_nt = nt;
   g_huff_lk = lk;

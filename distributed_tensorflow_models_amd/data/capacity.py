@@ -16,7 +16,7 @@ import logging
 import os
 
 # img/s per host CPU core (tools/decode_cpu_cost.py on the MI355X box's host CPUs; see module docstring)
-IMG_S_PER_CPU = {"full": 1370.0, "split": 2440.0, "device": 24000.0}
+IMG_S_PER_CPU = {"full": 1370.0, "split": 2440.0, "device": 29000.0}
 
 # expected per-GPU consumption of the training step (bench.py on one MI355X, round 5), images/s
 PER_GPU_IMG_S = {"resnet_v1_50": 15000.0, "inception_v3_slim_old": 7400.0, "mobilenet_v1": 20000.0,

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--cfg", default="256x11")
+    ap.add_argument("--low-priority", type=int, default=0, help="decode stream at the least priority HIP allows")
     a = ap.parse_args()
     import torch
 
@@ -34,7 +35,9 @@ def main():
     dev = torch.device("cuda", 0)
     jp = make_jpegs(a.batch, seed=1)
     batch = jpeg.DeviceBatch([jpeg.scan_prep(j) for j in jp])
-    side = torch.cuda.Stream()
+    lo, hi = torch.cuda.Stream.priority_range()
+    side = torch.cuda.Stream(priority=lo) if a.low_priority else torch.cuda.Stream()
+    print("stream priority range (least, greatest) = (%d, %d); decode stream priority %d" % (lo, hi, side.priority))
     torch.manual_seed(1234)
     net = nets_factory.build("resnet_v1_50", num_classes=1000).to(dev)
     step = TrainStep(net, optimizer="momentum", lr=0.1, momentum=0.9)
@@ -70,8 +73,9 @@ def main():
         res[on].append((time.perf_counter() - t) / a.steps * 1e3)
     off, on = min(res[False]), min(res[True])
     print("ResNet-50 b%d step: %.3f ms without decode, %.3f ms with a %d-image device decode per step on a side stream "
-          "(+%.3f ms, %.2f %%); decode alone %.3f ms (%s)" % (a.batch, off, on, a.batch, on - off,
-                                                           100.0 * (on - off) / off, alone, a.cfg))
+          "(+%.3f ms, %.2f %%); decode alone %.3f ms (%s%s)" % (a.batch, off, on, a.batch, on - off,
+                                                             100.0 * (on - off) / off, alone, a.cfg,
+                                                             ", low priority" if a.low_priority else ""))
     print("blocks off:", ["%.3f" % v for v in res[False]], "on:", ["%.3f" % v for v in res[True]])
 
 
