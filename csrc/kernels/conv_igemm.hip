@@ -862,14 +862,18 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(ConvNTArgs a) {
 // one 8-row x 128-B LDS-DMA group per wave-instruction, AI + WI of them per wave per k-tile.
 // (32x32x16-MFMA forms of these tiles measured +0.6 % ResNet-50 step - LDS / DMA bound, not MFMA-issue bound -
 // and were removed: profiles/ab/r3_ab_mfma32_step.log)
-template <int PT, int CT, int NWP, int NS, int UD, bool SPL = false>
-__global__ __launch_bounds__(512) void conv_nt_w8_kernel(ConvNTArgs a) {
-  constexpr int NT = 512, NW = 8;
+// (NTH = 256 builds the 4-wave form - waves 2x2 of 128x128, 64 accumulator tiles per wave, 1 wave per SIMD: half the
+// LDS fragment reads per MFMA.  It measured 40 % slower per conv and 10-15 % per weight gradient (the 4-wave
+// wgrad_pipe <256, 256, 2, 2, 256>), ResNet-50 step +11 %: one wave per SIMD cannot cover the LDS / DMA latency
+// (profiles/r6/r6_s27_sweep_w4.log, r6_s27_ab_w4.log); not wired into the policy.)
+template <int PT, int CT, int NWP, int NS, int UD, bool SPL = false, int NTH = 512>
+__global__ __launch_bounds__(NTH) void conv_nt_w8_kernel(ConvNTArgs a) {
+  constexpr int NT = NTH, NW = NTH / 64;
   constexpr int BK = 64;
   constexpr int NWC = NW / NWP;
   constexpr int WP = PT / NWP, WC = CT / NWC;
   constexpr int TP = WP / 16, TC = WC / 16;
-  constexpr int AI = PT / 64, WI = CT / 64;  // 8-row DMA groups per wave per k-tile
+  constexpr int AI = PT / (8 * NW), WI = CT / (8 * NW);  // 8-row DMA groups per wave per k-tile
   constexpr int G = AI + WI;                 // DMA instructions per wave per k-tile
   constexpr int BUF = (PT + CT) * 128;
   constexpr int OROW = CT * 2 + 16;
@@ -2450,10 +2454,10 @@ static const bf16_t* zero_chunk() {
 }
 const void* dtm_zero_chunk() { return zero_chunk(); }  // (the stem-pool kernels' out-of-range tap source)
 
-template <int PT, int CT, int NWP, int NS, int UD, bool SPL = false>
+template <int PT, int CT, int NWP, int NS, int UD, bool SPL = false, int NTH = 512>
 static void launch_w8(const ConvNTArgs& a, hipStream_t st) {
   dim3 grid((a.K + CT - 1) / CT, (a.M + PT - 1) / PT, a.ngrp > 1 ? a.ngrp : 1);
-  hipLaunchKernelGGL((conv_nt_w8_kernel<PT, CT, NWP, NS, UD, SPL>), grid, dim3(512), 0, st, a);
+  hipLaunchKernelGGL((conv_nt_w8_kernel<PT, CT, NWP, NS, UD, SPL, NTH>), grid, dim3(NTH), 0, st, a);
 }
 
 template <int UD, bool SPL = false>
@@ -3247,10 +3251,10 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
               d->R, d->S, a.Kg, d->stride, in_scale != nullptr, bn != nullptr, dst ? dst->n : 0, wt);
   }
   const bool big = wt == 12 || wt == 13;  // 8-wave 256x256 (one block per CU)
-  const bool k64w = wt == 1 || wt == 7 || wt == 8 || wt == 11 || wt >= 14;  // 64-row tiles
+  const bool k64w = wt == 1 || wt == 7 || wt == 8 || wt == 11 || (wt >= 14 && wt <= 16);  // 64-row tiles
   const int MT = wt == 6 ? 32 : (k64w ? 64 : (big ? 256 : 128)), NT = (big || (k64w && wt != 1)) ? 256 : 128;
   if (big) occ = ((wenv == 12 || wenv == 13) && g_wgrad_occ != 4) ? g_wgrad_occ : 1;
-  if (wt >= 14) occ = (wenv >= 14 && g_wgrad_occ != 4) ? g_wgrad_occ : 1;  // (the BNA tiles: 1 block per CU)  // (sweeps: WTILES=12:<occ>)
+  if (wt >= 14 && wt <= 16) occ = (wenv >= 14 && g_wgrad_occ != 4) ? g_wgrad_occ : 1;  // (the BNA tiles: 1 block per CU)  // (sweeps: WTILES=12:<occ>)
   long tiles = (long)((a.Kg + NT - 1) / NT) * ((a.K + MT - 1) / MT);
   // register-staged tiles: 3 blocks' worth of splits per CU (sweeps: WTILES=<1|6|0>:<occ>, occ != 4)
   const int rs_occ = (wenv >= 0 && g_wgrad_occ != 4) ? g_wgrad_occ : 3;
