@@ -2623,11 +2623,18 @@ static void launch_direct_k(const ConvNTArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((conv3x3_direct_kernel<CIN, CT, SIDE>), dim3(a.K / CT, direct_workers_k<CIN, CT, SIDE>(a)),
                      dim3(256), 0, st, a, a.M / 128);
 }
+// 32-channel output tiles also for K % 64 == 0 (half the resident weights and staging: 2 blocks per CU instead of 1;
+// Inception-v3's 147x147 3x3 32 -> 64 forward 269 -> 227 us, profiles/r6/r6_s29_direct_ct32.log, step
+// r6_s30_ab_ct32_inception.log).  A/B knob dtm_conv_set_direct_ct32 / DTM_DIRECT_CT32=0.
+static int g_direct_ct32 = getenv("DTM_DIRECT_CT32") ? atoi(getenv("DTM_DIRECT_CT32")) : 1;
+DTM_API void dtm_conv_set_direct_ct32(int on) { g_direct_ct32 = on; }
 #define DTM_DIRECT_SEL(FN, ...)                                                                     \
   ((a.add_src || a.act_x)                                                                          \
        ? (a.C == 64 ? FN<64, 32, true>(__VA_ARGS__) : FN<32, 32, true>(__VA_ARGS__))                 \
-       : (a.C == 64 ? (a.K % 64 == 0 ? FN<64, 64, false>(__VA_ARGS__) : FN<64, 32, false>(__VA_ARGS__)) \
-                    : (a.K % 64 == 0 ? FN<32, 64, false>(__VA_ARGS__) : FN<32, 32, false>(__VA_ARGS__))))
+       : (a.C == 64 ? ((a.K % 64 == 0 && !g_direct_ct32) ? FN<64, 64, false>(__VA_ARGS__)           \
+                                                        : FN<64, 32, false>(__VA_ARGS__))           \
+                    : ((a.K % 64 == 0 && !g_direct_ct32) ? FN<32, 64, false>(__VA_ARGS__)           \
+                                                        : FN<32, 32, false>(__VA_ARGS__))))
 static int direct_workers(const ConvNTArgs& a) { return DTM_DIRECT_SEL(direct_workers_k, a); }
 static void launch_direct(const ConvNTArgs& a, hipStream_t st) { DTM_DIRECT_SEL(launch_direct_k, a, st); }
 
