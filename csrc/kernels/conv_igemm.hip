@@ -1958,6 +1958,191 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
   }
 }
 
+// Direct 3x3 stride-1 weight gradient for narrow layers (C in {32, 64} input channels, 32 dW rows per block; the
+// Inception-v3 stem's 147x147 3x3s and ResNet-50's 56x56 3x3 64 -> 64): dW[k][r][s][c] = sum_p dy[p][k] x[p+(r,s)][c].
+// As an implicit GEMM (conv_wgrad_kernel) every input pixel is fetched once per tap; here a persistent block walks
+// 8 x 16 output-pixel tiles and stages each tile's operands ONCE, transposed to channel-major in LDS so that the
+// reduction over pixels runs along contiguous memory: dy^T [32 k][128 px] and the (8+2)-row x halo as three
+// column-shifted copies [s][c][10 rows][16 cols] (tap column s is then an aligned 8-pixel read).  The optional
+// BN-apply prologue (relu(x*scale + shift), zero padding kept zero) is applied once per staged element.  Waves own
+// 16 input channels each (C = 64: all 9 taps; C = 32: two waves per channel group, taps 0-4 / 5-8) and both 16-row
+// halves of the block's 32 dW rows, so one dy^T fragment serves every tap and one x fragment both row halves.  The
+// next tile's operands are loaded into registers while this one is multiplied.  One fp32 slab per block, summed by
+// dtm_reduce_rows.
+template <int CIN, int KT>
+__global__ __launch_bounds__(256) void conv3x3_wgrad_direct_kernel(ConvWgradArgs a, int ntiles, int tiles_w,
+                                                                   int tiles_img) {
+  constexpr int TH = 8, TW = 16, HR = TH + 2, NKT = KT / 16;
+  constexpr int NCG = CIN / 8;                       // 8-channel groups of x
+  constexpr int NCT = CIN / 16;                      // 16-channel fragment columns
+  constexpr int WPC = 4 / NCT;                       // waves per channel group (2 or 1)
+  constexpr int TPW = (9 + WPC - 1) / WPC;           // taps per wave (5 or 9)
+  constexpr int CS = 168;                            // x copy row pitch per channel (elements): 16-lane reads hit
+                                                     // distinct banks
+  constexpr int DS = 136;                            // dy^T pitch per k (elements)
+  constexpr int XT = 3 * HR * 2 * NCG;               // x staging tasks (8 pixels x 8 channels) per tile
+  constexpr int XPT = (XT + 255) / 256;              // per thread
+  constexpr int DT = TH * 2 * (KT / 8);              // dy staging tasks per tile (64 / 128)
+  static_assert(DT <= 256, "one dy task per thread");
+  __shared__ __attribute__((aligned(16))) bf16_t xs[3 * CIN * CS];
+  __shared__ __attribute__((aligned(16))) bf16_t dyt[KT * DS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nb = gridDim.x * gridDim.y;
+  const int bid = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, nb);
+  const int bx = bid % gridDim.x, by0 = bid / gridDim.x;
+  const int k0 = bx * KT;
+  const int ct = wave % NCT, th = wave / NCT;        // this wave's 16 input channels and tap range
+  const int tap0 = th * TPW, tap1 = min(9, tap0 + TPW);
+  const bf16_t* xg = a.x;
+  const bf16_t* dg = a.dy;
+
+  uint4 xr[XPT][8], dr[8];
+  // loads of tile t's operands into registers (zeros out of range: padding, pixels past the map)
+  auto load = [&](int t) {
+    const int n = t / tiles_img, rem = t - n * tiles_img;
+    const int oh0 = (rem / tiles_w) * TH, ow0 = (rem % tiles_w) * TW;
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int q = tid + 256 * i;
+      const int cg = q % NCG, run = (q / NCG) % 2, hr = (q / (2 * NCG)) % HR, sc = q / (2 * NCG * HR);
+      const int ih = oh0 + hr - a.pad_h;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int iw = ow0 + run * 8 + j + sc - a.pad_w;
+        const bool v = q < XT && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        xr[i][j] = v ? *(const uint4*)(xg + (((size_t)n * a.H + ih) * a.W + iw) * CIN + cg * 8) : make_uint4(0, 0, 0, 0);
+      }
+    }
+    if (tid < DT) {
+      const int cg = tid % (KT / 8), run = (tid / (KT / 8)) % 2, row = tid / (KT / 4);
+      const int oh = oh0 + row;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int ow = ow0 + run * 8 + j;
+        const bool v = oh < a.P && ow < a.Q && k0 + cg * 8 < a.K;
+        dr[j] = v ? *(const uint4*)(dg + (((size_t)n * a.P + oh) * a.Q + ow) * a.K + k0 + cg * 8) : make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  // 8 pixels x 8 channels (rows = pixels) -> channel-major rows of 8 pixels: out[ch] = (q[0][ch] .. q[7][ch])
+  auto transpose = [&](const uint4 (&q)[8], uint4 (&o)[8]) {
+#pragma unroll
+    for (int ch = 0; ch < 8; ++ch) {
+      const uint32_t sel = (ch & 1) ? 0x07060302u : 0x05040100u;
+      uint32_t w[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint4& lo = q[2 * j];
+        const uint4& hi = q[2 * j + 1];
+        const uint32_t l = (ch >> 1) == 0 ? lo.x : (ch >> 1) == 1 ? lo.y : (ch >> 1) == 2 ? lo.z : lo.w;
+        const uint32_t h = (ch >> 1) == 0 ? hi.x : (ch >> 1) == 1 ? hi.y : (ch >> 1) == 2 ? hi.z : hi.w;
+        w[j] = __builtin_amdgcn_perm(h, l, sel);
+      }
+      o[ch] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  };
+  auto store = [&](int t) {
+    const int n = t / tiles_img, rem = t - n * tiles_img;
+    const int oh0 = (rem / tiles_w) * TH, ow0 = (rem % tiles_w) * TW;
+    (void)n;
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int q = tid + 256 * i;
+      if (q < XT) {
+        const int cg = q % NCG, run = (q / NCG) % 2, hr = (q / (2 * NCG)) % HR, sc = q / (2 * NCG * HR);
+        uint4 px[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) px[j] = xr[i][j];
+        if (a.in_scale) {  // BN-apply prologue on the valid (non-padding) pixels
+          const int ih = oh0 + hr - a.pad_h;
+          float sc8[8], sh8[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            sc8[e] = a.in_scale[cg * 8 + e];
+            sh8[e] = a.in_shift[cg * 8 + e];
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int iw = ow0 + run * 8 + j + sc - a.pad_w;
+            if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W) {
+              const uint32_t u[4] = {px[j].x, px[j].y, px[j].z, px[j].w};
+              uint32_t o[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                o[e] = pack2bf(fmaxf(fmaf(lo_bf(u[e]), sc8[2 * e], sh8[2 * e]), 0.f),
+                               fmaxf(fmaf(hi_bf(u[e]), sc8[2 * e + 1], sh8[2 * e + 1]), 0.f));
+              px[j] = make_uint4(o[0], o[1], o[2], o[3]);
+            }
+          }
+        }
+        uint4 o[8];
+        transpose(px, o);
+#pragma unroll
+        for (int ch = 0; ch < 8; ++ch)
+          *(uint4*)&xs[(sc * CIN + cg * 8 + ch) * CS + hr * 16 + run * 8] = o[ch];
+      }
+    }
+    if (tid < DT) {
+      const int cg = tid % (KT / 8), run = (tid / (KT / 8)) % 2, row = tid / (KT / 4);
+      uint4 o[8];
+      transpose(dr, o);
+#pragma unroll
+      for (int ch = 0; ch < 8; ++ch) *(uint4*)&dyt[(cg * 8 + ch) * DS + row * 16 + run * 8] = o[ch];
+    }
+  };
+
+  f32x4 acc[TPW][NKT];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i)
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) acc[i][kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, g = lane >> 4;
+  const int gy = gridDim.y;
+  int t = by0;
+  if (t < ntiles) load(t);
+  for (; t < ntiles; t += gy) {
+    store(t);
+    __syncthreads();
+    if (t + gy < ntiles) load(t + gy);  // (in flight while this tile is multiplied)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {  // 32 pixels = output rows 2 ks, 2 ks + 1
+      const int pix = ks * 32 + 8 * g;
+      short8 af[NKT];
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) af[kt] = *(const short8*)&dyt[(kt * 16 + fr) * DS + pix];
+      const int prow = 2 * ks + (g >> 1), pcol = 8 * (g & 1);
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) {
+        const int tap = tap0 + i;
+        if (tap < tap1) {
+          const int r = tap / 3, sc = tap - r * 3;
+          const short8 b = *(const short8*)&xs[(sc * CIN + ct * 16 + fr) * CS + (prow + r) * 16 + pcol];
+#pragma unroll
+          for (int kt = 0; kt < NKT; ++kt)
+            acc[i][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kt], b, acc[i][kt], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();  // (the next store overwrites the staged operands)
+  }
+  // this block's partial dW: lane holds rows kt*16 + 4 g + e, column ct*16 + fr of each tap
+  float* slab = a.dw + (size_t)by0 * a.K * a.Kg;
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int tap = tap0 + i;
+    if (tap < tap1) {
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int k = k0 + kt * 16 + 4 * g + e;
+          if (k < a.K) slab[(size_t)k * a.Kg + tap * CIN + ct * 16 + fr] = acc[i][kt][e];
+        }
+    }
+  }
+}
+
 // Pipelined LDS-DMA weight gradient (no input prologue): both pixel-major operand tiles go global ->
 // LDS by LDS-DMA straight into the [k/4][row/16][4][16] transposed-read image.  An LDS-DMA writes
 // lane-linear 16-B slots, so each lane loads the chunk whose tr_off position is its slot (the inverse
@@ -3161,6 +3346,45 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
                            const ConvDesc* d, int num_cus, const WgradBN* bn, void* stream,
                            const WgradDst* dst = nullptr);
 
+// direct 3x3 weight gradient (conv3x3_wgrad_direct_kernel) on maps of at least g_wgrad_direct_min pixels
+static int g_wgrad_direct = getenv("DTM_WGRAD_DIRECT") ? atoi(getenv("DTM_WGRAD_DIRECT")) : 1;
+static int g_wgrad_direct_min = 2500;
+DTM_API void dtm_conv_set_wgrad_direct(int on, int min_pixels) {
+  g_wgrad_direct = on;
+  if (min_pixels > 0) g_wgrad_direct_min = min_pixels;
+}
+template <int CIN, int KT>
+static int wgrad_direct_k(ConvWgradArgs& a, const ConvDesc* d, int num_cus, hipStream_t st, float* dw) {
+  static int occ = 0;
+  if (!occ) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv3x3_wgrad_direct_kernel<CIN, KT>, 256, 0) !=
+            hipSuccess ||
+        occ <= 0)
+      occ = 1;
+  }
+  const int tiles_w = (d->Q + 15) / 16, tiles_h = (d->P + 7) / 8, tiles_img = tiles_h * tiles_w;
+  const long ntiles = (long)d->N * tiles_img;
+  if (ntiles >= (1l << 31)) return -2;
+  const int ktiles = d->K / KT;
+  long workers = (long)occ * num_cus / ktiles;
+  if (workers < 1) workers = 1;
+  if (workers > ntiles) workers = ntiles;
+  float* ws = dtm_ws_get_stream((size_t)workers * a.K * a.Kg, st);
+  if (!ws) return -4;
+  a.dw = ws;
+  hipLaunchKernelGGL((conv3x3_wgrad_direct_kernel<CIN, KT>), dim3(ktiles, (unsigned)workers), dim3(256), 0, st, a,
+                     (int)ntiles, tiles_w, tiles_img);
+  dtm_reduce_rows(ws, (int)workers, a.K * a.Kg, a.K * a.Kg, dw, st);  // dW += sum over the workers' slabs
+  return 0;
+}
+static int g_wgrad_direct_kt = 64;  // dW rows per block when K % 64 == 0 (A/B: dtm_conv_set_wgrad_direct_kt)
+DTM_API void dtm_conv_set_wgrad_direct_kt(int kt) { g_wgrad_direct_kt = kt; }
+static int wgrad_direct(ConvWgradArgs& a, const ConvDesc* d, int num_cus, hipStream_t st, float* dw) {
+  const bool k64 = d->K % 64 == 0 && g_wgrad_direct_kt == 64;
+  if (d->C == 32) return k64 ? wgrad_direct_k<32, 64>(a, d, num_cus, st, dw) : wgrad_direct_k<32, 32>(a, d, num_cus, st, dw);
+  return k64 ? wgrad_direct_k<64, 64>(a, d, num_cus, st, dw) : wgrad_direct_k<64, 32>(a, d, num_cus, st, dw);
+}
+
 DTM_API int dtm_conv_wgrad(const void* x, const void* dy, float* dw, const float* in_scale,
                            const float* in_shift, const ConvDesc* d, int num_cus, void* stream) {
   return conv_wgrad_impl(x, dy, dw, in_scale, in_shift, d, num_cus, nullptr, stream);
@@ -3212,6 +3436,16 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   // logs: profiles/ab/README.md).  dtm_conv_set_wgrad_tile forces one (A/B experiments).
   if (g_wgrad_env == -2) g_wgrad_env = -1;
   const int wenv = g_wgrad_env;
+  // the direct 3x3 kernel (conv3x3_wgrad_direct_kernel; tile id 20 forces it where it applies)
+  // (automatic for 32 input channels: Inception-v3's 147x147 3x3 32 -> 32 / 64, 238 -> 162 / 277 -> 216 us, with the
+  //  BN-apply prologue 386 -> 199 / 407 -> 247 us; 64 channels lose on ResNet-50's 56x56 64 -> 64, 144 -> 187 us without
+  //  the prologue, 218 vs 223 with it: profiles/r6/r6_s33_wdirect_sweep.log)
+  if ((wenv == 20 || (wenv == -1 && g_wgrad_direct && d->C == 32)) && !bn && !dst && d->R == 3 && d->S == 3 &&
+      d->stride == 1 && (d->C == 32 || d->C == 64) && d->K % 32 == 0 && a.pix_bytes == d->C * 2 && d->pad_h <= 2 &&
+      d->pad_w <= 2 &&
+      d->P == d->H + 2 * d->pad_h - 2 && d->Q == d->W + 2 * d->pad_w - 2 &&
+      (d->H * d->W >= g_wgrad_direct_min || wenv == 20))
+    return wgrad_direct(a, d, num_cus, (hipStream_t)stream, dw);
   int wt = wenv >= 0 ? wenv : (d->K <= 64 ? 1 : 0);
   // <= 32 output channels: 32-row tiles (no half-empty 64-row tile; A/B knob dtm_conv_set_k32)
   if (wenv == -1 && wt == 1 && d->K <= 32 && g_k32_tile) wt = 6;

@@ -564,6 +564,43 @@ def test_conv_fwd_bn_multi_matches_separate(case):
             assert not sss[i].any()
 
 
+@pytest.mark.parametrize("prologue", [False, True])
+@pytest.mark.parametrize("case", [(2, 19, 21, 32, 32, "SAME"), (3, 17, 18, 32, 64, "VALID"), (2, 13, 15, 64, 64, "SAME"),
+                                  (1, 8, 40, 64, 96, "SAME"), (2, 25, 9, 32, 32, "VALID")])
+def test_conv3x3_wgrad_direct_matches_reference(prologue, case):
+    """conv3x3_wgrad_direct_kernel (wgrad tile 20: per 8x16 output tile, dy^T and three column-shifted x halo copies
+    staged once, channel-major, in LDS; the optional BN-apply prologue applied to the staged x with the zero padding
+    kept zero) against the fp32 reference: partial edge tiles, VALID / SAME padding, 32 / 64 input channels, one and
+    several 32-row dW tiles."""
+    import ctypes
+
+    from distributed_tensorflow_models_amd.ops import _lib
+    from distributed_tensorflow_models_amd.ops.geometry import conv_geom
+    N, H, W, C, K, pad = case
+    torch.manual_seed(1)
+    L = _lib.lib()
+    x = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16)
+    w = torch.randn(K, 3, 3, C, device=DEV).to(torch.bfloat16)
+    sc = torch.rand(C, device=DEV) + 0.5
+    sh = torch.randn(C, device=DEV) * 0.5
+    g = conv_geom(tuple(x.shape), tuple(w.shape), 1, pad)
+    d = g.as_desc(_lib.ConvDesc)
+    dy = torch.randn(N, g.P, g.Q, K, device=DEV).to(torch.bfloat16)
+    xin = torch.relu(x.float() * sc + sh).to(torch.bfloat16).float() if prologue else x.float()
+    wr = w.float().clone().requires_grad_()
+    ref.conv2d(xin, wr, None, 1, pad).backward(dy.float())
+    dw = torch.zeros(K, 3, 3, C, device=DEV)
+    L.dtm_conv_set_wgrad_tile(20, 0)
+    try:
+        rc = L.dtm_conv_wgrad(_lib.ptr(x), _lib.ptr(dy), _lib.ptr(dw), _lib.ptr(sc) if prologue else None,
+                              _lib.ptr(sh) if prologue else None, ctypes.byref(d), _lib.num_cus(), _lib.stream_ptr())
+        torch.cuda.synchronize()
+    finally:
+        L.dtm_conv_set_wgrad_tile(-1, 4)
+    assert rc == 0
+    assert _rel(dw, wr.grad) < 1e-3, _rel(dw, wr.grad)
+
+
 @pytest.mark.parametrize("tile", [0, 1, 6, 10, 11, 12, 13])
 @pytest.mark.parametrize("case", [(4, 15, 15, 64, 96, 3, 2), (2, 14, 14, 128, 256, 3, 1), (3, 7, 7, 512, 200, 1, 1),
                                   (2, 9, 9, 24, 40, 3, 1), (5, 8, 8, 64, 64, 1, 1), (4, 9, 9, 256, 512, 3, 1),

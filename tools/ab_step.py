@@ -5,7 +5,7 @@ median ms/step per variant; one device, one process: MI355X_MICROARCH 'DVFS give
 VARIANTS="base=;noW=wtile:-3;noT=tile:-3;fused=prologue:fused" python tools/ab_step.py
 keys: tile (conv_nt tile id), w8 (0/1: the 8-wave 256x256 conv tile in the shape policy), pp (0/1: its ping-pong
 form conv_nt_pp_kernel in place of conv_nt_w8_kernel), ct32 (0/1: 32-channel output tiles of the direct 3x3 kernel
-for K = 64), sbna (0/1: the stem's BN-fused wgrad on the pipelined
+for K = 64), wdir (0/1: the direct 3x3 weight gradient for 32 input channels), sbna (0/1: the stem's BN-fused wgrad on the pipelined
 64x256 tile), aocc (0-3: occupancy variants of the register-staged dgrads with post-ops), nocc (the same for
 their launches without side inputs), kwide (0/1: 64-channel
 tiles for K % 128 <= 64), few (0/1: streaming few-row slab reduction), sact (0/1: streaming 1x1 kernel for act
@@ -67,6 +67,7 @@ def apply(cfg):
     L.dtm_conv_set_w8(int(cfg.get("w8", "1")))
     L.dtm_conv_set_pp(int(cfg.get("pp", "0")))
     L.dtm_conv_set_direct_ct32(int(cfg.get("ct32", "1")))
+    L.dtm_conv_set_wgrad_direct(int(cfg.get("wdir", "1")), 0)
     L.dtm_conv_set_stem_bna(int(cfg.get("sbna", "1")))
     L.dtm_conv_set_act_occ(int(cfg.get("aocc", "2")))
     L.dtm_conv_set_nt_occ(int(cfg.get("nocc", "2")))
