@@ -3478,7 +3478,9 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* dw, const float
   if (wt >= 14 && wt <= 16 && (in_scale || !bn || d->K > 64)) wt = d->K <= 64 ? 1 : 0;
   // the stem (BN backward fused, 64 x <= 256): tile 15 - the g / y operand read once and pipelined, 385.7 -> 357.1 us
   // at batch 256 (tools/stem_sweep.py, profiles/r6/r6_s10_stem_wgrad.log)
-  if (wenv == -1 && g_stem_bna && bn && !in_scale && d->K <= 64 && a.Kg <= 256) wt = 15;
+  // (not for 32 output channels: Inception-v3's packed 3x3/2 stem, K 32 x Kg 96, runs 119 us on the 32-row register-
+  //  staged tile vs 294 us here - profiles/r6/r6_s41_stem_inception.log)
+  if (wenv == -1 && g_stem_bna && bn && !in_scale && d->K > 32 && d->K <= 64 && a.Kg <= 256) wt = 15;
   if (wt == 12 && g_tile_pp && wenv == -1) wt = 13;  // (the ping-pong form of the 256x256 tile, A/B knob dtm_conv_set_pp)
   if (wt != 0 && wt != 1 && wt != 6 && wt != 7 && wt != 8 && !(wt >= 10 && wt <= 16)) wt = 0;
   {
